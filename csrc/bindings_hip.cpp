@@ -1,0 +1,328 @@
+// torch bindings for the gfx950 kernels (distributed_tf_serving_amd/_hip*.so).
+//
+// Every entry point validates shapes, dtypes, devices and contiguity on the
+// host BEFORE launching, because a hand-written kernel that indexes past its
+// operands can take the whole GPU node down. Kernels run on the caller's
+// current HIP stream, so they compose with torch streams and HIP-graph capture.
+#include <torch/extension.h>
+
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+hipStream_t cur_stream(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e));
+}
+
+void check_dev(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_same_dev(const torch::Tensor& a, const torch::Tensor& b, const char* name) {
+  TORCH_CHECK(a.device() == b.device(), name, " must be on ", a.device());
+}
+
+const void* opt_ptr(const c10::optional<torch::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ---------------------------------------------------------------- K0
+torch::Tensor pack_ids(torch::Tensor ids, int64_t modulo, c10::optional<torch::Tensor> modulo_f,
+                       c10::optional<torch::Tensor> offset_f) {
+  check_dev(ids, "ids");
+  TORCH_CHECK(ids.dim() == 2, "ids must be [B, F]");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32, "ids must be int32/int64");
+  const int F = int(ids.size(1));
+  for (auto* o : {&modulo_f, &offset_f})
+    if (o->has_value()) {
+      check_dev(**o, "per-field table");
+      TORCH_CHECK((*o)->scalar_type() == torch::kInt64 && (*o)->numel() == F, "per-field tables must be int64 [F]");
+    }
+  c10::DeviceGuard g(ids.device());
+  auto out = torch::empty(ids.sizes(), ids.options().dtype(torch::kInt32));
+  check_hip(dtfs::launch_pack_ids(ids.data_ptr(), ids.scalar_type() == torch::kInt64, out.data_ptr<int32_t>(),
+                                  ids.numel(), F, modulo_f ? modulo_f->data_ptr<int64_t>() : nullptr,
+                                  offset_f ? offset_f->data_ptr<int64_t>() : nullptr, modulo, cur_stream(ids)),
+            "pack_ids");
+  return out;
+}
+
+// ---------------------------------------------------------------- K1
+std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor ids,
+                                 c10::optional<torch::Tensor> wts, int64_t modulo, c10::optional<torch::Tensor> modulo_f,
+                                 c10::optional<torch::Tensor> offset_f, double bias, bool want_x, bool want_fm,
+                                 bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables) {
+  check_dev(table, "table");
+  check_dev(ids, "ids");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
+  TORCH_CHECK(ids.dim() == 2, "ids must be [B, F]");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32, "ids must be int32/int64");
+  const int64_t B = ids.size(0), F = ids.size(1), D = table.size(1);
+  TORCH_CHECK(D == 8 || D == 16 || D == 32 || D == 64 || D == 128, "embedding dim must be 8/16/32/64/128");
+  check_same_dev(table, ids, "ids");
+  const int64_t V = table.size(0);
+  if (modulo_f.has_value() || offset_f.has_value()) {
+    TORCH_CHECK(modulo_f.has_value() && offset_f.has_value(), "modulo_f and offset_f go together");
+    for (auto* o : {&modulo_f, &offset_f}) {
+      check_dev(**o, "per-field table");
+      TORCH_CHECK((*o)->scalar_type() == torch::kInt64 && (*o)->numel() == F, "per-field tables must be int64 [F]");
+    }
+    // every (offset + row) must stay inside the table. The kernel also clamps
+    // rows into [0, V), so this (syncing) host check is a debugging aid that
+    // models run once at construction, not per batch.
+    auto mf = validate_tables ? modulo_f->cpu() : torch::Tensor();
+    auto of = validate_tables ? offset_f->cpu() : torch::Tensor();
+    for (int64_t f = 0; validate_tables && f < F; ++f) {
+      TORCH_CHECK(mf.data_ptr<int64_t>()[f] > 0, "per-field modulo must be > 0");
+      TORCH_CHECK(of.data_ptr<int64_t>()[f] >= 0 && of.data_ptr<int64_t>()[f] + mf.data_ptr<int64_t>()[f] <= V,
+                  "field ", f, " rows exceed the table");
+    }
+  } else {
+    TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]: ids are hashed onto rows");
+  }
+  if (wts) {
+    check_dev(*wts, "wts");
+    TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->sizes() == ids.sizes(), "wts must be fp32 [B, F]");
+  }
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
+  }
+  c10::DeviceGuard g(ids.device());
+  torch::Tensor x, fm;
+  if (want_x) {
+    if (out_x) {
+      check_dev(*out_x, "out_x");
+      TORCH_CHECK(out_x->scalar_type() == torch::kBFloat16 && out_x->numel() == B * F * D, "out_x must be bf16 [B, F*D]");
+      x = *out_x;
+    } else {
+      x = torch::empty({B, F * D}, table.options());
+    }
+  }
+  if (want_fm) fm = torch::empty({B}, table.options().dtype(torch::kFloat32));
+  check_hip(dtfs::launch_embed(table.data_ptr(), lin ? lin->data_ptr<float>() : nullptr, ids.data_ptr(),
+                               ids.scalar_type() == torch::kInt64, wts ? wts->data_ptr<float>() : nullptr, int(B),
+                               int(F), int(D), V, modulo, modulo_f ? modulo_f->data_ptr<int64_t>() : nullptr,
+                               offset_f ? offset_f->data_ptr<int64_t>() : nullptr, float(bias),
+                               want_x ? x.data_ptr() : nullptr, want_fm ? fm.data_ptr<float>() : nullptr, fm2,
+                               cur_stream(ids)),
+            "embed");
+  return {x, fm};
+}
+
+// ---------------------------------------------------------------- K1b
+torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
+                            c10::optional<torch::Tensor> psw, int64_t modulo, bool mean, bool out_bf16) {
+  check_dev(table, "table");
+  check_dev(idx, "indices");
+  check_dev(offsets, "offsets");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [R, D]");
+  TORCH_CHECK(idx.dim() == 1 && (idx.scalar_type() == torch::kInt64 || idx.scalar_type() == torch::kInt32),
+              "indices must be int32/int64 [nnz]");
+  TORCH_CHECK(offsets.dim() == 1 && offsets.scalar_type() == torch::kInt64 && offsets.numel() >= 1,
+              "offsets must be int64 [nbags+1]");
+  const int64_t D = table.size(1), R = table.size(0), nbags = offsets.numel() - 1;
+  TORCH_CHECK(D == 8 || D == 16 || D == 32 || D == 64 || D == 128, "embedding dim must be 8/16/32/64/128");
+  TORCH_CHECK(modulo > 0 && modulo <= R, "modulo must be in (0, rows]");
+  // offsets are clamped into [0, nnz] inside the kernel (no host sync here)
+  if (psw) {
+    check_dev(*psw, "per_sample_weights");
+    TORCH_CHECK(psw->scalar_type() == torch::kFloat32 && psw->numel() == idx.numel(), "per_sample_weights: fp32 [nnz]");
+  }
+  c10::DeviceGuard g(table.device());
+  auto out = torch::empty({nbags, D}, table.options().dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
+  check_hip(dtfs::launch_embedding_bag(table.data_ptr(), idx.data_ptr(), idx.scalar_type() == torch::kInt64,
+                                       offsets.data_ptr<int64_t>(), psw ? psw->data_ptr<float>() : nullptr, int(nbags),
+                                       idx.numel(), int(D), modulo, mean, out_bf16 ? nullptr : out.data_ptr<float>(),
+                                       out_bf16 ? out.data_ptr() : nullptr, D, cur_stream(table)),
+            "embedding_bag");
+  return out;
+}
+
+// ---------------------------------------------------------------- K4 / K3b
+torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor> bias, int64_t epi,
+                   c10::optional<torch::Tensor> x0, c10::optional<torch::Tensor> xl, bool out_f32,
+                   c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sw, c10::optional<torch::Tensor> out) {
+  check_dev(A, "A");
+  check_dev(W, "W");
+  check_same_dev(A, W, "W");
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2, "A [M,K], W [N,K]");
+  const bool fp8 = A.scalar_type() == torch::kFloat8_e4m3fn || A.scalar_type() == torch::kUInt8;
+  if (fp8) {
+    TORCH_CHECK(W.scalar_type() == A.scalar_type(), "fp8 GEMM needs fp8 (e4m3fn) A and W");
+    TORCH_CHECK(sa.has_value() && sw.has_value(), "fp8 GEMM needs row scales sa [M] and channel scales sw [N]");
+  } else {
+    TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && W.scalar_type() == torch::kBFloat16, "bf16 GEMM needs bf16 A, W");
+  }
+  const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "K mismatch: A ", A.sizes(), " W ", W.sizes());
+  TORCH_CHECK(fp8 ? K % 16 == 0 : K % 8 == 0, "K must be a multiple of 16 bytes");
+  TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31), "dims too large");
+  if (bias) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == N, "bias must be fp32 [N]");
+  }
+  if (sa) {
+    check_dev(*sa, "sa");
+    TORCH_CHECK(sa->scalar_type() == torch::kFloat32 && sa->numel() == M, "sa must be fp32 [M]");
+  }
+  if (sw) {
+    check_dev(*sw, "sw");
+    TORCH_CHECK(sw->scalar_type() == torch::kFloat32 && sw->numel() == N, "sw must be fp32 [N]");
+  }
+  TORCH_CHECK(epi >= 0 && epi <= 3, "epi must be 0..3");
+  if (epi == 3) {
+    TORCH_CHECK(x0.has_value() && xl.has_value(), "cross epilogue needs x0 and xl");
+    for (auto* t : {&x0, &xl}) {
+      check_dev(**t, "x0/xl");
+      TORCH_CHECK((*t)->scalar_type() == torch::kBFloat16 && (*t)->size(0) == M && (*t)->size(1) == N,
+                  "x0/xl must be bf16 [M, N]");
+    }
+  }
+  c10::DeviceGuard g(A.device());
+  torch::Tensor C;
+  if (out) {
+    check_dev(*out, "out");
+    TORCH_CHECK(out->size(0) == M && out->size(1) == N, "out must be [M, N]");
+    TORCH_CHECK(out->scalar_type() == (out_f32 ? torch::kFloat32 : torch::kBFloat16), "out dtype mismatch");
+    C = *out;
+  } else {
+    C = torch::empty({M, N}, A.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  }
+  check_hip(dtfs::launch_gemm(A.data_ptr(), K, W.data_ptr(), K, bias ? bias->data_ptr<float>() : nullptr,
+                              sa ? sa->data_ptr<float>() : nullptr, sw ? sw->data_ptr<float>() : nullptr, C.data_ptr(),
+                              N, out_f32, opt_ptr(x0), opt_ptr(xl), N, int(M), int(N), int(K), int(epi), fp8,
+                              cur_stream(A)),
+            "gemm");
+  return C;
+}
+
+// ---------------------------------------------------------------- K3
+std::vector<torch::Tensor> cross_v1(torch::Tensor x0, torch::Tensor w, torch::Tensor b, bool want_x,
+                                    c10::optional<torch::Tensor> head_w) {
+  check_dev(x0, "x0");
+  check_dev(w, "w");
+  check_dev(b, "b");
+  TORCH_CHECK(x0.scalar_type() == torch::kBFloat16 && x0.dim() == 2, "x0 must be bf16 [B, d]");
+  const int64_t B = x0.size(0), d = x0.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 64 * 8 * 8, "d must be a multiple of 8 and <= 4096");
+  TORCH_CHECK(w.scalar_type() == torch::kFloat32 && w.dim() == 2 && w.size(1) == d, "w must be fp32 [L, d]");
+  TORCH_CHECK(b.scalar_type() == torch::kFloat32 && b.sizes() == w.sizes(), "b must be fp32 [L, d]");
+  if (head_w) {
+    check_dev(*head_w, "head_w");
+    TORCH_CHECK(head_w->scalar_type() == torch::kFloat32 && head_w->numel() == d, "head_w must be fp32 [d]");
+  }
+  c10::DeviceGuard g(x0.device());
+  torch::Tensor x, dot;
+  if (want_x) x = torch::empty_like(x0);
+  if (head_w) dot = torch::empty({B}, x0.options().dtype(torch::kFloat32));
+  check_hip(dtfs::launch_cross_v1(x0.data_ptr(), d, int(B), int(d), int(w.size(0)), w.data_ptr<float>(),
+                                  b.data_ptr<float>(), want_x ? x.data_ptr() : nullptr, d,
+                                  head_w ? head_w->data_ptr<float>() : nullptr,
+                                  head_w ? dot.data_ptr<float>() : nullptr, cur_stream(x0)),
+            "cross_v1");
+  return {x, dot};
+}
+
+// ---------------------------------------------------------------- K5
+torch::Tensor dot_interaction(torch::Tensor dense, torch::Tensor emb, int64_t out_cols) {
+  check_dev(dense, "dense");
+  check_dev(emb, "emb");
+  TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && emb.scalar_type() == torch::kBFloat16, "bf16 inputs");
+  TORCH_CHECK(dense.dim() == 2 && dense.size(1) == 64, "dense must be [B, 64]");
+  TORCH_CHECK(emb.dim() == 3 && emb.size(0) == dense.size(0) && emb.size(2) == 64, "emb must be [B, T, 64]");
+  const int64_t B = dense.size(0), T = emb.size(1);
+  TORCH_CHECK(T + 1 <= 32, "dot interaction kernel handles T + 1 <= 32 vectors");
+  const int64_t used = 64 + (T + 1) * T / 2;
+  if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
+  TORCH_CHECK(out_cols >= used, "out_cols too small");
+  c10::DeviceGuard g(dense.device());
+  auto out = torch::empty({B, out_cols}, dense.options());
+  check_hip(dtfs::launch_dot_interaction(dense.data_ptr(), 64, emb.data_ptr(), int(T), int(B), out.data_ptr(),
+                                         out_cols, int(out_cols), cur_stream(dense)),
+            "dot_interaction");
+  return out;
+}
+
+// ---------------------------------------------------------------- K6
+torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<torch::Tensor> extra, bool sigmoid) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.dim() == 2, "x must be bf16 [M, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
+  TORCH_CHECK(w.scalar_type() == torch::kFloat32 && w.numel() == K, "w must be fp32 [K]");
+  if (extra) {
+    check_dev(*extra, "extra");
+    TORCH_CHECK(extra->scalar_type() == torch::kFloat32 && extra->numel() == M, "extra must be fp32 [M]");
+  }
+  c10::DeviceGuard g(x.device());
+  auto out = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  check_hip(dtfs::launch_head(x.data_ptr(), K, w.data_ptr<float>(), float(bias),
+                              extra ? extra->data_ptr<float>() : nullptr, int(M), int(K), sigmoid ? 2 : 0,
+                              out.data_ptr<float>(), cur_stream(x)),
+            "head");
+  return out;
+}
+
+// ---------------------------------------------------------------- fp8
+std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.dim() == 2, "x must be bf16 [M, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 16 == 0 && K <= 4096, "K must be a multiple of 16 and <= 4096");
+  c10::DeviceGuard g(x.device());
+  auto q = torch::empty({M, K}, x.options().dtype(torch::kFloat8_e4m3fn));
+  auto s = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  check_hip(dtfs::launch_quant_rows_fp8(x.data_ptr(), K, int(M), int(K), q.data_ptr(), K, s.data_ptr<float>(),
+                                        cur_stream(x)),
+            "quant_rows_fp8");
+  return {q, s};
+}
+
+// ---------------------------------------------------------------- K7
+std::vector<torch::Tensor> sort_scores(torch::Tensor s, bool descending, int64_t k) {
+  check_dev(s, "scores");
+  TORCH_CHECK(s.scalar_type() == torch::kFloat32 && s.dim() == 1, "scores must be fp32 [N]");
+  const int64_t n = s.numel();
+  TORCH_CHECK(n <= dtfs::sort_max_elems(), "sort kernel handles at most ", dtfs::sort_max_elems(), " scores");
+  if (k < 0 || k > n) k = n;
+  c10::DeviceGuard g(s.device());
+  auto out = torch::empty({k}, s.options());
+  auto perm = torch::empty({k}, s.options().dtype(torch::kInt64));
+  check_hip(dtfs::launch_sort_scores(s.data_ptr<float>(), int(n), descending, out.data_ptr<float>(),
+                                     perm.data_ptr<int64_t>(), int(k), cur_stream(s)),
+            "sort_scores");
+  return {out, perm};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "distributed_tf_serving_amd gfx950 kernels (MFMA GEMM, embedding gather/bag, interactions, sort)";
+  m.def("pack_ids", &pack_ids, py::arg("ids"), py::arg("modulo") = 0, py::arg("modulo_f") = py::none(),
+        py::arg("offset_f") = py::none());
+  m.def("embed", &embed, py::arg("table"), py::arg("lin"), py::arg("ids"), py::arg("wts"), py::arg("modulo"),
+        py::arg("modulo_f") = py::none(), py::arg("offset_f") = py::none(), py::arg("bias") = 0.0,
+        py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
+        py::arg("validate_tables") = false);
+  m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
+        py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
+        py::arg("out_bf16") = false);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("W"), py::arg("bias") = py::none(), py::arg("epi") = 0,
+        py::arg("x0") = py::none(), py::arg("xl") = py::none(), py::arg("out_f32") = false,
+        py::arg("sa") = py::none(), py::arg("sw") = py::none(), py::arg("out") = py::none());
+  m.def("cross_v1", &cross_v1, py::arg("x0"), py::arg("w"), py::arg("b"), py::arg("want_x") = true,
+        py::arg("head_w") = py::none());
+  m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0);
+  m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
+        py::arg("sigmoid") = true);
+  m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"));
+  m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
+  m.def("sort_max_elems", &dtfs::sort_max_elems);
+}

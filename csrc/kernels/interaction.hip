@@ -1,0 +1,253 @@
+// Feature-interaction kernels: K3 DCN cross v1 (all layers fused, optionally
+// fused with the cross half of the output head), K5 DLRM dot interaction on
+// MFMA, K6 output head (GEMV + bias + extra logit + sigmoid), fp8 row
+// quantisation for the fp8 towers.
+#include "common.h"
+#include "launchers.h"
+
+namespace dtfs {
+namespace kern {
+
+// ---------------------------------------------------------------- K3
+// x_{l+1} = x0 * (x_l . w_l) + b_l + x_l   for l < L, one wave per row, the
+// whole row (d <= 64 * 8 * MAXC) resident in registers across all layers.
+// Outputs: out_x = x_L (bf16, optional); out_dot[b] = x_L . head_w (optional).
+template <int MAXC>
+__global__ void __launch_bounds__(256) cross_v1_kernel(const bf16* __restrict__ x0, int64_t ldx, int B, int d, int L,
+                                                       const float* __restrict__ w, const float* __restrict__ bvec,
+                                                       bf16* __restrict__ out_x, int64_t ldo,
+                                                       const float* __restrict__ head_w, float* __restrict__ out_dot) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const int nch = d / 8;
+  float a0[MAXC][8], al[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x0 + row * ldx + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a0[c][j] = al[c][j] = bf2f(v[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a0[c][j] = al[c][j] = 0.f;
+    }
+  }
+  for (int l = 0; l < L; ++l) {
+    const float* wl = w + int64_t(l) * d;
+    const float* bl = bvec + int64_t(l) * d;
+    float p = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        const float4 w0 = *reinterpret_cast<const float4*>(wl + ch * 8);
+        const float4 w1 = *reinterpret_cast<const float4*>(wl + ch * 8 + 4);
+        p += al[c][0] * w0.x + al[c][1] * w0.y + al[c][2] * w0.z + al[c][3] * w0.w;
+        p += al[c][4] * w1.x + al[c][5] * w1.y + al[c][6] * w1.z + al[c][7] * w1.w;
+      }
+    }
+    const float s = wave_sum(p);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bl + ch * 8);
+        const float4 b1 = *reinterpret_cast<const float4*>(bl + ch * 8 + 4);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) al[c][j] = a0[c][j] * s + bb[j] + al[c][j];
+      }
+    }
+  }
+  float hd = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch >= nch) continue;
+    if (out_x) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(al[c][j]);
+      *reinterpret_cast<bf16x8*>(out_x + row * ldo + ch * 8) = o;
+    }
+    if (head_w) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hd += al[c][j] * head_w[ch * 8 + j];
+    }
+  }
+  if (out_dot) {
+    hd = wave_sum(hd);
+    if (lane == 0) out_dot[row] = hd;
+  }
+}
+
+// ---------------------------------------------------------------- K5
+// DLRM pairwise dot interaction for T+1 <= 32 vectors of D = 64:
+//   X = [dense; emb_0 .. emb_{T-1}]  (32 x 64 after zero padding)
+//   Z = X X^T  via 4 x v_mfma_f32_32x32x16_bf16 (A and B fragments are the
+//   same registers: lane (r, h) holds X[r][16s + 8h .. +8] for k-step s)
+//   out[b] = [dense (D) | Z[i][j] for i > j, row-major (T+1)T/2 | zero pad]
+__global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restrict__ dense, int64_t ldd,
+                                                           const bf16* __restrict__ emb, int T, int B,
+                                                           bf16* __restrict__ out, int64_t ldo, int out_cols) {
+  constexpr int D = 64;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int nv = T + 1;
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bf16x8 x = bf16x8{};
+    const int k = 16 * s + 8 * h;
+    if (r == 0) x = *reinterpret_cast<const bf16x8*>(dense + b * ldd + k);
+    else if (r < nv) x = *reinterpret_cast<const bf16x8*>(emb + (int64_t(b) * T + (r - 1)) * D + k);
+    // f32_32x32x16_bf16 operand = 8 bf16
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, x, acc, 0, 0, 0);
+  }
+  bf16* o = out + b * ldo;
+  // dense passthrough (lanes 0..7 copy 8 each)
+  if (lane < D / 8)
+    *reinterpret_cast<bf16x8*>(o + lane * 8) = *reinterpret_cast<const bf16x8*>(dense + b * ldd + lane * 8);
+  // C layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+  const int col = lane & 31;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int rowi = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    if (rowi < nv && col < rowi) o[D + rowi * (rowi - 1) / 2 + col] = f2bf(acc[reg]);
+  }
+  // zero the padding columns so the next GEMM's K tail reads zeros
+  const int used = D + nv * (nv - 1) / 2;
+  for (int c = used + lane; c < out_cols; c += 64) o[c] = f2bf(0.f);
+}
+
+// ---------------------------------------------------------------- K6
+// y[m] = act(x[m,:] . w + bias + extra[m]); one wave per row; act: 0 none, 2 sigmoid.
+__global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                                   float bias, const float* __restrict__ extra, int M, int K, int act,
+                                                   float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float p = 0.f;
+  for (int ch = lane; ch < K / 8; ch += 64) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + m * ldx + ch * 8);
+    const float4 w0 = *reinterpret_cast<const float4*>(w + ch * 8);
+    const float4 w1 = *reinterpret_cast<const float4*>(w + ch * 8 + 4);
+    p += bf2f(v[0]) * w0.x + bf2f(v[1]) * w0.y + bf2f(v[2]) * w0.z + bf2f(v[3]) * w0.w;
+    p += bf2f(v[4]) * w1.x + bf2f(v[5]) * w1.y + bf2f(v[6]) * w1.z + bf2f(v[7]) * w1.w;
+  }
+  p = wave_sum(p);
+  if (lane == 0) {
+    float v = p + bias + (extra ? extra[m] : 0.f);
+    out[m] = act == 2 ? sigmoidf(v) : v;
+  }
+}
+
+// ---------------------------------------------------------------- fp8 quant
+// Per-row dynamic e4m3 quantisation: scale = amax / 448, q = x / scale.
+template <int MAXC>
+__global__ void __launch_bounds__(256) quant_rows_kernel(const bf16* __restrict__ x, int64_t ldx, int M, int K,
+                                                         uint8_t* __restrict__ q, int64_t ldq, float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int nch = K / 8;
+  float v[MAXC][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      const bf16x8 t = *reinterpret_cast<const bf16x8*>(x + m * ldx + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[c][j] = bf2f(t[j]);
+        amax = fmaxf(amax, fabsf(v[c][j]));
+      }
+    }
+  }
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (lane == 0) scale[m] = s;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      int lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * inv, v[c][1] * inv, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * inv, v[c][3] * inv, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4] * inv, v[c][5] * inv, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][6] * inv, v[c][7] * inv, hi, true);
+      *reinterpret_cast<int2*>(q + m * ldq + ch * 8) = make_int2(lo, hi);
+    }
+  }
+}
+
+}  // namespace kern
+
+using namespace kern;
+
+hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
+                           void* out_x, int64_t ldo, const float* head_w, float* out_dot, hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  if (d % 8) return hipErrorInvalidValue;
+  const int chunks = (d / 8 + 63) / 64;
+  dim3 grid((B + 3) / 4), block(256);
+  const bf16* xi = static_cast<const bf16*>(x0);
+  bf16* xo = static_cast<bf16*>(out_x);
+#define CROSS_CASE(C)                                                                                          \
+  case C:                                                                                                     \
+    hipLaunchKernelGGL(cross_v1_kernel<C>, grid, block, 0, st, xi, ldx, B, d, L, w, b, xo, ldo, head_w, out_dot); \
+    break;
+  switch (chunks) {
+    CROSS_CASE(1) CROSS_CASE(2) CROSS_CASE(3) CROSS_CASE(4) CROSS_CASE(5) CROSS_CASE(6) CROSS_CASE(7) CROSS_CASE(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef CROSS_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* emb, int T, int B, void* out,
+                                  int64_t ldo, int out_cols, hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  if (T + 1 > 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dot_interact_kernel, dim3((B + 3) / 4), dim3(256), 0, st, static_cast<const bf16*>(dense), ldd,
+                     static_cast<const bf16*>(emb), T, B, static_cast<bf16*>(out), ldo, out_cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,
+                       int act, float* out, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (K % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, st, static_cast<const bf16*>(x), ldx, w, bias,
+                     extra, M, K, act, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void* q, int64_t ldq, float* scale,
+                                 hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (K % 8) return hipErrorInvalidValue;
+  const int chunks = (K / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), block(256);
+  const bf16* xi = static_cast<const bf16*>(x);
+  uint8_t* qo = static_cast<uint8_t*>(q);
+#define Q_CASE(C)                                                                                   \
+  case C: hipLaunchKernelGGL(quant_rows_kernel<C>, grid, block, 0, st, xi, ldx, M, K, qo, ldq, scale); break;
+  switch (chunks) {
+    Q_CASE(1) Q_CASE(2) Q_CASE(3) Q_CASE(4) Q_CASE(5) Q_CASE(6) Q_CASE(7) Q_CASE(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef Q_CASE
+  return hipGetLastError();
+}
+
+}  // namespace dtfs

@@ -1,0 +1,51 @@
+// Host-side launch entry points of the gfx950 kernels. Raw pointers + a HIP
+// stream only: no torch types, so the kernels compile with plain hipcc and the
+// launchers are capturable into HIP graphs (no allocation, no sync inside).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtfs {
+
+// K0: out[i] = offset[f] + ((ids[i] % m_f) + m_f) % m_f, f = i % F.
+hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n, int F, const int64_t* modulo_f,
+                           const int64_t* offset_f, int64_t modulo, hipStream_t st);
+
+// K1: weighted gather (+ first/second-order FM). out_x bf16 [B, F*D] and/or out_fm fp32 [B].
+hipError_t launch_embed(const void* table, const float* lin, const void* ids, bool ids64, const float* wts, int B,
+                        int F, int D, int64_t V, int64_t modulo, const int64_t* modulo_f, const int64_t* offset_f, float bias,
+                        void* out_x, float* out_fm, bool fm2, hipStream_t st);
+
+// K1b: sum/mean embedding bag with CSR offsets [nbags+1].
+hipError_t launch_embedding_bag(const void* table, const void* idx, bool idx64, const int64_t* offsets,
+                                const float* psw, int nbags, int64_t nnz, int D, int64_t modulo, bool mean, float* out_f32,
+                                void* out_bf16, int64_t out_stride, hipStream_t st);
+
+// K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
+hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
+                       const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
+                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st);
+
+// K3: DCN-v1 cross network, all L layers fused.
+hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
+                           void* out_x, int64_t ldo, const float* head_w, float* out_dot, hipStream_t st);
+
+// K5: DLRM dot interaction (T + 1 <= 32, D = 64).
+hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* emb, int T, int B, void* out,
+                                  int64_t ldo, int out_cols, hipStream_t st);
+
+// K6: y = act(x . w + bias + extra), act 0 none / 2 sigmoid.
+hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,
+                       int act, float* out, hipStream_t st);
+
+// fp8 (OCP e4m3) per-row quantisation.
+hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void* q, int64_t ldq, float* scale,
+                                 hipStream_t st);
+
+// K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
+int sort_max_elems();
+hipError_t launch_sort_scores(const float* in, int n, bool descending, float* out, int64_t* perm, int k_out,
+                              hipStream_t st);
+
+}  // namespace dtfs

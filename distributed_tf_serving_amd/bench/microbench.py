@@ -1,0 +1,110 @@
+"""Kernel micro-benchmarks on one GPU (hot ops vs the library baseline).
+
+    python -m distributed_tf_serving_amd.bench.microbench [--quick]
+
+Prints one JSON line per measurement: the op, its shape, mean microseconds
+over interleaved rounds (cdna_hip_programming.md §5.4 rule 24), achieved
+TFLOP/s or GB/s, and for GEMMs the hipBLASLt (torch.matmul) time on the same
+random operands.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+
+import torch
+
+from .. import ops
+
+
+def _time(fn, iters=50, rounds=5):
+    fn()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) * 1e3 / iters)
+    return statistics.median(res)
+
+
+def bench_gemm(M, N, K, act="relu", dev="cuda"):
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    ours = _time(lambda: ops.linear(x, W, b, act))
+    lib = _time(lambda: torch.relu(torch.addmm(b.to(torch.bfloat16), x, W.t())))
+    flops = 2.0 * M * N * K
+    xq, sx = ops.quant_rows_fp8(x)
+    wq, sw = ops.quant_rows_fp8(W)
+    f8 = _time(lambda: ops.linear_fp8(xq, sx, wq, sw, b, act))
+    return {"op": "gemm", "M": M, "N": N, "K": K, "us": round(ours, 2), "tflops": round(flops / ours / 1e6, 1),
+            "hipblaslt_us": round(lib, 2), "hipblaslt_tflops": round(flops / lib / 1e6, 1),
+            "fp8_us": round(f8, 2), "fp8_tflops": round(flops / f8 / 1e6, 1)}
+
+
+def bench_embed(B, F=43, D=64, V=1_000_000, dev="cuda"):
+    table = torch.randn(V, D, device=dev).to(torch.bfloat16)
+    lin = torch.randn(V, device=dev)
+    ids = torch.randint(0, V, (B, F), device=dev, dtype=torch.int32)
+    wts = torch.rand(B, F, device=dev)
+    us = _time(lambda: ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True))
+    byts = B * F * (D * 2 * 2 + 4 + 4 + 4)
+    ref = _time(lambda: (table[ids.long()] * wts.unsqueeze(-1).to(torch.bfloat16)).view(B, -1))
+    return {"op": "embed_fm", "B": B, "F": F, "D": D, "us": round(us, 2), "GBps": round(byts / us / 1e3, 1),
+            "torch_gather_us": round(ref, 2)}
+
+
+def bench_model(family, B, dev="cuda", graphs=True):
+    from ..config import ModelConfig
+    from ..models import build_model
+
+    cfg = ModelConfig(family=family)
+    if family == "dlrm":
+        cfg.table_rows = 1_000_000
+    m = build_model(cfg, dev)
+    ids = torch.randint(0, 1 << 30, (B, cfg.num_fields), device=dev)
+    wts = torch.rand(B, cfg.num_fields, device=dev)
+    eager = _time(lambda: m(ids, wts), iters=20)
+    out = {"op": f"model_{family}", "B": B, "eager_us": round(eager, 1)}
+    if graphs:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m(ids, wts)
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g):
+            m(ids, wts)
+        gt = _time(lambda: g.replay(), iters=50)
+        out["graph_us"] = round(gt, 1)
+        out["Mscores_per_s"] = round(B / gt, 2)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    shapes = [(512, 1024, 2752), (512, 512, 1024), (512, 256, 512), (4096, 1024, 2752), (8192, 1024, 2752),
+              (4096, 2752, 2752)]
+    if a.quick:
+        shapes = shapes[:2]
+    for s in shapes:
+        print(json.dumps(bench_gemm(*s)), flush=True)
+    for B in ([512] if a.quick else [512, 4096, 8192]):
+        print(json.dumps(bench_embed(B)), flush=True)
+    for fam in (["deepfm"] if a.quick else ["deepfm", "dcn", "dcn_v2", "wdl", "dlrm"]):
+        for B in ([512] if a.quick else [512, 4096]):
+            print(json.dumps(bench_model(fam, B)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

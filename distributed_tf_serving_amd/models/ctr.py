@@ -1,0 +1,267 @@
+"""CTR model families served by a shard backend.
+
+The reference serves a SavedModel called "DCN" whose inputs are
+``feat_ids`` int64 [B, F] and ``feat_wts`` float [B, F] and whose output
+``prediction_node`` is one CTR per candidate (reference DCNClient.java:33-35,
+97-108, 162). The graph itself is external (TF-Serving); SURVEY.md §2.2 E4
+lists the implied compute. Every family below consumes exactly that input
+signature (libsvm-style: an id and a weight per field; for DLRM the leading
+``num_dense`` fields carry dense values in ``feat_wts``) and produces
+sigmoid CTR scores, so any of them can stand behind the reference client.
+
+Forward passes are built only from :mod:`distributed_tf_serving_amd.ops`, so
+GPU tensors run the gfx950 kernels and CPU tensors run the fp32 reference
+math. Weights are random-init from ``cfg.seed`` (no checkpoints exist).
+
+===========  ==========================================================
+family       forward
+===========  ==========================================================
+wdl          sigmoid(wide(ids, wts) + head(MLP(emb)))
+deepfm       sigmoid(FM1 + FM2 + head(MLP(emb)))
+dcn          sigmoid(w_c . cross_v1^L(emb) + head(MLP(emb)))
+dcn_v2       sigmoid(w_c . cross_v2^L(emb) + head(MLP(emb)))  (fp8 towers opt.)
+dlrm         sigmoid(head(topMLP(dot(botMLP(dense), emb_t))))
+===========  ==========================================================
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from .. import ops
+from ..config import ModelConfig
+from .layers import DTYPES, MLP, Dense, init_uniform_, make_generator, pad8
+
+
+class CTRModel(nn.Module):
+    """Base: holds config, exposes ``forward(ids, wts) -> CTR [B] fp32``."""
+
+    family = "base"
+
+    def __init__(self, cfg: ModelConfig, device="cpu"):
+        super().__init__()
+        self.cfg = cfg
+        self.device_ = torch.device(device)
+        self.dtype = DTYPES[cfg.param_dtype]
+        self.gen = make_generator(cfg.seed, self.device_)
+
+    # -- metadata ----------------------------------------------------------
+    def signature(self) -> Dict[str, Dict]:
+        F = self.cfg.num_fields
+        return {
+            "inputs": {"feat_ids": ("DT_INT64", [-1, F]), "feat_wts": ("DT_FLOAT", [-1, F])},
+            "outputs": {"prediction_node": ("DT_FLOAT", [-1])},
+            "method_name": "tensorflow/serving/predict",
+        }
+
+    def param_bytes(self) -> int:
+        n = sum(p.numel() * p.element_size() for p in self.parameters())
+        n += sum(b.numel() * b.element_size() for b in self.buffers())
+        return n
+
+    def _embedding_table(self, rows: int, dim: int) -> nn.Parameter:
+        t = torch.empty(rows, dim, dtype=self.dtype, device=self.device_)
+        init_uniform_(t, 1.0 / math.sqrt(dim), self.gen)
+        return nn.Parameter(t, requires_grad=False)
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor]) -> torch.Tensor:
+        if wts is not None and wts.dtype != torch.float32:
+            wts = wts.float()
+        return self._forward(ids, wts)
+
+    def _forward(self, ids, wts):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+
+class WideDeep(CTRModel):
+    family = "wdl"
+
+    def __init__(self, cfg: ModelConfig, device="cpu"):
+        super().__init__(cfg, device)
+        V, D, F = cfg.vocab_size, cfg.embed_dim, cfg.num_fields
+        self.emb = self._embedding_table(V, D)
+        self.wide = nn.Parameter(init_uniform_(torch.empty(V, device=self.device_), 0.05, self.gen), requires_grad=False)
+        self.wide_bias = 0.0
+        self.mlp = MLP(F * D, cfg.mlp_dims, self.dtype, self.device_, self.gen)
+        self.head_w = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
+                                   requires_grad=False)
+        self.head_b = 0.0
+
+    def _forward(self, ids, wts):
+        x, wide = ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
+                            want_x=True, want_fm=True, fm2=False)
+        h = self.mlp(x)
+        return ops.head(h, self.head_w, self.head_b, extra=wide, sigmoid=True)
+
+
+class DeepFM(CTRModel):
+    family = "deepfm"
+
+    def __init__(self, cfg: ModelConfig, device="cpu"):
+        super().__init__(cfg, device)
+        V, D, F = cfg.vocab_size, cfg.embed_dim, cfg.num_fields
+        self.emb = self._embedding_table(V, D)
+        self.lin = nn.Parameter(init_uniform_(torch.empty(V, device=self.device_), 0.01, self.gen), requires_grad=False)
+        self.fm_bias = 0.0
+        self.mlp = MLP(F * D, cfg.mlp_dims, self.dtype, self.device_, self.gen, fp8=cfg.gemm_dtype == "fp8")
+        self.head_w = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
+                                   requires_grad=False)
+        self.head_b = 0.0
+
+    def _forward(self, ids, wts):
+        x, fm = ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
+                          want_x=True, want_fm=True, fm2=True)
+        h = self.mlp(x)
+        return ops.head(h, self.head_w, self.head_b, extra=fm, sigmoid=True)
+
+
+class DCN(CTRModel):
+    """Deep & Cross Network (v1) - the reference's served model name."""
+
+    family = "dcn"
+
+    def __init__(self, cfg: ModelConfig, device="cpu"):
+        super().__init__(cfg, device)
+        V, D, F, L = cfg.vocab_size, cfg.embed_dim, cfg.num_fields, cfg.num_cross_layers
+        d = F * D
+        self.emb = self._embedding_table(V, D)
+        self.cross_w = nn.Parameter(init_uniform_(torch.empty(L, d, device=self.device_), 1.0 / math.sqrt(d), self.gen),
+                                    requires_grad=False)
+        self.cross_b = nn.Parameter(torch.zeros(L, d, device=self.device_), requires_grad=False)
+        self.mlp = MLP(d, cfg.mlp_dims, self.dtype, self.device_, self.gen)
+        # head over concat(x_L, h): split into the cross part (fused into K3) and the deep part (K6)
+        self.head_wc = nn.Parameter(init_uniform_(torch.empty(d, device=self.device_), 0.5 / math.sqrt(d), self.gen),
+                                    requires_grad=False)
+        self.head_wd = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
+                                    requires_grad=False)
+        self.head_b = 0.0
+
+    def _forward(self, ids, wts):
+        x, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
+        _, cross_logit = ops.cross_v1(x, self.cross_w, self.cross_b, want_x=False, head_w=self.head_wc)
+        h = self.mlp(x)
+        return ops.head(h, self.head_wd, self.head_b, extra=cross_logit, sigmoid=True)
+
+
+class DCNv2(CTRModel):
+    """DCN-v2: full-rank (or low-rank) matrix cross layers; optional fp8 towers."""
+
+    family = "dcn_v2"
+
+    def __init__(self, cfg: ModelConfig, device="cpu"):
+        super().__init__(cfg, device)
+        V, D, F, L = cfg.vocab_size, cfg.embed_dim, cfg.num_fields, cfg.num_cross_layers
+        d = F * D
+        self.d = d
+        self.fp8 = cfg.gemm_dtype == "fp8"
+        self.emb = self._embedding_table(V, D)
+        self.low_rank = cfg.cross_rank > 0
+        if self.low_rank:
+            r = pad8(cfg.cross_rank)
+            self.cross_v = nn.ModuleList([Dense(d, r, "none", self.dtype, self.device_, self.gen, fp8=self.fp8)
+                                          for _ in range(L)])
+            self.cross_u = nn.ModuleList([Dense(r, d, "none", self.dtype, self.device_, self.gen) for _ in range(L)])
+        else:
+            self.cross = nn.ModuleList([Dense(d, d, "none", self.dtype, self.device_, self.gen, fp8=self.fp8)
+                                        for _ in range(L)])
+            for layer in self.cross:  # keep the stacked product well-conditioned
+                layer.weight.data.mul_(0.5)
+                if self.fp8:
+                    layer.quantize_fp8()
+        self.mlp = MLP(d, cfg.mlp_dims, self.dtype, self.device_, self.gen, fp8=self.fp8)
+        self.head_wc = nn.Parameter(init_uniform_(torch.empty(d, device=self.device_), 0.5 / math.sqrt(d), self.gen),
+                                    requires_grad=False)
+        self.head_wd = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
+                                    requires_grad=False)
+        self.head_b = 0.0
+
+    def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor) -> torch.Tensor:
+        if self.low_rank:
+            # x0 * (U (V xl) + b) + xl : the cross epilogue rides on the U GEMM
+            v = self.cross_v[i](xl)
+            u = self.cross_u[i]
+            return ops.cross_v2(x0, xl, u.weight, u.bias, a=v)
+        layer = self.cross[i]
+        if self.fp8:
+            xq, sx = ops.quant_rows_fp8(xl)
+            return ops.linear_fp8(xq, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
+        return ops.cross_v2(x0, xl, layer.weight, layer.bias)
+
+    def _forward(self, ids, wts):
+        x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
+        xl = x0
+        for i in range(self.cfg.num_cross_layers):
+            xl = self._cross_layer(i, x0, xl)
+        cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
+        h = self.mlp(x0)
+        return ops.head(h, self.head_wd, self.head_b, extra=cross_logit, sigmoid=True)
+
+
+class DLRM(CTRModel):
+    """DLRM: bottom MLP on dense fields, one table per sparse field, pairwise dot
+    interaction (K5, MFMA), top MLP. ``table_shards`` restricts the tables this
+    process materialises (embedding model parallelism, see parallel/)."""
+
+    family = "dlrm"
+
+    def __init__(self, cfg: ModelConfig, device="cpu", materialize_tables: bool = True):
+        super().__init__(cfg, device)
+        D, T = cfg.embed_dim, cfg.num_sparse
+        assert D == 64, "DLRM dot-interaction kernel is built for D = 64"
+        assert cfg.bottom_mlp[-1] == D, "bottom MLP must end at the embedding dim"
+        self.T = T
+        self.dense_k = pad8(cfg.num_dense)
+        self.bottom = MLP(cfg.num_dense, cfg.bottom_mlp, self.dtype, self.device_, self.gen)
+        self.inter_cols = ops.interaction_cols(T, D)
+        self.top = MLP(self.inter_cols, cfg.mlp_dims, self.dtype, self.device_, self.gen)
+        self.head_w = nn.Parameter(init_uniform_(torch.empty(self.top.out_dim, device=self.device_), 0.05, self.gen),
+                                   requires_grad=False)
+        self.head_b = 0.0
+        rows = cfg.table_rows
+        self.register_buffer("modulo_f", torch.full((T,), rows, dtype=torch.int64, device=self.device_),
+                             persistent=False)
+        self.register_buffer("offset_f", torch.arange(T, dtype=torch.int64, device=self.device_) * rows,
+                             persistent=False)
+        self.emb = self._embedding_table(T * rows, D) if materialize_tables else None
+
+    def dense_input(self, wts: torch.Tensor) -> torch.Tensor:
+        nd = self.cfg.num_dense
+        x = torch.zeros(wts.shape[0], self.dense_k, dtype=self.dtype, device=wts.device)
+        x[:, :nd] = wts[:, :nd]
+        return x
+
+    def sparse_ids(self, ids: torch.Tensor) -> torch.Tensor:
+        return ids[:, self.cfg.num_dense:].contiguous()
+
+    def lookup(self, ids: torch.Tensor) -> torch.Tensor:
+        """Local (single-process) lookup of every sparse field -> [B, T, D]."""
+        sp = self.sparse_ids(ids)
+        x, _ = ops.embed(self.emb, sp, None, modulo_f=self.modulo_f, offset_f=self.offset_f, want_x=True)
+        return x.view(ids.shape[0], self.T, self.cfg.embed_dim)
+
+    def interact_and_top(self, dense_out: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
+        z = ops.dot_interaction(dense_out, emb, self.inter_cols)
+        h = self.top(z)
+        return ops.head(h, self.head_w, self.head_b, sigmoid=True)
+
+    def _forward(self, ids, wts):
+        dense_out = self.bottom(self.dense_input(wts))
+        emb = self.lookup(ids)
+        return self.interact_and_top(dense_out, emb)
+
+
+FAMILIES = {c.family: c for c in (WideDeep, DeepFM, DCN, DCNv2, DLRM)}
+
+
+def build_model(cfg: ModelConfig, device="cpu", **kw) -> CTRModel:
+    try:
+        cls = FAMILIES[cfg.family]
+    except KeyError:
+        raise ValueError(f"unknown model family {cfg.family!r}; known: {sorted(FAMILIES)}") from None
+    m = cls(cfg, device=device, **kw).eval()
+    m.gen = None  # init-only RNG; keeps the module deep-copyable / movable
+    return m

@@ -1,0 +1,95 @@
+"""Parameter containers shared by the CTR model families.
+
+Weights are stored the way the kernels read them: embedding tables bf16
+[rows, D], dense weights bf16 [out, in] (reduction dim contiguous), biases and
+small vectors fp32. fp8 towers keep an OCP e4m3 copy of each weight with a
+per-output-channel fp32 scale.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+from torch import nn
+
+from .. import ops
+
+DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
+
+
+def pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def make_generator(seed: int, device) -> torch.Generator:
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return g
+
+
+def init_uniform_(t: torch.Tensor, bound: float, gen: torch.Generator) -> torch.Tensor:
+    with torch.no_grad():
+        if t.dtype in (torch.float32, torch.float64):
+            t.uniform_(-bound, bound, generator=gen)
+        else:  # draw in fp32 chunks to keep bf16 init device-side and bounded in memory
+            flat = t.view(-1)
+            step = 1 << 26
+            for i in range(0, flat.numel(), step):
+                n = min(step, flat.numel() - i)
+                buf = torch.empty(n, dtype=torch.float32, device=t.device).uniform_(-bound, bound, generator=gen)
+                flat[i:i + n].copy_(buf)
+    return t
+
+
+class Dense(nn.Module):
+    """One fully connected layer: y = act(x W^T + b) (K4 MFMA GEMM)."""
+
+    def __init__(self, in_dim: int, out_dim: int, act: str, dtype, device, gen, in_pad: Optional[int] = None,
+                 fp8: bool = False):
+        super().__init__()
+        self.in_dim, self.out_dim, self.act = in_dim, out_dim, act
+        self.k = in_pad if in_pad is not None else pad8(in_dim)
+        bound = math.sqrt(6.0 / (in_dim + out_dim)) * (math.sqrt(2.0) if act == "relu" else 1.0)
+        w = torch.zeros(out_dim, self.k, dtype=dtype, device=device)  # K padded to 16-byte rows
+        w[:, :in_dim].copy_(init_uniform_(torch.empty(out_dim, in_dim, device=device), bound, gen))
+        self.weight = nn.Parameter(w, requires_grad=False)
+        self.bias = nn.Parameter(init_uniform_(torch.empty(out_dim, dtype=torch.float32, device=device), 0.01, gen),
+                                 requires_grad=False)
+        self.fp8 = fp8
+        if fp8:
+            self.quantize_fp8()
+
+    def quantize_fp8(self) -> None:
+        wf = self.weight.float()
+        amax = wf.abs().amax(dim=1)
+        sw = torch.where(amax > 0, amax / ops.FP8_MAX, torch.ones_like(amax))
+        self.register_buffer("w_fp8", (wf / sw[:, None]).clamp(-ops.FP8_MAX, ops.FP8_MAX).to(torch.float8_e4m3fn),
+                             persistent=False)
+        self.register_buffer("w_scale", sw.contiguous(), persistent=False)
+        self.fp8 = True
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fp8:
+            xq, sx = ops.quant_rows_fp8(x)
+            return ops.linear_fp8(xq, sx, self.w_fp8, self.w_scale, self.bias, self.act)
+        return ops.linear(x, self.weight, self.bias, self.act)
+
+
+class MLP(nn.Module):
+    def __init__(self, in_dim: int, dims: Sequence[int], dtype, device, gen, fp8: bool = False,
+                 last_act: str = "relu"):
+        super().__init__()
+        layers: List[Dense] = []
+        d = in_dim
+        for i, h in enumerate(dims):
+            act = "relu" if i < len(dims) - 1 else last_act
+            layers.append(Dense(d, h, act, dtype, device, gen, fp8=fp8))
+            d = h
+        self.layers = nn.ModuleList(layers)
+        self.out_dim = d
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        for layer in self.layers:
+            x = layer(x)
+        return x

@@ -1,0 +1,233 @@
+"""CTR compute ops: gfx950 HIP kernels for GPU tensors, reference math on CPU.
+
+Every op dispatches on the device of its inputs:
+
+* GPU tensor -> the hand-written CDNA4 kernel in ``csrc/kernels`` (through the
+  ``_hip`` extension). There is no silent eager fallback: a missing extension
+  raises (see :mod:`._loader`).
+* CPU tensor -> the reference implementation in plain PyTorch (fp32 math).
+  This is both the CPU serving backend and the numerics oracle the GPU tests
+  compare against.
+
+Op inventory: K0 ``pack_ids``, K1 ``embed``, K1b
+``embedding_bag``, K2 FM (fused in ``embed``), K3 ``cross_v1``, K3b
+``cross_v2`` / ``linear_fp8``, K4 ``linear``, K5 ``dot_interaction``, K6
+``head``, K7 ``sort_scores``.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._loader import hip, hip_loaded, native  # noqa: F401
+
+_ACTS = {"none": 0, "relu": 1, "sigmoid": 2}
+
+FP8_MAX = 448.0  # OCP e4m3fn
+
+
+def _hash_rows(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None) -> torch.Tensor:
+    ids = ids.long()
+    if modulo_f is not None:
+        return offset_f.view(1, -1).to(ids.device) + torch.remainder(ids, modulo_f.view(1, -1).to(ids.device))
+    if modulo and modulo > 0:
+        return torch.remainder(ids, modulo)
+    return ids
+
+
+# ------------------------------------------------------------------ K0
+def pack_ids(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None) -> torch.Tensor:
+    """int64/int32 feature ids -> int32 table rows (``offset_f + id mod m``)."""
+    if ids.is_cuda:
+        return hip().pack_ids(ids.contiguous(), int(modulo), modulo_f, offset_f)
+    return _hash_rows(ids, modulo, modulo_f, offset_f).to(torch.int32)
+
+
+# ------------------------------------------------------------------ K1 (+K2)
+def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = None,
+          lin: Optional[torch.Tensor] = None, modulo: int = 0, modulo_f=None, offset_f=None,
+          bias: float = 0.0, want_x: bool = True, want_fm: bool = False, fm2: bool = False,
+          out_x: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """Weighted embedding gather with fused factorisation-machine terms.
+
+    x[b, f*D:(f+1)*D] = table[row(b, f)] * wts[b, f]
+    fm[b] = bias + sum_f lin[row]*wts  (if lin) + 0.5*sum_d((sum_f e)^2 - sum_f e^2)  (if fm2)
+    """
+    if ids.is_cuda:
+        if modulo_f is None and modulo <= 0:
+            modulo = table.shape[0]
+        x, fm = hip().embed(table, lin, ids.contiguous(), None if wts is None else wts.contiguous(), int(modulo),
+                            modulo_f, offset_f, float(bias), want_x, want_fm, fm2, out_x)
+        return (x if want_x else None), (fm if want_fm else None)
+    rows = _hash_rows(ids, modulo if modulo > 0 else table.shape[0], modulo_f, offset_f)
+    e = table[rows].float()  # [B, F, D]
+    if wts is not None:
+        e = e * wts.float().unsqueeze(-1)
+    x = None
+    if want_x:
+        x = e.reshape(e.shape[0], -1).to(table.dtype)
+        if out_x is not None:
+            out_x.copy_(x.view_as(out_x))
+            x = out_x
+    fm = None
+    if want_fm:
+        fm = torch.full((ids.shape[0],), float(bias), dtype=torch.float32)
+        if lin is not None:
+            w1 = lin[rows].float()
+            fm = fm + (w1 * (wts.float() if wts is not None else 1.0)).sum(1)
+        if fm2:
+            s = e.sum(1)
+            fm = fm + 0.5 * (s * s - (e * e).sum(1)).sum(1)
+    return x, fm
+
+
+# ------------------------------------------------------------------ K1b
+def embedding_bag(table: torch.Tensor, indices: torch.Tensor, offsets: torch.Tensor,
+                  per_sample_weights: Optional[torch.Tensor] = None, modulo: int = 0, mean: bool = False,
+                  out_bf16: bool = False) -> torch.Tensor:
+    """Sum (or mean) pooled multi-hot lookup; offsets are CSR [nbags + 1]."""
+    if table.is_cuda:
+        m = int(modulo) if modulo > 0 else table.shape[0]
+        return hip().embedding_bag(table, indices.contiguous(), offsets.contiguous(), per_sample_weights, m, mean,
+                                   out_bf16)
+    rows = _hash_rows(indices, modulo if modulo > 0 else table.shape[0])
+    out = torch.nn.functional.embedding_bag(rows, table.float(), offsets[:-1], mode="mean" if mean else "sum",
+                                            per_sample_weights=None if mean else per_sample_weights,
+                                            include_last_offset=False)
+    if mean and per_sample_weights is not None:
+        raise ValueError("per_sample_weights with mean pooling is not supported")
+    return out.to(torch.bfloat16) if out_bf16 else out
+
+
+# ------------------------------------------------------------------ K4 / K3b
+def linear(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, act: str = "none",
+           out_f32: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = act(x W^T + b) on MFMA (bf16 in, fp32 accumulate, bf16/fp32 out)."""
+    if x.is_cuda:
+        return hip().gemm(x, W, b, _ACTS[act], None, None, out_f32, None, None, out)
+    y = x.float() @ W.float().t()
+    if b is not None:
+        y = y + b.float()
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "sigmoid":
+        y = torch.sigmoid(y)
+    y = y if out_f32 else y.to(x.dtype if x.dtype != torch.float32 else torch.float32)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def cross_v2(x0: torch.Tensor, xl: torch.Tensor, W: torch.Tensor, b: torch.Tensor,
+             a: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """DCN-v2 cross layer x0 * (a W^T + b) + xl, fused in the GEMM epilogue.
+
+    ``a`` defaults to ``xl`` (full rank); the low-rank form passes a = V xl."""
+    a = xl if a is None else a
+    if x0.is_cuda:
+        return hip().gemm(a, W, b, 3, x0, xl, False, None, None, None)
+    y = a.float() @ W.float().t() + b.float()
+    return (x0.float() * y + xl.float()).to(x0.dtype)
+
+
+def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-row OCP e4m3 quantisation: (q, scale) with x ~= q * scale."""
+    if x.is_cuda:
+        return tuple(hip().quant_rows_fp8(x.contiguous()))
+    xf = x.float()
+    amax = xf.abs().amax(dim=1).clamp_min(0)
+    scale = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    q = (xf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, scale
+
+
+def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
+               b: Optional[torch.Tensor] = None, act: str = "none", out_f32: bool = False,
+               x0: Optional[torch.Tensor] = None, xl: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp8 x fp8 -> fp32-accumulated GEMM with row/channel scales (CDNA4 fp8 MFMA).
+
+    ``x0``/``xl`` given selects the DCN-v2 cross epilogue."""
+    epi = 3 if x0 is not None else _ACTS[act]
+    if xq.is_cuda:
+        return hip().gemm(xq, Wq, b, epi, x0, xl, out_f32, sx, sw, None)
+    y = (xq.float() * sx[:, None]) @ (Wq.float() * sw[:, None]).t()
+    if b is not None:
+        y = y + b.float()
+    if epi == 3:
+        y = x0.float() * y + xl.float()
+    elif act == "relu":
+        y = torch.relu(y)
+    elif act == "sigmoid":
+        y = torch.sigmoid(y)
+    return y if out_f32 else y.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------ K3
+def cross_v1(x0: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_x: bool = True,
+             head_w: Optional[torch.Tensor] = None):
+    """DCN cross network, all layers: x_{l+1} = x0 * (x_l . w_l) + b_l + x_l.
+
+    Returns (x_L or None, x_L . head_w or None)."""
+    if x0.is_cuda:
+        x, d = hip().cross_v1(x0.contiguous(), w, b, want_x, head_w)
+        return (x if want_x else None), (d if head_w is not None else None)
+    a0 = x0.float()
+    xl = a0
+    for l in range(w.shape[0]):
+        s = xl @ w[l].float()
+        xl = a0 * s[:, None] + b[l].float() + xl
+    dot = (xl @ head_w.float()) if head_w is not None else None
+    return (xl.to(x0.dtype) if want_x else None), dot
+
+
+# ------------------------------------------------------------------ K5
+def interaction_cols(num_sparse: int, dim: int = 64) -> int:
+    used = dim + (num_sparse + 1) * num_sparse // 2
+    return (used + 7) // 8 * 8
+
+
+def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0) -> torch.Tensor:
+    """DLRM: [dense | strictly-lower-triangular entries of X X^T | zero pad], X = [dense; emb]."""
+    T = emb.shape[1]
+    if out_cols <= 0:
+        out_cols = interaction_cols(T, dense.shape[1])
+    if dense.is_cuda:
+        return hip().dot_interaction(dense.contiguous(), emb.contiguous(), int(out_cols))
+    X = torch.cat([dense.float().unsqueeze(1), emb.float()], dim=1)  # [B, T+1, D]
+    Z = X @ X.transpose(1, 2)
+    li, lj = torch.tril_indices(T + 1, T + 1, offset=-1)
+    out = torch.zeros(dense.shape[0], out_cols, dtype=torch.float32)
+    out[:, : dense.shape[1]] = dense.float()
+    out[:, dense.shape[1]: dense.shape[1] + li.numel()] = Z[:, li, lj]
+    return out.to(dense.dtype)
+
+
+# ------------------------------------------------------------------ K6
+def head(x: torch.Tensor, w: torch.Tensor, bias: float = 0.0, extra: Optional[torch.Tensor] = None,
+         sigmoid: bool = True) -> torch.Tensor:
+    """CTR head: act(x . w + bias + extra) -> fp32 [M]."""
+    if x.is_cuda:
+        return hip().head(x.contiguous(), w, float(bias), extra, sigmoid)
+    y = x.float() @ w.float() + float(bias)
+    if extra is not None:
+        y = y + extra.float()
+    return torch.sigmoid(y) if sigmoid else y
+
+
+# ------------------------------------------------------------------ K7
+def sort_scores(scores: torch.Tensor, descending: bool = False, k: int = -1):
+    """Sorted scores + the candidate permutation (the reference drops the latter,
+    DCNClient.java:195). GPU: bitonic sort in LDS up to 8192 scores."""
+    n = scores.numel()
+    if k < 0 or k > n:
+        k = n
+    if scores.is_cuda and n <= hip().sort_max_elems():
+        s, p = hip().sort_scores(scores.contiguous().float(), descending, int(k))
+        return s, p
+    if scores.is_cuda:  # large lists: library sort (plain, not a hot fused op)
+        s, p = torch.sort(scores.float(), descending=descending, stable=True)
+        return s[:k], p[:k]
+    s, p = torch.sort(scores.float(), descending=descending, stable=True)
+    return s[:k], p[:k]

@@ -1,0 +1,217 @@
+"""Numerics of every gfx950 kernel against the fp32 PyTorch reference of the
+same op (the CPU path of distributed_tf_serving_amd.ops)."""
+import copy
+
+import pytest
+import torch
+
+from distributed_tf_serving_amd import ops
+from distributed_tf_serving_amd.config import ModelConfig
+from distributed_tf_serving_amd.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol, atol, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad}/{a.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+def test_pack_ids(cuda):
+    ids = torch.randint(-(1 << 40), 1 << 40, (33, 43), dtype=torch.int64)
+    out = ops.pack_ids(ids.to(cuda), modulo=1000003)
+    assert out.dtype == torch.int32
+    assert torch.equal(out.cpu(), ops.pack_ids(ids, modulo=1000003))
+    mf = torch.randint(1, 1000, (43,), dtype=torch.int64)
+    of = torch.cumsum(mf, 0) - mf
+    out = ops.pack_ids(ids.to(cuda), modulo_f=mf.to(cuda), offset_f=of.to(cuda))
+    assert torch.equal(out.cpu(), ops.pack_ids(ids, modulo_f=mf, offset_f=of))
+
+
+@pytest.mark.parametrize("D", [8, 16, 32, 64, 128])
+@pytest.mark.parametrize("F", [1, 43, 70])
+def test_embed_fm(cuda, D, F):
+    V, B = 5000, 37
+    g = torch.Generator().manual_seed(D * 100 + F)
+    table = (torch.rand(V, D, generator=g) - 0.5).to(torch.bfloat16)
+    lin = torch.rand(V, generator=g) - 0.5
+    ids = torch.randint(-10**9, 10**9, (B, F), generator=g)
+    wts = torch.rand(B, F, generator=g) * 2
+    for ids_dt in (torch.int64, torch.int32):
+        x, fm = ops.embed(table.to(cuda), ids.to(ids_dt).to(cuda), wts.to(cuda), lin=lin.to(cuda), modulo=V,
+                          bias=0.25, want_x=True, want_fm=True, fm2=True)
+        xr, fmr = ops.embed(table, ids.to(ids_dt), wts, lin=lin, modulo=V, bias=0.25, want_x=True, want_fm=True,
+                            fm2=True)
+        _close(x, xr, 1e-2, 1e-3, "x")
+        _close(fm, fmr, 2e-3, 2e-3 * F, "fm")
+    # no weights, no lin, only first-order off
+    x, fm = ops.embed(table.to(cuda), ids.to(cuda), None, modulo=V, want_x=True, want_fm=True, fm2=False)
+    xr, fmr = ops.embed(table, ids, None, modulo=V, want_x=True, want_fm=True, fm2=False)
+    _close(x, xr, 1e-2, 1e-3, "x nowts")
+    _close(fm, fmr, 1e-5, 1e-5, "bias only")
+
+
+def test_embed_per_field_tables(cuda):
+    T, rows, D, B = 30, 1000, 64, 19
+    table = (torch.rand(T * rows, D) - 0.5).to(torch.bfloat16)
+    mf = torch.full((T,), rows, dtype=torch.int64)
+    of = torch.arange(T, dtype=torch.int64) * rows
+    ids = torch.randint(0, 10**7, (B, T))
+    x, _ = ops.embed(table.to(cuda), ids.to(cuda), None, modulo_f=mf.to(cuda), offset_f=of.to(cuda))
+    xr, _ = ops.embed(table, ids, None, modulo_f=mf, offset_f=of)
+    _close(x, xr, 0, 0, "per-field")
+
+
+@pytest.mark.parametrize("mean", [False, True])
+def test_embedding_bag(cuda, mean):
+    R, D, nb = 3000, 64, 41
+    table = (torch.rand(R, D) - 0.5).to(torch.bfloat16)
+    lens = torch.randint(0, 9, (nb,))
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lens, 0)])
+    idx = torch.randint(0, 10**6, (int(offsets[-1]),))
+    psw = None if mean else torch.rand(idx.numel())
+    out = ops.embedding_bag(table.to(cuda), idx.to(cuda), offsets.to(cuda),
+                            None if psw is None else psw.to(cuda), modulo=R, mean=mean)
+    ref = ops.embedding_bag(table, idx, offsets, psw, modulo=R, mean=mean)
+    _close(out, ref, 1e-4, 1e-4, "bag")
+
+
+GEMM_SHAPES = [(1, 1024, 2752), (37, 256, 512), (100, 64, 16), (512, 1024, 2752), (513, 512, 1024),
+               (2048, 1024, 2752), (4096, 256, 512), (8192, 512, 1024), (300, 2752, 2752)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid"])
+def test_gemm_bf16(cuda, M, N, K, act):
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g)).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.linear(x.to(cuda), W.to(cuda), b.to(cuda), act, out_f32=True)
+    ref = ops.linear(x, W, b, act, out_f32=True)
+    _close(y, ref, 2e-3, 2e-3, f"gemm {M}x{N}x{K} {act}")
+    yb = ops.linear(x.to(cuda), W.to(cuda), b.to(cuda), act)
+    assert yb.dtype == torch.bfloat16
+    _close(yb, ref, 1e-2, 1e-2, "gemm bf16 out")
+
+
+def test_gemm_layout_asymmetric(cuda):
+    # A = I (padded), W asymmetric: C must equal W^T exactly (catches row/col swaps)
+    M = N = 64
+    K = 64
+    A = torch.eye(M, K).to(torch.bfloat16)
+    W = torch.arange(N * K, dtype=torch.float32).view(N, K).remainder(97).to(torch.bfloat16)
+    C = ops.linear(A.to(cuda), W.to(cuda), None, out_f32=True).cpu()
+    assert torch.equal(C, W.float().t())
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 128), (37, 256, 512), (512, 1024, 2752), (2048, 512, 1024)])
+def test_gemm_fp8(cuda, M, N, K):
+    g = torch.Generator().manual_seed(7 + M)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16) / K ** 0.5
+    xq, sx = ops.quant_rows_fp8(x)
+    wq, sw = ops.quant_rows_fp8(W.to(torch.bfloat16))
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.linear_fp8(xq.to(cuda), sx.to(cuda), wq.to(cuda), sw.to(cuda), b.to(cuda), "relu", out_f32=True)
+    ref = ops.linear_fp8(xq, sx, wq, sw, b, "relu", out_f32=True)
+    _close(y, ref, 2e-3, 2e-3, "fp8 gemm")
+
+
+def test_quant_rows_fp8(cuda):
+    x = (torch.randn(77, 2752) * 3).to(torch.bfloat16)
+    q, s = ops.quant_rows_fp8(x.to(cuda))
+    qr, sr = ops.quant_rows_fp8(x)
+    _close(s, sr, 1e-6, 0, "scale")
+    deq = q.cpu().float() * s.cpu()[:, None]
+    deqr = qr.float() * sr[:, None]
+    # at most one e4m3 ulp apart (multiply-by-reciprocal vs divide): 3 mantissa
+    # bits = 1/8 relative at the bottom of a binade
+    _close(deq, deqr, 0.126, 1e-6, "fp8 values")
+    exact = (deq == deqr).float().mean().item()
+    assert exact > 0.99, f"only {exact:.4f} of fp8 values bit-identical"
+
+
+def test_cross_v2_epilogue(cuda):
+    M, d = 130, 256
+    x0 = torch.randn(M, d).to(torch.bfloat16)
+    xl = torch.randn(M, d).to(torch.bfloat16)
+    W = (torch.randn(d, d) / d ** 0.5).to(torch.bfloat16)
+    b = torch.randn(d) * 0.1
+    y = ops.cross_v2(x0.to(cuda), xl.to(cuda), W.to(cuda), b.to(cuda))
+    ref = ops.cross_v2(x0, xl, W, b)
+    _close(y, ref, 2e-2, 2e-2, "cross_v2")
+
+
+@pytest.mark.parametrize("d", [64, 2752, 4096])
+def test_cross_v1(cuda, d):
+    B, L = 45, 3
+    x0 = (torch.randn(B, d) * 0.1).to(torch.bfloat16)
+    w = torch.randn(L, d) / d ** 0.5
+    b = torch.randn(L, d) * 0.01
+    hw = torch.randn(d) / d ** 0.5
+    x, dot = ops.cross_v1(x0.to(cuda), w.to(cuda), b.to(cuda), want_x=True, head_w=hw.to(cuda))
+    xr, dr = ops.cross_v1(x0, w, b, want_x=True, head_w=hw)
+    _close(x, xr, 1e-2, 1e-3, "cross_v1 x")
+    _close(dot, dr, 1e-3, 1e-3, "cross_v1 dot")
+
+
+@pytest.mark.parametrize("T", [1, 26, 30, 31])
+def test_dot_interaction(cuda, T):
+    B = 23
+    dense = torch.randn(B, 64).to(torch.bfloat16)
+    emb = torch.randn(B, T, 64).to(torch.bfloat16)
+    z = ops.dot_interaction(dense.to(cuda), emb.to(cuda))
+    zr = ops.dot_interaction(dense, emb)
+    assert z.shape == zr.shape
+    _close(z, zr, 1e-2, 5e-2, "dot")
+
+
+def test_head(cuda):
+    x = torch.randn(101, 256).to(torch.bfloat16)
+    w = torch.randn(256) * 0.05
+    e = torch.randn(101)
+    y = ops.head(x.to(cuda), w.to(cuda), 0.3, e.to(cuda), True)
+    _close(y, ops.head(x, w, 0.3, e, True), 1e-5, 1e-5, "head")
+
+
+@pytest.mark.parametrize("n", [1, 7, 1500, 4096, 8192])
+@pytest.mark.parametrize("desc", [False, True])
+def test_sort(cuda, n, desc):
+    s = torch.rand(n)
+    s[: n // 3] = s[n // 3: 2 * (n // 3)]  # ties
+    v, p = ops.sort_scores(s.to(cuda), descending=desc)
+    vr, pr = torch.sort(s, descending=desc, stable=True)
+    assert torch.equal(v.cpu(), vr)
+    assert torch.equal(s[p.cpu()], vr)
+    v, p = ops.sort_scores(s.to(cuda), descending=True, k=min(10, n))
+    assert torch.equal(v.cpu(), torch.sort(s, descending=True).values[: min(10, n)])
+
+
+@pytest.mark.parametrize("family", ["wdl", "deepfm", "dcn", "dcn_v2", "dlrm"])
+def test_models_gpu_vs_cpu(cuda, family):
+    cfg = ModelConfig(family=family, vocab_size=20000, table_rows=1000, embed_dim=64 if family == "dlrm" else 32,
+                      mlp_dims=(256, 128), bottom_mlp=(64, 64), num_cross_layers=2)
+    m = build_model(cfg, "cpu")
+    mg = copy.deepcopy(m).to(cuda)
+    ids = torch.randint(0, 10**9, (300, 43))
+    wts = torch.rand(300, 43)
+    y = mg(ids.to(cuda), wts.to(cuda))
+    yr = m(ids, wts)
+    _close(y, yr, 2e-2, 5e-3, family)
+
+
+def test_dcn_v2_fp8_close_to_bf16(cuda):
+    base = ModelConfig(family="dcn_v2", vocab_size=20000, embed_dim=32, mlp_dims=(256, 128), num_cross_layers=2)
+    m16 = build_model(base, "cpu").to(cuda)
+    f8 = copy.deepcopy(base)
+    f8.gemm_dtype = "fp8"
+    m8 = build_model(f8, "cpu").to(cuda)
+    ids = torch.randint(0, 10**9, (256, 43), device=cuda)
+    wts = torch.rand(256, 43, device=cuda)
+    a, b = m16(ids, wts), m8(ids, wts)
+    assert (a - b).abs().max().item() < 0.05
