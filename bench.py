@@ -1,0 +1,213 @@
+#!/usr/bin/env python
+"""Flagship serving benchmark: DeepFM CTR fan-out over N MI355X GPUs.
+
+Metric (BASELINE.json): CTR scores/sec for the whole node (+ request latency).
+Config: DeepFM-style CTR, 1M x 64 bf16 embeddings, 43 fields, 3-layer MLP
+(1024-512-256), client requests of 512 candidates (BASELINE config 2), fanned
+out over N GPUs with RCCL all-to-all over xGMI (config 3 at N=4).
+
+One timed step, on every rank, is a full serving round:
+
+  1. decode ``R`` serialized PredictRequests (512 candidates each; synthetic
+     Zipf feature ids, uniform weights; TF ``tensor_content`` encoding) with the
+     native codec straight into a pinned packed-row buffer (worker threads);
+  2. H2D -> RCCL all-to-all of candidate rows over all GPUs -> DeepFM forward
+     (gfx950 kernels, one HIP graph) -> all-to-all of scores back -> D2H;
+  3. encode R PredictResponses (``prediction_node`` float_val).
+
+Decode of step k+1 and encode of step k-1 overlap step k's GPU work (two
+pipeline slots); nothing is cached across steps (every step decodes and scores
+new request bytes from a rotating pool of distinct requests). Per-GPU work is
+fixed as N grows (weak scaling): global batch = N * R * 512 candidates/step.
+
+Launch: ``python bench.py`` (1 GPU) or, for N GPUs,
+``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
+127.0.0.1 --master-port P bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+from distributed_tf_serving_amd.config import ModelConfig  # noqa: E402
+from distributed_tf_serving_amd.models import build_model  # noqa: E402
+from distributed_tf_serving_amd.ops import native  # noqa: E402
+from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown  # noqa: E402
+from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E402
+from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E402
+from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
+from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
+
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--model", default="deepfm", choices=["deepfm", "dcn", "dcn_v2", "wdl", "dlrm"])
+    ap.add_argument("--request-rows", type=int, default=512, help="candidates per client request (config batch)")
+    ap.add_argument("--requests-per-gpu", type=int, default=16, help="requests coalesced per GPU per step")
+    ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"])
+    ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
+                    help="raw = tensor_content; packed = int64_val/float_val like the reference client")
+    ap.add_argument("--decode-threads", type=int, default=4)
+    ap.add_argument("--pool", type=int, default=8, help="distinct pre-serialized steps per rank")
+    ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
+    return ap.parse_args()
+
+
+def main():
+    a = parse_args()
+    ctx = init_from_env()
+    world, rank = ctx.world, ctx.rank
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = ctx.device
+    torch.manual_seed(1234)
+
+    cfg = ModelConfig(family=a.model, gemm_dtype=a.gemm_dtype)
+    if a.model == "dlrm":
+        cfg.table_rows = 1_000_000
+    model = build_model(cfg, dev)
+    F = cfg.num_fields
+    layout = PackedLayout(F)
+    B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
+    ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=2)
+    eng = FanoutEngine(ex, ctx, mode=a.mode)
+    eng.prepare(B)
+    nat = native()
+
+    rows_in = eng.contrib_rows(B)
+    n_req = rows_in // a.request_rows
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + rank)
+    pool = []
+    for _ in range(max(1, a.pool)):
+        pool.append([synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n_req)])
+
+    threads = max(1, a.decode_threads)
+    tp = cf.ThreadPoolExecutor(max_workers=threads + 1)
+
+    def decode(k: int, slot: int):
+        reqs = pool[k % len(pool)]
+        if not reqs:
+            return None
+        pb = nat.parse_batch(reqs, "feat_ids", "feat_wts", F)
+        buf = eng.host_in(B, slot)
+        ids_v, wts_v = layout.ids(buf), layout.wts(buf)
+        n = len(reqs)
+        if threads == 1 or n == 1:
+            pb.decode(ids_v, wts_v, 0, n)
+        else:
+            step = (n + threads - 1) // threads
+            futs = [tp.submit(pb.decode, ids_v, wts_v, s, min(n, s + step)) for s in range(0, n, step)]
+            for f in futs:
+                f.result()
+        errs = [e for e in pb.errors if e]
+        if errs:
+            raise RuntimeError(errs[0])
+        return pb
+
+    def encode(pb, scores: torch.Tensor):
+        if pb is None:
+            return []
+        return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores,
+                                          list(pb.rows), list(pb.offsets))
+
+    lat = []
+
+    def run(n_steps: int, record: bool):
+        pbs = {0: decode(0, 0)}
+        t_dec = {0: time.perf_counter()}
+        pending_enc = None
+        for k in range(n_steps):
+            slot = k % 2
+            h = eng.launch(B, slot)
+            nxt = tp.submit(decode, k + 1, (k + 1) % 2) if k + 1 < n_steps else None
+            t_next = time.perf_counter()
+            if pending_enc is not None:
+                pending_enc.result()
+            scores = h.wait()
+            pending_enc = tp.submit(encode, pbs.pop(k), scores)
+            if record:
+                lat.append(time.perf_counter() - t_dec.pop(k))
+            else:
+                t_dec.pop(k)
+            if nxt is not None:
+                pbs[k + 1] = nxt.result()
+                t_dec[k + 1] = t_next
+        if pending_enc is not None:
+            pending_enc.result()
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if ctx.is_distributed:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    run(max(1, a.warmup), record=False)
+    sync()
+    t0 = time.perf_counter()
+    run(a.steps, record=True)
+    sync()
+    el = time.perf_counter() - t0
+
+    t = torch.tensor([el], dtype=torch.float64, device=dev if ctx.backend == "nccl" else "cpu")
+    if ctx.is_distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+    total_scores = world * B * a.steps
+    value = total_scores / el_max
+    p50 = statistics.median(lat) * 1e3 if lat else None
+    p99 = float(np.percentile(lat, 99)) * 1e3 if lat else None
+    if rank == 0:
+        out = {
+            "metric": "CTR scores/sec (whole node)",
+            "value": round(value, 1),
+            "unit": "scores/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el_max / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
+            "dtype": "bf16" if a.gemm_dtype == "bf16" else "fp8",
+            "data": "synthetic (zipf feature ids over 2^40, uniform weights; random-init weights)",
+            "config": {
+                "model": f"{a.model} (1Mx64 emb, 43 fields, MLP 1024-512-256)" if a.model == "deepfm" else a.model,
+                "global_batch": world * B,
+                "request_rows": a.request_rows,
+                "requests_per_gpu_per_step": a.requests_per_gpu,
+                "seq_len": None,
+                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL)",
+                "encoding": a.encoding,
+            },
+            "p50_request_ms": None if p50 is None else round(p50, 3),
+            "p99_request_ms": None if p99 is None else round(p99, 3),
+        }
+        print(json.dumps(out), flush=True)
+    tp.shutdown(wait=True)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

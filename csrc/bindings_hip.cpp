@@ -58,10 +58,13 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
                                  c10::optional<torch::Tensor> offset_f, double bias, bool want_x, bool want_fm,
                                  bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables) {
   check_dev(table, "table");
-  check_dev(ids, "ids");
+  TORCH_CHECK(ids.is_cuda(), "ids must be a GPU tensor");
   TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
   TORCH_CHECK(ids.dim() == 2, "ids must be [B, F]");
   TORCH_CHECK(ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32, "ids must be int32/int64");
+  // ids / wts may be row views of a packed request buffer: unit inner stride,
+  // any row stride >= F
+  TORCH_CHECK(ids.stride(1) == 1 && ids.stride(0) >= ids.size(1), "ids rows must be contiguous");
   const int64_t B = ids.size(0), F = ids.size(1), D = table.size(1);
   TORCH_CHECK(D == 8 || D == 16 || D == 32 || D == 64 || D == 128, "embedding dim must be 8/16/32/64/128");
   check_same_dev(table, ids, "ids");
@@ -86,8 +89,10 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
     TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]: ids are hashed onto rows");
   }
   if (wts) {
-    check_dev(*wts, "wts");
-    TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->sizes() == ids.sizes(), "wts must be fp32 [B, F]");
+    TORCH_CHECK(wts->is_cuda() && wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->size(0) == B &&
+                    wts->size(1) == F && wts->stride(1) == 1 && wts->stride(0) >= F,
+                "wts must be fp32 [B, F] with contiguous rows");
+    check_same_dev(table, *wts, "wts");
   }
   if (lin) {
     check_dev(*lin, "lin");
@@ -105,13 +110,27 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
     }
   }
   if (want_fm) fm = torch::empty({B}, table.options().dtype(torch::kFloat32));
-  check_hip(dtfs::launch_embed(table.data_ptr(), lin ? lin->data_ptr<float>() : nullptr, ids.data_ptr(),
-                               ids.scalar_type() == torch::kInt64, wts ? wts->data_ptr<float>() : nullptr, int(B),
-                               int(F), int(D), V, modulo, modulo_f ? modulo_f->data_ptr<int64_t>() : nullptr,
-                               offset_f ? offset_f->data_ptr<int64_t>() : nullptr, float(bias),
-                               want_x ? x.data_ptr() : nullptr, want_fm ? fm.data_ptr<float>() : nullptr, fm2,
-                               cur_stream(ids)),
-            "embed");
+  dtfs::EmbedArgs a;
+  a.table = table.data_ptr();
+  a.lin = lin ? lin->data_ptr<float>() : nullptr;
+  a.ids = ids.data_ptr();
+  a.ids64 = ids.scalar_type() == torch::kInt64;
+  a.ids_ld = ids.stride(0);
+  a.wts = wts ? wts->data_ptr<float>() : nullptr;
+  a.wts_ld = wts ? wts->stride(0) : 0;
+  a.B = int(B);
+  a.F = int(F);
+  a.D = int(D);
+  a.V = V;
+  a.modulo = modulo;
+  a.modulo_f = modulo_f ? modulo_f->data_ptr<int64_t>() : nullptr;
+  a.offset_f = offset_f ? offset_f->data_ptr<int64_t>() : nullptr;
+  a.bias = float(bias);
+  a.out_x = want_x ? x.data_ptr() : nullptr;
+  a.x_ld = F * D;
+  a.out_fm = want_fm ? fm.data_ptr<float>() : nullptr;
+  a.fm2 = fm2 ? 1 : 0;
+  check_hip(dtfs::launch_embed(a, cur_stream(ids)), "embed");
   return {x, fm};
 }
 

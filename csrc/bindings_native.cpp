@@ -67,15 +67,32 @@ void decode_into(const ParsedRequest& r, const std::string& key, torch::Tensor d
                  int64_t id_modulo) {
   const wire::TensorView& t = r.get(key);
   if (t.unknown_rank) throw py::value_error("input '" + key + "' has unknown rank");
-  if (!dst.is_contiguous() || dst.device().type() != torch::kCPU)
-    throw py::value_error("decode destination must be a contiguous CPU tensor");
+  if (dst.device().type() != torch::kCPU) throw py::value_error("decode destination must be a CPU tensor");
   const int64_t n = t.num_elements();
-  if (offset < 0 || offset + n > dst.numel())
-    throw py::value_error("decode destination too small for input '" + key + "'");
   wire::DecodeOpts o;
   o.dst = dst_type_of(dst);
   o.id_modulo = id_modulo;
-  char* base = static_cast<char*>(dst.data_ptr()) + offset * dst.element_size();
+  char* base;
+  if (dst.dim() == 2 && !dst.is_contiguous()) {
+    // row view into a packed buffer: offset counts rows; input must be [rows, cols]
+    if (dst.stride(1) != 1 || dst.stride(0) < dst.size(1))
+      throw py::value_error("decode destination rows must have unit inner stride");
+    const int64_t cols = dst.size(1);
+    if (t.shape.empty() || t.shape.back() != cols)
+      throw py::value_error("input '" + key + "' last dim does not match the destination row width");
+    const int64_t rows = n / cols;
+    if (offset < 0 || offset + rows > dst.size(0))
+      throw py::value_error("decode destination too small for input '" + key + "'");
+    o.cols = cols;
+    o.ld = dst.stride(0);
+    base = static_cast<char*>(dst.data_ptr()) + offset * dst.stride(0) * dst.element_size();
+  } else {
+    if (!dst.is_contiguous()) throw py::value_error("decode destination must be contiguous or a 2-D row view");
+    if (dst.dim() == 2) offset *= dst.size(1);  // 2-D contiguous: offset counts rows
+    if (offset < 0 || offset + n > dst.numel())
+      throw py::value_error("decode destination too small for input '" + key + "'");
+    base = static_cast<char*>(dst.data_ptr()) + offset * dst.element_size();
+  }
   std::string err;
   bool ok;
   {
@@ -83,6 +100,174 @@ void decode_into(const ParsedRequest& r, const std::string& key, torch::Tensor d
     ok = wire::decode_into(t, base, n, o, &err);
   }
   if (!ok) throw py::value_error("input '" + key + "': " + err);
+}
+
+// A batch of serialized PredictRequests parsed in one GIL-free pass. Rows of
+// request i land at rows [row_offset[i], row_offset[i] + rows[i]) of the batch
+// destination; malformed requests get rows = 0 and an error string instead of
+// failing the batch (the server answers them INVALID_ARGUMENT).
+struct ParsedBatch {
+  std::vector<py::bytes> holders;
+  std::vector<wire::PredictRequestView> views;
+  std::vector<const wire::TensorView*> ids_t, wts_t;
+  std::vector<int64_t> rows, offsets;
+  std::vector<std::string> errors;
+  std::string ids_key, wts_key;
+  int64_t fields = 0, total_rows = 0;
+};
+
+std::shared_ptr<ParsedBatch> parse_batch(const std::vector<py::bytes>& reqs, const std::string& ids_key,
+                                         const std::string& wts_key, int64_t fields) {
+  auto b = std::make_shared<ParsedBatch>();
+  const size_t n = reqs.size();
+  b->holders = reqs;
+  b->views.resize(n);
+  b->ids_t.assign(n, nullptr);
+  b->wts_t.assign(n, nullptr);
+  b->rows.assign(n, 0);
+  b->offsets.assign(n, 0);
+  b->errors.assign(n, std::string());
+  b->ids_key = ids_key;
+  b->wts_key = wts_key;
+  b->fields = fields;
+  std::vector<std::pair<const char*, size_t>> bufs(n);
+  for (size_t i = 0; i < n; ++i) {
+    char* p;
+    Py_ssize_t len;
+    if (PyBytes_AsStringAndSize(b->holders[i].ptr(), &p, &len) != 0) throw py::error_already_set();
+    bufs[i] = {p, size_t(len)};
+  }
+  {
+    py::gil_scoped_release nogil;
+    int64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+      std::string err;
+      auto& v = b->views[i];
+      if (!wire::parse_predict_request(reinterpret_cast<const uint8_t*>(bufs[i].first), bufs[i].second, &v, &err)) {
+        b->errors[i] = "malformed PredictRequest: " + err;
+        continue;
+      }
+      const wire::TensorView* ti = v.find(ids_key);
+      const wire::TensorView* tw = wts_key.empty() ? nullptr : v.find(wts_key);
+      if (!ti) {
+        b->errors[i] = "input '" + ids_key + "' missing";
+        continue;
+      }
+      if (!wts_key.empty() && !tw) {
+        b->errors[i] = "input '" + wts_key + "' missing";
+        continue;
+      }
+      if (ti->unknown_rank || ti->shape.size() != 2 || ti->shape[1] != fields || ti->shape[0] < 0) {
+        b->errors[i] = "input '" + ids_key + "' must have shape [B, " + std::to_string(fields) + "]";
+        continue;
+      }
+      if (tw && tw->shape != ti->shape) {
+        b->errors[i] = "input '" + wts_key + "' shape differs from '" + ids_key + "'";
+        continue;
+      }
+      const int64_t n_el = ti->num_elements();
+      if ((ti->content.n == 0 && ti->num_values > n_el) || (tw && tw->content.n == 0 && tw->num_values > n_el)) {
+        b->errors[i] = "more values than the tensor shape holds";
+        continue;
+      }
+      b->ids_t[i] = ti;
+      b->wts_t[i] = tw;
+      b->rows[i] = ti->shape[0];
+      b->offsets[i] = off;
+      off += ti->shape[0];
+    }
+    b->total_rows = off;
+  }
+  return b;
+}
+
+// Decode requests [begin, end) of the batch into row views ids_dst / wts_dst
+// (row offset = base_row + offsets[i]). Errors found while decoding are stored
+// per request. GIL released throughout: call from several threads on disjoint
+// request ranges.
+void decode_batch_range(ParsedBatch& b, torch::Tensor ids_dst, c10::optional<torch::Tensor> wts_dst, int64_t begin,
+                        int64_t end, int64_t base_row, int64_t id_modulo) {
+  auto check_dst = [&](const torch::Tensor& d, const char* what) {
+    if (d.device().type() != torch::kCPU || d.dim() != 2 || d.stride(1) != 1 || d.size(1) != b.fields)
+      throw py::value_error(std::string(what) + " destination must be a CPU [rows, fields] row view");
+    if (base_row < 0 || base_row + b.total_rows > d.size(0))
+      throw py::value_error(std::string(what) + " destination has too few rows for the batch");
+  };
+  check_dst(ids_dst, "ids");
+  if (wts_dst) check_dst(*wts_dst, "wts");
+  const wire::DstType it = dst_type_of(ids_dst);
+  const wire::DstType wt = wts_dst ? dst_type_of(*wts_dst) : wire::DstType::F32;
+  char* ibase = static_cast<char*>(ids_dst.data_ptr());
+  char* wbase = wts_dst ? static_cast<char*>(wts_dst->data_ptr()) : nullptr;
+  const int64_t ild = ids_dst.stride(0), wld = wts_dst ? wts_dst->stride(0) : 0;
+  const size_t ies = ids_dst.element_size(), wes = wts_dst ? wts_dst->element_size() : 0;
+  begin = std::max<int64_t>(0, begin);
+  end = std::min<int64_t>(end, int64_t(b.views.size()));
+  py::gil_scoped_release nogil;
+  for (int64_t i = begin; i < end; ++i) {
+    if (!b.ids_t[i] || b.rows[i] == 0) continue;
+    const int64_t row = base_row + b.offsets[i];
+    const int64_t n = b.rows[i] * b.fields;
+    std::string err;
+    wire::DecodeOpts o;
+    o.dst = it;
+    o.id_modulo = id_modulo;
+    o.cols = b.fields;
+    o.ld = ild;
+    if (!wire::decode_into(*b.ids_t[i], ibase + size_t(row * ild) * ies, n, o, &err)) {
+      b.errors[i] = "input '" + b.ids_key + "': " + err;
+      continue;
+    }
+    if (wbase) {
+      wire::DecodeOpts ow;
+      ow.dst = wt;
+      ow.cols = b.fields;
+      ow.ld = wld;
+      if (b.wts_t[i]) {
+        if (!wire::decode_into(*b.wts_t[i], wbase + size_t(row * wld) * wes, n, ow, &err))
+          b.errors[i] = "input '" + b.wts_key + "': " + err;
+      }
+    }
+  }
+}
+
+// One PredictResponse per request: outputs[key] = scores[offsets[i] : +rows[i]]
+// as float_val (what the reference client reads, DCNClient.java:162).
+std::vector<py::bytes> encode_batch_responses(const std::string& name, const std::string& sig, py::object version,
+                                              const std::string& key, torch::Tensor scores,
+                                              const std::vector<int64_t>& rows, const std::vector<int64_t>& offsets,
+                                              bool raw) {
+  if (scores.device().type() != torch::kCPU || scores.scalar_type() != torch::kFloat32 || !scores.is_contiguous())
+    throw py::value_error("scores must be a contiguous CPU fp32 tensor");
+  if (rows.size() != offsets.size()) throw py::value_error("rows/offsets length mismatch");
+  wire::ModelSpecOut spec;
+  spec.name = name;
+  spec.signature_name = sig;
+  if (!version.is_none()) {
+    spec.has_version = true;
+    spec.version = version.cast<int64_t>();
+  }
+  const float* s = scores.data_ptr<float>();
+  const int64_t ns = scores.numel();
+  std::vector<std::string> outs(rows.size());
+  {
+    py::gil_scoped_release nogil;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      if (offsets[i] < 0 || rows[i] < 0 || offsets[i] + rows[i] > ns) continue;
+      wire::TensorOut t;
+      t.key = key;
+      t.dtype = wire::DT_FLOAT;
+      t.shape = {rows[i]};
+      t.data = s + offsets[i];
+      t.n = rows[i];
+      t.raw = raw;
+      outs[i] = wire::encode_predict_response(spec, {t});
+    }
+  }
+  std::vector<py::bytes> res;
+  res.reserve(outs.size());
+  for (auto& o : outs) res.emplace_back(o);
+  return res;
 }
 
 std::vector<wire::TensorOut> tensors_out(const std::vector<std::pair<std::string, torch::Tensor>>& items,
@@ -147,6 +332,30 @@ PYBIND11_MODULE(_native, m) {
            "Decode input `key` (TF fill semantics) into dst[offset: offset+numel], narrowing dtypes.");
 
   m.def("parse_predict_request", &parse_request, py::arg("data"));
+
+  py::class_<ParsedBatch, std::shared_ptr<ParsedBatch>>(m, "ParsedBatch")
+      .def_readonly("rows", &ParsedBatch::rows)
+      .def_readonly("offsets", &ParsedBatch::offsets)
+      .def_readonly("errors", &ParsedBatch::errors)
+      .def_readonly("total_rows", &ParsedBatch::total_rows)
+      .def_readonly("fields", &ParsedBatch::fields)
+      .def("__len__", [](const ParsedBatch& b) { return b.views.size(); })
+      .def("model_name", [](const ParsedBatch& b, size_t i) { return b.views.at(i).model_name; })
+      .def("signature_name", [](const ParsedBatch& b, size_t i) { return b.views.at(i).signature_name; })
+      .def("version", [](const ParsedBatch& b, size_t i) -> py::object {
+        const auto& v = b.views.at(i);
+        return v.has_version ? py::object(py::int_(v.version)) : py::object(py::none());
+      })
+      .def("output_filter", [](const ParsedBatch& b, size_t i) { return b.views.at(i).output_filter; })
+      .def("decode", &decode_batch_range, py::arg("ids_dst"), py::arg("wts_dst"), py::arg("begin") = 0,
+           py::arg("end") = int64_t(1) << 62, py::arg("base_row") = 0, py::arg("id_modulo") = 0);
+
+  m.def("parse_batch", &parse_batch, py::arg("requests"), py::arg("ids_key") = "feat_ids",
+        py::arg("wts_key") = "feat_wts", py::arg("fields") = 43,
+        "Parse many serialized PredictRequests (GIL released); see ParsedBatch.decode.");
+  m.def("encode_batch_responses", &encode_batch_responses, py::arg("model_name"), py::arg("signature_name"),
+        py::arg("version"), py::arg("key"), py::arg("scores"), py::arg("rows"), py::arg("offsets"),
+        py::arg("raw") = false);
 
   m.def(
       "encode_predict_response",

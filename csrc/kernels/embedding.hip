@@ -33,17 +33,18 @@ __global__ void __launch_bounds__(256) pack_ids_kernel(const IdT* __restrict__ i
 // out_x[b, f*D + d] = table[row(b,f), d] * wts[b,f]              (bf16)
 // out_fm[b] = bias + sum_f lin[row]*w  (first order, if lin)
 //           + 0.5 * sum_d ((sum_f e)^2 - sum_f e^2)  (second order, if fm2)
+// ids / wts may be strided row views (ids_ld / wts_ld elements per row), so a
+// packed request row [ids int64 x F | wts fp32 x F | pad] is read in place.
 template <int D, typename IdT>
-__global__ void __launch_bounds__(256) embed_kernel(const bf16* __restrict__ table, const float* __restrict__ lin,
-                                                    const IdT* __restrict__ ids, const float* __restrict__ wts,
-                                                    int B, int F, int64_t V, int64_t modulo, const int64_t* __restrict__ modulo_f,
-                                                    const int64_t* __restrict__ offset_f, float bias,
-                                                    bf16* __restrict__ out_x, float* __restrict__ out_fm, int fm2) {
+__global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
   constexpr int LPR = D / 8;          // lanes per table row (16 B each)
   constexpr int FPI = kWave / LPR;    // fields per wave-wide load
+  const bf16* __restrict__ table = static_cast<const bf16*>(a.table);
+  const IdT* __restrict__ ids = static_cast<const IdT*>(a.ids);
+  const int F = a.F;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (b >= B) return;
+  if (b >= a.B) return;
   const int sub = lane / LPR;         // which field of the instruction group
   const int dl = (lane % LPR) * 8;    // first dim this lane owns
 
@@ -58,17 +59,17 @@ __global__ void __launch_bounds__(256) embed_kernel(const bf16* __restrict__ tab
     int64_t row = 0;
     float w = 0.f;
     if (fl < F) {
-      const int64_t id = int64_t(ids[int64_t(b) * F + fl]);
-      const int64_t m = modulo_f ? modulo_f[fl] : modulo;
-      row = (offset_f ? offset_f[fl] : 0) + hash_row(id, m);
-      row = row < 0 ? 0 : (row >= V ? V - 1 : row);  // memory safety whatever the tables say
-      w = wts ? wts[int64_t(b) * F + fl] : 1.f;
-      if (lin) first += lin[row] * w;
+      const int64_t id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
+      const int64_t m = a.modulo_f ? a.modulo_f[fl] : a.modulo;
+      row = (a.offset_f ? a.offset_f[fl] : 0) + hash_row(id, m);
+      row = row < 0 ? 0 : (row >= a.V ? a.V - 1 : row);  // memory safety whatever the tables say
+      w = a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f;
+      if (a.lin) first += a.lin[row] * w;
     }
     const int nf = min(kWave, F - fbase);
     const int groups = (nf + FPI - 1) / FPI;
     // Issue every table load of this chunk before consuming any.
-    constexpr int MAXG = kWave / FPI;  // <= 8 for D=64
+    constexpr int MAXG = kWave / FPI;  // 8 for D=64
     bf16x8 v[MAXG];
     float wf[MAXG];
 #pragma unroll
@@ -83,6 +84,7 @@ __global__ void __launch_bounds__(256) embed_kernel(const bf16* __restrict__ tab
         wf[g] = 0.f;
       }
     }
+    bf16* __restrict__ out_x = static_cast<bf16*>(a.out_x);
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
       const int f = g * FPI + sub;
@@ -95,14 +97,14 @@ __global__ void __launch_bounds__(256) embed_kernel(const bf16* __restrict__ tab
           q[j] += e * e;
           o[j] = f2bf(e);
         }
-        if (out_x) *reinterpret_cast<bf16x8*>(out_x + (int64_t(b) * F + fbase + f) * D + dl) = o;
+        if (out_x) *reinterpret_cast<bf16x8*>(out_x + int64_t(b) * a.x_ld + int64_t(fbase + f) * D + dl) = o;
       }
     }
   }
 
-  if (!out_fm) return;
+  if (!a.out_fm) return;
   float fm = 0.f;
-  if (fm2) {
+  if (a.fm2) {
     // sum over fields: lanes with the same (lane % LPR) own the same dims
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -119,8 +121,8 @@ __global__ void __launch_bounds__(256) embed_kernel(const bf16* __restrict__ tab
     }
     fm = 0.5f * wave_sum(part);
   }
-  const float fo = lin ? wave_sum(first) : 0.f;
-  if (lane == 0) out_fm[b] = bias + fo + fm;
+  const float fo = a.lin ? wave_sum(first) : 0.f;
+  if (lane == 0) a.out_fm[b] = a.bias + fo + fm;
 }
 
 // ---------------------------------------------------------------- K1b
@@ -187,31 +189,21 @@ hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n,
 }
 
 template <int D>
-static void embed_dispatch_ids(const void* ids, bool ids64, const bf16* table, const float* lin, const float* wts,
-                               int B, int F, int64_t V, int64_t modulo, const int64_t* modulo_f, const int64_t* offset_f,
-                               float bias, bf16* out_x, float* out_fm, int fm2, hipStream_t st) {
+static void embed_dispatch(const EmbedArgs& a, hipStream_t st) {
   const int rows_per_block = 4;
-  dim3 grid((B + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
-  if (ids64)
-    hipLaunchKernelGGL((embed_kernel<D, int64_t>), grid, block, 0, st, table, lin, static_cast<const int64_t*>(ids),
-                       wts, B, F, V, modulo, modulo_f, offset_f, bias, out_x, out_fm, fm2);
-  else
-    hipLaunchKernelGGL((embed_kernel<D, int32_t>), grid, block, 0, st, table, lin, static_cast<const int32_t*>(ids),
-                       wts, B, F, V, modulo, modulo_f, offset_f, bias, out_x, out_fm, fm2);
+  dim3 grid((a.B + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
+  if (a.ids64) hipLaunchKernelGGL((embed_kernel<D, int64_t>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((embed_kernel<D, int32_t>), grid, block, 0, st, a);
 }
 
-hipError_t launch_embed(const void* table, const float* lin, const void* ids, bool ids64, const float* wts, int B,
-                        int F, int D, int64_t V, int64_t modulo, const int64_t* modulo_f, const int64_t* offset_f, float bias,
-                        void* out_x, float* out_fm, bool fm2, hipStream_t st) {
-  if (B == 0) return hipSuccess;
-  const bf16* t = static_cast<const bf16*>(table);
-  bf16* x = static_cast<bf16*>(out_x);
-  switch (D) {
-    case 8: embed_dispatch_ids<8>(ids, ids64, t, lin, wts, B, F, V, modulo, modulo_f, offset_f, bias, x, out_fm, fm2, st); break;
-    case 16: embed_dispatch_ids<16>(ids, ids64, t, lin, wts, B, F, V, modulo, modulo_f, offset_f, bias, x, out_fm, fm2, st); break;
-    case 32: embed_dispatch_ids<32>(ids, ids64, t, lin, wts, B, F, V, modulo, modulo_f, offset_f, bias, x, out_fm, fm2, st); break;
-    case 64: embed_dispatch_ids<64>(ids, ids64, t, lin, wts, B, F, V, modulo, modulo_f, offset_f, bias, x, out_fm, fm2, st); break;
-    case 128: embed_dispatch_ids<128>(ids, ids64, t, lin, wts, B, F, V, modulo, modulo_f, offset_f, bias, x, out_fm, fm2, st); break;
+hipError_t launch_embed(const EmbedArgs& a, hipStream_t st) {
+  if (a.B == 0) return hipSuccess;
+  switch (a.D) {
+    case 8: embed_dispatch<8>(a, st); break;
+    case 16: embed_dispatch<16>(a, st); break;
+    case 32: embed_dispatch<32>(a, st); break;
+    case 64: embed_dispatch<64>(a, st); break;
+    case 128: embed_dispatch<128>(a, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -13,9 +13,26 @@ hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n,
                            const int64_t* offset_f, int64_t modulo, hipStream_t st);
 
 // K1: weighted gather (+ first/second-order FM). out_x bf16 [B, F*D] and/or out_fm fp32 [B].
-hipError_t launch_embed(const void* table, const float* lin, const void* ids, bool ids64, const float* wts, int B,
-                        int F, int D, int64_t V, int64_t modulo, const int64_t* modulo_f, const int64_t* offset_f, float bias,
-                        void* out_x, float* out_fm, bool fm2, hipStream_t st);
+struct EmbedArgs {
+  const void* table = nullptr;     // bf16 [V, D]
+  const float* lin = nullptr;      // fp32 [V] first-order weights (optional)
+  const void* ids = nullptr;       // int32/int64 [B, ids_ld] (first F used)
+  bool ids64 = true;
+  int64_t ids_ld = 0;
+  const float* wts = nullptr;      // fp32 [B, wts_ld] (optional)
+  int64_t wts_ld = 0;
+  int B = 0, F = 0, D = 0;
+  int64_t V = 0;                   // table rows (rows are clamped into [0, V))
+  int64_t modulo = 0;              // shared-table hashing
+  const int64_t* modulo_f = nullptr;  // per-field tables: row = offset_f[f] + id mod modulo_f[f]
+  const int64_t* offset_f = nullptr;
+  float bias = 0.f;
+  void* out_x = nullptr;           // bf16 [B, x_ld]
+  int64_t x_ld = 0;
+  float* out_fm = nullptr;         // fp32 [B]
+  int fm2 = 0;
+};
+hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 
 // K1b: sum/mean embedding bag with CSR offsets [nbags+1].
 hipError_t launch_embedding_bag(const void* table, const void* idx, bool idx64, const int64_t* offsets,

@@ -333,31 +333,72 @@ inline int64_t apply_mod(int64_t id, int64_t m) {
   return r < 0 ? r + m : r;
 }
 
-// Writes element i of the destination.
+// Writes logical element i of the destination. The destination is a row view:
+// `cols` elements per row, rows `ld` elements apart (ld == cols: contiguous),
+// so a packed request row [ids | wts | pad] can be filled in place.
 struct Writer {
   void* dst;
   DstType type;
   int64_t mod;
+  int64_t cols;
+  int64_t ld;
+  bool contiguous;
+  int64_t next_i = 0, r = 0, c = 0;  // sequential-access cursor
 
-  inline void put_int(int64_t i, int64_t v) const {
+  Writer(void* d, DstType t, int64_t m, int64_t cols_, int64_t ld_)
+      : dst(d), type(t), mod(m), cols(cols_ > 0 ? cols_ : 1), ld(ld_ > 0 ? ld_ : cols_), contiguous(ld_ <= 0 || ld_ == cols_) {}
+
+  inline int64_t at(int64_t i) {
+    if (contiguous) return i;
+    if (i != next_i) {
+      r = i / cols;
+      c = i % cols;
+    }
+    const int64_t p = r * ld + c;
+    next_i = i + 1;
+    if (++c == cols) {
+      c = 0;
+      ++r;
+    }
+    return p;
+  }
+  inline void put_int(int64_t i, int64_t v) {
+    const int64_t p = at(i);
     switch (type) {
-      case DstType::I32: static_cast<int32_t*>(dst)[i] = int32_t(apply_mod(v, mod)); break;
-      case DstType::I64: static_cast<int64_t*>(dst)[i] = apply_mod(v, mod); break;
-      case DstType::F32: static_cast<float*>(dst)[i] = float(v); break;
-      case DstType::BF16: static_cast<uint16_t*>(dst)[i] = f32_to_bf16(float(v)); break;
+      case DstType::I32: static_cast<int32_t*>(dst)[p] = int32_t(apply_mod(v, mod)); break;
+      case DstType::I64: static_cast<int64_t*>(dst)[p] = apply_mod(v, mod); break;
+      case DstType::F32: static_cast<float*>(dst)[p] = float(v); break;
+      case DstType::BF16: static_cast<uint16_t*>(dst)[p] = f32_to_bf16(float(v)); break;
     }
   }
-  inline void put_float(int64_t i, float v) const {
+  inline void put_float(int64_t i, float v) {
+    const int64_t p = at(i);
     switch (type) {
-      case DstType::F32: static_cast<float*>(dst)[i] = v; break;
-      case DstType::BF16: static_cast<uint16_t*>(dst)[i] = f32_to_bf16(v); break;
+      case DstType::F32: static_cast<float*>(dst)[p] = v; break;
+      case DstType::BF16: static_cast<uint16_t*>(dst)[p] = f32_to_bf16(v); break;
       default: break;  // rejected earlier
     }
   }
+  inline void put_bits16(int64_t i, uint16_t h) { static_cast<uint16_t*>(dst)[at(i)] = h; }
   size_t elem_size() const { return (type == DstType::I64) ? 8 : (type == DstType::BF16 ? 2 : 4); }
-  void copy_elem(int64_t to, int64_t from) const {
-    size_t es = elem_size();
-    std::memcpy(static_cast<char*>(dst) + to * es, static_cast<char*>(dst) + from * es, es);
+  // Row-wise copy of n same-typed source elements (memcpy path).
+  void copy_rows(const uint8_t* src, int64_t n) {
+    const size_t es = elem_size();
+    if (contiguous) {
+      std::memcpy(dst, src, size_t(n) * es);
+      return;
+    }
+    for (int64_t i = 0, row = 0; i < n; i += cols, ++row) {
+      const int64_t k = std::min<int64_t>(cols, n - i);
+      std::memcpy(static_cast<char*>(dst) + size_t(row * ld) * es, src + size_t(i) * es, size_t(k) * es);
+    }
+  }
+  void fill_from(int64_t from, int64_t i0, int64_t n) {  // elements [i0, n) = element `from`
+    const size_t es = elem_size();
+    int64_t pf = contiguous ? from : (from / cols) * ld + from % cols;
+    char buf[8];
+    std::memcpy(buf, static_cast<char*>(dst) + size_t(pf) * es, es);
+    for (int64_t i = i0; i < n; ++i) std::memcpy(static_cast<char*>(dst) + size_t(at(i)) * es, buf, es);
   }
 };
 
@@ -472,16 +513,17 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
   const bool dst_int = opts.dst == DstType::I32 || opts.dst == DstType::I64;
   if (dst_int && is_float_dtype(t.dtype)) return *err = "cannot decode a floating tensor into integer ids", false;
   if (t.dtype == DT_STRING || dtype_size(t.dtype) == 0) return *err = "unsupported tensor dtype", false;
-  Writer w{dst, opts.dst, dst_int ? opts.id_modulo : 0};
+  const int64_t mod = dst_int ? opts.id_modulo : 0;
+  Writer w(dst, opts.dst, mod, opts.cols > 0 ? opts.cols : n, opts.ld);
 
   if (t.content.n > 0) {
-    size_t es = dtype_size(t.dtype);
+    const size_t es = dtype_size(t.dtype);
     if (t.content.n != size_t(n) * es) return *err = "tensor_content size does not match shape", false;
     const uint8_t* p = t.content.p;
     switch (t.dtype) {
       case DT_FLOAT:
         if (opts.dst == DstType::F32) {
-          std::memcpy(dst, p, size_t(n) * 4);
+          w.copy_rows(p, n);
         } else {
           for (int64_t i = 0; i < n; ++i) {
             float f;
@@ -505,25 +547,19 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
         }
         return true;
       case DT_BFLOAT16:
+        if (opts.dst == DstType::BF16) {
+          w.copy_rows(p, n);
+          return true;
+        }
         for (int64_t i = 0; i < n; ++i) {
           uint16_t h;
           std::memcpy(&h, p + 2 * i, 2);
-          if (opts.dst == DstType::BF16) static_cast<uint16_t*>(dst)[i] = h;
-          else w.put_float(i, bf16_to_f32(h));
+          w.put_float(i, bf16_to_f32(h));
         }
         return true;
       case DT_INT64: case DT_UINT64:
-        if (opts.dst == DstType::I64 && opts.id_modulo <= 0) {
-          std::memcpy(dst, p, size_t(n) * 8);
-          return true;
-        }
-        if (opts.dst == DstType::I32 && opts.id_modulo <= 0) {
-          int32_t* d = static_cast<int32_t*>(dst);
-          for (int64_t i = 0; i < n; ++i) {
-            int64_t v;
-            std::memcpy(&v, p + 8 * i, 8);
-            d[i] = int32_t(v);
-          }
+        if (opts.dst == DstType::I64 && mod <= 0) {
+          w.copy_rows(p, n);
           return true;
         }
         for (int64_t i = 0; i < n; ++i) {
@@ -533,8 +569,8 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
         }
         return true;
       case DT_INT32:
-        if (opts.dst == DstType::I32 && opts.id_modulo <= 0) {
-          std::memcpy(dst, p, size_t(n) * 4);
+        if (opts.dst == DstType::I32 && mod <= 0) {
+          w.copy_rows(p, n);
           return true;
         }
         for (int64_t i = 0; i < n; ++i) {
@@ -579,8 +615,8 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
   const int64_t k = t.num_values;
   if (k > n) return *err = "more values than the tensor shape holds", false;
   if (n == 0) return true;
-  if (k == 0) {  // empty: zero fill
-    std::memset(dst, 0, size_t(n) * w.elem_size());
+  if (k == 0) {  // empty typed field: zero fill
+    for (int64_t i = 0; i < n; ++i) w.put_int(i, 0);
     return true;
   }
   int64_t i = 0;
@@ -588,17 +624,15 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
     if (t.dtype == DT_HALF || t.dtype == DT_BFLOAT16) {
       const bool bf = t.dtype == DT_BFLOAT16;
       if (!for_each_int(t, [&](uint64_t v) {
-            uint16_t h = uint16_t(v);
-            if (bf && opts.dst == DstType::BF16) static_cast<uint16_t*>(dst)[i++] = h;
+            const uint16_t h = uint16_t(v);
+            if (bf && opts.dst == DstType::BF16) w.put_bits16(i++, h);
             else w.put_float(i++, bf ? bf16_to_f32(h) : half_to_f32(h));
           }))
         return *err = "bad packed varint", false;
-    } else if (opts.dst == DstType::I32 && t.dtype == DT_INT64 && t.packed.size() == 1 && t.unpacked.empty()) {
-      // Hot path: reference feat_ids (int64_val packed) -> int32 row ids.
-      int32_t* d = static_cast<int32_t*>(dst);
+    } else if (t.dtype == DT_INT64 && dst_int && t.packed.size() == 1 && t.unpacked.empty()) {
+      // Hot path: reference feat_ids (int64_val packed) -> row ids.
       const uint8_t* p = t.packed[0].p;
       const uint8_t* e = p + t.packed[0].n;
-      const int64_t m = opts.id_modulo;
       while (p < e) {
         uint64_t v = *p++;
         if (v & 0x80) {
@@ -612,7 +646,7 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
             shift += 7;
           } while ((b & 0x80) && shift < 70);
         }
-        d[i++] = int32_t(m > 0 ? apply_mod(int64_t(v), m) : int64_t(v));
+        w.put_int(i++, int64_t(v));
       }
     } else {
       const int dt = t.dtype;
@@ -621,8 +655,8 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
     }
   } else if (t.value_fixed32) {
     if (opts.dst == DstType::F32 && t.packed.size() == 1 && t.unpacked.empty()) {
-      std::memcpy(dst, t.packed[0].p, t.packed[0].n);  // reference feat_wts: float_val packed
-      i = int64_t(t.packed[0].n / 4);
+      i = int64_t(t.packed[0].n / 4);  // reference feat_wts: float_val packed
+      w.copy_rows(t.packed[0].p, i);
     } else {
       for_each_f32(t, [&](float f) { w.put_float(i++, f); });
     }
@@ -631,7 +665,7 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
   } else {
     return *err = "tensor has no typed value field for its dtype", false;
   }
-  for (; i < n; ++i) w.copy_elem(i, k - 1);  // fill: repeat the last value
+  if (i < n) w.fill_from(k - 1, i, n);  // fill: repeat the last value
   return true;
 }
 

@@ -87,6 +87,8 @@ bool parse_tensor(const uint8_t* buf, size_t len, TensorView* out, std::string* 
 struct DecodeOpts {
   DstType dst = DstType::F32;
   int64_t id_modulo = 0;  // >0: ids become ((id % m) + m) % m (hash into table rows)
+  int64_t cols = 0;       // destination row view: elements per row (0: contiguous)
+  int64_t ld = 0;         // elements between row starts (0 or == cols: contiguous)
 };
 
 // Decode the tensor's elements (with TF fill semantics) into dst, which must

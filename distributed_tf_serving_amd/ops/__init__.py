@@ -36,6 +36,13 @@ def _hash_rows(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None)
     return ids
 
 
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """Row views with unit inner stride pass through (kernels take a row stride)."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t
+    return t.contiguous()
+
+
 # ------------------------------------------------------------------ K0
 def pack_ids(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None) -> torch.Tensor:
     """int64/int32 feature ids -> int32 table rows (``offset_f + id mod m``)."""
@@ -57,7 +64,7 @@ def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = 
     if ids.is_cuda:
         if modulo_f is None and modulo <= 0:
             modulo = table.shape[0]
-        x, fm = hip().embed(table, lin, ids.contiguous(), None if wts is None else wts.contiguous(), int(modulo),
+        x, fm = hip().embed(table, lin, _rows(ids), None if wts is None else _rows(wts), int(modulo),
                             modulo_f, offset_f, float(bias), want_x, want_fm, fm2, out_x)
         return (x if want_x else None), (fm if want_fm else None)
     rows = _hash_rows(ids, modulo if modulo > 0 else table.shape[0], modulo_f, offset_f)

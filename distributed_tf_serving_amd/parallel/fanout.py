@@ -1,0 +1,210 @@
+"""Candidate fan-out across the GPUs of a node (RCCL over xGMI).
+
+The reference client splits one request's candidates across N TF-Serving hosts
+and gathers the scores back (reference DCNClient.java:46-74 split, :146-164
+dispatch + join). Here the hosts are the ranks of one process group and the
+network hop becomes collectives on device buffers of packed rows
+(:mod:`..serving.packing`):
+
+``scatter``   the reference topology: rank 0 is the only front door; its
+              ``world * B`` rows are scattered (C1) and per-rank scores are
+              gathered back to it (C2).
+``alltoall``  every rank is a front door; each rank's ``B`` rows are split
+              across all GPUs and scores return to the submitting rank with a
+              second all-to-all. Same per-request fan-out as ``scatter`` but
+              the host->GPU traffic is spread over every GPU's PCIe link, so it
+              scales with N instead of saturating rank 0's link.
+``local``     no fan-out (each rank serves its own rows): the baseline.
+
+Per step every rank runs, on its own HIP streams::
+
+    H2D (copy stream) -> collective -> graph(forward) -> collective -> D2H
+
+with two pipeline slots, so step k+1's H2D and host-side decode overlap step
+k's compute. Equal split sizes keep every collective shape static (no count
+exchange; graph-friendly).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..serving.executor import ShardExecutor
+from .dist import DistContext
+
+MODES = ("alltoall", "scatter", "local")
+
+
+@dataclass
+class StepHandle:
+    B: int
+    slot: int
+    host_out: torch.Tensor
+    event: Optional[object] = None
+    t_submit: float = 0.0
+    t_done: float = 0.0
+
+    def wait(self) -> torch.Tensor:
+        if self.event is not None:
+            self.event.synchronize()
+        self.t_done = time.perf_counter()
+        return self.host_out
+
+
+class FanoutEngine:
+    def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None):
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        self.ex = executor
+        self.ctx = ctx
+        self.world = ctx.world if ctx.is_distributed else 1
+        self.rank = ctx.rank if ctx.is_distributed else 0
+        self.mode = mode if self.world > 1 else "local"
+        self.group = group
+        self.layout = executor.layout
+        self.dev = executor.device
+        self.cuda = self.dev.type == "cuda"
+        if self.cuda:
+            self.h2d_stream = torch.cuda.Stream(self.dev)
+            self.d2h_stream = torch.cuda.Stream(self.dev)
+        self._host_in: Dict[Tuple[int, int], torch.Tensor] = {}
+        self._host_out: Dict[Tuple[int, int], torch.Tensor] = {}
+        self._dev_send: Dict[Tuple[int, int], torch.Tensor] = {}
+        self._dev_back: Dict[Tuple[int, int], torch.Tensor] = {}
+        self._ev_in_free: Dict[int, object] = {}
+        self._ev_out_free: Dict[int, object] = {}
+
+    # -- geometry ------------------------------------------------------------
+    def contrib_rows(self, B: int) -> int:
+        """Rows this rank submits per step when every GPU computes B rows."""
+        if self.mode == "scatter":
+            return self.world * B if self.rank == 0 else 0
+        return B
+
+    def check_bucket(self, B: int) -> None:
+        if self.mode == "alltoall" and B % self.world:
+            raise ValueError(f"bucket {B} must be divisible by world size {self.world} for all-to-all fan-out")
+
+    def host_in(self, B: int, slot: int = 0) -> torch.Tensor:
+        """Pinned host buffer [contrib_rows(B), W] the front door decodes into."""
+        key = (B, slot)
+        t = self._host_in.get(key)
+        if t is None:
+            t = self.layout.alloc(max(1, self.contrib_rows(B)), pin=self.cuda)
+            self._host_in[key] = t
+        return t
+
+    def host_out(self, B: int, slot: int = 0) -> torch.Tensor:
+        key = (B, slot)
+        t = self._host_out.get(key)
+        if t is None:
+            t = torch.zeros(max(1, self.contrib_rows(B)), dtype=torch.float32, pin_memory=self.cuda)
+            self._host_out[key] = t
+        return t
+
+    def _dev(self, store, key, shape, dtype):
+        t = store.get(key)
+        if t is None:
+            t = torch.zeros(shape, dtype=dtype, device=self.dev)
+            store[key] = t
+        return t
+
+    def prepare(self, B: int) -> None:
+        self.check_bucket(B)
+        for s in range(self.ex.slots):
+            self.host_in(B, s)
+            self.host_out(B, s)
+            self.ex.prepare(B, s)
+
+    # -- one step --------------------------------------------------------------
+    def launch(self, B: int, slot: int = 0) -> StepHandle:
+        """Enqueue one fan-out step for bucket B from host_in(B, slot).
+
+        Returns immediately on GPU (all work is stream-ordered); call
+        ``handle.wait()`` for the scores in host_out(B, slot)."""
+        self.check_bucket(B)
+        key = (B, slot)
+        h_in, h_out = self.host_in(B, slot), self.host_out(B, slot)
+        rows = self.contrib_rows(B)
+        t0 = time.perf_counter()
+        exec_in = self.ex.input_buffer(B, slot)
+        if not self.cuda:
+            return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
+
+        cur = torch.cuda.current_stream(self.dev)
+        ev_in_free = self._ev_in_free.get(slot)
+        ev_out_free = self._ev_out_free.get(slot)
+        # H2D: straight into the executor's graph input when there is no fan-out
+        if self.mode == "local":
+            send = exec_in
+        else:
+            send = self._dev(self._dev_send, key, (max(1, rows), self.layout.words), torch.int64)
+        with torch.cuda.stream(self.h2d_stream):
+            # WAR: wait only until this slot's previous step has consumed its
+            # input, so this H2D overlaps the previous step's compute
+            if ev_in_free is not None:
+                self.h2d_stream.wait_event(ev_in_free)
+            if rows:
+                send[:rows].copy_(h_in[:rows], non_blocking=True)
+        cur.wait_stream(self.h2d_stream)
+
+        if self.mode == "alltoall":
+            dist.all_to_all_single(exec_in, send, group=self.group)
+        elif self.mode == "scatter":
+            chunks = list(send[: self.world * B].chunk(self.world)) if self.rank == 0 else None
+            dist.scatter(exec_in, chunks, src=0, group=self.group)
+        if self.mode != "local":
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._ev_in_free[slot] = ev
+
+        if ev_out_free is not None:  # WAR on this slot's graph output / back buffer
+            cur.wait_event(ev_out_free)
+        scores = self.ex.run(B, slot)
+        if self.mode == "local":
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._ev_in_free[slot] = ev
+
+        if self.mode == "alltoall":
+            back = self._dev(self._dev_back, key, (B,), torch.float32)
+            dist.all_to_all_single(back, scores, group=self.group)
+        elif self.mode == "scatter":
+            back = self._dev(self._dev_back, key, (self.world * B,), torch.float32) if self.rank == 0 else None
+            dist.gather(scores, list(back.chunk(self.world)) if self.rank == 0 else None, dst=0, group=self.group)
+        else:
+            back = scores
+
+        done = torch.cuda.Event()
+        with torch.cuda.stream(self.d2h_stream):
+            self.d2h_stream.wait_stream(cur)
+            if rows:
+                h_out[:rows].copy_(back[:rows], non_blocking=True)
+            done.record(self.d2h_stream)
+        self._ev_out_free[slot] = done
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=done, t_submit=t0)
+
+    def _launch_cpu(self, B, slot, h_in, h_out, rows, exec_in, t0) -> StepHandle:
+        if self.mode == "alltoall":
+            dist.all_to_all_single(exec_in, h_in[:B].contiguous(), group=self.group)
+        elif self.mode == "scatter":
+            chunks = list(h_in[: self.world * B].chunk(self.world)) if self.rank == 0 else None
+            dist.scatter(exec_in, chunks, src=0, group=self.group)
+        else:
+            exec_in[:B].copy_(h_in[:B])
+        scores = self.ex.run(B, slot).contiguous()
+        if self.mode == "alltoall":
+            back = torch.empty(B, dtype=torch.float32)
+            dist.all_to_all_single(back, scores, group=self.group)
+        elif self.mode == "scatter":
+            back = torch.empty(self.world * B, dtype=torch.float32) if self.rank == 0 else None
+            dist.gather(scores, list(back.chunk(self.world)) if self.rank == 0 else None, dst=0, group=self.group)
+        else:
+            back = scores
+        if rows:
+            h_out[:rows].copy_(back[:rows])
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=None, t_submit=t0)
