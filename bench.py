@@ -65,16 +65,19 @@ def parse_args():
     ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"])
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")
-    ap.add_argument("--decode-threads", type=int, default=4)
+    ap.add_argument("--decode-threads", type=int, default=8)
     ap.add_argument("--pool", type=int, default=8, help="distinct pre-serialized steps per rank")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
+    ap.add_argument("--diag-skip-host", action="store_true",
+                    help="DIAGNOSTIC ONLY (not a valid measurement): reuse decoded buffers to isolate GPU time")
     return ap.parse_args()
 
 
 def main():
     a = parse_args()
+    os.environ.setdefault("DTFS_HOST_THREADS", str(max(1, a.decode_threads)))
     ctx = init_from_env()
     world, rank = ctx.world, ctx.rank
     if world != a.gpus and rank == 0:
@@ -89,7 +92,8 @@ def main():
     F = cfg.num_fields
     layout = PackedLayout(F)
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
-    ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=2)
+    slots = 3
+    ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
     eng = FanoutEngine(ex, ctx, mode=a.mode)
     eng.prepare(B)
     nat = native()
@@ -101,24 +105,20 @@ def main():
     for _ in range(max(1, a.pool)):
         pool.append([synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n_req)])
 
-    threads = max(1, a.decode_threads)
-    tp = cf.ThreadPoolExecutor(max_workers=threads + 1)
+    tp = cf.ThreadPoolExecutor(max_workers=2)   # response encode
+    dtp = cf.ThreadPoolExecutor(max_workers=1)  # request decode (fans out into the native pool)
+    diag_pb = nat.parse_batch(pool[0], "feat_ids", "feat_wts", F) if pool[0] else None
 
     def decode(k: int, slot: int):
         reqs = pool[k % len(pool)]
         if not reqs:
             return None
+        if a.diag_skip_host and k >= 2:  # diagnostic only: GPU pipeline without host decode
+            return diag_pb
         pb = nat.parse_batch(reqs, "feat_ids", "feat_wts", F)
         buf = eng.host_in(B, slot)
         ids_v, wts_v = layout.ids(buf), layout.wts(buf)
-        n = len(reqs)
-        if threads == 1 or n == 1:
-            pb.decode(ids_v, wts_v, 0, n)
-        else:
-            step = (n + threads - 1) // threads
-            futs = [tp.submit(pb.decode, ids_v, wts_v, s, min(n, s + step)) for s in range(0, n, step)]
-            for f in futs:
-                f.result()
+        pb.decode(ids_v, wts_v)  # row chunks spread over the native host pool (DTFS_HOST_THREADS)
         errs = [e for e in pb.errors if e]
         if errs:
             raise RuntimeError(errs[0])
@@ -131,29 +131,52 @@ def main():
                                           list(pb.rows), list(pb.offsets))
 
     lat = []
+    phase = {"decode": 0.0, "enc_wait": 0.0, "launch": 0.0, "gpu_wait": 0.0}
 
     def run(n_steps: int, record: bool):
-        pbs = {0: decode(0, 0)}
-        t_dec = {0: time.perf_counter()}
-        pending_enc = None
-        for k in range(n_steps):
-            slot = k % 2
-            h = eng.launch(B, slot)
-            nxt = tp.submit(decode, k + 1, (k + 1) % 2) if k + 1 < n_steps else None
-            t_next = time.perf_counter()
-            if pending_enc is not None:
-                pending_enc.result()
-            scores = h.wait()
-            pending_enc = tp.submit(encode, pbs.pop(k), scores)
+        # Three-stage pipeline over S = 3 buffer slots:
+        #   decode(k+2) [host pool]  ||  H2D(k+1) [SDMA]  ||  forward(k) [GPU]
+        # and encode(k-1) on a host thread. Slot j % S is reused by step j only
+        # after step j-S has completed (its H2D read host_in) and been encoded
+        # (its D2H wrote host_out).
+        S = slots
+        t_start, dec, enc, handles, pbs = {}, {}, {}, {}, {}
+
+        def start_decode(j):
+            t_start[j] = time.perf_counter()
+            dec[j] = dtp.submit(decode, j, j % S)
+
+        def finish(j):
+            t = time.perf_counter()
+            scores = handles.pop(j).wait()
+            phase["gpu_wait"] += time.perf_counter() - t
             if record:
-                lat.append(time.perf_counter() - t_dec.pop(k))
+                lat.append(time.perf_counter() - t_start.pop(j))
             else:
-                t_dec.pop(k)
-            if nxt is not None:
-                pbs[k + 1] = nxt.result()
-                t_dec[k + 1] = t_next
-        if pending_enc is not None:
-            pending_enc.result()
+                t_start.pop(j)
+            enc[j] = tp.submit(encode, pbs.pop(j), scores)
+
+        for j in range(min(2, n_steps)):
+            start_decode(j)
+        for k in range(n_steps):
+            t1 = time.perf_counter()
+            pbs[k] = dec.pop(k).result()
+            t2 = time.perf_counter()
+            if k - S in enc:
+                enc.pop(k - S).result()
+            t3 = time.perf_counter()
+            handles[k] = eng.launch(B, k % S)
+            t4 = time.perf_counter()
+            phase["decode"] += t2 - t1
+            phase["enc_wait"] += t3 - t2
+            phase["launch"] += t4 - t3
+            if k >= 1:
+                finish(k - 1)  # two steps in flight on the GPU
+            if k + 2 < n_steps:
+                start_decode(k + 2)  # its slot held step k-1: done above
+        finish(n_steps - 1)
+        for f in enc.values():
+            f.result()
 
     def sync():
         if dev.type == "cuda":
@@ -165,6 +188,8 @@ def main():
 
     run(max(1, a.warmup), record=False)
     sync()
+    for key in phase:
+        phase[key] = 0.0
     t0 = time.perf_counter()
     run(a.steps, record=True)
     sync()
@@ -205,6 +230,9 @@ def main():
             "p99_request_ms": None if p99 is None else round(p99, 3),
         }
         print(json.dumps(out), flush=True)
+        if a.json_extra:
+            per = {k: round(v / a.steps * 1e6, 1) for k, v in phase.items()}
+            print(json.dumps({"host_phase_us_per_step": per}), file=sys.stderr, flush=True)
     tp.shutdown(wait=True)
     shutdown()
 

@@ -11,6 +11,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/launchers.h"
+#include "runtime/step_runner.h"
 
 namespace {
 
@@ -344,4 +345,26 @@ PYBIND11_MODULE(_hip, m) {
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);
+
+  py::class_<dtfs::runtime::StepRunner>(m, "StepRunner",
+                                        "Native per-GPU step launcher: SDMA H2D + graph launch per pipeline slot")
+      .def(py::init<int, int>(), py::arg("device"), py::arg("slots"))
+      .def(
+          "launch",
+          [](dtfs::runtime::StepRunner& r, int slot, torch::Tensor dst, torch::Tensor src, int64_t nbytes,
+             uintptr_t graph_exec) {
+            TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "dst must be a contiguous GPU tensor");
+            TORCH_CHECK(src.device().is_cpu() && src.is_contiguous() && src.is_pinned(),
+                        "src must be a contiguous pinned host tensor");
+            TORCH_CHECK(nbytes >= 0 && nbytes <= int64_t(dst.nbytes()) && nbytes <= int64_t(src.nbytes()),
+                        "nbytes out of range");
+            TORCH_CHECK(graph_exec != 0, "null graph exec");
+            r.launch(slot, dst.data_ptr(), src.data_ptr(), nbytes, reinterpret_cast<hipGraphExec_t>(graph_exec));
+          },
+          py::arg("slot"), py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("graph_exec"))
+      .def("wait", &dtfs::runtime::StepRunner::wait, py::arg("slot"), py::call_guard<py::gil_scoped_release>())
+      .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
+      .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
+      .def_property_readonly("compute_stream",
+                             [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
 }

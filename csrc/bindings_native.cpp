@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include "runtime/batcher.h"
+#include "runtime/thread_pool.h"
 #include "wire/tensor_codec.h"
 
 namespace py = pybind11;
@@ -204,31 +205,62 @@ void decode_batch_range(ParsedBatch& b, torch::Tensor ids_dst, c10::optional<tor
   begin = std::max<int64_t>(0, begin);
   end = std::min<int64_t>(end, int64_t(b.views.size()));
   py::gil_scoped_release nogil;
+  // Work items: a raw (tensor_content) request is split into row chunks so even
+  // one large request spreads over the pool; typed-field (varint) requests
+  // decode as a whole (their values cannot be addressed by row).
+  struct Item {
+    int64_t req, r0, r1;
+  };
+  constexpr int64_t kChunkRows = 128;
+  std::vector<Item> items;
   for (int64_t i = begin; i < end; ++i) {
     if (!b.ids_t[i] || b.rows[i] == 0) continue;
-    const int64_t row = base_row + b.offsets[i];
-    const int64_t n = b.rows[i] * b.fields;
+    const bool raw = b.ids_t[i]->content.n > 0 && (!b.wts_t[i] || b.wts_t[i]->content.n > 0);
+    if (!raw) {
+      items.push_back({i, 0, b.rows[i]});
+      continue;
+    }
+    for (int64_t r = 0; r < b.rows[i]; r += kChunkRows) items.push_back({i, r, std::min(b.rows[i], r + kChunkRows)});
+  }
+  std::vector<std::string> errs(items.size());
+  auto sub = [](const wire::TensorView& t, int64_t e0, int64_t e1) {
+    wire::TensorView v;  // content-only view of elements [e0, e1)
+    v.dtype = t.dtype;
+    const size_t es = t.content.n / size_t(std::max<int64_t>(1, t.num_elements()));
+    v.content.p = t.content.p + size_t(e0) * es;
+    v.content.n = size_t(e1 - e0) * es;
+    return v;
+  };
+  runtime::ThreadPool::global().parallel_for(int64_t(items.size()), [&](int64_t k) {
+    const Item& itm = items[k];
+    const int64_t i = itm.req;
+    const bool whole = itm.r0 == 0 && itm.r1 == b.rows[i];
+    const int64_t row = base_row + b.offsets[i] + itm.r0;
+    const int64_t e0 = itm.r0 * b.fields, e1 = itm.r1 * b.fields, n = e1 - e0;
     std::string err;
     wire::DecodeOpts o;
     o.dst = it;
     o.id_modulo = id_modulo;
     o.cols = b.fields;
     o.ld = ild;
-    if (!wire::decode_into(*b.ids_t[i], ibase + size_t(row * ild) * ies, n, o, &err)) {
-      b.errors[i] = "input '" + b.ids_key + "': " + err;
-      continue;
+    const bool ok_ids = whole ? wire::decode_into(*b.ids_t[i], ibase + size_t(row * ild) * ies, n, o, &err)
+                              : wire::decode_into(sub(*b.ids_t[i], e0, e1), ibase + size_t(row * ild) * ies, n, o, &err);
+    if (!ok_ids) {
+      errs[k] = "input '" + b.ids_key + "': " + err;
+      return;
     }
-    if (wbase) {
+    if (wbase && b.wts_t[i]) {
       wire::DecodeOpts ow;
       ow.dst = wt;
       ow.cols = b.fields;
       ow.ld = wld;
-      if (b.wts_t[i]) {
-        if (!wire::decode_into(*b.wts_t[i], wbase + size_t(row * wld) * wes, n, ow, &err))
-          b.errors[i] = "input '" + b.wts_key + "': " + err;
-      }
+      const bool ok = whole ? wire::decode_into(*b.wts_t[i], wbase + size_t(row * wld) * wes, n, ow, &err)
+                            : wire::decode_into(sub(*b.wts_t[i], e0, e1), wbase + size_t(row * wld) * wes, n, ow, &err);
+      if (!ok) errs[k] = "input '" + b.wts_key + "': " + err;
     }
-  }
+  });
+  for (size_t k = 0; k < items.size(); ++k)
+    if (!errs[k].empty() && b.errors[items[k].req].empty()) b.errors[items[k].req] = errs[k];
 }
 
 // One PredictResponse per request: outputs[key] = scores[offsets[i] : +rows[i]]

@@ -36,8 +36,9 @@ NATIVE_SOURCES = [
     "bindings_native.cpp",
     "wire/tensor_codec.cpp",
     "runtime/batcher.cpp",
+    "runtime/thread_pool.cpp",
 ]
-HIP_HOST_SOURCES = ["bindings_hip.cpp"]
+HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp"]
 
 
 def _torch_paths():

@@ -39,6 +39,21 @@ from .dist import DistContext
 MODES = ("alltoall", "scatter", "local")
 
 
+class _RunnerEvent:
+    """Adapter so a StepHandle can wait on a native StepRunner slot."""
+
+    __slots__ = ("runner", "slot")
+
+    def __init__(self, runner, slot):
+        self.runner, self.slot = runner, slot
+
+    def synchronize(self):
+        self.runner.wait(self.slot)
+
+    def query(self) -> bool:
+        return self.runner.query(self.slot)
+
+
 @dataclass
 class StepHandle:
     B: int
@@ -56,7 +71,8 @@ class StepHandle:
 
 
 class FanoutEngine:
-    def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None):
+    def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
+                 step_graphs: bool = True, native_launch: bool = True):
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.ex = executor
@@ -77,6 +93,10 @@ class FanoutEngine:
         self._dev_back: Dict[Tuple[int, int], torch.Tensor] = {}
         self._ev_in_free: Dict[int, object] = {}
         self._ev_out_free: Dict[int, object] = {}
+        self.step_graphs = step_graphs
+        self.native_launch = native_launch
+        self._runner = None
+        self._step_graph: Dict[Tuple[int, int], object] = {}
 
     # -- geometry ------------------------------------------------------------
     def contrib_rows(self, B: int) -> int:
@@ -118,7 +138,71 @@ class FanoutEngine:
         for s in range(self.ex.slots):
             self.host_in(B, s)
             self.host_out(B, s)
-            self.ex.prepare(B, s)
+            if self._step_graphs_enabled():
+                self._capture_step(B, s)
+            else:
+                self.ex.prepare(B, s)
+
+    # -- whole-step graphs (no fan-out) ------------------------------------------
+    def _step_graphs_enabled(self) -> bool:
+        return self.cuda and self.mode == "local" and self.ex.use_graphs and self.step_graphs
+
+    def _capture_step(self, B: int, slot: int) -> None:
+        """Capture forward -> D2H of one (bucket, slot) as ONE HIP graph.
+
+        The H2D is deliberately NOT in the graph: inside a graph ROCm turns a
+        memcpy node into a blit kernel that competes with the GEMMs for CUs
+        (measured: both slowed ~2x), while an eager pinned H2D on its own stream
+        runs on an SDMA engine and overlaps the previous step's kernels for free.
+        All compute stays on one stream: two forwards sharing the chip only
+        thrash each other's L2."""
+        key = (B, slot)
+        if key in self._step_graph:
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        h_out = self.host_out(B, slot)
+        buf = self.ex.input_buffer(B, slot)
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+        side.synchronize()
+        pool = self.ex._pools.get(("step", slot))
+        if pool is None:
+            pool = self.ex._pools[("step", slot)] = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool, stream=side):
+            h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+        self._step_graph[key] = g
+
+    def _launch_step_graph(self, B: int, slot: int, h_in, h_out, rows: int, t0: float) -> StepHandle:
+        self._capture_step(B, slot)
+        if self.native_launch:
+            # C++ StepRunner: SDMA H2D + hipGraphLaunch + events, no torch stream
+            # bookkeeping in the loop (csrc/runtime/step_runner.cpp)
+            if self._runner is None:
+                from ..ops import hip
+
+                self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
+            buf = self.ex.input_buffer(B, slot)
+            nbytes = B * self.layout.row_bytes
+            self._runner.launch(slot, buf, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
+            return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot),
+                              t_submit=t0)
+        cur = torch.cuda.current_stream(self.dev)
+        buf = self.ex.input_buffer(B, slot)
+        ev_in_free = self._ev_in_free.get(slot)
+        with torch.cuda.stream(self.h2d_stream):  # SDMA, overlaps the previous step
+            if ev_in_free is not None:
+                self.h2d_stream.wait_event(ev_in_free)
+            buf.copy_(h_in[:B], non_blocking=True)
+        cur.wait_stream(self.h2d_stream)
+        self._step_graph[(B, slot)].replay()
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._ev_in_free[slot] = ev
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=ev, t_submit=t0)
 
     # -- one step --------------------------------------------------------------
     def launch(self, B: int, slot: int = 0) -> StepHandle:
@@ -134,6 +218,8 @@ class FanoutEngine:
         exec_in = self.ex.input_buffer(B, slot)
         if not self.cuda:
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
+        if self._step_graphs_enabled():
+            return self._launch_step_graph(B, slot, h_in, h_out, rows, t0)
 
         cur = torch.cuda.current_stream(self.dev)
         ev_in_free = self._ev_in_free.get(slot)
