@@ -49,6 +49,7 @@ from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown  # 
 from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E402
 from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E402
 from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
+from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
 
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -92,7 +93,7 @@ def main():
     F = cfg.num_fields
     layout = PackedLayout(F)
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
-    slots = 3
+    slots = 4
     ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
     eng = FanoutEngine(ex, ctx, mode=a.mode)
     eng.prepare(B)
@@ -105,8 +106,6 @@ def main():
     for _ in range(max(1, a.pool)):
         pool.append([synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n_req)])
 
-    tp = cf.ThreadPoolExecutor(max_workers=2)   # response encode
-    dtp = cf.ThreadPoolExecutor(max_workers=1)  # request decode (fans out into the native pool)
     diag_pb = nat.parse_batch(pool[0], "feat_ids", "feat_wts", F) if pool[0] else None
 
     def decode(k: int, slot: int):
@@ -130,53 +129,14 @@ def main():
         return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores,
                                           list(pb.rows), list(pb.offsets))
 
-    lat = []
-    phase = {"decode": 0.0, "enc_wait": 0.0, "launch": 0.0, "gpu_wait": 0.0}
+    # decode(k+3) || H2D(k+1..k+2) [SDMA] || forward(k) [GPU] || encode(k-1)
+    pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1,
+                        produce=decode, consume=lambda k, pb, scores: encode(pb, scores))
+    phase = pipe.phase
+    lat = pipe.latencies
 
     def run(n_steps: int, record: bool):
-        # Three-stage pipeline over S = 3 buffer slots:
-        #   decode(k+2) [host pool]  ||  H2D(k+1) [SDMA]  ||  forward(k) [GPU]
-        # and encode(k-1) on a host thread. Slot j % S is reused by step j only
-        # after step j-S has completed (its H2D read host_in) and been encoded
-        # (its D2H wrote host_out).
-        S = slots
-        t_start, dec, enc, handles, pbs = {}, {}, {}, {}, {}
-
-        def start_decode(j):
-            t_start[j] = time.perf_counter()
-            dec[j] = dtp.submit(decode, j, j % S)
-
-        def finish(j):
-            t = time.perf_counter()
-            scores = handles.pop(j).wait()
-            phase["gpu_wait"] += time.perf_counter() - t
-            if record:
-                lat.append(time.perf_counter() - t_start.pop(j))
-            else:
-                t_start.pop(j)
-            enc[j] = tp.submit(encode, pbs.pop(j), scores)
-
-        for j in range(min(2, n_steps)):
-            start_decode(j)
-        for k in range(n_steps):
-            t1 = time.perf_counter()
-            pbs[k] = dec.pop(k).result()
-            t2 = time.perf_counter()
-            if k - S in enc:
-                enc.pop(k - S).result()
-            t3 = time.perf_counter()
-            handles[k] = eng.launch(B, k % S)
-            t4 = time.perf_counter()
-            phase["decode"] += t2 - t1
-            phase["enc_wait"] += t3 - t2
-            phase["launch"] += t4 - t3
-            if k >= 1:
-                finish(k - 1)  # two steps in flight on the GPU
-            if k + 2 < n_steps:
-                start_decode(k + 2)  # its slot held step k-1: done above
-        finish(n_steps - 1)
-        for f in enc.values():
-            f.result()
+        pipe.run(n_steps, record=record)
 
     def sync():
         if dev.type == "cuda":
@@ -188,8 +148,7 @@ def main():
 
     run(max(1, a.warmup), record=False)
     sync()
-    for key in phase:
-        phase[key] = 0.0
+    pipe.reset_stats()
     t0 = time.perf_counter()
     run(a.steps, record=True)
     sync()
@@ -233,7 +192,7 @@ def main():
         if a.json_extra:
             per = {k: round(v / a.steps * 1e6, 1) for k, v in phase.items()}
             print(json.dumps({"host_phase_us_per_step": per}), file=sys.stderr, flush=True)
-    tp.shutdown(wait=True)
+    pipe.close()
     shutdown()
 
 

@@ -167,7 +167,8 @@ torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tenso
 // ---------------------------------------------------------------- K4 / K3b
 torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor> bias, int64_t epi,
                    c10::optional<torch::Tensor> x0, c10::optional<torch::Tensor> xl, bool out_f32,
-                   c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sw, c10::optional<torch::Tensor> out) {
+                   c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sw, c10::optional<torch::Tensor> out,
+                   int64_t variant) {
   check_dev(A, "A");
   check_dev(W, "W");
   check_same_dev(A, W, "W");
@@ -195,8 +196,8 @@ torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor
     check_dev(*sw, "sw");
     TORCH_CHECK(sw->scalar_type() == torch::kFloat32 && sw->numel() == N, "sw must be fp32 [N]");
   }
-  TORCH_CHECK(epi >= 0 && epi <= 3, "epi must be 0..3");
-  if (epi == 3) {
+  TORCH_CHECK((epi & 15) <= 3 && epi >= 0 && epi < 32, "epi must be 0..3 (+16: M-fastest tile order)");
+  if ((epi & 15) == 3) {
     TORCH_CHECK(x0.has_value() && xl.has_value(), "cross epilogue needs x0 and xl");
     for (auto* t : {&x0, &xl}) {
       check_dev(**t, "x0/xl");
@@ -217,7 +218,7 @@ torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor
   check_hip(dtfs::launch_gemm(A.data_ptr(), K, W.data_ptr(), K, bias ? bias->data_ptr<float>() : nullptr,
                               sa ? sa->data_ptr<float>() : nullptr, sw ? sw->data_ptr<float>() : nullptr, C.data_ptr(),
                               N, out_f32, opt_ptr(x0), opt_ptr(xl), N, int(M), int(N), int(K), int(epi), fp8,
-                              cur_stream(A)),
+                              cur_stream(A), int(variant)),
             "gemm");
   return C;
 }
@@ -336,7 +337,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("out_bf16") = false);
   m.def("gemm", &gemm, py::arg("A"), py::arg("W"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("x0") = py::none(), py::arg("xl") = py::none(), py::arg("out_f32") = false,
-        py::arg("sa") = py::none(), py::arg("sw") = py::none(), py::arg("out") = py::none());
+        py::arg("sa") = py::none(), py::arg("sw") = py::none(), py::arg("out") = py::none(),
+        py::arg("variant") = 0);
   m.def("cross_v1", &cross_v1, py::arg("x0"), py::arg("w"), py::arg("b"), py::arg("want_x") = true,
         py::arg("head_w") = py::none());
   m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0);

@@ -54,7 +54,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   // consecutive tiles walk M first so one XCD shares W panels
-  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  // Tile order: N-fastest by default, so each XCD's contiguous run of tiles is
+  // a few row panels x ALL column panels - the big activation panel is pulled
+  // into that XCD's L2 once and reused by every column tile (the weight panel
+  // is small). epi bit 4 selects the M-fastest order instead (A/B testing).
+  const bool m_fast = (epi & 16) != 0;
+  const int tm = m_fast ? tile % tiles_m : tile / tiles_n;
+  const int tn = m_fast ? tile / tiles_m : tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -162,14 +168,360 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
         float v = acc[i][j][r];
         if (FP8) v *= swn * (sa ? sa[m] : 1.f);
         v += bn;
-        if (epi == EPI_RELU) v = fmaxf(v, 0.f);
-        else if (epi == EPI_SIGMOID) v = sigmoidf(v);
-        else if (epi == EPI_CROSS) v = bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
+        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
+        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
+        else if ((epi & 15) == EPI_CROSS) v =bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
         if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
         else C[m * ldc + n] = v;
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA variant (cdna_hip_programming.md §5 "global_load_lds", 2-phase
+// structure): tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR
+// round trip, no ds_write pass). The LDS image stays lane-linear (one
+// wave-instruction = 8 rows x 128 B) and the XOR swizzle moves to the per-lane
+// SOURCE chunk (rule 21), so the fragment reads use the same swz() as above.
+// Requires K % (128 / elem bytes) == 0; rows past M / N are clamped (their
+// results are never stored).
+template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+__global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
+    const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
+    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
+  constexpr int NW = WM_ * WN_;
+  constexpr int EB = FP8 ? 1 : 2;
+  constexpr int WTM = BM / WM_, WTN = BN / WN_;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int IA = BM / 8, IB = BN / 8;  // 1-KiB LDS-DMA instructions per tile
+  static_assert(IA % NW == 0 && IB % NW == 0, "tile rows must split evenly over waves");
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE_BYTES];
+
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // Tile order: N-fastest by default, so each XCD's contiguous run of tiles is
+  // a few row panels x ALL column panels - the big activation panel is pulled
+  // into that XCD's L2 once and reused by every column tile (the weight panel
+  // is small). epi bit 4 selects the M-fastest order instead (A/B testing).
+  const bool m_fast = (epi & 16) != 0;
+  const int tm = m_fast ? tile % tiles_m : tile / tiles_n;
+  const int tn = m_fast ? tile / tiles_m : tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN_, wn = wid % WN_;
+
+  // per-lane source offsets (row within the 8-row group, swizzled chunk)
+  const int lr = lane >> 3, ls = lane & 7;
+  int64_t a_off[IA / NW], b_off[IB / NW];
+#pragma unroll
+  for (int j = 0; j < IA / NW; ++j) {
+    const int r = 8 * (wid + j * NW) + lr;
+    const int gm = min(m0 + r, M - 1);
+    a_off[j] = int64_t(gm) * lda * EB + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < IB / NW; ++j) {
+    const int r = 8 * (wid + j * NW) + lr;
+    const int gn = min(n0 + r, N - 1);
+    b_off[j] = int64_t(gn) * ldw * EB + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+  auto stage = [&](int buf, int kt) {
+    uint8_t* base = smem + buf * STAGE_BYTES;
+    const int64_t kb0 = int64_t(kt) * 128;
+#pragma unroll
+    for (int j = 0; j < IA / NW; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(A + a_off[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + j * NW) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int j = 0; j < IB / NW; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(W + b_off[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + (wid + j * NW) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K * EB) / 128;
+  const int fr = lane & 15, fq = lane >> 4;
+  stage(0, 0);
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);  // DMA of the next tile under this tile's MFMAs
+    const uint8_t* as = smem + cur * STAGE_BYTES;
+    const uint8_t* bs = as + BM * 128;
+    if constexpr (!FP8) {
+      // Issue every fragment read of the K tile (both 32-deep halves) before
+      // the first MFMA, so the second half's LDS latency hides under the
+      // first half's MFMAs (the compiler then waits lgkmcnt(N), not 0).
+      bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(as + swz(wm * WTM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * WTN + j * 16 + fr, kk * 4 + fq));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      // schedule: first half's reads, then its MFMAs interleaved with the
+      // second half's reads (2 MFMA : 1 ds_read), then the rest of the MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+#pragma unroll
+      for (int g = 0; g < TM + TN; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (TM + TN), 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        fp8x8 af[TM], bfr[TN];
+        const int ch = kk * 2 + (fq >> 1), hoff = (fq & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const fp8x8*>(as + swz(wm * WTM + i * 16 + fr, ch) + hoff);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const fp8x8*>(bs + swz(wn * WTN + j * 16 + fr, ch) + hoff);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading this one
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * 16 + fr;
+    if (n >= N) continue;
+    const float bn = bias ? bias[n] : 0.f;
+    const float swn = sw ? sw[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r];
+        if (FP8) v *= swn * (sa ? sa[m] : 1.f);
+        v += bn;
+        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
+        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
+        else if ((epi & 15) == EPI_CROSS) v =bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
+        if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
+        else C[m * ldc + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+static void launch_glds(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
+                        const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M,
+                        int N, int K, int epi, hipStream_t st) {
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM_, WN_, FP8, OutT>), dim3(grid), dim3(WM_ * WN_ * 64), 0, st,
+                     static_cast<const uint8_t*>(A), lda, static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc,
+                     X0, XL, ldx, M, N, K, epi);
+}
+
+// ---------------------------------------------------------------------------
+// Deep-pipelined LDS-DMA variant: a STAGES-deep ring of K tiles with PREFETCH =
+// STAGES - 1 tiles in flight across barriers (cdna_hip_programming.md §5
+// "Pipelining across barriers"): every iteration issues the DMA for tile
+// kt + PREFETCH, computes tile kt, then waits with a COUNTED vmcnt that leaves
+// the just-issued tile in flight (never vmcnt(0) in the loop) and a raw
+// s_barrier (not __syncthreads, whose fence would drain the DMA).
+// Ring-slot hazards: slot (kt+P)%S was last read in iteration kt+P-S <= kt-1,
+// which every wave finished before the barrier ending that iteration (WAR);
+// tile kt+1 is read only after the vmcnt + barrier of iteration kt (RAW).
+template <int BM, int BN, int WM_, int WN_, int STAGES, bool FP8, typename OutT>
+__global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
+    const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
+    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
+  constexpr int NW = WM_ * WN_;
+  constexpr int EB = FP8 ? 1 : 2;
+  constexpr int WTM = BM / WM_, WTN = BN / WN_;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // LDS-DMA instructions per wave per tile
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "tile rows must split evenly over waves");
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  constexpr int PF = STAGES - 1;
+  constexpr int LOADS = IA + IB;
+
+  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE_BYTES];
+
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const bool m_fast = (epi & 16) != 0;
+  const int tm = m_fast ? tile % tiles_m : tile / tiles_n;
+  const int tn = m_fast ? tile / tiles_m : tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN_, wn = wid % WN_;
+
+  const int lr = lane >> 3, ls = lane & 7;
+  const uint8_t* a_src[IA];
+  const uint8_t* b_src[IB];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int r = 8 * (wid + j * NW) + lr;
+    a_src[j] = A + int64_t(min(m0 + r, M - 1)) * lda * EB + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int r = 8 * (wid + j * NW) + lr;
+    b_src[j] = W + int64_t(min(n0 + r, N - 1)) * ldw * EB + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+  auto stage = [&](int slot, int kt) {
+    uint8_t* base = smem + slot * STAGE_BYTES;
+    const int64_t kb0 = int64_t(kt) * 128;
+#pragma unroll
+    for (int j = 0; j < IA; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(a_src[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + j * NW) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int j = 0; j < IB; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(b_src[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + (wid + j * NW) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K * EB) / 128;
+  const int fr = lane & 15, fq = lane >> 4;
+  // prologue: PF tiles in flight, tile 0 landed
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (p < nk) stage(p, p);
+  if (nk > 1) {
+    static_assert(PF <= 3, "extend the prologue wait ladder");
+    // wait for tile 0 only: leave tiles 1..PF-1 (LOADS each) in flight
+    if constexpr (PF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+    else if constexpr (PF == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nk < PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // short K: drain (rare)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int slot = kt % STAGES;
+    const bool issue = kt + PF < nk;
+    if (issue) stage((kt + PF) % STAGES, kt + PF);
+    const uint8_t* as = smem + slot * STAGE_BYTES;
+    const uint8_t* bs = as + BM * 128;
+    if constexpr (!FP8) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm * WTM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * WTN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        fp8x8 af[TM], bfr[TN];
+        const int ch = kk * 2 + (fq >> 1), hoff = (fq & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const fp8x8*>(as + swz(wm * WTM + i * 16 + fr, ch) + hoff);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const fp8x8*>(bs + swz(wn * WTN + j * 16 + fr, ch) + hoff);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // RAW for tile kt+1: this wave's loads for it are done once at most the
+    // tiles issued after it are outstanding; every wave's, after the barrier.
+    if (kt + 1 < nk) {
+      const int ahead = min(PF - 1, nk - 1 - (kt + 1));  // tiles after kt+1 already issued
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's ds_reads retired (WAR)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // keep the next tile's ds_reads below the barrier
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * 16 + fr;
+    if (n >= N) continue;
+    const float bn = bias ? bias[n] : 0.f;
+    const float swn = sw ? sw[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r];
+        if (FP8) v *= swn * (sa ? sa[m] : 1.f);
+        v += bn;
+        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
+        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
+        else if ((epi & 15) == EPI_CROSS) v = bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
+        if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
+        else C[m * ldc + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM_, int WN_, int STAGES, bool FP8, typename OutT>
+static void launch_pipe(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
+                        const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M,
+                        int N, int K, int epi, hipStream_t st) {
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM_, WN_, STAGES, FP8, OutT>), dim3(grid), dim3(WM_ * WN_ * 64), 0, st,
+                     static_cast<const uint8_t*>(A), lda, static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc,
+                     X0, XL, ldx, M, N, K, epi);
 }
 
 template <int BM, int BN, bool FP8, typename OutT>
@@ -187,8 +539,53 @@ static void launch_cfg(const void* A, int64_t lda, const void* W, int64_t ldw, c
 template <bool FP8, typename OutT>
 static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                      const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M, int N,
-                     int K, int epi, hipStream_t st) {
+                     int K, int epi, hipStream_t st, int variant) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  const int EB = FP8 ? 1 : 2;
+  const bool glds_ok = (K * EB) % 128 == 0;
+  if (variant == 0 && glds_ok) {
+    // Measured on MI355X (bench/microbench.py --gemm-variants, interleaved):
+    //  * M <= 1024 (one request's candidates): 64x64 tiles, 4-deep LDS ring
+    //  * >= 256 tiles of 256x256: the 256x256 8-wave tile (best at M = 16K)
+    //  * >= 512 tiles of 128x128: 128x128 2-stage LDS-DMA, 2 blocks/CU
+    //  * otherwise (narrow N, e.g. the 512/256-wide MLP layers): 64x64 LDS-DMA
+    if (M <= 1024) variant = 8;
+    else if (blocks(256, 256) >= 256) variant = 9;
+    else if (blocks(128, 128) >= 512) variant = 2;
+    else variant = 4;
+  }
+  if (variant == 2 && glds_ok) {
+    launch_glds<128, 128, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 3 && glds_ok) {
+    launch_glds<256, 128, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 4 && glds_ok) {
+    launch_glds<64, 64, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 5 && glds_ok) {
+    launch_pipe<256, 128, 4, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 6 && glds_ok) {
+    launch_pipe<128, 128, 2, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 7 && glds_ok) {
+    launch_pipe<128, 128, 2, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 8 && glds_ok) {
+    launch_pipe<64, 64, 2, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 9 && glds_ok) {
+    launch_pipe<256, 256, 2, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
   if (blocks(128, 128) >= 256)
     launch_cfg<128, 128, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
   else if (blocks(64, 128) >= 256)
@@ -205,17 +602,17 @@ using namespace kern;
 
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
-                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st) {
+                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st, int variant) {
   if (M == 0 || N == 0) return hipSuccess;
   if ((fp8 ? K % 16 : K % 8) != 0) return hipErrorInvalidValue;  // 16-byte row chunks
   const bf16* x0 = static_cast<const bf16*>(X0);
   const bf16* xl = static_cast<const bf16*>(XL);
   if (fp8) {
-    if (out_f32) dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st);
-    else dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st);
+    if (out_f32) dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
+    else dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
   } else {
-    if (out_f32) dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st);
-    else dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st);
+    if (out_f32) dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
+    else dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
   }
   return hipGetLastError();
 }

@@ -42,7 +42,8 @@ hipError_t launch_embedding_bag(const void* table, const void* idx, bool idx64, 
 // K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
-                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st);
+                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st,
+                       int variant = 0);
 
 // K3: DCN-v1 cross network, all L layers fused.
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,

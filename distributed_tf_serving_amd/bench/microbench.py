@@ -48,6 +48,35 @@ def bench_gemm(M, N, K, act="relu", dev="cuda"):
             "fp8_us": round(f8, 2), "fp8_tflops": round(flops / f8 / 1e6, 1)}
 
 
+def bench_gemm_variants(M, N, K, dev="cuda", variants=(0, 2, 3, 4, 5, 6, 7, 8, 9)):
+    """Interleaved A/B of the GEMM kernel variants in one process (rule 24)."""
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    h = ops.hip()
+    ref = h.gemm(x, W, b, 1, None, None, True, None, None, None, 0)
+    res = {"op": "gemm_variants", "M": M, "N": N, "K": K}
+    # variant >= 100: same kernel as (variant - 100) with the legacy M-fastest tile order
+    def call(v, f32=False):
+        return h.gemm(x, W, b, 1 | (16 if v >= 100 else 0), None, None, f32, None, None, None, v % 100)
+    fns = {v: (lambda v=v: call(v)) for v in variants}
+    for v in variants:
+        out = call(v, True)
+        err = (out - ref).abs().max().item()
+        res[f"v{v}_maxerr"] = round(err, 5)
+    times = {v: [] for v in variants}
+    for _ in range(5):
+        for v in variants:
+            times[v].append(_time(fns[v], iters=20, rounds=1))
+    for v in variants:
+        us = statistics.median(times[v])
+        res[f"v{v}_us"] = round(us, 2)
+        res[f"v{v}_tf"] = round(2.0 * M * N * K / us / 1e6, 1)
+    lib = _time(lambda: torch.addmm(b.to(torch.bfloat16), x, W.t()))
+    res["hipblaslt_us"] = round(lib, 2)
+    return res
+
+
 def bench_embed(B, F=43, D=64, V=1_000_000, dev="cuda"):
     table = torch.randn(V, D, device=dev).to(torch.bfloat16)
     lin = torch.randn(V, device=dev)
@@ -91,8 +120,14 @@ def bench_model(family, B, dev="cuda", graphs=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--gemm-variants", action="store_true")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.gemm_variants:
+        for s in [(8192, 1024, 2752), (8192, 512, 1024), (8192, 256, 512), (16384, 1024, 2752), (4096, 1024, 2752),
+                  (512, 1024, 2752), (4096, 2752, 2752)]:
+            print(json.dumps(bench_gemm_variants(*s)), flush=True)
+        return
     shapes = [(512, 1024, 2752), (512, 512, 1024), (512, 256, 512), (4096, 1024, 2752), (8192, 1024, 2752),
               (4096, 2752, 2752)]
     if a.quick:
