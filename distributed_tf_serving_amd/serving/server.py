@@ -1,0 +1,113 @@
+"""ModelServer: the TF-Serving ModelServer equivalent for one GPU (or CPU).
+
+Builds a servable per configured model (random-init weights of the configured
+architecture), captures its HIP graphs for every batch bucket, starts its
+batching scheduler, and serves the PredictionService in-process and/or over
+gRPC::
+
+    python -m distributed_tf_serving_amd.serving.server --preset deepfm_1gpu --port 9999
+    python -m distributed_tf_serving_amd.serving.server --preset wdl_tiny_cpu --port 9999 --device cpu
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import signal
+from typing import Optional
+
+import torch
+
+from ..config import Config, load_preset
+from ..models import build_model
+from ..parallel.dist import DistContext
+from ..parallel.fanout import FanoutEngine
+from .batching import BatchingScheduler
+from .executor import ShardExecutor
+from .packing import PackedLayout
+from .registry import ModelRegistry, Servable, Signature
+from .service import PredictionServiceImpl
+
+log = logging.getLogger(__name__)
+
+
+def pick_device(pref: str = "auto") -> torch.device:
+    if pref == "cpu" or (pref == "auto" and not torch.cuda.is_available()):
+        return torch.device("cpu")
+    if pref.startswith("cuda") and ":" in pref:
+        return torch.device(pref)
+    return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+
+
+def build_servable(cfg: Config, device=None, version: Optional[int] = None, slots: int = 3) -> Servable:
+    sc = cfg.serving
+    dev = torch.device(device) if device is not None else pick_device(sc.device)
+    model = build_model(cfg.model, dev)
+    layout = PackedLayout(cfg.model.num_fields)
+    buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
+    ex = ShardExecutor(model, layout, buckets, dev, use_graphs=sc.use_graphs, slots=slots)
+    eng = FanoutEngine(ex, DistContext(device=dev), mode="local")
+    for B in buckets:
+        eng.prepare(B)
+    sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
+                              max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name)
+    sig = model.signature()
+    sigs = {sc.signature_name: Signature(inputs=sig["inputs"], outputs=sig["outputs"], method_name=sig["method_name"])}
+    return Servable(name=sc.model_name, version=sc.version if version is None else version, model=model,
+                    scheduler=sched, signatures=sigs, ids_key=sc.ids_key, wts_key=sc.wts_key,
+                    output_key=sc.output_key, fields=cfg.model.num_fields)
+
+
+class ModelServer:
+    def __init__(self, cfg: Config, device=None):
+        self.cfg = cfg
+        self.registry = ModelRegistry()
+        self.registry.load(build_servable(cfg, device))
+        self.service = PredictionServiceImpl(self.registry, cfg.serving.request_timeout_s)
+        self.front = None
+
+    def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32):
+        from .grpc_server import GrpcFrontDoor
+
+        self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers).start()
+        return self.front.port
+
+    def stop(self) -> None:
+        if self.front is not None:
+            self.front.stop()
+            self.front = None
+        self.registry.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="MI355X CTR model server (TF-Serving PredictionService)")
+    ap.add_argument("--preset", default="deepfm_1gpu")
+    ap.add_argument("--port", type=int, default=9999)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--model-name", default=None)
+    ap.add_argument("--grpc-workers", type=int, default=32)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    cfg = load_preset(a.preset)
+    if a.model_name:
+        cfg.serving.model_name = a.model_name
+    srv = ModelServer(cfg, device=a.device)
+    port = srv.start_grpc(a.port, a.host, a.grpc_workers)
+    print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
+    signal.signal(signal.SIGTERM, lambda *_: srv.stop())
+    try:
+        srv.front.wait()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        srv.stop()
+
+
+if __name__ == "__main__":
+    main()
