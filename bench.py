@@ -48,6 +48,7 @@ from distributed_tf_serving_amd.ops import native  # noqa: E402
 from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown  # noqa: E402
 from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E402
 from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E402
+from distributed_tf_serving_amd.serving.arena import ArenaLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
@@ -66,6 +67,8 @@ def parse_args():
     ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"])
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")
+    ap.add_argument("--ingest", default="arena", choices=["arena", "packed"],
+                    help="arena: host parses framing, GPU unpacks raw request bytes; packed: host decodes rows")
     ap.add_argument("--decode-threads", type=int, default=8)
     ap.add_argument("--pool", type=int, default=8, help="distinct pre-serialized steps per rank")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "fp8"])
@@ -95,7 +98,9 @@ def main():
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
     slots = 4
     ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
-    eng = FanoutEngine(ex, ctx, mode=a.mode)
+    rows_in_max = B * (ctx.world if a.mode == "scatter" else 1)
+    arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
+    eng = FanoutEngine(ex, ctx, mode=a.mode, ingest=a.ingest, arena=arena_layout)
     eng.prepare(B)
     nat = native()
 
@@ -108,10 +113,27 @@ def main():
 
     diag_pb = nat.parse_batch(pool[0], "feat_ids", "feat_wts", F) if pool[0] else None
 
+    if a.ingest == "arena":
+        # Requests are received into pinned arenas (a ring of a.pool receive
+        # buffers, as an RDMA / shared-memory transport would deliver them);
+        # every step re-parses its arena's framing on the host and the GPU
+        # unpacks the raw payloads (csrc/kernels/ingest.hip).
+        arenas, spans = [], []
+        for reqs in pool:
+            ar = arena_layout.alloc(pin=dev.type == "cuda")
+            spans.append(arena_layout.place(ar, reqs) if reqs else [])
+            arenas.append(ar)
+
     def decode(k: int, slot: int):
         reqs = pool[k % len(pool)]
         if not reqs:
             return None
+        if a.ingest == "arena":
+            ab = arena_layout.build(arenas[k % len(pool)], spans[k % len(pool)])
+            errs = [e for e in ab.errors if e]
+            if errs:
+                raise RuntimeError(errs[0])
+            return (ab, arenas[k % len(pool)])
         if a.diag_skip_host and k >= 2:  # diagnostic only: GPU pipeline without host decode
             return diag_pb
         pb = nat.parse_batch(reqs, "feat_ids", "feat_wts", F)
@@ -126,12 +148,22 @@ def main():
     def encode(pb, scores: torch.Tensor):
         if pb is None:
             return []
+        if isinstance(pb, tuple):
+            pb = pb[0]
         return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores,
                                           list(pb.rows), list(pb.offsets))
 
+    def launch(k: int, slot: int, ctx_k):
+        if a.ingest == "arena" and ctx_k is not None:
+            ab, ar = ctx_k
+            return eng.launch(B, slot, src=ar, nbytes=ab.used_bytes)
+        if a.ingest == "arena":  # a rank with no requests (scatter mode, rank > 0)
+            return eng.launch(B, slot, nbytes=0)
+        return eng.launch(B, slot)
+
     # decode(k+3) || H2D(k+1..k+2) [SDMA] || forward(k) [GPU] || encode(k-1)
-    pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1,
-                        produce=decode, consume=lambda k, pb, scores: encode(pb, scores))
+    pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1, produce=decode,
+                        consume=lambda k, pb, scores: encode(pb, scores), launch=launch)
     phase = pipe.phase
     lat = pipe.latencies
 

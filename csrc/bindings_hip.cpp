@@ -291,6 +291,22 @@ torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<
   return out;
 }
 
+// ---------------------------------------------------------------- K0 ingest
+void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
+  check_dev(arena, "arena");
+  check_dev(packed, "packed");
+  check_same_dev(arena, packed, "packed");
+  TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.numel() > dtfs::kArenaPayloadOff, "arena: uint8 [cap]");
+  TORCH_CHECK(packed.scalar_type() == torch::kInt64 && packed.dim() == 2, "packed must be int64 [B, W]");
+  TORCH_CHECK(packed.size(1) * 8 >= 12 * fields, "packed rows too narrow for the field count");
+  c10::DeviceGuard g(arena.device());
+  // descriptor offsets come from the (validated) host parse of this arena; the
+  // kernel additionally bounds n_req by the descriptor capacity
+  check_hip(dtfs::launch_unpack_arena(arena.data_ptr(), packed.data_ptr<int64_t>(), int(packed.size(0)), int(fields),
+                                      int(packed.size(1)), dtfs::kArenaMaxRequests, cur_stream(arena)),
+            "unpack_arena");
+}
+
 // ---------------------------------------------------------------- fp8
 std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x) {
   check_dev(x, "x");
@@ -345,6 +361,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true);
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"));
+  m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);
 

@@ -34,6 +34,13 @@ struct EmbedArgs {
 };
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 
+// K0 ingest: request arena (header + descriptors + raw request bytes) -> packed
+// rows [B, W] int64 (serving/arena.py, csrc/runtime/arena.h share the layout).
+constexpr int kArenaPayloadOff = 64 + 32 * 1024;  // descriptors: up to 1024 requests
+constexpr int kArenaMaxRequests = 1024;
+hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
+                               hipStream_t st);
+
 // K1b: sum/mean embedding bag with CSR offsets [nbags+1].
 hipError_t launch_embedding_bag(const void* table, const void* idx, bool idx64, const int64_t* offsets,
                                 const float* psw, int nbags, int64_t nnz, int D, int64_t modulo, bool mean, float* out_f32,

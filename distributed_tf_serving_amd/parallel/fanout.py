@@ -72,9 +72,21 @@ class StepHandle:
 
 class FanoutEngine:
     def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
-                 step_graphs: bool = True, native_launch: bool = True):
+                 step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None):
+        """``ingest="packed"``: the host decodes into packed rows (host_in) and
+        the H2D moves rows. ``ingest="arena"``: the host only parses request
+        framing into a request arena (serving/arena.py); the H2D moves the raw
+        request bytes and the GPU unpacks rows (csrc/kernels/ingest.hip)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
+        if ingest not in ("packed", "arena"):
+            raise ValueError("ingest must be 'packed' or 'arena'")
+        if ingest == "arena" and arena is None:
+            raise ValueError("arena ingest needs an ArenaLayout")
+        self.ingest = ingest
+        self.arena = arena
+        self._host_arena: Dict[int, torch.Tensor] = {}
+        self._dev_arena: Dict[int, torch.Tensor] = {}
         self.ex = executor
         self.ctx = ctx
         self.world = ctx.world if ctx.is_distributed else 1
@@ -126,6 +138,24 @@ class FanoutEngine:
             self._host_out[key] = t
         return t
 
+    def host_arena(self, slot: int = 0) -> torch.Tensor:
+        """Pinned request arena of a slot (arena ingest)."""
+        t = self._host_arena.get(slot)
+        if t is None:
+            t = self._host_arena[slot] = self.arena.alloc(pin=self.cuda)
+        return t
+
+    def dev_arena(self, slot: int = 0) -> torch.Tensor:
+        t = self._dev_arena.get(slot)
+        if t is None:
+            t = self._dev_arena[slot] = self.arena.alloc(device=self.dev)
+        return t
+
+    def _unpack(self, arena_dev: torch.Tensor, packed: torch.Tensor) -> None:
+        from ..ops import hip
+
+        hip().unpack_arena(arena_dev, packed, self.layout.fields)
+
     def _dev(self, store, key, shape, dtype):
         t = store.get(key)
         if t is None:
@@ -162,22 +192,34 @@ class FanoutEngine:
         cur = torch.cuda.current_stream(self.dev)
         h_out = self.host_out(B, slot)
         buf = self.ex.input_buffer(B, slot)
+        arena_dev = self.dev_arena(slot) if self.ingest == "arena" else None
+
+        def body():
+            if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows
+                self._unpack(arena_dev, buf)
+            h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(2):
-                h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+                body()
         side.synchronize()
         pool = self.ex._pools.get(("step", slot))
         if pool is None:
             pool = self.ex._pools[("step", slot)] = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool, stream=side):
-            h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+            body()
         self._step_graph[key] = g
 
-    def _launch_step_graph(self, B: int, slot: int, h_in, h_out, rows: int, t0: float) -> StepHandle:
+    def _launch_step_graph(self, B: int, slot: int, h_in, h_out, rows: int, t0: float,
+                           nbytes: Optional[int] = None) -> StepHandle:
         self._capture_step(B, slot)
+        # H2D target: the graph's packed-row input, or (arena ingest) the slot's device arena
+        dst = self.dev_arena(slot) if self.ingest == "arena" else self.ex.input_buffer(B, slot)
+        if nbytes is None:
+            nbytes = B * self.layout.row_bytes
         if self.native_launch:
             # C++ StepRunner: SDMA H2D + hipGraphLaunch + events, no torch stream
             # bookkeeping in the loop (csrc/runtime/step_runner.cpp)
@@ -185,18 +227,16 @@ class FanoutEngine:
                 from ..ops import hip
 
                 self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
-            buf = self.ex.input_buffer(B, slot)
-            nbytes = B * self.layout.row_bytes
-            self._runner.launch(slot, buf, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
+            self._runner.launch(slot, dst, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
             return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot),
                               t_submit=t0)
         cur = torch.cuda.current_stream(self.dev)
-        buf = self.ex.input_buffer(B, slot)
         ev_in_free = self._ev_in_free.get(slot)
         with torch.cuda.stream(self.h2d_stream):  # SDMA, overlaps the previous step
             if ev_in_free is not None:
                 self.h2d_stream.wait_event(ev_in_free)
-            buf.copy_(h_in[:B], non_blocking=True)
+            dst.view(-1)[: nbytes // dst.element_size()].copy_(
+                h_in.view(-1)[: nbytes // h_in.element_size()], non_blocking=True)
         cur.wait_stream(self.h2d_stream)
         self._step_graph[(B, slot)].replay()
         ev = torch.cuda.Event()
@@ -205,21 +245,36 @@ class FanoutEngine:
         return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=ev, t_submit=t0)
 
     # -- one step --------------------------------------------------------------
-    def launch(self, B: int, slot: int = 0) -> StepHandle:
-        """Enqueue one fan-out step for bucket B from host_in(B, slot).
+    def launch(self, B: int, slot: int = 0, src: Optional[torch.Tensor] = None,
+               nbytes: Optional[int] = None) -> StepHandle:
+        """Enqueue one fan-out step for bucket B.
 
+        Input: host_in(B, slot) packed rows, or with arena ingest the request
+        arena ``src`` (default host_arena(slot)) of which ``nbytes`` are used.
         Returns immediately on GPU (all work is stream-ordered); call
         ``handle.wait()`` for the scores in host_out(B, slot)."""
         self.check_bucket(B)
         key = (B, slot)
-        h_in, h_out = self.host_in(B, slot), self.host_out(B, slot)
+        h_out = self.host_out(B, slot)
+        arena_mode = self.ingest == "arena"
+        if arena_mode:
+            h_in = self.host_arena(slot) if src is None else src
+            if nbytes is None:
+                raise ValueError("arena ingest: pass nbytes (ArenaBatch.used_bytes)")
+        else:
+            h_in = self.host_in(B, slot) if src is None else src
         rows = self.contrib_rows(B)
         t0 = time.perf_counter()
         exec_in = self.ex.input_buffer(B, slot)
         if not self.cuda:
+            if arena_mode:  # host reference of the GPU unpack
+                packed = self.host_in(B, slot)
+                if rows:
+                    self.arena.unpack_cpu(h_in, packed[:rows])
+                h_in = packed
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
         if self._step_graphs_enabled():
-            return self._launch_step_graph(B, slot, h_in, h_out, rows, t0)
+            return self._launch_step_graph(B, slot, h_in, h_out, rows, t0, nbytes)
 
         cur = torch.cuda.current_stream(self.dev)
         ev_in_free = self._ev_in_free.get(slot)
@@ -234,9 +289,14 @@ class FanoutEngine:
             # input, so this H2D overlaps the previous step's compute
             if ev_in_free is not None:
                 self.h2d_stream.wait_event(ev_in_free)
-            if rows:
+            if rows and arena_mode:
+                ad = self.dev_arena(slot)
+                ad[:nbytes].copy_(h_in[:nbytes], non_blocking=True)
+            elif rows:
                 send[:rows].copy_(h_in[:rows], non_blocking=True)
         cur.wait_stream(self.h2d_stream)
+        if rows and arena_mode:
+            self._unpack(self.dev_arena(slot), send[:rows])
 
         if self.mode == "alltoall":
             dist.all_to_all_single(exec_in, send, group=self.group)

@@ -24,11 +24,15 @@ from typing import Any, Callable, Dict, List, Optional
 
 class StepPipeline:
     def __init__(self, engine, B: int, slots: int = 3, depth: int = 2,
-                 produce: Callable[[int, int], Any] = None, consume: Callable[[int, Any, Any], Any] = None):
+                 produce: Callable[[int, int], Any] = None, consume: Callable[[int, Any, Any], Any] = None,
+                 launch: Optional[Callable[[int, int, Any], Any]] = None):
+        """``launch(k, slot, ctx)`` overrides ``engine.launch(B, slot)`` (e.g. to
+        pass an arena and its used byte count)."""
         if slots < depth + 1:
             raise ValueError("need slots >= depth + 1")
         self.eng, self.B, self.S, self.depth = engine, B, slots, depth
         self.produce, self.consume = produce, consume
+        self.launch_fn = launch
         self.dec_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtfs-decode")
         self.enc_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtfs-encode")
         self.latencies: List[float] = []
@@ -71,7 +75,10 @@ class StepPipeline:
             if f is not None:
                 f.result()
             t3 = time.perf_counter()
-            handles[k] = self.eng.launch(self.B, k % S)
+            if self.launch_fn is not None:
+                handles[k] = self.launch_fn(k, k % S, ctxs[k])
+            else:
+                handles[k] = self.eng.launch(self.B, k % S)
             t4 = time.perf_counter()
             self.phase["decode_wait"] += t2 - t1
             self.phase["enc_wait"] += t3 - t2

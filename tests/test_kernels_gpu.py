@@ -215,3 +215,21 @@ def test_dcn_v2_fp8_close_to_bf16(cuda):
     wts = torch.rand(256, 43, device=cuda)
     a, b = m16(ids, wts), m8(ids, wts)
     assert (a - b).abs().max().item() < 0.05
+
+
+def test_unpack_arena_gpu_matches_cpu(cuda):
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    A, L = ArenaLayout(43, 2048), PackedLayout(43)
+    ar = A.alloc()
+    s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=5)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((1, True), (300, True), (17, False), (512, True))]
+    ab = A.build(ar, A.place(ar, reqs))
+    assert ab.total_rows == 830 and not any(ab.errors)
+    ref = A.unpack_cpu(ar, L.alloc(1024))
+    got = L.alloc(1024, device=cuda)
+    got.fill_(-1)
+    ops.hip().unpack_arena(ar.to(cuda), got, 43)
+    assert torch.equal(got.cpu(), ref)  # rows past total_rows are zeroed too
