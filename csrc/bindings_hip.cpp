@@ -291,6 +291,56 @@ torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<
   return out;
 }
 
+// ---------------------------------------------------------------- K4+K6 fused
+torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, int64_t act, torch::Tensor hw,
+                        double hbias, c10::optional<torch::Tensor> extra, bool sigmoid,
+                        c10::optional<torch::Tensor> out) {
+  check_dev(A, "A");
+  check_dev(W, "W");
+  check_dev(bias, "bias");
+  check_dev(hw, "hw");
+  check_same_dev(A, W, "W");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && W.scalar_type() == torch::kBFloat16, "A, W must be bf16");
+  TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "A [M, K], W [N, K]");
+  TORCH_CHECK(A.is_contiguous() && W.is_contiguous(), "A, W must be contiguous");
+  const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+  TORCH_CHECK(K % 64 == 0, "gemm_head needs K % 64 == 0");
+  TORCH_CHECK(N > 0 && N <= 256, "gemm_head needs 0 < N <= 256");
+  TORCH_CHECK(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
+  TORCH_CHECK(bias.scalar_type() == torch::kFloat32 && bias.numel() == N, "bias must be fp32 [N]");
+  TORCH_CHECK(hw.scalar_type() == torch::kFloat32 && hw.numel() == N, "hw must be fp32 [N]");
+  if (extra) {
+    check_dev(*extra, "extra");
+    TORCH_CHECK(extra->scalar_type() == torch::kFloat32 && extra->numel() == M, "extra must be fp32 [M]");
+  }
+  c10::DeviceGuard g(A.device());
+  torch::Tensor y;
+  if (out) {
+    TORCH_CHECK(out->scalar_type() == torch::kFloat32 && out->numel() == M && out->is_contiguous(),
+                "out must be fp32 [M] contiguous");
+    // out may be pinned host memory (mapped): the kernel writes scores straight to the host
+    TORCH_CHECK(out->is_cuda() || out->is_pinned(), "out must be on the device or pinned host memory");
+    y = *out;
+  } else {
+    y = torch::empty({M}, A.options().dtype(torch::kFloat32));
+  }
+  float* yp = y.data_ptr<float>();
+  if (!y.is_cuda()) {
+    // pinned host allocations are mapped at the same virtual address on ROCm;
+    // prefer the runtime's answer when it has one
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, yp, 0) == hipSuccess && dp)
+      yp = static_cast<float*>(dp);
+    else
+      (void)hipGetLastError();
+  }
+  check_hip(dtfs::launch_gemm_head(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr<float>(), int(act),
+                                   hw.data_ptr<float>(), float(hbias), extra ? extra->data_ptr<float>() : nullptr,
+                                   sigmoid ? 2 : 0, yp, int(M), int(N), int(K), cur_stream(A)),
+            "gemm_head");
+  return y;
+}
+
 // ---------------------------------------------------------------- K0 ingest
 void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
   check_dev(arena, "arena");
@@ -360,6 +410,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0);
   m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true);
+  m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
+        py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"));
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);

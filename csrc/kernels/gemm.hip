@@ -349,6 +349,136 @@ static void launch_glds(const void* A, int64_t lda, const void* W, int64_t ldw, 
 }
 
 // ---------------------------------------------------------------------------
+// K4+K6 fused: the last MLP layer and the CTR head in one kernel.
+//   h = act(A W^T + b)            [M, N]   (never written to memory)
+//   y[m] = out_act(h[m,:] . hw + hbias + extra[m])
+// One workgroup owns BM rows x ALL N columns (N <= 256), so the row dot
+// product is reduced in-block: lanes sharing a row (xor-shuffle over the 16
+// column lanes of a 16x16 tile) then the 4 waves through LDS. Saves the head
+// kernel, its launch gap and the [M, N] activation round trip. y may be a
+// device pointer or a mapped pinned-host pointer (scores land on the host
+// straight from the kernel).
+template <int BM, int TN>
+__global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                        const uint8_t* __restrict__ W, int64_t ldw,
+                                                        const float* __restrict__ bias, int act,
+                                                        const float* __restrict__ hw, float hbias,
+                                                        const float* __restrict__ extra, int out_act,
+                                                        float* __restrict__ y, int M, int N, int K) {
+  constexpr int WN_ = 4, NW = 4;
+  constexpr int BN = 16 * TN * WN_;
+  constexpr int TM = BM / 16;
+  constexpr int IA = BM / 8, IB = BN / 8;
+  static_assert(IA % NW == 0 && IB % NW == 0, "tile rows must split evenly over waves");
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE_BYTES + NW * BM * 4];
+  float* red = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
+
+  const int m0 = blockIdx.x * BM;
+  const int lane = threadIdx.x & 63;
+  const int wn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane >> 3, ls = lane & 7;
+  int64_t a_off[IA / NW], b_off[IB / NW];
+#pragma unroll
+  for (int j = 0; j < IA / NW; ++j) {
+    const int r = 8 * (wn + j * NW) + lr;
+    a_off[j] = int64_t(min(m0 + r, M - 1)) * lda * 2 + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < IB / NW; ++j) {
+    const int r = 8 * (wn + j * NW) + lr;
+    b_off[j] = int64_t(min(r, N - 1)) * ldw * 2 + ((ls ^ ((r >> 1) & 7)) << 4);
+  }
+  auto stage = [&](int buf, int kt) {
+    uint8_t* base = smem + buf * STAGE_BYTES;
+    const int64_t kb0 = int64_t(kt) * 128;
+#pragma unroll
+    for (int j = 0; j < IA / NW; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(A + a_off[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + (wn + j * NW) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int j = 0; j < IB / NW; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(W + b_off[j] + kb0),
+                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + (wn + j * NW) * 1024),
+                                       16, 0, 0);
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (K * 2) / 128;
+  const int fr = lane & 15, fq = lane >> 4;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const uint8_t* as = smem + cur * STAGE_BYTES;
+    const uint8_t* bs = as + BM * 128;
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[kk][i] = *reinterpret_cast<const bf16x8*>(as + swz(i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * 16 * TN + j * 16 + fr, kk * 4 + fq));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+  // epilogue: per-row partial dot over this wave's columns
+  float part[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = wn * 16 * TN + j * 16 + fr;
+    const bool ok = n < N;
+    const float bn = ok ? bias[n] : 0.f;
+    const float wv = ok ? hw[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + bn;
+        if (act == EPI_RELU) v = fmaxf(v, 0.f);
+        part[i][r] += v * wv;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = part[i][r];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (fr == 0) red[wn * BM + i * 16 + fq * 4 + r] = v;
+    }
+  __syncthreads();
+  for (int row = threadIdx.x; row < BM; row += blockDim.x) {
+    const int m = m0 + row;
+    if (m >= M) continue;
+    float s = hbias + (extra ? extra[m] : 0.f);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * BM + row];
+    y[m] = out_act == EPI_SIGMOID ? sigmoidf(s) : s;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Deep-pipelined LDS-DMA variant: a STAGES-deep ring of K tiles with PREFETCH =
 // STAGES - 1 tiles in flight across barriers (cdna_hip_programming.md §5
 // "Pipelining across barriers"): every iteration issues the DMA for tile
@@ -599,6 +729,32 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
 }  // namespace kern
 
 using namespace kern;
+
+hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
+                            const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
+                            int K, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if ((K * 2) % 128 != 0 || N > 256 || N <= 0) return hipErrorInvalidValue;
+  const uint8_t* a = static_cast<const uint8_t*>(A);
+  const uint8_t* w = static_cast<const uint8_t*>(W);
+  // 32-row tiles give >= 256 workgroups at the bench batch (8192 rows)
+  const bool small = M >= 4096;
+  if (N > 128) {
+    if (small)
+      hipLaunchKernelGGL((gemm_head_kernel<32, 4>), dim3((M + 31) / 32), dim3(256), 0, st, a, lda, w, ldw, bias, act,
+                         hw, hbias, extra, out_act, y, M, N, K);
+    else
+      hipLaunchKernelGGL((gemm_head_kernel<64, 4>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act,
+                         hw, hbias, extra, out_act, y, M, N, K);
+  } else if (N > 64) {
+    hipLaunchKernelGGL((gemm_head_kernel<64, 2>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act, hw,
+                       hbias, extra, out_act, y, M, N, K);
+  } else {
+    hipLaunchKernelGGL((gemm_head_kernel<64, 1>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act, hw,
+                       hbias, extra, out_act, y, M, N, K);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,

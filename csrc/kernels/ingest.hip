@@ -48,18 +48,27 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
       wts_src = payload + desc[4 * lo + 1] + lr * (4 * F);
     }
   }
+  // Each lane produces one aligned 8-byte output word from a possibly
+  // misaligned source: three aligned dword loads + byte funnel shifts
+  // (v_alignbyte) instead of eight byte loads. The ids and wts spans are
+  // multiples of 4 bytes long, so a word never straddles them except at the
+  // ids|wts boundary, which is 8-aligned in the output (8F bytes).
   for (int c = lane; c < W; c += 64) {
     const int b0 = 8 * c;
     uint64_t v = 0;
-    if (ids_src) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int b = b0 + j;
-        uint64_t byte = 0;
-        if (b < ids_bytes) byte = ids_src[b];
-        else if (b < row_bytes) byte = wts_src[b - ids_bytes];
-        v |= byte << (8 * j);
-      }
+    if (ids_src && b0 < row_bytes) {
+      const uint8_t* s = b0 < ids_bytes ? ids_src + b0 : wts_src + (b0 - ids_bytes);
+      const int avail = b0 < ids_bytes ? 8 : min(8, row_bytes - b0);  // 8, or 4 at the wts tail
+      const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+      const int sh = int(a & 3);
+      // load exactly the dwords the span covers (never read past it)
+      const uint32_t w0 = w[0];
+      const uint32_t w1 = (avail == 8 || sh) ? w[1] : 0u;
+      const uint32_t w2 = (avail == 8 && sh) ? w[2] : 0u;
+      const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+      v = avail == 8 ? (uint64_t(hi) << 32) | lo : uint64_t(lo);
     }
     dst[c] = int64_t(v);
   }

@@ -52,6 +52,11 @@ hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, c
                        int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st,
                        int variant = 0);
 
+// K4+K6 fused: y[m] = out_act(act(A W^T + b)[m,:] . hw + hbias + extra[m]); N <= 256, bf16.
+hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
+                            const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
+                            int K, hipStream_t st);
+
 // K3: DCN-v1 cross network, all L layers fused.
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
                            void* out_x, int64_t ldo, const float* head_w, float* out_dot, hipStream_t st);

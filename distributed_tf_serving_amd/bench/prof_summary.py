@@ -1,0 +1,77 @@
+"""Summarise a rocprofv3 ``--kernel-trace --stats`` run (rocpd SQLite output)
+into a markdown table for ``profiles/``.
+
+    python -m distributed_tf_serving_amd.bench.prof_summary gpurun_out/prof/run_results.db \
+        --steps 110 --title "bench.py R=16" > profiles/bench_r16.md
+
+Per kernel: calls, total / mean / min / max us, share of GPU busy time, and
+per-step cost (total / steps). Also reports the steady-state step period
+(median gap between consecutive launches of the step's last kernel) and the
+idle gap between steps, the two numbers the serving pipeline is tuned on.
+"""
+from __future__ import annotations
+
+import argparse
+import re
+import sqlite3
+import statistics
+from collections import defaultdict
+
+
+def _short(name: str) -> str:
+    name = re.sub(r"\(.*$", "", name)  # drop argument lists
+    name = name.replace("void ", "").replace("dtfs::kern::", "")
+    return name[:90]
+
+
+def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "") -> str:
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, start, end, duration from kernels order by start"))
+    copies = list(c.execute("select name, start, end, duration, size from memory_copies order by start"))
+    agg = defaultdict(list)
+    for name, s, e, d in rows:
+        agg[_short(name)].append(d / 1e3)
+    busy = sum(sum(v) for v in agg.values())
+    out = [f"# {title or db}", ""]
+    if rows:
+        span = (rows[-1][2] - rows[0][1]) / 1e3
+        out.append(f"kernels: {len(rows)} dispatches, GPU busy {busy:.0f} us over a {span:.0f} us trace span "
+                   f"({100 * busy / max(span, 1e-9):.1f}% busy)")
+    out += ["", "| kernel | calls | total us | mean us | min us | max us | % busy |" +
+            (" us/step |" if steps else ""),
+            "|---|---:|---:|---:|---:|---:|---:|" + ("---:|" if steps else "")]
+    for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+        t = sum(v)
+        line = (f"| `{k}` | {len(v)} | {t:.0f} | {statistics.mean(v):.2f} | {min(v):.2f} | {max(v):.2f} | "
+                f"{100 * t / max(busy, 1e-9):.1f} |")
+        if steps:
+            line += f" {t / steps:.2f} |"
+        out.append(line)
+    if copies:
+        cagg = defaultdict(list)
+        for name, s, e, d, size in copies:
+            cagg[(name, size)].append(d / 1e3)
+        out += ["", "| memory copy | bytes | calls | mean us | GB/s |", "|---|---:|---:|---:|---:|"]
+        for (name, size), v in sorted(cagg.items(), key=lambda kv: -len(kv[1]))[:12]:
+            m = statistics.mean(v)
+            out.append(f"| {name} | {size} | {len(v)} | {m:.2f} | {size / max(m, 1e-9) / 1e3:.1f} |")
+    if last_kernel:
+        ends = [(s, e) for name, s, e, d in rows if last_kernel in name]
+        if len(ends) > 4:
+            period = statistics.median((b[1] - a[1]) / 1e3 for a, b in zip(ends, ends[1:]))
+            out += ["", f"steady-state period between `{last_kernel}` launches: {period:.1f} us (median)"]
+    return "\n".join(out) + "\n"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("--title", default="")
+    ap.add_argument("--last-kernel", default="", help="substring of the step's final kernel, for the step period")
+    a = ap.parse_args()
+    print(summarize(a.db, a.steps, a.title, a.last_kernel), end="")
+
+
+if __name__ == "__main__":
+    main()

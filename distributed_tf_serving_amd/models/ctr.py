@@ -94,8 +94,7 @@ class WideDeep(CTRModel):
     def _forward(self, ids, wts):
         x, wide = ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
                             want_x=True, want_fm=True, fm2=False)
-        h = self.mlp(x)
-        return ops.head(h, self.head_w, self.head_b, extra=wide, sigmoid=True)
+        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide)
 
 
 class DeepFM(CTRModel):
@@ -115,8 +114,7 @@ class DeepFM(CTRModel):
     def _forward(self, ids, wts):
         x, fm = ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
                           want_x=True, want_fm=True, fm2=True)
-        h = self.mlp(x)
-        return ops.head(h, self.head_w, self.head_b, extra=fm, sigmoid=True)
+        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm)
 
 
 class DCN(CTRModel):
@@ -143,8 +141,7 @@ class DCN(CTRModel):
     def _forward(self, ids, wts):
         x, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
         _, cross_logit = ops.cross_v1(x, self.cross_w, self.cross_b, want_x=False, head_w=self.head_wc)
-        h = self.mlp(x)
-        return ops.head(h, self.head_wd, self.head_b, extra=cross_logit, sigmoid=True)
+        return self.mlp.forward_head(x, self.head_wd, self.head_b, extra=cross_logit)
 
 
 class DCNv2(CTRModel):
@@ -197,8 +194,7 @@ class DCNv2(CTRModel):
         for i in range(self.cfg.num_cross_layers):
             xl = self._cross_layer(i, x0, xl)
         cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
-        h = self.mlp(x0)
-        return ops.head(h, self.head_wd, self.head_b, extra=cross_logit, sigmoid=True)
+        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit)
 
 
 class DLRM(CTRModel):
@@ -245,8 +241,7 @@ class DLRM(CTRModel):
 
     def interact_and_top(self, dense_out: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
         z = ops.dot_interaction(dense_out, emb, self.inter_cols)
-        h = self.top(z)
-        return ops.head(h, self.head_w, self.head_b, sigmoid=True)
+        return self.top.forward_head(z, self.head_w, self.head_b)
 
     def _forward(self, ids, wts):
         dense_out = self.bottom(self.dense_input(wts))

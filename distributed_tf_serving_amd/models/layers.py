@@ -93,3 +93,14 @@ class MLP(nn.Module):
         for layer in self.layers:
             x = layer(x)
         return x
+
+    def forward_head(self, x: torch.Tensor, head_w: torch.Tensor, head_b: float,
+                     extra: Optional[torch.Tensor] = None, sigmoid: bool = True) -> torch.Tensor:
+        """MLP then CTR head. On the GPU the last layer and the head run as one
+        kernel (ops.linear_head) whenever its shape allows."""
+        for layer in self.layers[:-1]:
+            x = layer(x)
+        last = self.layers[-1]
+        if x.is_cuda and not last.fp8 and last.act in ("relu", "none") and ops.linear_head_ok(x, last.weight):
+            return ops.linear_head(x, last.weight, last.bias, last.act, head_w, head_b, extra=extra, sigmoid=sigmoid)
+        return ops.head(last(x), head_w, head_b, extra=extra, sigmoid=sigmoid)

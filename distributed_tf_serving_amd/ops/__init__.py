@@ -223,6 +223,34 @@ def head(x: torch.Tensor, w: torch.Tensor, bias: float = 0.0, extra: Optional[to
     return torch.sigmoid(y) if sigmoid else y
 
 
+def linear_head_ok(x: torch.Tensor, W: torch.Tensor) -> bool:
+    """Shapes the fused last-layer+head kernel covers (bf16, K % 64, N <= 256)."""
+    return (x.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and x.shape[1] % 64 == 0
+            and 0 < W.shape[0] <= 256)
+
+
+def linear_head(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: str, hw: torch.Tensor, hbias: float = 0.0,
+                extra: Optional[torch.Tensor] = None, sigmoid: bool = True,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K4+K6 fused: out_act(act(x W^T + b) . hw + hbias + extra) -> fp32 [M].
+
+    The [M, N] activation of the last MLP layer never leaves registers; ``out``
+    may be pinned host memory (the kernel then writes scores to the host)."""
+    if x.is_cuda:
+        return hip().gemm_head(x.contiguous(), W, b, _ACTS[act], hw, float(hbias), extra, sigmoid, out)
+    h = x.float() @ W.float().t() + b.float()
+    if act == "relu":
+        h = torch.relu(h)
+    y = h @ hw.float() + float(hbias)  # the fused kernel keeps h in fp32 (no bf16 round trip)
+    if extra is not None:
+        y = y + extra.float()
+    y = torch.sigmoid(y) if sigmoid else y
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
 # ------------------------------------------------------------------ K7
 def sort_scores(scores: torch.Tensor, descending: bool = False, k: int = -1):
     """Sorted scores + the candidate permutation (the reference drops the latter,

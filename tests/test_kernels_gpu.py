@@ -179,6 +179,34 @@ def test_head(cuda):
     _close(y, ops.head(x, w, 0.3, e, True), 1e-5, 1e-5, "head")
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 512), (37, 256, 512), (4096, 256, 512), (8192, 256, 512),
+                                   (5000, 256, 1024), (300, 128, 256), (77, 64, 128), (129, 40, 64)])
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_linear_head_fused(cuda, M, N, K, act):
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    hw = torch.randn(N, generator=g) * 0.05
+    e = torch.randn(M, generator=g)
+    for extra, sig in ((e, True), (None, False)):
+        y = ops.linear_head(x.to(cuda), W.to(cuda), b.to(cuda), act, hw.to(cuda), 0.2,
+                            None if extra is None else extra.to(cuda), sig)
+        ref = ops.linear_head(x, W, b, act, hw, 0.2, extra, sig)
+        _close(y, ref, 1e-4, 1e-3, f"linear_head {M}x{N}x{K} {act}")
+
+
+def test_linear_head_into_pinned_host(cuda):
+    M, N, K = 2048, 256, 512
+    x = torch.randn(M, K).to(torch.bfloat16)
+    W = (torch.randn(N, K) / K ** 0.5).to(torch.bfloat16)
+    b, hw = torch.randn(N) * 0.1, torch.randn(N) * 0.05
+    out = torch.zeros(M, dtype=torch.float32).pin_memory()
+    ops.linear_head(x.to(cuda), W.to(cuda), b.to(cuda), "relu", hw.to(cuda), 0.0, None, True, out=out)
+    torch.cuda.synchronize()
+    _close(out, ops.linear_head(x, W, b, "relu", hw, 0.0, None, True), 1e-4, 1e-3, "linear_head pinned")
+
+
 @pytest.mark.parametrize("n", [1, 7, 1500, 4096, 8192])
 @pytest.mark.parametrize("desc", [False, True])
 def test_sort(cuda, n, desc):
