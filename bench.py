@@ -8,17 +8,25 @@ out over N GPUs with RCCL all-to-all over xGMI (config 3 at N=4).
 
 One timed step, on every rank, is a full serving round:
 
-  1. decode ``R`` serialized PredictRequests (512 candidates each; synthetic
-     Zipf feature ids, uniform weights; TF ``tensor_content`` encoding) with the
-     native codec straight into a pinned packed-row buffer (worker threads);
-  2. H2D -> RCCL all-to-all of candidate rows over all GPUs -> DeepFM forward
-     (gfx950 kernels, one HIP graph) -> all-to-all of scores back -> D2H;
+  1. ingest ``R`` serialized PredictRequests (512 candidates each; synthetic
+     Zipf feature ids, uniform weights; TF ``tensor_content`` encoding). With
+     ``--ingest arena`` (default) the native host code parses every request's
+     protobuf framing in its pinned receive arena and writes descriptors; one
+     SDMA copy moves the arena and a GPU kernel unpacks the candidate rows.
+     With ``--ingest packed`` the host thread pool decodes rows itself;
+  2. RCCL all-to-all of candidate rows over all GPUs -> model forward (gfx950
+     kernels, one HIP graph) -> all-to-all of scores back -> D2H;
   3. encode R PredictResponses (``prediction_node`` float_val).
 
-Decode of step k+1 and encode of step k-1 overlap step k's GPU work (two
-pipeline slots); nothing is cached across steps (every step decodes and scores
-new request bytes from a rotating pool of distinct requests). Per-GPU work is
-fixed as N grows (weak scaling): global batch = N * R * 512 candidates/step.
+Four pipeline slots, three steps in flight: ingest of step k+3, the H2D of
+k+1..k+2, the forward of k and the encode of k-1 overlap. Nothing is cached
+across steps: every step re-parses and scores request bytes from a rotating
+pool of distinct requests. Per-GPU work is fixed as N grows (weak scaling):
+global batch = N * R * 512 candidates/step.
+
+``--model`` picks the BASELINE config's preset: deepfm (configs 2/3), dlrm
+(config 4: 100M-row tables sharded over the ranks), dcn_v2 (config 5: fp8
+towers).
 
 Launch: ``python bench.py`` (1 GPU) or, for N GPUs,
 ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
@@ -42,8 +50,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
-from distributed_tf_serving_amd.config import ModelConfig  # noqa: E402
-from distributed_tf_serving_amd.models import build_model  # noqa: E402
+from distributed_tf_serving_amd.config import ModelConfig, load_preset  # noqa: E402
+from distributed_tf_serving_amd.parallel.embedding_sharding import (MI355X_HBM_BYTES,  # noqa: E402
+                                                                    build_parallel_model)
 from distributed_tf_serving_amd.ops import native  # noqa: E402
 from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown  # noqa: E402
 from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E402
@@ -54,6 +63,18 @@ from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E4
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
 
 BASELINE_VALUE = None  # the reference publishes no numbers
+# --model -> configs/<preset>.yaml (BASELINE configs 2/3, 4, 5)
+PRESETS = {"deepfm": "deepfm_1gpu", "dlrm": "dlrm_sharded8", "dcn_v2": "dcn_v2_fp8"}
+
+
+def describe_model(cfg: ModelConfig) -> str:
+    mlp = "-".join(str(d) for d in cfg.mlp_dims)
+    if cfg.family == "dlrm":
+        return (f"dlrm ({cfg.num_sparse} tables x {cfg.table_rows:,} rows x {cfg.embed_dim}, {cfg.num_dense} dense, "
+                f"bottom {'-'.join(str(d) for d in cfg.bottom_mlp)}, top {mlp})")
+    rows = f"{cfg.vocab_size // 1_000_000}M" if cfg.vocab_size % 1_000_000 == 0 else str(cfg.vocab_size)
+    extra = f", {cfg.num_cross_layers} cross layers" if cfg.family in ("dcn", "dcn_v2") else ""
+    return f"{cfg.family} ({rows}x{cfg.embed_dim} emb, {cfg.num_fields} fields, MLP {mlp}{extra})"
 
 
 def parse_args():
@@ -71,7 +92,9 @@ def parse_args():
                     help="arena: host parses framing, GPU unpacks raw request bytes; packed: host decodes rows")
     ap.add_argument("--decode-threads", type=int, default=8)
     ap.add_argument("--pool", type=int, default=8, help="distinct pre-serialized steps per rank")
-    ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--gemm-dtype", default=None, choices=["bf16", "fp8"],
+                    help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
+    ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
     ap.add_argument("--diag-skip-host", action="store_true",
@@ -89,10 +112,24 @@ def main():
     dev = ctx.device
     torch.manual_seed(1234)
 
-    cfg = ModelConfig(family=a.model, gemm_dtype=a.gemm_dtype)
+    preset = PRESETS.get(a.model)
+    cfg = load_preset(preset).model if preset else ModelConfig(family=a.model)
+    if a.gemm_dtype:
+        cfg.gemm_dtype = a.gemm_dtype
     if a.model == "dlrm":
-        cfg.table_rows = 1_000_000
-    model = build_model(cfg, dev)
+        # config 4: 100M-row tables sharded over the ranks; a job too small to
+        # hold them (e.g. 1 GPU: 384 GB > 288 GB) gets the largest row count
+        # that fits its HBM budget, and reports it
+        T, D = cfg.num_sparse, cfg.embed_dim
+        rows = a.table_rows or cfg.table_rows
+        fit = int(0.8 * MI355X_HBM_BYTES * world // (T * D * 2)) // 1_000_000 * 1_000_000
+        if rows > fit:
+            if rank == 0:
+                print(f"note: {T} x {rows:,} rows do not fit {world} GPU(s); using {fit:,} rows/table",
+                      file=sys.stderr)
+            rows = fit
+        cfg.table_rows = rows
+    model = build_parallel_model(cfg, dev, ctx)
     F = cfg.num_fields
     layout = PackedLayout(F)
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
@@ -206,15 +243,17 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
-            "dtype": "bf16" if a.gemm_dtype == "bf16" else "fp8",
+            "dtype": cfg.gemm_dtype,
             "data": "synthetic (zipf feature ids over 2^40, uniform weights; random-init weights)",
             "config": {
-                "model": f"{a.model} (1Mx64 emb, 43 fields, MLP 1024-512-256)" if a.model == "deepfm" else a.model,
+                "model": describe_model(cfg),
                 "global_batch": world * B,
                 "request_rows": a.request_rows,
                 "requests_per_gpu_per_step": a.requests_per_gpu,
                 "seq_len": None,
-                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL)",
+                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL)" + (
+                    f" + embedding-mp{world} ({len(model.plan.row_wise())} row-wise tables, all-to-all)"
+                    if hasattr(model, "plan") else ""),
                 "encoding": a.encoding,
             },
             "p50_request_ms": None if p50 is None else round(p50, 3),

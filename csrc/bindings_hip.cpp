@@ -57,7 +57,8 @@ torch::Tensor pack_ids(torch::Tensor ids, int64_t modulo, c10::optional<torch::T
 std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor ids,
                                  c10::optional<torch::Tensor> wts, int64_t modulo, c10::optional<torch::Tensor> modulo_f,
                                  c10::optional<torch::Tensor> offset_f, double bias, bool want_x, bool want_fm,
-                                 bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables) {
+                                 bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables,
+                                 c10::optional<torch::Tensor> shard_lo_f, c10::optional<torch::Tensor> shard_n_f) {
   check_dev(table, "table");
   TORCH_CHECK(ids.is_cuda(), "ids must be a GPU tensor");
   TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
@@ -79,14 +80,25 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
     // every (offset + row) must stay inside the table. The kernel also clamps
     // rows into [0, V), so this (syncing) host check is a debugging aid that
     // models run once at construction, not per batch.
+    if (shard_lo_f.has_value() || shard_n_f.has_value()) {
+      TORCH_CHECK(shard_lo_f.has_value() && shard_n_f.has_value(), "shard_lo_f and shard_n_f go together");
+      for (auto* o : {&shard_lo_f, &shard_n_f}) {
+        check_dev(**o, "shard range");
+        TORCH_CHECK((*o)->scalar_type() == torch::kInt64 && (*o)->numel() == F, "shard ranges must be int64 [F]");
+      }
+    }
     auto mf = validate_tables ? modulo_f->cpu() : torch::Tensor();
     auto of = validate_tables ? offset_f->cpu() : torch::Tensor();
+    auto sn = validate_tables && shard_n_f ? shard_n_f->cpu() : torch::Tensor();
     for (int64_t f = 0; validate_tables && f < F; ++f) {
       TORCH_CHECK(mf.data_ptr<int64_t>()[f] > 0, "per-field modulo must be > 0");
-      TORCH_CHECK(of.data_ptr<int64_t>()[f] >= 0 && of.data_ptr<int64_t>()[f] + mf.data_ptr<int64_t>()[f] <= V,
+      // a row-wise shard holds n_f rows at offset_f; a whole table holds modulo_f rows
+      const int64_t held = sn.defined() ? sn.data_ptr<int64_t>()[f] : mf.data_ptr<int64_t>()[f];
+      TORCH_CHECK(of.data_ptr<int64_t>()[f] >= 0 && held >= 0 && of.data_ptr<int64_t>()[f] + held <= V,
                   "field ", f, " rows exceed the table");
     }
   } else {
+    TORCH_CHECK(!shard_lo_f.has_value() && !shard_n_f.has_value(), "row shards need per-field tables");
     TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]: ids are hashed onto rows");
   }
   if (wts) {
@@ -126,6 +138,8 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
   a.modulo = modulo;
   a.modulo_f = modulo_f ? modulo_f->data_ptr<int64_t>() : nullptr;
   a.offset_f = offset_f ? offset_f->data_ptr<int64_t>() : nullptr;
+  a.shard_lo_f = shard_lo_f ? shard_lo_f->data_ptr<int64_t>() : nullptr;
+  a.shard_n_f = shard_n_f ? shard_n_f->data_ptr<int64_t>() : nullptr;
   a.bias = float(bias);
   a.out_x = want_x ? x.data_ptr() : nullptr;
   a.x_ld = F * D;
@@ -397,7 +411,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("embed", &embed, py::arg("table"), py::arg("lin"), py::arg("ids"), py::arg("wts"), py::arg("modulo"),
         py::arg("modulo_f") = py::none(), py::arg("offset_f") = py::none(), py::arg("bias") = 0.0,
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
-        py::arg("validate_tables") = false);
+        py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none());
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
         py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
         py::arg("out_bf16") = false);

@@ -61,9 +61,16 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
     if (fl < F) {
       const int64_t id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
       const int64_t m = a.modulo_f ? a.modulo_f[fl] : a.modulo;
-      row = (a.offset_f ? a.offset_f[fl] : 0) + hash_row(id, m);
+      int64_t g = hash_row(id, m);
+      bool own = true;
+      if (a.shard_lo_f) {
+        g -= a.shard_lo_f[fl];
+        own = g >= 0 && g < a.shard_n_f[fl];
+        g = own ? g : 0;
+      }
+      row = (a.offset_f ? a.offset_f[fl] : 0) + g;
       row = row < 0 ? 0 : (row >= a.V ? a.V - 1 : row);  // memory safety whatever the tables say
-      w = a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f;
+      w = own ? (a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f) : 0.f;
       if (a.lin) first += a.lin[row] * w;
     }
     const int nf = min(kWave, F - fbase);

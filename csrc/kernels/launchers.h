@@ -26,6 +26,11 @@ struct EmbedArgs {
   int64_t modulo = 0;              // shared-table hashing
   const int64_t* modulo_f = nullptr;  // per-field tables: row = offset_f[f] + id mod modulo_f[f]
   const int64_t* offset_f = nullptr;
+  // row-wise sharded tables: this process holds global rows [lo_f, lo_f + n_f)
+  // of field f's table at offset_f[f]; ids hashing outside contribute zeros
+  // (the partial embeddings are summed across ranks by a reduce-scatter)
+  const int64_t* shard_lo_f = nullptr;
+  const int64_t* shard_n_f = nullptr;
   float bias = 0.f;
   void* out_x = nullptr;           // bf16 [B, x_ld]
   int64_t x_ld = 0;

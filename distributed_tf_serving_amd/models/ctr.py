@@ -33,7 +33,7 @@ from torch import nn
 
 from .. import ops
 from ..config import ModelConfig
-from .layers import DTYPES, MLP, Dense, init_uniform_, make_generator, pad8
+from .layers import DTYPES, MLP, Dense, hashed_uniform_rows_, init_uniform_, make_generator, pad8
 
 
 class CTRModel(nn.Module):
@@ -222,7 +222,16 @@ class DLRM(CTRModel):
                              persistent=False)
         self.register_buffer("offset_f", torch.arange(T, dtype=torch.int64, device=self.device_) * rows,
                              persistent=False)
-        self.emb = self._embedding_table(T * rows, D) if materialize_tables else None
+        self.emb = None
+        if materialize_tables:
+            t = torch.empty(T * rows, D, dtype=self.dtype, device=self.device_)
+            for f in range(T):  # per-table hashed init: shards built elsewhere match these rows exactly
+                hashed_uniform_rows_(t[f * rows:(f + 1) * rows], f, 0, cfg.seed, self.table_bound)
+            self.emb = nn.Parameter(t, requires_grad=False)
+
+    @property
+    def table_bound(self) -> float:
+        return 1.0 / math.sqrt(self.cfg.embed_dim)
 
     def dense_input(self, wts: torch.Tensor) -> torch.Tensor:
         nd = self.cfg.num_dense

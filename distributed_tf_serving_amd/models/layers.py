@@ -42,6 +42,43 @@ def init_uniform_(t: torch.Tensor, bound: float, gen: torch.Generator) -> torch.
     return t
 
 
+_M64 = (1 << 64) - 1
+
+
+def _s64(c: int) -> int:
+    """uint64 constant -> the int64 with the same bits (torch has no uint64 math)."""
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _lsr(z: torch.Tensor, s: int) -> torch.Tensor:
+    """Logical right shift of int64 bits."""
+    return torch.bitwise_and(torch.bitwise_right_shift(z, s), (1 << (64 - s)) - 1)
+
+
+def hashed_uniform_rows_(out: torch.Tensor, table_id: int, row_lo: int, seed: int, bound: float,
+                         chunk_rows: int = 1 << 19) -> torch.Tensor:
+    """Fill ``out`` [n, D] with U(-bound, bound) values that depend only on
+    (seed, table_id, global row, column): any row shard of a table can be
+    initialised on its own rank, and a sharded model matches the unsharded one
+    bit for bit (splitmix64 of the element index; identical on CPU and GPU)."""
+    n, D = out.shape
+    dev = out.device
+    cols = torch.arange(D, device=dev, dtype=torch.int64)
+    salt = _s64((seed * 0x9E3779B97F4A7C15 + table_id * 0xD1B54A32D192ED03) & _M64)
+    with torch.no_grad():
+        for r0 in range(0, n, chunk_rows):
+            r1 = min(n, r0 + chunk_rows)
+            rows = torch.arange(row_lo + r0, row_lo + r1, device=dev, dtype=torch.int64)
+            z = rows[:, None] * D + cols[None, :] + salt
+            z = z + _s64(0x9E3779B97F4A7C15)
+            z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+            z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+            z = torch.bitwise_xor(z, _lsr(z, 31))
+            u = _lsr(z, 40).to(torch.float32) * (1.0 / (1 << 24))  # top 24 bits -> [0, 1)
+            out[r0:r1].copy_((u * 2.0 - 1.0) * bound)
+    return out
+
+
 class Dense(nn.Module):
     """One fully connected layer: y = act(x W^T + b) (K4 MFMA GEMM)."""
 

@@ -55,19 +55,31 @@ def pack_ids(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None) -
 def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = None,
           lin: Optional[torch.Tensor] = None, modulo: int = 0, modulo_f=None, offset_f=None,
           bias: float = 0.0, want_x: bool = True, want_fm: bool = False, fm2: bool = False,
-          out_x: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+          out_x: Optional[torch.Tensor] = None, shard_lo_f: Optional[torch.Tensor] = None,
+          shard_n_f: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """Weighted embedding gather with fused factorisation-machine terms.
 
     x[b, f*D:(f+1)*D] = table[row(b, f)] * wts[b, f]
     fm[b] = bias + sum_f lin[row]*wts  (if lin) + 0.5*sum_d((sum_f e)^2 - sum_f e^2)  (if fm2)
+
+    ``shard_lo_f``/``shard_n_f`` (row-wise sharded tables): field f's table
+    here holds global rows [lo, lo + n) at ``offset_f[f]``; ids hashing
+    elsewhere contribute zeros.
     """
     if ids.is_cuda:
         if modulo_f is None and modulo <= 0:
             modulo = table.shape[0]
         x, fm = hip().embed(table, lin, _rows(ids), None if wts is None else _rows(wts), int(modulo),
-                            modulo_f, offset_f, float(bias), want_x, want_fm, fm2, out_x)
+                            modulo_f, offset_f, float(bias), want_x, want_fm, fm2, out_x, False, shard_lo_f, shard_n_f)
         return (x if want_x else None), (fm if want_fm else None)
-    rows = _hash_rows(ids, modulo if modulo > 0 else table.shape[0], modulo_f, offset_f)
+    if shard_lo_f is not None:
+        g = torch.remainder(ids.long(), modulo_f.view(1, -1)) - shard_lo_f.view(1, -1)
+        own = (g >= 0) & (g < shard_n_f.view(1, -1))
+        rows = offset_f.view(1, -1) + torch.where(own, g, torch.zeros_like(g))
+        w_own = own.float() if wts is None else wts.float() * own
+        wts = w_own
+    else:
+        rows = _hash_rows(ids, modulo if modulo > 0 else table.shape[0], modulo_f, offset_f)
     e = table[rows].float()  # [B, F, D]
     if wts is not None:
         e = e * wts.float().unsqueeze(-1)

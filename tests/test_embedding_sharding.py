@@ -1,0 +1,146 @@
+"""Embedding model parallelism (BASELINE config 4): planner, hashed shard init,
+and the sharded DLRM forward over gloo (world 2 and 3) against the unsharded
+model - table-wise, row-wise and mixed placements."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_tf_serving_amd.config import ModelConfig
+from distributed_tf_serving_amd.models.layers import hashed_uniform_rows_
+from distributed_tf_serving_amd.parallel.embedding_sharding import (GiB, MI355X_HBM_BYTES, Placement, ShardingPlan,
+                                                                    TableSpec, dlrm_tables, plan_sharding)
+from distributed_tf_serving_amd.parallel.dist import split_rows
+
+
+def _small_cfg():
+    return ModelConfig(family="dlrm", num_fields=20, num_dense=5, table_rows=997, embed_dim=64,
+                       bottom_mlp=(32, 64), mlp_dims=(64, 32))
+
+
+def test_plan_config4_table_wise_fits_8_ranks():
+    cfg = ModelConfig(family="dlrm", num_fields=43, num_dense=13, table_rows=100_000_000, embed_dim=64)
+    tables = dlrm_tables(cfg)
+    assert len(tables) == 30 and tables[0].bytes == 100_000_000 * 128
+    plan = plan_sharding(tables, 8)
+    load = plan.rank_bytes()
+    assert sum(load) == 30 * 12_800_000_000
+    assert max(load) <= 0.8 * MI355X_HBM_BYTES
+    assert not plan.row_wise()  # 12.8 GB tables balance table-wise (4/4/4/4/4/4/3/3)
+    assert sorted(len(plan.table_wise(r)) for r in range(8)) == [3, 3, 4, 4, 4, 4, 4, 4]
+    assert "imbalance" in plan.describe()
+
+
+def test_plan_single_gpu_overflows():
+    cfg = ModelConfig(family="dlrm", num_fields=43, num_dense=13, table_rows=100_000_000, embed_dim=64)
+    with pytest.raises(MemoryError, match="budget"):
+        plan_sharding(dlrm_tables(cfg), 1)  # 384 GB of tables > one MI355X
+
+
+def test_plan_auto_row_wise_for_huge_table():
+    tables = [TableSpec("big", 2_000_000_000, 64)] + [TableSpec(f"s{i}", 1_000_000, 64) for i in range(6)]
+    plan = plan_sharding(tables, 4)
+    assert plan.row_wise() == [0]
+    p = plan.placement(0)
+    assert sum(n for _, n in p.ranges) == 2_000_000_000 and p.ranges == split_rows(2_000_000_000, 4)
+    assert all(plan.placement(i).kind == "table" for i in range(1, 7))
+    load = plan.rank_bytes()
+    assert max(load) / (sum(load) / 4) < 1.05
+
+
+def test_plan_policies():
+    tables = [TableSpec(f"t{i}", 1000 * (i + 1), 64) for i in range(5)]
+    assert len(plan_sharding(tables, 3, policy="row").row_wise()) == 5
+    assert plan_sharding(tables, 3, policy="table").row_wise() == []
+    with pytest.raises(ValueError):
+        plan_sharding(tables, 3, policy="bogus")
+
+
+def test_hashed_init_shards_match_full():
+    full = torch.empty(1000, 64)
+    hashed_uniform_rows_(full, 3, 0, 42, 0.125, chunk_rows=128)
+    part = torch.empty(300, 64)
+    hashed_uniform_rows_(part, 3, 500, 42, 0.125)
+    assert torch.equal(full[500:800], part)
+    assert full.abs().max() <= 0.125 and full.std() > 0.05
+    other = torch.empty(1000, 64)
+    hashed_uniform_rows_(other, 4, 0, 42, 0.125)
+    assert not torch.equal(full, other)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mixed_plan(cfg, world):
+    plan = plan_sharding(dlrm_tables(cfg), world, policy="table")
+    # make every third table row-wise
+    pl = []
+    for p in plan.placements:
+        if p.table % 3 == 0:
+            pl.append(Placement(p.table, "row", ranges=split_rows(cfg.table_rows, world)))
+        else:
+            pl.append(p)
+    return ShardingPlan(plan.tables, world, pl, plan.budget_bytes)
+
+
+def _worker(rank, world, port, policy, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown
+    from distributed_tf_serving_amd.parallel.embedding_sharding import ShardedDLRM
+
+    try:
+        ctx = init_from_env(device="cpu")
+        cfg = _small_cfg()
+        plan = _mixed_plan(cfg, world) if policy == "mixed" else None
+        m = ShardedDLRM(cfg, ctx, plan=plan, policy=policy if policy != "mixed" else "auto")
+        ref = build_model(cfg)
+        g = torch.Generator().manual_seed(7 + rank)
+        ids = torch.randint(0, 10**12, (B, cfg.num_fields), generator=g)
+        wts = torch.rand(B, cfg.num_fields, generator=g)
+        out = m(ids, wts)
+        want = ref(ids, wts)
+        err = (out - want).abs().max().item()
+        q.put((rank, err, m.emb.local_bytes(), len(m.plan.row_wise())))
+        shutdown()
+    except Exception as e:  # pragma: no cover - surfaced by the assertion below
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world,policy", [(2, "table"), (3, "table"), (2, "row"), (3, "mixed")])
+def test_sharded_dlrm_matches_unsharded(world, policy):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    B = 6
+    procs = [ctx.Process(target=_worker, args=(r, world, port, policy, B, q)) for r in range(world)]
+    [p.start() for p in procs]
+    res = {}
+    for _ in range(world):
+        r, err, nbytes, nrw = q.get(timeout=240)
+        res[r] = (err, nbytes, nrw)
+    [p.join(timeout=60) for p in procs]
+    cfg = _small_cfg()
+    full_bytes = cfg.num_sparse * cfg.table_rows * 64 * 2
+    for r in range(world):
+        err, nbytes, nrw = res[r]
+        assert isinstance(err, float), f"rank {r} failed: {err}"
+        assert err < 1e-5, f"rank {r}: sharded scores differ by {err}"
+        assert nbytes < full_bytes  # each rank holds only its shards
+        if policy == "row":
+            assert nrw == cfg.num_sparse
+        if policy == "mixed":
+            assert 0 < nrw < cfg.num_sparse
+    assert sum(res[r][1] for r in range(world)) == pytest.approx(full_bytes, rel=0.01)

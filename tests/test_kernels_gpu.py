@@ -66,6 +66,38 @@ def test_embed_per_field_tables(cuda):
     _close(x, xr, 0, 0, "per-field")
 
 
+def test_embed_row_shards(cuda):
+    # row-wise sharded tables: rows outside [lo, lo+n) must contribute zeros
+    T, rows, D, B = 6, 1000, 64, 33
+    lo = torch.tensor([0, 250, 500, 750, 100, 999], dtype=torch.int64)
+    n = torch.tensor([250, 250, 250, 250, 0, 1], dtype=torch.int64)
+    of = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), n[:-1]]), 0)
+    table = (torch.rand(int(n.sum()) + 1, D) - 0.5).to(torch.bfloat16)
+    mf = torch.full((T,), rows, dtype=torch.int64)
+    ids = torch.randint(0, 10**7, (B, T))
+    wts = torch.rand(B, T)
+    args = dict(modulo_f=mf, offset_f=of, shard_lo_f=lo, shard_n_f=n)
+    x, _ = ops.embed(table.to(cuda), ids.to(cuda), wts.to(cuda), **{k: v.to(cuda) for k, v in args.items()})
+    xr, _ = ops.embed(table, ids, wts, **args)
+    _close(x, xr, 0, 0, "row shards")
+    assert (xr.view(B, T, D)[:, 4] == 0).all()  # empty shard
+    own = (torch.remainder(ids, rows) - lo >= 0) & (torch.remainder(ids, rows) - lo < n)
+    assert ((xr.view(B, T, D).abs().sum(-1) > 0) <= own).all()
+
+
+def test_sharded_dlrm_single_rank_gpu(cuda):
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.parallel.dist import DistContext
+    from distributed_tf_serving_amd.parallel.embedding_sharding import ShardedDLRM
+
+    cfg = ModelConfig(family="dlrm", table_rows=5000, mlp_dims=(256, 128))
+    ref = build_model(cfg, cuda)
+    m = ShardedDLRM(cfg, DistContext(device=cuda), device=cuda)
+    ids = torch.randint(0, 1 << 40, (300, 43), device=cuda)
+    wts = torch.rand(300, 43, device=cuda)
+    _close(m(ids, wts), ref(ids, wts), 0, 1e-6, "sharded dlrm (1 rank)")
+
+
 @pytest.mark.parametrize("mean", [False, True])
 def test_embedding_bag(cuda, mean):
     R, D, nb = 3000, 64, 41
