@@ -96,6 +96,10 @@ def parse_args():
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--force-fanout", action="store_true",
+                    help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
+    ap.add_argument("--no-native-fanout", action="store_true",
+                    help="N>1: issue collectives through torch.distributed instead of the C++ StepRunner")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
     ap.add_argument("--diag-skip-host", action="store_true",
                     help="DIAGNOSTIC ONLY (not a valid measurement): reuse decoded buffers to isolate GPU time")
@@ -137,8 +141,13 @@ def main():
     ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
     rows_in_max = B * (ctx.world if a.mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
-    eng = FanoutEngine(ex, ctx, mode=a.mode, ingest=a.ingest, arena=arena_layout)
+    eng = FanoutEngine(ex, ctx, mode=a.mode, ingest=a.ingest, arena=arena_layout, force_fanout=a.force_fanout,
+                       native_fanout=not a.no_native_fanout)
     eng.prepare(B)
+    if eng.mode != "local":
+        # one synthetic step checked against a local forward on every rank; a
+        # failure anywhere switches every rank to the torch.distributed path
+        eng.self_check(B, seed=rank)
     nat = native()
 
     rows_in = eng.contrib_rows(B)
@@ -251,7 +260,8 @@ def main():
                 "request_rows": a.request_rows,
                 "requests_per_gpu_per_step": a.requests_per_gpu,
                 "seq_len": None,
-                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL)" + (
+                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
+                               + (", native C++ step" if eng.native_fanout_active else "") + ")" + (
                     f" + embedding-mp{world} ({len(model.plan.row_wise())} row-wise tables, all-to-all)"
                     if hasattr(model, "plan") else ""),
                 "encoding": a.encoding,

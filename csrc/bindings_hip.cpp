@@ -11,6 +11,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/launchers.h"
+#include "comm/rccl_comm.h"
 #include "runtime/step_runner.h"
 
 namespace {
@@ -447,9 +448,105 @@ PYBIND11_MODULE(_hip, m) {
             r.launch(slot, dst.data_ptr(), src.data_ptr(), nbytes, reinterpret_cast<hipGraphExec_t>(graph_exec));
           },
           py::arg("slot"), py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("graph_exec"))
+      .def(
+          "launch_fanout",
+          [](dtfs::runtime::StepRunner& r, int slot, torch::Tensor h2d_dst, torch::Tensor h2d_src, int64_t h2d_bytes,
+             uintptr_t ingress_exec, dtfs::comm::RcclComm& cin, int mode, torch::Tensor send, torch::Tensor recv,
+             uintptr_t forward_exec, dtfs::comm::RcclComm& cout, torch::Tensor scores, torch::Tensor back,
+             torch::Tensor h_out, int64_t d2h_bytes) {
+            TORCH_CHECK(mode == 0 || mode == 1, "mode: 0 all-to-all, 1 scatter/gather");
+            TORCH_CHECK(cin.nranks() == cout.nranks() && cin.rank() == cout.rank(), "communicator mismatch");
+            const int W = cin.nranks();
+            for (auto* t : {&h2d_dst, &send, &recv, &scores, &back})
+              TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "fan-out buffers must be contiguous GPU tensors");
+            TORCH_CHECK(h2d_src.device().is_cpu() && h2d_src.is_pinned() && h_out.is_pinned(),
+                        "host buffers must be pinned");
+            TORCH_CHECK(h2d_bytes >= 0 && h2d_bytes <= int64_t(h2d_dst.nbytes()) &&
+                            h2d_bytes <= int64_t(h2d_src.nbytes()),
+                        "h2d_bytes out of range");
+            // all-to-all: send/recv (and scores/back) are this rank's B rows,
+            // B/W to / from each peer. scatter/gather: recv/scores are this
+            // rank's B rows; the root's send/back hold W x B.
+            size_t in_bytes, out_bytes;
+            if (mode == 0) {
+              TORCH_CHECK(send.nbytes() == recv.nbytes() && recv.nbytes() % W == 0,
+                          "all-to-all: send and recv must match and split evenly over the ranks");
+              TORCH_CHECK(back.nbytes() == scores.nbytes() && scores.nbytes() % W == 0,
+                          "all-to-all: scores and back must match and split evenly over the ranks");
+              in_bytes = recv.nbytes() / W;
+              out_bytes = scores.nbytes() / W;
+            } else {
+              in_bytes = recv.nbytes();
+              out_bytes = scores.nbytes();
+              if (cin.rank() == 0) {
+                TORCH_CHECK(send.nbytes() >= in_bytes * W, "scatter: root send smaller than world x recv");
+                TORCH_CHECK(back.nbytes() >= out_bytes * W, "gather: root back smaller than world x scores");
+              }
+            }
+            TORCH_CHECK(d2h_bytes >= 0 && size_t(d2h_bytes) <= back.nbytes() && size_t(d2h_bytes) <= h_out.nbytes(),
+                        "d2h_bytes out of range");
+            TORCH_CHECK(forward_exec != 0, "null forward graph");
+            dtfs::runtime::FanoutStep s;
+            s.h2d_dst = h2d_dst.data_ptr();
+            s.h2d_src = h2d_src.data_ptr();
+            s.h2d_bytes = h2d_bytes;
+            s.ingress = reinterpret_cast<hipGraphExec_t>(ingress_exec);
+            s.cin = &cin;
+            s.mode = mode;
+            s.send = send.data_ptr();
+            s.recv = recv.data_ptr();
+            s.in_bytes = in_bytes;
+            s.forward = reinterpret_cast<hipGraphExec_t>(forward_exec);
+            s.cout = &cout;
+            s.scores = scores.data_ptr();
+            s.back = back.data_ptr();
+            s.out_bytes = out_bytes;
+            s.h_out = h_out.data_ptr();
+            s.d2h_bytes = size_t(d2h_bytes);
+            r.launch_fanout(slot, s);
+          },
+          py::arg("slot"), py::arg("h2d_dst"), py::arg("h2d_src"), py::arg("h2d_bytes"), py::arg("ingress_exec"),
+          py::arg("cin"), py::arg("mode"), py::arg("send"), py::arg("recv"), py::arg("forward_exec"), py::arg("cout"),
+          py::arg("scores"), py::arg("back"), py::arg("h_out"), py::arg("d2h_bytes"))
       .def("wait", &dtfs::runtime::StepRunner::wait, py::arg("slot"), py::call_guard<py::gil_scoped_release>())
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
+
+  m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
+  m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });
+  py::class_<dtfs::comm::RcclComm>(m, "RcclComm", "Native RCCL communicator (fan-out collectives over xGMI)")
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
+             std::string id(uid);  // convert while holding the GIL
+             py::gil_scoped_release nogil;  // ncclCommInitRank blocks until every rank joins
+             return std::make_unique<dtfs::comm::RcclComm>(id, nranks, rank, device);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def_property_readonly("rank", &dtfs::comm::RcclComm::rank)
+      .def_property_readonly("nranks", &dtfs::comm::RcclComm::nranks)
+      .def(
+          "alltoall",
+          [](dtfs::comm::RcclComm& c, torch::Tensor send, torch::Tensor recv) {
+            TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+                        "contiguous GPU tensors");
+            TORCH_CHECK(send.nbytes() == recv.nbytes() && send.nbytes() % c.nranks() == 0,
+                        "send/recv must be equal and divisible by the world size");
+            c10::DeviceGuard g(send.device());
+            c.alltoall(send.data_ptr(), recv.data_ptr(), send.nbytes() / c.nranks(), cur_stream(send));
+          },
+          py::arg("send"), py::arg("recv"))
+      .def(
+          "allgather",
+          [](dtfs::comm::RcclComm& c, torch::Tensor send, torch::Tensor recv) {
+            TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+                        "contiguous GPU tensors");
+            TORCH_CHECK(recv.nbytes() == send.nbytes() * c.nranks(), "recv must be world x send");
+            c10::DeviceGuard g(send.device());
+            c.allgather(send.data_ptr(), recv.data_ptr(), send.nbytes(), cur_stream(send));
+          },
+          py::arg("send"), py::arg("recv"))
+      .def("async_error", &dtfs::comm::RcclComm::async_error)
+      .def("abort", &dtfs::comm::RcclComm::abort)
+      .def_property_readonly("aborted", &dtfs::comm::RcclComm::aborted);
 }

@@ -1,0 +1,63 @@
+// Native RCCL communicator for the candidate fan-out (SURVEY.md §2.3
+// "csrc/comm/rccl_fanout.cpp", collectives C1/C2).
+//
+// The reference fans candidates out over per-host gRPC channels (reference
+// DCNClient.java:118-135 channels, :146-164 dispatch/join). Inside one MI355X
+// node the hop is xGMI, and the collectives are issued from C++ straight onto
+// HIP streams by the StepRunner, so a fan-out step costs no Python and no
+// ProcessGroup bookkeeping per step. Bootstrap reuses torch.distributed only
+// to broadcast the 128-byte ncclUniqueId.
+//
+// Every message of a step has a static size (equal per-rank splits), so the
+// ops are plain ncclAllToAll / grouped send-recv with no count exchange.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+
+namespace dtfs {
+namespace comm {
+
+// Path of the librccl to use (PyTorch's bundled copy); must be set before the
+// first RCCL call. Symbols are resolved with dlopen/dlsym, nothing is linked.
+void set_library(const std::string& path);
+std::string unique_id();  // ncclGetUniqueId, as raw bytes
+
+class RcclComm {
+ public:
+  RcclComm(const std::string& uid, int nranks, int rank, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int rank() const { return rank_; }
+  int nranks() const { return nranks_; }
+
+  // recv[r] = rank r's send[me]; `bytes` per peer.
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t st);
+  // root's send[r] -> rank r's recv (bytes each). send is only read on root.
+  void scatter(const void* send, void* recv, size_t bytes, int root, hipStream_t st);
+  // every rank's send -> root's recv[r] (bytes each).
+  void gather(const void* send, void* recv, size_t bytes, int root, hipStream_t st);
+  // recv[r] = rank r's send.
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st);
+
+  // "" when healthy, else the asynchronous RCCL error (failure detection).
+  std::string async_error();
+  // Abort in-flight operations (a peer died / a deadline passed); the
+  // communicator is unusable afterwards.
+  void abort();
+  bool aborted() const { return aborted_; }
+
+ private:
+  void check(ncclResult_t r, const char* what);
+  ncclComm_t comm_ = nullptr;
+  int nranks_ = 1, rank_ = 0, device_ = 0;
+  bool aborted_ = false;
+};
+
+}  // namespace comm
+}  // namespace dtfs

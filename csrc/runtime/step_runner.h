@@ -15,8 +15,37 @@
 #include <cstdint>
 #include <vector>
 
+#include "../comm/rccl_comm.h"
+
 namespace dtfs {
 namespace runtime {
+
+// One fan-out step (world > 1), all pointers device unless noted:
+//   copy stream : H2D h2d_src (pinned host) -> h2d_dst
+//   ingress     : [ingress graph, e.g. GPU unpack of the request arena]
+//                 -> collective-in (all-to-all / scatter of packed rows)
+//   compute     : forward graph (recv rows -> scores)
+//   egress      : collective-out (all-to-all / gather of scores) -> D2H
+// Ingress and egress have their own streams and communicators, so step k+1's
+// row exchange and step k-1's score exchange overlap step k's forward.
+struct FanoutStep {
+  void* h2d_dst = nullptr;
+  const void* h2d_src = nullptr;
+  int64_t h2d_bytes = 0;
+  hipGraphExec_t ingress = nullptr;
+  comm::RcclComm* cin = nullptr;
+  int mode = 0;  // 0 = all-to-all, 1 = scatter from / gather to rank 0
+  const void* send = nullptr;
+  void* recv = nullptr;
+  size_t in_bytes = 0;   // per peer
+  hipGraphExec_t forward = nullptr;
+  comm::RcclComm* cout = nullptr;
+  const void* scores = nullptr;
+  void* back = nullptr;
+  size_t out_bytes = 0;  // per peer
+  void* h_out = nullptr;  // pinned host
+  size_t d2h_bytes = 0;
+};
 
 class StepRunner {
  public:
@@ -29,6 +58,8 @@ class StepRunner {
   // launch graph_exec on the compute stream once the copy has landed. The H2D
   // waits only for the previous step of the same slot to have consumed dst.
   void launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph);
+  // Enqueue one fan-out step (see FanoutStep).
+  void launch_fanout(int slot, const FanoutStep& s);
   // Block until the slot's last step has finished (scores are on the host).
   void wait(int slot);
   bool query(int slot);
@@ -39,8 +70,9 @@ class StepRunner {
 
  private:
   int device_;
-  hipStream_t copy_ = nullptr, compute_ = nullptr;
-  std::vector<hipEvent_t> h2d_done_, done_;
+  void ensure_fanout_streams();
+  hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
+  std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
   std::vector<bool> used_;
 };
 

@@ -38,7 +38,7 @@ NATIVE_SOURCES = [
     "runtime/batcher.cpp",
     "runtime/thread_pool.cpp",
 ]
-HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp"]
+HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp"]
 
 
 def _torch_paths():
@@ -141,7 +141,8 @@ def build_hip(verbose=False, force=False) -> str:
     if force or jobs or not os.path.exists(out):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "--hip-link", "-o", out, *objs,
               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-              "-lamdhip64", f"-Wl,-rpath,{tlib}"], verbose)
+              # RCCL is not linked: csrc/comm resolves it from torch's loaded copy
+              "-lamdhip64", "-ldl", f"-Wl,-rpath,{tlib}"], verbose)
     return out
 
 

@@ -42,7 +42,17 @@ def hip():
                     raise RuntimeError(
                         "gfx950 kernels (_hip) are not built: run `python -m distributed_tf_serving_amd._build`"
                     ) from e
+            _hip_mod.rccl_set_library(_torch_rccl_path())
     return _hip_mod
+
+
+def _torch_rccl_path() -> str:
+    """PyTorch's bundled librccl (the one ProcessGroupNCCL uses); the system
+    copy only when torch ships none."""
+    import torch
+
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so.1"
 
 
 def native():

@@ -72,11 +72,18 @@ class StepHandle:
 
 class FanoutEngine:
     def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
-                 step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None):
+                 step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None,
+                 native_fanout: bool = True, force_fanout: bool = False):
         """``ingest="packed"``: the host decodes into packed rows (host_in) and
         the H2D moves rows. ``ingest="arena"``: the host only parses request
         framing into a request arena (serving/arena.py); the H2D moves the raw
-        request bytes and the GPU unpacks rows (csrc/kernels/ingest.hip)."""
+        request bytes and the GPU unpacks rows (csrc/kernels/ingest.hip).
+
+        ``native_fanout`` (GPU, world > 1): the whole fan-out step is enqueued
+        from C++ (StepRunner.launch_fanout) with native RCCL communicators
+        (csrc/comm) - ingress and egress exchanges on their own streams and
+        communicators, overlapping the forward graph. ``force_fanout`` keeps
+        the fan-out mode on a 1-rank job (exercises that path on one GPU)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         if ingest not in ("packed", "arena"):
@@ -91,8 +98,13 @@ class FanoutEngine:
         self.ctx = ctx
         self.world = ctx.world if ctx.is_distributed else 1
         self.rank = ctx.rank if ctx.is_distributed else 0
-        self.mode = mode if self.world > 1 else "local"
+        self.mode = mode if (self.world > 1 or force_fanout) else "local"
         self.group = group
+        self.native_fanout = native_fanout
+        self.force_fanout = force_fanout
+        self._cin = self._cout = None
+        self._ingress_graph: Dict[Tuple[int, int], object] = {}
+        self.native_fanout_active = False
         self.layout = executor.layout
         self.dev = executor.device
         self.cuda = self.dev.type == "cuda"
@@ -165,6 +177,11 @@ class FanoutEngine:
 
     def prepare(self, B: int) -> None:
         self.check_bucket(B)
+        native = self._native_fanout_enabled()
+        if self.force_fanout and self.world == 1 and self.mode != "local" and not native:
+            raise RuntimeError("force_fanout on one rank needs the native fan-out path (GPU + HIP graphs)")
+        if native:
+            self._ensure_comms()
         for s in range(self.ex.slots):
             self.host_in(B, s)
             self.host_out(B, s)
@@ -172,6 +189,146 @@ class FanoutEngine:
                 self._capture_step(B, s)
             else:
                 self.ex.prepare(B, s)
+            if native:
+                self._capture_ingress(B, s)
+        self.native_fanout_active = native
+
+    # -- native fan-out (world > 1) -----------------------------------------------
+    def _native_fanout_enabled(self) -> bool:
+        return (self.cuda and self.mode in ("alltoall", "scatter") and self.native_fanout and self.native_launch
+                and self.ex.use_graphs and not getattr(self.ex.model, "has_collectives", False))
+
+    def _ensure_comms(self) -> None:
+        if self._cin is None:
+            from .native_comm import create_comm
+
+            # two communicators: the row exchange of step k+1 and the score
+            # exchange of step k-1 run concurrently on different streams
+            self._cin = create_comm(self.ctx, self.group)
+            self._cout = create_comm(self.ctx, self.group)
+
+    def _send_buf(self, B: int, slot: int) -> torch.Tensor:
+        rows = self.contrib_rows(B)
+        return self._dev(self._dev_send, (B, slot), (max(1, rows), self.layout.words), torch.int64)
+
+    def _back_buf(self, B: int, slot: int) -> torch.Tensor:
+        n = B if self.mode == "alltoall" else (self.world * B if self.rank == 0 else 1)
+        return self._dev(self._dev_back, (B, slot), (n,), torch.float32)
+
+    def _capture_ingress(self, B: int, slot: int) -> None:
+        """Arena ingest: capture the GPU unpack (request bytes -> the slot's send
+        rows) as a small graph the StepRunner launches on the ingress stream."""
+        key = (B, slot)
+        self._send_buf(B, slot)
+        self._back_buf(B, slot)
+        rows = self.contrib_rows(B)
+        if self.ingest != "arena" or rows == 0 or key in self._ingress_graph:
+            return
+        arena_dev, send = self.dev_arena(slot), self._send_buf(B, slot)
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            self._unpack(arena_dev, send[:rows])
+        side.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            self._unpack(arena_dev, send[:rows])
+        self._ingress_graph[key] = g
+
+    def _launch_native_fanout(self, B: int, slot: int, h_in, h_out, rows: int, t0: float,
+                              nbytes: Optional[int]) -> StepHandle:
+        key = (B, slot)
+        self.ex.prepare(B, slot)
+        self._capture_ingress(B, slot)
+        if self._runner is None:
+            from ..ops import hip
+
+            self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
+        send, back = self._send_buf(B, slot), self._back_buf(B, slot)
+        if self.ingest == "arena":
+            dst = self.dev_arena(slot)
+            h2d = int(nbytes or 0) if rows else 0
+        else:
+            dst = send
+            h2d = rows * self.layout.row_bytes
+        ing = self._ingress_graph.get(key)
+        self._runner.launch_fanout(
+            slot, dst, h_in, h2d, ing.raw_cuda_graph_exec() if ing is not None else 0,
+            self._cin, 0 if self.mode == "alltoall" else 1, send, self.ex.input_buffer(B, slot),
+            self.ex._graphs[key].raw_cuda_graph_exec(), self._cout, self.ex._out[key], back, h_out, rows * 4)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot), t_submit=t0)
+
+    def self_check(self, B: int, seed: int = 0, atol: float = 1e-5, slot: int = 0) -> bool:
+        """Run one fan-out step on synthetic requests and compare every score
+        with a local forward of the same candidate rows. With the native path
+        active, a failure on ANY rank turns it off on every rank (eager
+        torch.distributed path instead). Collective; returns the agreed result."""
+        from ..client.synth import SyntheticRequests
+
+        rows = self.contrib_rows(B)
+        F = self.layout.fields
+        ok = True
+        err = ""
+        try:
+            synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=seed + 7919 * self.rank)
+            ids = wts = None
+            if rows:
+                a_ids, a_wts = synth.arrays(rows)
+                ids, wts = torch.from_numpy(a_ids), torch.from_numpy(a_wts)
+            if rows and self.ingest == "arena":
+                from ..ops import native
+
+                reqs, per = [], 512
+                for s in range(0, rows, per):
+                    n = min(per, rows - s)
+                    reqs.append(native().encode_predict_request(
+                        "DCN", "serving_default", None,
+                        [("feat_ids", ids[s:s + n].contiguous()), ("feat_wts", wts[s:s + n].contiguous())], True))
+                ar = self.host_arena(slot)
+                ab = self.arena.build(ar, self.arena.place(ar, reqs))
+                h = self.launch(B, slot, src=ar, nbytes=ab.used_bytes)
+            else:
+                buf = self.host_in(B, slot)
+                if rows:
+                    self.layout.ids(buf)[:rows].copy_(ids)
+                    self.layout.wts(buf)[:rows].copy_(wts)
+                h = self.launch(B, slot, nbytes=0 if self.ingest == "arena" else None)
+            got = h.wait().clone()
+            if rows:
+                want = self.ex.model(ids.to(self.dev), wts.to(self.dev)).float().cpu()
+                diff = (got - want).abs().max().item()
+                ok = bool(diff <= atol)
+                err = f"max |diff| {diff:.3g}"
+        except Exception as e:  # surfaced through the agreement below
+            ok, err = False, repr(e)
+        if self.ctx.is_distributed:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                device=self.dev if self.ctx.backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            all_ok = bool(flag.item())
+        else:
+            all_ok = ok
+        if not all_ok and self.native_fanout_active:
+            import sys
+
+            print(f"[fanout] rank {self.rank}: native fan-out self-check failed ({err or 'on another rank'}); "
+                  f"using the torch.distributed path", file=sys.stderr, flush=True)
+            self.native_fanout_active = False
+            if self.cuda:
+                torch.cuda.synchronize(self.dev)
+        return all_ok
+
+    def comm_error(self) -> Optional[str]:
+        """Asynchronous RCCL error of the native communicators (failure detection)."""
+        from .native_comm import check_comms
+
+        return check_comms(self._cin, self._cout)
+
+    def abort(self) -> None:
+        """Abort the native communicators (a peer is gone / a deadline passed)."""
+        for c in (self._cin, self._cout):
+            if c is not None:
+                c.abort()
 
     # -- whole-step graphs (no fan-out) ------------------------------------------
     def _step_graphs_enabled(self) -> bool:
@@ -275,6 +432,8 @@ class FanoutEngine:
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
         if self._step_graphs_enabled():
             return self._launch_step_graph(B, slot, h_in, h_out, rows, t0, nbytes)
+        if self.native_fanout_active:
+            return self._launch_native_fanout(B, slot, h_in, h_out, rows, t0, nbytes)
 
         cur = torch.cuda.current_stream(self.dev)
         ev_in_free = self._ev_in_free.get(slot)

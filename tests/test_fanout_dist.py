@@ -37,7 +37,7 @@ def _worker(rank, world, port, mode, B, q):
         L = PackedLayout(43)
         ex = ShardExecutor(m, L, [B], "cpu", slots=2)
         eng = FanoutEngine(ex, ctx, mode=mode)
-        results = []
+        results = [(eng.contrib_rows(B), eng.self_check(B))]  # collective self-check (agreed across ranks)
         for step in range(3):
             rows = eng.contrib_rows(B)
             g = torch.Generator().manual_seed(100 * step + rank)
