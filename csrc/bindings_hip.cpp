@@ -373,16 +373,20 @@ void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
 }
 
 // ---------------------------------------------------------------- fp8
-std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x) {
+std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x, int64_t k_pad) {
   check_dev(x, "x");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.dim() == 2, "x must be bf16 [M, K]");
+  TORCH_CHECK(x.stride(1) == 1, "x rows must be contiguous");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(K % 16 == 0 && K <= 4096, "K must be a multiple of 16 and <= 4096");
+  TORCH_CHECK(K % 8 == 0 && K <= 4096, "K must be a multiple of 8 and <= 4096");
+  TORCH_CHECK(k_pad >= 1 && k_pad <= 256, "k_pad must be in [1, 256]");
+  const int64_t Kq = (K + k_pad - 1) / k_pad * k_pad;
+  TORCH_CHECK(Kq % 16 == 0, "padded K must be a multiple of 16");
   c10::DeviceGuard g(x.device());
-  auto q = torch::empty({M, K}, x.options().dtype(torch::kFloat8_e4m3fn));
+  auto q = torch::empty({M, Kq}, x.options().dtype(torch::kFloat8_e4m3fn));
   auto s = torch::empty({M}, x.options().dtype(torch::kFloat32));
-  check_hip(dtfs::launch_quant_rows_fp8(x.data_ptr(), K, int(M), int(K), q.data_ptr(), K, s.data_ptr<float>(),
-                                        cur_stream(x)),
+  check_hip(dtfs::launch_quant_rows_fp8(x.data_ptr(), x.stride(0), int(M), int(K), q.data_ptr(), Kq,
+                                        s.data_ptr<float>(), cur_stream(x), int(Kq)),
             "quant_rows_fp8");
   return {q, s};
 }
@@ -427,7 +431,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
-  m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"));
+  m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);

@@ -2,9 +2,10 @@
 //
 //   C[m, n] = epilogue( sum_k A[m, k] * W[n, k] )       A: [M][K], W: [N][K]
 //
-// bf16 operands use v_mfma_f32_16x16x32_bf16; fp8 (OCP e4m3) operands use
-// v_mfma_f32_16x16x32_fp8_fp8 with a per-row activation scale and a
-// per-output-channel weight scale folded into the epilogue.
+// bf16 operands use v_mfma_f32_16x16x32_bf16; fp8 (OCP e4m3) operands use the
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales; 2x the
+// plain fp8 MFMA rate) with a per-row activation scale and a per-output-channel
+// weight scale folded into the epilogue.
 //
 // Structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop"):
 //   * 256 threads = 4 waves in a 2x2 grid; wave tile (BM/2)x(BN/2) made of
@@ -26,11 +27,28 @@
 namespace dtfs {
 namespace kern {
 
-typedef long fp8x8;  // 8 x e4m3 packed, the fp8 MFMA operand type
+typedef int i32x8 __attribute__((ext_vector_type(8)));  // 32 x e4m3, the block-scaled MFMA operand
 
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_SIGMOID = 2, EPI_CROSS = 3 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// fp8 K tile on the block-scaled MFMA: v_mfma_scale_f32_16x16x128_f8f6f4 with
+// e4m3 operands and unit E8M0 block scales (127 = 2^0) runs at 2x the rate of
+// the non-scaled v_mfma_f32_16x16x32_fp8_fp8 (which only matches bf16;
+// cdna_hip_programming.md §3 "MFMA rate per dtype"), and one instruction
+// covers the whole 128-byte K tile. The real scales (per activation row, per
+// weight channel) stay in the fp32 epilogue. Lane l holds row l&15,
+// k = 32*(l>>4) .. +31 = 16-B chunks 2*(l>>4) and 2*(l>>4)+1 of the row.
+__device__ __forceinline__ i32x8 mx_frag(const uint8_t* tile, int row, int fq) {
+  const i32x4 lo = *reinterpret_cast<const i32x4*>(tile + swz(row, 2 * fq));
+  const i32x4 hi = *reinterpret_cast<const i32x4*>(tile + swz(row, 2 * fq + 1));
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__device__ __forceinline__ f32x4 mx_mfma(const i32x8& a, const i32x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
 
 template <int BM, int BN, bool FP8, typename OutT>
 __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W,
@@ -131,22 +149,18 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     } else {
-      // fp8: 4 MFMA k-steps of 32 per 128-element tile; lane reads 8 bytes at
-      // byte 32*kk + 8*fq = chunk 2*kk + (fq>>1), half (fq&1).
+      // fp8: one block-scaled 16x16x128 MFMA per output tile covers the whole
+      // 128-element K tile (the loader zero-fills past K, so a partial last
+      // tile contributes zeros)
+      i32x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        fp8x8 af[TM], bfr[TN];
-        const int ch = kk * 2 + (fq >> 1), hoff = (fq & 1) * 8;
+      for (int i = 0; i < TM; ++i) af[i] = mx_frag(as, wm * WM + i * 16 + fr, fq);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const fp8x8*>(as + swz(wm * WM + i * 16 + fr, ch) + hoff);
+      for (int j = 0; j < TN; ++j) bfr[j] = mx_frag(bs, wn * WN + j * 16 + fr, fq);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const fp8x8*>(bs + swz(wn * WN + j * 16 + fr, ch) + hoff);
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
@@ -293,22 +307,17 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
       }
       __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
     } else {
+      i32x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        fp8x8 af[TM], bfr[TN];
-        const int ch = kk * 2 + (fq >> 1), hoff = (fq & 1) * 8;
+      for (int i = 0; i < TM; ++i) af[i] = mx_frag(as, wm * WTM + i * 16 + fr, fq);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const fp8x8*>(as + swz(wm * WTM + i * 16 + fr, ch) + hoff);
+      for (int j = 0; j < TN; ++j) bfr[j] = mx_frag(bs, wn * WTN + j * 16 + fr, fq);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const fp8x8*>(bs + swz(wn * WTN + j * 16 + fr, ch) + hoff);
-        __builtin_amdgcn_s_setprio(1);
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading this one
   }
@@ -591,20 +600,15 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     } else {
+      i32x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        fp8x8 af[TM], bfr[TN];
-        const int ch = kk * 2 + (fq >> 1), hoff = (fq & 1) * 8;
+      for (int i = 0; i < TM; ++i) af[i] = mx_frag(as, wm * WTM + i * 16 + fr, fq);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const fp8x8*>(as + swz(wm * WTM + i * 16 + fr, ch) + hoff);
+      for (int j = 0; j < TN; ++j) bfr[j] = mx_frag(bs, wn * WTN + j * 16 + fr, fq);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const fp8x8*>(bs + swz(wn * WTN + j * 16 + fr, ch) + hoff);
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
     }
     // RAW for tile kt+1: this wave's loads for it are done once at most the
     // tiles issued after it are outstanding; every wave's, after the barrier.
@@ -679,8 +683,10 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     //  * >= 256 tiles of 256x256: the 256x256 8-wave tile (best at M = 16K)
     //  * >= 512 tiles of 128x128: 128x128 2-stage LDS-DMA, 2 blocks/CU
     //  * otherwise (narrow N, e.g. the 512/256-wide MLP layers): 64x64 LDS-DMA
+    // (256x256 only when N fills whole tiles: at N = 2752 its ragged last
+    // column panel made it 13 % slower than 128x128)
     if (M <= 1024) variant = 8;
-    else if (blocks(256, 256) >= 256) variant = 9;
+    else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 9;
     else if (blocks(128, 128) >= 512) variant = 2;
     else variant = 4;
   }
@@ -714,6 +720,23 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
   }
   if (variant == 9 && glds_ok) {
     launch_pipe<256, 256, 2, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  // narrow-N tiles (the 512- and 256-wide MLP layers)
+  if (variant == 10 && glds_ok) {
+    launch_glds<128, 64, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 11 && glds_ok) {
+    launch_glds<64, 128, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 12 && glds_ok) {
+    launch_glds<128, 64, 4, 1, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 13 && glds_ok) {
+    launch_pipe<128, 64, 2, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   if (blocks(128, 128) >= 256)

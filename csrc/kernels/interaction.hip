@@ -153,11 +153,14 @@ __global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, i
 // Per-row dynamic e4m3 quantisation: scale = amax / 448, q = x / scale.
 template <int MAXC>
 __global__ void __launch_bounds__(256) quant_rows_kernel(const bf16* __restrict__ x, int64_t ldx, int M, int K,
-                                                         uint8_t* __restrict__ q, int64_t ldq, float* __restrict__ scale) {
+                                                         uint8_t* __restrict__ q, int64_t ldq, float* __restrict__ scale,
+                                                         int Kq) {
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (m >= M) return;
   const int nch = K / 8;
+  // zero the K padding (columns [K, Kq)) the 128-deep fp8 MFMA tiles read
+  for (int ch = nch + lane; ch < Kq / 8; ch += 64) *reinterpret_cast<int2*>(q + m * ldq + ch * 8) = make_int2(0, 0);
   float v[MAXC][8];
   float amax = 0.f;
 #pragma unroll
@@ -233,15 +236,16 @@ hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, c
 }
 
 hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void* q, int64_t ldq, float* scale,
-                                 hipStream_t st) {
+                                 hipStream_t st, int Kq) {
   if (M == 0) return hipSuccess;
-  if (K % 8) return hipErrorInvalidValue;
+  if (Kq <= 0) Kq = K;
+  if (K % 8 || Kq % 8 || Kq < K || ldq < Kq) return hipErrorInvalidValue;
   const int chunks = (K / 8 + 63) / 64;
   dim3 grid((M + 3) / 4), block(256);
   const bf16* xi = static_cast<const bf16*>(x);
   uint8_t* qo = static_cast<uint8_t*>(q);
 #define Q_CASE(C)                                                                                   \
-  case C: hipLaunchKernelGGL(quant_rows_kernel<C>, grid, block, 0, st, xi, ldx, M, K, qo, ldq, scale); break;
+  case C: hipLaunchKernelGGL(quant_rows_kernel<C>, grid, block, 0, st, xi, ldx, M, K, qo, ldq, scale, Kq); break;
   switch (chunks) {
     Q_CASE(1) Q_CASE(2) Q_CASE(3) Q_CASE(4) Q_CASE(5) Q_CASE(6) Q_CASE(7) Q_CASE(8)
     default: return hipErrorInvalidValue;

@@ -75,8 +75,10 @@ hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, c
                        int act, float* out, hipStream_t st);
 
 // fp8 (OCP e4m3) per-row quantisation.
+// Kq >= K: output row width; columns [K, Kq) are zeroed (K padding for the
+// 128-deep block-scaled fp8 MFMA). 0 = K.
 hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void* q, int64_t ldq, float* scale,
-                                 hipStream_t st);
+                                 hipStream_t st, int Kq = 0);
 
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();

@@ -124,9 +124,11 @@ def main():
     a = ap.parse_args()
     torch.manual_seed(0)
     if a.gemm_variants:
-        for s in [(8192, 1024, 2752), (8192, 512, 1024), (8192, 256, 512), (16384, 1024, 2752), (4096, 1024, 2752),
-                  (512, 1024, 2752), (4096, 2752, 2752)]:
-            print(json.dumps(bench_gemm_variants(*s)), flush=True)
+        narrow = (0, 2, 4, 8, 10, 11, 12, 13)
+        wide = (0, 2, 3, 5, 9)
+        for s, v in [((8192, 512, 1024), narrow), ((16384, 512, 1024), narrow), ((8192, 256, 512), narrow),
+                     ((8192, 1024, 2752), wide), ((16384, 1024, 2752), wide), ((8192, 2752, 2752), wide)]:
+            print(json.dumps(bench_gemm_variants(*s, variants=v)), flush=True)
         return
     shapes = [(512, 1024, 2752), (512, 512, 1024), (512, 256, 512), (4096, 1024, 2752), (8192, 1024, 2752),
               (4096, 2752, 2752)]

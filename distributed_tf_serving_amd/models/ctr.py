@@ -68,12 +68,14 @@ class CTRModel(nn.Module):
         return nn.Parameter(t, requires_grad=False)
 
     @torch.no_grad()
-    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor]) -> torch.Tensor:
+    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """CTR [B] fp32. ``out`` (fp32 [B], device or pinned host) receives the
+        scores straight from the head kernel (no separate D2H copy)."""
         if wts is not None and wts.dtype != torch.float32:
             wts = wts.float()
-        return self._forward(ids, wts)
+        return self._forward(ids, wts, out)
 
-    def _forward(self, ids, wts):  # pragma: no cover - abstract
+    def _forward(self, ids, wts, out=None):  # pragma: no cover - abstract
         raise NotImplementedError
 
 
@@ -91,10 +93,10 @@ class WideDeep(CTRModel):
                                    requires_grad=False)
         self.head_b = 0.0
 
-    def _forward(self, ids, wts):
+    def _forward(self, ids, wts, out=None):
         x, wide = ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
                             want_x=True, want_fm=True, fm2=False)
-        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide)
+        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide, out=out)
 
 
 class DeepFM(CTRModel):
@@ -111,10 +113,10 @@ class DeepFM(CTRModel):
                                    requires_grad=False)
         self.head_b = 0.0
 
-    def _forward(self, ids, wts):
+    def _forward(self, ids, wts, out=None):
         x, fm = ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
                           want_x=True, want_fm=True, fm2=True)
-        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm)
+        return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm, out=out)
 
 
 class DCN(CTRModel):
@@ -138,10 +140,10 @@ class DCN(CTRModel):
                                     requires_grad=False)
         self.head_b = 0.0
 
-    def _forward(self, ids, wts):
+    def _forward(self, ids, wts, out=None):
         x, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
         _, cross_logit = ops.cross_v1(x, self.cross_w, self.cross_b, want_x=False, head_w=self.head_wc)
-        return self.mlp.forward_head(x, self.head_wd, self.head_b, extra=cross_logit)
+        return self.mlp.forward_head(x, self.head_wd, self.head_b, extra=cross_logit, out=out)
 
 
 class DCNv2(CTRModel):
@@ -184,17 +186,17 @@ class DCNv2(CTRModel):
             return ops.cross_v2(x0, xl, u.weight, u.bias, a=v)
         layer = self.cross[i]
         if self.fp8:
-            xq, sx = ops.quant_rows_fp8(xl)
+            xq, sx = ops.quant_rows_fp8(xl, ops.FP8_K_PAD)
             return ops.linear_fp8(xq, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
-    def _forward(self, ids, wts):
+    def _forward(self, ids, wts, out=None):
         x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
         xl = x0
         for i in range(self.cfg.num_cross_layers):
             xl = self._cross_layer(i, x0, xl)
         cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
-        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit)
+        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out)
 
 
 class DLRM(CTRModel):
@@ -248,14 +250,14 @@ class DLRM(CTRModel):
         x, _ = ops.embed(self.emb, sp, None, modulo_f=self.modulo_f, offset_f=self.offset_f, want_x=True)
         return x.view(ids.shape[0], self.T, self.cfg.embed_dim)
 
-    def interact_and_top(self, dense_out: torch.Tensor, emb: torch.Tensor) -> torch.Tensor:
+    def interact_and_top(self, dense_out: torch.Tensor, emb: torch.Tensor, out=None) -> torch.Tensor:
         z = ops.dot_interaction(dense_out, emb, self.inter_cols)
-        return self.top.forward_head(z, self.head_w, self.head_b)
+        return self.top.forward_head(z, self.head_w, self.head_b, out=out)
 
-    def _forward(self, ids, wts):
+    def _forward(self, ids, wts, out=None):
         dense_out = self.bottom(self.dense_input(wts))
         emb = self.lookup(ids)
-        return self.interact_and_top(dense_out, emb)
+        return self.interact_and_top(dense_out, emb, out=out)
 
 
 FAMILIES = {c.family: c for c in (WideDeep, DeepFM, DCN, DCNv2, DLRM)}

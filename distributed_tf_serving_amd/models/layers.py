@@ -101,14 +101,17 @@ class Dense(nn.Module):
         wf = self.weight.float()
         amax = wf.abs().amax(dim=1)
         sw = torch.where(amax > 0, amax / ops.FP8_MAX, torch.ones_like(amax))
-        self.register_buffer("w_fp8", (wf / sw[:, None]).clamp(-ops.FP8_MAX, ops.FP8_MAX).to(torch.float8_e4m3fn),
-                             persistent=False)
+        q = (wf / sw[:, None]).clamp(-ops.FP8_MAX, ops.FP8_MAX).to(torch.float8_e4m3fn)
+        kq = -(-q.shape[1] // ops.FP8_K_PAD) * ops.FP8_K_PAD  # zero K padding: whole 128-deep MFMA tiles
+        if kq != q.shape[1]:
+            q = torch.cat([q, torch.zeros(q.shape[0], kq - q.shape[1], dtype=q.dtype, device=q.device)], dim=1)
+        self.register_buffer("w_fp8", q.contiguous(), persistent=False)
         self.register_buffer("w_scale", sw.contiguous(), persistent=False)
         self.fp8 = True
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fp8:
-            xq, sx = ops.quant_rows_fp8(x)
+            xq, sx = ops.quant_rows_fp8(x, ops.FP8_K_PAD)
             return ops.linear_fp8(xq, sx, self.w_fp8, self.w_scale, self.bias, self.act)
         return ops.linear(x, self.weight, self.bias, self.act)
 
@@ -132,12 +135,19 @@ class MLP(nn.Module):
         return x
 
     def forward_head(self, x: torch.Tensor, head_w: torch.Tensor, head_b: float,
-                     extra: Optional[torch.Tensor] = None, sigmoid: bool = True) -> torch.Tensor:
+                     extra: Optional[torch.Tensor] = None, sigmoid: bool = True,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """MLP then CTR head. On the GPU the last layer and the head run as one
-        kernel (ops.linear_head) whenever its shape allows."""
+        kernel (ops.linear_head) whenever its shape allows; it writes ``out``
+        (device or pinned host memory) directly."""
         for layer in self.layers[:-1]:
             x = layer(x)
         last = self.layers[-1]
         if x.is_cuda and not last.fp8 and last.act in ("relu", "none") and ops.linear_head_ok(x, last.weight):
-            return ops.linear_head(x, last.weight, last.bias, last.act, head_w, head_b, extra=extra, sigmoid=sigmoid)
-        return ops.head(last(x), head_w, head_b, extra=extra, sigmoid=sigmoid)
+            return ops.linear_head(x, last.weight, last.bias, last.act, head_w, head_b, extra=extra, sigmoid=sigmoid,
+                                   out=out)
+        y = ops.head(last(x), head_w, head_b, extra=extra, sigmoid=sigmoid)
+        if out is not None:
+            out.copy_(y, non_blocking=True)
+            return out
+        return y

@@ -151,14 +151,23 @@ def cross_v2(x0: torch.Tensor, xl: torch.Tensor, W: torch.Tensor, b: torch.Tenso
     return (x0.float() * y + xl.float()).to(x0.dtype)
 
 
-def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Dynamic per-row OCP e4m3 quantisation: (q, scale) with x ~= q * scale."""
+FP8_K_PAD = 128  # K granularity of the block-scaled fp8 MFMA (16x16x128) tiles
+
+
+def quant_rows_fp8(x: torch.Tensor, k_pad: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-row OCP e4m3 quantisation: (q, scale) with x ~= q * scale.
+
+    ``k_pad``: q's row width is K rounded up to it, zero-filled (fp8 GEMM
+    operands use FP8_K_PAD so every K tile is a full 128-deep MFMA)."""
     if x.is_cuda:
-        return tuple(hip().quant_rows_fp8(x.contiguous()))
+        return tuple(hip().quant_rows_fp8(_rows(x), int(k_pad)))
     xf = x.float()
     amax = xf.abs().amax(dim=1).clamp_min(0)
     scale = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
     q = (xf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    Kq = -(-x.shape[1] // k_pad) * k_pad
+    if Kq != x.shape[1]:
+        q = torch.cat([q, torch.zeros(x.shape[0], Kq - x.shape[1], dtype=q.dtype)], dim=1)
     return q, scale
 
 

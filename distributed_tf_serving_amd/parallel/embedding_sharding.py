@@ -358,10 +358,15 @@ class ShardedDLRM(nn.Module):
         return self.dense.param_bytes() + self.emb.local_bytes()
 
     @torch.no_grad()
-    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor]) -> torch.Tensor:
+    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor], out: Optional[torch.Tensor] = None):
         if wts is not None and wts.dtype != torch.float32:
             wts = wts.float()
         d = self.dense
         dense_out = d.bottom(d.dense_input(wts))
         emb = self.emb(d.sparse_ids(ids))
-        return d.interact_and_top(dense_out, emb)
+        return d.interact_and_top(dense_out, emb, out=out)
+
+    @property
+    def has_collectives(self) -> bool:
+        """The forward issues collectives (not capturable into the step graph)."""
+        return self.plan.world > 1

@@ -354,7 +354,9 @@ class FanoutEngine:
         def body():
             if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows
                 self._unpack(arena_dev, buf)
-            h_out[:B].copy_(self.ex._forward(buf), non_blocking=True)
+            # the head kernel writes the scores straight into pinned host memory
+            # (no D2H copy node, which a graph would run as a blit kernel)
+            self.ex._forward(buf, out=h_out[:B])
 
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(cur)

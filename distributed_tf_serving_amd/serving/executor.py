@@ -26,7 +26,8 @@ class ShardExecutor:
         self.buckets = sorted(set(int(b) for b in buckets))
         self.device = torch.device(device)
         self.is_cuda = self.device.type == "cuda"
-        self.use_graphs = bool(use_graphs and self.is_cuda)
+        # a forward that issues collectives itself (sharded DLRM tables) runs eagerly
+        self.use_graphs = bool(use_graphs and self.is_cuda and not getattr(model, "has_collectives", False))
         self.slots = max(1, int(slots))
         self.warmup = warmup
         self._inp: Dict[Tuple[int, int], torch.Tensor] = {}
@@ -55,8 +56,10 @@ class ShardExecutor:
             self._inp[key] = buf
         return buf
 
-    def _forward(self, buf: torch.Tensor) -> torch.Tensor:
-        return self.model(self.layout.ids(buf), self.layout.wts(buf))
+    def _forward(self, buf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if out is None:
+            return self.model(self.layout.ids(buf), self.layout.wts(buf))
+        return self.model(self.layout.ids(buf), self.layout.wts(buf), out=out)
 
     def prepare(self, B: int, slot: int = 0) -> None:
         """Allocate (and on GPU capture) bucket B for a slot ahead of traffic."""

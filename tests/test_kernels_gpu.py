@@ -154,6 +154,21 @@ def test_gemm_fp8(cuda, M, N, K):
     _close(y, ref, 2e-3, 2e-3, "fp8 gemm")
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 64, 128), (300, 512, 2752), (8192, 1024, 2752), (1000, 2752, 2752)])
+def test_gemm_fp8_k_padded(cuda, M, N, K):
+    # the model path: K padded to 128 (zero columns), full 128-deep MX-fp8 tiles
+    g = torch.Generator().manual_seed(11 + M)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16) / K ** 0.5
+    xq, sx = ops.quant_rows_fp8(x.to(cuda), ops.FP8_K_PAD)
+    wq, sw = ops.quant_rows_fp8(W.to(cuda), ops.FP8_K_PAD)
+    assert xq.shape[1] % 128 == 0 and (xq[:, K:].view(torch.uint8) == 0).all()
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.linear_fp8(xq, sx, wq, sw, b.to(cuda), "relu", out_f32=True)
+    ref = ops.linear_fp8(xq.cpu(), sx.cpu(), wq.cpu(), sw.cpu(), b, "relu", out_f32=True)
+    _close(y, ref, 2e-3, 2e-3, "fp8 gemm (K padded)")
+
+
 def test_quant_rows_fp8(cuda):
     x = (torch.randn(77, 2752) * 3).to(torch.bfloat16)
     q, s = ops.quant_rows_fp8(x.to(cuda))
