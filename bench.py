@@ -97,6 +97,8 @@ def parse_args():
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--loop", default="native", choices=["native", "python"],
+                    help="native: per-step host loop in C++ (csrc/runtime/serving_loop.cpp); python: StepPipeline")
     ap.add_argument("--force-fanout", action="store_true",
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--no-native-fanout", action="store_true",
@@ -208,14 +210,55 @@ def main():
             return eng.launch(B, slot, nbytes=0)
         return eng.launch(B, slot)
 
-    # decode(k+3) || H2D(k+1..k+2) [SDMA] || forward(k) [GPU] || encode(k-1)
-    pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1, produce=decode,
-                        consume=lambda k, pb, scores: encode(pb, scores), launch=launch)
-    phase = pipe.phase
-    lat = pipe.latencies
+    use_native_loop = a.loop == "native" and dev.type == "cuda" and a.ingest == "arena" and not a.no_graphs
+    if use_native_loop:
+        try:
+            loop_slots = eng.loop_slots(B)
+        except RuntimeError as e:  # e.g. a forward with collectives (sharded DLRM): Python pipeline
+            if rank == 0:
+                print(f"note: native loop unavailable ({e}); using the Python pipeline", file=sys.stderr)
+            use_native_loop = False
+    if use_native_loop:
+        # the whole per-step host loop in C++ (csrc/runtime/serving_loop.cpp):
+        # parse(k+3) || H2D(k+1..k+2) [SDMA] || step graph(k) [GPU] || encode(k-1)
+        from distributed_tf_serving_amd.ops import hip
 
-    def run(n_steps: int, record: bool):
-        pipe.run(n_steps, record=record)
+        nloop = hip().ServingLoop(eng.runner(), dict(depth=slots - 1, fields=F, max_rows=arena_layout.max_rows,
+                                                     version=1), loop_slots)
+        for ar, sp in zip(arenas, spans):
+            nloop.add_input(ar, sp)
+        lat: list = []
+        phase = {"parse": 0.0, "launch": 0.0, "gpu_wait": 0.0, "encode": 0.0}
+
+        def run(n_steps: int, record: bool):
+            st = nloop.run(n_steps, record)
+            if st["errors"]:
+                raise RuntimeError(f"{st['errors']} requests failed in the native loop")
+            if record:
+                lat.extend(x * 1e-6 for x in st["latency_us"])
+                for k_src, k_dst in (("parse_us", "parse"), ("launch_us", "launch"), ("wait_us", "gpu_wait"),
+                                     ("encode_us", "encode")):
+                    phase[k_dst] += st[k_src] * 1e-6
+
+        class _NoPipe:
+            def reset_stats(self):
+                lat.clear()
+                for k in phase:
+                    phase[k] = 0.0
+
+            def close(self):
+                pass
+
+        pipe = _NoPipe()
+    else:
+        # decode(k+3) || H2D(k+1..k+2) [SDMA] || forward(k) [GPU] || encode(k-1)
+        pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1, produce=decode,
+                            consume=lambda k, pb, scores: encode(pb, scores), launch=launch)
+        phase = pipe.phase
+        lat = pipe.latencies
+
+        def run(n_steps: int, record: bool):
+            pipe.run(n_steps, record=record)
 
     def sync():
         if dev.type == "cuda":

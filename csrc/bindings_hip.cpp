@@ -12,6 +12,7 @@
 
 #include "kernels/launchers.h"
 #include "comm/rccl_comm.h"
+#include "runtime/serving_loop.h"
 #include "runtime/step_runner.h"
 
 namespace {
@@ -407,6 +408,110 @@ std::vector<torch::Tensor> sort_scores(torch::Tensor s, bool descending, int64_t
   return {out, perm};
 }
 
+// ---------------------------------------------------------------- fan-out step
+// Validates the device/host buffers of one fan-out step (everything but the
+// per-step H2D source) and computes the per-peer message sizes.
+dtfs::runtime::FanoutStep make_fanout_step(torch::Tensor h2d_dst, uintptr_t ingress_exec, dtfs::comm::RcclComm& cin,
+                                           int mode, torch::Tensor send, torch::Tensor recv, uintptr_t forward_exec,
+                                           dtfs::comm::RcclComm& cout, torch::Tensor scores, torch::Tensor back,
+                                           torch::Tensor h_out, int64_t d2h_bytes) {
+  TORCH_CHECK(mode == 0 || mode == 1, "mode: 0 all-to-all, 1 scatter/gather");
+  TORCH_CHECK(cin.nranks() == cout.nranks() && cin.rank() == cout.rank(), "communicator mismatch");
+  const int W = cin.nranks();
+  for (auto* t : {&h2d_dst, &send, &recv, &scores, &back})
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "fan-out buffers must be contiguous GPU tensors");
+  TORCH_CHECK(h_out.device().is_cpu() && h_out.is_pinned(), "h_out must be pinned host memory");
+  // all-to-all: send/recv (and scores/back) are this rank's B rows, B/W to /
+  // from each peer. scatter/gather: recv/scores are this rank's B rows; the
+  // root's send/back hold W x B.
+  size_t in_bytes, out_bytes;
+  if (mode == 0) {
+    TORCH_CHECK(send.nbytes() == recv.nbytes() && recv.nbytes() % W == 0,
+                "all-to-all: send and recv must match and split evenly over the ranks");
+    TORCH_CHECK(back.nbytes() == scores.nbytes() && scores.nbytes() % W == 0,
+                "all-to-all: scores and back must match and split evenly over the ranks");
+    in_bytes = recv.nbytes() / W;
+    out_bytes = scores.nbytes() / W;
+  } else {
+    in_bytes = recv.nbytes();
+    out_bytes = scores.nbytes();
+    if (cin.rank() == 0) {
+      TORCH_CHECK(send.nbytes() >= in_bytes * W, "scatter: root send smaller than world x recv");
+      TORCH_CHECK(back.nbytes() >= out_bytes * W, "gather: root back smaller than world x scores");
+    }
+  }
+  TORCH_CHECK(d2h_bytes >= 0 && size_t(d2h_bytes) <= back.nbytes() && size_t(d2h_bytes) <= h_out.nbytes(),
+              "d2h_bytes out of range");
+  TORCH_CHECK(forward_exec != 0, "null forward graph");
+  dtfs::runtime::FanoutStep s;
+  s.h2d_dst = h2d_dst.data_ptr();
+  s.ingress = reinterpret_cast<hipGraphExec_t>(ingress_exec);
+  s.cin = &cin;
+  s.mode = mode;
+  s.send = send.data_ptr();
+  s.recv = recv.data_ptr();
+  s.in_bytes = in_bytes;
+  s.forward = reinterpret_cast<hipGraphExec_t>(forward_exec);
+  s.cout = &cout;
+  s.scores = scores.data_ptr();
+  s.back = back.data_ptr();
+  s.out_bytes = out_bytes;
+  s.h_out = h_out.data_ptr();
+  s.d2h_bytes = size_t(d2h_bytes);
+  return s;
+}
+
+// ServingLoop + the Python objects whose memory it points into.
+struct PyServingLoop {
+  std::unique_ptr<dtfs::runtime::ServingLoop> loop;
+  std::vector<py::object> keep;
+};
+
+PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list slots) {
+  auto* p = new PyServingLoop();
+  p->keep.push_back(runner_obj);
+  auto& runner = runner_obj.cast<dtfs::runtime::StepRunner&>();
+  dtfs::runtime::LoopConfig c;
+  c.depth = cfg.contains("depth") ? cfg["depth"].cast<int>() : 3;
+  c.fields = cfg["fields"].cast<int64_t>();
+  c.max_rows = cfg["max_rows"].cast<int64_t>();
+  if (cfg.contains("ids_key")) c.ids_key = cfg["ids_key"].cast<std::string>();
+  if (cfg.contains("wts_key")) c.wts_key = cfg["wts_key"].cast<std::string>();
+  if (cfg.contains("model_name")) c.model_name = cfg["model_name"].cast<std::string>();
+  if (cfg.contains("signature_name")) c.signature_name = cfg["signature_name"].cast<std::string>();
+  if (cfg.contains("output_key")) c.output_key = cfg["output_key"].cast<std::string>();
+  if (cfg.contains("version") && !cfg["version"].is_none()) c.version = cfg["version"].cast<int64_t>();
+  std::vector<dtfs::runtime::LoopSlot> ls;
+  for (auto item : slots) {
+    py::dict d = item.cast<py::dict>();
+    p->keep.push_back(d);
+    dtfs::runtime::LoopSlot s;
+    torch::Tensor h_out = d["h_out"].cast<torch::Tensor>();
+    TORCH_CHECK(h_out.device().is_cpu() && h_out.is_pinned() && h_out.scalar_type() == torch::kFloat32 &&
+                    h_out.is_contiguous(),
+                "h_out must be a pinned contiguous fp32 tensor");
+    s.h_out = h_out.data_ptr<float>();
+    s.h_out_len = h_out.numel();
+    torch::Tensor dst = d["h2d_dst"].cast<torch::Tensor>();
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_dst must be a contiguous GPU tensor");
+    if (d.contains("fanout") && d["fanout"].cast<bool>()) {
+      s.fanout = true;
+      s.fan = make_fanout_step(dst, d["ingress_exec"].cast<uintptr_t>(), d["cin"].cast<dtfs::comm::RcclComm&>(),
+                               d["mode"].cast<int>(), d["send"].cast<torch::Tensor>(), d["recv"].cast<torch::Tensor>(),
+                               d["forward_exec"].cast<uintptr_t>(), d["cout"].cast<dtfs::comm::RcclComm&>(),
+                               d["scores"].cast<torch::Tensor>(), d["back"].cast<torch::Tensor>(), h_out,
+                               d["d2h_bytes"].cast<int64_t>());
+    } else {
+      s.h2d_dst = dst.data_ptr();
+      s.graph = reinterpret_cast<hipGraphExec_t>(d["graph_exec"].cast<uintptr_t>());
+      TORCH_CHECK(s.graph != nullptr, "null step graph");
+    }
+    ls.push_back(s);
+  }
+  p->loop = std::make_unique<dtfs::runtime::ServingLoop>(&runner, c, std::move(ls));
+  return p;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hip, m) {
@@ -458,55 +563,14 @@ PYBIND11_MODULE(_hip, m) {
              uintptr_t ingress_exec, dtfs::comm::RcclComm& cin, int mode, torch::Tensor send, torch::Tensor recv,
              uintptr_t forward_exec, dtfs::comm::RcclComm& cout, torch::Tensor scores, torch::Tensor back,
              torch::Tensor h_out, int64_t d2h_bytes) {
-            TORCH_CHECK(mode == 0 || mode == 1, "mode: 0 all-to-all, 1 scatter/gather");
-            TORCH_CHECK(cin.nranks() == cout.nranks() && cin.rank() == cout.rank(), "communicator mismatch");
-            const int W = cin.nranks();
-            for (auto* t : {&h2d_dst, &send, &recv, &scores, &back})
-              TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "fan-out buffers must be contiguous GPU tensors");
-            TORCH_CHECK(h2d_src.device().is_cpu() && h2d_src.is_pinned() && h_out.is_pinned(),
-                        "host buffers must be pinned");
+            TORCH_CHECK(h2d_src.device().is_cpu() && h2d_src.is_pinned(), "h2d_src must be pinned host memory");
             TORCH_CHECK(h2d_bytes >= 0 && h2d_bytes <= int64_t(h2d_dst.nbytes()) &&
                             h2d_bytes <= int64_t(h2d_src.nbytes()),
                         "h2d_bytes out of range");
-            // all-to-all: send/recv (and scores/back) are this rank's B rows,
-            // B/W to / from each peer. scatter/gather: recv/scores are this
-            // rank's B rows; the root's send/back hold W x B.
-            size_t in_bytes, out_bytes;
-            if (mode == 0) {
-              TORCH_CHECK(send.nbytes() == recv.nbytes() && recv.nbytes() % W == 0,
-                          "all-to-all: send and recv must match and split evenly over the ranks");
-              TORCH_CHECK(back.nbytes() == scores.nbytes() && scores.nbytes() % W == 0,
-                          "all-to-all: scores and back must match and split evenly over the ranks");
-              in_bytes = recv.nbytes() / W;
-              out_bytes = scores.nbytes() / W;
-            } else {
-              in_bytes = recv.nbytes();
-              out_bytes = scores.nbytes();
-              if (cin.rank() == 0) {
-                TORCH_CHECK(send.nbytes() >= in_bytes * W, "scatter: root send smaller than world x recv");
-                TORCH_CHECK(back.nbytes() >= out_bytes * W, "gather: root back smaller than world x scores");
-              }
-            }
-            TORCH_CHECK(d2h_bytes >= 0 && size_t(d2h_bytes) <= back.nbytes() && size_t(d2h_bytes) <= h_out.nbytes(),
-                        "d2h_bytes out of range");
-            TORCH_CHECK(forward_exec != 0, "null forward graph");
-            dtfs::runtime::FanoutStep s;
-            s.h2d_dst = h2d_dst.data_ptr();
+            auto s = make_fanout_step(h2d_dst, ingress_exec, cin, mode, send, recv, forward_exec, cout, scores, back,
+                                      h_out, d2h_bytes);
             s.h2d_src = h2d_src.data_ptr();
             s.h2d_bytes = h2d_bytes;
-            s.ingress = reinterpret_cast<hipGraphExec_t>(ingress_exec);
-            s.cin = &cin;
-            s.mode = mode;
-            s.send = send.data_ptr();
-            s.recv = recv.data_ptr();
-            s.in_bytes = in_bytes;
-            s.forward = reinterpret_cast<hipGraphExec_t>(forward_exec);
-            s.cout = &cout;
-            s.scores = scores.data_ptr();
-            s.back = back.data_ptr();
-            s.out_bytes = out_bytes;
-            s.h_out = h_out.data_ptr();
-            s.d2h_bytes = size_t(d2h_bytes);
             r.launch_fanout(slot, s);
           },
           py::arg("slot"), py::arg("h2d_dst"), py::arg("h2d_src"), py::arg("h2d_bytes"), py::arg("ingress_exec"),
@@ -517,6 +581,44 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
+
+  py::class_<PyServingLoop>(m, "ServingLoop",
+                            "Native per-rank serving loop: parse -> H2D + step graph (or fan-out) -> encode")
+      .def(py::init(&make_serving_loop), py::arg("runner"), py::arg("config"), py::arg("slots"))
+      .def(
+          "add_input",
+          [](PyServingLoop& p, torch::Tensor arena, const std::vector<std::pair<int64_t, int64_t>>& spans) {
+            TORCH_CHECK(arena.device().is_cpu() && arena.is_pinned() && arena.is_contiguous() &&
+                            arena.scalar_type() == torch::kUInt8,
+                        "arena must be a pinned contiguous uint8 tensor");
+            p.keep.push_back(py::cast(arena));
+            p.loop->add_input(arena.data_ptr<uint8_t>(), arena.numel(), spans);
+          },
+          py::arg("arena"), py::arg("spans"))
+      .def(
+          "run",
+          [](PyServingLoop& p, int64_t n, bool record) {
+            dtfs::runtime::LoopStats s;
+            {
+              py::gil_scoped_release nogil;
+              s = p.loop->run(n, record);
+            }
+            py::dict d;
+            d["latency_us"] = s.latency_us;
+            d["steps"] = s.steps;
+            d["requests"] = s.requests;
+            d["rows"] = s.rows;
+            d["errors"] = s.errors;
+            d["response_bytes"] = s.response_bytes;
+            d["parse_us"] = s.parse_us;
+            d["launch_us"] = s.launch_us;
+            d["wait_us"] = s.wait_us;
+            d["encode_us"] = s.encode_us;
+            d["wall_us"] = s.wall_us;
+            return d;
+          },
+          py::arg("n_steps"), py::arg("record") = true)
+      .def_property_readonly("slots", [](const PyServingLoop& p) { return p.loop->slots(); });
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });

@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "runtime/batcher.h"
+#include "runtime/arena.h"
 #include "runtime/thread_pool.h"
 #include "wire/tensor_codec.h"
 
@@ -267,187 +268,60 @@ void decode_batch_range(ParsedBatch& b, torch::Tensor ids_dst, c10::optional<tor
 }
 
 // ---------------------------------------------------------------- request arena
-// Layout shared with csrc/kernels/ingest.hip and serving/arena.py:
-//   [0]   int32 n_req      [8] int64 total_rows
-//   [64]  n_req x {ids_off, wts_off, rows, dst_row} int64 (offsets into payload)
-//   [kArenaPayloadOff] payload: serialized requests (+ scratch for decoded typed fields)
-constexpr int64_t kArenaPayloadOff = 64 + 32 * 1024;
-constexpr int64_t kArenaMaxRequests = 1024;
+// Thin wrappers over csrc/runtime/arena.cpp (layout documented there).
+using runtime::ArenaBatch;
+using runtime::kArenaMaxRequests;
+using runtime::kArenaPayloadOff;
 
-struct ArenaBatch {
-  std::vector<int64_t> rows, offsets;
-  std::vector<std::string> errors;
-  int64_t total_rows = 0, used_bytes = 0, n_valid = 0, n_decoded = 0;
-};
+void check_arena(const torch::Tensor& arena) {
+  if (arena.device().type() != torch::kCPU || !arena.is_contiguous() || arena.scalar_type() != torch::kUInt8)
+    throw py::value_error("arena must be a contiguous CPU uint8 tensor");
+}
 
 // Copy serialized requests into the arena payload (parallel memcpy, GIL-free);
 // returns their (offset, length) spans relative to the payload start.
 std::vector<std::pair<int64_t, int64_t>> arena_place(torch::Tensor arena, const std::vector<py::bytes>& reqs,
                                                      int64_t start) {
-  if (arena.device().type() != torch::kCPU || !arena.is_contiguous() || arena.scalar_type() != torch::kUInt8)
-    throw py::value_error("arena must be a contiguous CPU uint8 tensor");
+  check_arena(arena);
   std::vector<std::pair<const char*, size_t>> src(reqs.size());
-  std::vector<std::pair<int64_t, int64_t>> spans(reqs.size());
-  int64_t off = start;
   for (size_t i = 0; i < reqs.size(); ++i) {
     char* p;
     Py_ssize_t len;
     if (PyBytes_AsStringAndSize(reqs[i].ptr(), &p, &len) != 0) throw py::error_already_set();
     src[i] = {p, size_t(len)};
-    spans[i] = {off, int64_t(len)};
-    off += (int64_t(len) + 7) & ~int64_t(7);
   }
-  if (kArenaPayloadOff + off > arena.numel()) throw py::value_error("arena too small for the batch");
-  uint8_t* payload = arena.data_ptr<uint8_t>() + kArenaPayloadOff;
   py::gil_scoped_release nogil;
-  runtime::ThreadPool::global().parallel_for(int64_t(reqs.size()), [&](int64_t i) {
-    std::memcpy(payload + spans[i].first, src[i].first, src[i].second);
-  });
-  return spans;
+  try {
+    return runtime::arena_place(arena.data_ptr<uint8_t>(), arena.numel(), src, start);
+  } catch (const std::invalid_argument& e) {
+    py::gil_scoped_acquire g;
+    throw py::value_error(e.what());
+  }
 }
 
-// Parse the requests that sit in the arena payload and write the descriptor
-// table. Raw DT_INT64 / DT_FLOAT tensor_content payloads are referenced in
-// place (the GPU gathers them); any other encoding (typed int64_val/float_val,
-// other dtypes, fill semantics) is decoded on the host into scratch space after
-// the last request, in raw form, and referenced from there.
 ArenaBatch arena_build(torch::Tensor arena, const std::vector<std::pair<int64_t, int64_t>>& spans,
                        const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows) {
-  if (arena.device().type() != torch::kCPU || !arena.is_contiguous() || arena.scalar_type() != torch::kUInt8)
-    throw py::value_error("arena must be a contiguous CPU uint8 tensor");
-  if (int64_t(spans.size()) > kArenaMaxRequests) throw py::value_error("too many requests for one arena");
-  uint8_t* base = arena.data_ptr<uint8_t>();
-  uint8_t* payload = base + kArenaPayloadOff;
-  const int64_t cap = arena.numel() - kArenaPayloadOff;
-  ArenaBatch out;
-  const size_t n = spans.size();
-  out.rows.assign(n, 0);
-  out.offsets.assign(n, 0);
-  out.errors.assign(n, std::string());
-  int64_t end = 0;
-  for (const auto& s : spans) {
-    if (s.first < 0 || s.second < 0 || s.first + s.second > cap) throw py::value_error("request span outside arena");
-    end = std::max(end, s.first + s.second);
+  check_arena(arena);
+  py::gil_scoped_release nogil;
+  try {
+    return runtime::arena_build(arena.data_ptr<uint8_t>(), arena.numel(), spans, ids_key, wts_key, fields, max_rows);
+  } catch (const std::invalid_argument& e) {
+    py::gil_scoped_acquire g;
+    throw py::value_error(e.what());
   }
-  int64_t scratch = (end + 63) & ~int64_t(63);
-  int64_t* desc = reinterpret_cast<int64_t*>(base + 64);
-  struct Job {
-    int64_t req;
-    const wire::TensorView *ti, *tw;
-    int64_t ne, ids_off, wts_off, ids_scratch, wts_scratch, slot;
-  };
-  std::vector<Job> jobs;
-  {
-    py::gil_scoped_release nogil;
-    std::vector<wire::PredictRequestView> views(n);
-    int64_t nd = 0, row = 0;
-    for (size_t i = 0; i < n; ++i) {
-      std::string err;
-      auto& v = views[i];
-      if (!wire::parse_predict_request(payload + spans[i].first, size_t(spans[i].second), &v, &err)) {
-        out.errors[i] = "malformed PredictRequest: " + err;
-        continue;
-      }
-      const wire::TensorView* ti = v.find(ids_key);
-      const wire::TensorView* tw = v.find(wts_key);
-      if (!ti || !tw) {
-        out.errors[i] = "input '" + (ti ? wts_key : ids_key) + "' missing";
-        continue;
-      }
-      if (ti->unknown_rank || ti->shape.size() != 2 || ti->shape[1] != fields || ti->shape[0] < 0 ||
-          tw->shape != ti->shape) {
-        out.errors[i] = "inputs must have shape [B, " + std::to_string(fields) + "]";
-        continue;
-      }
-      const int64_t rows = ti->shape[0], ne = rows * fields;
-      if (row + rows > max_rows) {
-        out.errors[i] = "batch exceeds the arena's row capacity";
-        continue;
-      }
-      const bool ids_raw = ti->content.n > 0 && ti->dtype == wire::DT_INT64 && ti->content.n == size_t(ne) * 8;
-      const bool wts_raw = tw->content.n > 0 && tw->dtype == wire::DT_FLOAT && tw->content.n == size_t(ne) * 4;
-      if ((!ids_raw && ti->num_values > ne) || (!wts_raw && tw->num_values > ne)) {
-        out.errors[i] = "more values than the tensor shape holds";
-        continue;
-      }
-      // plan: raw payloads are referenced in place; the rest get scratch space
-      // and are decoded below, in parallel
-      int64_t need = (ids_raw ? 0 : ((ne * 8 + 63) & ~int64_t(63))) + (wts_raw ? 0 : ((ne * 4 + 63) & ~int64_t(63)));
-      if (scratch + need > cap) {
-        out.errors[i] = "arena scratch exhausted";
-        continue;
-      }
-      Job j{int64_t(i), ti, tw, ne, ids_raw ? int64_t(ti->content.p - payload) : -1,
-            wts_raw ? int64_t(tw->content.p - payload) : -1, 0, 0, nd};
-      if (!ids_raw) {
-        j.ids_scratch = scratch;
-        scratch += (ne * 8 + 63) & ~int64_t(63);
-      }
-      if (!wts_raw) {
-        j.wts_scratch = scratch;
-        scratch += (ne * 4 + 63) & ~int64_t(63);
-      }
-      jobs.push_back(j);
-      desc[4 * nd + 0] = ids_raw ? j.ids_off : j.ids_scratch;
-      desc[4 * nd + 1] = wts_raw ? j.wts_off : j.wts_scratch;
-      desc[4 * nd + 2] = rows;
-      desc[4 * nd + 3] = row;
-      ++nd;
-      out.rows[i] = rows;
-      out.offsets[i] = row;
-      row += rows;
-    }
-    // typed-field (varint / float_val) decode, one request per pool task
-    std::vector<std::string> errs(jobs.size());
-    runtime::ThreadPool::global().parallel_for(int64_t(jobs.size()), [&](int64_t k) {
-      const Job& j = jobs[k];
-      std::string err;
-      if (j.ids_off < 0) {
-        wire::DecodeOpts o;
-        o.dst = wire::DstType::I64;
-        if (!wire::decode_into(*j.ti, payload + j.ids_scratch, j.ne, o, &err)) errs[k] = "input '" + ids_key + "': " + err;
-      }
-      if (j.wts_off < 0 && errs[k].empty()) {
-        wire::DecodeOpts o;
-        o.dst = wire::DstType::F32;
-        if (!wire::decode_into(*j.tw, payload + j.wts_scratch, j.ne, o, &err)) errs[k] = "input '" + wts_key + "': " + err;
-      }
-    });
-    for (size_t k = 0; k < jobs.size(); ++k) {
-      if (jobs[k].ids_off < 0) ++out.n_decoded;
-      // decode failed late: its rows stay in the batch (scored, dropped), the
-      // request itself is answered with the error
-      if (!errs[k].empty()) out.errors[jobs[k].req] = errs[k];
-    }
-    *reinterpret_cast<int32_t*>(base) = int32_t(nd);
-    *reinterpret_cast<int64_t*>(base + 8) = row;
-    out.total_rows = row;
-    out.n_valid = nd;
-    out.used_bytes = kArenaPayloadOff + std::max(end, scratch);
-  }
-  return out;
 }
 
 // Host reference of the GPU unpack (tests, CPU serving): arena -> packed rows.
 void arena_unpack_cpu(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
+  check_arena(arena);
   if (packed.scalar_type() != torch::kInt64 || packed.dim() != 2 || !packed.is_contiguous())
     throw py::value_error("packed must be a contiguous int64 [B, W] tensor");
+  if (packed.size(1) * 8 < 12 * fields) throw py::value_error("packed rows too narrow for the field count");
   const uint8_t* base = arena.data_ptr<uint8_t>();
-  const int32_t n = *reinterpret_cast<const int32_t*>(base);
-  const int64_t* desc = reinterpret_cast<const int64_t*>(base + 64);
-  const uint8_t* payload = base + kArenaPayloadOff;
   uint8_t* dst = reinterpret_cast<uint8_t*>(packed.data_ptr<int64_t>());
   const int64_t W = packed.size(1), B = packed.size(0);
   py::gil_scoped_release nogil;
-  std::memset(dst, 0, size_t(B * W * 8));
-  for (int32_t i = 0; i < n; ++i) {
-    for (int64_t r = 0; r < desc[4 * i + 2]; ++r) {
-      const int64_t row = desc[4 * i + 3] + r;
-      if (row >= B) break;
-      std::memcpy(dst + row * W * 8, payload + desc[4 * i + 0] + r * 8 * fields, size_t(8 * fields));
-      std::memcpy(dst + row * W * 8 + 8 * fields, payload + desc[4 * i + 1] + r * 4 * fields, size_t(4 * fields));
-    }
-  }
+  runtime::arena_unpack_cpu(base, dst, B, W, fields);
 }
 
 // One PredictResponse per request: outputs[key] = scores[offsets[i] : +rows[i]]

@@ -50,6 +50,77 @@ __device__ __forceinline__ f32x4 mx_mfma(const i32x8& a, const i32x8& b, const f
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 
+// Every kernel below issues its MFMAs as D = W_frag x A_frag^T, i.e. it
+// computes the TRANSPOSED 16x16 output tile: with the C/D layout (col =
+// lane & 15, row = 4 * (lane >> 4) + r) a lane then holds C[m = fr][n = 4 fq
+// .. 4 fq + 3] - four consecutive output columns of one row. The epilogue
+// reads bias / scales / x0 / xl and writes C as 8- or 16-byte vectors per lane
+// instead of 2- or 4-byte scalars (the DCN-v2 cross epilogue touches three
+// [M, N] bf16 tensors).
+template <bool FP8, int TM, int TN, typename OutT>
+__device__ __forceinline__ void store_acc_t(const f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq, int M, int N,
+                                            const float* __restrict__ bias, const float* __restrict__ sa,
+                                            const float* __restrict__ sw, OutT* __restrict__ C, int64_t ldc,
+                                            const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx,
+                                            int epi) {
+  const int e = epi & 15;
+  const bool vec = ((N | int(ldc) | int(ldx)) & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = mb + i * 16 + fr;
+    if (m >= M) continue;
+    const float sam = (FP8 && sa) ? sa[m] : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = nb + j * 16 + fq * 4;
+      if (n >= N) continue;
+      float v[4];
+      if (vec) {  // N % 4 == 0 and n % 4 == 0: all four columns exist
+        const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
+        if (FP8 && sw) s4 = *reinterpret_cast<const f32x4*>(sw + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[i][j][r];
+          if (FP8) x *= s4[r] * sam;
+          x += b4[r];
+          if (e == EPI_RELU) x = fmaxf(x, 0.f);
+          else if (e == EPI_SIGMOID) x = sigmoidf(x);
+          v[r] = x;
+        }
+        if (e == EPI_CROSS) {
+          const bf16x4 x0 = *reinterpret_cast<const bf16x4*>(X0 + int64_t(m) * ldx + n);
+          const bf16x4 xl = *reinterpret_cast<const bf16x4*>(XL + int64_t(m) * ldx + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = bf2f(x0[r]) * v[r] + bf2f(xl[r]);
+        }
+        if constexpr (sizeof(OutT) == 2) {
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+          *reinterpret_cast<bf16x4*>(C + int64_t(m) * ldc + n) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(C + int64_t(m) * ldc + n) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nn = n + r;
+          if (nn >= N) break;
+          float x = acc[i][j][r];
+          if (FP8) x *= (sw ? sw[nn] : 1.f) * sam;
+          x += bias ? bias[nn] : 0.f;
+          if (e == EPI_RELU) x = fmaxf(x, 0.f);
+          else if (e == EPI_SIGMOID) x = sigmoidf(x);
+          else if (e == EPI_CROSS) x = bf2f(X0[int64_t(m) * ldx + nn]) * x + bf2f(XL[int64_t(m) * ldx + nn]);
+          if constexpr (sizeof(OutT) == 2) C[int64_t(m) * ldc + nn] = f2bf(x);
+          else C[int64_t(m) * ldc + nn] = x;
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN, bool FP8, typename OutT>
 __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W,
                                                    int64_t ldw, const float* __restrict__ bias,
@@ -146,7 +217,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     } else {
       // fp8: one block-scaled 16x16x128 MFMA per output tile covers the whole
@@ -160,36 +231,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(bfr[j], af[i], acc[i][j]);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
 
-  // Epilogue. C/D layout (16x16): col = lane & 15, row = 4 * (lane >> 4) + r.
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + fr;
-    if (n >= N) continue;
-    const float bn = bias ? bias[n] : 0.f;
-    const float swn = sw ? sw[n] : 1.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + fq * 4 + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r];
-        if (FP8) v *= swn * (sa ? sa[m] : 1.f);
-        v += bn;
-        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
-        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
-        else if ((epi & 15) == EPI_CROSS) v =bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
-        if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
-        else C[m * ldc + n] = v;
-      }
-    }
-  }
+  store_acc_t<FP8>(acc, m0 + wm * WM, n0 + wn * WN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
 // ---------------------------------------------------------------------------
@@ -295,17 +343,8 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      // schedule: first half's reads, then its MFMAs interleaved with the
-      // second half's reads (2 MFMA : 1 ds_read), then the rest of the MFMAs
-      __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
-#pragma unroll
-      for (int g = 0; g < TM + TN; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (TM + TN), 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
     } else {
       i32x8 af[TM], bfr[TN];
 #pragma unroll
@@ -316,35 +355,13 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(bfr[j], af[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading this one
   }
 
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + j * 16 + fr;
-    if (n >= N) continue;
-    const float bn = bias ? bias[n] : 0.f;
-    const float swn = sw ? sw[n] : 1.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r];
-        if (FP8) v *= swn * (sa ? sa[m] : 1.f);
-        v += bn;
-        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
-        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
-        else if ((epi & 15) == EPI_CROSS) v =bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
-        if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
-        else C[m * ldc + n] = v;
-      }
-    }
-  }
+  store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
 template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
@@ -597,7 +614,7 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
     } else {
       i32x8 af[TM], bfr[TN];
@@ -608,7 +625,7 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(bfr[j], af[i], acc[i][j]);
     }
     // RAW for tile kt+1: this wave's loads for it are done once at most the
     // tiles issued after it are outstanding; every wave's, after the barrier.
@@ -623,29 +640,7 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
     }
   }
 
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + j * 16 + fr;
-    if (n >= N) continue;
-    const float bn = bias ? bias[n] : 0.f;
-    const float swn = sw ? sw[n] : 1.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r];
-        if (FP8) v *= swn * (sa ? sa[m] : 1.f);
-        v += bn;
-        if ((epi & 15) == EPI_RELU) v = fmaxf(v, 0.f);
-        else if ((epi & 15) == EPI_SIGMOID) v = sigmoidf(v);
-        else if ((epi & 15) == EPI_CROSS) v = bf2f(X0[m * ldx + n]) * v + bf2f(XL[m * ldx + n]);
-        if constexpr (sizeof(OutT) == 2) C[m * ldc + n] = f2bf(v);
-        else C[m * ldc + n] = v;
-      }
-    }
-  }
+  store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
 template <int BM, int BN, int WM_, int WN_, int STAGES, bool FP8, typename OutT>
@@ -688,6 +683,7 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     if (M <= 1024) variant = 8;
     else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 9;
     else if (blocks(128, 128) >= 512) variant = 2;
+    else if (blocks(128, 64) >= 512) variant = 10;  // 8192 x 512: 15.5 us vs 16.9 (64x64)
     else variant = 4;
   }
   if (variant == 2 && glds_ok) {

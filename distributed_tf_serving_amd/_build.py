@@ -37,8 +37,11 @@ NATIVE_SOURCES = [
     "wire/tensor_codec.cpp",
     "runtime/batcher.cpp",
     "runtime/thread_pool.cpp",
+    "runtime/arena.cpp",
 ]
-HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp"]
+HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp", "runtime/serving_loop.cpp",
+                    # shared with _native (the loop parses arenas / encodes responses itself)
+                    "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp"]
 
 
 def _torch_paths():
@@ -122,7 +125,8 @@ def build_hip(verbose=False, force=False) -> str:
     hdr = _headers_mtime()
     dev_flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-x", "hip", f"-I{CSRC}",
                  "-munsafe-fp-atomics", "-Wno-unused-result"]
-    host_flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__=1",
+    host_flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", f"-I{CSRC}",
+                  "-D__HIP_PLATFORM_AMD__=1",
                   "-DUSE_ROCM=1", "-DHIPBLAS_V2", "-I/opt/rocm/include", "-Wno-unused-result"] + \
                  [f"-I{p}" for p in tinc + _py_includes()] + _common_defs("_hip", abi)
     objs, jobs = [], []

@@ -240,10 +240,7 @@ class FanoutEngine:
         key = (B, slot)
         self.ex.prepare(B, slot)
         self._capture_ingress(B, slot)
-        if self._runner is None:
-            from ..ops import hip
-
-            self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
+        self.runner()
         send, back = self._send_buf(B, slot), self._back_buf(B, slot)
         if self.ingest == "arena":
             dst = self.dev_arena(slot)
@@ -318,6 +315,44 @@ class FanoutEngine:
                 torch.cuda.synchronize(self.dev)
         return all_ok
 
+    def runner(self):
+        """The native StepRunner of this engine's device (created on first use)."""
+        if self._runner is None:
+            from ..ops import hip
+
+            self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
+        return self._runner
+
+    def loop_slots(self, B: int):
+        """Per-slot launch descriptions for the native ServingLoop
+        (csrc/runtime/serving_loop.cpp): a local step graph, or a fan-out step."""
+        if not self.cuda or self.ingest != "arena":
+            raise RuntimeError("the native serving loop needs a GPU and arena ingest")
+        self.prepare(B)
+        out = []
+        rows = self.contrib_rows(B)
+        for s in range(self.ex.slots):
+            h_out = self.host_out(B, s)
+            if self._step_graphs_enabled():
+                self._capture_step(B, s)
+                out.append(dict(h2d_dst=self.dev_arena(s), graph_exec=self._step_graph[(B, s)].raw_cuda_graph_exec(),
+                                h_out=h_out))
+            elif self.native_fanout_active:
+                key = (B, s)
+                self.ex.prepare(B, s)
+                self._capture_ingress(B, s)
+                ing = self._ingress_graph.get(key)
+                out.append(dict(
+                    fanout=True, h2d_dst=self.dev_arena(s),
+                    ingress_exec=ing.raw_cuda_graph_exec() if ing is not None else 0,
+                    cin=self._cin, cout=self._cout, mode=0 if self.mode == "alltoall" else 1,
+                    send=self._send_buf(B, s), recv=self.ex.input_buffer(B, s),
+                    forward_exec=self.ex._graphs[key].raw_cuda_graph_exec(), scores=self.ex._out[key],
+                    back=self._back_buf(B, s), h_out=h_out, d2h_bytes=rows * 4))
+            else:
+                raise RuntimeError("no native step path for this engine (graphs disabled or fan-out fell back)")
+        return out
+
     def comm_error(self) -> Optional[str]:
         """Asynchronous RCCL error of the native communicators (failure detection)."""
         from .native_comm import check_comms
@@ -382,11 +417,7 @@ class FanoutEngine:
         if self.native_launch:
             # C++ StepRunner: SDMA H2D + hipGraphLaunch + events, no torch stream
             # bookkeeping in the loop (csrc/runtime/step_runner.cpp)
-            if self._runner is None:
-                from ..ops import hip
-
-                self._runner = hip().StepRunner(self.dev.index if self.dev.index is not None else 0, self.ex.slots)
-            self._runner.launch(slot, dst, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
+            self.runner().launch(slot, dst, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
             return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot),
                               t_submit=t0)
         cur = torch.cuda.current_stream(self.dev)

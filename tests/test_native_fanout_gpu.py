@@ -36,6 +36,46 @@ def test_rccl_comm_single_rank(cuda):
     assert c.aborted
 
 
+@pytest.mark.parametrize("mode", ["local", "alltoall", "scatter"])
+def test_native_serving_loop(cuda, mode):
+    """The C++ ServingLoop (parse -> H2D + step graph / fan-out -> encode) over a
+    ring of request arenas; the last step's scores match a local forward."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.ops import hip, native
+
+    cfg = ModelConfig(family="deepfm", vocab_size=50_000)
+    m = build_model(cfg, cuda)
+    F = cfg.num_fields
+    L = PackedLayout(F)
+    B, S, R = 1024, 4, 4
+    ex = ShardExecutor(m, L, [B], cuda, slots=S)
+    AL = ArenaLayout(F, max_rows=B)
+    eng = FanoutEngine(ex, DistContext(device=cuda), mode="alltoall" if mode == "local" else mode, ingest="arena",
+                       arena=AL, force_fanout=mode != "local")
+    loop = hip().ServingLoop(eng.runner(), dict(depth=S - 1, fields=F, max_rows=B, version=1), eng.loop_slots(B))
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=5)
+    inputs = []
+    for p in range(5):
+        ids, wts = synth.arrays(B)
+        ids, wts = torch.from_numpy(ids), torch.from_numpy(wts)
+        reqs = [native().encode_predict_request("DCN", "serving_default", None,
+                                                [("feat_ids", ids[i:i + B // R]), ("feat_wts", wts[i:i + B // R])],
+                                                True)
+                for i in range(0, B, B // R)]
+        ar = AL.alloc(pin=True)
+        loop.add_input(ar, AL.place(ar, reqs))
+        inputs.append((ids, wts))
+    n = 11
+    st = loop.run(n, True)
+    assert st["errors"] == 0 and st["requests"] == n * R and st["rows"] == n * B
+    assert st["response_bytes"] > n * B * 4 and len(st["latency_us"]) == n
+    last = n - 1
+    ids, wts = inputs[last % len(inputs)]
+    got = eng.host_out(B, last % S)[:B].clone()
+    want = m(ids.to(cuda), wts.to(cuda)).float().cpu()
+    assert (got - want).abs().max().item() < 1e-5
+
+
 @pytest.mark.parametrize("mode", ["alltoall", "scatter"])
 @pytest.mark.parametrize("ingest", ["packed", "arena"])
 def test_native_fanout_step_matches_local(cuda, mode, ingest):
