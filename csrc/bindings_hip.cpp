@@ -501,10 +501,15 @@ PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list s
                                d["forward_exec"].cast<uintptr_t>(), d["cout"].cast<dtfs::comm::RcclComm&>(),
                                d["scores"].cast<torch::Tensor>(), d["back"].cast<torch::Tensor>(), h_out,
                                d["d2h_bytes"].cast<int64_t>());
+      if (d.contains("forward_seq") && !d["forward_seq"].is_none())
+        s.fan.forward_seq = &d["forward_seq"].cast<dtfs::runtime::KernelSequence&>();
+      if (d.contains("ingress_seq") && !d["ingress_seq"].is_none())
+        s.fan.ingress_seq = &d["ingress_seq"].cast<dtfs::runtime::KernelSequence&>();
     } else {
       s.h2d_dst = dst.data_ptr();
-      s.graph = reinterpret_cast<hipGraphExec_t>(d["graph_exec"].cast<uintptr_t>());
-      TORCH_CHECK(s.graph != nullptr, "null step graph");
+      if (d.contains("seq") && !d["seq"].is_none()) s.seq = &d["seq"].cast<dtfs::runtime::KernelSequence&>();
+      if (d.contains("graph_exec")) s.graph = reinterpret_cast<hipGraphExec_t>(d["graph_exec"].cast<uintptr_t>());
+      TORCH_CHECK(s.graph != nullptr || s.seq != nullptr, "slot needs a step graph or kernel sequence");
     }
     ls.push_back(s);
   }
@@ -581,6 +586,23 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
+
+  py::class_<dtfs::runtime::KernelSequence>(m, "KernelSequence",
+                                            "A captured HIP graph replayed as direct kernel launches")
+      .def(py::init([](uintptr_t graph) {
+             TORCH_CHECK(graph != 0, "null hipGraph_t (capture with torch.cuda.CUDAGraph(keep_graph=True))");
+             return std::make_unique<dtfs::runtime::KernelSequence>(reinterpret_cast<hipGraph_t>(graph));
+           }),
+           py::arg("graph"))
+      .def(
+          "launch",
+          [](const dtfs::runtime::KernelSequence& s, uintptr_t stream) {
+            s.launch(stream ? reinterpret_cast<hipStream_t>(stream)
+                            : c10::hip::getCurrentHIPStream().stream());
+          },
+          py::arg("stream") = 0)
+      .def_property_readonly("size", &dtfs::runtime::KernelSequence::size)
+      .def("describe", &dtfs::runtime::KernelSequence::describe);
 
   py::class_<PyServingLoop>(m, "ServingLoop",
                             "Native per-rank serving loop: parse -> H2D + step graph (or fan-out) -> encode")

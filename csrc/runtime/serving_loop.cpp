@@ -25,7 +25,8 @@ ServingLoop::ServingLoop(StepRunner* runner, LoopConfig cfg, std::vector<LoopSlo
   if (int(slots_.size()) < cfg_.depth + 1) throw std::invalid_argument("need slots >= depth + 1");
   if (int(slots_.size()) > runner_->slots()) throw std::invalid_argument("more loop slots than runner slots");
   for (const auto& s : slots_) {
-    if (s.fanout ? (!s.fan.forward || !s.fan.cin || !s.fan.cout) : (!s.graph || !s.h2d_dst))
+    if (s.fanout ? (!(s.fan.forward || s.fan.forward_seq) || !s.fan.cin || !s.fan.cout)
+                 : (!(s.graph || s.seq) || !s.h2d_dst))
       throw std::invalid_argument("incomplete loop slot");
     if (!s.h_out) throw std::invalid_argument("loop slot without host scores");
   }
@@ -168,7 +169,8 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         f.h2d_bytes = nbytes;
         runner_->launch_fanout(slot, f);
       } else {
-        runner_->launch(slot, s.h2d_dst, in.arena, nbytes, s.graph);
+        if (s.seq) runner_->launch_seq(slot, s.h2d_dst, in.arena, nbytes, s.seq);
+        else runner_->launch(slot, s.h2d_dst, in.arena, nbytes, s.graph);
       }
       launch_us += now_us() - t0;
       {

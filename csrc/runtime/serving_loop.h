@@ -31,6 +31,7 @@ namespace runtime {
 struct LoopSlot {
   void* h2d_dst = nullptr;           // device arena of the slot (local launch)
   hipGraphExec_t graph = nullptr;    // local: unpack + forward + scores -> h_out
+  const KernelSequence* seq = nullptr;  // local, preferred: the same step as direct launches
   bool fanout = false;
   FanoutStep fan;                    // fan-out: everything but h2d_src / h2d_bytes
   const float* h_out = nullptr;      // pinned scores of the slot

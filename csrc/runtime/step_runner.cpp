@@ -50,7 +50,8 @@ void StepRunner::ensure_fanout_streams() {
 
 void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
-  if (!s.cin || !s.cout || !s.forward) throw std::invalid_argument("fan-out step needs both communicators and a graph");
+  if (!s.cin || !s.cout || !(s.forward || s.forward_seq))
+    throw std::invalid_argument("fan-out step needs both communicators and a forward");
   ck(hipSetDevice(device_), "hipSetDevice");
   ensure_fanout_streams();
   // copy: WAR on the slot's buffers (its previous step is entirely done)
@@ -60,13 +61,15 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
   // ingress: unpack + row exchange, off the compute stream
   ck(hipStreamWaitEvent(ingress_, h2d_done_[slot], 0), "hipStreamWaitEvent(ingress)");
-  if (s.ingress) ck(hipGraphLaunch(s.ingress, ingress_), "hipGraphLaunch(ingress)");
+  if (s.ingress_seq) s.ingress_seq->launch(ingress_);
+  else if (s.ingress) ck(hipGraphLaunch(s.ingress, ingress_), "hipGraphLaunch(ingress)");
   if (s.mode == 0) s.cin->alltoall(s.send, s.recv, s.in_bytes, ingress_);
   else s.cin->scatter(s.send, s.recv, s.in_bytes, 0, ingress_);
   ck(hipEventRecord(in_done_[slot], ingress_), "hipEventRecord(in)");
   // compute: the forward graph
   ck(hipStreamWaitEvent(compute_, in_done_[slot], 0), "hipStreamWaitEvent(compute)");
-  ck(hipGraphLaunch(s.forward, compute_), "hipGraphLaunch(forward)");
+  if (s.forward_seq) s.forward_seq->launch(compute_);
+  else ck(hipGraphLaunch(s.forward, compute_), "hipGraphLaunch(forward)");
   ck(hipEventRecord(fwd_done_[slot], compute_), "hipEventRecord(fwd)");
   // egress: score exchange + D2H (SDMA)
   ck(hipStreamWaitEvent(egress_, fwd_done_[slot], 0), "hipStreamWaitEvent(egress)");
@@ -88,6 +91,19 @@ void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hi
   ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
   ck(hipStreamWaitEvent(compute_, h2d_done_[slot], 0), "hipStreamWaitEvent(compute)");
   ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
+  ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
+  used_[slot] = true;
+}
+
+void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq) {
+  if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
+  if (!seq) throw std::invalid_argument("null kernel sequence");
+  ck(hipSetDevice(device_), "hipSetDevice");
+  if (used_[slot]) ck(hipStreamWaitEvent(copy_, done_[slot], 0), "hipStreamWaitEvent(copy)");
+  if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, copy_), "hipMemcpyAsync(H2D)");
+  ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
+  ck(hipStreamWaitEvent(compute_, h2d_done_[slot], 0), "hipStreamWaitEvent(compute)");
+  seq->launch(compute_);
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
   used_[slot] = true;
 }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../comm/rccl_comm.h"
+#include "kernel_seq.h"
 
 namespace dtfs {
 namespace runtime {
@@ -45,6 +46,9 @@ struct FanoutStep {
   size_t out_bytes = 0;  // per peer
   void* h_out = nullptr;  // pinned host
   size_t d2h_bytes = 0;
+  // optional: replay these instead of launching the graphs (same kernels)
+  const KernelSequence* ingress_seq = nullptr;
+  const KernelSequence* forward_seq = nullptr;
 };
 
 class StepRunner {
@@ -58,6 +62,8 @@ class StepRunner {
   // launch graph_exec on the compute stream once the copy has landed. The H2D
   // waits only for the previous step of the same slot to have consumed dst.
   void launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph);
+  // Same, replaying the step as direct kernel launches (no graph-launch gap).
+  void launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq);
   // Enqueue one fan-out step (see FanoutStep).
   void launch_fanout(int slot, const FanoutStep& s);
   // Block until the slot's last step has finished (scores are on the host).

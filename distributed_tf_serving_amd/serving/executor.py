@@ -83,9 +83,12 @@ class ShardExecutor:
             pool = self._pools.get(slot)
             if pool is None:
                 pool = self._pools[slot] = torch.cuda.graph_pool_handle()
-            g = torch.cuda.CUDAGraph()
+            # keep the hipGraph_t: the native loop replays its nodes as direct
+            # launches (runtime/kernel_seq.cpp); replay() uses the instantiated exec
+            g = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(g, pool=pool):
                 out = self._forward(buf)
+            g.instantiate()
             self._graphs[key] = g
             self._out[key] = out
 
