@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import threading
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -60,7 +61,11 @@ class ShardError(RuntimeError):
 class FanoutClient:
     def __init__(self, backends: Sequence[Backend], spec: RequestSpec = RequestSpec(), pool_threads: int = 16,
                  full_async: bool = True, sort_scores: bool = True, timeout_s: Optional[float] = None,
-                 executor: Optional[cf.Executor] = None):
+                 executor: Optional[cf.Executor] = None, failover: bool = False, cooldown_s: float = 5.0):
+        """``failover``: a shard whose backend fails (error or ``timeout_s``)
+        is re-split over the backends still healthy and retried, and the failed
+        backend is skipped by new requests for ``cooldown_s`` (degraded mode;
+        the reference abandons the request, DCNClient.java:185-188)."""
         if not backends:
             raise ValueError("need at least one backend")
         self.backends = list(backends)
@@ -68,9 +73,26 @@ class FanoutClient:
         self.full_async = full_async
         self.sort_scores = sort_scores
         self.timeout_s = timeout_s
+        self.failover = failover
+        self.cooldown_s = cooldown_s
+        self._down_until = [0.0] * len(self.backends)
+        self._health_lock = threading.Lock()
+        self.failovers = 0
         self._own_pool = executor is None
         self.pool = executor or cf.ThreadPoolExecutor(max_workers=pool_threads, thread_name_prefix="dtfs-fanout")
         self.nat = native()
+
+    # -- health -----------------------------------------------------------------
+    def healthy(self) -> List[int]:
+        """Backends not in cool-down (all of them if every one is down)."""
+        now = time.monotonic()
+        with self._health_lock:
+            alive = [i for i, t in enumerate(self._down_until) if t <= now]
+        return alive or list(range(len(self.backends)))
+
+    def mark_down(self, i: int) -> None:
+        with self._health_lock:
+            self._down_until[i] = time.monotonic() + self.cooldown_s
 
     # -- encoding -------------------------------------------------------------
     def encode(self, ids: torch.Tensor, wts: torch.Tensor) -> bytes:
@@ -86,19 +108,42 @@ class FanoutClient:
         return torch.tensor(list(t.float_val), dtype=torch.float32)
 
     # -- fan-out ----------------------------------------------------------------
-    def _shard_call(self, i: int, ids: torch.Tensor, wts: torch.Tensor) -> torch.Tensor:
+    def _call(self, i: int, ids: torch.Tensor, wts: torch.Tensor) -> torch.Tensor:
         be = self.backends[i]
         try:
             return self.decode_scores(be.predict(self.encode(ids, wts), self.timeout_s))
         except BaseException as e:  # noqa: BLE001
             raise ShardError(i, be.name, e) from e
 
+    def _shard_call(self, i: int, ids: torch.Tensor, wts: torch.Tensor) -> torch.Tensor:
+        try:
+            return self._call(i, ids, wts)
+        except ShardError:
+            if not self.failover:
+                raise
+            self.mark_down(i)
+            alive = [j for j in self.healthy() if j != i and self._down_until[j] <= time.monotonic()]
+            if not alive:
+                raise
+            self.failovers += 1
+            # degraded mode: re-split this shard over the surviving backends
+            outs = []
+            for j, (s, k) in zip(alive, split_rows(ids.shape[0], len(alive))):
+                if k:
+                    try:
+                        outs.append(self._call(j, ids[s:s + k], wts[s:s + k]))
+                    except ShardError:
+                        self.mark_down(j)
+                        raise
+            return torch.cat(outs)
+
     def predict_async(self, ids, wts) -> cf.Future:
         """Returns a Future[FanoutResult] (CompletableFuture analogue)."""
         ids = torch.as_tensor(ids, dtype=torch.int64)
         wts = torch.as_tensor(wts, dtype=torch.float32)
         n = ids.shape[0]
-        parts = [(i, s, k) for i, (s, k) in enumerate(split_rows(n, len(self.backends))) if k > 0]
+        targets = self.healthy() if self.failover else list(range(len(self.backends)))
+        parts = [(targets[i], s, k) for i, (s, k) in enumerate(split_rows(n, len(targets))) if k > 0]
         futs = {self.pool.submit(self._shard_call, i, ids[s:s + k], wts[s:s + k]): i for i, s, k in parts}
         out: cf.Future = cf.Future()
         if not futs:

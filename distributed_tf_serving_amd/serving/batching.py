@@ -43,11 +43,18 @@ class WorkItem:
 
 class BatchingScheduler:
     def __init__(self, engine, max_batch_rows: int = 8192, batch_timeout_us: int = 200,
-                 max_queued_rows: int = 1 << 22, depth: int = 2, name: str = "model"):
+                 max_queued_rows: int = 1 << 22, depth: int = 2, name: str = "model",
+                 fanout_world: int = 1, on_launch: Optional[Callable[[int, int], None]] = None):
+        """``fanout_world`` > 1: this is the front door of a scatter fan-out
+        (parallel/fanout.py): a step of bucket B carries up to world x B rows,
+        split across the ranks. ``on_launch(B, slot)`` runs right before each
+        step is launched (serving/cluster.py tells the follower ranks)."""
         self.eng = engine
         self.ex = engine.ex
         self.layout = engine.layout
-        self.max_rows = min(int(max_batch_rows), self.ex.max_rows)
+        self.world = max(1, int(fanout_world))
+        self.on_launch = on_launch
+        self.max_rows = min(int(max_batch_rows), self.ex.max_rows) * self.world
         self.depth = max(1, min(depth, self.ex.slots - 1)) if self.ex.slots > 1 else 1
         self.batcher = native().DynamicBatcher(self.max_rows, int(batch_timeout_us), int(max_queued_rows))
         self._items: Dict[int, WorkItem] = {}
@@ -136,7 +143,7 @@ class BatchingScheduler:
 
     def _launch(self, batch):
         rows = batch.rows
-        B = self.ex.bucket_for(rows)
+        B = self.ex.bucket_for(-(-rows // self.world))  # rows per GPU
         slot = self._slot
         self._slot = (self._slot + 1) % self.ex.slots
         buf = self.eng.host_in(B, slot)
@@ -158,9 +165,12 @@ class BatchingScheduler:
                 continue
             plan.append((w, off))
             off += w.rows
-        if off < B:  # padding rows: valid ids, zero weights (their scores are dropped)
-            ids_v[off:B].zero_()
-            wts_v[off:B].zero_()
+        total = B * self.world
+        if off < total:  # padding rows: valid ids, zero weights (their scores are dropped)
+            ids_v[off:total].zero_()
+            wts_v[off:total].zero_()
+        if self.on_launch is not None:
+            self.on_launch(B, slot)
         handle = self.eng.launch(B, slot)
         return handle, plan, off
 

@@ -38,18 +38,35 @@ def pick_device(pref: str = "auto") -> torch.device:
     return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
 
 
-def build_servable(cfg: Config, device=None, version: Optional[int] = None, slots: int = 3) -> Servable:
+def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistContext] = None,
+                 mode: str = "local") -> FanoutEngine:
+    """Model + executor + fan-out engine of one rank, every bucket prepared
+    (HIP graphs captured). With ``ctx`` of a multi-rank job, DLRM tables are
+    sharded over the ranks (parallel/embedding_sharding.py)."""
+    from ..parallel.embedding_sharding import build_parallel_model
+
     sc = cfg.serving
-    dev = torch.device(device) if device is not None else pick_device(sc.device)
-    model = build_model(cfg.model, dev)
+    dev = torch.device(device) if device is not None else (ctx.device if ctx is not None else pick_device(sc.device))
+    ctx = ctx or DistContext(device=dev)
+    model = build_parallel_model(cfg.model, dev, ctx)
     layout = PackedLayout(cfg.model.num_fields)
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=sc.use_graphs, slots=slots)
-    eng = FanoutEngine(ex, DistContext(device=dev), mode="local")
+    eng = FanoutEngine(ex, ctx, mode=mode)
     for B in buckets:
         eng.prepare(B)
+    return eng
+
+
+def build_servable(cfg: Config, device=None, version: Optional[int] = None, slots: int = 3,
+                   engine: Optional[FanoutEngine] = None, on_launch=None) -> Servable:
+    sc = cfg.serving
+    eng = engine or build_engine(cfg, device, slots)
+    model = eng.ex.model
+    world = eng.world if eng.mode == "scatter" else 1
     sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
-                              max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name)
+                              max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name,
+                              fanout_world=world, on_launch=on_launch)
     sig = model.signature()
     sigs = {sc.signature_name: Signature(inputs=sig["inputs"], outputs=sig["outputs"], method_name=sig["method_name"])}
     return Servable(name=sc.model_name, version=sc.version if version is None else version, model=model,
@@ -92,12 +109,18 @@ def main(argv=None):
     ap.add_argument("--device", default=None)
     ap.add_argument("--model-name", default=None)
     ap.add_argument("--grpc-workers", type=int, default=32)
+    ap.add_argument("--inject-fault", default="",
+                    help="failure testing, e.g. 'after:100,kind:error' (serving/faults.py)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     cfg = load_preset(a.preset)
     if a.model_name:
         cfg.serving.model_name = a.model_name
     srv = ModelServer(cfg, device=a.device)
+    if a.inject_fault:
+        from .faults import FaultInjector, FaultSpec, FaultyService
+
+        srv.service = FaultyService(srv.service, FaultInjector(FaultSpec.parse(a.inject_fault)))
     port = srv.start_grpc(a.port, a.host, a.grpc_workers)
     print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())

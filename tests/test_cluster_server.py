@@ -1,0 +1,96 @@
+"""Multi-rank model server over gloo (CPU): rank 0 is the PredictionService
+front door + dynamic batcher, ranks > 0 follow the step control channel; every
+batch is scattered over all ranks and gathered back (reference topology:
+DCNClient.java:146-164, moved inside the node)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    from distributed_tf_serving_amd.config import Config, ModelConfig
+
+    cfg = Config()
+    cfg.model = ModelConfig(family="deepfm", vocab_size=5000, embed_dim=16, mlp_dims=(32, 16))
+    cfg.serving.device = "cpu"
+    cfg.serving.max_batch_rows = 64
+    cfg.serving.allowed_batch_sizes = (16, 64)
+    cfg.serving.batch_timeout_us = 500
+    return cfg
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown
+    from distributed_tf_serving_amd.serving.cluster import ClusterServer
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire.tensor import make_tensor_proto, to_ndarray
+
+    try:
+        ctx = init_from_env(device="cpu")
+        cfg = _cfg()
+        srv = ClusterServer(cfg, ctx)
+        if rank == 0:
+            ref = build_model(cfg.model)
+            rng = np.random.default_rng(3)
+            errs = []
+            for rows in (1, 7, 50, 64, 130):  # 130 > world x 64: split into several steps
+                ids = rng.integers(0, 1 << 40, size=(rows, 43), dtype=np.int64)
+                wts = rng.random((rows, 43), dtype=np.float32)
+                req = pb.PredictRequest()
+                req.model_spec.name = cfg.serving.model_name
+                req.model_spec.signature_name = "serving_default"
+                req.inputs["feat_ids"].CopyFrom(make_tensor_proto(ids))
+                req.inputs["feat_wts"].CopyFrom(make_tensor_proto(wts))
+                resp = srv.service.predict(req, timeout_s=60)
+                got = to_ndarray(resp.outputs["prediction_node"])
+                want = ref(torch.from_numpy(ids), torch.from_numpy(wts)).numpy()
+                errs.append(float(np.abs(got - want).max()))
+            stats = srv.registry.resolve(cfg.serving.model_name).scheduler.stats()
+            srv.stop()
+            q.put((rank, errs, stats["steps"]))
+        else:
+            n = srv.serve_follower()
+            srv.stop()
+            q.put((rank, None, n))
+        shutdown()
+    except Exception:  # pragma: no cover - surfaced by the assertion below
+        import traceback
+
+        q.put((rank, traceback.format_exc(), -1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cluster_server_scatter_gather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    res = {}
+    for _ in range(world):
+        r, payload, steps = q.get(timeout=300)
+        res[r] = (payload, steps)
+    [p.join(timeout=60) for p in procs]
+    errs, steps0 = res[0]
+    assert isinstance(errs, list), f"rank 0 failed: {errs}"
+    assert max(errs) < 1e-5, errs
+    for r in range(1, world):
+        assert res[r][1] == steps0, f"rank {r} followed {res[r][1]} steps, rank 0 ran {steps0}: {res[r][0]}"
