@@ -10,6 +10,7 @@
 #include "runtime/batcher.h"
 #include "runtime/arena.h"
 #include "runtime/thread_pool.h"
+#include "runtime/trace.h"
 #include "wire/tensor_codec.h"
 
 namespace py = pybind11;
@@ -538,4 +539,8 @@ PYBIND11_MODULE(_native, m) {
       .def("stats", &runtime::DynamicBatcher::stats);
 
   m.def("now_us", &runtime::now_us);
+  m.def("trace_enabled", &trace::enabled);
+  m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));
+  m.def("trace_pop", &trace::pop);
+  m.def("trace_mark", [](const std::string& s) { trace::mark(s.c_str()); }, py::arg("name"));
 }

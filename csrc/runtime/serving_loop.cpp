@@ -8,6 +8,7 @@
 #include <thread>
 
 #include "../wire/tensor_codec.h"
+#include "trace.h"
 
 namespace dtfs {
 namespace runtime {
@@ -80,6 +81,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         }
         const Input& in = inputs_[size_t(k % P)];
         const double t0 = now_us();
+        trace::Range tr("parse");
         ArenaBatch b = arena_build(in.arena, in.capacity, in.spans, cfg_.ids_key, cfg_.wts_key, cfg_.fields,
                                    cfg_.max_rows);
         const double t1 = now_us();
@@ -104,6 +106,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
           if (abort) return;
         }
         const double t0 = now_us();
+        trace::Range tr("encode");
         const ArenaBatch& b = parsed[size_t(j)];
         const LoopSlot& s = slots_[size_t(j % S)];
         int64_t bytes = 0, req = 0, rows = 0, errs = 0;
@@ -139,9 +142,11 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
   });
 
   double launch_us = 0, wait_us = 0;
+  const bool s_fanout_any = slots_[0].fanout;
   const double wall0 = now_us();
   auto finish = [&](int64_t j) {
     const double t0 = now_us();
+    trace::Range tr("gpu_wait");
     runner_->wait(int(j % S));
     const double t1 = now_us();
     wait_us += t1 - t0;
@@ -158,6 +163,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         if (abort) break;
       }
       const double t0 = now_us();
+      trace::Range tr(s_fanout_any ? "launch_fanout" : "launch");
       const Input& in = inputs_[size_t(k % P)];
       const ArenaBatch& b = parsed[size_t(k)];
       const int slot = int(k % S);

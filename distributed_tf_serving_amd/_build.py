@@ -38,11 +38,12 @@ NATIVE_SOURCES = [
     "runtime/batcher.cpp",
     "runtime/thread_pool.cpp",
     "runtime/arena.cpp",
+    "runtime/trace.cpp",
 ]
 HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp", "runtime/serving_loop.cpp",
                     "runtime/kernel_seq.cpp",
                     # shared with _native (the loop parses arenas / encodes responses itself)
-                    "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp"]
+                    "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp", "runtime/trace.cpp"]
 
 
 def _torch_paths():
