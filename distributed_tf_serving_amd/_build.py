@@ -97,14 +97,25 @@ def _py_includes():
     return [sysconfig.get_paths()["include"]]
 
 
-def build_native(verbose=False, force=False) -> str:
+SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+
+
+def build_native(verbose=False, force=False, sanitize=False) -> str:
+    """``sanitize``: ASan + UBSan host build of the native runtime (SURVEY.md
+    §5.2), into its own object dir. Run it with the sanitizer runtime
+    preloaded, e.g. ``scripts/sanitize_native.sh``; rebuild without the flag
+    afterwards (the instrumented .so replaces the normal one in-tree)."""
     tdir, tinc, tlib, abi = _torch_paths()
     out = os.path.join(PKG_DIR, "_native" + EXT_SUFFIX)
-    odir = os.path.join(BUILD, "native")
+    odir = os.path.join(BUILD, "native_asan" if sanitize else "native")
     os.makedirs(odir, exist_ok=True)
     hdr = _headers_mtime()
-    flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-fvisibility=hidden",
+    flags = ["-O1" if sanitize else "-O3", "-g" if sanitize else "-g0", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function", "-fvisibility=hidden",
              f"-I{CSRC}"] + [f"-I{p}" for p in tinc + _py_includes()] + _common_defs("_native", abi)
+    if sanitize:
+        flags += SANITIZE_FLAGS
+        force = True  # the output name is shared with the normal build
     objs, jobs = [], []
     for s in NATIVE_SOURCES:
         src = os.path.join(CSRC, s)
@@ -114,8 +125,8 @@ def build_native(verbose=False, force=False) -> str:
             jobs.append([CXX, *flags, "-c", src, "-o", obj])
     _compile_all(jobs, verbose)
     if force or jobs or not os.path.exists(out):
-        _run([CXX, "-shared", "-o", out, *objs, f"-L{tlib}", "-lc10", "-ltorch", "-ltorch_cpu",
-              "-ltorch_python", f"-Wl,-rpath,{tlib}"], verbose)
+        _run([CXX, "-shared", "-o", out, *objs, *(SANITIZE_FLAGS if sanitize else []), f"-L{tlib}", "-lc10",
+              "-ltorch", "-ltorch_cpu", "-ltorch_python", "-ldl", f"-Wl,-rpath,{tlib}"], verbose)
     return out
 
 
@@ -167,11 +178,14 @@ if __name__ == "__main__":
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--native-only", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="ASan+UBSan host build of _native (implies --native-only)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     if a.clean:
         clean()
         sys.exit(0)
-    print(build_native(a.verbose, a.force))
+    print(build_native(a.verbose, a.force or a.sanitize, sanitize=a.sanitize))
+    if a.sanitize:
+        sys.exit(0)
     if not a.native_only:
         print(build_hip(a.verbose, a.force))
