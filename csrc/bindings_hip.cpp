@@ -151,6 +151,56 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
   return {x, fm};
 }
 
+// K0+K1(+K2): the gather reads ids / weights straight from a device request
+// arena (csrc/runtime/arena.h) - no separate unpack kernel, no packed rows.
+std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor arena,
+                                       int64_t B, int64_t F, int64_t modulo, double bias, bool want_x, bool want_fm,
+                                       bool fm2, c10::optional<torch::Tensor> out_x) {
+  check_dev(table, "table");
+  check_dev(arena, "arena");
+  check_same_dev(table, arena, "arena");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
+  TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.is_contiguous() && arena.numel() > dtfs::kArenaPayloadOff,
+              "arena must be a contiguous uint8 device buffer");
+  const int64_t D = table.size(1), V = table.size(0);
+  TORCH_CHECK(D == 8 || D == 16 || D == 32 || D == 64 || D == 128, "embedding dim must be 8/16/32/64/128");
+  TORCH_CHECK(F >= 1 && F <= 64, "arena gather handles 1..64 fields");
+  TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]");
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
+  }
+  c10::DeviceGuard g(table.device());
+  torch::Tensor x, fm;
+  if (want_x) {
+    if (out_x) {
+      check_dev(*out_x, "out_x");
+      TORCH_CHECK(out_x->scalar_type() == torch::kBFloat16 && out_x->numel() == B * F * D, "out_x must be bf16 [B, F*D]");
+      x = *out_x;
+    } else {
+      x = torch::empty({B, F * D}, table.options());
+    }
+  }
+  if (want_fm) fm = torch::empty({B}, table.options().dtype(torch::kFloat32));
+  dtfs::EmbedArgs a;
+  a.table = table.data_ptr();
+  a.lin = lin ? lin->data_ptr<float>() : nullptr;
+  a.arena = arena.data_ptr();
+  a.ids64 = true;
+  a.B = int(B);
+  a.F = int(F);
+  a.D = int(D);
+  a.V = V;
+  a.modulo = modulo;
+  a.bias = float(bias);
+  a.out_x = want_x ? x.data_ptr() : nullptr;
+  a.x_ld = F * D;
+  a.out_fm = want_fm ? fm.data_ptr<float>() : nullptr;
+  a.fm2 = fm2 ? 1 : 0;
+  check_hip(dtfs::launch_embed(a, cur_stream(table)), "embed_arena");
+  return {x, fm};
+}
+
 // ---------------------------------------------------------------- K1b
 torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
                             c10::optional<torch::Tensor> psw, int64_t modulo, bool mean, bool out_bf16) {
@@ -527,6 +577,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("modulo_f") = py::none(), py::arg("offset_f") = py::none(), py::arg("bias") = 0.0,
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
         py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none());
+  m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
+        py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
+        py::arg("fm2") = false, py::arg("out_x") = py::none());
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
         py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
         py::arg("out_bf16") = false);

@@ -49,6 +49,49 @@ __device__ __forceinline__ int64_t hash_row(int64_t id, int64_t modulo) {
   return r < 0 ? r + modulo : r;
 }
 
+// Unaligned little-endian loads from byte-addressed buffers (protobuf
+// tensor_content has no alignment): aligned dword loads + v_alignbyte funnel
+// shifts instead of byte loads. Reads only the dwords the value overlaps.
+__device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const int sh = int(a & 3);
+  const uint32_t w0 = w[0], w1 = w[1];
+  const uint32_t w2 = sh ? w[2] : 0u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const int sh = int(a & 3);
+  const uint32_t w0 = w[0];
+  const uint32_t w1 = sh ? w[1] : 0u;
+  return __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// Request-arena header (csrc/runtime/arena.h): n_req @0, total_rows @8,
+// row_table_off @16 ({ids_off, wts_off} int32 per row, payload-relative).
+struct ArenaRow {
+  const uint8_t* ids;  // 8 * F bytes of int64 ids, or nullptr (padding row)
+  const uint8_t* wts;  // 4 * F bytes of fp32 weights
+};
+
+__device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payload_off, int64_t r) {
+  const int64_t total = *reinterpret_cast<const int64_t*>(arena + 8);
+  ArenaRow out{nullptr, nullptr};
+  if (r < total) {
+    const uint8_t* payload = arena + payload_off;
+    const int64_t rt = *reinterpret_cast<const int64_t*>(arena + 16);
+    const int2 o = reinterpret_cast<const int2*>(payload + rt)[r];
+    out.ids = payload + o.x;
+    out.wts = payload + o.y;
+  }
+  return out;
+}
+
 // Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so give each XCD a contiguous run of tiles so

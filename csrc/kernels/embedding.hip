@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) pack_ids_kernel(const IdT* __restrict__ i
 //           + 0.5 * sum_d ((sum_f e)^2 - sum_f e^2)  (second order, if fm2)
 // ids / wts may be strided row views (ids_ld / wts_ld elements per row), so a
 // packed request row [ids int64 x F | wts fp32 x F | pad] is read in place.
-template <int D, typename IdT>
+template <int D, typename IdT, bool ARENA>
 __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
   constexpr int LPR = D / 8;          // lanes per table row (16 B each)
   constexpr int FPI = kWave / LPR;    // fields per wave-wide load
@@ -45,6 +45,8 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (b >= a.B) return;
+  ArenaRow arow{nullptr, nullptr};
+  if constexpr (ARENA) arow = arena_row(static_cast<const uint8_t*>(a.arena), kArenaPayloadOff, b);
   const int sub = lane / LPR;         // which field of the instruction group
   const int dl = (lane % LPR) * 8;    // first dim this lane owns
 
@@ -59,7 +61,15 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
     int64_t row = 0;
     float w = 0.f;
     if (fl < F) {
-      const int64_t id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
+      int64_t id;
+      float w_in;
+      if constexpr (ARENA) {  // padding rows (no request): id 0, weight 0 -> zero contribution
+        id = arow.ids ? int64_t(load_u64_unaligned(arow.ids + 8 * fl)) : 0;
+        w_in = arow.ids ? __uint_as_float(load_u32_unaligned(arow.wts + 4 * fl)) : 0.f;
+      } else {
+        id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
+        w_in = a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f;
+      }
       const int64_t m = a.modulo_f ? a.modulo_f[fl] : a.modulo;
       int64_t g = hash_row(id, m);
       bool own = true;
@@ -70,7 +80,7 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
       }
       row = (a.offset_f ? a.offset_f[fl] : 0) + g;
       row = row < 0 ? 0 : (row >= a.V ? a.V - 1 : row);  // memory safety whatever the tables say
-      w = own ? (a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f) : 0.f;
+      w = own ? w_in : 0.f;
       if (a.lin) first += a.lin[row] * w;
     }
     const int nf = min(kWave, F - fbase);
@@ -199,8 +209,9 @@ template <int D>
 static void embed_dispatch(const EmbedArgs& a, hipStream_t st) {
   const int rows_per_block = 4;
   dim3 grid((a.B + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
-  if (a.ids64) hipLaunchKernelGGL((embed_kernel<D, int64_t>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((embed_kernel<D, int32_t>), grid, block, 0, st, a);
+  if (a.arena) hipLaunchKernelGGL((embed_kernel<D, int64_t, true>), grid, block, 0, st, a);
+  else if (a.ids64) hipLaunchKernelGGL((embed_kernel<D, int64_t, false>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((embed_kernel<D, int32_t, false>), grid, block, 0, st, a);
 }
 
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st) {

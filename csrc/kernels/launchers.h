@@ -31,6 +31,10 @@ struct EmbedArgs {
   // (the partial embeddings are summed across ranks by a reduce-scatter)
   const int64_t* shard_lo_f = nullptr;
   const int64_t* shard_n_f = nullptr;
+  // request arena (csrc/runtime/arena.h): when set, row b's ids / weights are
+  // read straight from the raw request bytes (ids / wts above are unused) -
+  // the embedding gather doubles as the ingest unpack
+  const void* arena = nullptr;
   float bias = 0.f;
   void* out_x = nullptr;           // bf16 [B, x_ld]
   int64_t x_ld = 0;

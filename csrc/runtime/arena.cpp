@@ -1,6 +1,7 @@
 #include "arena.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <stdexcept>
 
@@ -134,11 +135,24 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
     // request itself is answered with the error
     if (!errs[k].empty()) out.errors[jobs[k].req] = errs[k];
   }
+  // per-row offset table: {ids_off, wts_off} int32 (payload-relative)
+  const int64_t rt = (std::max(end, scratch) + 63) & ~int64_t(63);
+  if (rt + row * 8 > cap) throw std::invalid_argument("arena too small for the row table");
+  if (rt + row * 8 > int64_t(INT32_MAX)) throw std::invalid_argument("arena payload exceeds 2 GiB");
+  int32_t* tab = reinterpret_cast<int32_t*>(payload + rt);
+  for (int64_t d = 0; d < nd; ++d) {
+    const int64_t io = desc[4 * d + 0], wo = desc[4 * d + 1], rows = desc[4 * d + 2], r0 = desc[4 * d + 3];
+    for (int64_t r = 0; r < rows; ++r) {
+      tab[2 * (r0 + r) + 0] = int32_t(io + r * 8 * fields);
+      tab[2 * (r0 + r) + 1] = int32_t(wo + r * 4 * fields);
+    }
+  }
   *reinterpret_cast<int32_t*>(base) = int32_t(nd);
   *reinterpret_cast<int64_t*>(base + 8) = row;
+  *reinterpret_cast<int64_t*>(base + 16) = rt;
   out.total_rows = row;
   out.n_valid = nd;
-  out.used_bytes = kArenaPayloadOff + std::max(end, scratch);
+  out.used_bytes = kArenaPayloadOff + rt + row * 8;
   return out;
 }
 

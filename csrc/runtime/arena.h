@@ -1,10 +1,11 @@
 // Request arena: the host side of zero-copy ingest (serving/arena.py,
 // csrc/kernels/ingest.hip share this layout).
 //
-//   [0]   int32 n_req      [8] int64 total_rows
+//   [0]   int32 n_req      [8] int64 total_rows      [16] int64 row_table_off
 //   [64]  n_req x {ids_off, wts_off, rows, dst_row} int64 (offsets into payload)
 //   [kArenaPayloadOff] payload: serialized PredictRequests (+ scratch for
-//                      host-decoded typed fields)
+//                      host-decoded typed fields), then at row_table_off a
+//                      {ids_off, wts_off} int32 pair per candidate row
 //
 // The host parses only protobuf framing and writes descriptors; raw
 // tensor_content payloads are referenced in place and the GPU gathers the

@@ -58,6 +58,9 @@ KernelSequence::KernelSequence(hipGraph_t graph) {
     } else if (t == hipGraphNodeTypeMemcpy) {
       op.kind = 1;
       ck(hipGraphMemcpyNodeGetParams(nodes[i], &op.mc), "hipGraphMemcpyNodeGetParams");
+      const hipMemcpy3DParms& c = op.mc;
+      if (c.srcArray || c.dstArray || c.extent.height > 1 || c.extent.depth > 1 || !c.srcPtr.ptr || !c.dstPtr.ptr)
+        throw std::runtime_error("unsupported memcpy node (not a plain 1-D copy)");
     } else if (t == hipGraphNodeTypeMemset) {
       op.kind = 2;
       ck(hipGraphMemsetNodeGetParams(nodes[i], &op.ms), "hipGraphMemsetNodeGetParams");
@@ -78,7 +81,11 @@ void KernelSequence::launch(hipStream_t st) const {
       ck(hipLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st),
          "hipLaunchKernel");
     } else if (op.kind == 1) {
-      ck(hipMemcpy3DAsync(&op.mc, st), "hipMemcpy3DAsync");
+      // a captured 1-D hipMemcpyAsync (checked at construction)
+      const hipMemcpy3DParms& c = op.mc;
+      const char* src = static_cast<const char*>(c.srcPtr.ptr) + c.srcPos.x;
+      char* dst = static_cast<char*>(c.dstPtr.ptr) + c.dstPos.x;
+      ck(hipMemcpyAsync(dst, src, c.extent.width, c.kind, st), "hipMemcpyAsync");
     } else {
       const hipMemsetParams& m = op.ms;
       if (m.elementSize == 1) ck(hipMemsetD8Async(hipDeviceptr_t(m.dst), uint8_t(m.value), m.width, st), "memset");

@@ -78,9 +78,21 @@ class CTRModel(nn.Module):
     def _forward(self, ids, wts, out=None):  # pragma: no cover - abstract
         raise NotImplementedError
 
+    # families whose only use of ids / weights is the first embedding gather
+    # can read them straight from a request arena (ops.ArenaRows)
+    supports_arena = False
+
+    @torch.no_grad()
+    def forward_arena(self, arena: torch.Tensor, B: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """CTR [B] for the first B candidate rows of a (device) request arena."""
+        if not self.supports_arena:
+            raise NotImplementedError(f"{self.family} reads dense features; unpack the arena first")
+        return self._forward(ops.ArenaRows(arena, int(B), self.cfg.num_fields), None, out)
+
 
 class WideDeep(CTRModel):
     family = "wdl"
+    supports_arena = True
 
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__(cfg, device)
@@ -101,6 +113,7 @@ class WideDeep(CTRModel):
 
 class DeepFM(CTRModel):
     family = "deepfm"
+    supports_arena = True
 
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__(cfg, device)
@@ -123,6 +136,7 @@ class DCN(CTRModel):
     """Deep & Cross Network (v1) - the reference's served model name."""
 
     family = "dcn"
+    supports_arena = True
 
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__(cfg, device)
@@ -150,6 +164,7 @@ class DCNv2(CTRModel):
     """DCN-v2: full-rank (or low-rank) matrix cross layers; optional fp8 towers."""
 
     family = "dcn_v2"
+    supports_arena = True
 
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__(cfg, device)

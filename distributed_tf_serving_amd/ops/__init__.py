@@ -16,6 +16,7 @@ Op inventory: K0 ``pack_ids``, K1 ``embed``, K1b
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Optional, Tuple
 
 import torch
@@ -51,6 +52,30 @@ def pack_ids(ids: torch.Tensor, modulo: int = 0, modulo_f=None, offset_f=None) -
     return _hash_rows(ids, modulo, modulo_f, offset_f).to(torch.int32)
 
 
+@dataclass(frozen=True)
+class ArenaRows:
+    """Candidate rows still inside a request arena (serving/arena.py): passed
+    as ``ids`` to :func:`embed`, the gather reads each row's ids and weights
+    from the raw request bytes (K0 fused into K1)."""
+
+    arena: torch.Tensor  # uint8 arena (device for the kernel, host for the reference)
+    B: int
+    F: int
+
+    @property
+    def shape(self):
+        return (self.B, self.F)
+
+
+def _arena_unpack_host(rows: "ArenaRows") -> Tuple[torch.Tensor, torch.Tensor]:
+    from ..serving.packing import PackedLayout
+
+    L = PackedLayout(rows.F)
+    packed = L.alloc(rows.B)
+    native().arena_unpack_cpu(rows.arena.cpu().contiguous(), packed, rows.F)
+    return L.ids(packed), L.wts(packed)
+
+
 # ------------------------------------------------------------------ K1 (+K2)
 def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = None,
           lin: Optional[torch.Tensor] = None, modulo: int = 0, modulo_f=None, offset_f=None,
@@ -65,7 +90,19 @@ def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = 
     ``shard_lo_f``/``shard_n_f`` (row-wise sharded tables): field f's table
     here holds global rows [lo, lo + n) at ``offset_f[f]``; ids hashing
     elsewhere contribute zeros.
+
+    ``ids`` may be :class:`ArenaRows` (then ``wts`` is None): rows come from
+    the raw request bytes of a request arena.
     """
+    if isinstance(ids, ArenaRows):
+        if modulo_f is not None or shard_lo_f is not None:
+            raise ValueError("arena rows support the shared-table gather only")
+        if ids.arena.is_cuda:
+            m = int(modulo) if modulo > 0 else table.shape[0]
+            x, fm = hip().embed_arena(table, lin, ids.arena, int(ids.B), int(ids.F), m, float(bias), want_x,
+                                      want_fm, fm2, out_x)
+            return (x if want_x else None), (fm if want_fm else None)
+        ids, wts = _arena_unpack_host(ids)
     if ids.is_cuda:
         if modulo_f is None and modulo <= 0:
             modulo = table.shape[0]

@@ -26,6 +26,7 @@ exchange; graph-friendly).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, Optional, Tuple
@@ -344,7 +345,10 @@ class FanoutEngine:
                 return None
             k = id(g)
             if k not in self._seqs:
-                self._seqs[k] = hip().KernelSequence(g.raw_cuda_graph())
+                try:
+                    self._seqs[k] = hip().KernelSequence(g.raw_cuda_graph())
+                except RuntimeError:  # a node type the sequence cannot replay: keep the graph
+                    self._seqs[k] = None
             return self._seqs[k]
 
         out = []
@@ -406,11 +410,17 @@ class FanoutEngine:
         buf = self.ex.input_buffer(B, slot)
         arena_dev = self.dev_arena(slot) if self.ingest == "arena" else None
 
+        fused_ingest = (arena_dev is not None and getattr(self.ex.model, "supports_arena", False)
+                        and os.environ.get("DTFS_ARENA_UNPACK", "0") != "1")
+
         def body():
-            if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows
-                self._unpack(arena_dev, buf)
             # the head kernel writes the scores straight into pinned host memory
             # (no D2H copy node, which a graph would run as a blit kernel)
+            if fused_ingest:  # K0 fused into K1: the gather reads the request bytes
+                self.ex.model.forward_arena(arena_dev, B, out=h_out[:B])
+                return
+            if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows
+                self._unpack(arena_dev, buf)
             self.ex._forward(buf, out=h_out[:B])
 
         side = torch.cuda.Stream(self.dev)

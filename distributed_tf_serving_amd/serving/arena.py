@@ -9,8 +9,11 @@ step's HIP graph. Requests that are not raw ``tensor_content`` int64/fp32 are
 decoded on the host into arena scratch space in raw form, so the GPU side is
 uniform.
 
-Layout (shared with csrc): header (n_req int32 @0, total_rows int64 @8),
-descriptors {ids_off, wts_off, rows, dst_row} int64 @64, payload @ARENA_PAYLOAD_OFF.
+Layout (shared with csrc): header (n_req int32 @0, total_rows int64 @8,
+row_table_off int64 @16), descriptors {ids_off, wts_off, rows, dst_row} int64
+@64, payload @ARENA_PAYLOAD_OFF; after the last request (and any scratch) a row
+table {ids_off, wts_off} int32 per candidate row, so a GPU thread finds its
+row's features with one load instead of a search over the descriptors.
 """
 from __future__ import annotations
 
@@ -35,8 +38,9 @@ class ArenaLayout:
     @property
     def capacity(self) -> int:
         # serialized rows (varints can reach ~14 B/feature) + host-decoded scratch (12 B/feature)
-        per_row = 28 * self.fields
-        return self.payload_off + self.max_rows * per_row + self.max_requests * 1024
+        # + the per-row offset table (8 B/row)
+        per_row = 28 * self.fields + 8
+        return self.payload_off + self.max_rows * per_row + self.max_requests * 1024 + 128
 
     def alloc(self, device="cpu", pin: bool = False) -> torch.Tensor:
         return torch.zeros(self.capacity, dtype=torch.uint8, device=device, pin_memory=pin)

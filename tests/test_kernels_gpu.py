@@ -308,3 +308,29 @@ def test_unpack_arena_gpu_matches_cpu(cuda):
     got.fill_(-1)
     ops.hip().unpack_arena(ar.to(cuda), got, 43)
     assert torch.equal(got.cpu(), ref)  # rows past total_rows are zeroed too
+
+
+@pytest.mark.parametrize("family", ["deepfm", "wdl", "dcn", "dcn_v2"])
+def test_forward_arena_matches_packed(cuda, family):
+    # K0 fused into K1: the gather reads ids / weights from the raw request bytes
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    cfg = ModelConfig(family=family, vocab_size=20_000)
+    m = build_model(cfg, cuda)
+    A, L = ArenaLayout(43, 2048), PackedLayout(43)
+    ar = A.alloc()
+    s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=9)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, True), (17, False), (200, True))]
+    ab = A.build(ar, A.place(ar, reqs))
+    B = 512  # > total_rows: padding rows must score like zero-weight rows
+    packed = A.unpack_cpu(ar, L.alloc(B))
+    want = m(L.ids(packed).to(cuda), L.wts(packed).to(cuda)).cpu()
+    got = m.forward_arena(ar.to(cuda), B).cpu()
+    _close(got[:ab.total_rows], want[:ab.total_rows], 0, 1e-6, f"{family} arena vs packed")
+    _close(got, want, 0, 1e-6, f"{family} arena padding rows")
+    out = torch.zeros(B, dtype=torch.float32).pin_memory()
+    m.forward_arena(ar.to(cuda), B, out=out)
+    torch.cuda.synchronize()
+    _close(out, want, 0, 1e-6, f"{family} arena into pinned host")
