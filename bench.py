@@ -84,7 +84,9 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="deepfm", choices=["deepfm", "dcn", "dcn_v2", "wdl", "dlrm"])
     ap.add_argument("--request-rows", type=int, default=512, help="candidates per client request (config batch)")
-    ap.add_argument("--requests-per-gpu", type=int, default=16, help="requests coalesced per GPU per step")
+    ap.add_argument("--requests-per-gpu", type=int, default=32,
+                    help="requests coalesced per GPU per step (32 x 512 = 16384 rows = the preset's max batch; "
+                         "16 halves p50 latency for ~20%% less throughput)")
     ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"])
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")

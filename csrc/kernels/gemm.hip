@@ -505,6 +505,230 @@ __global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// 256x256 "8-phase" GEMM (cdna_hip_programming.md §5, "The 256² 8-phase
+// template": staggered wave groups + counted vmcnt + raw barriers).
+//
+// 512 threads = 8 waves; wave (wr = wid>>2, wc = wid&3) owns rows 128wr..+128
+// and cols 64wc..+64 (acc[8][4] 16x16 tiles). K tile = 128 bytes per row
+// (64 bf16 / 128 fp8); two LDS buffers of 64 KiB (A 256 rows | B 256 rows).
+// Each K tile is computed in 4 phases, one C quadrant (4 x 2 tiles) each:
+//   p0 (qm0,qn0): ds_read A[qm0] + B[qn0]    p1 (qm0,qn1): ds_read B[qn1]
+//   p2 (qm1,qn1): ds_read A[qm1]             p3 (qm1,qn0): ds_read B[qn0]
+// and every phase stages one quarter of a later K tile with 2 LDS-DMA
+// instructions per thread. Quarters are sliced to match the reads - Aq = the
+// qm-th 64 rows of both row groups, Bq = the qn-th 32 columns of every wave's 64
+// - so each is last read early in its tile and can be restaged two phases later:
+//   p0: Aq1(t+1)   p1: Bq0(t+1)   p2: Aq0(t+2)   p3: Bq1(t+2)
+// One counted wait per K tile (p3, before its first barrier) retires t+1's
+// quarters and keeps t+2's two in flight, so the DMA never drains in the loop.
+// Phase = ds_read + stage | s_barrier | lgkmcnt(0) | 16 MFMA | s_barrier; waves
+// 4-7 run one barrier behind waves 0-3, so while one group issues its MFMAs
+// the other issues its LDS reads / DMA. Hazard rules (guide, "Read a staged
+// buffer one phase AFTER the wait that retires it"; WAR >= 2 phases after the
+// last read): quarter X of tile u staged at phase s, first read at phase r:
+//   Aq0: s=4u-6 r=4u   Bq1: s=4u-5 r=4u+1   Aq1: s=4u-4 r=4u+2   Bq0: s=4u-3 r=4u
+// all retired by the wait at phase 4u-1 (<= r-1); restaged >= 2 phases after
+// their last reads (Aq0 p0, Bq1 p1, Aq1 p2, Bq0 p3 of tile u-2 / u-1).
+template <bool FP8, typename OutT>
+__global__ void __launch_bounds__(512) gemm_8ph_kernel(
+    const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
+    const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
+    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int EB = FP8 ? 1 : 2;
+  constexpr int BUF = (BM + BN) * 128;  // 64 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;  // N-fastest
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane >> 3, ls = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // staging geometry: quarter q of A / B = 16 groups of 8 contiguous LDS rows;
+  // this wave stages groups wid and wid + 8 of every quarter
+  auto a_row = [&](int qm, int g) { return (g < 8 ? 0 : 128) + 64 * qm + 8 * (g & 7); };
+  auto b_row = [&](int qn, int g) { return 64 * (g >> 2) + 32 * qn + 8 * (g & 3); };
+  int64_t a_src[2][2], b_src[2][2];  // [quarter][j]
+  int a_dst[2][2], b_dst[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int g = wid + 8 * j;
+      const int ra = a_row(q, g), rb = b_row(q, g);
+      const int r_a = ra + lr, r_b = rb + lr;  // this lane's LDS row
+      a_src[q][j] = int64_t(min(m0 + r_a, M - 1)) * lda * EB + ((ls ^ ((r_a >> 1) & 7)) << 4);
+      b_src[q][j] = int64_t(min(n0 + r_b, N - 1)) * ldw * EB + ((ls ^ ((r_b >> 1) & 7)) << 4);
+      a_dst[q][j] = ra * 128;
+      b_dst[q][j] = BM * 128 + rb * 128;
+    }
+  auto stage_a = [&](int q, int kt) {
+    uint8_t* base = smem + (kt & 1) * BUF;
+    const int64_t kb = int64_t(kt) * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(A + a_src[q][j] + kb),
+                                       (__attribute__((address_space(3))) void*)(base + a_dst[q][j]), 16, 0, 0);
+  };
+  auto stage_b = [&](int q, int kt) {
+    uint8_t* base = smem + (kt & 1) * BUF;
+    const int64_t kb = int64_t(kt) * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(W + b_src[q][j] + kb),
+                                       (__attribute__((address_space(3))) void*)(base + b_dst[q][j]), 16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K * EB) / 128;
+  // prologue: tile 0 whole + tile 1's Aq0, Bq0 (staged at phases -2, -1 of the
+  // steady-state schedule below)
+  stage_a(0, 0);
+  stage_b(0, 0);
+  stage_b(1, 0);
+  stage_a(1, 0);
+  if (nk > 1) {
+    stage_a(0, 1);
+    stage_b(0, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+  asm volatile("" ::: "memory");
+
+  // fragments (bf16: [kk][tile] 8 x bf16, fp8: [tile] 32 x e4m3); both B
+  // column halves stay in registers for the whole K tile (no B re-read)
+  bf16x8 fa[2][4], fb[2][2][2];
+  i32x8 xa[4], xb[2][2];
+  auto read_a = [&](const uint8_t* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 128 * wr + 64 * qm + 16 * i + fr;
+      if constexpr (FP8) {
+        xa[i] = mx_frag(buf, row, fq);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
+      }
+    }
+  };
+  auto read_b = [&](const uint8_t* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 64 * wc + 32 * qn + 16 * j + fr;
+      if constexpr (FP8) {
+        xb[qn][j] = mx_frag(buf + BM * 128, row, fq);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          fb[qn][kk][j] = *reinterpret_cast<const bf16x8*>(buf + BM * 128 + swz(row, kk * 4 + fq));
+      }
+    }
+  };
+  // one quadrant: 4 x 2 output tiles (transposed MFMA: D = W . A^T, see store_acc_t)
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4& c = acc[4 * qm + i][2 * qn + j];
+        if constexpr (FP8) {
+          c = mx_mfma(xb[qn][j], xa[i], c);
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[kk][i], c, 0, 0, 0);
+        }
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // Wait so that the quarter staged 4 phases ago has landed: keep the
+  // quarters staged at phases phi-3..phi (2 DMA instructions each) in flight.
+  // Quarter staging phases: Aq0(u) 4u-6, Bq0(u) 4u-5, Bq1(u) 4u-4, Aq1(u) 4u-3
+  // (u < nk), so the last one is at 4nk-7.
+  const int last_stage = 4 * nk - 7;
+  auto wait_dma = [&](int phi) {
+    const int hi = min(phi, last_stage), lo = max(phi - 3, -2);
+    const int keep = hi >= lo ? hi - lo + 1 : 0;
+    if (keep >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (keep == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (keep == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (keep == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  // Phase = reads | stage one quarter | counted wait | barrier | MFMAs | barrier
+  //   p0: read A[qm0] B[qn0], stage Bq1(t+1)      p1: read B[qn1], stage Aq1(t+1)
+  //   p2: read A[qm1],        stage Aq0(t+2)      p3: (no reads), stage Bq0(t+2)
+  // WAR: each quarter is restaged >= 2 phases after its last read (Aq0, Bq0 at
+  // p0; Bq1 p1; Aq1 p2). RAW: a quarter staged at phase s is retired by the
+  // wait of phase s+4 and first read at phase >= s+5.
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* buf = smem + (t & 1) * BUF;
+    const bool s1 = t + 1 < nk, s2 = t + 2 < nk;
+    const int phi = 4 * t;
+    // p0
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (s1) stage_b(1, t + 1);
+    wait_dma(phi);
+    barrier();
+    mma(0, 0);
+    barrier();
+    // p1
+    read_b(buf, 1);
+    if (s1) stage_a(1, t + 1);
+    wait_dma(phi + 1);
+    barrier();
+    mma(0, 1);
+    barrier();
+    // p2
+    read_a(buf, 1);
+    if (s2) stage_a(0, t + 2);
+    wait_dma(phi + 2);
+    barrier();
+    mma(1, 1);
+    barrier();
+    // p3
+    if (s2) stage_b(0, t + 2);
+    wait_dma(phi + 3);
+    barrier();
+    mma(1, 0);
+    barrier();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
+
+  store_acc_t<FP8>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+}
+
+template <bool FP8, typename OutT>
+static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
+                       const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M,
+                       int N, int K, int epi, hipStream_t st) {
+  const int grid = ((M + 255) / 256) * ((N + 255) / 256);
+  hipLaunchKernelGGL((gemm_8ph_kernel<FP8, OutT>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(A), lda,
+                     static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi);
+}
+
+// ---------------------------------------------------------------------------
 // Deep-pipelined LDS-DMA variant: a STAGES-deep ring of K tiles with PREFETCH =
 // STAGES - 1 tiles in flight across barriers (cdna_hip_programming.md §5
 // "Pipelining across barriers"): every iteration issues the DMA for tile
@@ -678,11 +902,14 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     //  * >= 256 tiles of 256x256: the 256x256 8-wave tile (best at M = 16K)
     //  * >= 512 tiles of 128x128: 128x128 2-stage LDS-DMA, 2 blocks/CU
     //  * otherwise (narrow N, e.g. the 512/256-wide MLP layers): 64x64 LDS-DMA
-    // (256x256 only when N fills whole tiles: at N = 2752 its ragged last
-    // column panel made it 13 % slower than 128x128)
+    //  * >= 256 whole 256x256 tiles: the 8-phase kernel (16384x1024x2752: 81.8 us
+    //    vs 87.2 for 8-wave 128x128); a ragged last column panel (N = 2752)
+    //    or fewer tiles than CUs loses to 128x128
+    //  * >= 512 tiles of 128x128: 8 waves per block (2 per SIMD): 46.1 us vs
+    //    48.9 for 4 waves at 8192x1024x2752
     if (M <= 1024) variant = 8;
-    else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 9;
-    else if (blocks(128, 128) >= 512) variant = 2;
+    else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 17;
+    else if (blocks(128, 128) >= 512) variant = 14;
     else if (blocks(128, 64) >= 512) variant = 10;  // 8192 x 512: 15.5 us vs 16.9 (64x64)
     else variant = 4;
   }
@@ -729,6 +956,24 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
   }
   if (variant == 12 && glds_ok) {
     launch_glds<128, 64, 4, 1, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  // 256x256 8-phase (staggered wave groups, counted vmcnt)
+  if (variant == 17 && glds_ok) {
+    launch_8ph<FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  // 8-wave 128x128 tiles (2 waves per SIMD inside one block)
+  if (variant == 14 && glds_ok) {
+    launch_glds<128, 128, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 15 && glds_ok) {
+    launch_glds<128, 128, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    return;
+  }
+  if (variant == 16 && glds_ok) {
+    launch_glds<128, 256, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   if (variant == 13 && glds_ok) {

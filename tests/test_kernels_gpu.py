@@ -131,6 +131,33 @@ def test_gemm_bf16(cuda, M, N, K, act):
     _close(yb, ref, 1e-2, 1e-2, "gemm bf16 out")
 
 
+@pytest.mark.parametrize("variant", [14, 15, 17])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 128), (8192, 1024, 2752), (1000, 2752, 2752),
+                                   (16384, 512, 1024), (513, 1024, 192)])
+def test_gemm_variants_bf16(cuda, variant, M, N, K):
+    g = torch.Generator().manual_seed(M + 7 * N + K + variant)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    h = ops.hip()
+    for _ in range(3):  # repeat: a pipeline race shows up as run-to-run differences
+        y = h.gemm(x.to(cuda), W.to(cuda), b.to(cuda), 1, None, None, True, None, None, None, variant)
+        _close(y, ops.linear(x, W, b, "relu", out_f32=True), 2e-3, 2e-3, f"v{variant} {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (8192, 2752, 2752), (700, 1024, 2816)])
+def test_gemm_8phase_fp8(cuda, M, N, K):
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    xq, sx = ops.quant_rows_fp8(x.to(cuda), ops.FP8_K_PAD)
+    wq, sw = ops.quant_rows_fp8(W.to(cuda), ops.FP8_K_PAD)
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.hip().gemm(xq, wq, b.to(cuda), 1, None, None, True, sx, sw, None, 17)
+    ref = ops.linear_fp8(xq.cpu(), sx.cpu(), wq.cpu(), sw.cpu(), b, "relu", out_f32=True)
+    _close(y, ref, 2e-3, 2e-3, "fp8 8-phase")
+
+
 def test_gemm_layout_asymmetric(cuda):
     # A = I (padded), W asymmetric: C must equal W^T exactly (catches row/col swaps)
     M = N = 64
