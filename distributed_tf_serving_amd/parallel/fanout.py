@@ -107,6 +107,7 @@ class FanoutEngine:
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
+        self._native_disabled = False
         self.layout = executor.layout
         self.dev = executor.device
         self.cuda = self.dev.type == "cuda"
@@ -193,7 +194,8 @@ class FanoutEngine:
                 self.ex.prepare(B, s)
             if native:
                 self._capture_ingress(B, s)
-        self.native_fanout_active = native
+        # a failed self-check disables the native path for good (every rank agreed)
+        self.native_fanout_active = native and not self._native_disabled
 
     # -- native fan-out (world > 1) -----------------------------------------------
     def _native_fanout_enabled(self) -> bool:
@@ -314,6 +316,7 @@ class FanoutEngine:
             print(f"[fanout] rank {self.rank}: native fan-out self-check failed ({err or 'on another rank'}); "
                   f"using the torch.distributed path", file=sys.stderr, flush=True)
             self.native_fanout_active = False
+            self._native_disabled = True
             if self.cuda:
                 torch.cuda.synchronize(self.dev)
         return all_ok
