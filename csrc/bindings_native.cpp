@@ -529,7 +529,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("max_queued_rows") = 0)
       .def("submit", &runtime::DynamicBatcher::submit, py::arg("ticket"), py::arg("rows"),
            py::arg("deadline_us") = 0)
-      .def("next_batch", &runtime::DynamicBatcher::next_batch, py::arg("wait_us") = -1,
+      .def("next_batch", &runtime::DynamicBatcher::next_batch, py::arg("wait_us") = -1, py::arg("eager") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("close", &runtime::DynamicBatcher::close)
       .def_property_readonly("closed", &runtime::DynamicBatcher::closed)

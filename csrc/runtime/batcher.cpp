@@ -28,7 +28,7 @@ bool DynamicBatcher::submit(int64_t ticket, int64_t rows, int64_t deadline_us) {
   return true;
 }
 
-Batch DynamicBatcher::next_batch(int64_t wait_us) {
+Batch DynamicBatcher::next_batch(int64_t wait_us, bool eager) {
   Batch b;
   std::unique_lock<std::mutex> lk(mu_);
   const int64_t give_up = wait_us < 0 ? -1 : now_us() + wait_us;
@@ -44,7 +44,7 @@ Batch DynamicBatcher::next_batch(int64_t wait_us) {
     if (!q_.empty()) {
       const bool full = queued_rows_ >= max_batch_rows_;
       const int64_t ready_at = q_.front().enqueue_us + timeout_us_;
-      if (full || t >= ready_at || closed_) {
+      if (full || eager || t >= ready_at || closed_) {
         // Take whole requests until the next one would overflow the batch.
         while (!q_.empty()) {
           const BatchItem& it = q_.front();

@@ -58,7 +58,9 @@ class DynamicBatcher {
 
   // Blocks up to wait_us (<0: forever) for a batch. An empty batch with
   // closed=false means the wait timed out with nothing queued.
-  Batch next_batch(int64_t wait_us);
+  // eager=true: take whatever is queued as soon as anything is (the caller's
+  // device is idle, so waiting for the batch timeout only adds latency).
+  Batch next_batch(int64_t wait_us, bool eager = false);
 
   void close();
   bool closed() const;

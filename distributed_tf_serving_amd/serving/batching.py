@@ -54,6 +54,7 @@ class BatchingScheduler:
         self.layout = engine.layout
         self.world = max(1, int(fanout_world))
         self.on_launch = on_launch
+        self.eager_when_idle = True
         self.max_rows = min(int(max_batch_rows), self.ex.max_rows) * self.world
         self.depth = max(1, min(depth, self.ex.slots - 1)) if self.ex.slots > 1 else 1
         self.batcher = native().DynamicBatcher(self.max_rows, int(batch_timeout_us), int(max_queued_rows))
@@ -118,7 +119,9 @@ class BatchingScheduler:
     def _loop(self) -> None:
         inflight: Deque = collections.deque()
         while True:
-            batch = self.batcher.next_batch(0 if inflight else 50_000)
+            # idle device: dispatch whatever is queued right away (latency);
+            # steps in flight: accumulate up to the batch timeout (throughput)
+            batch = self.batcher.next_batch(0 if inflight else 50_000, self.eager_when_idle and not inflight)
             for it in batch.expired:
                 w = self._pop(it.ticket)
                 if w is not None:

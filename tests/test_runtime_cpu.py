@@ -32,6 +32,18 @@ def test_batcher_full_batch_and_order():
     assert b.next_batch(0).closed
 
 
+def test_batcher_eager_when_idle():
+    b = native().DynamicBatcher(100, 10_000_000, 0)  # 10 s batch timeout
+    b.submit(1, 10)
+    b.submit(2, 20)
+    assert b.next_batch(0).items == []  # not full, timeout far away
+    t = time.perf_counter()
+    batch = b.next_batch(0, True)  # idle device: take what is queued now
+    assert [i.ticket for i in batch.items] == [1, 2] and batch.rows == 30
+    assert time.perf_counter() - t < 0.5
+    b.close()
+
+
 def test_batcher_timeout_and_oversize():
     b = native().DynamicBatcher(64, 2000, 0)
     b.submit(1, 10)
