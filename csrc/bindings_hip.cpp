@@ -358,6 +358,30 @@ torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<
 }
 
 // ---------------------------------------------------------------- K4+K6 fused
+// Scores [M] fp32 of a fused head kernel: ``out`` (device or pinned host
+// memory, which the kernel then writes directly) or a new device tensor.
+float* score_out(const torch::Tensor& like, int64_t M, const c10::optional<torch::Tensor>& out, torch::Tensor& y) {
+  if (out) {
+    TORCH_CHECK(out->scalar_type() == torch::kFloat32 && out->numel() == M && out->is_contiguous(),
+                "out must be fp32 [M] contiguous");
+    TORCH_CHECK(out->is_cuda() || out->is_pinned(), "out must be on the device or pinned host memory");
+    y = *out;
+  } else {
+    y = torch::empty({M}, like.options().dtype(torch::kFloat32));
+  }
+  float* yp = y.data_ptr<float>();
+  if (!y.is_cuda()) {
+    // pinned host allocations are mapped at the same virtual address on ROCm;
+    // prefer the runtime's answer when it has one
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, yp, 0) == hipSuccess && dp)
+      yp = static_cast<float*>(dp);
+    else
+      (void)hipGetLastError();
+  }
+  return yp;
+}
+
 torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, int64_t act, torch::Tensor hw,
                         double hbias, c10::optional<torch::Tensor> extra, bool sigmoid,
                         c10::optional<torch::Tensor> out) {
@@ -381,25 +405,7 @@ torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, in
   }
   c10::DeviceGuard g(A.device());
   torch::Tensor y;
-  if (out) {
-    TORCH_CHECK(out->scalar_type() == torch::kFloat32 && out->numel() == M && out->is_contiguous(),
-                "out must be fp32 [M] contiguous");
-    // out may be pinned host memory (mapped): the kernel writes scores straight to the host
-    TORCH_CHECK(out->is_cuda() || out->is_pinned(), "out must be on the device or pinned host memory");
-    y = *out;
-  } else {
-    y = torch::empty({M}, A.options().dtype(torch::kFloat32));
-  }
-  float* yp = y.data_ptr<float>();
-  if (!y.is_cuda()) {
-    // pinned host allocations are mapped at the same virtual address on ROCm;
-    // prefer the runtime's answer when it has one
-    void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, yp, 0) == hipSuccess && dp)
-      yp = static_cast<float*>(dp);
-    else
-      (void)hipGetLastError();
-  }
+  float* yp = score_out(A, M, out, y);
   check_hip(dtfs::launch_gemm_head(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr<float>(), int(act),
                                    hw.data_ptr<float>(), float(hbias), extra ? extra->data_ptr<float>() : nullptr,
                                    sigmoid ? 2 : 0, yp, int(M), int(N), int(K), cur_stream(A)),
@@ -594,6 +600,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
+  m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
+        "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
+        "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);

@@ -42,6 +42,9 @@ struct EmbedArgs {
   int fm2 = 0;
 };
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
+// Pipelined K1 kernel geometry: resident-wave cap (0 = one row per wave) and
+// rows in flight per wave (1 or 2).
+void set_embed_wave_cap(int waves, int rows_in_flight = 1);
 
 // K0 ingest: request arena (header + descriptors + raw request bytes) -> packed
 // rows [B, W] int64 (serving/arena.py, csrc/runtime/arena.h share the layout).

@@ -121,8 +121,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", action="store_true")
+    ap.add_argument("--embed-study", action="store_true")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.embed_study:
+        for r in embed_study():
+            print(json.dumps(r), flush=True)
+        return
     if a.gemm_variants:
         narrow = (0, 10, 14, 17)
         wide = (0, 2, 9, 14, 17)
@@ -141,6 +146,40 @@ def main():
     for fam in (["deepfm"] if a.quick else ["deepfm", "dcn", "dcn_v2", "wdl", "dlrm"]):
         for B in ([512] if a.quick else [512, 4096]):
             print(json.dumps(bench_model(fam, B)), flush=True)
+
+
+
+def embed_study(B=16384, F=43, D=64, V=1_000_000, dev="cuda"):
+    """Where the K1 time goes at the bench shape: id distribution, x write, FM terms."""
+    from ..client.synth import SyntheticRequests
+
+    table = torch.randn(V, D, device=dev).to(torch.bfloat16)
+    lin = torch.randn(V, device=dev)
+    out = []
+    for dist in ("zipf", "uniform"):
+        ids_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist=dist).arrays(B)
+        ids = torch.from_numpy(ids_np).to(dev)
+        wts = torch.from_numpy(wts_np).to(dev)
+        for name, kw in (("x+fm", dict(want_x=True, want_fm=True, fm2=True, lin=lin)),
+                         ("fm_only", dict(want_x=False, want_fm=True, fm2=True, lin=lin)),
+                         ("x_only", dict(want_x=True, want_fm=False))):
+            us = _time(lambda: ops.embed(table, ids, wts, modulo=V, **kw))
+            out.append({"op": "embed_study", "dist": dist, "variant": name, "B": B, "us": round(us, 2)})
+    # resident-wave cap of the pipelined gather (rows per wave = B / cap; 0 = one row per wave)
+    ids_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf").arrays(B)
+    ids, wts = torch.from_numpy(ids_np).to(dev), torch.from_numpy(wts_np).to(dev)
+    h = ops.hip()
+    for cap in (0, 2048, 4096, 8192, 16384):
+        h.set_embed_wave_cap(cap)
+        us = _time(lambda: ops.embed(table, ids, wts, modulo=V, want_x=True, want_fm=True, fm2=True, lin=lin))
+        out.append({"op": "embed_study", "dist": "zipf", "variant": f"x+fm wave_cap={cap}", "B": B, "us": round(us, 2)})
+    h.set_embed_wave_cap(4096)
+    x = torch.empty(B, F * D, device=dev, dtype=torch.bfloat16)
+    us = _time(lambda: x.fill_(1.0))
+    out.append({"op": "embed_study", "variant": "fill_x (write-BW floor)", "us": round(us, 2),
+                "GBps": round(x.numel() * 2 / us / 1e3, 1)})
+    return out
+
 
 
 if __name__ == "__main__":

@@ -139,7 +139,10 @@ class MLP(nn.Module):
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """MLP then CTR head. On the GPU the last layer and the head run as one
         kernel (ops.linear_head) whenever its shape allows; it writes ``out``
-        (device or pinned host memory) directly."""
+        (device or pinned host memory) directly. (Fusing the last TWO layers
+        as well streams both weights through every 64-row block: measured
+        48.0 us vs 34.5 us for GEMM + fused head at 16384 rows on MI355X -
+        weight-load latency bound - so that fusion is not used.)"""
         for layer in self.layers[:-1]:
             x = layer(x)
         last = self.layers[-1]

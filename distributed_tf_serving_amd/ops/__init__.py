@@ -12,7 +12,7 @@ Every op dispatches on the device of its inputs:
 Op inventory: K0 ``pack_ids``, K1 ``embed``, K1b
 ``embedding_bag``, K2 FM (fused in ``embed``), K3 ``cross_v1``, K3b
 ``cross_v2`` / ``linear_fp8``, K4 ``linear``, K5 ``dot_interaction``, K6
-``head``, K7 ``sort_scores``.
+``head``, K4+K6 ``linear_head``, K7 ``sort_scores``.
 """
 from __future__ import annotations
 

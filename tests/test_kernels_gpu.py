@@ -361,3 +361,53 @@ def test_forward_arena_matches_packed(cuda, family):
     m.forward_arena(ar.to(cuda), B, out=out)
     torch.cuda.synchronize()
     _close(out, want, 0, 1e-6, f"{family} arena into pinned host")
+
+
+def test_deepfm_full_mlp_gpu_vs_cpu(cuda):
+    # the serving MLP 2752 -> 1024 -> 512 -> 256: 8-phase GEMM, narrow GEMM, fused last layer + head
+    cfg = ModelConfig(family="deepfm", vocab_size=20000)
+    m = build_model(cfg, "cpu")
+    mg = copy.deepcopy(m).to(cuda)
+    ids = torch.randint(0, 10**9, (300, 43))
+    wts = torch.rand(300, 43)
+    _close(mg(ids.to(cuda), wts.to(cuda)), m(ids, wts), 2e-2, 5e-3, "deepfm full MLP")
+
+
+@pytest.mark.parametrize("waves", [4, 8, 64])
+def test_embed_pipelined_rows_per_wave(cuda, waves):
+    # the pipelined gather with many rows per wave (next row's ids prefetched),
+    # extreme ids for the multiply-high modulo, and the arena-fed variant
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    V, D, F, B = 99991, 64, 43, 1000
+    g = torch.Generator().manual_seed(waves)
+    table = (torch.rand(V, D, generator=g) - 0.5).to(torch.bfloat16)
+    lin = torch.rand(V, generator=g) - 0.5
+    ids = torch.randint(-(1 << 62), 1 << 62, (B, F), generator=g)
+    ids[0, :4] = torch.tensor([-(1 << 63), (1 << 63) - 1, -1, 0])
+    wts = torch.rand(B, F, generator=g)
+    h = ops.hip()
+    try:
+        h.set_embed_wave_cap(waves)
+        x, fm = ops.embed(table.to(cuda), ids.to(cuda), wts.to(cuda), lin=lin.to(cuda), modulo=V, bias=0.1,
+                          want_x=True, want_fm=True, fm2=True)
+        xr, fmr = ops.embed(table, ids, wts, lin=lin, modulo=V, bias=0.1, want_x=True, want_fm=True, fm2=True)
+        _close(x, xr, 1e-2, 1e-3, "pipelined x")
+        _close(fm, fmr, 2e-3, 2e-3 * F, "pipelined fm")
+        A, L = ArenaLayout(F, 2048), PackedLayout(F)
+        ar = A.alloc()
+        s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=waves)
+        reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, True), (17, False), (200, True))]
+        ab = A.build(ar, A.place(ar, reqs))
+        packed = A.unpack_cpu(ar, L.alloc(512))
+        want = ops.embed(table.to(cuda), L.ids(packed).to(cuda), L.wts(packed).to(cuda), lin=lin.to(cuda), modulo=V,
+                         want_x=True, want_fm=True, fm2=True)
+        got = ops.embed(table.to(cuda), ops.ArenaRows(ar.to(cuda), 512, F), None, lin=lin.to(cuda), modulo=V,
+                        want_x=True, want_fm=True, fm2=True)
+        assert ab.total_rows == 470
+        _close(got[0], want[0], 0, 0, "arena x")
+        _close(got[1], want[1], 0, 1e-6, "arena fm")
+    finally:
+        h.set_embed_wave_cap(4096)

@@ -224,3 +224,4 @@ def test_step_pipeline_cpu():
     assert sorted(got) == list(range(9)) and len(pipe.latencies) == 9
     for k in range(9):
         assert torch.allclose(got[k], m(*data[k]), atol=1e-6)
+
