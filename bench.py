@@ -99,6 +99,7 @@ def parse_args():
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight = slots - 1)")
     ap.add_argument("--loop", default="native", choices=["native", "python"],
                     help="native: per-step host loop in C++ (csrc/runtime/serving_loop.cpp); python: StepPipeline")
     ap.add_argument("--force-fanout", action="store_true",
@@ -142,7 +143,7 @@ def main():
     F = cfg.num_fields
     layout = PackedLayout(F)
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
-    slots = 4
+    slots = a.slots
     ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
     rows_in_max = B * (ctx.world if a.mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
@@ -212,6 +213,7 @@ def main():
             return eng.launch(B, slot, nbytes=0)
         return eng.launch(B, slot)
 
+    score_check = {"steps": 0, "mismatched_steps": 0}
     use_native_loop = a.loop == "native" and dev.type == "cuda" and a.ingest == "arena" and not a.no_graphs
     if use_native_loop:
         try:
@@ -231,12 +233,21 @@ def main():
             nloop.add_input(ar, sp)
         lat: list = []
         phase = {"parse": 0.0, "launch": 0.0, "gpu_wait": 0.0, "encode": 0.0}
+        n_inputs = len(arenas)
 
         def run(n_steps: int, record: bool):
             st = nloop.run(n_steps, record)
             if st["errors"]:
                 raise RuntimeError(f"{st['errors']} requests failed in the native loop")
             if record:
+                # every replay of one input must give the same scores: a step
+                # whose scores the host read before they landed shows up here
+                ref = {}
+                for k, v in enumerate(st["score_sum"]):
+                    r = ref.setdefault(k % n_inputs, v)
+                    if abs(v - r) > 1e-6 * max(1.0, abs(r)):
+                        score_check["mismatched_steps"] += 1
+                score_check["steps"] += len(st["score_sum"])
                 lat.extend(x * 1e-6 for x in st["latency_us"])
                 for k_src, k_dst in (("parse_us", "parse"), ("launch_us", "launch"), ("wait_us", "gpu_wait"),
                                      ("encode_us", "encode")):
@@ -315,6 +326,9 @@ def main():
             "p50_request_ms": None if p50 is None else round(p50, 3),
             "p99_request_ms": None if p99 is None else round(p99, 3),
         }
+        if score_check["steps"]:
+            out["score_check"] = ("ok" if not score_check["mismatched_steps"] else
+                                  f"{score_check['mismatched_steps']}/{score_check['steps']} steps differ")
         print(json.dumps(out), flush=True)
         if a.json_extra:
             per = {k: round(v / a.steps * 1e6, 1) for k, v in phase.items()}

@@ -429,6 +429,14 @@ void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
             "unpack_arena");
 }
 
+void pull_host(torch::Tensor dst, torch::Tensor src, int64_t nbytes, int64_t blocks) {
+  check_dev(dst, "dst");
+  TORCH_CHECK(src.device().is_cpu() && src.is_pinned(), "src must be pinned host memory");
+  TORCH_CHECK(nbytes >= 0 && nbytes <= dst.nbytes() && nbytes <= src.nbytes(), "nbytes out of range");
+  c10::DeviceGuard g(dst.device());
+  check_hip(dtfs::launch_pull_host(dst.data_ptr(), src.data_ptr(), nbytes, int(blocks), cur_stream(dst)), "pull_host");
+}
+
 // ---------------------------------------------------------------- fp8
 std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x, int64_t k_pad) {
   check_dev(x, "x");
@@ -605,6 +613,7 @@ PYBIND11_MODULE(_hip, m) {
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
+  m.def("pull_host", &pull_host, py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("blocks") = 128);
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);
 
@@ -646,6 +655,7 @@ PYBIND11_MODULE(_hip, m) {
       .def("wait", &dtfs::runtime::StepRunner::wait, py::arg("slot"), py::call_guard<py::gil_scoped_release>())
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
+      .def_property_readonly("event_mode", &dtfs::runtime::StepRunner::event_mode)
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
 
@@ -689,6 +699,7 @@ PYBIND11_MODULE(_hip, m) {
             }
             py::dict d;
             d["latency_us"] = s.latency_us;
+            d["score_sum"] = s.score_sum;
             d["steps"] = s.steps;
             d["requests"] = s.requests;
             d["rows"] = s.rows;

@@ -13,6 +13,8 @@
 // dword loads + byte funnel shifts and written as aligned 8-byte words.
 // Models whose only consumer of ids / weights is the embedding gather skip
 // this kernel: the gather reads the arena rows itself (embedding.hip).
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -42,7 +44,56 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
   }
 }
 
+// H2D by the GPU itself: waves read the pinned request arena over PCIe and
+// write device memory. Replaces the SDMA copy of the serving step: an SDMA
+// command costs 10-17 us of idle engine time between back-to-back copies
+// (bench/copy_pipe.py), which on an H2D-paced step is lost throughput. The
+// waves are almost all waiting on PCIe reads, use no LDS and few VGPRs, so
+// they co-reside with the forward's kernels. U independent 16-B loads per
+// lane are in flight (the host side is uncached, coherent memory).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int U>
+__global__ void __launch_bounds__(256) pull_host_kernel(const u32x4_t* __restrict__ src, u32x4_t* __restrict__ dst,
+                                                        int64_t n16) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x * U;
+  for (int64_t base = int64_t(blockIdx.x) * blockDim.x * U + threadIdx.x; base < n16; base += stride) {
+    u32x4_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int64_t i = base + int64_t(j) * blockDim.x;
+      if (i < n16) v[j] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int64_t i = base + int64_t(j) * blockDim.x;
+      if (i < n16) dst[i] = v[j];
+    }
+  }
+}
+
+__global__ void pull_host_tail_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int n) {
+  if (int(threadIdx.x) < n) dst[threadIdx.x] = src[threadIdx.x];
+}
+
 }  // namespace kern
+
+hipError_t launch_pull_host(void* dst, const void* src, int64_t nbytes, int blocks, hipStream_t st) {
+  if (nbytes <= 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return hipErrorInvalidValue;
+  const int64_t n16 = nbytes / 16;
+  const int tail = int(nbytes - n16 * 16);
+  if (blocks <= 0) blocks = 128;
+  const int64_t need = (n16 + 256 * 4 - 1) / (256 * 4);
+  if (need < blocks) blocks = int(std::max<int64_t>(1, need));
+  if (n16 > 0)
+    hipLaunchKernelGGL(kern::pull_host_kernel<4>, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const kern::u32x4_t*>(src), static_cast<kern::u32x4_t*>(dst), n16);
+  if (tail)
+    hipLaunchKernelGGL(kern::pull_host_tail_kernel, dim3(1), dim3(64), 0, st,
+                       static_cast<const uint8_t*>(src) + n16 * 16, static_cast<uint8_t*>(dst) + n16 * 16, tail);
+  return hipGetLastError();
+}
 
 hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
                                hipStream_t st) {

@@ -1,5 +1,7 @@
 #include "kernel_seq.h"
 
+#include <hip/hip_ext.h>
+
 #include <map>
 #include <stdexcept>
 
@@ -75,11 +77,18 @@ KernelSequence::KernelSequence(hipGraph_t graph) {
   }
 }
 
-void KernelSequence::launch(hipStream_t st) const {
-  for (const Op& op : ops_) {
+void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind) const {
+  const bool bind_last = done && bind && !ops_.empty() && ops_.back().kind == 0;
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    const Op& op = ops_[i];
     if (op.kind == 0) {
-      ck(hipLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st),
-         "hipLaunchKernel");
+      if (bind_last && i + 1 == ops_.size())
+        ck(hipExtLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st,
+                              nullptr, done, 0),
+           "hipExtLaunchKernel");
+      else
+        ck(hipLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st),
+           "hipLaunchKernel");
     } else if (op.kind == 1) {
       // a captured 1-D hipMemcpyAsync (checked at construction)
       const hipMemcpy3DParms& c = op.mc;
@@ -94,6 +103,7 @@ void KernelSequence::launch(hipStream_t st) const {
       else ck(hipMemsetD32Async(hipDeviceptr_t(m.dst), int(m.value), m.width, st), "memset");
     }
   }
+  if (done && !bind_last) ck(hipEventRecord(done, st), "hipEventRecord");
 }
 
 std::string KernelSequence::describe() const {

@@ -24,8 +24,11 @@ namespace runtime {
 class KernelSequence {
  public:
   explicit KernelSequence(hipGraph_t graph);
-  // Enqueue every node on `st`, in dependency order.
-  void launch(hipStream_t st) const;
+  // Enqueue every node on `st`, in dependency order. With `done`, the event
+  // completes with the last node: bound to the last kernel's own dispatch
+  // (hipExtLaunchKernel stop event) when `bind` is set and the last node is a
+  // kernel, otherwise recorded after it.
+  void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false) const;
   int size() const { return int(ops_.size()); }
   std::string describe() const;
 

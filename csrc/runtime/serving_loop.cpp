@@ -48,7 +48,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
   if (n <= 0) return st;
 
   std::vector<ArenaBatch> parsed(static_cast<size_t>(n));
-  std::vector<double> t_start(size_t(n), 0.0), t_done(size_t(n), 0.0);
+  std::vector<double> t_start(size_t(n), 0.0), t_done(size_t(n), 0.0), sums(record ? size_t(n) : 0, 0.0);
   std::vector<char> parse_done(size_t(n), 0), finished(size_t(n), 0), encoded(size_t(n), 0);
   int64_t next_launch = 0;
   std::mutex mu;
@@ -110,11 +110,14 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         const ArenaBatch& b = parsed[size_t(j)];
         const LoopSlot& s = slots_[size_t(j % S)];
         int64_t bytes = 0, req = 0, rows = 0, errs = 0;
+        double sum = 0;
         for (size_t i = 0; i < b.rows.size(); ++i) {
           if (!b.errors[i].empty() || b.offsets[i] + b.rows[i] > s.h_out_len) {
             ++errs;
             continue;
           }
+          if (record)  // what the host actually read: checks the step-done signal's visibility
+            for (int64_t r = 0; r < b.rows[i]; ++r) sum += double(s.h_out[b.offsets[i] + r]);
           wire::TensorOut t;
           t.key = cfg_.output_key;
           t.dtype = wire::DT_FLOAT;
@@ -128,6 +131,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         }
         const double t1 = now_us();
         std::lock_guard<std::mutex> lk(mu);
+        if (record) sums[size_t(j)] = sum;
         encode_us += t1 - t0;
         resp_bytes += bytes;
         n_req += req;
@@ -207,6 +211,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
   if (record) {
     st.latency_us.resize(size_t(n));
     for (int64_t k = 0; k < n; ++k) st.latency_us[size_t(k)] = t_done[size_t(k)] - t_start[size_t(k)];
+    st.score_sum = std::move(sums);
   }
   return st;
 }

@@ -49,6 +49,7 @@ struct LoopConfig {
 
 struct LoopStats {
   std::vector<double> latency_us;  // per step: parse start -> scores on the host
+  std::vector<double> score_sum;   // per step: sum of the scores the encoder read (record only)
   int64_t steps = 0, requests = 0, rows = 0, errors = 0, response_bytes = 0;
   double parse_us = 0, launch_us = 0, wait_us = 0, encode_us = 0, wall_us = 0;
 };

@@ -1,7 +1,10 @@
 #include "step_runner.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace dtfs {
 namespace runtime {
@@ -12,28 +15,67 @@ void ck(hipError_t e, const char* what) {
 }
 }  // namespace
 
-StepRunner::StepRunner(int device, int slots) : device_(device) {
+// How the compute stream signals "step done" (bench/wait_gap.py: an event
+// recorded after the last kernel costs ~6 us of idle GPU before the next
+// kernel - the marker's system-scope release writes back and invalidates L2):
+//   0  hipEventRecord marker, default (system-scope) fence
+//   1  hipEventRecord marker, device-scope release
+//   2  event bound to the last kernel's dispatch (hipExtLaunchKernel stop event)
+//   3  2 + no system fence (the scores reach the host through uncached
+//      pinned-memory stores the kernel itself issued)
+// DTFS_EVENT_MODE overrides the default.
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  if (e && *e) return std::atoi(e);
+  return dflt;
+}
+static int event_mode() { return env_int("DTFS_EVENT_MODE", 0); }
+
+StepRunner::StepRunner(int device, int slots) : device_(device), event_mode_(event_mode()) {
   if (slots < 1) slots = 1;
   ck(hipSetDevice(device), "hipSetDevice");
   ck(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking), "hipStreamCreate(copy)");
+  // Consecutive steps' H2D copies alternate over DTFS_H2D_STREAMS copy
+  // streams (default 2). Back-to-back SDMA copies on one stream leave the
+  // engine idle ~15 us between commands; on two streams one copy's setup
+  // overlaps the other's transfer: 8.6 MB per step every ~153 us instead of
+  // ~173 us (bench/copy_pipe.py on MI355X). DTFS_COPY_WAIT=1 keeps the copy
+  // stream's WAR wait on the slot's previous step even when the host has
+  // already seen it complete.
+  // The extra streams are created on first use, so a fan-out runner (one copy
+  // stream) never holds them.
+  n_copy_ = std::max(1, std::min(4, env_int("DTFS_H2D_STREAMS", 2)));
+  copy_wait_always_ = env_int("DTFS_COPY_WAIT", 0) != 0;
+  spin_wait_ = env_int("DTFS_SPIN_WAIT", 0) != 0;
   ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
   h2d_done_.resize(slots);
   done_.resize(slots);
   used_.assign(slots, false);
+  observed_.reset(new std::atomic<bool>[size_t(slots)]);
+  for (int i = 0; i < slots; ++i) observed_[i].store(false);
   for (int i = 0; i < slots; ++i) {
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
-    ck(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming), "hipEventCreate");
+    ck(hipEventCreateWithFlags(&done_[i], done_flags()), "hipEventCreate");
   }
+}
+
+unsigned StepRunner::done_flags() const {
+  unsigned f = hipEventDisableTiming;
+  if (event_mode_ == 1) f |= hipEventReleaseToDevice;
+  if (event_mode_ == 3) f |= hipEventDisableSystemFence;
+  return f;
 }
 
 StepRunner::~StepRunner() {
   hipSetDevice(device_);
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamSynchronize(s);
+  for (hipStream_t s : extra_copy_) hipStreamSynchronize(s);
   for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_})
     for (auto e : *v) hipEventDestroy(e);
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamDestroy(s);
+  for (hipStream_t s : extra_copy_) hipStreamDestroy(s);
 }
 
 void StepRunner::ensure_fanout_streams() {
@@ -44,8 +86,32 @@ void StepRunner::ensure_fanout_streams() {
   fwd_done_.resize(done_.size());
   for (size_t i = 0; i < done_.size(); ++i) {
     ck(hipEventCreateWithFlags(&in_done_[i], hipEventDisableTiming), "hipEventCreate");
-    ck(hipEventCreateWithFlags(&fwd_done_[i], hipEventDisableTiming), "hipEventCreate");
+    ck(hipEventCreateWithFlags(&fwd_done_[i], done_flags()), "hipEventCreate");
   }
+}
+
+void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate) {
+  hipStream_t st = copy_;
+  if (alternate && n_copy_ > 1 && extra_copy_.empty()) {
+    for (int i = 1; i < n_copy_; ++i) {
+      hipStream_t x;
+      ck(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate(copy2)");
+      extra_copy_.push_back(x);
+    }
+  }
+  if (alternate && !extra_copy_.empty()) {
+    const size_t i = size_t(n_h2d_++ % uint64_t(extra_copy_.size() + 1));
+    if (i) st = extra_copy_[i - 1];
+  }
+  // WAR on the slot's buffers: its previous step must have finished reading
+  // them. Skipped when the host already saw that step complete (the serving
+  // loop waits for step k-3 before launching k).
+  if (used_[slot] && (copy_wait_always_ || !observed_[slot].load(std::memory_order_acquire)))
+    ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
+  if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D)");
+  ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
+  ck(hipStreamWaitEvent(consumer, h2d_done_[slot], 0), "hipStreamWaitEvent(h2d)");
+  observed_[slot].store(false, std::memory_order_release);
 }
 
 void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
@@ -54,13 +120,12 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
     throw std::invalid_argument("fan-out step needs both communicators and a forward");
   ck(hipSetDevice(device_), "hipSetDevice");
   ensure_fanout_streams();
-  // copy: WAR on the slot's buffers (its previous step is entirely done)
-  if (used_[slot]) ck(hipStreamWaitEvent(copy_, done_[slot], 0), "hipStreamWaitEvent(copy)");
-  if (s.h2d_bytes > 0)
-    ck(hipMemcpyAsync(s.h2d_dst, s.h2d_src, size_t(s.h2d_bytes), hipMemcpyHostToDevice, copy_), "hipMemcpyAsync(H2D)");
-  ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
-  // ingress: unpack + row exchange, off the compute stream
-  ck(hipStreamWaitEvent(ingress_, h2d_done_[slot], 0), "hipStreamWaitEvent(ingress)");
+  // copy (WAR on the slot's buffers), then ingress: unpack + row exchange, off
+  // the compute stream
+  // one copy stream here: with the ingress / egress streams a second one
+  // shares a hardware queue (GPU_MAX_HW_QUEUES = 4) and serialises the step
+  // (329 vs 187 us per step measured)
+  h2d(slot, s.h2d_dst, s.h2d_src, s.h2d_bytes, ingress_, false);
   if (s.ingress_seq) s.ingress_seq->launch(ingress_);
   else if (s.ingress) ck(hipGraphLaunch(s.ingress, ingress_), "hipGraphLaunch(ingress)");
   if (s.mode == 0) s.cin->alltoall(s.send, s.recv, s.in_bytes, ingress_);
@@ -68,9 +133,12 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   ck(hipEventRecord(in_done_[slot], ingress_), "hipEventRecord(in)");
   // compute: the forward graph
   ck(hipStreamWaitEvent(compute_, in_done_[slot], 0), "hipStreamWaitEvent(compute)");
-  if (s.forward_seq) s.forward_seq->launch(compute_);
-  else ck(hipGraphLaunch(s.forward, compute_), "hipGraphLaunch(forward)");
-  ck(hipEventRecord(fwd_done_[slot], compute_), "hipEventRecord(fwd)");
+  if (s.forward_seq) {
+    s.forward_seq->launch(compute_, fwd_done_[slot], event_mode_ >= 2);
+  } else {
+    ck(hipGraphLaunch(s.forward, compute_), "hipGraphLaunch(forward)");
+    ck(hipEventRecord(fwd_done_[slot], compute_), "hipEventRecord(fwd)");
+  }
   // egress: score exchange + D2H (SDMA)
   ck(hipStreamWaitEvent(egress_, fwd_done_[slot], 0), "hipStreamWaitEvent(egress)");
   if (s.mode == 0) s.cout->alltoall(s.scores, s.back, s.out_bytes, egress_);
@@ -84,12 +152,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
 void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
-  // WAR: the previous step on this slot must have finished reading dst (its
-  // graph ends after the forward), so wait for its completion event.
-  if (used_[slot]) ck(hipStreamWaitEvent(copy_, done_[slot], 0), "hipStreamWaitEvent(copy)");
-  if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, copy_), "hipMemcpyAsync(H2D)");
-  ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
-  ck(hipStreamWaitEvent(compute_, h2d_done_[slot], 0), "hipStreamWaitEvent(compute)");
+  h2d(slot, dst, src, nbytes, compute_, true);
   ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
   used_[slot] = true;
@@ -99,18 +162,27 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
-  if (used_[slot]) ck(hipStreamWaitEvent(copy_, done_[slot], 0), "hipStreamWaitEvent(copy)");
-  if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, copy_), "hipMemcpyAsync(H2D)");
-  ck(hipEventRecord(h2d_done_[slot], copy_), "hipEventRecord(h2d)");
-  ck(hipStreamWaitEvent(compute_, h2d_done_[slot], 0), "hipStreamWaitEvent(compute)");
-  seq->launch(compute_);
-  ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
+  h2d(slot, dst, src, nbytes, compute_, true);
+  seq->launch(compute_, done_[slot], event_mode_ >= 2);
   used_[slot] = true;
 }
 
 void StepRunner::wait(int slot) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
-  if (used_[slot]) ck(hipEventSynchronize(done_[slot]), "hipEventSynchronize");
+  if (used_[slot]) {
+    if (spin_wait_) {
+      // poll instead of blocking in the runtime (DTFS_SPIN_WAIT=1)
+      for (;;) {
+        const hipError_t e = hipEventQuery(done_[slot]);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) ck(e, "hipEventQuery");
+        std::this_thread::yield();
+      }
+    } else {
+      ck(hipEventSynchronize(done_[slot]), "hipEventSynchronize");
+    }
+  }
+  observed_[slot].store(true, std::memory_order_release);
 }
 
 bool StepRunner::query(int slot) {
@@ -118,6 +190,7 @@ bool StepRunner::query(int slot) {
   hipError_t e = hipEventQuery(done_[slot]);
   if (e == hipErrorNotReady) return false;
   ck(e, "hipEventQuery");
+  observed_[slot].store(true, std::memory_order_release);
   return true;
 }
 

@@ -12,7 +12,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "../comm/rccl_comm.h"
@@ -71,11 +73,23 @@ class StepRunner {
   bool query(int slot);
   // Microseconds between the slot's last H2D start and compute end (diagnostic).
   int slots() const { return int(done_.size()); }
+  int event_mode() const { return event_mode_; }
   hipStream_t compute_stream() const { return compute_; }
   hipStream_t copy_stream() const { return copy_; }
 
  private:
   int device_;
+  int event_mode_ = 0;
+  unsigned done_flags() const;
+  void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
+  int n_copy_ = 1;
+  bool copy_wait_always_ = false;
+  bool spin_wait_ = false;
+  std::vector<hipStream_t> extra_copy_;  // more H2D streams, used round-robin with copy_
+  uint64_t n_h2d_ = 0;
+  // host saw the slot's last step complete (set by wait/query, possibly from
+  // another thread than the launcher)
+  std::unique_ptr<std::atomic<bool>[]> observed_;
   void ensure_fanout_streams();
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;

@@ -69,6 +69,11 @@ def test_native_serving_loop(cuda, mode):
     st = loop.run(n, True)
     assert st["errors"] == 0 and st["requests"] == n * R and st["rows"] == n * B
     assert st["response_bytes"] > n * B * 4 and len(st["latency_us"]) == n
+    # every step's scores as the encoder read them: replays of one input agree
+    sums = st["score_sum"]
+    assert len(sums) == n
+    for k in range(len(inputs), n):
+        assert abs(sums[k] - sums[k - len(inputs)]) <= 1e-6 * max(1.0, abs(sums[k])), (k, sums)
     last = n - 1
     ids, wts = inputs[last % len(inputs)]
     got = eng.host_out(B, last % S)[:B].clone()
