@@ -429,6 +429,14 @@ void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
             "unpack_arena");
 }
 
+void arena_varint_decode(torch::Tensor arena, int64_t blocks) {
+  check_dev(arena, "arena");
+  TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.numel() > dtfs::kArenaPayloadOff, "arena: uint8 [cap]");
+  c10::DeviceGuard g(arena.device());
+  // chunk offsets come from the validated host build of this arena
+  check_hip(dtfs::launch_arena_varint(arena.data_ptr(), int(blocks), cur_stream(arena)), "arena_varint_decode");
+}
+
 void pull_host(torch::Tensor dst, torch::Tensor src, int64_t nbytes, int64_t blocks) {
   check_dev(dst, "dst");
   TORCH_CHECK(src.device().is_cpu() && src.is_pinned(), "src must be pinned host memory");
@@ -539,6 +547,7 @@ PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list s
   c.depth = cfg.contains("depth") ? cfg["depth"].cast<int>() : 3;
   c.fields = cfg["fields"].cast<int64_t>();
   c.max_rows = cfg["max_rows"].cast<int64_t>();
+  if (cfg.contains("varint_chunks")) c.varint_chunks = cfg["varint_chunks"].cast<int64_t>();
   if (cfg.contains("ids_key")) c.ids_key = cfg["ids_key"].cast<std::string>();
   if (cfg.contains("wts_key")) c.wts_key = cfg["wts_key"].cast<std::string>();
   if (cfg.contains("model_name")) c.model_name = cfg["model_name"].cast<std::string>();
@@ -613,6 +622,7 @@ PYBIND11_MODULE(_hip, m) {
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
+  m.def("arena_varint_decode", &arena_varint_decode, py::arg("arena"), py::arg("blocks") = 256);
   m.def("pull_host", &pull_host, py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("blocks") = 128);
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);

@@ -301,11 +301,13 @@ std::vector<std::pair<int64_t, int64_t>> arena_place(torch::Tensor arena, const 
 }
 
 ArenaBatch arena_build(torch::Tensor arena, const std::vector<std::pair<int64_t, int64_t>>& spans,
-                       const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows) {
+                       const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows,
+                       int64_t varint_chunks) {
   check_arena(arena);
   py::gil_scoped_release nogil;
   try {
-    return runtime::arena_build(arena.data_ptr<uint8_t>(), arena.numel(), spans, ids_key, wts_key, fields, max_rows);
+    return runtime::arena_build(arena.data_ptr<uint8_t>(), arena.numel(), spans, ids_key, wts_key, fields, max_rows,
+                                varint_chunks);
   } catch (const std::invalid_argument& e) {
     py::gil_scoped_acquire g;
     throw py::value_error(e.what());
@@ -451,12 +453,16 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("total_rows", &ArenaBatch::total_rows)
       .def_readonly("used_bytes", &ArenaBatch::used_bytes)
       .def_readonly("n_valid", &ArenaBatch::n_valid)
-      .def_readonly("n_decoded", &ArenaBatch::n_decoded);
+      .def_readonly("n_decoded", &ArenaBatch::n_decoded)
+      .def_readonly("n_gpu_varint", &ArenaBatch::n_gpu_varint);
   m.attr("ARENA_PAYLOAD_OFF") = kArenaPayloadOff;
   m.attr("ARENA_MAX_REQUESTS") = kArenaMaxRequests;
   m.def("arena_place", &arena_place, py::arg("arena"), py::arg("requests"), py::arg("start") = 0);
   m.def("arena_build", &arena_build, py::arg("arena"), py::arg("spans"), py::arg("ids_key") = "feat_ids",
-        py::arg("wts_key") = "feat_wts", py::arg("fields") = 43, py::arg("max_rows") = int64_t(1) << 40);
+        py::arg("wts_key") = "feat_wts", py::arg("fields") = 43, py::arg("max_rows") = int64_t(1) << 40,
+        py::arg("varint_chunks") = 0);
+  m.def("arena_varint_capacity", &runtime::arena_varint_capacity, py::arg("max_rows"), py::arg("fields"),
+        py::arg("max_requests") = runtime::kArenaMaxRequests);
   m.def("arena_unpack_cpu", &arena_unpack_cpu, py::arg("arena"), py::arg("packed"), py::arg("fields"));
 
   m.def("parse_batch", &parse_batch, py::arg("requests"), py::arg("ids_key") = "feat_ids",

@@ -76,7 +76,108 @@ __global__ void pull_host_tail_kernel(const uint8_t* __restrict__ src, uint8_t* 
   if (int(threadIdx.x) < n) dst[threadIdx.x] = src[threadIdx.x];
 }
 
+// Packed varint int64_val ids -> int64, on the GPU (csrc/runtime/arena.h,
+// "VarintChunk"). One block per 4096-byte chunk of a request's varint run,
+// 16 bytes per lane: a lane finds the terminator bytes (MSB clear) in its
+// bytes, a block scan of their counts plus the chunk's first index (from the
+// host, which counted terminators to validate the value count) gives each
+// varint's index, and the lane holding a terminator decodes that varint by
+// walking back over its continuation bytes (<= 9, possibly in the previous
+// lane's or chunk's bytes). Blocks loop over chunks (grid is fixed at graph
+// capture; the chunk count is read from the arena header).
+struct VarintChunkDev {
+  int64_t src_off, dst_off;
+  int32_t len, first_idx, n_values, blob_lo;
+};
+
+__global__ void __launch_bounds__(256) arena_varint_kernel(uint8_t* __restrict__ arena) {
+  // chunk bytes staged in LDS behind a 16-byte prefix (a varint is at most 10
+  // bytes, so a lane's first varint starts within the previous 16 bytes)
+  __shared__ __attribute__((aligned(16))) uint32_t buf[(16 + 4096) / 4];
+  __shared__ int wave_tot[4];
+  const int n_chunks = *reinterpret_cast<const int32_t*>(arena + 32);
+  uint8_t* payload = arena + kArenaPayloadOff;
+  const VarintChunkDev* tab =
+      reinterpret_cast<const VarintChunkDev*>(payload + *reinterpret_cast<const int64_t*>(arena + 24));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const VarintChunkDev ch = tab[c];
+    const uint8_t* src = payload + ch.src_off;
+    int64_t* dst = reinterpret_cast<int64_t*>(payload + ch.dst_off);
+    const int len = min(ch.len, 4096);
+    // stage [src - 16, src + 4096) with aligned dword loads + funnel shifts;
+    // bytes before the run read as terminators, past the chunk as continuations
+    for (int d = threadIdx.x; d < (16 + 4096) / 4; d += 256) {
+      const int k0 = 4 * d - 16;
+      uint32_t v = load_u32_unaligned(src + k0);
+      if (k0 < -ch.blob_lo || k0 + 4 > len) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + j;
+          const uint32_t fill = k < -ch.blob_lo ? 0u : (k >= len ? 0x80u : ((v >> (8 * j)) & 0xffu));
+          v = (v & ~(0xffu << (8 * j))) | (fill << (8 * j));
+        }
+      }
+      buf[d] = v;
+    }
+    __syncthreads();
+    const int lo = threadIdx.x * 16;
+    const uint4 pw = *reinterpret_cast<const uint4*>(buf + lo / 4);      // the 16 bytes before mine
+    const uint4 mw = *reinterpret_cast<const uint4*>(buf + lo / 4 + 4);  // my 16 bytes
+    const uint32_t pv[4] = {pw.x, pw.y, pw.z, pw.w}, mv[4] = {mw.x, mw.y, mw.z, mw.w};
+    unsigned term = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) term |= unsigned(((mv[j >> 2] >> (8 * (j & 3) + 7)) & 1u) == 0) << j;
+    // block exclusive scan of the terminator counts
+    const int cnt = __popc(term);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wave_tot[wid] = incl;
+    __syncthreads();
+    int idx = ch.first_idx + incl - cnt;
+    for (int q = 0; q < wid; ++q) idx += wave_tot[q];
+    // forward scan in registers: the partial varint entering my bytes comes
+    // from the previous 16, then every terminator emits one value
+    uint64_t acc = 0;
+    int sh = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t x = (pv[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      if (x & 0x80u) {
+        if (sh < 64) acc |= uint64_t(x & 0x7fu) << sh;
+        sh += 7;
+      } else {
+        acc = 0;
+        sh = 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t x = (mv[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      if (sh < 64) acc |= uint64_t(x & 0x7fu) << sh;
+      sh += 7;
+      if (!(x & 0x80u)) {
+        if (idx < ch.n_values) dst[idx] = int64_t(acc);
+        ++idx;
+        acc = 0;
+        sh = 0;
+      }
+    }
+    __syncthreads();  // buf / wave_tot are rewritten by the next chunk
+  }
+}
+
 }  // namespace kern
+
+hipError_t launch_arena_varint(void* arena, int blocks, hipStream_t st) {
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kern::arena_varint_kernel, dim3(blocks), dim3(256), 0, st, static_cast<uint8_t*>(arena));
+  return hipGetLastError();
+}
 
 hipError_t launch_pull_host(void* dst, const void* src, int64_t nbytes, int blocks, hipStream_t st) {
   if (nbytes <= 0) return hipSuccess;

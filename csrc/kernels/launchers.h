@@ -52,6 +52,9 @@ constexpr int kArenaPayloadOff = 64 + 32 * 1024;  // descriptors: up to 1024 req
 constexpr int kArenaMaxRequests = 1024;
 hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
                                hipStream_t st);
+// Packed varint ids of a built arena -> its device-only int64 id region
+// (csrc/runtime/arena.h VarintChunk); blocks loop over the chunk table.
+hipError_t launch_arena_varint(void* arena, int blocks, hipStream_t st);
 // H2D pulled by GPU waves from pinned host memory (16-B aligned src and dst).
 hipError_t launch_pull_host(void* dst, const void* src, int64_t nbytes, int blocks, hipStream_t st);
 

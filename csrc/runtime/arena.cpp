@@ -27,8 +27,37 @@ std::vector<Span> arena_place(uint8_t* arena, int64_t capacity, const std::vecto
   return spans;
 }
 
+
+int64_t arena_varint_capacity(int64_t max_rows, int64_t fields, int64_t max_requests) {
+  // <= 10 bytes per int64 varint, plus one partial chunk per request
+  return (max_rows * fields * 10 + kVarintChunk - 1) / kVarintChunk + max_requests;
+}
+
+void arena_varint_cpu(uint8_t* base) {
+  const int64_t vt = *reinterpret_cast<const int64_t*>(base + 24);
+  const int32_t n = *reinterpret_cast<const int32_t*>(base + 32);
+  uint8_t* payload = base + kArenaPayloadOff;
+  const VarintChunk* tab = reinterpret_cast<const VarintChunk*>(payload + vt);
+  for (int32_t c = 0; c < n; ++c) {
+    const VarintChunk& ch = tab[c];
+    const uint8_t* src = payload + ch.src_off;
+    int64_t* dst = reinterpret_cast<int64_t*>(payload + ch.dst_off);
+    int64_t idx = ch.first_idx;
+    for (int32_t j = 0; j < ch.len; ++j) {
+      if (src[j] & 0x80) continue;
+      uint64_t v = src[j] & 0x7f;
+      for (int64_t k = int64_t(j) - 1, steps = 0; k >= -int64_t(ch.blob_lo) && steps < 9; --k, ++steps) {
+        if ((src[k] & 0x80) == 0) break;
+        v = (v << 7) | (src[k] & 0x7f);
+      }
+      if (idx < ch.n_values) dst[idx] = int64_t(v);
+      ++idx;
+    }
+  }
+}
+
 ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>& spans, const std::string& ids_key,
-                       const std::string& wts_key, int64_t fields, int64_t max_rows) {
+                       const std::string& wts_key, int64_t fields, int64_t max_rows, int64_t varint_chunks) {
   if (int64_t(spans.size()) > kArenaMaxRequests) throw std::invalid_argument("too many requests for one arena");
   uint8_t* payload = base + kArenaPayloadOff;
   const int64_t cap = capacity - kArenaPayloadOff;
@@ -50,13 +79,59 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
     int64_t ne, ids_off, wts_off, ids_scratch, wts_scratch;
   };
   std::vector<Job> jobs;
+  struct GpuJob {
+    int64_t desc, src_off, len, ne, req;
+  };
+  std::vector<GpuJob> gjobs;
+  int64_t n_chunks = 0;
   std::vector<wire::PredictRequestView> views(n);
   int64_t nd = 0, row = 0;
+  // framing parse, one request per pool task (packed varint fields are
+  // counted here: ~6 bytes per id for ids over 2^40)
+  // Packed varint ids are counted once, per GPU decode chunk (the counts
+  // validate the value count and give each chunk its first index).
+  std::vector<char> parsed_ok(n, 0);
+  std::vector<std::string> perr(n);
+  std::vector<std::vector<int32_t>> chunk_counts(n);
+  // framing only (~1 us per request), then the counting on the pool for the
+  // requests that have uncounted varints
+  std::vector<int64_t> to_count;
   for (size_t i = 0; i < n; ++i) {
-    std::string err;
+    parsed_ok[i] = wire::parse_predict_request(payload + spans[i].first, size_t(spans[i].second), &views[i], &perr[i],
+                                               false);
+    if (!parsed_ok[i]) continue;
+    for (const auto& kv : views[i].inputs)
+      if (kv.second.num_values < 0) {
+        to_count.push_back(int64_t(i));
+        break;
+      }
+  }
+  auto count_one = [&](int64_t i) {
+    for (auto& kv : views[size_t(i)].inputs) {
+      wire::TensorView& t = kv.second;
+      if (t.num_values >= 0) continue;
+      int64_t total = int64_t(t.unpacked.size());
+      if (kv.first == ids_key && t.packed.size() == 1) {
+        auto& cc = chunk_counts[size_t(i)];
+        const wire::Span& sp = t.packed[0];
+        for (size_t lo = 0; lo < sp.n; lo += size_t(kVarintChunk)) {
+          cc.push_back(int32_t(wire::count_varint_terminators(sp.p + lo, std::min(size_t(kVarintChunk), sp.n - lo))));
+          total += cc.back();
+        }
+      } else {
+        for (const wire::Span& sp : t.packed) total += wire::count_varint_terminators(sp.p, sp.n);
+      }
+      t.num_values = total;
+    }
+  };
+  if (to_count.size() > 1)
+    ThreadPool::global().parallel_for(int64_t(to_count.size()), [&](int64_t k) { count_one(to_count[size_t(k)]); });
+  else if (!to_count.empty())
+    count_one(to_count[0]);
+  for (size_t i = 0; i < n; ++i) {
     auto& v = views[i];
-    if (!wire::parse_predict_request(payload + spans[i].first, size_t(spans[i].second), &v, &err)) {
-      out.errors[i] = "malformed PredictRequest: " + err;
+    if (!parsed_ok[i]) {
+      out.errors[i] = "malformed PredictRequest: " + perr[i];
       continue;
     }
     const wire::TensorView* ti = v.find(ids_key);
@@ -76,22 +151,37 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
       continue;
     }
     const bool ids_raw = ti->content.n > 0 && ti->dtype == wire::DT_INT64 && ti->content.n == size_t(ne) * 8;
-    const bool wts_raw = tw->content.n > 0 && tw->dtype == wire::DT_FLOAT && tw->content.n == size_t(ne) * 4;
+    // packed float_val holds the same little-endian bytes as tensor_content
+    const bool wts_packed = tw->content.n == 0 && tw->dtype == wire::DT_FLOAT && tw->value_fixed32 &&
+                            tw->packed.size() == 1 && tw->unpacked.empty() && tw->packed[0].n == size_t(ne) * 4;
+    const bool wts_raw = wts_packed ||
+                         (tw->content.n > 0 && tw->dtype == wire::DT_FLOAT && tw->content.n == size_t(ne) * 4);
+    const uint8_t* wts_bytes = wts_packed ? tw->packed[0].p : tw->content.p;
+    // packed varint ids -> GPU decode (one run of varints, exactly ne values)
+    const int64_t ids_chunks = (!ids_raw && ti->content.n == 0 && ti->dtype == wire::DT_INT64 &&
+                                ti->value_packed_varint && ti->packed.size() == 1 && ti->unpacked.empty() &&
+                                ti->num_values == ne && ne > 0)
+                                   ? (int64_t(ti->packed[0].n) + kVarintChunk - 1) / kVarintChunk
+                                   : 0;
+    const bool ids_gpu = ids_chunks > 0 && n_chunks + ids_chunks <= varint_chunks;
     if ((!ids_raw && ti->num_values > ne) || (!wts_raw && tw->num_values > ne)) {
       out.errors[i] = "more values than the tensor shape holds";
       continue;
     }
     // plan: raw payloads are referenced in place; the rest get scratch space
     // and are decoded below, in parallel
-    const int64_t need =
-        (ids_raw ? 0 : ((ne * 8 + 63) & ~int64_t(63))) + (wts_raw ? 0 : ((ne * 4 + 63) & ~int64_t(63)));
+    const int64_t need = (ids_raw || ids_gpu ? 0 : ((ne * 8 + 63) & ~int64_t(63))) +
+                         (wts_raw ? 0 : ((ne * 4 + 63) & ~int64_t(63)));
     if (scratch + need > cap) {
       out.errors[i] = "arena scratch exhausted";
       continue;
     }
-    Job j{int64_t(i), ti, tw, ne, ids_raw ? int64_t(ti->content.p - payload) : -1,
-          wts_raw ? int64_t(tw->content.p - payload) : -1, 0, 0};
-    if (!ids_raw) {
+    Job j{int64_t(i), ti, tw, ne, ids_raw ? int64_t(ti->content.p - payload) : (ids_gpu ? 0 : -1),
+          wts_raw ? int64_t(wts_bytes - payload) : -1, 0, 0};
+    if (ids_gpu) {
+      gjobs.push_back({nd, int64_t(ti->packed[0].p - payload), int64_t(ti->packed[0].n), ne, int64_t(i)});
+      n_chunks += ids_chunks;
+    } else if (!ids_raw) {
       j.ids_scratch = scratch;
       scratch += (ne * 8 + 63) & ~int64_t(63);
     }
@@ -100,7 +190,7 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
       scratch += (ne * 4 + 63) & ~int64_t(63);
     }
     jobs.push_back(j);
-    desc[4 * nd + 0] = ids_raw ? j.ids_off : j.ids_scratch;
+    desc[4 * nd + 0] = ids_raw ? j.ids_off : (ids_gpu ? -1 : j.ids_scratch);
     desc[4 * nd + 1] = wts_raw ? j.wts_off : j.wts_scratch;
     desc[4 * nd + 2] = rows;
     desc[4 * nd + 3] = row;
@@ -135,10 +225,44 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
     // request itself is answered with the error
     if (!errs[k].empty()) out.errors[jobs[k].req] = errs[k];
   }
-  // per-row offset table: {ids_off, wts_off} int32 (payload-relative)
+  // per-row offset table: {ids_off, wts_off} int32 (payload-relative), then
+  // the varint chunk table (both copied to the GPU), then the device-only
+  // region the varint kernel decodes ids into
   const int64_t rt = (std::max(end, scratch) + 63) & ~int64_t(63);
-  if (rt + row * 8 > cap) throw std::invalid_argument("arena too small for the row table");
-  if (rt + row * 8 > int64_t(INT32_MAX)) throw std::invalid_argument("arena payload exceeds 2 GiB");
+  const int64_t vt = (rt + row * 8 + 63) & ~int64_t(63);
+  const int64_t vt_end = vt + n_chunks * int64_t(sizeof(VarintChunk));
+  int64_t dec = (vt_end + 63) & ~int64_t(63);
+  for (const GpuJob& g : gjobs) dec += g.ne * 8;
+  if (std::max(vt_end, dec) > cap) throw std::invalid_argument("arena too small for the row table");
+  if (std::max(vt_end, dec) > int64_t(INT32_MAX)) throw std::invalid_argument("arena payload exceeds 2 GiB");
+  {
+    // chunk tables, one request per pool task
+    VarintChunk* vtab = reinterpret_cast<VarintChunk*>(payload + vt);
+    std::vector<int64_t> first_chunk(gjobs.size()), dst(gjobs.size());
+    int64_t d = (vt_end + 63) & ~int64_t(63), c = 0;
+    for (size_t k = 0; k < gjobs.size(); ++k) {
+      desc[4 * gjobs[k].desc + 0] = d;
+      dst[k] = d;
+      first_chunk[k] = c;
+      c += (gjobs[k].len + kVarintChunk - 1) / kVarintChunk;
+      d += gjobs[k].ne * 8;
+    }
+    for (size_t k = 0; k < gjobs.size(); ++k) {
+      const GpuJob& g = gjobs[k];
+      const auto& cc = chunk_counts[size_t(g.req)];
+      int64_t before = 0, ci = first_chunk[k];
+      for (int64_t lo = 0, q = 0; lo < g.len; lo += kVarintChunk, ++q) {
+        VarintChunk& ch = vtab[ci++];
+        ch.src_off = g.src_off + lo;
+        ch.dst_off = dst[k];
+        ch.len = int32_t(std::min(kVarintChunk, g.len - lo));
+        ch.first_idx = int32_t(before);
+        ch.n_values = int32_t(g.ne);
+        ch.blob_lo = int32_t(lo);
+        before += cc[size_t(q)];
+      }
+    }
+  }
   int32_t* tab = reinterpret_cast<int32_t*>(payload + rt);
   for (int64_t d = 0; d < nd; ++d) {
     const int64_t io = desc[4 * d + 0], wo = desc[4 * d + 1], rows = desc[4 * d + 2], r0 = desc[4 * d + 3];
@@ -150,13 +274,18 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
   *reinterpret_cast<int32_t*>(base) = int32_t(nd);
   *reinterpret_cast<int64_t*>(base + 8) = row;
   *reinterpret_cast<int64_t*>(base + 16) = rt;
+  *reinterpret_cast<int64_t*>(base + 24) = vt;
+  *reinterpret_cast<int32_t*>(base + 32) = int32_t(n_chunks);
   out.total_rows = row;
   out.n_valid = nd;
-  out.used_bytes = kArenaPayloadOff + rt + row * 8;
+  out.n_gpu_varint = int64_t(gjobs.size());
+  out.used_bytes = kArenaPayloadOff + vt_end;
   return out;
 }
 
 void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, int64_t fields) {
+  // the GPU decodes varint ids in its own copy of the arena; do the same here
+  arena_varint_cpu(const_cast<uint8_t*>(base));
   const int32_t n = std::min<int32_t>(*reinterpret_cast<const int32_t*>(base), int32_t(kArenaMaxRequests));
   const int64_t* desc = reinterpret_cast<const int64_t*>(base + 64);
   const uint8_t* payload = base + kArenaPayloadOff;

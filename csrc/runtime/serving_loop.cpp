@@ -83,7 +83,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         const double t0 = now_us();
         trace::Range tr("parse");
         ArenaBatch b = arena_build(in.arena, in.capacity, in.spans, cfg_.ids_key, cfg_.wts_key, cfg_.fields,
-                                   cfg_.max_rows);
+                                   cfg_.max_rows, cfg_.varint_chunks);
         const double t1 = now_us();
         std::lock_guard<std::mutex> lk(mu);
         parsed[size_t(k)] = std::move(b);

@@ -42,6 +42,7 @@ struct LoopConfig {
   int depth = 3;
   int64_t fields = 43;
   int64_t max_rows = 0;
+  int64_t varint_chunks = 0;  // > 0: packed varint ids are decoded on the GPU (arena.h)
   std::string ids_key = "feat_ids", wts_key = "feat_wts";
   std::string model_name = "DCN", signature_name = "serving_default", output_key = "prediction_node";
   int64_t version = -1;  // < 0: unset

@@ -1,6 +1,10 @@
 // Zero-copy PredictRequest / PredictResponse codec. See tensor_codec.h.
 #include "tensor_codec.h"
 
+#include <immintrin.h>
+
+#include <algorithm>
+
 #include <cmath>
 #include <cstring>
 
@@ -145,11 +149,48 @@ float bf16_to_f32(uint16_t h) {
   return f;
 }
 
-int64_t count_varints(const Span& s) {
+namespace {
+int64_t count_terms_sse2(const uint8_t* p, size_t n) {
+  // bytes with MSB clear compare > -1 as int8: subtract the 0xFF masks from a
+  // per-byte counter (<= 255 steps), then sum the counters with SAD
   int64_t c = 0;
-  for (size_t i = 0; i < s.n; ++i) c += (s.p[i] & 0x80) == 0;
+  size_t i = 0;
+  const __m128i neg1 = _mm_set1_epi8(-1), zero = _mm_setzero_si128();
+  while (i + 16 <= n) {
+    __m128i acc = zero;
+    const size_t stop = std::min(n - 15, i + 16 * 255);
+    for (; i < stop; i += 16)
+      acc = _mm_sub_epi8(acc, _mm_cmpgt_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), neg1));
+    const __m128i s = _mm_sad_epu8(acc, zero);
+    c += _mm_cvtsi128_si64(s) + _mm_cvtsi128_si64(_mm_unpackhi_epi64(s, s));
+  }
+  for (; i < n; ++i) c += (p[i] & 0x80) == 0;
   return c;
 }
+
+__attribute__((target("avx2"))) int64_t count_terms_avx2(const uint8_t* p, size_t n) {
+  int64_t c = 0;
+  size_t i = 0;
+  const __m256i neg1 = _mm256_set1_epi8(-1), zero = _mm256_setzero_si256();
+  while (i + 32 <= n) {
+    __m256i acc = zero;
+    const size_t stop = std::min(n - 31, i + 32 * 255);
+    for (; i < stop; i += 32)
+      acc = _mm256_sub_epi8(acc,
+                            _mm256_cmpgt_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + i)), neg1));
+    const __m256i s = _mm256_sad_epu8(acc, zero);
+    c += _mm256_extract_epi64(s, 0) + _mm256_extract_epi64(s, 1) + _mm256_extract_epi64(s, 2) +
+         _mm256_extract_epi64(s, 3);
+  }
+  return c + count_terms_sse2(p + i, n - i);
+}
+
+const bool g_avx2 = __builtin_cpu_supports("avx2");
+}  // namespace
+
+int64_t count_terms(const uint8_t* p, size_t n) { return g_avx2 ? count_terms_avx2(p, n) : count_terms_sse2(p, n); }
+
+int64_t count_varints(const Span& s) { return count_terms(s.p, s.n); }
 
 bool parse_shape(Span s, TensorView* t, std::string* err) {
   Reader r{s.p, s.p + s.n};
@@ -192,7 +233,7 @@ struct RawChunk {
   uint64_t scalar;
 };
 
-bool parse_tensor_impl(Span s, TensorView* t, std::string* err) {
+bool parse_tensor_impl(Span s, TensorView* t, std::string* err, bool count_varints_ = true) {
   Reader r{s.p, s.p + s.n};
   std::vector<RawChunk> chunks;
   while (!r.eof()) {
@@ -241,11 +282,15 @@ bool parse_tensor_impl(Span s, TensorView* t, std::string* err) {
   t->value_fixed32 = kind == WT_FIXED32;
   t->value_fixed64 = kind == WT_FIXED64;
   t->num_values = 0;
+  bool uncounted = false;  // packed varints left for the caller to count (see header)
   for (const RawChunk& c : chunks) {
     if (c.field != t->value_field) continue;
     if (c.packed) {
       t->packed.push_back(c.span);
-      if (kind == WT_VARINT) t->num_values += count_varints(c.span);
+      if (kind == WT_VARINT) {
+        if (count_varints_) t->num_values += count_varints(c.span);
+        else uncounted = true;
+      }
       else if (kind == WT_FIXED32) {
         if (c.span.n % 4) return *err = "packed fixed32 length not a multiple of 4", false;
         t->num_values += int64_t(c.span.n / 4);
@@ -263,6 +308,7 @@ bool parse_tensor_impl(Span s, TensorView* t, std::string* err) {
       t->num_values += 1;
     }
   }
+  if (uncounted) t->num_values = -1;
   return true;
 }
 
@@ -428,7 +474,8 @@ bool parse_tensor(const uint8_t* buf, size_t len, TensorView* out, std::string* 
   return parse_tensor_impl(Span{buf, len}, out, err);
 }
 
-bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* out, std::string* err) {
+bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* out, std::string* err,
+                           bool count_packed_varints) {
   Reader r{buf, buf + len};
   while (!r.eof()) {
     uint64_t tag;
@@ -489,7 +536,7 @@ bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* o
         }
       }
       TensorView tv;
-      if (!parse_tensor_impl(value, &tv, err)) return false;
+      if (!parse_tensor_impl(value, &tv, err, count_packed_varints)) return false;
       // Map semantics: the last entry for a key wins.
       bool replaced = false;
       for (auto& kv : out->inputs)
@@ -812,6 +859,8 @@ std::string encode_predict_request(const ModelSpecOut& spec, const std::vector<T
   }
   return o.s;
 }
+
+int64_t count_varint_terminators(const uint8_t* p, size_t n) { return count_terms(p, n); }
 
 }  // namespace wire
 }  // namespace dtfs

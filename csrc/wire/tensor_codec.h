@@ -79,7 +79,15 @@ struct PredictRequestView {
 
 // Parse a serialized tensorflow.serving.PredictRequest. Returns false and sets
 // *err on malformed input. The view keeps pointers into [buf, buf+len).
-bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* out, std::string* err);
+// count_packed_varints = false leaves num_values = -1 for packed varint
+// fields (the caller counts them itself, e.g. the arena build, which counts
+// per GPU decode chunk anyway).
+bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* out, std::string* err,
+                           bool count_packed_varints = true);
+
+// Terminator bytes (MSB clear) = complete varints in [p, p + n); AVX2 when
+// the CPU has it.
+int64_t count_varint_terminators(const uint8_t* p, size_t n);
 
 // Parse one serialized TensorProto.
 bool parse_tensor(const uint8_t* buf, size_t len, TensorView* out, std::string* err);

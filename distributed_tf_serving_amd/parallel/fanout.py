@@ -169,6 +169,7 @@ class FanoutEngine:
     def _unpack(self, arena_dev: torch.Tensor, packed: torch.Tensor) -> None:
         from ..ops import hip
 
+        self.arena.decode_varints(arena_dev)
         hip().unpack_arena(arena_dev, packed, self.layout.fields)
 
     def _dev(self, store, key, shape, dtype):
@@ -420,6 +421,7 @@ class FanoutEngine:
             # the head kernel writes the scores straight into pinned host memory
             # (no D2H copy node, which a graph would run as a blit kernel)
             if fused_ingest:  # K0 fused into K1: the gather reads the request bytes
+                self.arena.decode_varints(arena_dev)
                 self.ex.model.forward_arena(arena_dev, B, out=h_out[:B])
                 return
             if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows

@@ -30,6 +30,29 @@ class ArenaLayout:
     fields: int
     max_rows: int
     max_requests: int = 1024
+    # packed varint int64_val ids (the reference client's encoding) decoded on
+    # the GPU (csrc/runtime/arena.h, csrc/kernels/ingest.hip) instead of on
+    # the host pool: the H2D copy carries the compact wire bytes
+    gpu_varint: bool = True
+
+    @property
+    def varint_chunks(self) -> int:
+        """Chunk-table capacity handed to the host build (0: host decode)."""
+        if not self.gpu_varint:
+            return 0
+        return native().arena_varint_capacity(self.max_rows, self.fields, self.max_requests)
+
+    @property
+    def varint_blocks(self) -> int:
+        """Grid of the varint kernel (blocks loop over the chunks)."""
+        return min(1024, self.varint_chunks)
+
+    def decode_varints(self, arena_dev: torch.Tensor) -> None:
+        """GPU varint decode of a built, copied arena (no-op grid if none)."""
+        if self.gpu_varint:
+            from ..ops import hip
+
+            hip().arena_varint_decode(arena_dev, self.varint_blocks)
 
     @property
     def payload_off(self) -> int:
@@ -40,7 +63,8 @@ class ArenaLayout:
         # serialized rows (varints can reach ~14 B/feature) + host-decoded scratch (12 B/feature)
         # + the per-row offset table (8 B/row)
         per_row = 28 * self.fields + 8
-        return self.payload_off + self.max_rows * per_row + self.max_requests * 1024 + 128
+        return (self.payload_off + self.max_rows * per_row + self.max_requests * 1024 + 128
+                + 32 * self.varint_chunks)
 
     def alloc(self, device="cpu", pin: bool = False) -> torch.Tensor:
         return torch.zeros(self.capacity, dtype=torch.uint8, device=device, pin_memory=pin)
@@ -51,7 +75,8 @@ class ArenaLayout:
 
     def build(self, arena: torch.Tensor, spans: Sequence[Tuple[int, int]], ids_key="feat_ids", wts_key="feat_wts"):
         """Parse in place + write descriptors; returns ArenaBatch (rows/offsets/errors/used_bytes)."""
-        return native().arena_build(arena, list(spans), ids_key, wts_key, self.fields, self.max_rows)
+        return native().arena_build(arena, list(spans), ids_key, wts_key, self.fields, self.max_rows,
+                                    self.varint_chunks)
 
     def unpack_cpu(self, arena: torch.Tensor, packed: torch.Tensor) -> torch.Tensor:
         native().arena_unpack_cpu(arena, packed, self.fields)

@@ -329,11 +329,13 @@ def test_unpack_arena_gpu_matches_cpu(cuda):
     s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=5)
     reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((1, True), (300, True), (17, False), (512, True))]
     ab = A.build(ar, A.place(ar, reqs))
-    assert ab.total_rows == 830 and not any(ab.errors)
+    assert ab.total_rows == 830 and not any(ab.errors) and ab.n_gpu_varint == 1
+    dev = ar.to(cuda)  # before the CPU reference fills the host copy's decoded-id region
     ref = A.unpack_cpu(ar, L.alloc(1024))
     got = L.alloc(1024, device=cuda)
     got.fill_(-1)
-    ops.hip().unpack_arena(ar.to(cuda), got, 43)
+    A.decode_varints(dev)  # packed varint ids of the 17-row request, on the GPU
+    ops.hip().unpack_arena(dev, got, 43)
     assert torch.equal(got.cpu(), ref)  # rows past total_rows are zeroed too
 
 
@@ -351,16 +353,57 @@ def test_forward_arena_matches_packed(cuda, family):
     s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=9)
     reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, True), (17, False), (200, True))]
     ab = A.build(ar, A.place(ar, reqs))
+    dev = ar.to(cuda)
+    A.decode_varints(dev)
     B = 512  # > total_rows: padding rows must score like zero-weight rows
     packed = A.unpack_cpu(ar, L.alloc(B))
     want = m(L.ids(packed).to(cuda), L.wts(packed).to(cuda)).cpu()
-    got = m.forward_arena(ar.to(cuda), B).cpu()
+    got = m.forward_arena(dev, B).cpu()
     _close(got[:ab.total_rows], want[:ab.total_rows], 0, 1e-6, f"{family} arena vs packed")
     _close(got, want, 0, 1e-6, f"{family} arena padding rows")
     out = torch.zeros(B, dtype=torch.float32).pin_memory()
-    m.forward_arena(ar.to(cuda), B, out=out)
+    m.forward_arena(dev, B, out=out)
     torch.cuda.synchronize()
     _close(out, want, 0, 1e-6, f"{family} arena into pinned host")
+
+
+def test_arena_varint_gpu_decode(cuda):
+    # packed varint ids (reference client encoding) decoded by the GPU kernel:
+    # multi-chunk runs, varints straddling 4 KiB chunk and lane boundaries,
+    # 10-byte negative ids, 1-byte small ids
+    from distributed_tf_serving_amd.ops import native
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    F = 43
+    g = torch.Generator().manual_seed(3)
+    A, L = ArenaLayout(F, 4096), PackedLayout(F)
+    ar = A.alloc()
+    reqs, want = [], []
+    for n, kind in ((700, "mixed"), (1, "small"), (900, "neg"), (333, "mixed")):
+        if kind == "small":
+            ids = torch.randint(1, 100, (n, F), generator=g)
+        elif kind == "neg":
+            ids = torch.randint(-(1 << 62), 1 << 62, (n, F), generator=g)
+        else:
+            ids = torch.randint(0, 1 << 40, (n, F), generator=g) >> torch.randint(0, 40, (n, F), generator=g)
+        wts = torch.rand(n, F, generator=g)
+        reqs.append(native().encode_predict_request("DCN", "serving_default", None,
+                                                    [("feat_ids", ids), ("feat_wts", wts)], False))
+        want.append((ids, wts))
+    ab = A.build(ar, A.place(ar, reqs))
+    assert not any(ab.errors) and ab.n_gpu_varint == 4 and ab.n_decoded == 0
+    dev = ar.to(cuda)
+    A.decode_varints(dev)
+    B = ab.total_rows
+    got = L.alloc(B, device=cuda)
+    ops.hip().unpack_arena(dev, got, F)
+    got = got.cpu()
+    ids_all = torch.cat([w[0] for w in want])
+    wts_all = torch.cat([w[1] for w in want])
+    assert torch.equal(L.ids(got), ids_all)
+    assert torch.equal(L.wts(got), wts_all)
+    assert torch.equal(A.unpack_cpu(ar, L.alloc(B)), got)
 
 
 def test_deepfm_full_mlp_gpu_vs_cpu(cuda):
@@ -401,10 +444,12 @@ def test_embed_pipelined_rows_per_wave(cuda, waves):
         s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=waves)
         reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, True), (17, False), (200, True))]
         ab = A.build(ar, A.place(ar, reqs))
+        dev = ar.to(cuda)
+        A.decode_varints(dev)
         packed = A.unpack_cpu(ar, L.alloc(512))
         want = ops.embed(table.to(cuda), L.ids(packed).to(cuda), L.wts(packed).to(cuda), lin=lin.to(cuda), modulo=V,
                          want_x=True, want_fm=True, fm2=True)
-        got = ops.embed(table.to(cuda), ops.ArenaRows(ar.to(cuda), 512, F), None, lin=lin.to(cuda), modulo=V,
+        got = ops.embed(table.to(cuda), ops.ArenaRows(dev, 512, F), None, lin=lin.to(cuda), modulo=V,
                         want_x=True, want_fm=True, fm2=True)
         assert ab.total_rows == 470
         _close(got[0], want[0], 0, 0, "arena x")

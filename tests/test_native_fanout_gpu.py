@@ -52,7 +52,8 @@ def test_native_serving_loop(cuda, mode):
     AL = ArenaLayout(F, max_rows=B)
     eng = FanoutEngine(ex, DistContext(device=cuda), mode="alltoall" if mode == "local" else mode, ingest="arena",
                        arena=AL, force_fanout=mode != "local")
-    loop = hip().ServingLoop(eng.runner(), dict(depth=S - 1, fields=F, max_rows=B, version=1), eng.loop_slots(B))
+    loop = hip().ServingLoop(eng.runner(), dict(depth=S - 1, fields=F, max_rows=B, version=1,
+                                                        varint_chunks=AL.varint_chunks), eng.loop_slots(B))
     synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=5)
     inputs = []
     for p in range(5):
