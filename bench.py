@@ -228,6 +228,7 @@ def main():
         from distributed_tf_serving_amd.ops import hip
 
         nloop = hip().ServingLoop(eng.runner(), dict(depth=slots - 1, fields=F, max_rows=arena_layout.max_rows,
+                                                     varint_chunks=arena_layout.varint_chunks,
                                                      version=1), loop_slots)
         for ar, sp in zip(arenas, spans):
             nloop.add_input(ar, sp)

@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
 // Requires K % (128 / elem bytes) == 0; rows past M / N are clamped (their
 // results are never stored).
 template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
-__global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
+__device__ __forceinline__ void gemm_glds_body(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
     int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
@@ -362,6 +362,17 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(
   }
 
   store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+}
+
+#define DTFS_GLDS_ARGS                                                                                              \
+  const uint8_t *__restrict__ A, int64_t lda, const uint8_t *__restrict__ W, int64_t ldw,                           \
+      const float *__restrict__ bias, const float *__restrict__ sa, const float *__restrict__ sw,                   \
+      OutT *__restrict__ C, int64_t ldc, const bf16 *__restrict__ X0, const bf16 *__restrict__ XL, int64_t ldx,     \
+      int M, int N, int K, int epi
+
+template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+__global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(DTFS_GLDS_ARGS) {
+  gemm_glds_body<BM, BN, WM_, WN_, FP8, OutT>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi);
 }
 
 template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>

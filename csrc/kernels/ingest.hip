@@ -173,6 +173,8 @@ __global__ void __launch_bounds__(256) arena_varint_kernel(uint8_t* __restrict__
 
 }  // namespace kern
 
+const void* arena_varint_kernel_fn() { return reinterpret_cast<const void*>(&kern::arena_varint_kernel); }
+
 hipError_t launch_arena_varint(void* arena, int blocks, hipStream_t st) {
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(kern::arena_varint_kernel, dim3(blocks), dim3(256), 0, st, static_cast<uint8_t*>(arena));

@@ -55,6 +55,9 @@ hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F,
 // Packed varint ids of a built arena -> its device-only int64 id region
 // (csrc/runtime/arena.h VarintChunk); blocks loop over the chunk table.
 hipError_t launch_arena_varint(void* arena, int blocks, hipStream_t st);
+// Host stub of that kernel (lets a replayed step skip it when no request of
+// the step has varint ids: runtime/kernel_seq.cpp).
+const void* arena_varint_kernel_fn();
 // H2D pulled by GPU waves from pinned host memory (16-B aligned src and dst).
 hipError_t launch_pull_host(void* dst, const void* src, int64_t nbytes, int blocks, hipStream_t st);
 

@@ -2,6 +2,8 @@
 
 #include <hip/hip_ext.h>
 
+#include "../kernels/launchers.h"
+
 #include <map>
 #include <stdexcept>
 
@@ -57,6 +59,7 @@ KernelSequence::KernelSequence(hipGraph_t graph) {
       op.kind = 0;
       ck(hipGraphKernelNodeGetParams(nodes[i], &op.k), "hipGraphKernelNodeGetParams");
       if (!op.k.kernelParams) throw std::runtime_error("kernel node without kernelParams (extra-style launch)");
+      op.varint = op.k.func == arena_varint_kernel_fn();
     } else if (t == hipGraphNodeTypeMemcpy) {
       op.kind = 1;
       ck(hipGraphMemcpyNodeGetParams(nodes[i], &op.mc), "hipGraphMemcpyNodeGetParams");
@@ -77,10 +80,11 @@ KernelSequence::KernelSequence(hipGraph_t graph) {
   }
 }
 
-void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind) const {
+void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool skip_varint) const {
   const bool bind_last = done && bind && !ops_.empty() && ops_.back().kind == 0;
   for (size_t i = 0; i < ops_.size(); ++i) {
     const Op& op = ops_[i];
+    if (skip_varint && op.varint && i + 1 < ops_.size()) continue;
     if (op.kind == 0) {
       if (bind_last && i + 1 == ops_.size())
         ck(hipExtLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st,

@@ -28,13 +28,16 @@ class KernelSequence {
   // completes with the last node: bound to the last kernel's own dispatch
   // (hipExtLaunchKernel stop event) when `bind` is set and the last node is a
   // kernel, otherwise recorded after it.
-  void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false) const;
+  // skip_varint: leave out the arena varint-decode kernel (the host parse
+  // found no packed varint ids in this step's requests).
+  void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false, bool skip_varint = false) const;
   int size() const { return int(ops_.size()); }
   std::string describe() const;
 
  private:
   struct Op {
     int kind = 0;  // 0 kernel, 1 memcpy, 2 memset
+    bool varint = false;
     hipKernelNodeParams k{};
     hipMemcpy3DParms mc{};
     hipMemsetParams ms{};

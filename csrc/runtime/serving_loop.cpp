@@ -179,7 +179,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
         f.h2d_bytes = nbytes;
         runner_->launch_fanout(slot, f);
       } else {
-        if (s.seq) runner_->launch_seq(slot, s.h2d_dst, in.arena, nbytes, s.seq);
+        if (s.seq) runner_->launch_seq(slot, s.h2d_dst, in.arena, nbytes, s.seq, b.n_gpu_varint == 0);
         else runner_->launch(slot, s.h2d_dst, in.arena, nbytes, s.graph);
       }
       launch_us += now_us() - t0;

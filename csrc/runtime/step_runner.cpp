@@ -158,12 +158,13 @@ void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hi
   used_[slot] = true;
 }
 
-void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq) {
+void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq,
+                            bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d(slot, dst, src, nbytes, compute_, true);
-  seq->launch(compute_, done_[slot], event_mode_ >= 2);
+  seq->launch(compute_, done_[slot], event_mode_ >= 2, skip_varint);
   used_[slot] = true;
 }
 

@@ -65,7 +65,8 @@ class StepRunner {
   // waits only for the previous step of the same slot to have consumed dst.
   void launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph);
   // Same, replaying the step as direct kernel launches (no graph-launch gap).
-  void launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq);
+  void launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq,
+                  bool skip_varint = false);
   // Enqueue one fan-out step (see FanoutStep).
   void launch_fanout(int slot, const FanoutStep& s);
   // Block until the slot's last step has finished (scores are on the host).

@@ -122,8 +122,14 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
+    ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.variants:
+        shape, vs = a.variants.split(":")
+        M, N, K = (int(x) for x in shape.split(","))
+        print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
+        return
     if a.embed_study:
         for r in embed_study():
             print(json.dumps(r), flush=True)

@@ -36,10 +36,13 @@ def test_rccl_comm_single_rank(cuda):
     assert c.aborted
 
 
-@pytest.mark.parametrize("mode", ["local", "alltoall", "scatter"])
-def test_native_serving_loop(cuda, mode):
+@pytest.mark.parametrize("mode,raw", [("local", True), ("local", False), ("alltoall", True), ("alltoall", False),
+                                      ("scatter", True)])
+def test_native_serving_loop(cuda, mode, raw):
     """The C++ ServingLoop (parse -> H2D + step graph / fan-out -> encode) over a
-    ring of request arenas; the last step's scores match a local forward."""
+    ring of request arenas; the last step's scores match a local forward.
+    raw=False: packed varint requests, decoded on the GPU (the local replay
+    skips the varint kernel for steps without any)."""
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.ops import hip, native
 
@@ -61,7 +64,7 @@ def test_native_serving_loop(cuda, mode):
         ids, wts = torch.from_numpy(ids), torch.from_numpy(wts)
         reqs = [native().encode_predict_request("DCN", "serving_default", None,
                                                 [("feat_ids", ids[i:i + B // R]), ("feat_wts", wts[i:i + B // R])],
-                                                True)
+                                                raw or p == 1)
                 for i in range(0, B, B // R)]
         ar = AL.alloc(pin=True)
         loop.add_input(ar, AL.place(ar, reqs))
