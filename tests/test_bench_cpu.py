@@ -1,0 +1,56 @@
+"""bench.py contract on CPU: the driver's launch line (torch.distributed.run,
+one rank per device, 127.0.0.1 rendezvous) with gloo, world sizes 1 and 2,
+tiny step shapes. Checks the single JSON line the driver parses (whole-job
+value, n_gpus, steps/warmup, weak scaling, global batch = N x per-rank rows)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_bench(n: int, extra=()):
+    args = ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--requests-per-gpu", "1",
+            "--request-rows", "64", "--pool", "2", *extra]
+    if n == 1:
+        cmd = [sys.executable, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only, one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_json_contract(n):
+    out = _run_bench(n)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
+    assert out["higher_is_better"] is True and out["scaling"] == "weak"
+    assert out["dtype"] == "bf16" and "synthetic" in out["data"]
+    assert out["config"]["global_batch"] == n * 64
+    assert out["value"] > 0
+    # value is the whole-job rate: global rows per step / seconds per step
+    assert out["value"] == pytest.approx(n * 64 / (out["ms_per_step"] * 1e-3), rel=0.02)
+    assert f"candidate-dp{n}" in out["config"]["parallelism"]
+
+
+def test_bench_scatter_mode_world2():
+    out = _run_bench(2, ("--mode", "scatter"))
+    assert "scatter" in out["config"]["parallelism"] and out["config"]["global_batch"] == 128
