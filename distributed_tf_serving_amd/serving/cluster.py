@@ -77,6 +77,7 @@ class ClusterServer:
         self.registry: Optional[ModelRegistry] = None
         self.service: Optional[PredictionServiceImpl] = None
         self.front = None
+        self.metrics = None
         self.steps_followed = 0
         if self.rank == 0:
             on_launch = self.ctrl.send if self.ctrl is not None else None
@@ -85,11 +86,18 @@ class ClusterServer:
             self.service = PredictionServiceImpl(self.registry, cfg.serving.request_timeout_s)
 
     # -- rank 0 -------------------------------------------------------------------
-    def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32) -> int:
+    def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32,
+                   monitoring_port: Optional[int] = None) -> int:
+        """monitoring_port: also serve Prometheus metrics (serving/monitoring.py)."""
         from .grpc_server import GrpcFrontDoor
+        from .monitoring import ServingMetrics
 
         assert self.rank == 0, "only rank 0 is a front door"
-        self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers).start()
+        self.metrics = ServingMetrics(self.registry)
+        self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers,
+                                   metrics=self.metrics).start()
+        if monitoring_port is not None:
+            self.metrics.serve_http(monitoring_port, host)
         return self.front.port
 
     # -- ranks > 0 ----------------------------------------------------------------
@@ -116,6 +124,8 @@ class ClusterServer:
 
     def stop(self) -> None:
         if self.rank == 0:
+            if self.metrics is not None:
+                self.metrics.stop()
             if self.front is not None:
                 self.front.stop()
                 self.front = None
@@ -131,13 +141,15 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=9999)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--grpc-workers", type=int, default=32)
+    ap.add_argument("--monitoring-port", type=int, default=None,
+                    help="serve Prometheus metrics over HTTP on this port (rank 0)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     ctx = init_from_env()
     srv = ClusterServer(load_preset(a.preset), ctx)
     try:
         if srv.rank == 0:
-            port = srv.start_grpc(a.port, a.host, a.grpc_workers)
+            port = srv.start_grpc(a.port, a.host, a.grpc_workers, a.monitoring_port)
             print(f"serving on port {port} over {ctx.world} GPU(s)", flush=True)
             signal.signal(signal.SIGTERM, lambda *_: srv.front.stop() if srv.front else None)
             try:

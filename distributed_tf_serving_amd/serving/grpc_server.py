@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import logging
+import time
 from typing import Optional
 
 import grpc
@@ -28,31 +29,39 @@ log = logging.getLogger(__name__)
 _ident = lambda b: b  # noqa: E731 - raw bytes in / out
 
 
-def _wrap(fn, ctx_timeout=True):
+def _wrap(fn, api: str = "", metrics=None, ctx_timeout=True):
     def handler(request, context):
+        t0 = time.perf_counter()
+        status = "OK"
         try:
             t = context.time_remaining() if ctx_timeout else None
             return fn(request, t if t is not None and t < 1e8 else None)
         except ServingError as e:
+            status = e.grpc_code().name
             context.abort(e.grpc_code(), e.message)
         except Exception as e:  # noqa: BLE001
+            status = "INTERNAL"
             log.exception("RPC failed")
             context.abort(grpc.StatusCode.INTERNAL, str(e))
+        finally:
+            if metrics is not None:
+                metrics.observe(api, status, t0)
 
     return handler
 
 
-def make_handler(service: PredictionServiceImpl) -> grpc.GenericRpcHandler:
+def make_handler(service: PredictionServiceImpl, metrics=None) -> grpc.GenericRpcHandler:
     M = pb.METHODS
 
     def msg_handler(name, fn):
         req_cls, resp_cls = M[name]
         return grpc.unary_unary_rpc_method_handler(
-            _wrap(fn), request_deserializer=req_cls.FromString, response_serializer=resp_cls.SerializeToString)
+            _wrap(fn, name, metrics), request_deserializer=req_cls.FromString,
+            response_serializer=resp_cls.SerializeToString)
 
     handlers = {
         "Predict": grpc.unary_unary_rpc_method_handler(
-            _wrap(lambda data, t: service.predict_bytes(data, t)), request_deserializer=_ident,
+            _wrap(lambda data, t: service.predict_bytes(data, t), "Predict", metrics), request_deserializer=_ident,
             response_serializer=_ident),
         "Classify": msg_handler("Classify", lambda r, t: service.classify(r, t)),
         "Regress": msg_handler("Regress", lambda r, t: service.regress(r, t)),
@@ -64,13 +73,14 @@ def make_handler(service: PredictionServiceImpl) -> grpc.GenericRpcHandler:
 
 class GrpcFrontDoor:
     def __init__(self, service: PredictionServiceImpl, port: int = 9999, host: str = "0.0.0.0",
-                 max_workers: int = 32, max_message_mb: int = 64):
+                 max_workers: int = 32, max_message_mb: int = 64, metrics=None):
         self.service = service
+        self.metrics = metrics  # serving/monitoring.py ServingMetrics (optional)
         opts = [("grpc.max_receive_message_length", max_message_mb << 20),
                 ("grpc.max_send_message_length", max_message_mb << 20)]
         self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="dtfs-grpc"),
                                   options=opts)
-        self.server.add_generic_rpc_handlers((make_handler(service),))
+        self.server.add_generic_rpc_handlers((make_handler(service, metrics),))
         self.port = self.server.add_insecure_port(f"{host}:{port}")
         if self.port == 0:
             raise RuntimeError(f"could not bind {host}:{port}")

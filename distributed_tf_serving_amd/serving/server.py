@@ -23,6 +23,7 @@ from ..parallel.dist import DistContext
 from ..parallel.fanout import FanoutEngine
 from .batching import BatchingScheduler
 from .executor import ShardExecutor
+from .monitoring import ServingMetrics
 from .packing import PackedLayout
 from .registry import ModelRegistry, Servable, Signature
 from .service import PredictionServiceImpl
@@ -80,15 +81,22 @@ class ModelServer:
         self.registry = ModelRegistry()
         self.registry.load(build_servable(cfg, device))
         self.service = PredictionServiceImpl(self.registry, cfg.serving.request_timeout_s)
+        self.metrics = ServingMetrics(self.registry)
         self.front = None
 
     def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32):
         from .grpc_server import GrpcFrontDoor
 
-        self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers).start()
+        self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers,
+                                   metrics=self.metrics).start()
         return self.front.port
 
+    def start_monitoring(self, port: int, host: str = "0.0.0.0") -> int:
+        """Prometheus text format over HTTP (TF-Serving's monitoring endpoint)."""
+        return self.metrics.serve_http(port, host)
+
     def stop(self) -> None:
+        self.metrics.stop()
         if self.front is not None:
             self.front.stop()
             self.front = None
@@ -109,6 +117,8 @@ def main(argv=None):
     ap.add_argument("--device", default=None)
     ap.add_argument("--model-name", default=None)
     ap.add_argument("--grpc-workers", type=int, default=32)
+    ap.add_argument("--monitoring-port", type=int, default=None,
+                    help="serve Prometheus metrics over HTTP on this port (TF-Serving monitoring endpoint)")
     ap.add_argument("--inject-fault", default="",
                     help="failure testing, e.g. 'after:100,kind:error' (serving/faults.py)")
     a = ap.parse_args(argv)
@@ -122,6 +132,8 @@ def main(argv=None):
 
         srv.service = FaultyService(srv.service, FaultInjector(FaultSpec.parse(a.inject_fault)))
     port = srv.start_grpc(a.port, a.host, a.grpc_workers)
+    if a.monitoring_port is not None:
+        srv.start_monitoring(a.monitoring_port, a.host)
     print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:

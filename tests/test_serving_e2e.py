@@ -212,3 +212,35 @@ def test_oversized_request_is_split(server):
 def test_service_error_codes():
     e = ServingError(Code.NOT_FOUND, "x")
     assert e.grpc_code() == grpc.StatusCode.NOT_FOUND
+
+
+def test_prometheus_metrics(server):
+    """TF-Serving's monitoring endpoint: RPC counts by API/status, latency
+    histogram and the batching scheduler's counters, over HTTP."""
+    import urllib.request
+
+    srv, port = server
+    be = GrpcBackend(f"127.0.0.1:{port}")
+    try:
+        be.predict(build_request(reference_shape=False).SerializeToString(), 30)
+        bad = build_request(reference_shape=False)
+        bad.model_spec.name = "nope"
+        with pytest.raises(Exception):
+            be.predict(bad.SerializeToString(), 30)
+    finally:
+        be.close()
+    mport = srv.start_monitoring(0, "127.0.0.1")
+    body = urllib.request.urlopen(f"http://127.0.0.1:{mport}/monitoring/prometheus/metrics", timeout=10).read()
+    text = body.decode()
+    assert ":tensorflow:serving:request_count_total" in text
+
+    def val(prefix):
+        lines = [ln for ln in text.splitlines() if ln.startswith(prefix)]
+        assert lines, prefix
+        return float(lines[0].rsplit(" ", 1)[1])
+
+    assert val(':tensorflow:serving:request_count_total{API="Predict",status="OK"}') >= 1
+    assert val(':tensorflow:serving:request_count_total{API="Predict",status="NOT_FOUND"}') >= 1
+    assert val(':tensorflow:serving:request_latency_count{API="Predict"}') >= 2
+    assert val(':tensorflow:serving:rows_served_total{model_name="DCN",version="1"}') >= 1
+    assert val(':tensorflow:serving:batching_avg_batch_rows{model_name="DCN",version="1"}') > 0
