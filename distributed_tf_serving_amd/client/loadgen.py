@@ -34,6 +34,7 @@ from ..config import add_client_args, client_from_args
 from .backends import GrpcBackend, InProcessBackend
 from .fanout_client import FanoutClient, RequestSpec
 from .synth import SyntheticRequests
+from ..utils.gc_tuning import freeze_heap
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -148,6 +149,7 @@ def main(argv=None):
     ap.add_argument("--inproc-preset", default=None, help="start N in-process servers with this preset")
     ap.add_argument("--quiet", action="store_true", help="suppress per-request lines")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-gc-freeze", action="store_true", help="leave CPython's cyclic GC at its defaults")
     a = ap.parse_args(argv)
     c = client_from_args(a)
     servers = []
@@ -168,6 +170,8 @@ def main(argv=None):
                           sort_scores=c.sort_scores, timeout_s=c.deadline_s or None)
     lg = LoadGenerator(client, c.candidates, fields=c.fields, id_mode=c.id_mode, id_space=c.id_space, seed=c.seed,
                        verbose=not a.quiet)
+    if not a.no_gc_freeze:
+        freeze_heap()  # a GC pause in the load generator is client-side latency, not the server's
     try:
         if c.qps > 0:
             summary = lg.open_loop(c.qps, c.requests * c.concurrency, warmup=c.warmup)

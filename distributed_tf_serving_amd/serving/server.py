@@ -21,6 +21,7 @@ from ..config import Config, load_preset
 from ..models import build_model
 from ..parallel.dist import DistContext
 from ..parallel.fanout import FanoutEngine
+from ..utils.gc_tuning import freeze_heap
 from .batching import BatchingScheduler
 from .executor import ShardExecutor
 from .monitoring import ServingMetrics
@@ -121,6 +122,8 @@ def main(argv=None):
                     help="serve Prometheus metrics over HTTP on this port (TF-Serving monitoring endpoint)")
     ap.add_argument("--inject-fault", default="",
                     help="failure testing, e.g. 'after:100,kind:error' (serving/faults.py)")
+    ap.add_argument("--no-gc-freeze", action="store_true",
+                    help="leave CPython's cyclic GC at its defaults (utils/gc_tuning.py)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     cfg = load_preset(a.preset)
@@ -134,6 +137,8 @@ def main(argv=None):
     port = srv.start_grpc(a.port, a.host, a.grpc_workers)
     if a.monitoring_port is not None:
         srv.start_monitoring(a.monitoring_port, a.host)
+    if not a.no_gc_freeze:
+        logging.getLogger(__name__).info("gc: %s", freeze_heap())
     print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:
