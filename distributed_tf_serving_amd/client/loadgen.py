@@ -34,7 +34,7 @@ from ..config import add_client_args, client_from_args
 from .backends import GrpcBackend, InProcessBackend
 from .fanout_client import FanoutClient, RequestSpec
 from .synth import SyntheticRequests
-from ..utils.gc_tuning import freeze_heap
+from ..utils.gc_tuning import tune_for_serving
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -171,7 +171,7 @@ def main(argv=None):
     lg = LoadGenerator(client, c.candidates, fields=c.fields, id_mode=c.id_mode, id_space=c.id_space, seed=c.seed,
                        verbose=not a.quiet)
     if not a.no_gc_freeze:
-        freeze_heap()  # a GC pause in the load generator is client-side latency, not the server's
+        tune_for_serving()  # a GC pause in the load generator is client-side latency, not the server's
     try:
         if c.qps > 0:
             summary = lg.open_loop(c.qps, c.requests * c.concurrency, warmup=c.warmup)

@@ -30,7 +30,7 @@ import torch.distributed as dist
 
 from ..config import Config, load_preset
 from ..parallel.dist import DistContext, init_from_env, shutdown
-from ..utils.gc_tuning import freeze_heap
+from ..utils.gc_tuning import tune_for_serving
 from .registry import ModelRegistry
 from .server import build_engine, build_servable
 from .service import PredictionServiceImpl
@@ -151,7 +151,7 @@ def main(argv=None):
     try:
         if srv.rank == 0:
             port = srv.start_grpc(a.port, a.host, a.grpc_workers, a.monitoring_port)
-        freeze_heap()  # every rank: a GC pause on a follower stalls the step's collectives too
+        tune_for_serving()  # every rank: a GC pause on a follower stalls the step's collectives too
         if srv.rank == 0:
             print(f"serving on port {port} over {ctx.world} GPU(s)", flush=True)
             signal.signal(signal.SIGTERM, lambda *_: srv.front.stop() if srv.front else None)

@@ -21,7 +21,7 @@ from ..config import Config, load_preset
 from ..models import build_model
 from ..parallel.dist import DistContext
 from ..parallel.fanout import FanoutEngine
-from ..utils.gc_tuning import freeze_heap
+from ..utils.gc_tuning import tune_for_serving
 from .batching import BatchingScheduler
 from .executor import ShardExecutor
 from .monitoring import ServingMetrics
@@ -138,7 +138,7 @@ def main(argv=None):
     if a.monitoring_port is not None:
         srv.start_monitoring(a.monitoring_port, a.host)
     if not a.no_gc_freeze:
-        logging.getLogger(__name__).info("gc: %s", freeze_heap())
+        logging.getLogger(__name__).info("gc: %s", tune_for_serving())
     print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:

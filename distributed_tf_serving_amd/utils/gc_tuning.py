@@ -15,8 +15,13 @@ front door's way of getting the same tail behaviour.
 from __future__ import annotations
 
 import gc
+import sys
 
 _DEFAULT_GEN0 = 50_000
+# CPython hands the GIL to a waiting thread only every switch interval (5 ms by
+# default); a gRPC worker whose batch just completed can sit behind the
+# load-generator or encoder thread for that long.
+_DEFAULT_SWITCH_S = 5e-4
 
 
 def freeze_heap(gen0_threshold: int = _DEFAULT_GEN0) -> dict:
@@ -30,6 +35,15 @@ def freeze_heap(gen0_threshold: int = _DEFAULT_GEN0) -> dict:
     _, g1, g2 = gc.get_threshold()
     gc.set_threshold(max(gen0_threshold, 1), g1, g2)
     return {"frozen": gc.get_freeze_count(), "threshold": gc.get_threshold()}
+
+
+def tune_for_serving(gen0_threshold: int = _DEFAULT_GEN0, switch_interval_s: float = _DEFAULT_SWITCH_S) -> dict:
+    """:func:`freeze_heap` plus a shorter GIL switch interval (serving processes)."""
+    rep = freeze_heap(gen0_threshold)
+    if switch_interval_s > 0:
+        sys.setswitchinterval(switch_interval_s)
+    rep["switch_interval_s"] = sys.getswitchinterval()
+    return rep
 
 
 def unfreeze_heap() -> None:

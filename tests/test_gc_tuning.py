@@ -2,7 +2,9 @@
 generation-2 collections never walk it on the request path."""
 import gc
 
-from distributed_tf_serving_amd.utils.gc_tuning import freeze_heap, unfreeze_heap
+import sys
+
+from distributed_tf_serving_amd.utils.gc_tuning import freeze_heap, tune_for_serving, unfreeze_heap
 
 
 def test_freeze_and_unfreeze():
@@ -27,3 +29,14 @@ def test_entry_points_opt_out_flag():
     from distributed_tf_serving_amd.serving import server
     for mod in (loadgen, server):
         assert "--no-gc-freeze" in open(mod.__file__).read()
+
+
+def test_tune_for_serving_sets_switch_interval():
+    before, sw = gc.get_threshold(), sys.getswitchinterval()
+    try:
+        rep = tune_for_serving(switch_interval_s=1e-3)
+        assert abs(rep["switch_interval_s"] - 1e-3) < 1e-9
+    finally:
+        unfreeze_heap()
+        gc.set_threshold(*before)
+        sys.setswitchinterval(sw)
