@@ -39,5 +39,20 @@ run_preset() {  # preset port candidates id_mode qps...
   return $rc
 }
 
+
+# the reference's own closed-loop shape (6 clients x 1000 requests, DCNClient.java:205-241), one backend
+if [ "${CLOSED_LOOP:-0}" = 1 ]; then
+  timeout -k 10 300 python -u -m distributed_tf_serving_amd.serving.server --preset reference_dcn --port 9997 \
+      > "$OUT/server_closed.log" 2>&1 &
+  spid=$!
+  wait_port 9997 && timeout -k 10 120 python -u -m distributed_tf_serving_amd.client.loadgen \
+      --hosts 127.0.0.1:9997 --backends 1 --candidates 1500 --id-mode reference --quiet \
+      --json-out "$OUT/reference_closed_loop.json" > "$OUT/loadgen_closed.log" 2>&1
+  rc=$?
+  kill "$spid"; wait "$spid" 2>/dev/null
+  cat "$OUT/reference_closed_loop.json"; echo
+  exit $rc
+fi
+
 run_preset deepfm_1gpu 9999 512 zipf 250 500 1000 2000 && \
 run_preset reference_dcn 9998 1500 reference 250 500 1000
