@@ -61,6 +61,7 @@ from distributed_tf_serving_amd.serving.arena import ArenaLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
+from distributed_tf_serving_amd.utils.gc_tuning import tune_for_serving  # noqa: E402
 
 BASELINE_VALUE = None  # the reference publishes no numbers
 # --model -> configs/<preset>.yaml (BASELINE configs 2/3, 4, 5)
@@ -282,6 +283,7 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    tune_for_serving()  # same process tuning as the gRPC server (utils/gc_tuning.py)
     run(max(1, a.warmup), record=False)
     sync()
     pipe.reset_stats()
