@@ -23,7 +23,7 @@ EOF
 
 run_preset() {  # preset port candidates id_mode qps...
   local preset=$1 port=$2 cand=$3 idm=$4; shift 4
-  timeout -k 10 400 python -u -m distributed_tf_serving_amd.serving.server --preset "$preset" --port "$port" \
+  timeout -k 10 400 python -u -m distributed_tf_serving_amd.serving.server --preset "$preset" --port "$port" --grpc-workers "${GRPC_WORKERS:-32}" \
       > "$OUT/server_$preset.log" 2>&1 &
   local spid=$!
   if ! wait_port "$port"; then echo "server $preset did not come up"; kill "$spid"; return 1; fi
@@ -54,5 +54,5 @@ if [ "${CLOSED_LOOP:-0}" = 1 ]; then
   exit $rc
 fi
 
-run_preset deepfm_1gpu 9999 512 zipf 250 500 1000 2000 && \
-run_preset reference_dcn 9998 1500 reference 250 500 1000
+run_preset deepfm_1gpu 9999 512 zipf ${DEEPFM_QPS:-250 500 1000 2000} && \
+{ [ "${SKIP_DCN:-0}" = 1 ] || run_preset reference_dcn 9998 1500 reference 250 500 1000; }
