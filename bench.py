@@ -1,36 +1,36 @@
 #!/usr/bin/env python
-"""Flagship serving benchmark: DeepFM CTR fan-out over N MI355X GPUs.
+"""Flagship serving benchmark: DeepFM CTR served by the native live server on N MI355X GPUs.
 
-Metric (BASELINE.json): CTR scores/sec for the whole node (+ request latency).
-Config: DeepFM-style CTR, 1M x 64 bf16 embeddings, 43 fields, 3-layer MLP
-(1024-512-256), client requests of 512 candidates (BASELINE config 2), fanned
-out over N GPUs with RCCL all-to-all over xGMI (config 3 at N=4).
+Metric (BASELINE.json): CTR scores/sec for the whole node + p50 request latency
+at a fixed QPS. Config: DeepFM-style CTR, 1M x 64 bf16 embeddings, 43 fields,
+3-layer MLP (1024-512-256), client requests of 512 candidates (BASELINE config
+2); at N > 1 every request's candidates are fanned out over all GPUs with RCCL
+all-to-all over xGMI (config 3 at N=4).
 
-One timed step, on every rank, is a full serving round:
+What is timed is the SERVED path, the one the gRPC front door and in-process
+clients use (serving/live.py -> csrc/runtime/live_server.cpp):
 
-  1. ingest ``R`` serialized PredictRequests (512 candidates each; synthetic
-     Zipf feature ids, uniform weights; TF ``tensor_content`` encoding). With
-     ``--ingest arena`` (default) the native host code parses every request's
-     protobuf framing in its pinned receive arena and writes descriptors; one
-     SDMA copy moves the arena and a GPU kernel unpacks the candidate rows.
-     With ``--ingest packed`` the host thread pool decodes rows itself;
-  2. RCCL all-to-all of candidate rows over all GPUs -> model forward (gfx950
-     kernels, one HIP graph) -> all-to-all of scores back -> D2H;
-  3. encode R PredictResponses (``prediction_node`` float_val).
+  client threads (native load generator, csrc/runtime/loadgen.cpp) submit
+  serialized PredictRequests (synthetic Zipf ids, uniform weights, TF
+  ``tensor_content``) -> validation + admission into the open dynamic batch ->
+  ONE copy of the request bytes into a pinned arena -> launcher thread: batch
+  closed at max rows (32 x 512 = 16384) / timeout, framing parse, SDMA H2D,
+  step kernels (GPU unpack + gather + FM + MFMA GEMMs + fused head; at N > 1 the
+  native fan-out step with its two all-to-alls) -> completer thread: bounded
+  wait, one PredictResponse encoded per request -> the client's completion.
 
-Four pipeline slots, three steps in flight: ingest of step k+3, the H2D of
-k+1..k+2, the forward of k and the encode of k-1 overlap. Nothing is cached
-across steps: every step re-parses and scores request bytes from a rotating
-pool of distinct requests. Per-GPU work is fixed as N grows (weak scaling):
-global batch = N * R * 512 candidates/step.
-
-``--model`` picks the BASELINE config's preset: deepfm (configs 2/3), dlrm
-(config 4: 100M-row tables sharded over the ranks), dcn_v2 (config 5: fp8
-towers).
+One "step" = one GPU batch = ``--requests-per-gpu`` requests on every rank.
+The closed loop keeps ``(slots + 2) x R`` requests outstanding; the clock runs
+from the completion that ends warmup step W to the one that ends step W + K,
+inside one continuous run (the pipeline stays primed across the boundary).
+N=1 also reports: scores checked against an fp32 CPU forward of the same
+weights, the p50/p99 of an open-loop run at ``--qps`` (fixed offered load), and
+the literal config-2 point (one 512-candidate request per step, concurrency 1).
 
 Launch: ``python bench.py`` (1 GPU) or, for N GPUs,
 ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
-127.0.0.1 --master-port P bench.py --gpus N``.
+127.0.0.1 --master-port P bench.py --gpus N``. ``--loop replay`` runs the
+engine-only replay loop of round 1 (diagnostic, not the served path).
 """
 from __future__ import annotations
 
@@ -50,7 +50,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
-from distributed_tf_serving_amd.config import ModelConfig, load_preset  # noqa: E402
+from distributed_tf_serving_amd.config import ModelConfig, ServingConfig, load_preset  # noqa: E402
 from distributed_tf_serving_amd.parallel.embedding_sharding import (MI355X_HBM_BYTES,  # noqa: E402
                                                                     build_parallel_model)
 from distributed_tf_serving_amd.ops import native  # noqa: E402
@@ -58,6 +58,7 @@ from distributed_tf_serving_amd.parallel.dist import init_from_env, shutdown  # 
 from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E402
 from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E402
 from distributed_tf_serving_amd.serving.arena import ArenaLayout  # noqa: E402
+from distributed_tf_serving_amd.serving.live import LiveScheduler  # noqa: E402
 from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
@@ -86,43 +87,41 @@ def parse_args():
     ap.add_argument("--model", default="deepfm", choices=["deepfm", "dcn", "dcn_v2", "wdl", "dlrm"])
     ap.add_argument("--request-rows", type=int, default=512, help="candidates per client request (config batch)")
     ap.add_argument("--requests-per-gpu", type=int, default=32,
-                    help="requests coalesced per GPU per step (32 x 512 = 16384 rows = the preset's max batch; "
-                         "16 halves p50 latency for ~20%% less throughput)")
-    ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"])
+                    help="requests per GPU batch (32 x 512 = 16384 rows = the preset's max batch)")
+    ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"],
+                    help="N > 1: alltoall = every request fanned out over all GPUs (config 3); local = one "
+                         "independent replica per GPU; scatter = rank 0 is the only front door")
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")
-    ap.add_argument("--ingest", default="arena", choices=["arena", "packed"],
-                    help="arena: host parses framing, GPU unpacks raw request bytes; packed: host decodes rows")
     ap.add_argument("--decode-threads", type=int, default=4,
                     help="native host pool per rank (4 measured best on a 16-CPU MI355X slice)")
-    ap.add_argument("--pool", type=int, default=8, help="distinct pre-serialized steps per rank")
+    ap.add_argument("--client-threads", type=int, default=8, help="load-generator submitting threads per rank")
+    ap.add_argument("--pool", type=int, default=64, help="distinct pre-serialized requests per rank")
     ap.add_argument("--gemm-dtype", default=None, choices=["bf16", "fp8"],
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight = slots - 1)")
-    ap.add_argument("--loop", default="native", choices=["native", "python"],
-                    help="native: per-step host loop in C++ (csrc/runtime/serving_loop.cpp); python: StepPipeline")
+    ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight)")
+    ap.add_argument("--batch-timeout-us", type=int, default=200)
+    ap.add_argument("--qps", type=float, default=20000.0,
+                    help="N=1: offered load of the fixed-QPS latency run (requests/s; 0 = skip)")
+    ap.add_argument("--qps-seconds", type=float, default=1.0)
+    ap.add_argument("--loop", default="live", choices=["live", "replay", "python"],
+                    help="live: the served path (default); replay / python: engine-only diagnostics (round 1)")
     ap.add_argument("--force-fanout", action="store_true",
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--no-native-fanout", action="store_true",
                     help="N>1: issue collectives through torch.distributed instead of the C++ StepRunner")
+    ap.add_argument("--step-timeout-s", type=float, default=30.0,
+                    help="a step not finished by then fails the run instead of hanging it")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
-    ap.add_argument("--diag-skip-host", action="store_true",
-                    help="DIAGNOSTIC ONLY (not a valid measurement): reuse decoded buffers to isolate GPU time")
     return ap.parse_args()
 
 
-def main():
-    a = parse_args()
-    os.environ.setdefault("DTFS_HOST_THREADS", str(max(1, a.decode_threads)))
-    ctx = init_from_env()
+def build(a, ctx):
+    """Model, executor and fan-out engine of this rank (arena ingest)."""
     world, rank = ctx.world, ctx.rank
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = ctx.device
-    torch.manual_seed(1234)
-
     preset = PRESETS.get(a.model)
     cfg = load_preset(preset).model if preset else ModelConfig(family=a.model)
     if a.gemm_dtype:
@@ -142,137 +141,190 @@ def main():
         cfg.table_rows = rows
     model = build_parallel_model(cfg, dev, ctx)
     F = cfg.num_fields
-    layout = PackedLayout(F)
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
-    slots = a.slots
-    ex = ShardExecutor(model, layout, [B], dev, use_graphs=not a.no_graphs, slots=slots)
-    rows_in_max = B * (ctx.world if a.mode == "scatter" else 1)
+    mode = a.mode if world > 1 else ("alltoall" if a.force_fanout else "local")
+    ex = ShardExecutor(model, PackedLayout(F), [B], dev, use_graphs=not a.no_graphs, slots=a.slots)
+    rows_in_max = B * (world if mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
-    eng = FanoutEngine(ex, ctx, mode=a.mode, ingest=a.ingest, arena=arena_layout, force_fanout=a.force_fanout,
+    eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
                        native_fanout=not a.no_native_fanout)
     eng.prepare(B)
     if eng.mode != "local":
         # one synthetic step checked against a local forward on every rank; a
         # failure anywhere switches every rank to the torch.distributed path
         eng.self_check(B, seed=rank)
-    nat = native()
+    return cfg, model, eng, B
 
+
+def request_pool(a, ctx, eng, B, F):
     rows_in = eng.contrib_rows(B)
     n_req = rows_in // a.request_rows
-    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + rank)
-    pool = []
-    for _ in range(max(1, a.pool)):
-        pool.append([synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n_req)])
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank)
+    n = max(1, a.pool) if n_req else 0
+    return [synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n)], n_req
 
-    diag_pb = nat.parse_batch(pool[0], "feat_ids", "feat_wts", F) if pool[0] else None
 
-    if a.ingest == "arena":
-        # Requests are received into pinned arenas (a ring of a.pool receive
-        # buffers, as an RDMA / shared-memory transport would deliver them);
-        # every step re-parses its arena's framing on the host and the GPU
-        # unpacks the raw payloads (csrc/kernels/ingest.hip).
-        arenas, spans = [], []
-        for reqs in pool:
-            ar = arena_layout.alloc(pin=dev.type == "cuda")
-            spans.append(arena_layout.place(ar, reqs) if reqs else [])
-            arenas.append(ar)
+def fp32_check(cfg, model, live, request: bytes) -> dict:
+    """Scores of one served request vs an fp32 forward of the same weights on
+    the CPU (the ops' reference math)."""
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
+
+    if model.param_bytes() > (4 << 30):
+        return {"status": "skipped (model too large for a CPU copy)"}
+    ref = build_model(cfg, "cpu")
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    if cfg.gemm_dtype == "fp8":
+        for m in ref.modules():
+            if hasattr(m, "quantize_fp8") and getattr(m, "fp8", False):
+                m.quantize_fp8()
+    req = pb.PredictRequest.FromString(request)
+    ids = torch.from_numpy(T.to_ndarray(req.inputs["feat_ids"]))
+    wts = torch.from_numpy(T.to_ndarray(req.inputs["feat_wts"]))
+    want = ref(ids, wts).float()
+    resp = pb.PredictResponse.FromString(live.predict_bytes(request, 30.0))
+    got = torch.from_numpy(T.to_ndarray(resp.outputs["prediction_node"]))
+    diff = float((got - want).abs().max())
+    tol = 5e-2 if cfg.gemm_dtype == "fp8" else 2e-2
+    return {"status": "ok" if diff <= tol else "MISMATCH", "max_abs_diff": round(diff, 6), "tol": tol,
+            "rows": int(got.numel())}
+
+
+def pct(lat_us, q):
+    return round(float(np.percentile(lat_us, q)) * 1e-3, 3) if len(lat_us) else None
+
+
+def run_live(a, ctx, cfg, model, eng, B):
+    world, rank, dev = ctx.world, ctx.rank, ctx.device
+    F = cfg.num_fields
+    R = a.requests_per_gpu
+    pool, n_req = request_pool(a, ctx, eng, B, F)
+    lockstep = eng.mode != "local"
+    conc = (a.slots + 2) * max(1, n_req)
+    # lockstep (fan-out): every rank launches exactly this many steps, empty
+    # ones included, so the collectives of the last steps always pair up
+    max_steps = a.warmup + a.steps + -(-conc // max(1, n_req)) + 4 if lockstep else -1
+    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=(B,), batch_timeout_us=a.batch_timeout_us,
+                       max_queued_rows=1 << 24, max_request_rows=1 << 20)
+    live = LiveScheduler(eng, sc, buckets=[B], depth=a.slots, lockstep=lockstep, max_steps=max_steps,
+                         step_timeout_s=a.step_timeout_s, start_paused=lockstep)
+    extra = {}
+    if world == 1 and pool:
+        extra["fp32_check"] = fp32_check(cfg, model, live, pool[0])
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if ctx.is_distributed:
+            dist.barrier()
+
+    tune_for_serving()  # same process tuning as the gRPC server (utils/gc_tuning.py)
+    sync()
+    if lockstep:
+        live.resume()  # every rank is past its start-up collectives: the step cadence may begin
+    if pool:
+        r = live.run_load(pool, warmup=a.warmup * n_req, count=a.steps * n_req, concurrency=conc,
+                          threads=a.client_threads, timeout_us=int(a.step_timeout_s * 1e6))
+    else:  # a rank without requests (scatter followers): its steps run in lockstep with rank 0's
+        r = {"window_us": 0.0, "latency_us": [], "errors": 0, "ok": 0}
+    if lockstep:
+        live.close()  # finishes the fixed-length run (empty steps until max_steps)
+    sync()
+    window_s = r["window_us"] * 1e-6
+    if r["errors"] and rank == 0:
+        print(f"warning: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr)
+    lat = r["latency_us"]
+    extra["p50_request_ms"], extra["p99_request_ms"] = pct(lat, 50), pct(lat, 99)
+    extra["requests_failed"] = int(r["errors"])
+
+    if world == 1 and pool and not lockstep:
+        if a.qps > 0:
+            n = max(200, int(a.qps * a.qps_seconds))
+            q = live.run_load(pool, warmup=n // 10, count=n, qps=a.qps, threads=a.client_threads,
+                              timeout_us=int(a.step_timeout_s * 1e6))
+            extra["fixed_qps"] = {"qps": a.qps, "request_rows": a.request_rows,
+                                  "scores_per_s": round(a.qps * a.request_rows, 1),
+                                  "p50_ms": pct(q["latency_us"], 50), "p99_ms": pct(q["latency_us"], 99),
+                                  "errors": int(q["errors"])}
+            extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
+        # BASELINE config 2 literally: one 512-candidate request at a time
+        c1 = live.run_load(pool, warmup=20, count=300, concurrency=1, threads=1,
+                           timeout_us=int(a.step_timeout_s * 1e6))
+        w = c1["window_us"] * 1e-6
+        extra["config2_batch512"] = {"concurrency": 1, "p50_ms": pct(c1["latency_us"], 50),
+                                     "p99_ms": pct(c1["latency_us"], 99),
+                                     "scores_per_s": round(300 * a.request_rows / w, 1) if w > 0 else None}
+    st = live.stats()
+    extra["server"] = {k: st[k] for k in ("steps", "full_steps", "timeout_steps", "eager_steps", "empty_steps",
+                                          "blocked_submits")}
+    if a.json_extra and rank == 0:
+        per = {k: round(st[k] / max(1, st["steps"]), 1) for k in ("copy_us", "build_us", "launch_us", "wait_us",
+                                                                  "encode_us")}
+        print(json.dumps({"server_us_per_step": per, "stats": st}), file=sys.stderr, flush=True)
+    live.close()
+    return window_s, extra
+
+
+def run_replay(a, ctx, cfg, model, eng, B):
+    """Round-1 engine-only loop (diagnostic): pre-placed arenas replayed by the
+    C++ ServingLoop or the Python StepPipeline. Not the served path."""
+    world, rank, dev = ctx.world, ctx.rank, ctx.device
+    F = cfg.num_fields
+    pool, n_req = request_pool(a, ctx, eng, B, F)
+    pool = [pool[i * n_req:(i + 1) * n_req] for i in range(max(1, len(pool) // max(1, n_req)))] if n_req else [[]]
+    arena_layout = eng.arena
+    nat = native()
+    arenas, spans = [], []
+    for reqs in pool:
+        ar = arena_layout.alloc(pin=dev.type == "cuda")
+        spans.append(arena_layout.place(ar, reqs) if reqs else [])
+        arenas.append(ar)
 
     def decode(k: int, slot: int):
-        reqs = pool[k % len(pool)]
-        if not reqs:
+        if not pool[k % len(pool)]:
             return None
-        if a.ingest == "arena":
-            ab = arena_layout.build(arenas[k % len(pool)], spans[k % len(pool)])
-            errs = [e for e in ab.errors if e]
-            if errs:
-                raise RuntimeError(errs[0])
-            return (ab, arenas[k % len(pool)])
-        if a.diag_skip_host and k >= 2:  # diagnostic only: GPU pipeline without host decode
-            return diag_pb
-        pb = nat.parse_batch(reqs, "feat_ids", "feat_wts", F)
-        buf = eng.host_in(B, slot)
-        ids_v, wts_v = layout.ids(buf), layout.wts(buf)
-        pb.decode(ids_v, wts_v)  # row chunks spread over the native host pool (DTFS_HOST_THREADS)
-        errs = [e for e in pb.errors if e]
+        ab = arena_layout.build(arenas[k % len(pool)], spans[k % len(pool)])
+        errs = [e for e in ab.errors if e]
         if errs:
             raise RuntimeError(errs[0])
-        return pb
-
-    def encode(pb, scores: torch.Tensor):
-        if pb is None:
-            return []
-        if isinstance(pb, tuple):
-            pb = pb[0]
-        return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores,
-                                          list(pb.rows), list(pb.offsets))
+        return (ab, arenas[k % len(pool)])
 
     def launch(k: int, slot: int, ctx_k):
-        if a.ingest == "arena" and ctx_k is not None:
+        if ctx_k is not None:
             ab, ar = ctx_k
             return eng.launch(B, slot, src=ar, nbytes=ab.used_bytes)
-        if a.ingest == "arena":  # a rank with no requests (scatter mode, rank > 0)
-            return eng.launch(B, slot, nbytes=0)
-        return eng.launch(B, slot)
+        return eng.launch(B, slot, nbytes=0)
 
-    score_check = {"steps": 0, "mismatched_steps": 0}
-    use_native_loop = a.loop == "native" and dev.type == "cuda" and a.ingest == "arena" and not a.no_graphs
-    if use_native_loop:
-        try:
-            loop_slots = eng.loop_slots(B)
-        except RuntimeError as e:  # e.g. a forward with collectives (sharded DLRM): Python pipeline
-            if rank == 0:
-                print(f"note: native loop unavailable ({e}); using the Python pipeline", file=sys.stderr)
-            use_native_loop = False
-    if use_native_loop:
-        # the whole per-step host loop in C++ (csrc/runtime/serving_loop.cpp):
-        # parse(k+3) || H2D(k+1..k+2) [SDMA] || step graph(k) [GPU] || encode(k-1)
+    def encode(pb_, scores):
+        if pb_ is None:
+            return []
+        ab = pb_[0]
+        return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores, list(ab.rows),
+                                          list(ab.offsets))
+
+    if a.loop == "replay" and dev.type == "cuda" and not a.no_graphs:
         from distributed_tf_serving_amd.ops import hip
 
-        nloop = hip().ServingLoop(eng.runner(), dict(depth=slots - 1, fields=F, max_rows=arena_layout.max_rows,
-                                                     varint_chunks=arena_layout.varint_chunks,
-                                                     version=1), loop_slots)
+        nloop = hip().ServingLoop(eng.runner(), dict(depth=a.slots - 1, fields=F, max_rows=arena_layout.max_rows,
+                                                     varint_chunks=arena_layout.varint_chunks, version=1),
+                                  eng.loop_slots(B))
         for ar, sp in zip(arenas, spans):
             nloop.add_input(ar, sp)
-        lat: list = []
-        phase = {"parse": 0.0, "launch": 0.0, "gpu_wait": 0.0, "encode": 0.0}
-        n_inputs = len(arenas)
+        lat = []
 
-        def run(n_steps: int, record: bool):
+        def run(n_steps, record):
             st = nloop.run(n_steps, record)
             if st["errors"]:
                 raise RuntimeError(f"{st['errors']} requests failed in the native loop")
             if record:
-                # every replay of one input must give the same scores: a step
-                # whose scores the host read before they landed shows up here
-                ref = {}
-                for k, v in enumerate(st["score_sum"]):
-                    r = ref.setdefault(k % n_inputs, v)
-                    if abs(v - r) > 1e-6 * max(1.0, abs(r)):
-                        score_check["mismatched_steps"] += 1
-                score_check["steps"] += len(st["score_sum"])
-                lat.extend(x * 1e-6 for x in st["latency_us"])
-                for k_src, k_dst in (("parse_us", "parse"), ("launch_us", "launch"), ("wait_us", "gpu_wait"),
-                                     ("encode_us", "encode")):
-                    phase[k_dst] += st[k_src] * 1e-6
-
-        class _NoPipe:
-            def reset_stats(self):
-                lat.clear()
-                for k in phase:
-                    phase[k] = 0.0
-
-            def close(self):
-                pass
-
-        pipe = _NoPipe()
+                lat.extend(st["latency_us"])
     else:
-        # decode(k+3) || H2D(k+1..k+2) [SDMA] || forward(k) [GPU] || encode(k-1)
-        pipe = StepPipeline(eng, B, slots=slots, depth=slots - 1, produce=decode,
-                            consume=lambda k, pb, scores: encode(pb, scores), launch=launch)
-        phase = pipe.phase
+        pipe = StepPipeline(eng, B, slots=a.slots, depth=a.slots - 1, produce=decode,
+                            consume=lambda k, pb_, scores: encode(pb_, scores), launch=launch)
         lat = pipe.latencies
 
-        def run(n_steps: int, record: bool):
+        def run(n_steps, record):
             pipe.run(n_steps, record=record)
 
     def sync():
@@ -283,24 +335,52 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    tune_for_serving()  # same process tuning as the gRPC server (utils/gc_tuning.py)
+    tune_for_serving()
     run(max(1, a.warmup), record=False)
     sync()
-    pipe.reset_stats()
     t0 = time.perf_counter()
     run(a.steps, record=True)
     sync()
     el = time.perf_counter() - t0
+    lat_us = [x if a.loop == "replay" else x * 1e6 for x in lat]
+    return el, {"p50_request_ms": pct(lat_us, 50), "p99_request_ms": pct(lat_us, 99),
+                "note": "engine-only replay loop (diagnostic), not the served path"}
+
+
+def main():
+    a = parse_args()
+    if os.environ.get("DTFS_HANG_DUMP_S"):  # debugging aid: every thread's stack, then exit
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["DTFS_HANG_DUMP_S"]), exit=True)
+    os.environ.setdefault("DTFS_HOST_THREADS", str(max(1, a.decode_threads)))
+    ctx = init_from_env()
+    world, rank = ctx.world, ctx.rank
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = ctx.device
+    torch.manual_seed(1234)
+    cfg, model, eng, B = build(a, ctx)
+    if a.loop == "live":
+        el, extra = run_live(a, ctx, cfg, model, eng, B)
+    else:
+        el, extra = run_replay(a, ctx, cfg, model, eng, B)
 
     t = torch.tensor([el], dtype=torch.float64, device=dev if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
     total_scores = world * B * a.steps
-    value = total_scores / el_max
-    p50 = statistics.median(lat) * 1e3 if lat else None
-    p99 = float(np.percentile(lat, 99)) * 1e3 if lat else None
+    value = total_scores / el_max if el_max > 0 else 0.0
     if rank == 0:
+        if eng.mode == "local":
+            par = f"candidate-dp{world} (" + ("one GPU, no fan-out" if world == 1 else
+                                              "one independent replica per GPU, no collectives") + ")"
+        else:
+            par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
+                   + (", native C++ step" if eng.native_fanout_active else ", torch.distributed") + ")")
+        if hasattr(model, "plan"):
+            par += f" + embedding-mp{world} ({len(model.plan.row_wise())} row-wise tables, all-to-all)"
         out = {
             "metric": "CTR scores/sec (whole node)",
             "value": round(value, 1),
@@ -320,23 +400,14 @@ def main():
                 "request_rows": a.request_rows,
                 "requests_per_gpu_per_step": a.requests_per_gpu,
                 "seq_len": None,
-                "parallelism": f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
-                               + (", native C++ step" if eng.native_fanout_active else "") + ")" + (
-                    f" + embedding-mp{world} ({len(model.plan.row_wise())} row-wise tables, all-to-all)"
-                    if hasattr(model, "plan") else ""),
+                "parallelism": par,
                 "encoding": a.encoding,
+                "path": ("served: native live server (batching, arena copy, parse, step, encode) driven by "
+                         "in-process native client threads") if a.loop == "live" else f"engine-only {a.loop} loop",
             },
-            "p50_request_ms": None if p50 is None else round(p50, 3),
-            "p99_request_ms": None if p99 is None else round(p99, 3),
         }
-        if score_check["steps"]:
-            out["score_check"] = ("ok" if not score_check["mismatched_steps"] else
-                                  f"{score_check['mismatched_steps']}/{score_check['steps']} steps differ")
+        out.update(extra)
         print(json.dumps(out), flush=True)
-        if a.json_extra:
-            per = {k: round(v / a.steps * 1e6, 1) for k, v in phase.items()}
-            print(json.dumps({"host_phase_us_per_step": per}), file=sys.stderr, flush=True)
-    pipe.close()
     shutdown()
 
 

@@ -13,6 +13,7 @@
 #include "kernels/launchers.h"
 #include "comm/rccl_comm.h"
 #include "runtime/serving_loop.h"
+#include "live_bindings.h"
 #include "runtime/step_runner.h"
 
 namespace {
@@ -539,6 +540,39 @@ struct PyServingLoop {
   std::vector<py::object> keep;
 };
 
+// One native loop slot from its Python description (FanoutEngine.loop_slots).
+dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object>* keep) {
+  keep->push_back(d);
+  dtfs::runtime::LoopSlot s;
+  torch::Tensor h_out = d["h_out"].cast<torch::Tensor>();
+  TORCH_CHECK(h_out.device().is_cpu() && h_out.is_pinned() && h_out.scalar_type() == torch::kFloat32 &&
+                  h_out.is_contiguous(),
+              "h_out must be a pinned contiguous fp32 tensor");
+  s.h_out = h_out.data_ptr<float>();
+  s.h_out_len = h_out.numel();
+  torch::Tensor dst = d["h2d_dst"].cast<torch::Tensor>();
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_dst must be a contiguous GPU tensor");
+  if (d.contains("fanout") && d["fanout"].cast<bool>()) {
+    s.fanout = true;
+    s.fan = make_fanout_step(dst, d["ingress_exec"].cast<uintptr_t>(), d["cin"].cast<dtfs::comm::RcclComm&>(),
+                             d["mode"].cast<int>(), d["send"].cast<torch::Tensor>(), d["recv"].cast<torch::Tensor>(),
+                             d["forward_exec"].cast<uintptr_t>(), d["cout"].cast<dtfs::comm::RcclComm&>(),
+                             d["scores"].cast<torch::Tensor>(), d["back"].cast<torch::Tensor>(), h_out,
+                             d["d2h_bytes"].cast<int64_t>());
+    if (d.contains("forward_seq") && !d["forward_seq"].is_none())
+      s.fan.forward_seq = &d["forward_seq"].cast<dtfs::runtime::KernelSequence&>();
+    if (d.contains("ingress_seq") && !d["ingress_seq"].is_none())
+      s.fan.ingress_seq = &d["ingress_seq"].cast<dtfs::runtime::KernelSequence&>();
+  } else {
+    s.h2d_dst = dst.data_ptr();
+    s.h2d_cap = int64_t(dst.nbytes());
+    if (d.contains("seq") && !d["seq"].is_none()) s.seq = &d["seq"].cast<dtfs::runtime::KernelSequence&>();
+    if (d.contains("graph_exec")) s.graph = reinterpret_cast<hipGraphExec_t>(d["graph_exec"].cast<uintptr_t>());
+    TORCH_CHECK(s.graph != nullptr || s.seq != nullptr, "slot needs a step graph or kernel sequence");
+  }
+  return s;
+}
+
 PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list slots) {
   auto* p = new PyServingLoop();
   p->keep.push_back(runner_obj);
@@ -555,38 +589,94 @@ PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list s
   if (cfg.contains("output_key")) c.output_key = cfg["output_key"].cast<std::string>();
   if (cfg.contains("version") && !cfg["version"].is_none()) c.version = cfg["version"].cast<int64_t>();
   std::vector<dtfs::runtime::LoopSlot> ls;
-  for (auto item : slots) {
-    py::dict d = item.cast<py::dict>();
-    p->keep.push_back(d);
-    dtfs::runtime::LoopSlot s;
-    torch::Tensor h_out = d["h_out"].cast<torch::Tensor>();
-    TORCH_CHECK(h_out.device().is_cpu() && h_out.is_pinned() && h_out.scalar_type() == torch::kFloat32 &&
-                    h_out.is_contiguous(),
-                "h_out must be a pinned contiguous fp32 tensor");
-    s.h_out = h_out.data_ptr<float>();
-    s.h_out_len = h_out.numel();
-    torch::Tensor dst = d["h2d_dst"].cast<torch::Tensor>();
-    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_dst must be a contiguous GPU tensor");
-    if (d.contains("fanout") && d["fanout"].cast<bool>()) {
-      s.fanout = true;
-      s.fan = make_fanout_step(dst, d["ingress_exec"].cast<uintptr_t>(), d["cin"].cast<dtfs::comm::RcclComm&>(),
-                               d["mode"].cast<int>(), d["send"].cast<torch::Tensor>(), d["recv"].cast<torch::Tensor>(),
-                               d["forward_exec"].cast<uintptr_t>(), d["cout"].cast<dtfs::comm::RcclComm&>(),
-                               d["scores"].cast<torch::Tensor>(), d["back"].cast<torch::Tensor>(), h_out,
-                               d["d2h_bytes"].cast<int64_t>());
-      if (d.contains("forward_seq") && !d["forward_seq"].is_none())
-        s.fan.forward_seq = &d["forward_seq"].cast<dtfs::runtime::KernelSequence&>();
-      if (d.contains("ingress_seq") && !d["ingress_seq"].is_none())
-        s.fan.ingress_seq = &d["ingress_seq"].cast<dtfs::runtime::KernelSequence&>();
-    } else {
-      s.h2d_dst = dst.data_ptr();
-      if (d.contains("seq") && !d["seq"].is_none()) s.seq = &d["seq"].cast<dtfs::runtime::KernelSequence&>();
-      if (d.contains("graph_exec")) s.graph = reinterpret_cast<hipGraphExec_t>(d["graph_exec"].cast<uintptr_t>());
-      TORCH_CHECK(s.graph != nullptr || s.seq != nullptr, "slot needs a step graph or kernel sequence");
-    }
-    ls.push_back(s);
-  }
+  for (auto item : slots) ls.push_back(loop_slot_from(item.cast<py::dict>(), &p->keep));
   p->loop = std::make_unique<dtfs::runtime::ServingLoop>(&runner, c, std::move(ls));
+  return p;
+}
+
+// ---------------------------------------------------------------- live server (GPU backend)
+// The device side of a GPU live server: the StepRunner plus, per bucket and
+// slot, the step to launch (direct kernel launches of the captured step, its
+// graph, or the fan-out step with its RCCL communicators).
+class GpuBackend : public dtfs::runtime::StepBackend {
+ public:
+  GpuBackend(dtfs::runtime::StepRunner* runner, std::vector<int64_t> buckets,
+             std::vector<std::vector<dtfs::runtime::LoopSlot>> slots)
+      : runner_(runner), buckets_(std::move(buckets)), slots_(std::move(slots)) {
+    TORCH_CHECK(!slots_.empty() && slots_.size() == buckets_.size(), "one slot list per bucket");
+    const size_t S = slots_[0].size();
+    TORCH_CHECK(S >= 1 && int(S) <= runner_->slots(), "slot count must be in [1, runner slots]");
+    for (const auto& v : slots_) TORCH_CHECK(v.size() == S, "every bucket needs the same number of slots");
+    for (const auto& v : slots_)
+      for (const auto& s : v)
+        if (s.fanout)
+          for (auto* c : {s.fan.cin, s.fan.cout})
+            if (std::find(comms_.begin(), comms_.end(), c) == comms_.end()) comms_.push_back(c);
+  }
+  int slots() const override { return int(slots_[0].size()); }
+  const std::vector<int64_t>& buckets() const override { return buckets_; }
+  void launch(int slot, int b, const uint8_t* arena, const dtfs::runtime::ArenaBatch& batch) override {
+    const auto& s = slots_[size_t(b)][size_t(slot)];
+    // the header + descriptors always travel, so an empty (lockstep) step
+    // sees zero rows instead of the slot's previous batch
+    const int64_t nbytes = batch.used_bytes;
+    if (s.fanout) {
+      dtfs::runtime::FanoutStep f = s.fan;
+      f.h2d_src = arena;
+      f.h2d_bytes = nbytes;
+      runner_->launch_fanout(slot, f);
+    } else {
+      if (nbytes > s.h2d_cap) throw std::runtime_error("batch larger than the device arena");
+      if (s.seq) runner_->launch_seq(slot, s.h2d_dst, arena, nbytes, s.seq, batch.n_gpu_varint == 0);
+      else runner_->launch(slot, s.h2d_dst, arena, nbytes, s.graph);
+    }
+  }
+  bool wait(int slot, int64_t timeout_us, std::string* err) override {
+    return runner_->wait_for(slot, timeout_us, comms_, err);
+  }
+  const float* scores(int slot, int b) const override { return slots_[size_t(b)][size_t(slot)].h_out; }
+  int64_t scores_len(int slot, int b) const override { return slots_[size_t(b)][size_t(slot)].h_out_len; }
+  void abort() override {
+    for (auto* c : comms_)
+      if (c && !c->aborted()) c->abort();
+  }
+
+ private:
+  dtfs::runtime::StepRunner* runner_;
+  std::vector<int64_t> buckets_;
+  std::vector<std::vector<dtfs::runtime::LoopSlot>> slots_;  // [bucket][slot]
+  std::vector<dtfs::comm::RcclComm*> comms_;
+};
+
+struct PyGpuLive {
+  std::vector<py::object> keep;
+  std::unique_ptr<GpuBackend> backend;
+  std::unique_ptr<dtfs::runtime::LiveServer> srv;
+  ~PyGpuLive() {
+    py::gil_scoped_release nogil;
+    srv.reset();
+  }
+};
+
+// buckets: [(rows, [slot dict per slot]), ...] ascending.
+PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, py::list arenas) {
+  auto* p = new PyGpuLive();
+  p->keep.push_back(runner_obj);
+  auto& runner = runner_obj.cast<dtfs::runtime::StepRunner&>();
+  std::vector<int64_t> rows;
+  std::vector<std::vector<dtfs::runtime::LoopSlot>> slots;
+  for (auto item : buckets) {
+    py::tuple t = item.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 2, "bucket entries are (rows, slots)");
+    rows.push_back(t[0].cast<int64_t>());
+    std::vector<dtfs::runtime::LoopSlot> v;
+    for (auto d : t[1].cast<py::list>()) v.push_back(loop_slot_from(d.cast<py::dict>(), &p->keep));
+    slots.push_back(std::move(v));
+  }
+  auto ar = dtfs_live::arenas_from(arenas, true, &p->keep);
+  p->backend = std::make_unique<GpuBackend>(&runner, std::move(rows), std::move(slots));
+  p->srv = std::make_unique<dtfs::runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg),
+                                                       std::move(ar));
   return p;
 }
 
@@ -724,6 +814,14 @@ PYBIND11_MODULE(_hip, m) {
           },
           py::arg("n_steps"), py::arg("record") = true)
       .def_property_readonly("slots", [](const PyServingLoop& p) { return p.loop->slots(); });
+
+  {
+    py::class_<PyGpuLive> c(m, "LiveServer",
+                            "Live serving core (csrc/runtime/live_server.h) on this GPU: requests are batched into "
+                            "pinned arenas and run as captured step kernels (or the fan-out step)");
+    c.def(py::init(&make_gpu_live), py::arg("runner"), py::arg("config"), py::arg("buckets"), py::arg("arenas"));
+    dtfs_live::def_live_methods(c);
+  }
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });

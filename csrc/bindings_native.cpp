@@ -12,6 +12,7 @@
 #include "runtime/thread_pool.h"
 #include "runtime/trace.h"
 #include "wire/tensor_codec.h"
+#include "live_bindings.h"
 
 namespace py = pybind11;
 using namespace dtfs;
@@ -174,6 +175,13 @@ std::shared_ptr<ParsedBatch> parse_batch(const std::vector<py::bytes>& reqs, con
       const int64_t n_el = ti->num_elements();
       if ((ti->content.n == 0 && ti->num_values > n_el) || (tw && tw->content.n == 0 && tw->num_values > n_el)) {
         b->errors[i] = "more values than the tensor shape holds";
+        continue;
+      }
+      auto content_ok = [n_el](const wire::TensorView* t) {
+        return !t || t->content.n == 0 || t->content.n == size_t(n_el) * wire::element_size(t->dtype);
+      };
+      if (!content_ok(ti) || !content_ok(tw)) {
+        b->errors[i] = "tensor_content size does not match shape";
         continue;
       }
       b->ids_t[i] = ti;
@@ -396,6 +404,92 @@ wire::ModelSpecOut spec_of(const std::string& name, const std::string& sig, py::
   return s;
 }
 
+// ---------------------------------------------------------------- live server (CPU backend)
+// The device side of a CPU live server is a Python callable
+// forward(arena_index, slot, bucket_index) that scores the parsed arena into
+// scores[slot][bucket_index] (serving/live.py: FanoutEngine.launch on CPU).
+// Used for BASELINE config 1 (Wide&Deep-tiny on a CPU backend) and to test the
+// batching core without a GPU.
+class PyCpuBackend : public runtime::StepBackend {
+ public:
+  PyCpuBackend(std::vector<int64_t> buckets, std::vector<std::vector<torch::Tensor>> scores,
+               std::vector<const uint8_t*> arenas, py::function fwd)
+      : buckets_(std::move(buckets)), arenas_(std::move(arenas)), fwd_(std::move(fwd)) {
+    TORCH_CHECK(!scores.empty(), "need at least one slot");
+    for (auto& per_slot : scores) {
+      TORCH_CHECK(per_slot.size() == buckets_.size(), "scores: one tensor per bucket per slot");
+      std::vector<std::pair<const float*, int64_t>> v;
+      for (size_t b = 0; b < per_slot.size(); ++b) {
+        const auto& t = per_slot[b];
+        TORCH_CHECK(t.device().is_cpu() && t.is_contiguous() && t.scalar_type() == torch::kFloat32,
+                    "scores must be contiguous CPU fp32 tensors");
+        v.emplace_back(t.data_ptr<float>(), t.numel());
+      }
+      scores_.push_back(std::move(v));
+    }
+    err_.assign(scores_.size(), std::string());
+  }
+  ~PyCpuBackend() override {
+    py::gil_scoped_acquire g;
+    fwd_ = py::function();
+  }
+  int slots() const override { return int(scores_.size()); }
+  const std::vector<int64_t>& buckets() const override { return buckets_; }
+  void launch(int slot, int b, const uint8_t* arena, const runtime::ArenaBatch&) override {
+    const auto it = std::find(arenas_.begin(), arenas_.end(), arena);
+    if (it == arenas_.end()) throw std::runtime_error("unknown arena");
+    py::gil_scoped_acquire g;
+    try {
+      fwd_(int(it - arenas_.begin()), slot, b);
+      err_[size_t(slot)].clear();
+    } catch (py::error_already_set& e) {
+      err_[size_t(slot)] = e.what();  // reported by wait(): the step failed
+    }
+  }
+  bool wait(int slot, int64_t, std::string* err) override {
+    if (err_[size_t(slot)].empty()) return true;
+    *err = err_[size_t(slot)];
+    return false;
+  }
+  const float* scores(int slot, int b) const override { return scores_[size_t(slot)][size_t(b)].first; }
+  int64_t scores_len(int slot, int b) const override { return scores_[size_t(slot)][size_t(b)].second; }
+
+ private:
+  std::vector<int64_t> buckets_;
+  std::vector<std::vector<std::pair<const float*, int64_t>>> scores_;
+  std::vector<const uint8_t*> arenas_;
+  py::function fwd_;
+  std::vector<std::string> err_;
+};
+
+struct PyCpuLive {
+  std::vector<py::object> keep;
+  std::unique_ptr<PyCpuBackend> backend;
+  std::unique_ptr<runtime::LiveServer> srv;
+  ~PyCpuLive() {
+    py::gil_scoped_release nogil;  // the server threads may need the GIL to finish
+    srv.reset();
+  }
+};
+
+PyCpuLive* make_cpu_live(py::dict cfg, std::vector<int64_t> buckets, py::list scores, py::list arenas,
+                         py::function fwd) {
+  auto* p = new PyCpuLive();
+  auto ar = dtfs_live::arenas_from(arenas, false, &p->keep);
+  std::vector<const uint8_t*> bases;
+  for (auto& a : ar) bases.push_back(a.first);
+  std::vector<std::vector<torch::Tensor>> sc;
+  for (auto per_slot : scores) {
+    std::vector<torch::Tensor> v;
+    for (auto t : per_slot.cast<py::list>()) v.push_back(t.cast<torch::Tensor>());
+    sc.push_back(std::move(v));
+  }
+  p->keep.push_back(scores);
+  p->backend = std::make_unique<PyCpuBackend>(std::move(buckets), std::move(sc), std::move(bases), fwd);
+  p->srv = std::make_unique<runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg), std::move(ar));
+  return p;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -544,6 +638,15 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("batch_timeout_us", &runtime::DynamicBatcher::batch_timeout_us)
       .def("stats", &runtime::DynamicBatcher::stats);
 
+  {
+    py::class_<PyCpuLive> c(m, "LiveServer",
+                            "Live serving core (csrc/runtime/live_server.h) with a CPU backend: a Python "
+                            "forward(arena_index, slot, bucket_index) scores each batch");
+    c.def(py::init(&make_cpu_live), py::arg("config"), py::arg("buckets"), py::arg("scores"), py::arg("arenas"),
+          py::arg("forward"));
+    dtfs_live::def_live_methods(c);
+  }
+  m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
   m.def("now_us", &runtime::now_us);
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));

@@ -1,0 +1,182 @@
+// Python surface of runtime::LiveServer, shared by _native (CPU backend) and
+// _hip (GPU backend). Each module registers its own LiveServer class around a
+// holder type H with members `srv` (std::unique_ptr<LiveServer>) and `keep`
+// (Python objects whose memory the server points into).
+#pragma once
+
+#include <torch/extension.h>
+
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "runtime/batcher.h"
+#include "runtime/live_server.h"
+#include "runtime/loadgen.h"
+
+namespace dtfs_live {
+
+namespace py = pybind11;
+using dtfs::runtime::LiveConfig;
+using dtfs::runtime::LiveServer;
+using dtfs::runtime::Reply;
+
+inline LiveConfig live_config_from(const py::dict& d) {
+  LiveConfig c;
+  auto get = [&](const char* k) { return d.contains(k) && !d[k].is_none(); };
+  if (get("fields")) c.fields = d["fields"].cast<int64_t>();
+  if (get("ids_key")) c.ids_key = d["ids_key"].cast<std::string>();
+  if (get("wts_key")) c.wts_key = d["wts_key"].cast<std::string>();
+  if (get("model_name")) c.model_name = d["model_name"].cast<std::string>();
+  if (get("signature_name")) c.signature_name = d["signature_name"].cast<std::string>();
+  if (get("output_key")) c.output_key = d["output_key"].cast<std::string>();
+  if (get("version")) c.version = d["version"].cast<int64_t>();
+  if (get("max_batch_rows")) c.max_batch_rows = d["max_batch_rows"].cast<int64_t>();
+  if (get("batch_timeout_us")) c.batch_timeout_us = d["batch_timeout_us"].cast<int64_t>();
+  if (get("depth")) c.depth = d["depth"].cast<int>();
+  if (get("varint_chunks")) c.varint_chunks = d["varint_chunks"].cast<int64_t>();
+  if (get("max_pending")) c.max_pending = d["max_pending"].cast<int64_t>();
+  if (get("eager_when_idle")) c.eager_when_idle = d["eager_when_idle"].cast<bool>();
+  if (get("lockstep")) c.lockstep = d["lockstep"].cast<bool>();
+  if (get("max_steps")) c.max_steps = d["max_steps"].cast<int64_t>();
+  if (get("step_timeout_us")) c.step_timeout_us = d["step_timeout_us"].cast<int64_t>();
+  if (get("start_paused")) c.start_paused = d["start_paused"].cast<bool>();
+  return c;
+}
+
+// Host arenas: contiguous uint8 CPU tensors (pinned for a GPU backend).
+inline std::vector<std::pair<uint8_t*, int64_t>> arenas_from(const py::list& arenas, bool need_pinned,
+                                                             std::vector<py::object>* keep) {
+  std::vector<std::pair<uint8_t*, int64_t>> out;
+  for (auto a : arenas) {
+    torch::Tensor t = a.cast<torch::Tensor>();
+    TORCH_CHECK(t.device().is_cpu() && t.is_contiguous() && t.scalar_type() == torch::kUInt8,
+                "arenas must be contiguous CPU uint8 tensors");
+    TORCH_CHECK(!need_pinned || t.is_pinned(), "a GPU live server needs pinned arenas");
+    keep->push_back(py::reinterpret_borrow<py::object>(a));
+    out.emplace_back(t.data_ptr<uint8_t>(), t.numel());
+  }
+  return out;
+}
+
+inline int64_t deadline_from(double timeout_s) {
+  return timeout_s > 0 ? dtfs::runtime::now_us() + int64_t(timeout_s * 1e6) : 0;
+}
+
+inline std::pair<const uint8_t*, size_t> bytes_view(const py::bytes& b) {
+  char* p;
+  Py_ssize_t n;
+  if (PyBytes_AsStringAndSize(b.ptr(), &p, &n) != 0) throw py::error_already_set();
+  return {reinterpret_cast<const uint8_t*>(p), size_t(n)};
+}
+
+template <class H>
+void def_live_methods(py::class_<H>& c) {
+  c.def(
+       "predict",
+       [](H& h, py::bytes data, double timeout_s) {
+         auto v = bytes_view(data);
+         Reply r;
+         {
+           py::gil_scoped_release nogil;
+           r = h.srv->predict(v.first, v.second, deadline_from(timeout_s));
+         }
+         return py::make_tuple(r.code, r.message, py::bytes(r.response));
+       },
+       py::arg("request"), py::arg("timeout_s") = 0.0,
+       "Serve one serialized PredictRequest; returns (code, message, response bytes). code 0 = OK, otherwise a "
+       "gRPC status code (1000: more rows than one batch, split and resubmit).")
+      .def(
+          "submit",
+          [](H& h, py::bytes data, double timeout_s, py::function cb) {
+            auto v = bytes_view(data);
+            // the callback object is released with the GIL held, wherever the
+            // last reference goes away
+            auto fn = std::shared_ptr<py::function>(new py::function(cb), [](py::function* f) {
+              py::gil_scoped_acquire g;
+              delete f;
+            });
+            const int64_t dl = deadline_from(timeout_s);
+            py::gil_scoped_release nogil;
+            h.srv->submit(v.first, v.second, dl, [fn](Reply&& r) {
+              py::gil_scoped_acquire g;
+              try {
+                (*fn)(r.code, r.message, py::bytes(r.response));
+              } catch (py::error_already_set& e) {
+                e.discard_as_unraisable("LiveServer completion callback");
+              }
+            });
+          },
+          py::arg("request"), py::arg("timeout_s"), py::arg("callback"),
+          "Asynchronous submit: callback(code, message, response) runs on the server's completion thread.")
+      .def(
+          "run_load",
+          [](H& h, const std::vector<std::string>& requests, py::dict spec) {
+            dtfs::runtime::LoadSpec s;
+            auto get = [&](const char* k) { return spec.contains(k) && !spec[k].is_none(); };
+            if (get("warmup")) s.warmup = spec["warmup"].cast<int64_t>();
+            if (get("count")) s.count = spec["count"].cast<int64_t>();
+            if (get("tail")) s.tail = spec["tail"].cast<int64_t>();
+            if (get("concurrency")) s.concurrency = spec["concurrency"].cast<int>();
+            if (get("qps")) s.qps = spec["qps"].cast<double>();
+            if (get("poisson")) s.poisson = spec["poisson"].cast<bool>();
+            if (get("threads")) s.threads = spec["threads"].cast<int>();
+            if (get("timeout_us")) s.timeout_us = spec["timeout_us"].cast<int64_t>();
+            if (get("seed")) s.seed = spec["seed"].cast<uint64_t>();
+            dtfs::runtime::LoadResult r;
+            {
+              py::gil_scoped_release nogil;
+              r = dtfs::runtime::run_load(*h.srv, requests, s);
+            }
+            py::dict o;
+            o["latency_us"] = r.latency_us;
+            o["submitted"] = r.submitted;
+            o["ok"] = r.ok;
+            o["errors"] = r.errors;
+            o["window_us"] = r.window_us;
+            o["wall_us"] = r.wall_us;
+            o["first_error"] = r.first_error;
+            o["first_error_code"] = r.first_error_code;
+            return o;
+          },
+          py::arg("requests"), py::arg("spec"),
+          "Native load generator over submit(): closed loop (concurrency) or open loop (qps).")
+      .def(
+          "stats",
+          [](H& h) {
+            auto s = h.srv->stats();
+            py::dict o;
+            o["submitted"] = s.submitted;
+            o["rejected"] = s.rejected;
+            o["completed"] = s.completed;
+            o["failed"] = s.failed;
+            o["expired"] = s.expired;
+            o["steps"] = s.steps;
+            o["rows"] = s.rows;
+            o["padded_rows"] = s.padded_rows;
+            o["empty_steps"] = s.empty_steps;
+            o["full_steps"] = s.full_steps;
+            o["timeout_steps"] = s.timeout_steps;
+            o["eager_steps"] = s.eager_steps;
+            o["blocked_submits"] = s.blocked_submits;
+            o["copy_us"] = s.copy_us;
+            o["build_us"] = s.build_us;
+            o["launch_us"] = s.launch_us;
+            o["wait_us"] = s.wait_us;
+            o["encode_us"] = s.encode_us;
+            o["broken"] = s.broken;
+            o["error"] = s.error;
+            return o;
+          })
+      .def("resume", [](H& h) { h.srv->resume(); })
+      .def("close", [](H& h) {
+        py::gil_scoped_release nogil;
+        h.srv->close();
+      })
+      .def_property_readonly("broken", [](H& h) { return h.srv->broken(); })
+      .def_property_readonly("max_rows", [](H& h) { return h.srv->max_rows(); });
+}
+
+}  // namespace dtfs_live

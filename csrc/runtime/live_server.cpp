@@ -1,0 +1,554 @@
+#include "live_server.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <stdexcept>
+
+#include "../wire/tensor_codec.h"
+#include "batcher.h"  // now_us()
+#include "trace.h"
+
+namespace dtfs {
+namespace runtime {
+
+namespace {
+int64_t align8(int64_t x) { return (x + 7) & ~int64_t(7); }
+
+std::string shape_str(const std::vector<int64_t>& s) {
+  std::string o = "[";
+  for (size_t i = 0; i < s.size(); ++i) o += (i ? ", " : "") + std::to_string(s[i]);
+  return o + "]";
+}
+}  // namespace
+
+LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas)
+    : backend_(backend), cfg_(std::move(cfg)) {
+  if (!backend_) throw std::invalid_argument("null StepBackend");
+  const auto& bk = backend_->buckets();
+  if (bk.empty() || !std::is_sorted(bk.begin(), bk.end()) || bk.front() <= 0)
+    throw std::invalid_argument("buckets must be ascending positive row counts");
+  const int S = backend_->slots();
+  if (S < 1) throw std::invalid_argument("backend has no slots");
+  cfg_.depth = std::max(1, std::min(cfg_.depth, S));
+  max_rows_ = cfg_.max_batch_rows > 0 ? std::min(cfg_.max_batch_rows, bk.back()) : bk.back();
+  if (int(arenas.size()) < cfg_.depth + 2)
+    throw std::invalid_argument("need at least depth + 2 host arenas (one filling, one sealed, depth in flight)");
+  int64_t cap = INT64_MAX;
+  for (const auto& a : arenas) {
+    if (!a.first || a.second <= kArenaPayloadOff + 4096) throw std::invalid_argument("bad host arena");
+    cap = std::min(cap, a.second);
+  }
+  // arena_build appends, after the requests: 64-byte aligned scratch for
+  // host-decoded typed fields, the row table, the varint chunk table and the
+  // device-only decoded-id region; need_of() plans for the worst case of each
+  arena_budget_ = cap - kArenaPayloadOff - 1024;
+  arenas_.resize(arenas.size());
+  for (size_t i = 0; i < arenas.size(); ++i) {
+    arenas_[i].base = arenas[i].first;
+    arenas_[i].capacity = arenas[i].second;
+    free_.push_back(int(i));
+  }
+  slot_busy_.assign(size_t(S), 0);
+  paused_ = cfg_.start_paused;
+  launcher_ = std::thread([this] { launcher_loop(); });
+  completer_ = std::thread([this] { completer_loop(); });
+}
+
+LiveServer::~LiveServer() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+int64_t LiveServer::need_of(int64_t len, int64_t rows) const {
+  const int64_t ne = rows * cfg_.fields;
+  // bytes + typed-field scratch (int64 ids 8 B + fp32 weights 4 B per element,
+  // or the GPU varint id region) + row table + varint chunk entries + alignment
+  return align8(len) + 12 * ne + 8 * rows + 32 * (len / kVarintChunk + 2) + 256;
+}
+
+int LiveServer::bucket_for(int64_t rows) const {
+  const auto& bk = backend_->buckets();
+  if (cfg_.lockstep) return int(bk.size()) - 1;
+  for (size_t i = 0; i < bk.size(); ++i)
+    if (bk[i] >= rows) return int(i);
+  return int(bk.size()) - 1;
+}
+
+void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Completion done) {
+  auto reject = [&](int code, std::string msg) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++st_.rejected;
+    }
+    done(Reply{code, std::move(msg), std::string()});
+  };
+  // framing + signature checks on the caller's thread (parallel across callers)
+  wire::PredictRequestView v;
+  std::string err;
+  if (!wire::parse_predict_request(data, n, &v, &err, false))
+    return reject(kInvalidArgument, "malformed PredictRequest: " + err);
+  if (v.model_name != cfg_.model_name)
+    return reject(kNotFound, "Servable not found for request: Latest(" + v.model_name + ")");
+  if (v.has_version && (cfg_.version < 0 || v.version != cfg_.version))
+    return reject(kNotFound, "Servable not found for request: Specific(" + v.model_name + ", " +
+                                 std::to_string(v.version) + ")");
+  if (!v.signature_name.empty() && v.signature_name != cfg_.signature_name)
+    return reject(kInvalidArgument, "Serving signature name: \"" + v.signature_name +
+                                        "\" not found in signature def of model " + cfg_.model_name);
+  for (const auto& k : v.output_filter)
+    if (k != cfg_.output_key) return reject(kInvalidArgument, "output tensor alias not found in signature: " + k);
+  const wire::TensorView* ti = v.find(cfg_.ids_key);
+  const wire::TensorView* tw = v.find(cfg_.wts_key);
+  if (!ti || !tw)
+    return reject(kInvalidArgument, "input tensor alias not found in signature: " + (ti ? cfg_.wts_key : cfg_.ids_key));
+  if (ti->unknown_rank || ti->shape.size() != 2 || ti->shape[1] != cfg_.fields || ti->shape[0] < 0)
+    return reject(kInvalidArgument, cfg_.ids_key + " must have shape [B, " + std::to_string(cfg_.fields) + "], got " +
+                                        shape_str(ti->shape));
+  if (tw->shape != ti->shape)
+    return reject(kInvalidArgument, cfg_.wts_key + " shape " + shape_str(tw->shape) + " != " + shape_str(ti->shape));
+  if (ti->dtype != wire::DT_INT64 && ti->dtype != wire::DT_INT32)
+    return reject(kInvalidArgument, cfg_.ids_key + " must be DT_INT64 or DT_INT32");
+  const int64_t rows = ti->shape[0];
+  wire::ModelSpecOut spec{cfg_.model_name, v.signature_name.empty() ? cfg_.signature_name : v.signature_name,
+                          cfg_.version >= 0, cfg_.version};
+  if (rows == 0) {
+    wire::TensorOut t;
+    t.key = cfg_.output_key;
+    t.shape = {0};
+    done(Reply{kOk, "", wire::encode_predict_response(spec, {t})});
+    return;
+  }
+  if (rows > max_rows_)
+    return reject(kOversize, "request has " + std::to_string(rows) + " rows; a batch holds at most " +
+                                 std::to_string(max_rows_));
+  const int64_t need = need_of(int64_t(n), rows);
+  if (need > arena_budget_) return reject(kOversize, "request does not fit one arena");
+
+  const int64_t t0 = now_us();
+  int a = -1;
+  int64_t off = 0;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (broken_) {
+      lk.unlock();
+      return reject(kUnavailable, "server unavailable: " + error_);
+    }
+    if (closing_) {
+      lk.unlock();
+      return reject(kUnavailable, "server is shutting down");
+    }
+    if (pending_ >= cfg_.max_pending) {
+      lk.unlock();
+      return reject(kResourceExhausted, "batching queue is full");
+    }
+    bool blocked = false;
+    for (;;) {
+      if (open_ >= 0) {
+        Arena& o = arenas_[size_t(open_)];
+        if (o.rows + rows <= max_rows_ && o.need + need <= arena_budget_ &&
+            int64_t(o.pend.size()) < kArenaMaxRequests)
+          break;
+        // the open batch is full for this request: seal it, take a fresh arena
+        sealed_.push_back(open_);
+        open_ = -1;
+        cv_launch_.notify_all();
+        continue;
+      }
+      if (!free_.empty()) {
+        open_ = free_.front();
+        free_.pop_front();
+        continue;
+      }
+      // every arena is queued or in flight: wait for one (bounded by the deadline)
+      if (!blocked) {
+        blocked = true;
+        ++st_.blocked_submits;
+      }
+      auto ready = [&] { return broken_ || closing_ || open_ >= 0 || !free_.empty(); };
+      if (deadline_us > 0) {
+        const int64_t left = deadline_us - now_us();
+        if (left <= 0 || !cv_space_.wait_for(lk, std::chrono::microseconds(left), ready)) {
+          lk.unlock();
+          return reject(kDeadlineExceeded, "request deadline exceeded while waiting for a batch slot");
+        }
+      } else {
+        cv_space_.wait(lk, ready);
+      }
+      if (broken_ || closing_) {
+        lk.unlock();
+        return reject(kUnavailable, broken_ ? "server unavailable: " + error_ : "server is shutting down");
+      }
+    }
+    a = open_;
+    Arena& o = arenas_[size_t(a)];
+    off = o.used;
+    o.used += align8(int64_t(n));
+    o.rows += rows;
+    o.need += need;
+    if (o.pend.empty()) {
+      o.t_first = t0;
+      cv_launch_.notify_all();  // eager dispatch / batch timeout start now
+    }
+    o.pend.push_back(Pending{off, int64_t(n), rows, deadline_us, t0, std::move(done)});
+    ++o.writers;
+    ++pending_;
+    ++st_.submitted;
+    if (o.rows >= max_rows_) {  // exactly full: hand it over without waiting for the next request
+      sealed_.push_back(open_);
+      open_ = -1;
+      cv_launch_.notify_all();
+    }
+  }
+  // the one copy of the request: into pinned memory the DMA engine reads
+  std::memcpy(arenas_[size_t(a)].base + kArenaPayloadOff + off, data, n);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    st_.copy_us += double(now_us() - t0);
+    if (--arenas_[size_t(a)].writers == 0) cv_launch_.notify_all();
+  }
+}
+
+Reply LiveServer::predict(const uint8_t* data, size_t n, int64_t deadline_us) {
+  std::mutex m;
+  std::condition_variable cv;
+  bool ready = false;
+  Reply out;
+  submit(data, n, deadline_us, [&](Reply&& r) {
+    std::lock_guard<std::mutex> lk(m);
+    out = std::move(r);
+    ready = true;
+    cv.notify_one();
+  });
+  std::unique_lock<std::mutex> lk(m);
+  cv.wait(lk, [&] { return ready; });
+  return out;
+}
+
+void LiveServer::fail_all(std::vector<Pending>& ps, int code, const std::string& msg) {
+  for (auto& p : ps) {
+    if (p.done) p.done(Reply{code, msg, std::string()});
+    p.done = nullptr;
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  pending_ -= int64_t(ps.size());
+  st_.failed += int64_t(ps.size());
+  if (code == kDeadlineExceeded) st_.expired += int64_t(ps.size());
+}
+
+void LiveServer::go_broken(const std::string& why) {
+  std::vector<Pending> orphans;
+  bool first = false;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!broken_) {
+      first = true;
+      broken_ = true;
+      error_ = why;
+    }
+    // queued batches will never launch: answer them now (writers still
+    // copying finish their memcpy; their Pending entries are taken here)
+    for (int a : sealed_)
+      for (auto& p : arenas_[size_t(a)].pend) orphans.push_back(std::move(p));
+    for (int a : sealed_) arenas_[size_t(a)].pend.clear();
+    if (open_ >= 0) {
+      for (auto& p : arenas_[size_t(open_)].pend) orphans.push_back(std::move(p));
+      arenas_[size_t(open_)].pend.clear();
+    }
+    cv_launch_.notify_all();
+    cv_space_.notify_all();
+    cv_done_.notify_all();
+  }
+  if (first) {
+    try {
+      backend_->abort();
+    } catch (...) {
+    }
+  }
+  fail_all(orphans, kUnavailable, "server unavailable: " + why);
+}
+
+void LiveServer::release(int a, int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Arena& ar = arenas_[size_t(a)];
+  ar.used = ar.rows = ar.need = ar.t_first = 0;
+  ar.pend.clear();
+  free_.push_back(a);
+  if (slot >= 0) {
+    slot_busy_[size_t(slot)] = 0;
+    --inflight_;
+  }
+  cv_space_.notify_all();
+  cv_launch_.notify_all();
+}
+
+void LiveServer::launcher_loop() {
+  const int S = backend_->slots();
+  const int nb = int(backend_->buckets().size());
+  for (;;) {
+    int a = -1, slot = -1;
+    std::vector<Pending> pend;
+    bool stop = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      // a free slot first: while the device is busy, requests keep filling the
+      // open batch (fuller steps under load)
+      auto slot_free = [&] { return inflight_ < cfg_.depth && !slot_busy_[size_t(next_slot_)]; };
+      auto drained = [&] {
+        const bool fixed_run = cfg_.lockstep && cfg_.max_steps >= 0 && steps_launched_ < cfg_.max_steps;
+        return closing_ && !fixed_run && sealed_.empty() && (open_ < 0 || arenas_[size_t(open_)].pend.empty());
+      };
+      cv_launch_.wait(lk, [&] { return broken_ || (!paused_ && (drained() || slot_free())) || (paused_ && closing_); });
+      if (paused_ && closing_) break;  // never started: nothing was launched
+      if (broken_ || !slot_free()) break;
+      for (;;) {
+        if (cfg_.max_steps >= 0 && steps_launched_ >= cfg_.max_steps) {
+          stop = true;
+          break;
+        }
+        if (!sealed_.empty()) {
+          a = sealed_.front();
+          sealed_.pop_front();
+          ++st_.full_steps;
+          break;
+        }
+        const int64_t now = now_us();
+        int64_t wake = 0;
+        if (open_ >= 0 && !arenas_[size_t(open_)].pend.empty()) {
+          const Arena& o = arenas_[size_t(open_)];
+          const bool idle = cfg_.eager_when_idle && !cfg_.lockstep && inflight_ == 0;
+          if (closing_ || idle || now >= o.t_first + cfg_.batch_timeout_us) {
+            a = open_;
+            open_ = -1;
+            ++(idle ? st_.eager_steps : st_.timeout_steps);
+            break;
+          }
+          wake = o.t_first + cfg_.batch_timeout_us;
+        } else if (closing_ && !(cfg_.lockstep && cfg_.max_steps >= 0)) {
+          // (a fixed-length lockstep run keeps launching empty steps until
+          // max_steps: the other ranks' steps pair with them)
+          stop = true;
+          break;
+        } else if (cfg_.lockstep) {
+          // fan-out: the other ranks launch this step too, requests or not
+          if (now >= last_launch_us_ + cfg_.batch_timeout_us) {
+            if (open_ >= 0) {
+              a = open_;
+              open_ = -1;
+            } else if (!free_.empty()) {
+              a = free_.front();
+              free_.pop_front();
+            }
+            if (a >= 0) {
+              ++st_.empty_steps;
+              break;
+            }
+          } else {
+            wake = last_launch_us_ + cfg_.batch_timeout_us;
+          }
+        }
+        if (broken_) break;
+        if (wake > 0) cv_launch_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
+        else cv_launch_.wait(lk);
+        if (broken_) break;
+      }
+      if (broken_ || stop) break;
+      // writers that reserved space in this batch finish their copies first
+      cv_launch_.wait(lk, [&] { return arenas_[size_t(a)].writers == 0; });
+      pend = std::move(arenas_[size_t(a)].pend);
+      arenas_[size_t(a)].pend.clear();
+      slot = next_slot_;
+      slot_busy_[size_t(slot)] = 1;
+      next_slot_ = (next_slot_ + 1) % S;
+      ++inflight_;
+      ++steps_launched_;
+      last_launch_us_ = now_us();
+    }
+    // requests whose deadline passed while queued are answered, not computed
+    const int64_t t0 = now_us();
+    std::vector<Pending> live, expired;
+    live.reserve(pend.size());
+    for (auto& p : pend) (p.deadline_us > 0 && t0 > p.deadline_us ? expired : live).push_back(std::move(p));
+    if (!expired.empty()) fail_all(expired, kDeadlineExceeded, "request deadline exceeded while queued");
+    std::vector<Span> spans;
+    spans.reserve(live.size());
+    for (const auto& p : live) spans.emplace_back(p.off, p.len);
+    Arena& ar = arenas_[size_t(a)];
+    ArenaBatch batch;
+    try {
+      trace::Range tr("live_build");
+      batch = arena_build(ar.base, ar.capacity, spans, cfg_.ids_key, cfg_.wts_key, cfg_.fields, max_rows_,
+                          cfg_.varint_chunks);
+    } catch (const std::exception& e) {
+      fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --steps_launched_;
+      }
+      release(a, slot);
+      continue;
+    }
+    const int64_t t1 = now_us();
+    if (batch.n_valid == 0 && !cfg_.lockstep) {
+      // nothing to compute: every request was malformed (or none left)
+      for (size_t i = 0; i < live.size(); ++i)
+        if (live[i].done) live[i].done(Reply{kInvalidArgument, batch.errors[i], std::string()});
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        pending_ -= int64_t(live.size());
+        st_.failed += int64_t(live.size());
+        --steps_launched_;
+      }
+      release(a, slot);
+      continue;
+    }
+    const int b = bucket_for(batch.total_rows);
+    try {
+      trace::Range tr("live_launch");
+      backend_->launch(slot, b, ar.base, batch);
+    } catch (const std::exception& e) {
+      const std::string why = std::string("step launch failed: ") + e.what();
+      fail_all(live, kUnavailable, why);
+      release(a, slot);
+      go_broken(why);
+      break;
+    }
+    const int64_t t2 = now_us();
+    std::lock_guard<std::mutex> lk(mu_);
+    st_.build_us += double(t1 - t0);
+    st_.launch_us += double(t2 - t1);
+    ++st_.steps;
+    st_.rows += batch.total_rows;
+    st_.padded_rows += backend_->buckets()[size_t(std::min(b, nb - 1))];
+    q_done_.push_back(InFlight{a, slot, b, std::move(batch), std::move(live), t2});
+    cv_done_.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    launcher_exited_ = true;
+    closing_ = true;  // a stopped launcher admits nothing more
+    cv_done_.notify_all();
+    cv_space_.notify_all();
+  }
+  // whatever is still queued will not be launched
+  std::vector<Pending> orphans;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int x : sealed_) {
+      for (auto& p : arenas_[size_t(x)].pend) orphans.push_back(std::move(p));
+      arenas_[size_t(x)].pend.clear();
+    }
+    if (open_ >= 0) {
+      for (auto& p : arenas_[size_t(open_)].pend) orphans.push_back(std::move(p));
+      arenas_[size_t(open_)].pend.clear();
+    }
+  }
+  if (!orphans.empty())
+    fail_all(orphans, kUnavailable, broken_ ? "server unavailable: " + error_ : "server stopped before the request ran");
+}
+
+void LiveServer::completer_loop() {
+  wire::ModelSpecOut spec{cfg_.model_name, cfg_.signature_name, cfg_.version >= 0, cfg_.version};
+  for (;;) {
+    InFlight f;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_done_.wait(lk, [&] { return !q_done_.empty() || launcher_exited_; });
+      if (q_done_.empty()) break;
+      f = std::move(q_done_.front());
+      q_done_.pop_front();
+    }
+    const int64_t t0 = now_us();
+    std::string err;
+    bool ok = false;
+    try {
+      trace::Range tr("live_wait");
+      // after a failure the remaining steps get a short grace period only
+      ok = backend_->wait(f.slot, broken_ ? 200'000 : cfg_.step_timeout_us, &err);
+      if (!ok && err.empty()) err = "step did not finish within the step timeout";
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    const int64_t t1 = now_us();
+    if (!ok) {
+      const std::string why = "GPU step failed: " + err;
+      fail_all(f.pend, kUnavailable, "server unavailable: " + why);
+      go_broken(why);
+      release(f.arena, f.slot);
+      continue;
+    }
+    const float* sc = backend_->scores(f.slot, f.bucket);
+    const int64_t sc_len = backend_->scores_len(f.slot, f.bucket);
+    int64_t n_ok = 0, n_bad = 0;
+    {
+      trace::Range tr("live_encode");
+      for (size_t i = 0; i < f.pend.size(); ++i) {
+        Pending& p = f.pend[i];
+        Reply r;
+        const std::string& e = f.batch.errors[i];
+        if (!e.empty()) {
+          r.code = kInvalidArgument;
+          r.message = e;
+          ++n_bad;
+        } else if (f.batch.offsets[i] + f.batch.rows[i] > sc_len) {
+          r.code = kInternal;
+          r.message = "scores buffer smaller than the batch";
+          ++n_bad;
+        } else {
+          wire::TensorOut t;
+          t.key = cfg_.output_key;
+          t.dtype = wire::DT_FLOAT;
+          t.shape = {f.batch.rows[i]};
+          t.data = sc + f.batch.offsets[i];
+          t.n = f.batch.rows[i];
+          r.response = wire::encode_predict_response(spec, {t});
+          ++n_ok;
+        }
+        if (p.done) p.done(std::move(r));
+        p.done = nullptr;
+      }
+    }
+    const int64_t t2 = now_us();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      pending_ -= int64_t(f.pend.size());
+      st_.completed += n_ok;
+      st_.failed += n_bad;
+      st_.wait_us += double(t1 - t0);
+      st_.encode_us += double(t2 - t1);
+    }
+    release(f.arena, f.slot);
+  }
+}
+
+void LiveServer::resume() {
+  std::lock_guard<std::mutex> lk(mu_);
+  paused_ = false;
+  last_launch_us_ = now_us();
+  cv_launch_.notify_all();
+}
+
+void LiveServer::close() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    closing_ = true;
+    cv_launch_.notify_all();
+    cv_space_.notify_all();
+  }
+  if (launcher_.joinable()) launcher_.join();
+  if (completer_.joinable()) completer_.join();
+}
+
+LiveStats LiveServer::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  LiveStats s = st_;
+  s.broken = broken_;
+  s.error = error_;
+  return s;
+}
+
+}  // namespace runtime
+}  // namespace dtfs

@@ -1,0 +1,164 @@
+#include "loadgen.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <random>
+#include <stdexcept>
+#include <thread>
+
+#include "batcher.h"  // now_us()
+
+namespace dtfs {
+namespace runtime {
+
+namespace {
+
+// Work queue of (request index, scheduled send time) handed to submitters.
+struct WorkQ {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int64_t, int64_t>> q;
+  bool stop = false;
+
+  void push(int64_t i, int64_t t) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.emplace_back(i, t);
+    }
+    cv.notify_one();
+  }
+  bool pop(std::pair<int64_t, int64_t>* out) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return stop || !q.empty(); });
+    if (q.empty()) return false;
+    *out = q.front();
+    q.pop_front();
+    return true;
+  }
+  void close() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+  }
+};
+
+}  // namespace
+
+LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const LoadSpec& spec) {
+  if (reqs.empty()) throw std::invalid_argument("no requests");
+  if (spec.count <= 0) throw std::invalid_argument("count must be > 0");
+  const bool open_loop = spec.qps > 0;
+  const int C = std::max(1, spec.concurrency);
+  const int64_t tail = open_loop ? 0 : (spec.tail < 0 ? C : spec.tail);
+  const int64_t total = spec.warmup + spec.count + tail;
+  const int64_t P = int64_t(reqs.size());
+
+  LoadResult res;
+  std::mutex mu;
+  std::condition_variable cv_all;
+  int64_t completed = 0;
+  double t_open = 0, t_close = 0;
+  std::vector<double> lat_sched;  // open loop: by request index
+  if (open_loop) lat_sched.assign(size_t(spec.warmup + spec.count), -1.0);
+  res.latency_us.reserve(size_t(spec.count));
+  WorkQ work;
+  std::atomic<int64_t> next{0};
+
+  auto on_done = [&](int64_t i, int64_t t_sched, Reply&& r) {
+    const int64_t t = now_us();
+    bool push_token = false;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      ++completed;
+      if (r.code == kOk) {
+        ++res.ok;
+      } else {
+        if (res.errors++ == 0) {
+          res.first_error = r.message;
+          res.first_error_code = r.code;
+        }
+      }
+      if (open_loop) {
+        if (i >= spec.warmup && i < spec.warmup + spec.count) lat_sched[size_t(i)] = double(t - t_sched);
+        if (completed == spec.warmup + spec.count) t_close = double(t);
+      } else {
+        // closed loop: the window is counted in completions, whatever their order
+        if (completed == spec.warmup) t_open = double(t);
+        if (completed > spec.warmup && completed <= spec.warmup + spec.count)
+          res.latency_us.push_back(double(t - t_sched));
+        if (completed == spec.warmup + spec.count) t_close = double(t);
+        push_token = true;
+      }
+      if (completed == total) cv_all.notify_all();
+    }
+    if (push_token) {
+      const int64_t k = next.fetch_add(1);
+      if (k < total) work.push(k, 0);
+    }
+  };
+
+  std::vector<std::thread> subs;
+  const int T = std::max(1, spec.threads);
+  const double wall0 = double(now_us());
+  for (int s = 0; s < T; ++s) {
+    subs.emplace_back([&] {
+      std::pair<int64_t, int64_t> w;
+      while (work.pop(&w)) {
+        const int64_t i = w.first;
+        const int64_t t_sched = open_loop ? w.second : now_us();
+        const std::string& r = reqs[size_t(i % P)];
+        const int64_t dl = spec.timeout_us > 0 ? t_sched + spec.timeout_us : 0;
+        srv.submit(reinterpret_cast<const uint8_t*>(r.data()), r.size(), dl,
+                   [&on_done, i, t_sched](Reply&& rep) { on_done(i, t_sched, std::move(rep)); });
+      }
+    });
+  }
+  if (spec.warmup == 0) t_open = double(now_us());
+  if (!open_loop) {
+    for (int c = 0; c < C && c < total; ++c) work.push(next.fetch_add(1), 0);
+  } else {
+    // schedule thread: request i is due at t0 + i / qps (uniform) or at
+    // exponential gaps; everything due is queued whenever it wakes, so a late
+    // wake-up sends a burst instead of drifting the offered rate
+    std::mt19937_64 rng(spec.seed);
+    std::exponential_distribution<double> expo(spec.qps);
+    const double t0 = double(now_us()) + 1000.0;
+    double t_next = t0;
+    for (int64_t i = 0; i < total; ++i) {
+      if (i == spec.warmup) t_open = t_next;
+      for (;;) {
+        const double now = double(now_us());
+        if (now >= t_next) break;
+        const double gap = t_next - now;
+        if (gap > 200) std::this_thread::sleep_for(std::chrono::microseconds(int64_t(gap - 100)));
+        else std::this_thread::yield();
+      }
+      work.push(i, int64_t(t_next));
+      t_next += spec.poisson ? expo(rng) * 1e6 : 1e6 / spec.qps;
+    }
+  }
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv_all.wait(lk, [&] { return completed >= total; });
+  }
+  work.close();
+  for (auto& t : subs) t.join();
+  res.submitted = total;
+  res.wall_us = double(now_us()) - wall0;
+  res.window_us = t_close - t_open;
+  if (open_loop) {
+    for (int64_t i = spec.warmup; i < spec.warmup + spec.count; ++i)
+      if (lat_sched[size_t(i)] >= 0) res.latency_us.push_back(lat_sched[size_t(i)]);
+  }
+  return res;
+}
+
+}  // namespace runtime
+}  // namespace dtfs

@@ -30,6 +30,7 @@ namespace runtime {
 
 struct LoopSlot {
   void* h2d_dst = nullptr;           // device arena of the slot (local launch)
+  int64_t h2d_cap = 0;               // its size in bytes
   hipGraphExec_t graph = nullptr;    // local: unpack + forward + scores -> h_out
   const KernelSequence* seq = nullptr;  // local, preferred: the same step as direct launches
   bool fanout = false;

@@ -1,6 +1,7 @@
 #include "step_runner.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -50,7 +51,7 @@ StepRunner::StepRunner(int device, int slots) : device_(device), event_mode_(eve
   ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
   h2d_done_.resize(slots);
   done_.resize(slots);
-  used_.assign(slots, false);
+  used_.assign(size_t(slots), 0);
   observed_.reset(new std::atomic<bool>[size_t(slots)]);
   for (int i = 0; i < slots; ++i) observed_[i].store(false);
   for (int i = 0; i < slots; ++i) {
@@ -146,7 +147,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   if (s.d2h_bytes > 0)
     ck(hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_), "hipMemcpyAsync(D2H)");
   ck(hipEventRecord(done_[slot], egress_), "hipEventRecord(done)");
-  used_[slot] = true;
+  used_[slot] = 1;
 }
 
 void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph) {
@@ -155,7 +156,7 @@ void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hi
   h2d(slot, dst, src, nbytes, compute_, true);
   ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
-  used_[slot] = true;
+  used_[slot] = 1;
 }
 
 void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq,
@@ -165,7 +166,7 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d(slot, dst, src, nbytes, compute_, true);
   seq->launch(compute_, done_[slot], event_mode_ >= 2, skip_varint);
-  used_[slot] = true;
+  used_[slot] = 1;
 }
 
 void StepRunner::wait(int slot) {
@@ -184,6 +185,45 @@ void StepRunner::wait(int slot) {
     }
   }
   observed_[slot].store(true, std::memory_order_release);
+}
+
+bool StepRunner::wait_for(int slot, int64_t timeout_us, const std::vector<comm::RcclComm*>& comms,
+                          std::string* err) {
+  if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  auto last_comm_check = t0;
+  if (used_[slot]) {
+    for (;;) {
+      const hipError_t e = hipEventQuery(done_[slot]);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) {
+        *err = std::string("hipEventQuery: ") + hipGetErrorString(e);
+        return false;
+      }
+      const auto now = clk::now();
+      const int64_t el = std::chrono::duration_cast<std::chrono::microseconds>(now - t0).count();
+      if (el > timeout_us) {
+        *err = "step not finished after " + std::to_string(el / 1000) + " ms";
+        return false;
+      }
+      if (!comms.empty() && now - last_comm_check > std::chrono::milliseconds(1)) {
+        last_comm_check = now;
+        for (auto* c : comms) {
+          if (!c) continue;
+          std::string ce = c->async_error();
+          if (!ce.empty()) {
+            *err = "RCCL: " + ce;
+            return false;
+          }
+        }
+      }
+      if (el < 2000) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+  observed_[slot].store(true, std::memory_order_release);
+  return true;
 }
 
 bool StepRunner::query(int slot) {

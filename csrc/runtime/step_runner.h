@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "../comm/rccl_comm.h"
@@ -71,6 +72,11 @@ class StepRunner {
   void launch_fanout(int slot, const FanoutStep& s);
   // Block until the slot's last step has finished (scores are on the host).
   void wait(int slot);
+  // Bounded wait: false when the step has not finished within timeout_us or a
+  // communicator reports an asynchronous error (*err says which). Polls the
+  // completion event (spin-yield for the first 2 ms, then 50 us sleeps) so a
+  // dead peer or a stuck kernel cannot block the caller forever.
+  bool wait_for(int slot, int64_t timeout_us, const std::vector<comm::RcclComm*>& comms, std::string* err);
   bool query(int slot);
   // Microseconds between the slot's last H2D start and compute end (diagnostic).
   int slots() const { return int(done_.size()); }
@@ -94,7 +100,7 @@ class StepRunner {
   void ensure_fanout_streams();
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
-  std::vector<bool> used_;
+  std::vector<char> used_;  // not vector<bool>: written by the launcher, read by the waiter
 };
 
 }  // namespace runtime

@@ -670,12 +670,15 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
   if (t.value_packed_varint) {
     if (t.dtype == DT_HALF || t.dtype == DT_BFLOAT16) {
       const bool bf = t.dtype == DT_BFLOAT16;
+      bool over = false;
       if (!for_each_int(t, [&](uint64_t v) {
             const uint16_t h = uint16_t(v);
-            if (bf && opts.dst == DstType::BF16) w.put_bits16(i++, h);
+            if (i >= n) over = true;
+            else if (bf && opts.dst == DstType::BF16) w.put_bits16(i++, h);
             else w.put_float(i++, bf ? bf16_to_f32(h) : half_to_f32(h));
           }))
         return *err = "bad packed varint", false;
+      if (over) return *err = "more values than the tensor shape holds", false;
     } else if (t.dtype == DT_INT64 && dst_int && t.packed.size() == 1 && t.unpacked.empty()) {
       // Hot path: reference feat_ids (int64_val packed) -> row ids.
       const uint8_t* p = t.packed[0].p;
@@ -688,27 +691,38 @@ bool decode_into(const TensorView& t, void* dst, int64_t n, const DecodeOpts& op
           uint8_t b;
           do {
             if (p >= e) return *err = "truncated varint", false;
+            if (shift >= 70) return *err = "varint longer than 10 bytes", false;
             b = *p++;
             v |= uint64_t(b & 0x7F) << shift;
             shift += 7;
-          } while ((b & 0x80) && shift < 70);
+          } while (b & 0x80);
         }
+        if (i >= n) return *err = "more values than the tensor shape holds", false;
         w.put_int(i++, int64_t(v));
       }
     } else {
       const int dt = t.dtype;
-      if (!for_each_int(t, [&](uint64_t v) { w.put_int(i++, int_from_varint(dt, v)); }))
+      bool over = false;
+      if (!for_each_int(t, [&](uint64_t v) {
+            if (i < n) w.put_int(i++, int_from_varint(dt, v));
+            else over = true;
+          }))
         return *err = "bad packed varint", false;
+      if (over) return *err = "more values than the tensor shape holds", false;
     }
   } else if (t.value_fixed32) {
     if (opts.dst == DstType::F32 && t.packed.size() == 1 && t.unpacked.empty()) {
-      i = int64_t(t.packed[0].n / 4);  // reference feat_wts: float_val packed
+      i = std::min<int64_t>(n, int64_t(t.packed[0].n / 4));  // reference feat_wts: float_val packed
       w.copy_rows(t.packed[0].p, i);
     } else {
-      for_each_f32(t, [&](float f) { w.put_float(i++, f); });
+      for_each_f32(t, [&](float f) {
+        if (i < n) w.put_float(i++, f);
+      });
     }
   } else if (t.value_fixed64) {
-    for_each_f64(t, [&](double d) { w.put_float(i++, float(d)); });
+    for_each_f64(t, [&](double d) {
+      if (i < n) w.put_float(i++, float(d));
+    });
   } else {
     return *err = "tensor has no typed value field for its dtype", false;
   }
@@ -861,6 +875,8 @@ std::string encode_predict_request(const ModelSpecOut& spec, const std::vector<T
 }
 
 int64_t count_varint_terminators(const uint8_t* p, size_t n) { return count_terms(p, n); }
+
+size_t element_size(int dtype) { return dtype_size(dtype); }
 
 }  // namespace wire
 }  // namespace dtfs

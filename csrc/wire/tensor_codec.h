@@ -89,6 +89,9 @@ bool parse_predict_request(const uint8_t* buf, size_t len, PredictRequestView* o
 // the CPU has it.
 int64_t count_varint_terminators(const uint8_t* p, size_t n);
 
+// Bytes per element of a TF DataType in tensor_content (0: unsupported).
+size_t element_size(int dtype);
+
 // Parse one serialized TensorProto.
 bool parse_tensor(const uint8_t* buf, size_t len, TensorView* out, std::string* err);
 

@@ -69,11 +69,14 @@ class ServingConfig:
     max_batch_rows: int = 8192        # dynamic batcher: rows per GPU batch
     batch_timeout_us: int = 200       # oldest request waits at most this long
     max_queued_rows: int = 1 << 22    # backpressure bound (rows)
+    max_request_rows: int = 1 << 18   # one request's candidates (checked before any allocation)
     allowed_batch_sizes: Tuple[int, ...] = (512, 1024, 2048, 4096, 8192)  # padding buckets (HIP graphs)
     num_batch_threads: int = 1
     use_graphs: bool = True           # capture each bucket's forward in a HIP graph
     device: str = "auto"              # auto | cpu | cuda
     request_timeout_s: float = 10.0
+    live: bool = True                 # native live server (csrc/runtime/live_server.h); False: Python scheduler
+    step_timeout_s: float = 10.0      # a GPU step that takes longer marks the server broken (UNAVAILABLE)
 
 
 @dataclass

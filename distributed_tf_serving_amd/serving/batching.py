@@ -44,7 +44,8 @@ class WorkItem:
 class BatchingScheduler:
     def __init__(self, engine, max_batch_rows: int = 8192, batch_timeout_us: int = 200,
                  max_queued_rows: int = 1 << 22, depth: int = 2, name: str = "model",
-                 fanout_world: int = 1, on_launch: Optional[Callable[[int, int], None]] = None):
+                 fanout_world: int = 1, on_launch: Optional[Callable[[int, int], None]] = None,
+                 max_request_rows: int = 1 << 18):
         """``fanout_world`` > 1: this is the front door of a scatter fan-out
         (parallel/fanout.py): a step of bucket B carries up to world x B rows,
         split across the ranks. ``on_launch(B, slot)`` runs right before each
@@ -56,6 +57,9 @@ class BatchingScheduler:
         self.on_launch = on_launch
         self.eager_when_idle = True
         self.max_rows = min(int(max_batch_rows), self.ex.max_rows) * self.world
+        # a request's declared rows are checked before anything is allocated for
+        # it (TF fill semantics let a ~100-byte request declare any shape)
+        self.max_request_rows = min(int(max_request_rows), int(max_queued_rows))
         self.depth = max(1, min(depth, self.ex.slots - 1)) if self.ex.slots > 1 else 1
         self.batcher = native().DynamicBatcher(self.max_rows, int(batch_timeout_us), int(max_queued_rows))
         self._items: Dict[int, WorkItem] = {}
@@ -72,6 +76,10 @@ class BatchingScheduler:
         fut: cf.Future = cf.Future()
         if rows <= 0:
             fut.set_result(torch.empty(0))
+            return fut
+        if rows > self.max_request_rows:
+            fut.set_exception(ServingError(
+                Code.INVALID_ARGUMENT, f"request has {rows} rows; this server accepts at most {self.max_request_rows}"))
             return fut
         if rows > self.max_rows:
             # larger than one GPU batch: split into row chunks, join in order

@@ -67,6 +67,14 @@ class ModelRegistry:
             if not vs:
                 self._models.pop(name, None)
 
+    def only(self) -> Optional[Servable]:
+        """The servable when exactly one (name, version) is loaded, else None."""
+        models = self._models
+        if len(models) != 1:
+            return None
+        vs = next(iter(models.values()))
+        return next(iter(vs.values())) if len(vs) == 1 else None
+
     def names(self) -> List[str]:
         return sorted(self._models)
 

@@ -22,8 +22,10 @@ from ..models import build_model
 from ..parallel.dist import DistContext
 from ..parallel.fanout import FanoutEngine
 from ..utils.gc_tuning import tune_for_serving
+from .arena import ArenaLayout
 from .batching import BatchingScheduler
 from .executor import ShardExecutor
+from .live import LiveScheduler
 from .monitoring import ServingMetrics
 from .packing import PackedLayout
 from .registry import ModelRegistry, Servable, Signature
@@ -40,11 +42,24 @@ def pick_device(pref: str = "auto") -> torch.device:
     return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
 
 
+def live_enabled(cfg: Config, mode: str = "local", model=None) -> bool:
+    """The native live server serves local (one-rank) servables whose step can
+    be replayed natively: a CPU model, or a GPU model with HIP graphs and no
+    collectives inside its forward."""
+    sc = cfg.serving
+    if not sc.live or mode != "local":
+        return False
+    if model is not None and getattr(model, "has_collectives", False):
+        return False
+    return True
+
+
 def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistContext] = None,
                  mode: str = "local") -> FanoutEngine:
     """Model + executor + fan-out engine of one rank, every bucket prepared
     (HIP graphs captured). With ``ctx`` of a multi-rank job, DLRM tables are
-    sharded over the ranks (parallel/embedding_sharding.py)."""
+    sharded over the ranks (parallel/embedding_sharding.py). A servable of the
+    live server ingests request arenas (the GPU unpacks raw request bytes)."""
     from ..parallel.embedding_sharding import build_parallel_model
 
     sc = cfg.serving
@@ -53,8 +68,16 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
     model = build_parallel_model(cfg.model, dev, ctx)
     layout = PackedLayout(cfg.model.num_fields)
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
-    ex = ShardExecutor(model, layout, buckets, dev, use_graphs=sc.use_graphs, slots=slots)
-    eng = FanoutEngine(ex, ctx, mode=mode)
+    use_graphs = sc.use_graphs
+    live = live_enabled(cfg, mode, model)
+    if live and dev.type == "cuda" and not use_graphs:
+        live = False  # the native step replays captured graphs
+    ex = ShardExecutor(model, layout, buckets, dev, use_graphs=use_graphs, slots=slots)
+    if live:
+        eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena",
+                           arena=ArenaLayout(cfg.model.num_fields, max_rows=max(buckets)))
+    else:
+        eng = FanoutEngine(ex, ctx, mode=mode)
     for B in buckets:
         eng.prepare(B)
     return eng
@@ -66,9 +89,13 @@ def build_servable(cfg: Config, device=None, version: Optional[int] = None, slot
     eng = engine or build_engine(cfg, device, slots)
     model = eng.ex.model
     world = eng.world if eng.mode == "scatter" else 1
-    sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
-                              max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name,
-                              fanout_world=world, on_launch=on_launch)
+    if eng.ingest == "arena" and eng.mode == "local" and on_launch is None:
+        sched = LiveScheduler(eng, sc, version=sc.version if version is None else version,
+                              step_timeout_s=sc.step_timeout_s)
+    else:
+        sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
+                                  max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name,
+                                  fanout_world=world, on_launch=on_launch, max_request_rows=sc.max_request_rows)
     sig = model.signature()
     sigs = {sc.signature_name: Signature(inputs=sig["inputs"], outputs=sig["outputs"], method_name=sig["method_name"])}
     return Servable(name=sc.model_name, version=sc.version if version is None else version, model=model,
@@ -134,11 +161,11 @@ def main(argv=None):
         from .faults import FaultInjector, FaultSpec, FaultyService
 
         srv.service = FaultyService(srv.service, FaultInjector(FaultSpec.parse(a.inject_fault)))
+    if not a.no_gc_freeze:  # after warm-up (graphs captured), before the port takes traffic
+        logging.getLogger(__name__).info("gc: %s", tune_for_serving())
     port = srv.start_grpc(a.port, a.host, a.grpc_workers)
     if a.monitoring_port is not None:
         srv.start_monitoring(a.monitoring_port, a.host)
-    if not a.no_gc_freeze:
-        logging.getLogger(__name__).info("gc: %s", tune_for_serving())
     print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:

@@ -103,7 +103,24 @@ class PredictionServiceImpl:
         return self.nat.encode_predict_response(s.name, sig or "serving_default", s.version,
                                                 [(s.output_key, scores.contiguous())], raw)
 
+    def _live_fast(self):
+        """The live scheduler when exactly one servable is loaded (the common
+        case): serialized requests go straight to its native server, which
+        validates model name / version / signature itself."""
+        only = self.registry.only()
+        sched = getattr(only, "scheduler", None) if only is not None else None
+        return sched if sched is not None and hasattr(sched, "predict_raw") else None
+
     def predict_bytes(self, data: bytes, timeout_s: Optional[float] = None) -> bytes:
+        live = self._live_fast()
+        if live is not None:
+            t = self.timeout_s if timeout_s is None else timeout_s
+            code, msg, resp = live.predict_raw(data, t)
+            if code == 0:
+                return resp
+            # NOT_FOUND / oversize: the general path resolves or splits
+            if code not in (Code.NOT_FOUND, live.OVERSIZE):
+                raise ServingError(Code(code) if code in Code._value2member_map_ else Code.UNKNOWN, msg)
         fut, ctx = self.predict_async_bytes(data, timeout_s)
         return self.encode_predict(ctx, self._wait(fut, timeout_s))
 

@@ -1,0 +1,94 @@
+"""The native live server on the GPU backend (StepRunner + captured step
+kernels): concurrent served requests vs the model's eager forward, bucket
+choice for partial batches, the native load generator, bounded waits."""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_tf_serving_amd.client.synth import SyntheticRequests
+from distributed_tf_serving_amd.config import load_preset
+from distributed_tf_serving_amd.ops import native
+from distributed_tf_serving_amd.serving.errors import Code
+from distributed_tf_serving_amd.serving.live import LiveScheduler
+from distributed_tf_serving_amd.serving.server import ModelServer
+from distributed_tf_serving_amd.wire import schema as pb
+from distributed_tf_serving_amd.wire import tensor as T
+
+pytestmark = pytest.mark.gpu
+F = 43
+
+
+@pytest.fixture(scope="module")
+def server():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = load_preset("deepfm_1gpu")
+    cfg.model.vocab_size = 200_000
+    cfg.serving.max_batch_rows = 2048
+    cfg.serving.allowed_batch_sizes = (256, 2048)
+    srv = ModelServer(cfg, device="cuda:0")
+    yield srv
+    srv.stop()
+
+
+def _scores(resp):
+    return T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+
+
+def test_gpu_server_is_live(server):
+    s = server.registry.resolve("DCN")
+    assert isinstance(s.scheduler, LiveScheduler)
+    assert type(s.scheduler.srv).__module__.endswith("_hip")
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_concurrent_served_requests_match_eager_forward(server, raw):
+    model = server.registry.resolve("DCN").model
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=21)
+    reqs = []
+    for i in range(40):
+        rows = [512, 1, 100, 37, 300][i % 5]
+        ids, wts = synth.arrays(rows)
+        data = native().encode_predict_request("DCN", "serving_default", None,
+                                               [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                               raw)
+        reqs.append((data, ids, wts))
+    with cf.ThreadPoolExecutor(16) as pool:
+        outs = list(pool.map(lambda r: server.service.predict_bytes(r[0], 30.0), reqs))
+    for (data, ids, wts), resp in zip(reqs, outs):
+        got = _scores(resp)
+        want = model(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+        np.testing.assert_allclose(got, want, atol=2e-5)
+    st = server.registry.resolve("DCN").scheduler.stats()
+    assert st["steps"] < st["submitted"] and not st["broken"]
+
+
+def test_oversize_request_split(server):
+    model = server.registry.resolve("DCN").model
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="uniform", seed=5)
+    ids, wts = synth.arrays(5000)  # > 2048 rows: three batch-sized parts
+    data = native().encode_predict_request("DCN", "", None, [("feat_ids", torch.from_numpy(ids)),
+                                                             ("feat_wts", torch.from_numpy(wts))], True)
+    got = _scores(server.service.predict_bytes(data, 30.0))
+    want = model(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+    np.testing.assert_allclose(got, want, atol=2e-5)
+
+
+def test_native_load_generator(server):
+    live = server.registry.resolve("DCN").scheduler
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=8)
+    reqs = [synth.serialized(512) for _ in range(16)]
+    r = live.run_load(reqs, warmup=32, count=256, concurrency=32, threads=4, timeout_us=20_000_000)
+    assert r["errors"] == 0 and r["ok"] == r["submitted"] and len(r["latency_us"]) == 256
+    q = live.run_load(reqs, warmup=20, count=200, qps=4000.0, threads=2, timeout_us=20_000_000)
+    assert q["errors"] == 0 and len(q["latency_us"]) == 200
+    assert np.median(q["latency_us"]) < 20_000  # us
+
+
+def test_deadline_exceeded_reported(server):
+    live = server.registry.resolve("DCN").scheduler
+    synth = SyntheticRequests(fields=F, seed=1)
+    code, msg, _ = live.predict_raw(synth.serialized(64), 1e-6)
+    assert code in (0, Code.DEADLINE_EXCEEDED)

@@ -1,0 +1,266 @@
+"""The native live server (csrc/runtime/live_server.cpp) on its CPU backend:
+concurrent requests are batched into arenas, scored, answered per request;
+validation, oversize split, deadlines, failure -> UNAVAILABLE, close, the native
+load generator (closed and open loop) and lockstep stepping. Scores are
+checked against the model's fp32 forward on the same rows."""
+import concurrent.futures as cf
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_tf_serving_amd.client.synth import SyntheticRequests
+from distributed_tf_serving_amd.config import load_preset
+from distributed_tf_serving_amd.ops import native
+from distributed_tf_serving_amd.serving.errors import Code, ServingError
+from distributed_tf_serving_amd.serving.live import LiveScheduler
+from distributed_tf_serving_amd.serving.server import ModelServer, build_engine
+from distributed_tf_serving_amd.wire import schema as pb
+from distributed_tf_serving_amd.wire import tensor as T
+
+F = 43
+
+
+def _cfg(max_rows=64, buckets=(8, 64), timeout_us=300):
+    cfg = load_preset("wdl_tiny_cpu")
+    cfg.serving.max_batch_rows = max_rows
+    cfg.serving.allowed_batch_sizes = tuple(buckets)
+    cfg.serving.batch_timeout_us = timeout_us
+    return cfg
+
+
+@pytest.fixture(scope="module")
+def server():
+    srv = ModelServer(_cfg(), device="cpu")
+    yield srv
+    srv.stop()
+
+
+def _scores(resp: bytes) -> np.ndarray:
+    return T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+
+
+def _expected(srv, ids, wts):
+    m = srv.registry.resolve("DCN").model
+    return m(torch.as_tensor(ids), torch.as_tensor(wts)).numpy()
+
+
+def test_server_uses_live_scheduler(server):
+    s = server.registry.resolve("DCN")
+    assert isinstance(s.scheduler, LiveScheduler)
+    assert server.service._live_fast() is s.scheduler
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_concurrent_requests_match_fp32_forward(server, raw):
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=3)
+    reqs = []
+    for i in range(48):
+        rows = [1, 5, 17, 64, 3, 40][i % 6]
+        ids, wts = synth.arrays(rows)
+        data = native().encode_predict_request("DCN", "serving_default", None,
+                                               [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                               raw)
+        reqs.append((data, ids, wts))
+    before = server.registry.resolve("DCN").scheduler.stats()["steps"]
+    with cf.ThreadPoolExecutor(12) as pool:
+        outs = list(pool.map(lambda r: server.service.predict_bytes(r[0], 10.0), reqs))
+    for (data, ids, wts), resp in zip(reqs, outs):
+        got = _scores(resp)
+        assert got.shape == (ids.shape[0],)
+        np.testing.assert_allclose(got, _expected(server, ids, wts), atol=1e-5)
+    st = server.registry.resolve("DCN").scheduler.stats()
+    assert st["steps"] > before
+    # requests were coalesced: fewer steps than requests
+    assert st["steps"] - before < len(reqs)
+
+
+def test_packed_reference_request_with_fill_semantics(server):
+    from distributed_tf_serving_amd.client.simple import build_request
+
+    req = build_request(reference_shape=True)  # DCNClientSimple: [1500,43] with 87 ids -> oversize + fill
+    resp = pb.PredictResponse.FromString(server.service.predict_bytes(req.SerializeToString(), 30.0))
+    got = T.to_ndarray(resp.outputs["prediction_node"])
+    ids = T.to_ndarray(req.inputs["feat_ids"])
+    wts = T.to_ndarray(req.inputs["feat_wts"])
+    assert got.shape == (1500,)  # 1500 rows > 64: split into batch-sized raw requests and joined
+    np.testing.assert_allclose(got, _expected(server, ids, wts), atol=1e-5)
+
+
+def test_validation_errors(server):
+    live = server.registry.resolve("DCN").scheduler
+    synth = SyntheticRequests(fields=F, seed=1)
+    ok = synth.serialized(4)
+    # wrong model name -> NOT_FOUND from the native server, same from the service
+    other = SyntheticRequests(fields=F, seed=1, model_name="nope").serialized(4)
+    code, msg, _ = live.predict_raw(other, 5.0)
+    assert code == Code.NOT_FOUND
+    with pytest.raises(ServingError) as ei:
+        server.service.predict_bytes(other, 5.0)
+    assert ei.value.code == Code.NOT_FOUND
+    # wrong signature
+    bad_sig = SyntheticRequests(fields=F, seed=1, signature_name="x").serialized(4)
+    code, msg, _ = live.predict_raw(bad_sig, 5.0)
+    assert code == Code.INVALID_ARGUMENT and "signature" in msg
+    # wrong width
+    bad_w = native().encode_predict_request("DCN", "", None, [("feat_ids", torch.zeros(2, 7, dtype=torch.int64)),
+                                                              ("feat_wts", torch.zeros(2, 7))], True)
+    code, msg, _ = live.predict_raw(bad_w, 5.0)
+    assert code == Code.INVALID_ARGUMENT and "shape" in msg
+    # garbage
+    code, msg, _ = live.predict_raw(b"\x0a\x05garbage", 5.0)
+    assert code == Code.INVALID_ARGUMENT
+    # a good request still works afterwards
+    code, msg, resp = live.predict_raw(ok, 5.0)
+    assert code == 0 and _scores(resp).shape == (4,)
+
+
+def test_overlong_varint_rejected_without_overwrite(server):
+    """10+ continuation bytes must not turn into extra ids."""
+    live = server.registry.resolve("DCN").scheduler
+
+    def varint(v):
+        out = bytearray()
+        while v >= 0x80:
+            out.append((v & 0x7F) | 0x80)
+            v >>= 7
+        out.append(v)
+        return bytes(out)
+
+    ids = pb.TensorProto()
+    ids.dtype = pb.DT_INT64
+    ids.tensor_shape.dim.add().size = 1
+    ids.tensor_shape.dim.add().size = F
+    blob = bytes([0x80] * 20) + bytes([0x01]) + varint(5) * (F - 1)
+    raw_ids = ids.SerializeToString() + bytes([0x52]) + varint(len(blob)) + blob  # field 10 (int64_val) packed
+    req = pb.PredictRequest()
+    req.model_spec.name = "DCN"
+    req.inputs["feat_wts"].CopyFrom(T.make_tensor_proto(np.ones((1, F), np.float32)))
+    data = bytearray(req.SerializeToString())
+    key = b"feat_ids"
+    entry = bytes([0x0A]) + varint(len(key)) + key + bytes([0x12]) + varint(len(raw_ids)) + raw_ids
+    data += bytes([0x12]) + varint(len(entry)) + entry  # PredictRequest.inputs map entry
+    data = bytes(data)
+    # host decoder (slow path / parse_batch): rejected outright
+    parsed = native().parse_predict_request(data)
+    with pytest.raises(ValueError, match="10 bytes|more values"):
+        parsed.decode_into("feat_ids", torch.zeros(1, F, dtype=torch.int64))
+    # arena path (the GPU decodes varints: a value per terminator byte, at most
+    # 10 bytes looked at): the request is answered with its declared shape and
+    # a valid request batched right behind it is scored exactly
+    synth = SyntheticRequests(fields=F, seed=11)
+    ids, wts = synth.arrays(6)
+    good = native().encode_predict_request("DCN", "", None,
+                                           [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                           True)
+    done = {}
+    ev = threading.Event()
+
+    def cb(name):
+        def f(code, msg, resp):
+            done[name] = (code, msg, resp)
+            if len(done) == 2:
+                ev.set()
+        return f
+
+    live.srv.submit(data, 5.0, cb("bad"))
+    live.srv.submit(good, 5.0, cb("good"))
+    assert ev.wait(10)
+    code, msg, resp = done["bad"]
+    assert code == Code.INVALID_ARGUMENT or _scores(resp).shape == (1,)
+    code, msg, resp = done["good"]
+    assert code == 0
+    np.testing.assert_allclose(_scores(resp), _expected(server, ids, wts), atol=1e-5)
+
+
+def test_max_request_rows_checked_before_allocation(server):
+    live = server.registry.resolve("DCN").scheduler
+    # a ~100-byte request declaring 10^8 rows (fill semantics) is refused up front
+    ids = pb.TensorProto(dtype=pb.DT_INT64, int64_val=[1])
+    ids.tensor_shape.dim.add().size = 100_000_000
+    ids.tensor_shape.dim.add().size = F
+    wts = pb.TensorProto(dtype=pb.DT_FLOAT, float_val=[1.0])
+    wts.tensor_shape.CopyFrom(ids.tensor_shape)
+    req = pb.PredictRequest()
+    req.model_spec.name = "DCN"
+    req.inputs["feat_ids"].CopyFrom(ids)
+    req.inputs["feat_wts"].CopyFrom(wts)
+    with pytest.raises(ServingError) as ei:
+        server.service.predict_bytes(req.SerializeToString(), 5.0)
+    assert ei.value.code == Code.INVALID_ARGUMENT and "at most" in ei.value.message
+    assert live.max_request_rows < 100_000_000
+
+
+def test_classify_and_predict_messages_use_live_engine(server):
+    synth = SyntheticRequests(fields=F, seed=9)
+    msg = synth.message(70)  # > one 64-row batch: two raw sub-requests
+    resp = server.service.predict(msg, 10.0)
+    ids = T.to_ndarray(msg.inputs["feat_ids"])
+    wts = T.to_ndarray(msg.inputs["feat_wts"])
+    np.testing.assert_allclose(T.to_ndarray(resp.outputs["prediction_node"]), _expected(server, ids, wts), atol=1e-5)
+
+
+def test_native_load_generator_closed_and_open_loop(server):
+    live = server.registry.resolve("DCN").scheduler
+    synth = SyntheticRequests(fields=F, seed=5)
+    reqs = [synth.serialized(16) for _ in range(8)]
+    r = live.run_load(reqs, warmup=8, count=64, concurrency=8, threads=3)
+    assert r["ok"] == r["submitted"] == 8 + 64 + 8 and r["errors"] == 0
+    assert len(r["latency_us"]) == 64 and r["window_us"] > 0
+    r = live.run_load(reqs, warmup=4, count=40, qps=2000.0, threads=2)
+    assert r["ok"] == 44 and len(r["latency_us"]) == 40
+    assert all(x > 0 for x in r["latency_us"])
+
+
+def _engine(cfg):
+    return build_engine(cfg, device="cpu", slots=2)
+
+
+def test_deadline_and_close_and_broken():
+    cfg = _cfg(max_rows=8, buckets=(8,), timeout_us=100)
+    eng = _engine(cfg)
+    live = LiveScheduler(eng, cfg.serving)
+    synth = SyntheticRequests(fields=F, seed=2)
+    data = synth.serialized(8)
+    assert live.predict_raw(data, 5.0)[0] == 0
+    live.close()
+    code, msg, _ = live.predict_raw(data, 5.0)
+    assert code == Code.UNAVAILABLE
+    # a forward that fails marks the server broken: every later request UNAVAILABLE, no hang
+    eng2 = _engine(cfg)
+    calls = {"n": 0}
+    orig = eng2.launch
+
+    def bad_launch(*a, **k):
+        calls["n"] += 1
+        if calls["n"] >= 2:
+            raise RuntimeError("injected device failure")
+        return orig(*a, **k)
+
+    eng2.launch = bad_launch
+    live2 = LiveScheduler(eng2, cfg.serving)
+    assert live2.predict_raw(data, 5.0)[0] == 0
+    code, msg, _ = live2.predict_raw(data, 5.0)
+    assert code == Code.UNAVAILABLE and "injected" in msg
+    assert live2.broken
+    assert live2.predict_raw(data, 5.0)[0] == Code.UNAVAILABLE
+    live2.close()
+
+
+def test_lockstep_launches_empty_steps_and_stops_at_max_steps():
+    cfg = _cfg(max_rows=8, buckets=(4, 8), timeout_us=200)
+    eng = _engine(cfg)
+    live = LiveScheduler(eng, cfg.serving, lockstep=True, max_steps=30)
+    synth = SyntheticRequests(fields=F, seed=4)
+    code, _, resp = live.predict_raw(synth.serialized(3), 5.0)
+    assert code == 0 and _scores(resp).shape == (3,)
+    deadline = native().now_us() + 5_000_000
+    while live.stats()["steps"] < 30 and native().now_us() < deadline:
+        threading.Event().wait(0.01)
+    st = live.stats()
+    assert st["steps"] == 30 and st["empty_steps"] >= 20
+    assert st["padded_rows"] == 30 * 8  # lockstep: always the largest bucket
+    code, msg, _ = live.predict_raw(synth.serialized(3), 5.0)
+    assert code == Code.UNAVAILABLE
+    live.close()
