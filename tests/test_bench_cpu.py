@@ -21,13 +21,14 @@ def _free_port() -> int:
 
 def _run_bench(n: int, extra=()):
     args = ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--requests-per-gpu", "1",
-            "--request-rows", "64", "--pool", "2", *extra]
+            "--request-rows", "64", "--pool", "2", "--client-threads", "2", *extra]
     if n == 1:
         cmd = [sys.executable, *args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -54,3 +55,16 @@ def test_bench_json_contract(n):
 def test_bench_scatter_mode_world2():
     out = _run_bench(2, ("--mode", "scatter"))
     assert "scatter" in out["config"]["parallelism"] and out["config"]["global_batch"] == 128
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,mode", [(4, "alltoall"), (8, "alltoall"), (4, "scatter"), (4, "local")])
+def test_bench_more_ranks(n, mode):
+    """World 4 and 8 over gloo, with requests (20 rows) that do not divide by
+    the world size: every rank must finish the same lockstep steps (no hang)
+    and the job reports the whole-node rate."""
+    out = _run_bench(n, ("--mode", mode, "--request-rows", "20", "--requests-per-gpu", "2"))
+    assert out["n_gpus"] == n and out["config"]["global_batch"] == n * 40
+    assert out["value"] == pytest.approx(n * 40 / (out["ms_per_step"] * 1e-3), rel=0.02)
+    assert out.get("requests_failed", 0) == 0
+    assert (mode in out["config"]["parallelism"]) or (mode == "local" and "replica" in out["config"]["parallelism"])
