@@ -39,6 +39,14 @@ def init_from_env(device: str = "auto", backend: Optional[str] = None, timeout_s
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("DTFS_SHARE_GPU") == "1" and world > 1:
+        # rehearsal of an N-rank job on fewer GPUs (a 1-GPU box): RCCL refuses
+        # two ranks on one device of one host, so every rank claims its own
+        # host id and the ranks talk over RCCL's socket transport instead of
+        # xGMI - same communicators, collectives and step protocol
+        os.environ["NCCL_HOSTID"] = f"dtfs-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     use_cuda = torch.cuda.is_available() if device == "auto" else device.startswith("cuda")
     if use_cuda:
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))

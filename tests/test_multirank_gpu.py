@@ -1,0 +1,41 @@
+"""N > 1 rehearsal on a 1-GPU box: bench.py with 2 and 3 ranks sharing the one
+GPU (DTFS_SHARE_GPU: each rank its own RCCL host id, socket transport). This
+runs the native fan-out step (two RCCL communicators, ingress / egress
+streams), the lockstep live servers and the bounded waits with more than one
+rank on real hardware - the path the 8-GPU node runs over xGMI."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n,mode", [(2, "alltoall"), (3, "alltoall"), (2, "scatter"), (2, "local")])
+def test_bench_ranks_sharing_one_gpu(n, mode):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
+           "--steps", "20", "--warmup", "4", "--requests-per-gpu", "4", "--request-rows", "96", "--mode", mode,
+           "--pool", "8", "--client-threads", "2", "--qps", "0", "--step-timeout-s", "20"]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    if mode != "local":
+        assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
