@@ -753,6 +753,19 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("cin"), py::arg("mode"), py::arg("send"), py::arg("recv"), py::arg("forward_exec"), py::arg("cout"),
           py::arg("scores"), py::arg("back"), py::arg("h_out"), py::arg("d2h_bytes"))
       .def("wait", &dtfs::runtime::StepRunner::wait, py::arg("slot"), py::call_guard<py::gil_scoped_release>())
+      .def(
+          "wait_for",
+          [](dtfs::runtime::StepRunner& r, int slot, double timeout_s, std::vector<dtfs::comm::RcclComm*> comms) {
+            std::string err;
+            bool ok;
+            {
+              py::gil_scoped_release nogil;
+              ok = r.wait_for(slot, int64_t(timeout_s * 1e6), comms, &err);
+            }
+            return py::make_tuple(ok, err);
+          },
+          py::arg("slot"), py::arg("timeout_s"), py::arg("comms") = std::vector<dtfs::comm::RcclComm*>(),
+          "Bounded wait for the slot's step: (ok, error). Also polls the communicators' async errors.")
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
       .def_property_readonly("event_mode", &dtfs::runtime::StepRunner::event_mode)

@@ -40,19 +40,44 @@ from .dist import DistContext
 MODES = ("alltoall", "scatter", "local")
 
 
+class StepTimeout(RuntimeError):
+    """A step did not finish within the step timeout (a peer rank is gone, a
+    communicator failed, or the device hangs): the caller fails the step's
+    requests instead of blocking forever."""
+
+
 class _RunnerEvent:
     """Adapter so a StepHandle can wait on a native StepRunner slot."""
 
-    __slots__ = ("runner", "slot")
+    __slots__ = ("runner", "slot", "comms")
 
-    def __init__(self, runner, slot):
-        self.runner, self.slot = runner, slot
+    def __init__(self, runner, slot, comms=()):
+        self.runner, self.slot, self.comms = runner, slot, [c for c in comms if c is not None]
 
-    def synchronize(self):
-        self.runner.wait(self.slot)
+    def synchronize(self, timeout_s: Optional[float] = None):
+        if timeout_s is None:
+            self.runner.wait(self.slot)
+            return
+        ok, err = self.runner.wait_for(self.slot, float(timeout_s), self.comms)
+        if not ok:
+            raise StepTimeout(f"GPU step failed: {err}")
 
     def query(self) -> bool:
         return self.runner.query(self.slot)
+
+
+def _wait_event(ev, timeout_s: Optional[float]) -> None:
+    """Bounded wait on a torch event or a _RunnerEvent."""
+    if isinstance(ev, _RunnerEvent) or timeout_s is None:
+        ev.synchronize(timeout_s) if isinstance(ev, _RunnerEvent) else ev.synchronize()
+        return
+    deadline = time.monotonic() + timeout_s
+    spins = 0
+    while not ev.query():
+        if time.monotonic() > deadline:
+            raise StepTimeout(f"GPU step not finished after {timeout_s:.1f} s")
+        spins += 1
+        time.sleep(0 if spins < 200 else 5e-5)
 
 
 @dataclass
@@ -63,10 +88,12 @@ class StepHandle:
     event: Optional[object] = None
     t_submit: float = 0.0
     t_done: float = 0.0
+    timeout_s: Optional[float] = None
 
     def wait(self) -> torch.Tensor:
+        """Scores of the step; raises StepTimeout past the engine's step timeout."""
         if self.event is not None:
-            self.event.synchronize()
+            _wait_event(self.event, self.timeout_s)
         self.t_done = time.perf_counter()
         return self.host_out
 
@@ -124,6 +151,9 @@ class FanoutEngine:
         self.native_launch = native_launch
         self._runner = None
         self._step_graph: Dict[Tuple[int, int], object] = {}
+        # bound on every StepHandle.wait (None = unbounded): a multi-rank step
+        # waits on its peers, and a dead peer must not block this rank forever
+        self.step_timeout_s: Optional[float] = float(os.environ.get("DTFS_STEP_TIMEOUT_S", "30"))
 
     # -- geometry ------------------------------------------------------------
     def contrib_rows(self, B: int) -> int:
@@ -259,7 +289,9 @@ class FanoutEngine:
             slot, dst, h_in, h2d, ing.raw_cuda_graph_exec() if ing is not None else 0,
             self._cin, 0 if self.mode == "alltoall" else 1, send, self.ex.input_buffer(B, slot),
             self.ex._graphs[key].raw_cuda_graph_exec(), self._cout, self.ex._out[key], back, h_out, rows * 4)
-        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot), t_submit=t0)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot,
+                                                                                   (self._cin, self._cout)),
+                          t_submit=t0, timeout_s=self.step_timeout_s)
 
     def self_check(self, B: int, seed: int = 0, atol: float = 1e-5, slot: int = 0) -> bool:
         """Run one fan-out step on synthetic requests and compare every score
@@ -455,7 +487,7 @@ class FanoutEngine:
             # bookkeeping in the loop (csrc/runtime/step_runner.cpp)
             self.runner().launch(slot, dst, h_in, nbytes, self._step_graph[(B, slot)].raw_cuda_graph_exec())
             return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot),
-                              t_submit=t0)
+                              t_submit=t0, timeout_s=self.step_timeout_s)
         cur = torch.cuda.current_stream(self.dev)
         ev_in_free = self._ev_in_free.get(slot)
         with torch.cuda.stream(self.h2d_stream):  # SDMA, overlaps the previous step
@@ -468,7 +500,7 @@ class FanoutEngine:
         ev = torch.cuda.Event()
         ev.record(cur)
         self._ev_in_free[slot] = ev
-        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=ev, t_submit=t0)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=ev, t_submit=t0, timeout_s=self.step_timeout_s)
 
     # -- one step --------------------------------------------------------------
     def launch(self, B: int, slot: int = 0, src: Optional[torch.Tensor] = None,
@@ -560,7 +592,7 @@ class FanoutEngine:
                 h_out[:rows].copy_(back[:rows], non_blocking=True)
             done.record(self.d2h_stream)
         self._ev_out_free[slot] = done
-        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=done, t_submit=t0)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=done, t_submit=t0, timeout_s=self.step_timeout_s)
 
     def _launch_cpu(self, B, slot, h_in, h_out, rows, exec_in, t0) -> StepHandle:
         if self.mode == "alltoall":

@@ -34,6 +34,10 @@ from .errors import Code, ServingError
 log = logging.getLogger(__name__)
 
 
+class _AfterLaunchNotice(Exception):
+    """A launch that failed after ``on_launch`` told the follower ranks."""
+
+
 @dataclass
 class WorkItem:
     rows: int
@@ -45,13 +49,20 @@ class BatchingScheduler:
     def __init__(self, engine, max_batch_rows: int = 8192, batch_timeout_us: int = 200,
                  max_queued_rows: int = 1 << 22, depth: int = 2, name: str = "model",
                  fanout_world: int = 1, on_launch: Optional[Callable[[int, int], None]] = None,
-                 max_request_rows: int = 1 << 18):
+                 max_request_rows: int = 1 << 18, on_broken: Optional[Callable[[str], None]] = None):
         """``fanout_world`` > 1: this is the front door of a scatter fan-out
         (parallel/fanout.py): a step of bucket B carries up to world x B rows,
         split across the ranks. ``on_launch(B, slot)`` runs right before each
         step is launched (serving/cluster.py tells the follower ranks)."""
         self.eng = engine
         self.ex = engine.ex
+        self.name = name
+        # a failed multi-rank step (launch error after the followers were told,
+        # a step timeout, a communicator error) leaves the ranks' collective
+        # sequences out of step: the scheduler is then BROKEN - every queued and
+        # later request fails UNAVAILABLE and on_broken(reason) tears down
+        self.on_broken = on_broken
+        self.broken: Optional[str] = None
         self.layout = engine.layout
         self.world = max(1, int(fanout_world))
         self.on_launch = on_launch
@@ -74,6 +85,9 @@ class BatchingScheduler:
     # -- client side -------------------------------------------------------------
     def submit(self, rows: int, fill, deadline_us: int = 0) -> cf.Future:
         fut: cf.Future = cf.Future()
+        if self.broken is not None:
+            fut.set_exception(ServingError(Code.UNAVAILABLE, f"server unavailable: {self.broken}"))
+            return fut
         if rows <= 0:
             fut.set_result(torch.empty(0))
             return fut
@@ -124,9 +138,44 @@ class BatchingScheduler:
         return out
 
     # -- worker ------------------------------------------------------------------
+    def mark_broken(self, reason: str) -> None:
+        """Stop serving (idempotent): queued and later requests fail UNAVAILABLE."""
+        if self.broken is not None:
+            return
+        self.broken = reason
+        log.error("batching scheduler of %s broken: %s", self.name, reason)
+        self.batcher.close()
+        if self.on_broken is not None:
+            try:
+                self.on_broken(reason)
+            except Exception:  # noqa: BLE001 - best effort teardown
+                log.exception("on_broken failed")
+
+    def _fail_items(self, items, reason: str) -> None:
+        for it in items:
+            w = self._pop(it.ticket)
+            if w is not None and not w.future.done():
+                w.future.set_exception(ServingError(Code.UNAVAILABLE, f"server unavailable: {reason}"))
+
     def _loop(self) -> None:
         inflight: Deque = collections.deque()
         while True:
+            if self.broken is not None:
+                # drain: everything still queued fails, in-flight steps get a short grace
+                while inflight:
+                    self._complete(inflight.popleft())
+                batch = self.batcher.next_batch(0, True)
+                self._fail_items(batch.items, self.broken)
+                self._fail_items(batch.expired, self.broken)
+                if batch.closed and not batch.items:
+                    with self._lock:
+                        left = list(self._items.values())
+                        self._items.clear()
+                    for w in left:
+                        if not w.future.done():
+                            w.future.set_exception(ServingError(Code.UNAVAILABLE, f"server unavailable: {self.broken}"))
+                    break
+                continue
             # idle device: dispatch whatever is queued right away (latency);
             # steps in flight: accumulate up to the batch timeout (throughput)
             batch = self.batcher.next_batch(0 if inflight else 50_000, self.eager_when_idle and not inflight)
@@ -137,6 +186,11 @@ class BatchingScheduler:
             if batch.items:
                 try:
                     inflight.append(self._launch(batch))
+                except _AfterLaunchNotice as e:
+                    # the followers already joined this step: the ranks are out of step
+                    self._fail_items(batch.items, f"step launch failed: {e.__cause__}")
+                    self.mark_broken(f"step launch failed after the followers were told: {e.__cause__}")
+                    continue
                 except Exception as e:  # noqa: BLE001 - fail the batch, keep serving
                     log.exception("batch launch failed")
                     for it in batch.items:
@@ -181,17 +235,34 @@ class BatchingScheduler:
             ids_v[off:total].zero_()
             wts_v[off:total].zero_()
         if self.on_launch is not None:
-            self.on_launch(B, slot)
-        handle = self.eng.launch(B, slot)
+            try:
+                self.on_launch(B, slot)
+            except Exception as e:  # the control channel is gone: nobody can join this step
+                for w, _ in plan:
+                    w.future.set_exception(ServingError(Code.UNAVAILABLE, f"step control failed: {e}"))
+                self.mark_broken(f"step control channel failed: {e}")
+                raise _AfterLaunchNotice() from e
+            try:
+                handle = self.eng.launch(B, slot)
+            except Exception as e:
+                for w, _ in plan:
+                    w.future.set_exception(ServingError(Code.UNAVAILABLE, f"step launch failed: {e}"))
+                raise _AfterLaunchNotice() from e
+        else:
+            handle = self.eng.launch(B, slot)
         return handle, plan, off
 
     def _complete(self, entry) -> None:
         handle, plan, rows = entry
+        if self.broken is not None and handle.timeout_s is not None:
+            handle.timeout_s = min(handle.timeout_s, 0.5)
         try:
             scores = handle.wait()
-        except Exception as e:  # noqa: BLE001
+        except Exception as e:  # noqa: BLE001 - a step that never finishes or failed
             for w, _ in plan:
-                w.future.set_exception(ServingError(Code.INTERNAL, f"GPU step failed: {e}"))
+                if not w.future.done():
+                    w.future.set_exception(ServingError(Code.UNAVAILABLE, f"server unavailable: {e}"))
+            self.mark_broken(str(e))
             return
         self.steps += 1
         self.rows_served += rows

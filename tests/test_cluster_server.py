@@ -94,3 +94,83 @@ def test_cluster_server_scatter_gather(world):
     assert max(errs) < 1e-5, errs
     for r in range(1, world):
         assert res[r][1] == steps0, f"rank {r} followed {res[r][1]} steps, rank 0 ran {steps0}: {res[r][0]}"
+
+
+def _fault_worker(rank, world, port, q, die_rank, die_after):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import time
+
+    from distributed_tf_serving_amd.parallel.dist import init_from_env
+    from distributed_tf_serving_amd.serving.cluster import ClusterServer
+    from distributed_tf_serving_amd.serving.errors import Code, ServingError
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire.tensor import make_tensor_proto
+
+    try:
+        ctx = init_from_env(device="cpu", timeout_s=8)
+        fault = {"after": die_after} if rank == die_rank else None
+        srv = ClusterServer(_cfg(), ctx, control_timeout_s=5, step_timeout_s=5, follower_fault=fault)
+        if rank == 0:
+            rng = np.random.default_rng(1)
+            outcomes = []
+            t_fail = None
+            t0 = time.monotonic()
+            for i in range(12):
+                ids = rng.integers(0, 1 << 40, size=(40, 43), dtype=np.int64)
+                wts = rng.random((40, 43), dtype=np.float32)
+                req = pb.PredictRequest()
+                req.model_spec.name = "DCN"
+                req.inputs["feat_ids"].CopyFrom(make_tensor_proto(ids))
+                req.inputs["feat_wts"].CopyFrom(make_tensor_proto(wts))
+                ts = time.monotonic()
+                try:
+                    srv.service.predict(req, timeout_s=20)
+                    outcomes.append("ok")
+                except ServingError as e:
+                    outcomes.append(e.code.name)
+                    if t_fail is None:
+                        t_fail = time.monotonic() - ts
+            q.put((rank, outcomes, t_fail, srv.broken, time.monotonic() - t0))
+            srv.stop()
+        else:
+            try:
+                n = srv.serve_follower()
+                q.put((rank, "stopped", n, None, 0))
+            except Exception as e:  # the surviving follower: rank 0 went silent / peers gone
+                q.put((rank, "raised", repr(e)[:200], None, 0))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, 0))
+
+
+def test_cluster_dead_follower_fails_requests_instead_of_hanging():
+    """A follower dies after 2 steps: rank 0 answers the affected and every later
+    request UNAVAILABLE within its step timeout (no hang), the surviving
+    follower gives up on its own (reference DCNClient.java:185-188
+    has no failure handling at all)."""
+    world, die_rank = 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, world, port, q, die_rank, 2)) for r in range(world)]
+    [p.start() for p in procs]
+    res = {}
+    for _ in range(world - 1):  # the dead rank reports nothing
+        item = q.get(timeout=240)
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert 0 in res and isinstance(res[0][1], list), res
+    outcomes, t_fail, broken = res[0][1], res[0][2], res[0][3]
+    assert outcomes[:2] == ["ok", "ok"], outcomes
+    assert "UNAVAILABLE" in outcomes and broken, (outcomes, broken)
+    first_bad = outcomes.index("UNAVAILABLE")
+    assert all(o == "UNAVAILABLE" for o in outcomes[first_bad:]), outcomes
+    assert t_fail is not None and t_fail < 20, t_fail
+    assert procs[die_rank].exitcode == 17
+    assert res[1][1] in ("raised", "stopped"), res[1]
