@@ -151,8 +151,28 @@ def main(argv=None):
                     help="failure testing, e.g. 'after:100,kind:error' (serving/faults.py)")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="leave CPython's cyclic GC at its defaults (utils/gc_tuning.py)")
+    ap.add_argument("--frontends", type=int, default=1,
+                    help="server processes sharing the port (SO_REUSEPORT), each with its own model replica and "
+                         "live server on the same GPU: scales the grpcio front door past one GIL "
+                         "(profiles/grpc_ceiling.md)")
+    ap.add_argument("--frontend-index", type=int, default=0, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    children = []
+    if a.frontends > 1 and a.frontend_index == 0:
+        # started before this process touches the GPU; each child is a full server
+        import subprocess
+        import sys
+
+        base = [x for x in (argv if argv is not None else sys.argv[1:])]
+        for i in range(1, a.frontends):
+            extra = ["--frontends", "1", "--frontend-index", str(i)]
+            args = [x for x in base]
+            if "--monitoring-port" in args:  # only frontend 0 serves metrics
+                j = args.index("--monitoring-port")
+                del args[j:j + 2]
+            children.append(subprocess.Popen([sys.executable, "-m", "distributed_tf_serving_amd.serving.server",
+                                              *args, *extra]))
     cfg = load_preset(a.preset)
     if a.model_name:
         cfg.serving.model_name = a.model_name
@@ -166,7 +186,9 @@ def main(argv=None):
     port = srv.start_grpc(a.port, a.host, a.grpc_workers)
     if a.monitoring_port is not None:
         srv.start_monitoring(a.monitoring_port, a.host)
-    print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}", flush=True)
+    if a.frontend_index == 0:
+        print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}"
+              + (f" ({a.frontends} frontend processes)" if a.frontends > 1 else ""), flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:
         srv.front.wait()
@@ -174,6 +196,13 @@ def main(argv=None):
         pass
     finally:
         srv.stop()
+        for c in children:
+            c.terminate()
+        for c in children:
+            try:
+                c.wait(timeout=30)
+            except Exception:  # noqa: BLE001
+                c.kill()
 
 
 if __name__ == "__main__":
