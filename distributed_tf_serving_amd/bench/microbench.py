@@ -43,9 +43,18 @@ def bench_gemm(M, N, K, act="relu", dev="cuda"):
     xq, sx = ops.quant_rows_fp8(x)
     wq, sw = ops.quant_rows_fp8(W)
     f8 = _time(lambda: ops.linear_fp8(xq, sx, wq, sw, b, act))
-    return {"op": "gemm", "M": M, "N": N, "K": K, "us": round(ours, 2), "tflops": round(flops / ours / 1e6, 1),
-            "hipblaslt_us": round(lib, 2), "hipblaslt_tflops": round(flops / lib / 1e6, 1),
-            "fp8_us": round(f8, 2), "fp8_tflops": round(flops / f8 / 1e6, 1)}
+    out = {"op": "gemm", "M": M, "N": N, "K": K, "us": round(ours, 2), "tflops": round(flops / ours / 1e6, 1),
+           "hipblaslt_us": round(lib, 2), "hipblaslt_tflops": round(flops / lib / 1e6, 1),
+           "fp8_us": round(f8, 2), "fp8_tflops": round(flops / f8 / 1e6, 1)}
+    try:  # hipBLASLt fp8 (e4m3, per-tensor scales) on the same shape
+        a8 = x.float().clamp(-448, 448).to(torch.float8_e4m3fn)
+        w8 = W.float().mul(K ** 0.5).clamp(-448, 448).to(torch.float8_e4m3fn)
+        one = torch.ones((), device=dev)
+        lib8 = _time(lambda: torch._scaled_mm(a8, w8.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16))
+        out.update(hipblaslt_fp8_us=round(lib8, 2), hipblaslt_fp8_tflops=round(flops / lib8 / 1e6, 1))
+    except Exception as e:  # noqa: BLE001 - not every torch build has a fp8 hipBLASLt path
+        out["hipblaslt_fp8"] = f"unavailable: {type(e).__name__}: {str(e)[:80]}"
+    return out
 
 
 def bench_gemm_variants(M, N, K, dev="cuda", variants=(0, 2, 3, 4, 5, 6, 7, 8, 9)):
@@ -123,8 +132,16 @@ def main():
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
+    ap.add_argument("--serving", action="store_true",
+                    help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.serving:
+        for s in ((16384, 1024, 2752), (16384, 512, 1024), (16384, 256, 512), (8192, 2752, 2752),
+                  (8192, 1024, 2752)):
+            print(json.dumps(bench_gemm(*s)), flush=True)
+        print(json.dumps(bench_embed(16384)), flush=True)
+        return
     if a.variants:
         shape, vs = a.variants.split(":")
         M, N, K = (int(x) for x in shape.split(","))
