@@ -114,6 +114,8 @@ def parse_args():
                     help="N>1: issue collectives through torch.distributed instead of the C++ StepRunner")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a step not finished by then fails the run instead of hanging it")
+    ap.add_argument("--no-narrow", action="store_true",
+                    help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed int32 rows / bf16")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
     return ap.parse_args()
 
@@ -208,7 +210,7 @@ def run_live(a, ctx, cfg, model, eng, B):
     sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=(B,), batch_timeout_us=a.batch_timeout_us,
                        max_queued_rows=1 << 24, max_request_rows=1 << 20)
     live = LiveScheduler(eng, sc, buckets=[B], depth=a.slots, lockstep=lockstep, max_steps=max_steps,
-                         step_timeout_s=a.step_timeout_s, start_paused=lockstep)
+                         step_timeout_s=a.step_timeout_s, start_paused=lockstep, narrow=not a.no_narrow)
     extra = {}
     if world == 1 and pool:
         extra["fp32_check"] = fp32_check(cfg, model, live, pool[0])
@@ -257,7 +259,9 @@ def run_live(a, ctx, cfg, model, eng, B):
                                      "scores_per_s": round(300 * a.request_rows / w, 1) if w > 0 else None}
     st = live.stats()
     extra["server"] = {k: st[k] for k in ("steps", "full_steps", "timeout_steps", "eager_steps", "empty_steps",
-                                          "blocked_submits")}
+                                          "blocked_submits", "narrowed")}
+    extra["ingest"] = ("host-narrowed int32 rows + bf16 weights (K0 on the submitting thread)" if live.narrow_modulo
+                       else "raw request bytes, unpacked on the GPU")
     if a.json_extra and rank == 0:
         per = {k: round(st[k] / max(1, st["steps"]), 1) for k in ("copy_us", "build_us", "launch_us", "wait_us",
                                                                   "encode_us")}

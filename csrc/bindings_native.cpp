@@ -13,6 +13,7 @@
 #include "runtime/trace.h"
 #include "wire/tensor_codec.h"
 #include "live_bindings.h"
+#include "runtime/narrow.h"
 
 namespace py = pybind11;
 using namespace dtfs;
@@ -647,6 +648,29 @@ PYBIND11_MODULE(_native, m) {
     dtfs_live::def_live_methods(c);
   }
   m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
+  m.def(
+      "narrow_ids",
+      [](torch::Tensor ids, int64_t modulo) {
+        TORCH_CHECK(ids.device().is_cpu() && ids.scalar_type() == torch::kInt64, "ids must be CPU int64");
+        TORCH_CHECK(modulo >= 1 && modulo < (int64_t(1) << 31), "modulo must be in [1, 2^31)");
+        auto src = ids.contiguous();
+        auto out = torch::empty(src.sizes(), torch::kInt32);
+        runtime::narrow_ids(reinterpret_cast<const uint8_t*>(src.data_ptr()), out.data_ptr<int32_t>(), src.numel(),
+                            modulo);
+        return out;
+      },
+      py::arg("ids"), py::arg("modulo"), "Host K0: int64 ids -> int32 rows (python-style id mod modulo).");
+  m.def(
+      "narrow_wts",
+      [](torch::Tensor w) {
+        TORCH_CHECK(w.device().is_cpu() && w.scalar_type() == torch::kFloat32, "weights must be CPU fp32");
+        auto src = w.contiguous();
+        auto out = torch::empty(src.sizes(), torch::kBFloat16);
+        runtime::narrow_wts(reinterpret_cast<const uint8_t*>(src.data_ptr()),
+                            reinterpret_cast<uint16_t*>(out.data_ptr()), src.numel());
+        return out;
+      },
+      py::arg("wts"), "Host K0: fp32 weights -> bf16 (round to nearest even).");
   m.def("now_us", &runtime::now_us);
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));

@@ -74,22 +74,37 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* p) {
 
 // Request-arena header (csrc/runtime/arena.h): n_req @0, total_rows @8,
 // row_table_off @16 ({ids_off, wts_off} int32 per row, payload-relative).
+// A row whose ids_off has bit 31 set was narrowed by the host while it copied
+// the request (runtime/narrow.h): int32 table rows + bf16 weights, aligned.
 struct ArenaRow {
-  const uint8_t* ids;  // 8 * F bytes of int64 ids, or nullptr (padding row)
-  const uint8_t* wts;  // 4 * F bytes of fp32 weights
+  const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: 4 * F of int32 rows), or nullptr (padding row)
+  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 2 * F of bf16)
+  bool narrow;
 };
 
 __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payload_off, int64_t r) {
   const int64_t total = *reinterpret_cast<const int64_t*>(arena + 8);
-  ArenaRow out{nullptr, nullptr};
+  ArenaRow out{nullptr, nullptr, false};
   if (r < total) {
     const uint8_t* payload = arena + payload_off;
     const int64_t rt = *reinterpret_cast<const int64_t*>(arena + 16);
     const int2 o = reinterpret_cast<const int2*>(payload + rt)[r];
-    out.ids = payload + o.x;
+    out.narrow = o.x < 0;
+    out.ids = payload + (o.x & 0x7fffffff);
     out.wts = payload + o.y;
   }
   return out;
+}
+
+// Feature f of an arena row: raw int64 id (narrow: int32 row) and fp32 weight.
+__device__ __forceinline__ void arena_feature(const ArenaRow& ar, int f, int64_t& id, float& w) {
+  if (ar.narrow) {
+    id = int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
+    w = __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(ar.wts)[f]) << 16);
+  } else {
+    id = int64_t(load_u64_unaligned(ar.ids + 8 * f));
+    w = __uint_as_float(load_u32_unaligned(ar.wts + 4 * f));
+  }
 }
 
 // Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5,

@@ -113,8 +113,9 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
       int64_t id;
       float w_in;
       if constexpr (ARENA) {  // padding rows (no request): id 0, weight 0 -> zero contribution
-        id = arow.ids ? int64_t(load_u64_unaligned(arow.ids + 8 * fl)) : 0;
-        w_in = arow.ids ? __uint_as_float(load_u32_unaligned(arow.wts + 4 * fl)) : 0.f;
+        id = 0;
+        w_in = 0.f;
+        if (arow.ids) arena_feature(arow, fl, id, w_in);
       } else {
         id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
         w_in = a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f;
@@ -220,10 +221,7 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
     if (!fl_ok || r >= B) return;
     if constexpr (ARENA) {  // padding rows (no request): id 0, weight 0 -> zero contribution
       const ArenaRow ar = arena_row(static_cast<const uint8_t*>(a.arena), kArenaPayloadOff, r);
-      if (ar.ids) {
-        id = int64_t(load_u64_unaligned(ar.ids + 8 * lane));
-        w = __uint_as_float(load_u32_unaligned(ar.wts + 4 * lane));
-      }
+      if (ar.ids) arena_feature(ar, lane, id, w);
     } else {
       id = int64_t(static_cast<const IdT*>(a.ids)[int64_t(r) * a.ids_ld + lane]);
       w = a.wts ? a.wts[int64_t(r) * a.wts_ld + lane] : 1.f;

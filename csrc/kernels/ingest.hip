@@ -28,6 +28,22 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
   if (r >= B) return;
   const ArenaRow src = arena_row(arena, kArenaPayloadOff, r);
   int64_t* dst = packed + int64_t(r) * W;
+  if (src.narrow) {  // host-narrowed row: int32 rows -> int64, bf16 -> fp32 (packed as 2 per word)
+    for (int c = lane; c < W; c += 64) {
+      uint64_t v = 0;
+      if (c < F) {
+        v = uint64_t(int64_t(reinterpret_cast<const int32_t*>(src.ids)[c]));
+      } else {
+        const int f0 = 2 * (c - F);
+        const uint16_t* wb = reinterpret_cast<const uint16_t*>(src.wts);
+        const uint32_t lo = f0 < F ? uint32_t(wb[f0]) << 16 : 0u;
+        const uint32_t hi = f0 + 1 < F ? uint32_t(wb[f0 + 1]) << 16 : 0u;
+        v = (uint64_t(hi) << 32) | lo;
+      }
+      dst[c] = int64_t(v);
+    }
+    return;
+  }
   const int ids_bytes = 8 * F, row_bytes = 12 * F;
   // The ids and wts spans are multiples of 4 bytes long, so an output word
   // never straddles them except at the ids|wts boundary, which is 8-aligned in

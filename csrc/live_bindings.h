@@ -43,6 +43,7 @@ inline LiveConfig live_config_from(const py::dict& d) {
   if (get("max_steps")) c.max_steps = d["max_steps"].cast<int64_t>();
   if (get("step_timeout_us")) c.step_timeout_us = d["step_timeout_us"].cast<int64_t>();
   if (get("start_paused")) c.start_paused = d["start_paused"].cast<bool>();
+  if (get("narrow_modulo")) c.narrow_modulo = d["narrow_modulo"].cast<int64_t>();
   return c;
 }
 
@@ -161,6 +162,7 @@ void def_live_methods(py::class_<H>& c) {
             o["timeout_steps"] = s.timeout_steps;
             o["eager_steps"] = s.eager_steps;
             o["blocked_submits"] = s.blocked_submits;
+            o["narrowed"] = s.narrowed;
             o["copy_us"] = s.copy_us;
             o["build_us"] = s.build_us;
             o["launch_us"] = s.launch_us;

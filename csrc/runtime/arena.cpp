@@ -58,18 +58,40 @@ void arena_varint_cpu(uint8_t* base) {
 
 ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>& spans, const std::string& ids_key,
                        const std::string& wts_key, int64_t fields, int64_t max_rows, int64_t varint_chunks) {
-  if (int64_t(spans.size()) > kArenaMaxRequests) throw std::invalid_argument("too many requests for one arena");
+  std::vector<ArenaItem> items(spans.size());
+  for (size_t i = 0; i < spans.size(); ++i) {
+    items[i].off = spans[i].first;
+    items[i].len = spans[i].second;
+  }
+  return arena_build_items(base, capacity, items, ids_key, wts_key, fields, max_rows, varint_chunks);
+}
+
+ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<ArenaItem>& items,
+                             const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows,
+                             int64_t varint_chunks) {
+  if (int64_t(items.size()) > kArenaMaxRequests) throw std::invalid_argument("too many requests for one arena");
   uint8_t* payload = base + kArenaPayloadOff;
   const int64_t cap = capacity - kArenaPayloadOff;
   ArenaBatch out;
-  const size_t n = spans.size();
+  const size_t n = items.size();
   out.rows.assign(n, 0);
   out.offsets.assign(n, 0);
   out.errors.assign(n, std::string());
+  std::vector<Span> spans(n);
   int64_t end = 0;
-  for (const auto& s : spans) {
-    if (s.first < 0 || s.second < 0 || s.first + s.second > cap) throw std::invalid_argument("request span outside arena");
-    end = std::max(end, s.first + s.second);
+  for (size_t i = 0; i < n; ++i) {
+    const ArenaItem& it = items[i];
+    if (it.narrow) {
+      const int64_t ne = it.rows * fields;
+      if (it.rows < 0 || it.ids_off < 0 || it.wts_off < 0 || it.ids_off % 4 || it.wts_off % 2 ||
+          it.ids_off + 4 * ne > cap || it.wts_off + 2 * ne > cap)
+        throw std::invalid_argument("narrow request outside arena");
+      end = std::max(end, std::max(it.ids_off + 4 * ne, it.wts_off + 2 * ne));
+      continue;
+    }
+    spans[i] = {it.off, it.len};
+    if (it.off < 0 || it.len < 0 || it.off + it.len > cap) throw std::invalid_argument("request span outside arena");
+    end = std::max(end, it.off + it.len);
   }
   int64_t scratch = (end + 63) & ~int64_t(63);
   int64_t* desc = reinterpret_cast<int64_t*>(base + 64);
@@ -97,6 +119,7 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
   // requests that have uncounted varints
   std::vector<int64_t> to_count;
   for (size_t i = 0; i < n; ++i) {
+    if (items[i].narrow) continue;
     parsed_ok[i] = wire::parse_predict_request(payload + spans[i].first, size_t(spans[i].second), &views[i], &perr[i],
                                                false);
     if (!parsed_ok[i]) continue;
@@ -129,6 +152,22 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
   else if (!to_count.empty())
     count_one(to_count[0]);
   for (size_t i = 0; i < n; ++i) {
+    if (items[i].narrow) {
+      const int64_t rows = items[i].rows;
+      if (row + rows > max_rows) {
+        out.errors[i] = "batch exceeds the arena's row capacity";
+        continue;
+      }
+      desc[4 * nd + 0] = items[i].ids_off | kNarrowFlag;
+      desc[4 * nd + 1] = items[i].wts_off;
+      desc[4 * nd + 2] = rows;
+      desc[4 * nd + 3] = row;
+      ++nd;
+      out.rows[i] = rows;
+      out.offsets[i] = row;
+      row += rows;
+      continue;
+    }
     auto& v = views[i];
     if (!parsed_ok[i]) {
       out.errors[i] = "malformed PredictRequest: " + perr[i];
@@ -266,6 +305,14 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
   int32_t* tab = reinterpret_cast<int32_t*>(payload + rt);
   for (int64_t d = 0; d < nd; ++d) {
     const int64_t io = desc[4 * d + 0], wo = desc[4 * d + 1], rows = desc[4 * d + 2], r0 = desc[4 * d + 3];
+    if (io & kNarrowFlag) {
+      const int64_t ni = io & ~kNarrowFlag;
+      for (int64_t r = 0; r < rows; ++r) {
+        tab[2 * (r0 + r) + 0] = int32_t(uint32_t(ni + r * 4 * fields) | 0x80000000u);
+        tab[2 * (r0 + r) + 1] = int32_t(wo + r * 2 * fields);
+      }
+      continue;
+    }
     for (int64_t r = 0; r < rows; ++r) {
       tab[2 * (r0 + r) + 0] = int32_t(io + r * 8 * fields);
       tab[2 * (r0 + r) + 1] = int32_t(wo + r * 4 * fields);
@@ -291,9 +338,25 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
   const uint8_t* payload = base + kArenaPayloadOff;
   std::memset(dst, 0, size_t(B * W * 8));
   for (int32_t i = 0; i < n; ++i) {
+    const bool narrow = (desc[4 * i + 0] & kNarrowFlag) != 0;
     for (int64_t r = 0; r < desc[4 * i + 2]; ++r) {
       const int64_t row = desc[4 * i + 3] + r;
       if (row >= B) break;
+      if (narrow) {  // int32 rows -> int64, bf16 -> fp32
+        const uint8_t* ip = payload + (desc[4 * i + 0] & ~kNarrowFlag) + r * 4 * fields;
+        const uint8_t* wp = payload + desc[4 * i + 1] + r * 2 * fields;
+        for (int64_t f = 0; f < fields; ++f) {
+          int32_t id;
+          uint16_t h;
+          std::memcpy(&id, ip + 4 * f, 4);
+          std::memcpy(&h, wp + 2 * f, 2);
+          const int64_t id64 = id;
+          const uint32_t bits = uint32_t(h) << 16;
+          std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
+          std::memcpy(dst + row * W * 8 + 8 * fields + 4 * f, &bits, 4);
+        }
+        continue;
+      }
       std::memcpy(dst + row * W * 8, payload + desc[4 * i + 0] + r * 8 * fields, size_t(8 * fields));
       std::memcpy(dst + row * W * 8 + 8 * fields, payload + desc[4 * i + 1] + r * 4 * fields, size_t(4 * fields));
     }

@@ -54,6 +54,19 @@ struct ArenaBatch {
 
 using Span = std::pair<int64_t, int64_t>;  // (payload offset, length)
 
+// One request of a batch: a serialized PredictRequest span (parsed here), or
+// a request whose candidate features the submitting thread already narrowed
+// into the payload (runtime/narrow.h: int32 table rows at ids_off, bf16
+// weights at wts_off; payload-relative). A narrow request's row-table entries
+// carry bit 31 of ids_off (the GPU reads 4 + 2 bytes per feature there) and
+// its descriptor's ids_off carries kNarrowFlag.
+struct ArenaItem {
+  int64_t off = 0, len = 0;
+  bool narrow = false;
+  int64_t rows = 0, ids_off = 0, wts_off = 0;
+};
+constexpr int64_t kNarrowFlag = int64_t(1) << 62;
+
 // Copy requests into the payload (parallel memcpy); returns their spans.
 std::vector<Span> arena_place(uint8_t* arena, int64_t capacity, const std::vector<std::pair<const char*, size_t>>& reqs,
                               int64_t start);
@@ -66,6 +79,10 @@ std::vector<Span> arena_place(uint8_t* arena, int64_t capacity, const std::vecto
 // ids are decoded on the host pool instead).
 ArenaBatch arena_build(uint8_t* arena, int64_t capacity, const std::vector<Span>& spans, const std::string& ids_key,
                        const std::string& wts_key, int64_t fields, int64_t max_rows, int64_t varint_chunks = 0);
+// Same over a mix of serialized and narrowed requests (results in item order).
+ArenaBatch arena_build_items(uint8_t* arena, int64_t capacity, const std::vector<ArenaItem>& items,
+                             const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows,
+                             int64_t varint_chunks = 0);
 
 // Host reference of the GPU varint kernel: fills the arena's device-only id
 // region from its chunk table (a no-op when the build decoded on the host).

@@ -8,6 +8,7 @@
 
 #include "../wire/tensor_codec.h"
 #include "batcher.h"  // now_us()
+#include "narrow.h"
 #include "trace.h"
 
 namespace dtfs {
@@ -15,6 +16,7 @@ namespace runtime {
 
 namespace {
 int64_t align8(int64_t x) { return (x + 7) & ~int64_t(7); }
+int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
 std::string shape_str(const std::vector<int64_t>& s) {
   std::string o = "[";
@@ -125,12 +127,26 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   if (rows > max_rows_)
     return reject(kOversize, "request has " + std::to_string(rows) + " rows; a batch holds at most " +
                                  std::to_string(max_rows_));
-  const int64_t need = need_of(int64_t(n), rows);
+  // narrowable: raw int64 ids + fp32 weights (tensor_content, or packed
+  // float_val, which holds the same bytes)
+  const int64_t ne = rows * cfg_.fields;
+  const uint8_t* ids_src = nullptr;
+  const uint8_t* wts_src = nullptr;
+  if (cfg_.narrow_modulo > 0 && ti->dtype == wire::DT_INT64 && ti->content.n == size_t(ne) * 8 &&
+      tw->dtype == wire::DT_FLOAT) {
+    ids_src = ti->content.p;
+    if (tw->content.n == size_t(ne) * 4) wts_src = tw->content.p;
+    else if (tw->content.n == 0 && tw->value_fixed32 && tw->packed.size() == 1 && tw->unpacked.empty() &&
+             tw->packed[0].n == size_t(ne) * 4)
+      wts_src = tw->packed[0].p;
+  }
+  const bool narrow = ids_src && wts_src;
+  const int64_t need = narrow ? align64(4 * ne) + align64(2 * ne) + 8 * rows + 256 : need_of(int64_t(n), rows);
   if (need > arena_budget_) return reject(kOversize, "request does not fit one arena");
 
   const int64_t t0 = now_us();
   int a = -1;
-  int64_t off = 0;
+  int64_t off = 0, pend_ids = 0, pend_wts = 0;
   {
     std::unique_lock<std::mutex> lk(mu_);
     if (broken_) {
@@ -185,15 +201,26 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
     }
     a = open_;
     Arena& o = arenas_[size_t(a)];
-    off = o.used;
-    o.used += align8(int64_t(n));
+    Pending p{0, int64_t(n), rows, deadline_us, t0, std::move(done)};
+    if (narrow) {
+      p.narrow = true;
+      p.ids_off = align64(o.used);
+      p.wts_off = align64(p.ids_off + 4 * ne);
+      o.used = p.wts_off + 2 * ne;
+      ++st_.narrowed;
+    } else {
+      off = p.off = o.used;
+      o.used += align8(int64_t(n));
+    }
     o.rows += rows;
     o.need += need;
     if (o.pend.empty()) {
       o.t_first = t0;
       cv_launch_.notify_all();  // eager dispatch / batch timeout start now
     }
-    o.pend.push_back(Pending{off, int64_t(n), rows, deadline_us, t0, std::move(done)});
+    pend_ids = p.ids_off;
+    pend_wts = p.wts_off;
+    o.pend.push_back(std::move(p));
     ++o.writers;
     ++pending_;
     ++st_.submitted;
@@ -204,7 +231,13 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
     }
   }
   // the one copy of the request: into pinned memory the DMA engine reads
-  std::memcpy(arenas_[size_t(a)].base + kArenaPayloadOff + off, data, n);
+  uint8_t* payload = arenas_[size_t(a)].base + kArenaPayloadOff;
+  if (narrow) {  // ... narrowed on the way (K0 on the host)
+    narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
+    narrow_wts(wts_src, reinterpret_cast<uint16_t*>(payload + pend_wts), ne);
+  } else {
+    std::memcpy(payload + off, data, n);
+  }
   {
     std::lock_guard<std::mutex> lk(mu_);
     st_.copy_us += double(now_us() - t0);
@@ -373,15 +406,23 @@ void LiveServer::launcher_loop() {
     live.reserve(pend.size());
     for (auto& p : pend) (p.deadline_us > 0 && t0 > p.deadline_us ? expired : live).push_back(std::move(p));
     if (!expired.empty()) fail_all(expired, kDeadlineExceeded, "request deadline exceeded while queued");
-    std::vector<Span> spans;
-    spans.reserve(live.size());
-    for (const auto& p : live) spans.emplace_back(p.off, p.len);
+    std::vector<ArenaItem> items(live.size());
+    for (size_t i = 0; i < live.size(); ++i) {
+      const Pending& p = live[i];
+      ArenaItem& it = items[i];
+      it.off = p.off;
+      it.len = p.len;
+      it.narrow = p.narrow;
+      it.rows = p.rows;
+      it.ids_off = p.ids_off;
+      it.wts_off = p.wts_off;
+    }
     Arena& ar = arenas_[size_t(a)];
     ArenaBatch batch;
     try {
       trace::Range tr("live_build");
-      batch = arena_build(ar.base, ar.capacity, spans, cfg_.ids_key, cfg_.wts_key, cfg_.fields, max_rows_,
-                          cfg_.varint_chunks);
+      batch = arena_build_items(ar.base, ar.capacity, items, cfg_.ids_key, cfg_.wts_key, cfg_.fields, max_rows_,
+                                cfg_.varint_chunks);
     } catch (const std::exception& e) {
       fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
       {

@@ -103,12 +103,17 @@ struct LiveConfig {
   // launcher thread must not start its empty-step cadence before every rank
   // has finished its own start-up collectives.
   bool start_paused = false;
+  // > 0: requests with raw tensor_content int64 ids + fp32 weights are
+  // narrowed by the submitting thread while it copies them (runtime/narrow.h):
+  // ids -> int32 rows (id mod narrow_modulo: the model's table size), weights
+  // -> bf16. Halves the H2D bytes; other encodings travel raw.
+  int64_t narrow_modulo = 0;
 };
 
 struct LiveStats {
   int64_t submitted = 0, rejected = 0, completed = 0, failed = 0, expired = 0;
   int64_t steps = 0, rows = 0, padded_rows = 0, empty_steps = 0;
-  int64_t full_steps = 0, timeout_steps = 0, eager_steps = 0, blocked_submits = 0;
+  int64_t full_steps = 0, timeout_steps = 0, eager_steps = 0, blocked_submits = 0, narrowed = 0;
   double copy_us = 0, build_us = 0, launch_us = 0, wait_us = 0, encode_us = 0;
   bool broken = false;
   std::string error;
@@ -144,6 +149,8 @@ class LiveServer {
   struct Pending {
     int64_t off, len, rows, deadline_us, t_arrive;
     Completion done;
+    bool narrow = false;
+    int64_t ids_off = 0, wts_off = 0;  // narrow: payload offsets of the int32 rows / bf16 weights
   };
   struct Arena {
     uint8_t* base = nullptr;

@@ -1,0 +1,118 @@
+#include "narrow.h"
+
+#include <immintrin.h>
+
+#include <cstring>
+
+namespace dtfs {
+namespace runtime {
+
+namespace {
+
+inline int32_t mod_scalar(int64_t v, int64_t m) {
+  int64_t r = v % m;
+  if (r < 0) r += m;
+  return int32_t(r);
+}
+
+inline uint16_t bf16_scalar(uint32_t u) {
+  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x0040u);  // quiet NaN, sign kept
+  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+void narrow_ids_scalar(const uint8_t* src, int32_t* dst, int64_t n, int64_t m) {
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t v;
+    std::memcpy(&v, src + 8 * i, 8);
+    dst[i] = mod_scalar(v, m);
+  }
+}
+
+void narrow_wts_scalar(const uint8_t* src, uint16_t* dst, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t u;
+    std::memcpy(&u, src + 4 * i, 4);
+    dst[i] = bf16_scalar(u);
+  }
+}
+
+// 4 ids per iteration. For 0 <= v < 2^52: d = double(v) exactly (magic-number
+// conversion), q = floor(d / m) is the quotient or one off, r = v - q*m is
+// corrected into [0, m) with one compare each way. Lanes outside that range
+// (negative or huge ids) are redone in scalar code.
+__attribute__((target("avx2,fma"))) void narrow_ids_avx2(const uint8_t* src, int32_t* dst, int64_t n, int64_t m) {
+  const __m256i magic_i = _mm256_set1_epi64x(0x4330000000000000LL);
+  const __m256d magic_d = _mm256_set1_pd(4503599627370496.0);  // 2^52
+  const __m256d inv_m = _mm256_set1_pd(1.0 / double(m));
+  const __m256i mv = _mm256_set1_epi64x(m);
+  const __m256i lim = _mm256_set1_epi64x((1LL << 52) - 1);
+  const __m256i zero = _mm256_setzero_si256();
+  const __m256i pick = _mm256_setr_epi32(0, 2, 4, 6, 0, 2, 4, 6);
+  int64_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 8 * i));
+    // range check: 0 <= v <= 2^52 - 1
+    const __m256i bad = _mm256_or_si256(_mm256_cmpgt_epi64(zero, v), _mm256_cmpgt_epi64(v, lim));
+    const __m256d d = _mm256_sub_pd(_mm256_castsi256_pd(_mm256_or_si256(v, magic_i)), magic_d);
+    const __m256d qd = _mm256_floor_pd(_mm256_mul_pd(d, inv_m));
+    // q (< 2^52) back to integer bits the same way
+    const __m256i q = _mm256_sub_epi64(_mm256_castpd_si256(_mm256_add_pd(qd, magic_d)), magic_i);
+    // q * m with 32x32->64 products: q = qh * 2^32 + ql, m < 2^31
+    const __m256i lo = _mm256_mul_epu32(q, mv);
+    const __m256i hi = _mm256_slli_epi64(_mm256_mul_epu32(_mm256_srli_epi64(q, 32), mv), 32);
+    __m256i r = _mm256_sub_epi64(v, _mm256_add_epi64(lo, hi));
+    r = _mm256_add_epi64(r, _mm256_and_si256(_mm256_cmpgt_epi64(zero, r), mv));                     // r < 0: += m
+    r = _mm256_sub_epi64(r, _mm256_andnot_si256(_mm256_cmpgt_epi64(mv, r), mv));                     // r >= m: -= m
+    const __m128i r32 = _mm256_castsi256_si128(_mm256_permutevar8x32_epi32(r, pick));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), r32);
+    if (!_mm256_testz_si256(bad, bad)) {
+      for (int k = 0; k < 4; ++k) {
+        int64_t x;
+        std::memcpy(&x, src + 8 * (i + k), 8);
+        dst[i + k] = mod_scalar(x, m);
+      }
+    }
+  }
+  narrow_ids_scalar(src + 8 * i, dst + i, n - i, m);
+}
+
+__attribute__((target("avx2"))) void narrow_wts_avx2(const uint8_t* src, uint16_t* dst, int64_t n) {
+  const __m256i one = _mm256_set1_epi32(1);
+  const __m256i bias = _mm256_set1_epi32(0x7fff);
+  const __m256i absmask = _mm256_set1_epi32(0x7fffffff);
+  const __m256i inf = _mm256_set1_epi32(0x7f800000);
+  const __m256i qnan = _mm256_set1_epi32(0x00400000);
+  int64_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    __m256i out[2];
+    for (int h = 0; h < 2; ++h) {
+      const __m256i u = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 4 * (i + 8 * h)));
+      const __m256i rnd = _mm256_add_epi32(bias, _mm256_and_si256(_mm256_srli_epi32(u, 16), one));
+      __m256i r = _mm256_srli_epi32(_mm256_add_epi32(u, rnd), 16);
+      const __m256i nan = _mm256_cmpgt_epi32(_mm256_and_si256(u, absmask), inf);
+      const __m256i keep = _mm256_srli_epi32(_mm256_or_si256(u, qnan), 16);
+      out[h] = _mm256_blendv_epi8(r, keep, nan);
+    }
+    // 2 x 8 dwords (each < 2^16) -> 16 words in order
+    const __m256i packed = _mm256_permute4x64_epi64(_mm256_packus_epi32(out[0], out[1]), 0xD8);
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + i), packed);
+  }
+  narrow_wts_scalar(src + 4 * i, dst + i, n - i);
+}
+
+const bool g_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+
+}  // namespace
+
+void narrow_ids(const uint8_t* src, int32_t* dst, int64_t n, int64_t modulo) {
+  if (g_avx2) narrow_ids_avx2(src, dst, n, modulo);
+  else narrow_ids_scalar(src, dst, n, modulo);
+}
+
+void narrow_wts(const uint8_t* src, uint16_t* dst, int64_t n) {
+  if (g_avx2) narrow_wts_avx2(src, dst, n);
+  else narrow_wts_scalar(src, dst, n);
+}
+
+}  // namespace runtime
+}  // namespace dtfs

@@ -58,6 +58,9 @@ StepRunner::StepRunner(int device, int slots) : device_(device), event_mode_(eve
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
     ck(hipEventCreateWithFlags(&done_[i], done_flags()), "hipEventCreate");
   }
+  gate_after_ = std::max(0, env_int("DTFS_H2D_GATE", 0));
+  gate_.resize(slots);
+  for (int i = 0; i < slots; ++i) ck(hipEventCreateWithFlags(&gate_[i], hipEventDisableTiming), "hipEventCreate");
 }
 
 unsigned StepRunner::done_flags() const {
@@ -72,7 +75,7 @@ StepRunner::~StepRunner() {
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamSynchronize(s);
   for (hipStream_t s : extra_copy_) hipStreamSynchronize(s);
-  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_})
+  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_, &gate_})
     for (auto e : *v) hipEventDestroy(e);
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamDestroy(s);
@@ -91,7 +94,8 @@ void StepRunner::ensure_fanout_streams() {
   }
 }
 
-void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate) {
+void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
+                     bool gated) {
   hipStream_t st = copy_;
   if (alternate && n_copy_ > 1 && extra_copy_.empty()) {
     for (int i = 1; i < n_copy_; ++i) {
@@ -109,6 +113,7 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
   // loop waits for step k-3 before launching k).
   if (used_[slot] && (copy_wait_always_ || !observed_[slot].load(std::memory_order_acquire)))
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
+  if (gated && last_gate_slot_ >= 0) ck(hipStreamWaitEvent(st, gate_[last_gate_slot_], 0), "hipStreamWaitEvent(gate)");
   if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D)");
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
   ck(hipStreamWaitEvent(consumer, h2d_done_[slot], 0), "hipStreamWaitEvent(h2d)");
@@ -164,8 +169,10 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
-  h2d(slot, dst, src, nbytes, compute_, true);
-  seq->launch(compute_, done_[slot], event_mode_ >= 2, skip_varint);
+  h2d(slot, dst, src, nbytes, compute_, true, true);
+  seq->launch(compute_, done_[slot], event_mode_ >= 2, skip_varint, gate_after_ > 0 ? gate_[slot] : nullptr,
+              gate_after_);
+  last_gate_slot_ = gate_after_ > 0 ? slot : -1;
   used_[slot] = 1;
 }
 

@@ -88,7 +88,8 @@ class StepRunner {
   int device_;
   int event_mode_ = 0;
   unsigned done_flags() const;
-  void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
+  void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
+           bool gated = false);
   int n_copy_ = 1;
   bool copy_wait_always_ = false;
   bool spin_wait_ = false;
@@ -100,6 +101,14 @@ class StepRunner {
   void ensure_fanout_streams();
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
+  // H2D gate (DTFS_H2D_GATE = k, default 0 = off): step k+1's H2D waits until
+  // step k's first k kernels (the embedding gather) have run, so the DMA
+  // overlaps the GEMMs instead of the latency-bound gather it slows ~2x
+  // (profiles/kernel_counters.md). Measured on MI355X it costs 2-13 % (the
+  // serialised H2D outweighs the faster gather: profiles/ingest_ab.md).
+  std::vector<hipEvent_t> gate_;
+  int gate_after_ = 0;
+  int last_gate_slot_ = -1;
   std::vector<char> used_;  // not vector<bool>: written by the launcher, read by the waiter
 };
 

@@ -77,6 +77,7 @@ class ServingConfig:
     request_timeout_s: float = 10.0
     live: bool = True                 # native live server (csrc/runtime/live_server.h); False: Python scheduler
     step_timeout_s: float = 10.0      # a GPU step that takes longer marks the server broken (UNAVAILABLE)
+    narrow_ingest: bool = True        # GPU live server: int64 ids -> int32 rows, fp32 weights -> bf16 on the host
 
 
 @dataclass

@@ -33,6 +33,10 @@ from .errors import Code, ServingError
 log = logging.getLogger(__name__)
 
 
+# families whose forward hashes every id with one modulo (cfg.vocab_size)
+NARROW_FAMILIES = ("wdl", "deepfm", "dcn", "dcn_v2")
+
+
 def _code(c: int) -> Code:
     try:
         return Code(int(c))
@@ -46,7 +50,7 @@ class LiveScheduler:
     def __init__(self, engine, serving_cfg, buckets: Optional[Sequence[int]] = None, n_arenas: Optional[int] = None,
                  depth: Optional[int] = None, lockstep: bool = False, max_steps: int = -1,
                  step_timeout_s: float = 10.0, model_name: Optional[str] = None, version: Optional[int] = None,
-                 start_paused: bool = False):
+                 start_paused: bool = False, narrow: Optional[bool] = None):
         if engine.ingest != "arena":
             raise ValueError("the live server needs an arena-ingest FanoutEngine")
         sc = serving_cfg
@@ -64,6 +68,15 @@ class LiveScheduler:
         self.output_key, self.ids_key, self.wts_key = sc.output_key, sc.ids_key, sc.wts_key
         self.signature_name = sc.signature_name
         depth = int(depth or self.ex.slots)
+        # host-side K0 (csrc/runtime/narrow.h): single-table families hash ids
+        # with one modulo (the table size), so the host can narrow them to
+        # int32 rows + bf16 weights while it copies each request
+        model = self.ex.model
+        can_narrow = (getattr(model, "family", "") in NARROW_FAMILIES
+                      and 0 < int(getattr(model.cfg, "vocab_size", 0)) < (1 << 31))
+        if narrow is None:  # default: GPU servables (a CPU backend gains nothing from fewer bytes)
+            narrow = bool(getattr(sc, "narrow_ingest", True)) and engine.cuda
+        self.narrow_modulo = int(model.cfg.vocab_size) if (narrow and can_narrow) else 0
         self.arenas = [self.layout.alloc(pin=engine.cuda) for _ in range(int(n_arenas or depth + 3))]
         self.config = dict(
             fields=self.fields, ids_key=sc.ids_key, wts_key=sc.wts_key, model_name=self.model_name,
@@ -73,7 +86,7 @@ class LiveScheduler:
             depth=depth, varint_chunks=self.layout.varint_chunks,
             max_pending=max(64, sc.max_queued_rows // max(1, min(self.buckets))),
             lockstep=lockstep, max_steps=max_steps, step_timeout_us=int(step_timeout_s * 1e6),
-            start_paused=start_paused)
+            start_paused=start_paused, narrow_modulo=self.narrow_modulo)
         if engine.cuda:
             from ..ops import hip
 

@@ -264,3 +264,49 @@ def test_lockstep_launches_empty_steps_and_stops_at_max_steps():
     code, msg, _ = live.predict_raw(synth.serialized(3), 5.0)
     assert code == Code.UNAVAILABLE
     live.close()
+
+
+def test_host_narrowing_matches_python():
+    """runtime/narrow.cpp (AVX2 + scalar tails) vs python's modulo and torch's bf16 cast."""
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([rng.integers(0, 1 << 40, 4099), rng.integers(-(1 << 62), 1 << 62, 1001),
+                           np.array([0, 1, -1, (1 << 52) - 1, 1 << 52, (1 << 63) - 1, -(1 << 63), 999_999,
+                                     1_000_000, 2_000_000, -1_000_000], dtype=np.int64)]).astype(np.int64)
+    for m in (1, 7, 1_000_000, (1 << 31) - 1):
+        got = native().narrow_ids(torch.from_numpy(vals), m).numpy()
+        want = np.array([int(v) % m for v in vals.tolist()], dtype=np.int64)
+        assert np.array_equal(got.astype(np.int64), want), m
+    w = torch.from_numpy(np.concatenate([rng.standard_normal(5003).astype(np.float32),
+                                         np.array([0.0, -0.0, 1e-40, 3.4e38, np.inf, -np.inf], np.float32)]))
+    got = native().narrow_wts(w)
+    assert torch.equal(got.view(torch.int16), w.to(torch.bfloat16).view(torch.int16))
+    nan = native().narrow_wts(torch.tensor([float("nan"), -float("nan")] * 9))
+    assert torch.isnan(nan.float()).all()
+
+
+def test_live_server_narrowed_ingest_matches_forward_with_bf16_weights():
+    cfg = _cfg(max_rows=64, buckets=(8, 64))
+    cfg.model.vocab_size = 100_000
+    eng = _engine(cfg)
+    live = LiveScheduler(eng, cfg.serving, narrow=True)
+    assert live.narrow_modulo == 100_000
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=12)
+    model = eng.ex.model
+    reqs = []
+    for rows in (1, 9, 33, 64, 5):
+        ids, wts = synth.arrays(rows)
+        raw = native().encode_predict_request("DCN", "", None, [("feat_ids", torch.from_numpy(ids)),
+                                                                ("feat_wts", torch.from_numpy(wts))], True)
+        packed = native().encode_predict_request("DCN", "", None, [("feat_ids", torch.from_numpy(ids)),
+                                                                   ("feat_wts", torch.from_numpy(wts))], False)
+        reqs.append((raw, packed, ids, wts))
+    with cf.ThreadPoolExecutor(6) as pool:
+        outs = list(pool.map(lambda r: (live.predict_bytes(r[0], 10.0), live.predict_bytes(r[1], 10.0)), reqs))
+    for (raw, packed, ids, wts), (r_raw, r_packed) in zip(reqs, outs):
+        w16 = torch.from_numpy(wts).to(torch.bfloat16).float()
+        want16 = model(torch.from_numpy(ids), w16).numpy()
+        want32 = model(torch.from_numpy(ids), torch.from_numpy(wts)).numpy()
+        np.testing.assert_allclose(_scores(r_raw), want16, atol=1e-5)      # narrowed: bf16 weights
+        np.testing.assert_allclose(_scores(r_packed), want32, atol=1e-5)   # packed varint ids travel raw
+    assert live.stats()["narrowed"] == len(reqs)
+    live.close()
