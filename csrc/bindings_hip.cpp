@@ -235,7 +235,8 @@ torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tenso
 torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor> bias, int64_t epi,
                    c10::optional<torch::Tensor> x0, c10::optional<torch::Tensor> xl, bool out_f32,
                    c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sw, c10::optional<torch::Tensor> out,
-                   int64_t variant) {
+                   int64_t variant, c10::optional<torch::Tensor> sa_blk, c10::optional<torch::Tensor> q_out,
+                   c10::optional<torch::Tensor> sq_out) {
   check_dev(A, "A");
   check_dev(W, "W");
   check_same_dev(A, W, "W");
@@ -243,8 +244,10 @@ torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor
   const bool fp8 = A.scalar_type() == torch::kFloat8_e4m3fn || A.scalar_type() == torch::kUInt8;
   if (fp8) {
     TORCH_CHECK(W.scalar_type() == A.scalar_type(), "fp8 GEMM needs fp8 (e4m3fn) A and W");
-    TORCH_CHECK(sa.has_value() && sw.has_value(), "fp8 GEMM needs row scales sa [M] and channel scales sw [N]");
+    TORCH_CHECK((sa.has_value() || sa_blk.has_value()) && sw.has_value(),
+                "fp8 GEMM needs row scales sa [M] (or MX block scales sa_blk) and channel scales sw [N]");
   } else {
+    TORCH_CHECK(!sa_blk && !q_out, "MX block scales are an fp8-path feature");
     TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && W.scalar_type() == torch::kBFloat16, "bf16 GEMM needs bf16 A, W");
   }
   const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
@@ -272,6 +275,35 @@ torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor
                   "x0/xl must be bf16 [M, N]");
     }
   }
+  dtfs::MxIO mx;
+  if (sa_blk) {
+    check_dev(*sa_blk, "sa_blk");
+    TORCH_CHECK(sa_blk->scalar_type() == torch::kUInt8 && sa_blk->dim() == 2 && sa_blk->size(0) == M &&
+                    sa_blk->size(1) >= K / 32 && sa_blk->stride(1) == 1 && sa_blk->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(sa_blk->data_ptr()) % 4 == 0,
+                "sa_blk must be uint8 [M, >= K/32] (E8M0 per 32 K elements)");
+    TORCH_CHECK(K % 128 == 0 && K <= 3072, "MX block scales need K % 128 == 0 and K <= 3072");
+    mx.sab = sa_blk->data_ptr<uint8_t>();
+    mx.ldsab = sa_blk->stride(0);
+  }
+  if (q_out) {
+    TORCH_CHECK(sq_out.has_value() && (epi & 15) == 3, "q_out needs sq_out and the cross epilogue");
+    check_dev(*q_out, "q_out");
+    check_dev(*sq_out, "sq_out");
+    TORCH_CHECK((q_out->scalar_type() == torch::kFloat8_e4m3fn || q_out->scalar_type() == torch::kUInt8) &&
+                    q_out->dim() == 2 && q_out->size(0) == M && q_out->size(1) >= N && q_out->size(1) % 32 == 0 &&
+                    q_out->stride(1) == 1 && q_out->stride(0) % 4 == 0,
+                "q_out must be e4m3 [M, >= N, multiple of 32]");
+    TORCH_CHECK(sq_out->scalar_type() == torch::kUInt8 && sq_out->dim() == 2 && sq_out->size(0) == M &&
+                    sq_out->size(1) >= q_out->size(1) / 32 && sq_out->stride(1) == 1,
+                "sq_out must be uint8 [M, >= q columns / 32]");
+    TORCH_CHECK(N % 32 == 0, "MX output needs N % 32 == 0");
+    mx.q = static_cast<uint8_t*>(q_out->data_ptr());
+    mx.ldq = q_out->stride(0);
+    mx.sq = sq_out->data_ptr<uint8_t>();
+    mx.ldsq = sq_out->stride(0);
+    mx.nq = int(q_out->size(1));
+  }
   c10::DeviceGuard g(A.device());
   torch::Tensor C;
   if (out) {
@@ -285,7 +317,7 @@ torch::Tensor gemm(torch::Tensor A, torch::Tensor W, c10::optional<torch::Tensor
   check_hip(dtfs::launch_gemm(A.data_ptr(), K, W.data_ptr(), K, bias ? bias->data_ptr<float>() : nullptr,
                               sa ? sa->data_ptr<float>() : nullptr, sw ? sw->data_ptr<float>() : nullptr, C.data_ptr(),
                               N, out_f32, opt_ptr(x0), opt_ptr(xl), N, int(M), int(N), int(K), int(epi), fp8,
-                              cur_stream(A), int(variant)),
+                              cur_stream(A), int(variant), (sa_blk || q_out) ? &mx : nullptr),
             "gemm");
   return C;
 }
@@ -699,7 +731,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("W"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("x0") = py::none(), py::arg("xl") = py::none(), py::arg("out_f32") = false,
         py::arg("sa") = py::none(), py::arg("sw") = py::none(), py::arg("out") = py::none(),
-        py::arg("variant") = 0);
+        py::arg("variant") = 0, py::arg("sa_blk") = py::none(), py::arg("q_out") = py::none(),
+        py::arg("sq_out") = py::none());
   m.def("cross_v1", &cross_v1, py::arg("x0"), py::arg("w"), py::arg("b"), py::arg("want_x") = true,
         py::arg("head_w") = py::none());
   m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0);

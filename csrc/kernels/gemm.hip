@@ -40,14 +40,27 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((ch
 // covers the whole 128-byte K tile. The real scales (per activation row, per
 // weight channel) stay in the fp32 epilogue. Lane l holds row l&15,
 // k = 32*(l>>4) .. +31 = 16-B chunks 2*(l>>4) and 2*(l>>4)+1 of the row.
+// Operand layout of the 16x16x128 f8f6f4 MFMA (measured, bench_native/mx_probe.hip):
+// lane (r = l & 15, q = l >> 4) holds row r, K [16q, 16q + 16) in its first 4
+// VGPRs and K [64 + 16q, 64 + 16q + 16) in the last 4; the scale operand of
+// lane (r, q) scales row r's K block [32q, 32q + 32). Loading 16-byte chunks q
+// and q + 4 of the 128-byte K row keeps logical K = hardware K, so the MX
+// block scales line up (any common permutation would do for unscaled use).
 __device__ __forceinline__ i32x8 mx_frag(const uint8_t* tile, int row, int fq) {
-  const i32x4 lo = *reinterpret_cast<const i32x4*>(tile + swz(row, 2 * fq));
-  const i32x4 hi = *reinterpret_cast<const i32x4*>(tile + swz(row, 2 * fq + 1));
+  const i32x4 lo = *reinterpret_cast<const i32x4*>(tile + swz(row, fq));
+  const i32x4 hi = *reinterpret_cast<const i32x4*>(tile + swz(row, fq + 4));
   return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
 __device__ __forceinline__ f32x4 mx_mfma(const i32x8& a, const i32x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// Same with a real E8M0 block scale for the b operand (the activation
+// fragment: lane l holds row l&15, K block l>>4, and supplies that block's
+// scale byte; OCP MX: value = e4m3 x 2^(scale - 127)).
+__device__ __forceinline__ f32x4 mx_mfma_sb(const i32x8& a, const i32x8& b, const f32x4& c, int scale_b) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, scale_b);
 }
 
 // Every kernel below issues its MFMAs as D = W_frag x A_frag^T, i.e. it
@@ -117,6 +130,83 @@ __device__ __forceinline__ void store_acc_t(const f32x4 (&acc)[TM][TN], int mb, 
           else C[int64_t(m) * ldc + nn] = x;
         }
       }
+    }
+  }
+}
+
+// DCN-v2 cross epilogue that ALSO emits its output as the next cross layer's
+// A operand in OCP MX-fp8: e4m3 values + one E8M0 scale per 32 consecutive
+// columns of a row (the K blocks of the consumer's 16x16x128 MFMA). A lane
+// holds 4 columns of a row in each of the tile pair (j, j+1) = 32 columns; the
+// 4 lanes sharing the row (fq = 0..3, xor-shuffle 16 / 32) reduce the block
+// maximum, so no row-wide pass is needed (replaces quant_rows on the cross
+// chain). Columns [N, nq) of q are written as zeros (the consumer's K padding).
+template <int TM, int TN, typename OutT>
+__device__ __forceinline__ void store_cross_mx(const f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq, int M, int N,
+                                               const float* __restrict__ bias, const float* __restrict__ sa,
+                                               const float* __restrict__ sw, OutT* __restrict__ C, int64_t ldc,
+                                               const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx,
+                                               const MxIO& mx) {
+  static_assert(TN % 2 == 0, "MX output needs column-tile pairs");
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = mb + i * 16 + fr;
+    const bool row_ok = m < M;
+    const float sam = (sa && row_ok) ? sa[m] : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; j += 2) {
+      float v[2][4];
+      float amax = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = nb + (j + h) * 16 + fq * 4;  // N % 32 == 0: all 4 columns in range or none
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[h][r] = 0.f;
+        if (row_ok && n < N) {
+          const bf16x4 x0 = *reinterpret_cast<const bf16x4*>(X0 + int64_t(m) * ldx + n);
+          const bf16x4 xl = *reinterpret_cast<const bf16x4*>(XL + int64_t(m) * ldx + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = acc[i][j + h][r] * (sw ? sw[n + r] : 1.f) * sam + (bias ? bias[n + r] : 0.f);
+            v[h][r] = bf2f(x0[r]) * x + bf2f(xl[r]);
+          }
+          if constexpr (sizeof(OutT) == 2) {
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(v[h][r]);
+            *reinterpret_cast<bf16x4*>(C + int64_t(m) * ldc + n) = o;
+          } else {
+            *reinterpret_cast<f32x4*>(C + int64_t(m) * ldc + n) = f32x4{v[h][0], v[h][1], v[h][2], v[h][3]};
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(v[h][r]));
+      }
+      // block max over the 4 lanes of this row (lanes fr, fr+16, fr+32, fr+48)
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      // E8M0 exponent: smallest e with amax / 2^e <= 448 (e4m3 max)
+      int e = 0;
+      if (amax > 0.f) {
+        int ex;
+        (void)frexpf(amax / 448.f, &ex);  // amax/448 = f * 2^ex, f in [0.5, 1)
+        e = ex;
+        if (ldexpf(448.f, e - 1) >= amax) e -= 1;
+        e = max(-127, min(127, e));
+      }
+      const float inv = ldexpf(1.f, -e);
+      if (!row_ok) continue;
+      const int n32 = nb + j * 16;  // first column of the 32-column block
+      if (n32 >= mx.nq) continue;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = nb + (j + h) * 16 + fq * 4;
+        int w = 0;
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(v[h][0] * inv, v[h][1] * inv, w, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(v[h][2] * inv, v[h][3] * inv, w, true);
+        *reinterpret_cast<int*>(mx.q + int64_t(m) * mx.ldq + n) = w;
+      }
+      if (fq == 0) mx.sq[int64_t(m) * mx.ldsq + n32 / 32] = uint8_t(e + 127);
     }
   }
 }
@@ -248,11 +338,16 @@ __global__ void __launch_bounds__(256) gemm_kernel(const uint8_t* __restrict__ A
 // SOURCE chunk (rule 21), so the fragment reads use the same swz() as above.
 // Requires K % (128 / elem bytes) == 0; rows past M / N are clamped (their
 // results are never stored).
-template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+constexpr int kMxMaxKBlocks = 96;  // MX-scaled A: K <= 3072 (the scale panel lives in LDS)
+
+// MXM (fp8 only): bit 0 = MX block scales on A (mx.sab), bit 1 = MX-fp8 output
+// (mx.q); separate instantiations, so the plain kernels keep their registers.
+template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT, int MXM = 0>
 __device__ __forceinline__ void gemm_glds_body(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
-    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
+    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi,
+    const MxIO& mx) {
   constexpr int NW = WM_ * WN_;
   constexpr int EB = FP8 ? 1 : 2;
   constexpr int WTM = BM / WM_, WTN = BN / WN_;
@@ -263,7 +358,8 @@ __device__ __forceinline__ void gemm_glds_body(
 
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE_BYTES];
 
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  // an MX-fp8 output also covers its zero K-padding columns [N, nq)
+  const int tiles_n = (((MXM & 2) ? max(N, mx.nq) : N) + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   // Tile order: N-fastest by default, so each XCD's contiguous run of tiles is
   // a few row panels x ALL column panels - the big activation panel is pulled
@@ -315,11 +411,56 @@ __device__ __forceinline__ void gemm_glds_body(
 
   const int nk = (K * EB) / 128;
   const int fr = lane & 15, fq = lane >> 4;
+  // MX activation block scales: this lane's row of fragment i, K block 4 kt + fq;
+  // prefetched one K tile ahead (the end-of-tile barrier waits for them).
+  // MX activation block scales: the block's whole [BM x K/32] scale panel is
+  // staged in LDS once (coalesced), laid out [K block][wave row group][fr][i]
+  // so a lane's TM scale bytes for one K block are one contiguous LDS word
+  // (per-K-tile scattered byte loads from global measured ~1.5x slower).
+  // The panel's dword loads are all issued before tile 0's DMA, and their LDS
+  // writes land before the barrier that waits for tile 0 (one round trip).
+  __shared__ __attribute__((aligned(16))) uint8_t sscale[(MXM & 1) ? kMxMaxKBlocks * BM : 4];
+  constexpr int NSW = (MXM & 1) ? (BM * kMxMaxKBlocks / 4 + NW * 64 - 1) / (NW * 64) : 1;
+  uint32_t swv[NSW];
+  const int KBW = K / 128;  // scale dwords per row
+  if constexpr ((MXM & 1) != 0) {
+#pragma unroll
+    for (int u = 0; u < NSW; ++u) {
+      const int idx = threadIdx.x + u * NW * 64;
+      if (idx < BM * KBW) {
+        const int r = idx / KBW, c = idx - r * KBW;
+        const int gm = min(m0 + r, M - 1);
+        swv[u] = *reinterpret_cast<const uint32_t*>(mx.sab + int64_t(gm) * mx.ldsab + 4 * c);
+      }
+    }
+  }
   stage(0, 0);
-  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
+  if constexpr ((MXM & 1) != 0) {
+#pragma unroll
+    for (int u = 0; u < NSW; ++u) {
+      const int idx = threadIdx.x + u * NW * 64;
+      if (idx < BM * KBW) {
+        const int r = idx / KBW, c = idx - r * KBW;
+        const int pos = (r / WTM) * WTM + (r % 16) * TM + (r % WTM) / 16;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) sscale[(4 * c + t) * BM + pos] = uint8_t(swv[u] >> (8 * t));
+      }
+    }
+  }
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 (and the scale panel) landed
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    // this K tile's MX scale word, read BEFORE the next tile's DMA is issued
+    // (an LDS read after it makes the compiler wait for the DMA first)
+    uint32_t sw4 = 0;
+    if constexpr ((MXM & 1) != 0) {
+      const uint8_t* sp = sscale + (4 * kt + fq) * BM + wm * WTM + fr * TM;
+      if constexpr (TM == 4) sw4 = *reinterpret_cast<const uint32_t*>(sp);
+      else if constexpr (TM == 2) sw4 = *reinterpret_cast<const uint16_t*>(sp);
+      else sw4 = *sp;
+    }
     if (kt + 1 < nk) stage(cur ^ 1, kt + 1);  // DMA of the next tile under this tile's MFMAs
+
     const uint8_t* as = smem + cur * STAGE_BYTES;
     const uint8_t* bs = as + BM * 128;
     if constexpr (!FP8) {
@@ -351,16 +492,31 @@ __device__ __forceinline__ void gemm_glds_body(
       for (int i = 0; i < TM; ++i) af[i] = mx_frag(as, wm * WTM + i * 16 + fr, fq);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = mx_frag(bs, wn * WTN + j * 16 + fr, fq);
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr ((MXM & 1) != 0) {
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+          const int sbi = int((sw4 >> (8 * i)) & 0xffu);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(bfr[j], af[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma_sb(bfr[j], af[i], acc[i][j], sbi);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mx_mfma(bfr[j], af[i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
     __syncthreads();  // next tile landed (vmcnt(0)) and everyone is done reading this one
   }
 
+  if constexpr (FP8 && (MXM & 2) != 0) {
+    store_cross_mx(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, mx);
+    return;
+  }
   store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
@@ -368,21 +524,23 @@ __device__ __forceinline__ void gemm_glds_body(
   const uint8_t *__restrict__ A, int64_t lda, const uint8_t *__restrict__ W, int64_t ldw,                           \
       const float *__restrict__ bias, const float *__restrict__ sa, const float *__restrict__ sw,                   \
       OutT *__restrict__ C, int64_t ldc, const bf16 *__restrict__ X0, const bf16 *__restrict__ XL, int64_t ldx,     \
-      int M, int N, int K, int epi
+      int M, int N, int K, int epi, MxIO mx
 
-template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT, int MXM>
 __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_glds_kernel(DTFS_GLDS_ARGS) {
-  gemm_glds_body<BM, BN, WM_, WN_, FP8, OutT>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi);
+  gemm_glds_body<BM, BN, WM_, WN_, FP8, OutT, MXM>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi,
+                                                   mx);
 }
 
-template <int BM, int BN, int WM_, int WN_, bool FP8, typename OutT>
+template <int BM, int BN, int WM_, int WN_, bool FP8, int MXM = 0, typename OutT>
 static void launch_glds(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                         const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M,
-                        int N, int K, int epi, hipStream_t st) {
-  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM_, WN_, FP8, OutT>), dim3(grid), dim3(WM_ * WN_ * 64), 0, st,
+                        int N, int K, int epi, hipStream_t st, const MxIO& mx = MxIO()) {
+  const int Nt = (MXM & 2) ? (N > mx.nq ? N : mx.nq) : N;
+  const int grid = ((M + BM - 1) / BM) * ((Nt + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM_, WN_, FP8, OutT, MXM>), dim3(grid), dim3(WM_ * WN_ * 64), 0, st,
                      static_cast<const uint8_t*>(A), lda, static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc,
-                     X0, XL, ldx, M, N, K, epi);
+                     X0, XL, ldx, M, N, K, epi, mx);
 }
 
 // ---------------------------------------------------------------------------
@@ -903,10 +1061,26 @@ static void launch_cfg(const void* A, int64_t lda, const void* W, int64_t ldw, c
 template <bool FP8, typename OutT>
 static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                      const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M, int N,
-                     int K, int epi, hipStream_t st, int variant) {
+                     int K, int epi, hipStream_t st, int variant, const MxIO& mx) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int EB = FP8 ? 1 : 2;
   const bool glds_ok = (K * EB) % 128 == 0;
+  if constexpr (FP8) {
+  if (mx.sab || mx.q) {
+    // block-scaled activations in / out: the LDS-DMA kernels (32-column-aligned
+    // wave tiles, a barrier per K tile so the scale-byte loads need no counting)
+    const bool big = blocks(128, 128) >= 512;
+#define DTFS_MX_LAUNCH(MXM)                                                                                         \
+  (big ? launch_glds<128, 128, 2, 4, FP8, MXM>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st, \
+                                               mx)                                                                  \
+       : launch_glds<64, 64, 2, 2, FP8, MXM>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st, mx))
+    if (mx.sab && mx.q) DTFS_MX_LAUNCH(3);
+    else if (mx.sab) DTFS_MX_LAUNCH(1);
+    else DTFS_MX_LAUNCH(2);
+#undef DTFS_MX_LAUNCH
+    return;
+  }
+  }
   if (variant == 0 && glds_ok) {
     // Measured on MI355X (bench/microbench.py --gemm-variants, interleaved):
     //  * M <= 1024 (one request's candidates): 64x64 tiles, 4-deep LDS ring
@@ -1033,17 +1207,24 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
 
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
-                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st, int variant) {
+                       int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st, int variant,
+                       const MxIO* mxp) {
   if (M == 0 || N == 0) return hipSuccess;
   if ((fp8 ? K % 16 : K % 8) != 0) return hipErrorInvalidValue;  // 16-byte row chunks
+  const MxIO mx = mxp ? *mxp : MxIO();
+  if ((mx.sab || mx.q) && (!fp8 || K % 128 != 0)) return hipErrorInvalidValue;
+  if (mx.sab && (K / 32 > kern::kMxMaxKBlocks || mx.ldsab % 4 != 0 || reinterpret_cast<uintptr_t>(mx.sab) % 4 != 0))
+    return hipErrorInvalidValue;
+  if (mx.q && ((epi & 15) != EPI_CROSS || !mx.sq || N % 32 != 0 || mx.nq < N || mx.nq % 32 != 0))
+    return hipErrorInvalidValue;
   const bf16* x0 = static_cast<const bf16*>(X0);
   const bf16* xl = static_cast<const bf16*>(XL);
   if (fp8) {
-    if (out_f32) dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
-    else dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
+    if (out_f32) dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant, mx);
+    else dispatch<true>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant, mx);
   } else {
-    if (out_f32) dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
-    else dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant);
+    if (out_f32) dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<float*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant, mx);
+    else dispatch<false>(A, lda, W, ldw, bias, sa, sw, static_cast<bf16*>(C), ldc, x0, xl, ldx, M, N, K, epi, st, variant, mx);
   }
   return hipGetLastError();
 }

@@ -66,11 +66,27 @@ hipError_t launch_embedding_bag(const void* table, const void* idx, bool idx64, 
                                 const float* psw, int nbags, int64_t nnz, int D, int64_t modulo, bool mean, float* out_f32,
                                 void* out_bf16, int64_t out_stride, hipStream_t st);
 
+// Block-scaled (OCP MX) fp8 activations on the fp8 GEMM path: e4m3 values with
+// one E8M0 scale byte per 32 consecutive K elements of a row.
+//   sab != nullptr : A's block scales [M][ldsab], fed to the MFMA scale operand
+//   q   != nullptr : the (cross) epilogue also writes its output as e4m3 q
+//                    [M][ldq] + block scales sq [M][ldsq]; columns [N, nq) of q
+//                    are zero (the consumer's K padding)
+struct MxIO {
+  const uint8_t* sab = nullptr;
+  int64_t ldsab = 0;
+  uint8_t* q = nullptr;
+  int64_t ldq = 0;
+  uint8_t* sq = nullptr;
+  int64_t ldsq = 0;
+  int nq = 0;
+};
+
 // K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
                        int64_t ldx, int M, int N, int K, int epi, bool fp8, hipStream_t st,
-                       int variant = 0);
+                       int variant = 0, const MxIO* mx = nullptr);
 
 // K4+K6 fused: y[m] = out_act(act(A W^T + b)[m,:] . hw + hbias + extra[m]); N <= 256, bf16.
 hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,

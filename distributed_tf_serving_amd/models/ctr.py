@@ -26,6 +26,7 @@ dlrm         sigmoid(head(topMLP(dot(botMLP(dense), emb_t))))
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -192,8 +193,13 @@ class DCNv2(CTRModel):
         self.head_wd = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
                                     requires_grad=False)
         self.head_b = 0.0
+        # MX-fp8 cross chain (DTFS_MX_CHAIN=0: per-row re-quantisation, for A/B)
+        self.mx_chain = os.environ.get("DTFS_MX_CHAIN", "1") != "0"
 
-    def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor) -> torch.Tensor:
+    def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None, emit_mx: int = 0):
+        """One cross layer. fp8: ``xq`` = (q, row scales | None, MX block scales
+        | None) of xl; ``emit_mx`` > 0 also returns this layer's output as the
+        next layer's MX-fp8 operand (q, block scales)."""
         if self.low_rank:
             # x0 * (U (V xl) + b) + xl : the cross epilogue rides on the U GEMM
             v = self.cross_v[i](xl)
@@ -201,17 +207,34 @@ class DCNv2(CTRModel):
             return ops.cross_v2(x0, xl, u.weight, u.bias, a=v)
         layer = self.cross[i]
         if self.fp8:
-            xq, sx = ops.quant_rows_fp8(xl, ops.FP8_K_PAD)
-            return ops.linear_fp8(xq, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
+            q, sx, sblk = xq if xq is not None else (*ops.quant_rows_fp8(xl, ops.FP8_K_PAD), None)
+            return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl, sx_blk=sblk,
+                                  emit_mx=emit_mx)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
     def _forward(self, ids, wts, out=None):
         x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
-        xl = x0
-        for i in range(self.cfg.num_cross_layers):
-            xl = self._cross_layer(i, x0, xl)
+        # fp8 towers: x0 is quantised once, for the first cross layer AND the
+        # first MLP layer (both read it); each cross layer's epilogue hands the
+        # next one its output already in MX-fp8 (e4m3 + per-32 E8M0 scales), so
+        # the chain has no separate quantisation pass.
+        fp8_full = self.fp8 and not self.low_rank
+        q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
+        nq = -(-self.d // ops.FP8_K_PAD) * ops.FP8_K_PAD
+        chain = fp8_full and self.mx_chain and self.d % ops.MX_BLOCK == 0 and nq <= ops.MX_MAX_K
+        xl, xq = x0, ((*q0, None) if q0 is not None else None)
+        L = self.cfg.num_cross_layers
+        for i in range(L):
+            emit = nq if (chain and i < L - 1) else 0
+            r = self._cross_layer(i, x0, xl, xq, emit)
+            if emit:
+                xl, q, sq = r
+                xq = (q, None, sq)
+            else:
+                xl, xq = r, None
         cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
-        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out)
+        mlp_q = q0 if (q0 is not None and self.mlp.layers[0].fp8 and self.mlp.layers[0].k == x0.shape[1]) else None
+        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out, xq=mlp_q)
 
 
 class DLRM(CTRModel):

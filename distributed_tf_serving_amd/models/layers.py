@@ -109,9 +109,10 @@ class Dense(nn.Module):
         self.register_buffer("w_scale", sw.contiguous(), persistent=False)
         self.fp8 = True
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, xq=None) -> torch.Tensor:
+        """``xq``: (q, scale) of x already quantised by the caller (fp8 layers)."""
         if self.fp8:
-            xq, sx = ops.quant_rows_fp8(x, ops.FP8_K_PAD)
+            xq, sx = xq if xq is not None else ops.quant_rows_fp8(x, ops.FP8_K_PAD)
             return ops.linear_fp8(xq, sx, self.w_fp8, self.w_scale, self.bias, self.act)
         return ops.linear(x, self.weight, self.bias, self.act)
 
@@ -136,15 +137,15 @@ class MLP(nn.Module):
 
     def forward_head(self, x: torch.Tensor, head_w: torch.Tensor, head_b: float,
                      extra: Optional[torch.Tensor] = None, sigmoid: bool = True,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, xq=None) -> torch.Tensor:
         """MLP then CTR head. On the GPU the last layer and the head run as one
         kernel (ops.linear_head) whenever its shape allows; it writes ``out``
         (device or pinned host memory) directly. (Fusing the last TWO layers
         as well streams both weights through every 64-row block: measured
         48.0 us vs 34.5 us for GEMM + fused head at 16384 rows on MI355X -
         weight-load latency bound - so that fusion is not used.)"""
-        for layer in self.layers[:-1]:
-            x = layer(x)
+        for k, layer in enumerate(self.layers[:-1]):
+            x = layer(x, xq if k == 0 else None)
         last = self.layers[-1]
         if x.is_cuda and not last.fp8 and last.act in ("relu", "none") and ops.linear_head_ok(x, last.weight):
             return ops.linear_head(x, last.weight, last.bias, last.act, head_w, head_b, extra=extra, sigmoid=sigmoid,

@@ -208,16 +208,62 @@ def quant_rows_fp8(x: torch.Tensor, k_pad: int = 1) -> Tuple[torch.Tensor, torch
     return q, scale
 
 
-def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
+MX_BLOCK = 32  # OCP MX: one E8M0 scale per 32 consecutive K elements
+MX_MAX_K = 3072  # MX-scaled GEMM input: the block's scale panel is staged in LDS
+
+
+def _mx_exponent(amax: torch.Tensor) -> torch.Tensor:
+    """Smallest e with amax / 2^e <= FP8_MAX (0 for an all-zero block)."""
+    m, ex = torch.frexp(amax / FP8_MAX)
+    e = torch.where(m == 0.5, ex - 1, ex)
+    return torch.where(amax > 0, e, torch.zeros_like(e)).clamp(-127, 127)
+
+
+def quant_mx_fp8(x: torch.Tensor, k_pad: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """OCP MX-fp8 quantisation of rows (CPU reference of the GEMM epilogue that
+    emits it): q e4m3 [M, Kq] and E8M0 scale bytes [M, Kq / 32] with
+    x ~= q * 2^(scale - 127) per 32-column block; K padding is zero (scale 127)."""
+    M, K = x.shape
+    Kq = -(-K // max(k_pad, MX_BLOCK)) * max(k_pad, MX_BLOCK)
+    xf = torch.zeros(M, Kq, dtype=torch.float32, device=x.device)
+    xf[:, :K] = x.float()
+    blk = xf.view(M, Kq // MX_BLOCK, MX_BLOCK)
+    e = _mx_exponent(blk.abs().amax(dim=2))
+    q = (blk * torch.exp2(-e.float())[:, :, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q.view(M, Kq), (e + 127).to(torch.uint8)
+
+
+def dequant_mx_fp8(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    return q.float() * torch.exp2(s.float() - 127).repeat_interleave(MX_BLOCK, dim=1)
+
+
+def linear_fp8(xq: torch.Tensor, sx: Optional[torch.Tensor], Wq: torch.Tensor, sw: torch.Tensor,
                b: Optional[torch.Tensor] = None, act: str = "none", out_f32: bool = False,
-               x0: Optional[torch.Tensor] = None, xl: Optional[torch.Tensor] = None) -> torch.Tensor:
+               x0: Optional[torch.Tensor] = None, xl: Optional[torch.Tensor] = None,
+               sx_blk: Optional[torch.Tensor] = None, emit_mx: int = 0):
     """fp8 x fp8 -> fp32-accumulated GEMM with row/channel scales (CDNA4 fp8 MFMA).
 
-    ``x0``/``xl`` given selects the DCN-v2 cross epilogue."""
+    ``x0``/``xl`` given selects the DCN-v2 cross epilogue.
+    ``sx_blk``: MX block scales of xq (uint8 E8M0 [M, K/32]) applied by the MFMA
+    itself, instead of (or on top of) the row scales ``sx``.
+    ``emit_mx = nq > 0`` (cross epilogue only): the epilogue also writes its
+    output as the next GEMM's MX-fp8 operand; returns (y, q [M, nq], scales
+    [M, nq/32])."""
     epi = 3 if x0 is not None else _ACTS[act]
+    if emit_mx and epi != 3:
+        raise ValueError("emit_mx needs the cross epilogue")
     if xq.is_cuda:
-        return hip().gemm(xq, Wq, b, epi, x0, xl, out_f32, sx, sw, None)
-    y = (xq.float() * sx[:, None]) @ (Wq.float() * sw[:, None]).t()
+        if emit_mx:
+            M = xq.shape[0]
+            q = torch.empty(M, emit_mx, dtype=torch.float8_e4m3fn, device=xq.device)
+            sq = torch.empty(M, emit_mx // MX_BLOCK, dtype=torch.uint8, device=xq.device)
+            y = hip().gemm(xq, Wq, b, epi, x0, xl, out_f32, sx, sw, None, 0, sx_blk, q, sq)
+            return y, q, sq
+        return hip().gemm(xq, Wq, b, epi, x0, xl, out_f32, sx, sw, None, 0, sx_blk)
+    xf = dequant_mx_fp8(xq, sx_blk) if sx_blk is not None else xq.float()
+    if sx is not None:
+        xf = xf * sx[:, None]
+    y = xf @ (Wq.float() * sw[:, None]).t()
     if b is not None:
         y = y + b.float()
     if epi == 3:
@@ -226,7 +272,10 @@ def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.T
         y = torch.relu(y)
     elif act == "sigmoid":
         y = torch.sigmoid(y)
-    return y if out_f32 else y.to(torch.bfloat16)
+    out = y if out_f32 else y.to(torch.bfloat16)
+    if emit_mx:
+        return (out,) + quant_mx_fp8(y, emit_mx)
+    return out
 
 
 # ------------------------------------------------------------------ K3

@@ -210,6 +210,65 @@ def test_quant_rows_fp8(cuda):
     assert exact > 0.99, f"only {exact:.4f} of fp8 values bit-identical"
 
 
+@pytest.mark.parametrize("M,N,K", [(100, 256, 512), (1000, 2752, 2816), (8192, 2752, 2816)])
+def test_gemm_mx_block_scaled_input(cuda, M, N, K):
+    # activations in OCP MX-fp8 (per-32 E8M0 block scales fed to the MFMA)
+    g = torch.Generator().manual_seed(3 + M)
+    x = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 6, (1, K // 32), generator=g).float()
+                                                     ).repeat_interleave(32, dim=1)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    q, s = ops.quant_mx_fp8(x, 128)
+    wq, sw = ops.quant_rows_fp8(W.to(cuda), ops.FP8_K_PAD)
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.linear_fp8(q.to(cuda), None, wq, sw, b.to(cuda), "relu", out_f32=True, sx_blk=s.to(cuda))
+    ref = ops.linear_fp8(q, None, wq.cpu(), sw.cpu(), b, "relu", out_f32=True, sx_blk=s)
+    _close(y, ref, 2e-3, 2e-3, f"MX-fp8 input {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("M", [100, 8192])
+def test_cross_mx_epilogue(cuda, M):
+    # the cross epilogue writes bf16 y AND y as the next layer's MX-fp8 operand
+    N, K = 2752, 2816
+    g = torch.Generator().manual_seed(M)
+    x0 = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    xl = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, N, generator=g) / N ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    xq, sx = ops.quant_rows_fp8(xl.to(cuda), ops.FP8_K_PAD)
+    wq, sw = ops.quant_rows_fp8(W.to(cuda), ops.FP8_K_PAD)
+    # poison the output buffers' previous contents: padding must be written
+    torch.cuda.empty_cache()
+    junk = torch.full((M, K), 0x7F, dtype=torch.uint8, device=cuda)
+    del junk
+    y, q, sq = ops.linear_fp8(xq, sx, wq, sw, b.to(cuda), x0=x0.to(cuda), xl=xl.to(cuda), emit_mx=K)
+    yr, qr, sqr = ops.linear_fp8(xq.cpu(), sx.cpu(), wq.cpu(), sw.cpu(), b, x0=x0, xl=xl, emit_mx=K)
+    _close(y, yr, 2e-2, 2e-2, "cross y")
+    assert q.shape == (M, K) and sq.shape == (M, K // 32)
+    assert (q[:, N:].view(torch.uint8) == 0).all(), "K padding of the MX output not zero"
+    assert (sq[:, N // 32:] == 127).all()
+    # the scale is the block's own exponent (same fp32 values up to accumulation order)
+    same = (sq.cpu() == sqr).float().mean().item()
+    assert same > 0.99, f"only {same:.4f} of block scales match"
+    # dequantised values: within one e4m3 step of the fp32 result, per block
+    deq = ops.dequant_mx_fp8(q.cpu(), sq.cpu())[:, :N]
+    yf = yr.float()
+    blk_amax = yf.abs().view(M, N // 32, 32).amax(dim=2).repeat_interleave(32, dim=1)
+    assert ((deq - yf).abs() <= blk_amax / 16 + 2e-2 * yf.abs() + 1e-3).all()
+
+
+def test_dcn_v2_fp8_mx_chain_matches_row_requant(cuda, monkeypatch):
+    base = ModelConfig(family="dcn_v2", vocab_size=20000, embed_dim=32, mlp_dims=(256, 128), num_cross_layers=3,
+                       gemm_dtype="fp8")
+    m = build_model(base, "cpu").to(cuda)
+    assert m.mx_chain
+    ids = torch.randint(0, 10**9, (512, 43), device=cuda)
+    wts = torch.rand(512, 43, device=cuda)
+    a = m(ids, wts)
+    m.mx_chain = False
+    b = m(ids, wts)
+    assert (a - b).abs().max().item() < 0.02
+
+
 def test_cross_v2_epilogue(cuda):
     M, d = 130, 256
     x0 = torch.randn(M, d).to(torch.bfloat16)
