@@ -10,10 +10,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef long i64x1;
 
-constexpr int N = 4096;
+constexpr int N = 65536;  // ~4 ms per launch: long enough for the clock to settle under load
+
+__device__ __forceinline__ unsigned hash32(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
 
 template <int KIND>
-__global__ void __launch_bounds__(256) loop(float* out, long long* cyc, int scale) {
+__global__ void __launch_bounds__(256) loop(float* out, long long* cyc, int scale, int rnd) {
   f32x4 c0{0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
   const int l = threadIdx.x;
   bf16x8 a, b;
@@ -24,6 +33,17 @@ __global__ void __launch_bounds__(256) loop(float* out, long long* cyc, int scal
     b[i] = (__bf16)(0.002f * (l - i));
     x[i] = 0x38383838 + l + i;
     y[i] = 0x30303030 + l - i;
+    if (rnd) {  // random operands: every mantissa bit toggles (the DVFS-relevant case)
+      const unsigned h0 = hash32(blockIdx.x * 4096u + l * 16u + i), h1 = hash32(h0 + 0x9e3779b9u);
+      a[i] = (__bf16)((int(h0 & 0xffff) - 32768) * (1.f / 32768.f));
+      b[i] = (__bf16)((int(h1 & 0xffff) - 32768) * (1.f / 32768.f));
+      x[i] = int(h0 & 0x77777777u);  // e4m3 bytes without NaN patterns
+      y[i] = int(h1 & 0x77777777u);
+    }
+  }
+  if (rnd) {
+    fa = (long(hash32(l * 7u + 1)) << 32 | hash32(l * 7u + 2)) & 0x7777777777777777L;
+    fb = (long(hash32(l * 7u + 3)) << 32 | hash32(l * 7u + 4)) & 0x7777777777777777L;
   }
   __syncthreads();
   const long long t0 = clock64();
@@ -57,16 +77,17 @@ int main() {
   hipMalloc(&cyc, 256 * sizeof(long long));
   const char* names[3] = {"bf16 16x16x32", "fp8 16x16x32", "MX-fp8 16x16x128 (scaled)"};
   const double flop[3] = {2.0 * 16 * 16 * 32, 2.0 * 16 * 16 * 32, 2.0 * 16 * 16 * 128};
+  for (int rnd = 0; rnd < 2; ++rnd)
   for (int k = 0; k < 3; ++k) {
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < 4; ++rep) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
       hipEventRecord(e0);
       // 256 blocks x 256 threads = one wave per SIMD on every CU
-      if (k == 0) hipLaunchKernelGGL(loop<0>, dim3(256), dim3(256), 0, 0, out, cyc, 127);
-      if (k == 1) hipLaunchKernelGGL(loop<1>, dim3(256), dim3(256), 0, 0, out, cyc, 127);
-      if (k == 2) hipLaunchKernelGGL(loop<2>, dim3(256), dim3(256), 0, 0, out, cyc, 127);
+      if (k == 0) hipLaunchKernelGGL(loop<0>, dim3(256), dim3(256), 0, 0, out, cyc, 127, rnd);
+      if (k == 1) hipLaunchKernelGGL(loop<1>, dim3(256), dim3(256), 0, 0, out, cyc, 127, rnd);
+      if (k == 2) hipLaunchKernelGGL(loop<2>, dim3(256), dim3(256), 0, 0, out, cyc, 127, rnd);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
@@ -78,9 +99,9 @@ int main() {
       avg /= 256;
       const double per = avg / (4.0 * N);
       const double tf = flop[k] * 4.0 * N * 1024 / (ms * 1e-3) / 1e12;  // 1024 waves
-      if (rep == 1)
-        printf("{\"mfma\": \"%s\", \"cycles_per_mfma\": %.2f, \"wall_ms\": %.3f, \"tflops\": %.1f}\n", names[k], per, ms,
-               tf);
+      if (rep == 3)
+        printf("{\"mfma\": \"%s\", \"operands\": \"%s\", \"cycles_per_mfma\": %.2f, \"wall_ms\": %.3f, \"tflops\": %.1f}\n",
+               names[k], rnd ? "random" : "structured", per, ms, tf);
     }
   }
   return 0;

@@ -1082,65 +1082,34 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
   }
   }
   if (variant == 0 && glds_ok) {
-    // Measured on MI355X (bench/microbench.py --gemm-variants, interleaved):
-    //  * M <= 1024 (one request's candidates): 64x64 tiles, 4-deep LDS ring
-    //  * >= 256 tiles of 256x256: the 256x256 8-wave tile (best at M = 16K)
-    //  * >= 512 tiles of 128x128: 128x128 2-stage LDS-DMA, 2 blocks/CU
-    //  * otherwise (narrow N, e.g. the 512/256-wide MLP layers): 64x64 LDS-DMA
-    //  * >= 256 whole 256x256 tiles: the 8-phase kernel (16384x1024x2752: 81.8 us
-    //    vs 87.2 for 8-wave 128x128); a ragged last column panel (N = 2752)
-    //    or fewer tiles than CUs loses to 128x128
-    //  * >= 512 tiles of 128x128: 8 waves per block (2 per SIMD): 46.1 us vs
-    //    48.9 for 4 waves at 8192x1024x2752
+    // The five tile variants kept (round-1/2 interleaved A/B sweeps, bench/
+    // microbench.py --variants; 11 other tilings measured slower everywhere were
+    // removed):
+    //  *  8: M <= 1024 (one request's candidates): 64x64, 4-deep LDS ring
+    //  * 17: >= 256 whole 256x256 tiles: the 8-phase kernel (16384x1024x2752:
+    //        81.8 us vs 87.2 for 8-wave 128x128); a ragged last column panel
+    //        (N = 2752) or fewer tiles than CUs loses to 14
+    //  * 14: >= 512 tiles of 128x128: 8 waves per block (2 per SIMD), 2 blocks/CU
+    //        (46.1 us vs 48.9 for 4 waves at 8192x1024x2752)
+    //  * 10: >= 512 tiles of 128x64 (8192 x 512: 15.5 us vs 16.9 for 64x64)
+    //  *  4: otherwise (narrow N): 64x64 LDS-DMA
+    // K not a multiple of one 128-byte K tile: the register-staged gemm_kernel.
     if (M <= 1024) variant = 8;
     else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 17;
     else if (blocks(128, 128) >= 512) variant = 14;
     else if (blocks(128, 64) >= 512) variant = 10;  // 8192 x 512: 15.5 us vs 16.9 (64x64)
     else variant = 4;
   }
-  if (variant == 2 && glds_ok) {
-    launch_glds<128, 128, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 3 && glds_ok) {
-    launch_glds<256, 128, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
   if (variant == 4 && glds_ok) {
     launch_glds<64, 64, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 5 && glds_ok) {
-    launch_pipe<256, 128, 4, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 6 && glds_ok) {
-    launch_pipe<128, 128, 2, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 7 && glds_ok) {
-    launch_pipe<128, 128, 2, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   if (variant == 8 && glds_ok) {
     launch_pipe<64, 64, 2, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
-  if (variant == 9 && glds_ok) {
-    launch_pipe<256, 256, 2, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  // narrow-N tiles (the 512- and 256-wide MLP layers)
   if (variant == 10 && glds_ok) {
     launch_glds<128, 64, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 11 && glds_ok) {
-    launch_glds<64, 128, 2, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 12 && glds_ok) {
-    launch_glds<128, 64, 4, 1, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   // 256x256 8-phase (staggered wave groups, counted vmcnt)
@@ -1148,21 +1117,8 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     launch_8ph<FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
-  // 8-wave 128x128 tiles (2 waves per SIMD inside one block)
   if (variant == 14 && glds_ok) {
     launch_glds<128, 128, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 15 && glds_ok) {
-    launch_glds<128, 128, 4, 2, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 16 && glds_ok) {
-    launch_glds<128, 256, 2, 4, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
-    return;
-  }
-  if (variant == 13 && glds_ok) {
-    launch_pipe<128, 64, 2, 2, 3, FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   if (blocks(128, 128) >= 256)

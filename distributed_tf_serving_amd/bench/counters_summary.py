@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 counter passes (scripts/gpu_counters.sh) per kernel.
+"""Summarise rocprofv3 counter passes (scripts/gpu_study.sh counters) per kernel.
 
 Reads every ``*counter_collection.csv`` under a directory (one rocprofv3 run
 per counter pass), averages each counter per dispatch of each kernel, and

@@ -6,7 +6,7 @@
 Builds the bench preset of the model (random-init weights), captures the
 forward at ``rows`` candidates (Zipf ids over 2^40, uniform weights) in a HIP
 graph and replays it ``iters`` times: every kernel of a serving step at its
-serving shape, nothing else (scripts/gpu_counters.sh runs one counter pass per
+serving shape, nothing else (scripts/gpu_study.sh counters runs one counter pass per
 invocation).
 """
 from __future__ import annotations

@@ -57,7 +57,7 @@ def bench_gemm(M, N, K, act="relu", dev="cuda"):
     return out
 
 
-def bench_gemm_variants(M, N, K, dev="cuda", variants=(0, 2, 3, 4, 5, 6, 7, 8, 9)):
+def bench_gemm_variants(M, N, K, dev="cuda", variants=(0, 4, 8, 10, 14, 17)):
     """Interleaved A/B of the GEMM kernel variants in one process (rule 24)."""
     x = torch.randn(M, K, device=dev).to(torch.bfloat16)
     W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
@@ -153,7 +153,7 @@ def main():
         return
     if a.gemm_variants:
         narrow = (0, 10, 14, 17)
-        wide = (0, 2, 9, 14, 17)
+        wide = (0, 4, 14, 17)
         for s, v in [((8192, 512, 1024), narrow), ((16384, 512, 1024), narrow), ((8192, 256, 512), narrow),
                      ((8192, 1024, 2752), wide), ((16384, 1024, 2752), wide), ((8192, 2752, 2752), wide)]:
             print(json.dumps(bench_gemm_variants(*s, variants=v)), flush=True)

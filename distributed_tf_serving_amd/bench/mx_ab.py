@@ -25,7 +25,8 @@ def _time(fn, iters=50):
 
 
 def main():
-    M, N = 16384, 2752
+    import sys
+    M, N = (int(sys.argv[1]) if len(sys.argv) > 1 else 16384), 2752
     K = 2816
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -52,6 +53,8 @@ def main():
     forms["row_in_mx_out"] = lambda: h.gemm(qr, wq, b, 3, x0, xl, False, sr, sw, None, 0, None, q_out, sq_out)
     forms["mx_in_mx_out"] = lambda: h.gemm(qm, wq, b, 3, x0, xl, False, None, sw, None, 0, sm, q_out, sq_out)
     forms["quant_rows"] = lambda: ops.quant_rows_fp8(xl, ops.FP8_K_PAD)
+    for v in (4, 10, 14, 17):
+        forms[f"row_scaled_variant{v}"] = (lambda v=v: h.gemm(qr, wq, b, 3, x0, xl, False, sr, sw, None, v))
     for name, fn in forms.items():
         us = _time(fn)
         print(json.dumps({"form": name, "us": round(us, 2), "pflops": round(flops / us / 1e9, 3)}), flush=True)

@@ -193,8 +193,13 @@ class DCNv2(CTRModel):
         self.head_wd = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
                                     requires_grad=False)
         self.head_b = 0.0
-        # MX-fp8 cross chain (DTFS_MX_CHAIN=0: per-row re-quantisation, for A/B)
-        self.mx_chain = os.environ.get("DTFS_MX_CHAIN", "1") != "0"
+        # MX-fp8 cross chain (each cross epilogue emits the next layer's e4m3 +
+        # E8M0 block-scaled operand) vs per-row re-quantisation between layers.
+        # Opt-in (DTFS_MX_CHAIN=1): interleaved A/B on one MI355X, bench.py
+        # --model dcn_v2: 0.973 ms/step chained vs 0.914 re-quantised
+        # (profiles/dcn_v2_mx_chain.md) - the 22 us quant pass it removes costs
+        # less than the block-scale epilogue + MX operand path it adds.
+        self.mx_chain = os.environ.get("DTFS_MX_CHAIN", "0") == "1"
 
     def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None, emit_mx: int = 0):
         """One cross layer. fp8: ``xq`` = (q, row scales | None, MX block scales

@@ -40,6 +40,7 @@ def test_dcn_v2_mx_chain_close_to_row_requant():
     cfg = ModelConfig(family="dcn_v2", vocab_size=2000, embed_dim=32, mlp_dims=(64,), num_cross_layers=3,
                       gemm_dtype="fp8")
     m = build_model(cfg, "cpu")
+    m.mx_chain = True
     ids = torch.randint(0, 10**9, (64, 43))
     w = torch.rand(64, 43)
     a = m(ids, w)
