@@ -49,7 +49,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((ch
 __device__ __forceinline__ i32x8 mx_frag(const uint8_t* tile, int row, int fq) {
   const i32x4 lo = *reinterpret_cast<const i32x4*>(tile + swz(row, fq));
   const i32x4 hi = *reinterpret_cast<const i32x4*>(tile + swz(row, fq + 4));
-  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 __device__ __forceinline__ f32x4 mx_mfma(const i32x8& a, const i32x8& b, const f32x4& c) {
@@ -70,43 +70,70 @@ __device__ __forceinline__ f32x4 mx_mfma_sb(const i32x8& a, const i32x8& b, cons
 // reads bias / scales / x0 / xl and writes C as 8- or 16-byte vectors per lane
 // instead of 2- or 4-byte scalars (the DCN-v2 cross epilogue touches three
 // [M, N] bf16 tensors).
-template <bool FP8, int TM, int TN, typename OutT>
+// GEMM epilogue: scales, bias, activation / DCN-v2 cross, bf16 or fp32 store.
+// Written so that the 32-tile unrolled 8-phase epilogue stays small and the
+// accumulators stay in registers:
+//  * one code path for every activation, selected by wave-uniform values
+//    (relu = max with 0 vs -inf; sigmoid / cross = uniform branches). A
+//    runtime switch INSIDE the unrolled tile loops made the 8-phase kernel's
+//    epilogue ~15k straight-line instructions (instruction-cache bound, 14-19
+//    us per block, bench_native/g8ph_stamps.hip); a switch around per-activation
+//    copies spilled the accumulators to scratch (528 B/lane).
+//  * every operand load (bias, scales, x0, xl) is issued ahead of its use
+//    (clamped in-bounds addresses; only the stores are predicated), not one
+//    load -> use -> store latency per tile.
+template <bool FP8, bool RAGGED = true, int TM, int TN, typename OutT>
 __device__ __forceinline__ void store_acc_t(const f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq, int M, int N,
                                             const float* __restrict__ bias, const float* __restrict__ sa,
                                             const float* __restrict__ sw, OutT* __restrict__ C, int64_t ldc,
                                             const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx,
                                             int epi) {
   const int e = epi & 15;
-  const bool vec = ((N | int(ldc) | int(ldx)) & 3) == 0;
+  const bool cross = e == EPI_CROSS, sig = e == EPI_SIGMOID;
+  const float lo = e == EPI_RELU ? 0.f : -__builtin_huge_valf();
+  if (!RAGGED || ((N | int(ldc) | int(ldx)) & 3) == 0) {  // N % 4 == 0: a lane's 4 columns exist together
+    // column-tile outer: per j one bias / scale vector, then every row tile's
+    // operand loads are issued before the first use (few live registers)
+    float sam[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = mb + i * 16 + fr;
-    if (m >= M) continue;
-    const float sam = (FP8 && sa) ? sa[m] : 1.f;
+    for (int i = 0; i < TM; ++i) sam[i] = (FP8 && sa) ? sa[min(mb + i * 16 + fr, M - 1)] : 1.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = nb + j * 16 + fq * 4;
-      if (n >= N) continue;
-      float v[4];
-      if (vec) {  // N % 4 == 0 and n % 4 == 0: all four columns exist
-        const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
-        if (FP8 && sw) s4 = *reinterpret_cast<const f32x4*>(sw + n);
+      const int nc = min(n, N - 4);
+      const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
+      if constexpr (FP8) {
+        if (sw) s4 = *reinterpret_cast<const f32x4*>(sw + nc);
+      }
+      bf16x4 x0[TM], xl[TM];
+      if (cross) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int64_t mc = min(mb + i * 16 + fr, M - 1);
+          x0[i] = *reinterpret_cast<const bf16x4*>(X0 + mc * ldx + nc);
+          xl[i] = *reinterpret_cast<const bf16x4*>(XL + mc * ldx + nc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + fr;
+        float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float x = acc[i][j][r];
-          if (FP8) x *= s4[r] * sam;
-          x += b4[r];
-          if (e == EPI_RELU) x = fmaxf(x, 0.f);
-          else if (e == EPI_SIGMOID) x = sigmoidf(x);
-          v[r] = x;
+          if constexpr (FP8) x *= s4[r] * sam[i];
+          v[r] = fmaxf(x + b4[r], lo);
         }
-        if (e == EPI_CROSS) {
-          const bf16x4 x0 = *reinterpret_cast<const bf16x4*>(X0 + int64_t(m) * ldx + n);
-          const bf16x4 xl = *reinterpret_cast<const bf16x4*>(XL + int64_t(m) * ldx + n);
+        if (sig) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = bf2f(x0[r]) * v[r] + bf2f(xl[r]);
+          for (int r = 0; r < 4; ++r) v[r] = sigmoidf(v[r]);
         }
+        if (cross) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = bf2f(x0[i][r]) * v[r] + bf2f(xl[i][r]);
+        }
+        if (m >= M || n >= N) continue;
         if constexpr (sizeof(OutT) == 2) {
           bf16x4 o;
 #pragma unroll
@@ -115,20 +142,32 @@ __device__ __forceinline__ void store_acc_t(const f32x4 (&acc)[TM][TN], int mb, 
         } else {
           *reinterpret_cast<f32x4*>(C + int64_t(m) * ldc + n) = f32x4{v[0], v[1], v[2], v[3]};
         }
-      } else {
+      }
+    }
+    return;
+  }
+  // ragged N (not a multiple of 4; no serving shape; only the register-staged
+  // fallback kernel instantiates it): per element
+  if constexpr (!RAGGED) return;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nn = n + r;
-          if (nn >= N) break;
-          float x = acc[i][j][r];
-          if (FP8) x *= (sw ? sw[nn] : 1.f) * sam;
-          x += bias ? bias[nn] : 0.f;
-          if (e == EPI_RELU) x = fmaxf(x, 0.f);
-          else if (e == EPI_SIGMOID) x = sigmoidf(x);
-          else if (e == EPI_CROSS) x = bf2f(X0[int64_t(m) * ldx + nn]) * x + bf2f(XL[int64_t(m) * ldx + nn]);
-          if constexpr (sizeof(OutT) == 2) C[int64_t(m) * ldc + nn] = f2bf(x);
-          else C[int64_t(m) * ldc + nn] = x;
-        }
+  for (int i = 0; i < TM; ++i) {
+    const int m = mb + i * 16 + fr;
+    if (m >= M) continue;
+    const float sam = (FP8 && sa) ? sa[m] : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = nb + j * 16 + fq * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nn = n + r;
+        if (nn >= N) break;
+        float x = acc[i][j][r];
+        if (FP8) x *= (sw ? sw[nn] : 1.f) * sam;
+        x = fmaxf(x + (bias ? bias[nn] : 0.f), lo);
+        if (sig) x = sigmoidf(x);
+        if (cross) x = bf2f(X0[int64_t(m) * ldx + nn]) * x + bf2f(XL[int64_t(m) * ldx + nn]);
+        if constexpr (sizeof(OutT) == 2) C[int64_t(m) * ldc + nn] = f2bf(x);
+        else C[int64_t(m) * ldc + nn] = x;
       }
     }
   }
@@ -517,7 +556,7 @@ __device__ __forceinline__ void gemm_glds_body(
     store_cross_mx(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, mx);
     return;
   }
-  store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  store_acc_t<FP8, false>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
 #define DTFS_GLDS_ARGS                                                                                              \
@@ -698,6 +737,24 @@ __global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restric
 //   Aq0: s=4u-6 r=4u   Bq1: s=4u-5 r=4u+1   Aq1: s=4u-4 r=4u+2   Bq0: s=4u-3 r=4u
 // all retired by the wait at phase 4u-1 (<= r-1); restaged >= 2 phases after
 // their last reads (Aq0 p0, Bq1 p1, Aq1 p2, Bq0 p3 of tile u-2 / u-1).
+// Diagnostic build only (bench_native/g8ph_stamps.hip defines it): lane 0 of
+// each wave records s_memrealtime (100 MHz) at kernel entry, after the
+// prologue, after the main loop and after the epilogue, into a buffer no
+// other code reads. Never defined in the extension build.
+#ifdef DTFS_8PH_STAMPS
+__device__ unsigned long long g_8ph_stamps[4096][8][4];
+#define DTFS_STAMP(k)                                                                        \
+  do {                                                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                                      \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_8ph_stamps[blockIdx.x][threadIdx.x >> 6][k] = t_; \
+  } while (0)
+#else
+#define DTFS_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 template <bool FP8, typename OutT>
 __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
@@ -707,6 +764,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   constexpr int EB = FP8 ? 1 : 2;
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+  DTFS_STAMP(0);
 
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -776,6 +834,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
   asm volatile("" ::: "memory");
+  DTFS_STAMP(1);
 
   // fragments (bf16: [kk][tile] 8 x bf16, fp8: [tile] 32 x e4m3); both B
   // column halves stay in registers for the whole K tile (no B re-read)
@@ -884,8 +943,10 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     barrier();
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
+  DTFS_STAMP(2);
 
-  store_acc_t<FP8>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  store_acc_t<FP8, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  DTFS_STAMP(3);
 }
 
 template <bool FP8, typename OutT>
@@ -1033,7 +1094,7 @@ __global__ void __launch_bounds__(WM_* WN_ * 64) gemm_pipe_kernel(
     }
   }
 
-  store_acc_t<FP8>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  store_acc_t<FP8, false>(acc, m0 + wm * WTM, n0 + wn * WTN, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
 }
 
 template <int BM, int BN, int WM_, int WN_, int STAGES, bool FP8, typename OutT>
@@ -1064,7 +1125,9 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
                      int K, int epi, hipStream_t st, int variant, const MxIO& mx) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int EB = FP8 ? 1 : 2;
-  const bool glds_ok = (K * EB) % 128 == 0;
+  // the LDS-DMA / 8-phase kernels need whole 128-byte K tiles and N % 4 == 0
+  // (their epilogue stores 4 columns per lane; ragged N -> register-staged)
+  const bool glds_ok = (K * EB) % 128 == 0 && N % 4 == 0;
   if constexpr (FP8) {
   if (mx.sab || mx.q) {
     // block-scaled activations in / out: the LDS-DMA kernels (32-column-aligned
@@ -1168,7 +1231,7 @@ hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, c
   if (M == 0 || N == 0) return hipSuccess;
   if ((fp8 ? K % 16 : K % 8) != 0) return hipErrorInvalidValue;  // 16-byte row chunks
   const MxIO mx = mxp ? *mxp : MxIO();
-  if ((mx.sab || mx.q) && (!fp8 || K % 128 != 0)) return hipErrorInvalidValue;
+  if ((mx.sab || mx.q) && (!fp8 || K % 128 != 0 || N % 4 != 0)) return hipErrorInvalidValue;
   if (mx.sab && (K / 32 > kern::kMxMaxKBlocks || mx.ldsab % 4 != 0 || reinterpret_cast<uintptr_t>(mx.sab) % 4 != 0))
     return hipErrorInvalidValue;
   if (mx.q && ((epi & 15) != EPI_CROSS || !mx.sq || N % 32 != 0 || mx.nq < N || mx.nq % 32 != 0))
