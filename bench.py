@@ -88,9 +88,10 @@ def parse_args():
     ap.add_argument("--request-rows", type=int, default=512, help="candidates per client request (config batch)")
     ap.add_argument("--requests-per-gpu", type=int, default=32,
                     help="requests per GPU batch (32 x 512 = 16384 rows = the preset's max batch)")
-    ap.add_argument("--mode", default="alltoall", choices=["alltoall", "scatter", "local"],
-                    help="N > 1: alltoall = every request fanned out over all GPUs (config 3); local = one "
-                         "independent replica per GPU; scatter = rank 0 is the only front door")
+    ap.add_argument("--mode", default=None, choices=["alltoall", "scatter", "local"],
+                    help="N > 1: alltoall = every request fanned out over all GPUs (config 3, default); local = "
+                         "one independent replica per GPU (default for dlrm: its tables are sharded instead and "
+                         "every step exchanges embeddings); scatter = rank 0 is the only front door")
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")
     ap.add_argument("--decode-threads", type=int, default=4,
@@ -100,6 +101,8 @@ def parse_args():
     ap.add_argument("--gemm-dtype", default=None, choices=["bf16", "fp8"],
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
+    ap.add_argument("--shard-tables", action="store_true",
+                    help="dlrm: shard the tables even on one GPU (exercises the embedding-exchange step program)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight)")
     ap.add_argument("--batch-timeout-us", type=int, default=200)
@@ -141,9 +144,14 @@ def build(a, ctx):
                       file=sys.stderr)
             rows = fit
         cfg.table_rows = rows
-    model = build_parallel_model(cfg, dev, ctx)
+    model = build_parallel_model(cfg, dev, ctx, shard_tables="on" if a.shard_tables else "auto")
     F = cfg.num_fields
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
+    sharded = getattr(model, "has_collectives", False) or (a.model == "dlrm" and a.shard_tables)
+    if a.mode is None:
+        a.mode = "local" if a.model == "dlrm" else "alltoall"
+    if sharded and a.mode != "local":
+        raise SystemExit("dlrm with sharded tables runs --mode local (the embedding exchange is the fan-out)")
     mode = a.mode if world > 1 else ("alltoall" if a.force_fanout else "local")
     ex = ShardExecutor(model, PackedLayout(F), [B], dev, use_graphs=not a.no_graphs, slots=a.slots)
     rows_in_max = B * (world if mode == "scatter" else 1)
@@ -151,7 +159,11 @@ def build(a, ctx):
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
                        native_fanout=not a.no_native_fanout)
     eng.prepare(B)
-    if eng.mode != "local":
+    if eng.program_active:
+        # one synthetic step of the native step program vs the eager forward (collective)
+        if not eng.self_check(B, seed=rank):
+            raise SystemExit(f"rank {rank}: the step program's scores differ from the eager forward")
+    elif eng.mode != "local":
         # one synthetic step checked against a local forward on every rank; a
         # failure anywhere switches every rank to the torch.distributed path
         eng.self_check(B, seed=rank)
@@ -202,7 +214,7 @@ def run_live(a, ctx, cfg, model, eng, B):
     F = cfg.num_fields
     R = a.requests_per_gpu
     pool, n_req = request_pool(a, ctx, eng, B, F)
-    lockstep = eng.mode != "local"
+    lockstep = eng.lockstep
     conc = (a.slots + 2) * max(1, n_req)
     # lockstep (fan-out): every rank launches exactly this many steps, empty
     # ones included, so the collectives of the last steps always pair up
@@ -384,7 +396,8 @@ def main():
             par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
                    + (", native C++ step" if eng.native_fanout_active else ", torch.distributed") + ")")
         if hasattr(model, "plan"):
-            par += f" + embedding-mp{world} ({len(model.plan.row_wise())} row-wise tables, all-to-all)"
+            par += (f" + embedding-mp{model.plan.world} ({len(model.plan.row_wise())} row-wise tables, all-to-all; "
+                    + ("native two-lane step program" if eng.program_active else "eager torch.distributed") + ")")
         out = {
             "metric": "CTR scores/sec (whole node)",
             "value": round(value, 1),

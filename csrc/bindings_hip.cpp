@@ -350,13 +350,30 @@ std::vector<torch::Tensor> cross_v1(torch::Tensor x0, torch::Tensor w, torch::Te
 }
 
 // ---------------------------------------------------------------- K5
-torch::Tensor dot_interaction(torch::Tensor dense, torch::Tensor emb, int64_t out_cols) {
+torch::Tensor dot_interaction(torch::Tensor dense, torch::Tensor emb, int64_t out_cols,
+                              c10::optional<torch::Tensor> emb_off, c10::optional<torch::Tensor> emb_stride) {
   check_dev(dense, "dense");
   check_dev(emb, "emb");
   TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && emb.scalar_type() == torch::kBFloat16, "bf16 inputs");
   TORCH_CHECK(dense.dim() == 2 && dense.size(1) == 64, "dense must be [B, 64]");
-  TORCH_CHECK(emb.dim() == 3 && emb.size(0) == dense.size(0) && emb.size(2) == 64, "emb must be [B, T, 64]");
-  const int64_t B = dense.size(0), T = emb.size(1);
+  const int64_t B = dense.size(0);
+  int64_t T;
+  if (emb_off.has_value() || emb_stride.has_value()) {
+    // table map: emb is a flat [N, 64] buffer; table t of row b is row off[t] + b * stride[t]
+    TORCH_CHECK(emb_off.has_value() && emb_stride.has_value(), "emb_off and emb_stride go together");
+    TORCH_CHECK(emb.dim() == 2 && emb.size(1) == 64, "mapped emb must be a flat [N, 64] buffer");
+    for (auto* o : {&emb_off, &emb_stride}) {
+      check_dev(**o, "table map");
+      TORCH_CHECK((*o)->scalar_type() == torch::kInt64 && (*o)->dim() == 1, "table map entries are int64 [T]");
+    }
+    T = emb_off->numel();
+    TORCH_CHECK(emb_stride->numel() == T, "emb_off and emb_stride must have T entries");
+    // the kernel clamps every mapped row into [0, N): no host sync here, so
+    // this call is capturable into a step graph
+  } else {
+    TORCH_CHECK(emb.dim() == 3 && emb.size(0) == B && emb.size(2) == 64, "emb must be [B, T, 64]");
+    T = emb.size(1);
+  }
   TORCH_CHECK(T + 1 <= 32, "dot interaction kernel handles T + 1 <= 32 vectors");
   const int64_t used = 64 + (T + 1) * T / 2;
   if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
@@ -364,8 +381,43 @@ torch::Tensor dot_interaction(torch::Tensor dense, torch::Tensor emb, int64_t ou
   c10::DeviceGuard g(dense.device());
   auto out = torch::empty({B, out_cols}, dense.options());
   check_hip(dtfs::launch_dot_interaction(dense.data_ptr(), 64, emb.data_ptr(), int(T), int(B), out.data_ptr(),
-                                         out_cols, int(out_cols), cur_stream(dense)),
+                                         out_cols, int(out_cols), cur_stream(dense),
+                                         emb_off ? emb_off->data_ptr<int64_t>() : nullptr,
+                                         emb_stride ? emb_stride->data_ptr<int64_t>() : nullptr, emb.size(0)),
             "dot_interaction");
+  return out;
+}
+
+// ---------------------------------------------------------------- K1b routing
+torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tensor col, torch::Tensor mod,
+                          torch::Tensor off, c10::optional<torch::Tensor> out_opt) {
+  TORCH_CHECK(ids.is_cuda() && ids.dim() == 2 && ids.stride(1) == 1 && ids.stride(0) >= ids.size(1),
+              "ids must be a GPU [B, F] row view with contiguous rows");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32, "ids must be int32/int64");
+  TORCH_CHECK(W >= 1 && tm >= 1, "W, tm >= 1");
+  check_dev(col, "col");
+  check_dev(mod, "mod");
+  check_dev(off, "off");
+  TORCH_CHECK(col.scalar_type() == torch::kInt32 && col.numel() == W * tm, "col must be int32 [W * tm]");
+  TORCH_CHECK(mod.scalar_type() == torch::kInt64 && mod.numel() == W * tm, "mod must be int64 [W * tm]");
+  TORCH_CHECK(off.scalar_type() == torch::kInt64 && off.numel() == W * tm, "off must be int64 [W * tm]");
+  check_same_dev(ids, col, "col");
+  // route columns are clamped into [0, F) by the kernel (capturable: no sync)
+  const int64_t B = ids.size(0), F = ids.size(1);
+  c10::DeviceGuard g(ids.device());
+  torch::Tensor out;
+  if (out_opt) {
+    check_dev(*out_opt, "out");
+    TORCH_CHECK(out_opt->scalar_type() == torch::kInt32 && out_opt->numel() == W * B * tm, "out must be int32 [W, B, tm]");
+    check_same_dev(ids, *out_opt, "out");
+    out = *out_opt;
+  } else {
+    out = torch::empty({W, B, tm}, ids.options().dtype(torch::kInt32));
+  }
+  check_hip(dtfs::launch_shard_route(ids.data_ptr(), ids.scalar_type() == torch::kInt64, ids.stride(0), int(B),
+                                     int(F), int(W), int(tm), col.data_ptr<int32_t>(), mod.data_ptr<int64_t>(),
+                                     off.data_ptr<int64_t>(), out.data_ptr<int32_t>(), cur_stream(ids)),
+            "shard_route");
   return out;
 }
 
@@ -566,6 +618,69 @@ dtfs::runtime::FanoutStep make_fanout_step(torch::Tensor h2d_dst, uintptr_t ingr
   return s;
 }
 
+// A programmed step (StepRunner::launch_program) from its Python description:
+// {"h2d_dst": tensor, "h2d_lane": int, "ops": [dict, ...]} with op dicts
+//   {"kind": "kernels", "lane": l, "seq": KernelSequence | None, "graph_exec": int}
+//   {"kind": "alltoall" | "allgather" | "reduce_scatter", "lane": l, "comm": RcclComm, "send": t, "recv": t}
+//   {"kind": "record" | "wait", "lane": l, "event": k}
+// Message sizes come from the tensors (validated here, once).
+dtfs::runtime::StepProgram program_from(const py::dict& d, std::vector<py::object>* keep) {
+  keep->push_back(d);
+  dtfs::runtime::StepProgram p;
+  torch::Tensor dst = d["h2d_dst"].cast<torch::Tensor>();
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_dst must be a contiguous GPU tensor");
+  p.h2d_dst = dst.data_ptr();
+  p.h2d_lane = d.contains("h2d_lane") ? d["h2d_lane"].cast<int>() : 1;
+  for (auto item : d["ops"].cast<py::list>()) {
+    py::dict o = item.cast<py::dict>();
+    dtfs::runtime::ProgOp op;
+    const std::string kind = o["kind"].cast<std::string>();
+    op.lane = o.contains("lane") ? o["lane"].cast<int>() : 0;
+    if (kind == "kernels") {
+      op.kind = dtfs::runtime::ProgOp::kKernels;
+      if (o.contains("seq") && !o["seq"].is_none()) op.seq = &o["seq"].cast<dtfs::runtime::KernelSequence&>();
+      if (o.contains("graph_exec")) op.graph = reinterpret_cast<hipGraphExec_t>(o["graph_exec"].cast<uintptr_t>());
+    } else if (kind == "record" || kind == "wait") {
+      op.kind = kind == "record" ? dtfs::runtime::ProgOp::kRecord : dtfs::runtime::ProgOp::kWait;
+      op.event = o["event"].cast<int>();
+    } else {
+      auto& c = o["comm"].cast<dtfs::comm::RcclComm&>();
+      torch::Tensor send = o["send"].cast<torch::Tensor>(), recv = o["recv"].cast<torch::Tensor>();
+      TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+                  "collective buffers must be contiguous GPU tensors");
+      const size_t W = size_t(c.nranks());
+      op.comm = &c;
+      op.send = send.data_ptr();
+      op.recv = recv.data_ptr();
+      if (kind == "alltoall") {
+        TORCH_CHECK(send.nbytes() == recv.nbytes() && send.nbytes() % W == 0,
+                    "all-to-all: send and recv must match and split evenly over the ranks");
+        op.kind = dtfs::runtime::ProgOp::kAllToAll;
+        op.bytes = send.nbytes() / W;
+      } else if (kind == "allgather") {
+        TORCH_CHECK(recv.nbytes() == send.nbytes() * W, "all-gather: recv must be world x send");
+        op.kind = dtfs::runtime::ProgOp::kAllGather;
+        op.bytes = send.nbytes();
+      } else if (kind == "reduce_scatter") {
+        TORCH_CHECK(send.scalar_type() == torch::kBFloat16 && recv.scalar_type() == torch::kBFloat16,
+                    "reduce-scatter buffers must be bf16");
+        TORCH_CHECK(size_t(send.numel()) == size_t(recv.numel()) * W, "reduce-scatter: send must be world x recv");
+        op.kind = dtfs::runtime::ProgOp::kReduceScatter;
+        op.bytes = size_t(recv.numel());
+      } else {
+        TORCH_CHECK(false, "unknown program op kind ", kind);
+      }
+    }
+    p.ops.push_back(op);
+  }
+  try {
+    p.validate();
+  } catch (const std::invalid_argument& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  return p;
+}
+
 // ServingLoop + the Python objects whose memory it points into.
 struct PyServingLoop {
   std::unique_ptr<dtfs::runtime::ServingLoop> loop;
@@ -584,7 +699,12 @@ dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object
   s.h_out_len = h_out.numel();
   torch::Tensor dst = d["h2d_dst"].cast<torch::Tensor>();
   TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_dst must be a contiguous GPU tensor");
-  if (d.contains("fanout") && d["fanout"].cast<bool>()) {
+  if (d.contains("program") && !d["program"].is_none()) {
+    s.program = true;
+    s.prog = program_from(d["program"].cast<py::dict>(), keep);
+    s.h2d_cap = int64_t(dst.nbytes());
+    TORCH_CHECK(s.prog.h2d_dst == dst.data_ptr(), "program h2d_dst must be the slot's h2d_dst");
+  } else if (d.contains("fanout") && d["fanout"].cast<bool>()) {
     s.fanout = true;
     s.fan = make_fanout_step(dst, d["ingress_exec"].cast<uintptr_t>(), d["cin"].cast<dtfs::comm::RcclComm&>(),
                              d["mode"].cast<int>(), d["send"].cast<torch::Tensor>(), d["recv"].cast<torch::Tensor>(),
@@ -639,11 +759,16 @@ class GpuBackend : public dtfs::runtime::StepBackend {
     const size_t S = slots_[0].size();
     TORCH_CHECK(S >= 1 && int(S) <= runner_->slots(), "slot count must be in [1, runner slots]");
     for (const auto& v : slots_) TORCH_CHECK(v.size() == S, "every bucket needs the same number of slots");
+    auto add = [&](dtfs::comm::RcclComm* c) {
+      if (c && std::find(comms_.begin(), comms_.end(), c) == comms_.end()) comms_.push_back(c);
+    };
     for (const auto& v : slots_)
-      for (const auto& s : v)
+      for (const auto& s : v) {
         if (s.fanout)
-          for (auto* c : {s.fan.cin, s.fan.cout})
-            if (std::find(comms_.begin(), comms_.end(), c) == comms_.end()) comms_.push_back(c);
+          for (auto* c : {s.fan.cin, s.fan.cout}) add(c);
+        if (s.program)
+          for (const auto& o : s.prog.ops) add(o.comm);
+      }
   }
   int slots() const override { return int(slots_[0].size()); }
   const std::vector<int64_t>& buckets() const override { return buckets_; }
@@ -652,7 +777,10 @@ class GpuBackend : public dtfs::runtime::StepBackend {
     // the header + descriptors always travel, so an empty (lockstep) step
     // sees zero rows instead of the slot's previous batch
     const int64_t nbytes = batch.used_bytes;
-    if (s.fanout) {
+    if (s.program) {
+      if (nbytes > s.h2d_cap) throw std::runtime_error("batch larger than the device arena");
+      runner_->launch_program(slot, s.prog, arena, nbytes);
+    } else if (s.fanout) {
       dtfs::runtime::FanoutStep f = s.fan;
       f.h2d_src = arena;
       f.h2d_bytes = nbytes;
@@ -735,7 +863,10 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sq_out") = py::none());
   m.def("cross_v1", &cross_v1, py::arg("x0"), py::arg("w"), py::arg("b"), py::arg("want_x") = true,
         py::arg("head_w") = py::none());
-  m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0);
+  m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0,
+        py::arg("emb_off") = py::none(), py::arg("emb_stride") = py::none());
+  m.def("shard_route", &shard_route, py::arg("ids"), py::arg("W"), py::arg("tm"), py::arg("col"), py::arg("mod"),
+        py::arg("off"), py::arg("out") = py::none());
   m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
@@ -785,6 +916,18 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("slot"), py::arg("h2d_dst"), py::arg("h2d_src"), py::arg("h2d_bytes"), py::arg("ingress_exec"),
           py::arg("cin"), py::arg("mode"), py::arg("send"), py::arg("recv"), py::arg("forward_exec"), py::arg("cout"),
           py::arg("scores"), py::arg("back"), py::arg("h_out"), py::arg("d2h_bytes"))
+      .def(
+          "launch_program",
+          [](dtfs::runtime::StepRunner& r, int slot, py::dict program, torch::Tensor h2d_src, int64_t h2d_bytes) {
+            std::vector<py::object> keep;  // the caller keeps the program's objects alive while it runs
+            auto p = program_from(program, &keep);
+            torch::Tensor dst = program["h2d_dst"].cast<torch::Tensor>();
+            TORCH_CHECK(h2d_src.device().is_cpu() && h2d_src.is_pinned(), "h2d_src must be pinned host memory");
+            TORCH_CHECK(h2d_bytes >= 0 && h2d_bytes <= int64_t(dst.nbytes()) && h2d_bytes <= int64_t(h2d_src.nbytes()),
+                        "h2d_bytes out of range");
+            r.launch_program(slot, p, h2d_src.data_ptr(), h2d_bytes);
+          },
+          py::arg("slot"), py::arg("program"), py::arg("h2d_src"), py::arg("h2d_bytes"))
       .def("wait", &dtfs::runtime::StepRunner::wait, py::arg("slot"), py::call_guard<py::gil_scoped_release>())
       .def(
           "wait_for",

@@ -23,6 +23,7 @@ struct Api {
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
   decltype(&ncclAllToAll) AllToAll = nullptr;
   decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclReduceScatter) ReduceScatter = nullptr;
   decltype(&ncclSend) Send = nullptr;
   decltype(&ncclRecv) Recv = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -53,6 +54,7 @@ const Api& api() {
       sym(h, "ncclGetErrorString", g_api.GetErrorString);
       sym(h, "ncclAllToAll", g_api.AllToAll);
       sym(h, "ncclAllGather", g_api.AllGather);
+      sym(h, "ncclReduceScatter", g_api.ReduceScatter);
       sym(h, "ncclSend", g_api.Send);
       sym(h, "ncclRecv", g_api.Recv);
       sym(h, "ncclGroupStart", g_api.GroupStart);
@@ -140,6 +142,11 @@ void RcclComm::gather(const void* send, void* recv, size_t bytes, int root, hipS
 void RcclComm::allgather(const void* send, void* recv, size_t bytes, hipStream_t st) {
   if (aborted_) throw std::runtime_error("communicator aborted");
   check(api().AllGather(send, recv, bytes, ncclUint8, comm_, st), "ncclAllGather");
+}
+
+void RcclComm::reduce_scatter_bf16(const void* send, void* recv, size_t elems, hipStream_t st) {
+  if (aborted_) throw std::runtime_error("communicator aborted");
+  check(api().ReduceScatter(send, recv, elems, ncclBfloat16, ncclSum, comm_, st), "ncclReduceScatter");
 }
 
 std::string RcclComm::async_error() {

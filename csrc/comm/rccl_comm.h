@@ -45,6 +45,11 @@ class RcclComm {
   // recv[r] = rank r's send.
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t st);
 
+  // recv = this rank's `elems`-long slice of the element-wise bf16 sum of every
+  // rank's send (W x elems). Row-wise sharded embedding tables: exactly one
+  // rank contributes a non-zero row, so the bf16 sum is exact.
+  void reduce_scatter_bf16(const void* send, void* recv, size_t elems, hipStream_t st);
+
   // "" when healthy, else the asynchronous RCCL error (failure detection).
   std::string async_error();
   // Abort in-flight operations (a peer died / a deadline passed); the

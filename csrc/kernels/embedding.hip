@@ -352,6 +352,30 @@ __global__ void __launch_bounds__(256) bag_kernel(const bf16* __restrict__ table
   }
 }
 
+
+// ---------------------------------------------------------------- K1b routing
+// Embedding model parallelism (parallel/embedding_sharding.py): the int32 row
+// every (candidate b, owned-table slot) pair looks up on the table's owner,
+// grouped by owner so ONE all-to-all hands each rank exactly its rows:
+//   out[(s*B + b)*tm + j] = off[s*tm + j] + (ids[b*ld + col[s*tm + j]] mod mod[s*tm + j])
+// s = owner rank, j = its j-th owned table (pad slots point at row off + 0).
+template <typename IdT>
+__global__ void __launch_bounds__(256) shard_route_kernel(const IdT* __restrict__ ids, int64_t ld, int B, int F,
+                                                          int W, int tm,
+                                                          const int32_t* __restrict__ col,
+                                                          const int64_t* __restrict__ mod,
+                                                          const int64_t* __restrict__ off, int32_t* __restrict__ out) {
+  const int64_t n = int64_t(W) * B * tm;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int j = int(i % tm);
+    const int64_t sb = i / tm;
+    const int b = int(sb % B), s = int(sb / B);
+    const int slot = s * tm + j;
+    const int c = min(max(col[slot], 0), F - 1);
+    out[i] = int32_t(off[slot] + hash_row(int64_t(ids[int64_t(b) * ld + c]), mod[slot]));
+  }
+}
+
 }  // namespace kern
 
 // ---------------------------------------------------------------- launchers
@@ -367,6 +391,21 @@ hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n,
   else
     hipLaunchKernelGGL(pack_ids_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, static_cast<const int32_t*>(ids),
                        out, n, F, modulo_f, offset_f, modulo);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_route(const void* ids, bool ids64, int64_t ld, int B, int F, int W, int tm, const int32_t* col,
+                              const int64_t* mod, const int64_t* off, int32_t* out, hipStream_t st) {
+  const int64_t n = int64_t(W) * B * tm;
+  if (n == 0) return hipSuccess;
+  if (F < 1) return hipErrorInvalidValue;
+  const int blocks = int(std::min<int64_t>((n + 255) / 256, 4096));
+  if (ids64)
+    hipLaunchKernelGGL(shard_route_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, static_cast<const int64_t*>(ids),
+                       ld, B, F, W, tm, col, mod, off, out);
+  else
+    hipLaunchKernelGGL(shard_route_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, static_cast<const int32_t*>(ids),
+                       ld, B, F, W, tm, col, mod, off, out);
   return hipGetLastError();
 }
 

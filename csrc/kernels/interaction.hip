@@ -91,7 +91,9 @@ __global__ void __launch_bounds__(256) cross_v1_kernel(const bf16* __restrict__ 
 //   out[b] = [dense (D) | Z[i][j] for i > j, row-major (T+1)T/2 | zero pad]
 __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restrict__ dense, int64_t ldd,
                                                            const bf16* __restrict__ emb, int T, int B,
-                                                           bf16* __restrict__ out, int64_t ldo, int out_cols) {
+                                                           bf16* __restrict__ out, int64_t ldo, int out_cols,
+                                                           const int64_t* __restrict__ emb_off,
+                                                           const int64_t* __restrict__ emb_stride, int64_t emb_rows) {
   constexpr int D = 64;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -106,7 +108,12 @@ __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restric
     bf16x8 x = bf16x8{};
     const int k = 16 * s + 8 * h;
     if (r == 0) x = *reinterpret_cast<const bf16x8*>(dense + b * ldd + k);
-    else if (r < nv) x = *reinterpret_cast<const bf16x8*>(emb + (int64_t(b) * T + (r - 1)) * D + k);
+    else if (r < nv) {
+      // table map: the embedding all-to-all's [owner][row][slot] layout in place
+      const int64_t er = emb_off ? min(max(emb_off[r - 1] + int64_t(b) * emb_stride[r - 1], int64_t(0)), emb_rows - 1)
+                                 : int64_t(b) * T + (r - 1);
+      x = *reinterpret_cast<const bf16x8*>(emb + er * D + k);
+    }
     // f32_32x32x16_bf16 operand = 8 bf16
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, x, acc, 0, 0, 0);
   }
@@ -218,11 +225,14 @@ hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, con
 }
 
 hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* emb, int T, int B, void* out,
-                                  int64_t ldo, int out_cols, hipStream_t st) {
+                                  int64_t ldo, int out_cols, hipStream_t st, const int64_t* emb_off,
+                                  const int64_t* emb_stride, int64_t emb_rows) {
   if (B == 0) return hipSuccess;
+  if (emb_off && emb_rows < 1) return hipErrorInvalidValue;
   if (T + 1 > 32) return hipErrorInvalidValue;
+  if ((emb_off == nullptr) != (emb_stride == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dot_interact_kernel, dim3((B + 3) / 4), dim3(256), 0, st, static_cast<const bf16*>(dense), ldd,
-                     static_cast<const bf16*>(emb), T, B, static_cast<bf16*>(out), ldo, out_cols);
+                     static_cast<const bf16*>(emb), T, B, static_cast<bf16*>(out), ldo, out_cols, emb_off, emb_stride, emb_rows);
   return hipGetLastError();
 }
 

@@ -12,6 +12,12 @@ namespace dtfs {
 hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n, int F, const int64_t* modulo_f,
                            const int64_t* offset_f, int64_t modulo, hipStream_t st);
 
+// K1b routing: out[(s*B + b)*tm + j] = off[s*tm+j] + (ids[b*ld + col[s*tm+j]] mod mod[s*tm+j])
+// (int32 rows grouped by owner rank for the embedding all-to-all); col is
+// clamped into [0, F).
+hipError_t launch_shard_route(const void* ids, bool ids64, int64_t ld, int B, int F, int W, int tm, const int32_t* col,
+                              const int64_t* mod, const int64_t* off, int32_t* out, hipStream_t st);
+
 // K1: weighted gather (+ first/second-order FM). out_x bf16 [B, F*D] and/or out_fm fp32 [B].
 struct EmbedArgs {
   const void* table = nullptr;     // bf16 [V, D]
@@ -97,9 +103,13 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
                            void* out_x, int64_t ldo, const float* head_w, float* out_dot, hipStream_t st);
 
-// K5: DLRM dot interaction (T + 1 <= 32, D = 64).
+// K5: DLRM dot interaction (T + 1 <= 32, D = 64). Table t's vector of row b is
+// emb row (b*T + t), or with a table map (emb_off / emb_stride, int64 [T])
+// emb row (emb_off[t] + b*emb_stride[t]), clamped into [0, emb_rows) - the
+// layout an embedding all-to-all leaves behind, read in place.
 hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* emb, int T, int B, void* out,
-                                  int64_t ldo, int out_cols, hipStream_t st);
+                                  int64_t ldo, int out_cols, hipStream_t st, const int64_t* emb_off = nullptr,
+                                  const int64_t* emb_stride = nullptr, int64_t emb_rows = 0);
 
 // K6: y = act(x . w + bias + extra), act 0 none / 2 sigmoid.
 hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,

@@ -26,8 +26,9 @@ ServingLoop::ServingLoop(StepRunner* runner, LoopConfig cfg, std::vector<LoopSlo
   if (int(slots_.size()) < cfg_.depth + 1) throw std::invalid_argument("need slots >= depth + 1");
   if (int(slots_.size()) > runner_->slots()) throw std::invalid_argument("more loop slots than runner slots");
   for (const auto& s : slots_) {
-    if (s.fanout ? (!(s.fan.forward || s.fan.forward_seq) || !s.fan.cin || !s.fan.cout)
-                 : (!(s.graph || s.seq) || !s.h2d_dst))
+    if (s.program ? !s.prog.h2d_dst
+        : s.fanout ? (!(s.fan.forward || s.fan.forward_seq) || !s.fan.cin || !s.fan.cout)
+                   : (!(s.graph || s.seq) || !s.h2d_dst))
       throw std::invalid_argument("incomplete loop slot");
     if (!s.h_out) throw std::invalid_argument("loop slot without host scores");
   }
@@ -173,7 +174,9 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
       const int slot = int(k % S);
       const LoopSlot& s = slots_[size_t(slot)];
       const int64_t nbytes = b.n_valid > 0 ? b.used_bytes : 0;
-      if (s.fanout) {
+      if (s.program) {
+        runner_->launch_program(slot, s.prog, in.arena, nbytes);
+      } else if (s.fanout) {
         FanoutStep f = s.fan;
         f.h2d_src = in.arena;
         f.h2d_bytes = nbytes;

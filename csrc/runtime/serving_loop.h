@@ -35,6 +35,8 @@ struct LoopSlot {
   const KernelSequence* seq = nullptr;  // local, preferred: the same step as direct launches
   bool fanout = false;
   FanoutStep fan;                    // fan-out: everything but h2d_src / h2d_bytes
+  bool program = false;
+  StepProgram prog;                  // programmed step (embedding-parallel models)
   const float* h_out = nullptr;      // pinned scores of the slot
   int64_t h_out_len = 0;
 };

@@ -75,7 +75,7 @@ StepRunner::~StepRunner() {
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamSynchronize(s);
   for (hipStream_t s : extra_copy_) hipStreamSynchronize(s);
-  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_, &gate_})
+  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_, &gate_, &prog_ev_})
     for (auto e : *v) hipEventDestroy(e);
   for (hipStream_t s : {compute_, copy_, ingress_, egress_})
     if (s) hipStreamDestroy(s);
@@ -152,6 +152,86 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   if (s.d2h_bytes > 0)
     ck(hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_), "hipMemcpyAsync(D2H)");
   ck(hipEventRecord(done_[slot], egress_), "hipEventRecord(done)");
+  used_[slot] = 1;
+}
+
+void StepProgram::validate() const {
+  if (h2d_lane != 0 && h2d_lane != 1) throw std::invalid_argument("program: h2d_lane must be 0 or 1");
+  // aux-lane work (the H2D landing there counts) must be covered by an aux
+  // record that the compute lane waits for, or the step could be reported done
+  // while its exchange is still running
+  int64_t aux_ops = h2d_lane == 1 ? 1 : 0, joined = 0;
+  bool recorded[kProgEvents] = {};
+  int64_t covers[kProgEvents] = {};  // aux ops before the event's record (aux lane records only)
+  for (const ProgOp& o : ops) {
+    if (o.lane != 0 && o.lane != 1) throw std::invalid_argument("program: lane must be 0 or 1");
+    switch (o.kind) {
+      case ProgOp::kKernels:
+        if (!o.seq && !o.graph) throw std::invalid_argument("program: kernels op without a sequence or graph");
+        break;
+      case ProgOp::kAllToAll:
+      case ProgOp::kAllGather:
+      case ProgOp::kReduceScatter:
+        if (!o.comm || !o.send || !o.recv) throw std::invalid_argument("program: collective without buffers");
+        break;
+      case ProgOp::kRecord:
+      case ProgOp::kWait:
+        if (o.event < 0 || o.event >= kProgEvents) throw std::invalid_argument("program: event index out of range");
+        break;
+      default:
+        throw std::invalid_argument("program: bad op kind");
+    }
+    if (o.kind == ProgOp::kRecord) {
+      recorded[o.event] = true;
+      covers[o.event] = o.lane == 1 ? aux_ops : 0;
+    } else if (o.kind == ProgOp::kWait) {
+      if (!recorded[o.event]) throw std::invalid_argument("program: event waited before it is recorded");
+      if (o.lane == 0) joined = std::max(joined, covers[o.event]);
+    } else if (o.lane == 1) {
+      ++aux_ops;
+    }
+  }
+  if (joined < aux_ops) throw std::invalid_argument("program: aux-lane work is not joined into the compute lane");
+}
+
+void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes) {
+  if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
+  ck(hipSetDevice(device_), "hipSetDevice");
+  ensure_fanout_streams();  // the aux lane is the ingress stream
+  if (prog_ev_.empty()) {
+    prog_ev_.resize(done_.size() * kProgEvents);
+    for (auto& e : prog_ev_) ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(program)");
+  }
+  hipStream_t lanes[2] = {compute_, ingress_};
+  // WAR on the slot's buffers + the H2D of the request bytes (one copy stream:
+  // a third hardware queue for copies would alias the aux lane's)
+  h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], false);
+  hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
+  for (const ProgOp& o : p.ops) {
+    hipStream_t st = lanes[o.lane];
+    switch (o.kind) {
+      case ProgOp::kKernels:
+        if (o.seq) o.seq->launch(st);
+        else ck(hipGraphLaunch(o.graph, st), "hipGraphLaunch(program)");
+        break;
+      case ProgOp::kAllToAll:
+        o.comm->alltoall(o.send, o.recv, o.bytes, st);
+        break;
+      case ProgOp::kAllGather:
+        o.comm->allgather(o.send, o.recv, o.bytes, st);
+        break;
+      case ProgOp::kReduceScatter:
+        o.comm->reduce_scatter_bf16(o.send, o.recv, o.bytes, st);
+        break;
+      case ProgOp::kRecord:
+        ck(hipEventRecord(ev[o.event], st), "hipEventRecord(program)");
+        break;
+      case ProgOp::kWait:
+        ck(hipStreamWaitEvent(st, ev[o.event], 0), "hipStreamWaitEvent(program)");
+        break;
+    }
+  }
+  ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
   used_[slot] = 1;
 }
 

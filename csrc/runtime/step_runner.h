@@ -54,6 +54,47 @@ struct FanoutStep {
   const KernelSequence* forward_seq = nullptr;
 };
 
+// A step as a short program over two device lanes - the compute stream and
+// an auxiliary stream - for models whose forward interleaves collectives with
+// kernels (embedding model parallelism, SURVEY §2.5 C3: ids all-to-all ->
+// owner-side gather -> embeddings all-to-all on the aux lane while the bottom
+// MLP runs on the compute lane). Ops run in list order on their lane; lanes
+// meet only through kRecord / kWait on per-slot events. The H2D lands before
+// the lane named by h2d_lane starts; the step is done when the compute lane
+// is, so every aux-lane op must be joined into the compute lane (validated).
+// All ranks enqueue the same collectives in the same order on the aux lane
+// with one communicator, so the exchange cannot cross-match between steps.
+struct ProgOp {
+  enum Kind : int {
+    kKernels = 0,        // seq (direct launches) or graph
+    kAllToAll = 1,       // comm: send -> recv, `bytes` per peer
+    kAllGather = 2,      // comm: send (`bytes`) -> recv (W x bytes)
+    kReduceScatter = 3,  // comm: bf16 sum, send (W x elems) -> recv (`bytes` = elems)
+    kRecord = 4,         // record per-slot event `event` on the lane
+    kWait = 5,           // lane waits for per-slot event `event`
+  };
+  int kind = kKernels;
+  int lane = 0;  // 0 compute, 1 aux
+  int event = 0;
+  const KernelSequence* seq = nullptr;
+  hipGraphExec_t graph = nullptr;
+  comm::RcclComm* comm = nullptr;
+  const void* send = nullptr;
+  void* recv = nullptr;
+  size_t bytes = 0;
+};
+constexpr int kProgEvents = 8;
+
+struct StepProgram {
+  void* h2d_dst = nullptr;
+  int h2d_lane = 1;
+  std::vector<ProgOp> ops;
+  // throws std::invalid_argument when an event index is out of range, an
+  // event is waited before it is recorded, or aux-lane work is never joined
+  // into the compute lane
+  void validate() const;
+};
+
 class StepRunner {
  public:
   StepRunner(int device, int slots);
@@ -70,6 +111,8 @@ class StepRunner {
                   bool skip_varint = false);
   // Enqueue one fan-out step (see FanoutStep).
   void launch_fanout(int slot, const FanoutStep& s);
+  // Enqueue one programmed step (see StepProgram).
+  void launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes);
   // Block until the slot's last step has finished (scores are on the host).
   void wait(int slot);
   // Bounded wait: false when the step has not finished within timeout_us or a
@@ -101,6 +144,7 @@ class StepRunner {
   void ensure_fanout_streams();
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
+  std::vector<hipEvent_t> prog_ev_;  // [slot * kProgEvents + k], created on first program launch
   // H2D gate (DTFS_H2D_GATE = k, default 0 = off): step k+1's H2D waits until
   // step k's first k kernels (the embedding gather) have run, so the DMA
   // overlaps the GEMMs instead of the latency-bound gather it slows ~2x

@@ -302,13 +302,25 @@ def interaction_cols(num_sparse: int, dim: int = 64) -> int:
     return (used + 7) // 8 * 8
 
 
-def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0) -> torch.Tensor:
-    """DLRM: [dense | strictly-lower-triangular entries of X X^T | zero pad], X = [dense; emb]."""
-    T = emb.shape[1]
+def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0,
+                    emb_off: Optional[torch.Tensor] = None, emb_stride: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """DLRM: [dense | strictly-lower-triangular entries of X X^T | zero pad], X = [dense; emb].
+
+    ``emb`` is [B, T, D], or with a table map (``emb_off`` / ``emb_stride``,
+    int64 [T]) a flat [N, D] buffer in which table t of row b is row
+    ``emb_off[t] + b * emb_stride[t]`` - the layout an embedding all-to-all
+    leaves behind, read in place (parallel/embedding_sharding.py)."""
+    mapped = emb_off is not None
+    T = int(emb_off.numel()) if mapped else emb.shape[1]
     if out_cols <= 0:
         out_cols = interaction_cols(T, dense.shape[1])
     if dense.is_cuda:
+        if mapped:
+            return hip().dot_interaction(dense.contiguous(), emb, int(out_cols), emb_off, emb_stride)
         return hip().dot_interaction(dense.contiguous(), emb.contiguous(), int(out_cols))
+    if mapped:
+        rows = emb_off.view(1, -1) + torch.arange(dense.shape[0]).view(-1, 1) * emb_stride.view(1, -1)
+        emb = emb[rows.clamp(0, emb.shape[0] - 1)]  # [B, T, D]
     X = torch.cat([dense.float().unsqueeze(1), emb.float()], dim=1)  # [B, T+1, D]
     Z = X @ X.transpose(1, 2)
     li, lj = torch.tril_indices(T + 1, T + 1, offset=-1)
@@ -316,6 +328,25 @@ def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0) -
     out[:, : dense.shape[1]] = dense.float()
     out[:, dense.shape[1]: dense.shape[1] + li.numel()] = Z[:, li, lj]
     return out.to(dense.dtype)
+
+
+# ------------------------------------------------------------------ K1b routing
+def shard_route(ids: torch.Tensor, W: int, tm: int, col: torch.Tensor, mod: torch.Tensor, off: torch.Tensor,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Embedding-parallel routing: int32 [W, B, tm] with
+    out[s, b, j] = off[s*tm + j] + (ids[b, col[s*tm + j]] mod mod[s*tm + j]),
+    i.e. the local row on owner rank s of its j-th table for candidate b."""
+    B = ids.shape[0]
+    if ids.is_cuda:
+        return hip().shard_route(_rows(ids), int(W), int(tm), col, mod, off, out)
+    else:
+        c = col.long().clamp(0, ids.shape[1] - 1)
+        r = (off.view(1, -1) + torch.remainder(ids.long()[:, c], mod.view(1, -1))).to(torch.int32)  # [B, W*tm]
+        r = r.view(B, W, tm).transpose(0, 1).contiguous()
+    if out is not None:
+        out.copy_(r.view(out.shape))
+        return out
+    return r
 
 
 # ------------------------------------------------------------------ K6

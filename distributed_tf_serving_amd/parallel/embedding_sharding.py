@@ -39,10 +39,11 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
-from .. import ops
+from .. import ops as ops_k
 from ..config import ModelConfig
 from ..models.ctr import DLRM
 from ..models.layers import DTYPES, hashed_uniform_rows_
+from . import step_program as sp
 from .dist import DistContext, split_rows
 
 GiB = 1 << 30
@@ -158,41 +159,33 @@ def dlrm_tables(cfg: ModelConfig) -> List[TableSpec]:
     return [TableSpec(f"t{f}", cfg.table_rows, cfg.embed_dim, eb) for f in range(cfg.num_sparse)]
 
 
-def _reduce_scatter_sum(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """out = this rank's slice (dim 0) of the sum over ranks of inp."""
-    if dist.get_backend(group) == "gloo":  # gloo has no reduce_scatter; all-reduce in fp32 and slice
-        full = inp.float()
-        dist.all_reduce(full, group=group)
-        r, n = dist.get_rank(group), out.shape[0]
-        out.copy_(full[r * n:(r + 1) * n])
-    else:
-        dist.reduce_scatter_tensor(out, inp, group=group)
-
-
-def _all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """out[r*B:(r+1)*B] = rank r's inp."""
-    if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
-    else:
-        dist.all_gather_into_tensor(out, inp, group=group)
-
-
-def _coll_dtype(t: torch.Tensor, group) -> torch.Tensor:
-    # gloo's CPU collectives: keep the wire dtype fp32 for bf16 payloads
-    return t.float() if (t.dtype == torch.bfloat16 and dist.get_backend(group) == "gloo") else t
-
-
 class ShardedEmbedding(nn.Module):
-    """This rank's shards of a set of one-hot embedding tables + the exchange.
+    """This rank's shards of a set of one-hot embedding tables + the exchange,
+    as step-program ops (parallel/step_program.py).
 
-    ``forward(sparse_ids [B, T]) -> [B, T, D]`` on every rank with the SAME B
-    (the fan-out engine hands every rank an equal slice)."""
+    ``program(ids, B, bufs)`` returns the aux-lane ops of one step for a batch
+    of B candidates whose table ids are columns ``col_base + t`` of ``ids``
+    ([B, F] int64/int32 row view); every rank runs the SAME B (the engine hands
+    every rank a full bucket). Afterwards table t of candidate b is row
+    ``map_off[t] + b * map_stride[t]`` of ``bufs["emb_all"]`` ([N, D] bf16),
+    which the DLRM interaction kernel reads in place:
+
+    * table-wise: ``shard_route`` writes each candidate's row on the owner,
+      grouped by owner ([W, B, tmax] int32, hashed on the sender so the owner
+      gathers with no modulo) -> ids all-to-all -> the owner gathers its
+      tables for every rank's candidates -> embeddings all-to-all back;
+    * row-wise: the same route with W = 1 (global table rows) -> all-gather ->
+      masked gather (rows outside this rank's range contribute zeros) ->
+      bf16 reduce-scatter (sum): exactly one rank owns each row, so it is exact.
+    Every message has a fixed shape for a given B (no count exchange), so the
+    step is capturable and replayed by the native StepRunner."""
 
     def __init__(self, plan: ShardingPlan, ctx: DistContext, seed: int, bound: float, dtype=torch.bfloat16,
-                 device="cpu", group=None):
+                 device="cpu", group=None, col_base: int = 0):
         super().__init__()
         self.plan, self.ctx, self.group = plan, ctx, group
         self.world, self.rank = plan.world, ctx.rank if plan.world > 1 else 0
+        self.col_base = int(col_base)
         dev = torch.device(device)
         T = len(plan.tables)
         self.T = T
@@ -202,118 +195,145 @@ class ShardedEmbedding(nn.Module):
         # ---- table-wise: tables owned here, and every rank's owned list
         self.tw_by_rank = [plan.table_wise(r) for r in range(self.world)]
         self.tmax = max((len(x) for x in self.tw_by_rank), default=0)
-        mine = self.tw_by_rank[self.rank]
         self.rw = plan.row_wise()
-        # local storage: [owned table-wise tables | row-wise shards], one buffer
-        rows_local, mod, off, lo, nn_ = 0, [], [], [], []
-        segs = []
-        for t in mine:
-            spec = plan.tables[t]
-            segs.append((t, 0, spec.rows, rows_local))
-            mod.append(spec.rows)
-            off.append(rows_local)
-            rows_local += spec.rows
-        # pad the owned-table list to tmax with table 0 of this rank (lookups discarded)
-        pad_mod = mod[0] if mod else 1
-        while len(mod) < self.tmax:
-            mod.append(pad_mod)
-            off.append(0)
-        rw_mod, rw_off, rw_lo, rw_n = [], [], [], []
-        for t in self.rw:
-            spec = plan.tables[t]
-            s, n = plan.placement(t).ranges[self.rank]
-            segs.append((t, s, n, rows_local))
-            rw_mod.append(spec.rows)
-            rw_off.append(rows_local)
-            rw_lo.append(s)
-            rw_n.append(n)
-            rows_local += n
-        self.rows_local = rows_local
-        self.segments = segs  # (table, global row lo, rows, local offset)
-        store = torch.empty(max(1, rows_local), self.D, dtype=dtype, device=dev)
-        for t, s, n, o in segs:
+        self.tw_tables = [t for t in range(T) if t not in self.rw]
+        # local storage per rank: [owned table-wise tables | row-wise shards], one buffer
+        def layout(r):
+            rows, offs, segs = 0, {}, []
+            for t in self.tw_by_rank[r]:
+                offs[t] = rows
+                segs.append((t, 0, plan.tables[t].rows, rows))
+                rows += plan.tables[t].rows
+            for t in self.rw:
+                s, n = plan.placement(t).ranges[r]
+                offs[t] = rows
+                segs.append((t, s, n, rows))
+                rows += n
+            return rows, offs, segs
+
+        lay = [layout(r) for r in range(self.world)]
+        self.rows_local, my_off, self.segments = lay[self.rank]  # segments: (table, global lo, rows, local offset)
+        store = torch.empty(max(1, self.rows_local), self.D, dtype=dtype, device=dev)
+        for t, s, n, o in self.segments:
             if n:
                 hashed_uniform_rows_(store[o:o + n], t, s, seed, bound)
         self.store = nn.Parameter(store, requires_grad=False)
         i64 = dict(dtype=torch.int64, device=dev)
-        self.register_buffer("tw_mod", torch.tensor(mod or [1], **i64), persistent=False)
-        self.register_buffer("tw_off", torch.tensor(off or [0], **i64), persistent=False)
-        self.register_buffer("rw_mod", torch.tensor(rw_mod or [1], **i64), persistent=False)
-        self.register_buffer("rw_off", torch.tensor(rw_off or [0], **i64), persistent=False)
-        self.register_buffer("rw_lo", torch.tensor(rw_lo or [0], **i64), persistent=False)
-        self.register_buffer("rw_n", torch.tensor(rw_n or [0], **i64), persistent=False)
-        # send-side column gather: slot (s, j) <- sparse column tw_by_rank[s][j] (pad: column 0)
-        send_cols = []
+        # table-wise route: slot (s, j) <- table tw_by_rank[s][j] (pad: column 0, row 0 of s)
+        cols, mods, offs = [], [], []
         for s in range(self.world):
-            cols = self.tw_by_rank[s] + [0] * (self.tmax - len(self.tw_by_rank[s]))
-            send_cols += cols
-        self.register_buffer("send_cols", torch.tensor(send_cols or [0], **i64), persistent=False)
-        # receive-side: output table t <- flat slot owner(t) * tmax + j
-        recv_slot = [0] * T
-        for s in range(self.world):
-            for j, t in enumerate(self.tw_by_rank[s]):
-                recv_slot[t] = s * self.tmax + j
-        self.register_buffer("recv_slot_tw", torch.tensor([recv_slot[t] for t in range(T) if t not in self.rw] or [0],
-                                                          **i64), persistent=False)
-        self.tw_tables = [t for t in range(T) if t not in self.rw]
-        self.register_buffer("tw_cols", torch.tensor(self.tw_tables or [0], **i64), persistent=False)
-        self.register_buffer("rw_cols", torch.tensor(self.rw or [0], **i64), persistent=False)
+            for j in range(self.tmax):
+                if j < len(self.tw_by_rank[s]):
+                    t = self.tw_by_rank[s][j]
+                    cols.append(self.col_base + t)
+                    mods.append(plan.tables[t].rows)
+                    offs.append(lay[s][1][t])
+                else:
+                    cols.append(self.col_base)
+                    mods.append(1)
+                    offs.append(0)
+        self.register_buffer("tw_col", torch.tensor(cols or [0], dtype=torch.int32, device=dev), persistent=False)
+        self.register_buffer("tw_mod", torch.tensor(mods or [1], **i64), persistent=False)
+        self.register_buffer("tw_off", torch.tensor(offs or [0], **i64), persistent=False)
+        # row-wise: route to global table rows, then the masked gather of my range
+        Tr = len(self.rw)
+        self.register_buffer("rw_col", torch.tensor([self.col_base + t for t in self.rw] or [0], dtype=torch.int32,
+                                                    device=dev), persistent=False)
+        self.register_buffer("rw_mod", torch.tensor([plan.tables[t].rows for t in self.rw] or [1], **i64),
+                             persistent=False)
+        self.register_buffer("rw_zero", torch.zeros(max(1, Tr), **i64), persistent=False)
+        self.register_buffer("rw_off", torch.tensor([my_off[t] for t in self.rw] or [0], **i64), persistent=False)
+        self.register_buffer("rw_lo", torch.tensor([plan.placement(t).ranges[self.rank][0] for t in self.rw] or [0],
+                                                   **i64), persistent=False)
+        self.register_buffer("rw_n", torch.tensor([plan.placement(t).ranges[self.rank][1] for t in self.rw] or [0],
+                                                  **i64), persistent=False)
+        # where table t of (local candidate) b lands after the exchange, per bucket B
+        self._maps: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 
     def local_bytes(self) -> int:
         return self.store.numel() * self.store.element_size()
 
-    # -- the exchange ------------------------------------------------------
-    def _lookup(self, ids: torch.Tensor, mod, off, lo=None, n=None) -> torch.Tensor:
-        x, _ = ops.embed(self.store, ids, None, modulo_f=mod, offset_f=off, want_x=True, shard_lo_f=lo, shard_n_f=n)
-        return x
+    # -- exchange buffers / table map ----------------------------------------
+    def n_tw_rows(self, B: int) -> int:
+        return self.world * B * self.tmax if self.tw_tables else 0
 
-    def _table_wise(self, sparse: torch.Tensor) -> torch.Tensor:
-        """-> [B, world * tmax, D]: slot s*tmax+j = table tw_by_rank[s][j] for my rows."""
-        B, W, tm, D = sparse.shape[0], self.world, self.tmax, self.D
-        send = sparse.index_select(1, self.send_cols).view(B, W, tm).transpose(0, 1).contiguous()  # [W, B, tm]
-        if W > 1:
-            recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send, group=self.group)
-        else:
-            recv = send
-        emb = self._lookup(recv.view(W * B, tm), self.tw_mod, self.tw_off).view(W, B, tm, D)  # my tables, all rows
-        if W > 1:
-            wire = _coll_dtype(emb, self.group)
-            back = torch.empty_like(wire)
-            dist.all_to_all_single(back, wire.contiguous(), group=self.group)
-            back = back.to(emb.dtype)
-        else:
-            back = emb
-        return back.permute(1, 0, 2, 3).reshape(B, W * tm, D)
-
-    def _row_wise(self, sparse: torch.Tensor) -> torch.Tensor:
-        """-> [B, T_rw, D]: partial lookups summed across ranks."""
-        B, W, D = sparse.shape[0], self.world, self.D
-        ids = sparse.index_select(1, self.rw_cols).contiguous()  # [B, T_rw]
-        Tr = ids.shape[1]
-        if W > 1:
-            gathered = torch.empty(W * B, Tr, dtype=ids.dtype, device=ids.device)
-            _all_gather_rows(gathered, ids, self.group)
-        else:
-            gathered = ids
-        part = self._lookup(gathered, self.rw_mod, self.rw_off, self.rw_lo, self.rw_n)  # [W*B, Tr*D]
-        if W > 1:
-            wire = _coll_dtype(part, self.group)
-            out = torch.empty(B, Tr * D, dtype=wire.dtype, device=wire.device)
-            _reduce_scatter_sum(out, wire, self.group)
-            part = out.to(part.dtype)
-        return part.view(B, Tr, D)
-
-    def forward(self, sparse_ids: torch.Tensor) -> torch.Tensor:
-        B = sparse_ids.shape[0]
-        sparse_ids = sparse_ids.contiguous()
-        out = torch.empty(B, self.T, self.D, dtype=self.store.dtype, device=sparse_ids.device)
+    def alloc(self, B: int) -> Dict[str, torch.Tensor]:
+        """Static exchange buffers of one (bucket, slot)."""
+        dev, W, tm, D, Tr = self.store.device, self.world, self.tmax, self.D, len(self.rw)
+        i32 = dict(dtype=torch.int32, device=dev)
+        bf = dict(dtype=self.store.dtype, device=dev)
+        bufs = {"emb_all": torch.zeros(max(1, self.n_tw_rows(B) + B * Tr), D, **bf)}
         if self.tw_tables:
-            tw = self._table_wise(sparse_ids)
-            out.index_copy_(1, self.tw_cols, tw.index_select(1, self.recv_slot_tw))
-        if self.rw:
-            out.index_copy_(1, self.rw_cols, self._row_wise(sparse_ids))
-        return out
+            bufs["send_ids"] = torch.zeros(W, B, tm, **i32)
+            bufs["recv_ids"] = torch.zeros(W, B, tm, **i32)
+            bufs["emb_send"] = torch.zeros(W * B, tm * D, **bf)
+        if Tr:
+            bufs["rw_ids"] = torch.zeros(1, B, Tr, **i32)
+            bufs["rw_all"] = torch.zeros(W, B, Tr, **i32)
+            bufs["rw_part"] = torch.zeros(W * B, Tr * D, **bf)
+        return bufs
+
+    def table_map(self, B: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(emb_off, emb_stride) int64 [T]: table t of candidate b is row
+        off[t] + b * stride[t] of emb_all (all-to-all recv region: [owner][b][j];
+        reduce-scatter region after it: [b][i])."""
+        m = self._maps.get(B)
+        if m is None:
+            off, stride = [0] * self.T, [1] * self.T
+            for s in range(self.world):
+                for j, t in enumerate(self.tw_by_rank[s]):
+                    off[t], stride[t] = s * B * self.tmax + j, self.tmax
+            base = self.n_tw_rows(B)
+            for i, t in enumerate(self.rw):
+                off[t], stride[t] = base + i, len(self.rw)
+            dev = self.store.device
+            m = self._maps[B] = (torch.tensor(off, dtype=torch.int64, device=dev),
+                                 torch.tensor(stride, dtype=torch.int64, device=dev))
+        return m
+
+    # -- one step's aux-lane ops -----------------------------------------------
+    def program(self, ids: torch.Tensor, B: int, bufs: Dict[str, torch.Tensor]) -> List[sp.Op]:
+        W, tm, D, Tr = self.world, self.tmax, self.D, len(self.rw)
+        ops: List[sp.Op] = []
+
+        def route():
+            if self.tw_tables:
+                ops_k.shard_route(ids, W, tm, self.tw_col, self.tw_mod, self.tw_off, out=bufs["send_ids"])
+            if Tr:
+                ops_k.shard_route(ids, 1, Tr, self.rw_col, self.rw_mod, self.rw_zero[:Tr], out=bufs["rw_ids"])
+
+        def lookup():
+            if self.tw_tables:  # rows arrive hashed and offset: the gather needs no modulo
+                ops_k.embed(self.store, bufs["recv_ids"].view(W * B, tm), None, modulo=self.store.shape[0],
+                            want_x=True, out_x=bufs["emb_send"])
+            if Tr:
+                ops_k.embed(self.store, bufs["rw_all"].view(W * B, Tr), None, modulo_f=self.rw_mod,
+                            offset_f=self.rw_off, want_x=True, out_x=bufs["rw_part"], shard_lo_f=self.rw_lo,
+                            shard_n_f=self.rw_n)
+
+        ops.append(sp.Kernels(sp.AUX, route, "route"))
+        ops.append(sp.Sync("record", sp.AUX, 0))  # ids routed: the dense tower may read the batch
+        if self.tw_tables:
+            ops.append(sp.Coll("alltoall", sp.AUX, bufs["send_ids"], bufs["recv_ids"]))
+        if Tr:
+            ops.append(sp.Coll("allgather", sp.AUX, bufs["rw_ids"], bufs["rw_all"]))
+        ops.append(sp.Kernels(sp.AUX, lookup, "lookup"))
+        nt = self.n_tw_rows(B)
+        if self.tw_tables:
+            ops.append(sp.Coll("alltoall", sp.AUX, bufs["emb_send"], bufs["emb_all"][:nt]))
+        if Tr:
+            ops.append(sp.Coll("reduce_scatter", sp.AUX, bufs["rw_part"], bufs["emb_all"][nt:nt + B * Tr]))
+        return ops
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        """Eager exchange (collective): ids [B, F] (tables at columns
+        col_base..) -> [B, T, D]."""
+        B = ids.shape[0]
+        bufs = self.alloc(B)
+        sp.run_eager(self.program(ids.contiguous(), B, bufs), self.group)
+        off, stride = self.table_map(B)
+        rows = off.view(1, -1) + torch.arange(B, device=off.device).view(-1, 1) * stride.view(1, -1)
+        return bufs["emb_all"][rows]
 
 
 def build_parallel_model(cfg: ModelConfig, device, ctx: Optional[DistContext] = None, shard_tables: str = "auto",
@@ -335,20 +355,23 @@ class ShardedDLRM(nn.Module):
 
     Dense towers (bottom / top MLP, head) are replicated - built from the same
     seed as ``models.ctr.DLRM`` so an unsharded DLRM gives identical scores -
-    and run data-parallel on this rank's candidates."""
+    and run data-parallel on this rank's candidates. One step is a two-lane
+    program (parallel/step_program.py): the table exchange on the aux lane,
+    the bottom MLP overlapping it on the compute lane, then the interaction
+    reads the exchanged embeddings in place and the top MLP + head finish."""
 
     family = "dlrm"
 
     def __init__(self, cfg: ModelConfig, ctx: DistContext, device="cpu", plan: Optional[ShardingPlan] = None,
                  policy: str = "auto", budget_bytes: int = int(0.8 * MI355X_HBM_BYTES), group=None):
         super().__init__()
-        self.cfg, self.ctx = cfg, ctx
+        self.cfg, self.ctx, self.group = cfg, ctx, group
         world = ctx.world if ctx.is_distributed else 1
         self.plan = plan or plan_sharding(dlrm_tables(cfg), world, budget_bytes, policy)
         self.dense = DLRM(cfg, device=device, materialize_tables=False)
         self.dense.gen = None
         self.emb = ShardedEmbedding(self.plan, ctx, cfg.seed, self.dense.table_bound, DTYPES[cfg.param_dtype],
-                                    device, group)
+                                    device, group, col_base=cfg.num_dense)
         self.device_ = torch.device(device)
 
     def signature(self):
@@ -357,16 +380,42 @@ class ShardedDLRM(nn.Module):
     def param_bytes(self) -> int:
         return self.dense.param_bytes() + self.emb.local_bytes()
 
+    def alloc(self, B: int) -> Dict[str, torch.Tensor]:
+        return self.emb.alloc(B)
+
+    def build_program(self, ids: torch.Tensor, wts: torch.Tensor, B: int, bufs: Dict[str, torch.Tensor],
+                      out: Optional[torch.Tensor] = None, state: Optional[dict] = None) -> List[sp.Op]:
+        """One step over static inputs: ids [B, F] / wts [B, F] row views,
+        scores -> ``out`` (or ``state["scores"]``)."""
+        d = self.dense
+        st = {} if state is None else state
+        emb_off, emb_stride = self.emb.table_map(B)
+        ops = self.emb.program(ids, B, bufs)
+        k = next(i for i, o in enumerate(ops) if isinstance(o, sp.Sync))  # after the route: the batch is read
+
+        def bottom():
+            w = wts if wts.dtype == torch.float32 else wts.float()
+            st["dense"] = d.bottom(d.dense_input(w))
+
+        def top():
+            z = ops_k.dot_interaction(st["dense"], bufs["emb_all"], d.inter_cols, emb_off, emb_stride)
+            st["scores"] = d.top.forward_head(z, d.head_w, d.head_b, out=out)
+
+        ops[k + 1:k + 1] = [sp.Sync("wait", sp.COMPUTE, 0), sp.Kernels(sp.COMPUTE, bottom, "bottom")]
+        ops += [sp.Sync("record", sp.AUX, 1), sp.Sync("wait", sp.COMPUTE, 1), sp.Kernels(sp.COMPUTE, top, "top")]
+        return ops
+
     @torch.no_grad()
     def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor], out: Optional[torch.Tensor] = None):
-        if wts is not None and wts.dtype != torch.float32:
-            wts = wts.float()
-        d = self.dense
-        dense_out = d.bottom(d.dense_input(wts))
-        emb = self.emb(d.sparse_ids(ids))
-        return d.interact_and_top(dense_out, emb, out=out)
+        """Eager step (collective: every rank calls it with the same B)."""
+        B = ids.shape[0]
+        st: dict = {}
+        sp.run_eager(self.build_program(ids, wts, B, self.alloc(B), out=out, state=st), self.group)
+        return st["scores"]
 
     @property
     def has_collectives(self) -> bool:
-        """The forward issues collectives (not capturable into the step graph)."""
+        """The forward issues collectives (the engine runs it as a step program)."""
         return self.plan.world > 1
+
+    supports_program = True

@@ -131,6 +131,10 @@ class FanoutEngine:
         self.native_fanout = native_fanout
         self.force_fanout = force_fanout
         self._cin = self._cout = None
+        self._cprog = None  # step-program communicator (embedding-parallel models)
+        self._programs: Dict[Tuple[int, int], object] = {}
+        self._prog_bufs: Dict[Tuple[int, int], dict] = {}
+        self.program_active = False
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
@@ -209,8 +213,24 @@ class FanoutEngine:
             store[key] = t
         return t
 
+    @property
+    def lockstep(self) -> bool:
+        """Every rank must launch every step (collectives inside the step):
+        a candidate fan-out, or a model whose forward exchanges embeddings."""
+        return self.mode != "local" or bool(getattr(self.ex.model, "has_collectives", False))
+
     def prepare(self, B: int) -> None:
         self.check_bucket(B)
+        if self._program_enabled():
+            if self._cprog is None:
+                from .native_comm import create_comm
+
+                self._cprog = create_comm(self.ctx, self.group)
+            for s in range(self.ex.slots):
+                self.host_out(B, s)
+                self._capture_program(B, s)
+            self.program_active = True
+            return
         native = self._native_fanout_enabled()
         if self.force_fanout and self.world == 1 and self.mode != "local" and not native:
             raise RuntimeError("force_fanout on one rank needs the native fan-out path (GPU + HIP graphs)")
@@ -227,6 +247,47 @@ class FanoutEngine:
                 self._capture_ingress(B, s)
         # a failed self-check disables the native path for good (every rank agreed)
         self.native_fanout_active = native and not self._native_disabled
+
+    # -- programmed steps (embedding-parallel models) ------------------------------
+    def _program_enabled(self) -> bool:
+        return (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"
+                and getattr(self.ex.model, "supports_program", False)
+                and os.environ.get("DTFS_STEP_PROGRAM", "1") != "0")
+
+    def _capture_program(self, B: int, slot: int) -> None:
+        """Build and capture the step program of one (bucket, slot): GPU unpack
+        of the request arena + the model's two-lane program, each kernel op
+        captured into its own graph (parallel/step_program.py)."""
+        from . import step_program as sp
+
+        key = (B, slot)
+        if key in self._programs:
+            return
+        model = self.ex.model
+        buf = self.ex.input_buffer(B, slot)
+        arena_dev = self.dev_arena(slot)
+        h_out = self.host_out(B, slot)
+        bufs = self._prog_bufs[key] = model.alloc(B)
+        state: dict = {}
+        ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
+        ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B], state=state)
+        # warm-up: one eager run (collective on every rank, like the capture below)
+        sp.run_eager(ops, self.group)
+        torch.cuda.synchronize(self.dev)
+        pools = {lane: torch.cuda.graph_pool_handle() for lane in (sp.COMPUTE, sp.AUX)}
+        streams = {lane: torch.cuda.Stream(self.dev) for lane in (sp.COMPUTE, sp.AUX)}
+        direct = os.environ.get("DTFS_STEP_LAUNCH", "direct") != "graph"
+        prog = sp.capture_native(ops, arena_dev, self._cprog, pools, streams, direct=direct)
+        prog.state = state  # the captured graphs' intermediate tensors live here
+        self._programs[key] = prog
+
+    def _launch_program(self, B: int, slot: int, h_in, h_out, rows: int, t0: float,
+                        nbytes: Optional[int]) -> StepHandle:
+        self._capture_program(B, slot)
+        prog = self._programs[(B, slot)]
+        self.runner().launch_program(slot, prog.spec, h_in, int(nbytes or 0))
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot, (self._cprog,)),
+                          t_submit=t0, timeout_s=self.step_timeout_s)
 
     # -- native fan-out (world > 1) -----------------------------------------------
     def _native_fanout_enabled(self) -> bool:
@@ -391,7 +452,10 @@ class FanoutEngine:
         rows = self.contrib_rows(B)
         for s in range(self.ex.slots):
             h_out = self.host_out(B, s)
-            if self._step_graphs_enabled():
+            if self.program_active:
+                self._capture_program(B, s)
+                out.append(dict(program=self._programs[(B, s)].spec, h2d_dst=self.dev_arena(s), h_out=h_out))
+            elif self._step_graphs_enabled():
                 self._capture_step(B, s)
                 g = self._step_graph[(B, s)]
                 out.append(dict(h2d_dst=self.dev_arena(s), graph_exec=g.raw_cuda_graph_exec(), seq=seq(g),
@@ -417,11 +481,11 @@ class FanoutEngine:
         """Asynchronous RCCL error of the native communicators (failure detection)."""
         from .native_comm import check_comms
 
-        return check_comms(self._cin, self._cout)
+        return check_comms(self._cin, self._cout, self._cprog)
 
     def abort(self) -> None:
         """Abort the native communicators (a peer is gone / a deadline passed)."""
-        for c in (self._cin, self._cout):
+        for c in (self._cin, self._cout, self._cprog):
             if c is not None:
                 c.abort()
 
@@ -531,6 +595,8 @@ class FanoutEngine:
                     self.arena.unpack_cpu(h_in, packed[:rows])
                 h_in = packed
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
+        if self.program_active:
+            return self._launch_program(B, slot, h_in, h_out, rows, t0, nbytes)
         if self._step_graphs_enabled():
             return self._launch_step_graph(B, slot, h_in, h_out, rows, t0, nbytes)
         if self.native_fanout_active:

@@ -68,3 +68,13 @@ def test_bench_more_ranks(n, mode):
     assert out["value"] == pytest.approx(n * 40 / (out["ms_per_step"] * 1e-3), rel=0.02)
     assert out.get("requests_failed", 0) == 0
     assert (mode in out["config"]["parallelism"]) or (mode == "local" and "replica" in out["config"]["parallelism"])
+
+
+@pytest.mark.slow
+def test_bench_sharded_dlrm_world2():
+    """DLRM with tables sharded over 2 gloo ranks: every step is the eager step
+    program (ids all-to-all, owner gather, embeddings all-to-all) in lockstep."""
+    out = _run_bench(2, ("--model", "dlrm", "--table-rows", "5000"))
+    par = out["config"]["parallelism"]
+    assert "embedding-mp2" in par and "candidate-dp2" in par, par
+    assert out.get("requests_failed", 0) == 0 and out["config"]["global_batch"] == 128

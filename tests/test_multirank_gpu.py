@@ -39,3 +39,27 @@ def test_bench_ranks_sharing_one_gpu(n, mode):
     assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
     if mode != "local":
         assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n):
+    """BASELINE config 4 shape on N ranks: DLRM tables sharded table-wise over
+    the ranks, every step a native two-lane step program (ids all-to-all ->
+    owner gather -> embeddings all-to-all on the aux lane, bottom MLP on the
+    compute lane), checked against the eager forward before the run."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
+           "--model", "dlrm", "--table-rows", "1000000", "--steps", "20", "--warmup", "4",
+           "--requests-per-gpu", "4", "--request-rows", "96", "--pool", "8", "--client-threads", "2",
+           "--qps", "0", "--step-timeout-s", "20"]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    par = out["config"]["parallelism"]
+    assert f"embedding-mp{n}" in par and "native two-lane step program" in par, par

@@ -1,0 +1,112 @@
+"""Embedding-parallel DLRM as a native two-lane step program on one GPU
+(parallel/step_program.py, StepRunner.launch_program): a 1-rank sharded DLRM
+(table-wise, row-wise and mixed placements; the exchanges are 1-rank RCCL
+collectives on the aux lane) against the unsharded model, the route and mapped
+interaction kernels against their fp32 CPU references, and the live server
+serving requests through the captured program."""
+import pytest
+import torch
+
+from distributed_tf_serving_amd import ops
+from distributed_tf_serving_amd.config import ModelConfig, ServingConfig
+from distributed_tf_serving_amd.models import build_model
+from distributed_tf_serving_amd.parallel.dist import DistContext
+from distributed_tf_serving_amd.parallel.embedding_sharding import (Placement, ShardedDLRM, ShardingPlan,
+                                                                    dlrm_tables, plan_sharding)
+from distributed_tf_serving_amd.parallel.fanout import FanoutEngine
+from distributed_tf_serving_amd.serving.arena import ArenaLayout
+from distributed_tf_serving_amd.serving.executor import ShardExecutor
+from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg():
+    return ModelConfig(family="dlrm", num_fields=43, num_dense=13, table_rows=200_003, embed_dim=64,
+                       bottom_mlp=(512, 256, 64), mlp_dims=(1024, 512, 256))
+
+
+def _plan(cfg, policy):
+    """1-rank plan; plan_sharding never picks row-wise at world 1, so the
+    row-wise placements are written out (the rank owns every row range)."""
+    base = plan_sharding(dlrm_tables(cfg), 1, policy="table")
+    row = {"table": lambda t: False, "row": lambda t: True, "mixed": lambda t: t % 3 == 0}[policy]
+    pl = [Placement(p.table, "row", ranges=[(0, cfg.table_rows)]) if row(p.table) else p for p in base.placements]
+    return ShardingPlan(base.tables, 1, pl, base.budget_bytes)
+
+
+def test_shard_route_matches_cpu(cuda):
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 1 << 40, (300, 43), generator=g)
+    W, tm = 3, 4
+    col = torch.randint(0, 43, (W * tm,), generator=g, dtype=torch.int64).to(torch.int32)
+    mod = torch.randint(1, 10_000, (W * tm,), generator=g)
+    off = torch.randint(0, 1 << 20, (W * tm,), generator=g)
+    want = ops.shard_route(ids, W, tm, col, mod, off)
+    got = ops.shard_route(ids.to(cuda), W, tm, col.to(cuda), mod.to(cuda), off.to(cuda))
+    torch.cuda.synchronize()
+    assert got.shape == (W, 300, tm) and torch.equal(got.cpu(), want)
+
+
+def test_dot_interaction_table_map_matches_cpu(cuda):
+    g = torch.Generator().manual_seed(4)
+    B, T, D = 257, 30, 64
+    dense = (torch.rand(B, D, generator=g) - 0.5).to(torch.bfloat16)
+    flat = (torch.rand(3 * B * 11 + 7, D, generator=g) - 0.5).to(torch.bfloat16)
+    off = torch.randint(0, 3 * B, (T,), generator=g)
+    stride = torch.randint(1, 11, (T,), generator=g)
+    want = ops.dot_interaction(dense, flat, 0, off, stride).float()
+    got = ops.dot_interaction(dense.to(cuda), flat.to(cuda), 0, off.to(cuda), stride.to(cuda))
+    torch.cuda.synchronize()
+    assert (got.float().cpu() - want).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("policy", ["table", "row", "mixed"])
+def test_sharded_dlrm_one_rank_matches_unsharded(cuda, policy):
+    cfg = _cfg()
+    ctx = DistContext(device=cuda)
+    m = ShardedDLRM(cfg, ctx, device=cuda, plan=_plan(cfg, policy)).eval()
+    ref = build_model(cfg, cuda)
+    g = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, 1 << 40, (700, cfg.num_fields), generator=g).to(cuda)
+    wts = torch.rand(700, cfg.num_fields, generator=g).to(cuda)
+    got, want = m(ids, wts), ref(ids, wts)
+    torch.cuda.synchronize()
+    assert (got - want).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("policy", ["table", "mixed"])
+def test_step_program_engine_and_live_server(cuda, policy):
+    """FanoutEngine captures the program per slot; StepRunner.launch_program
+    runs it (self_check vs the eager forward), then the native live server
+    serves requests through it."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.live import LiveScheduler
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
+
+    cfg = _cfg()
+    ctx = DistContext(device=cuda)
+    m = ShardedDLRM(cfg, ctx, device=cuda, plan=_plan(cfg, policy)).eval()
+    F, B, S = cfg.num_fields, 1024, 3
+    ex = ShardExecutor(m, PackedLayout(F), [B], cuda, slots=S)
+    eng = FanoutEngine(ex, ctx, mode="local", ingest="arena", arena=ArenaLayout(F, max_rows=B))
+    eng.prepare(B)
+    assert eng.program_active and eng.lockstep is False
+    assert eng.self_check(B, seed=2)
+    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=(B,), batch_timeout_us=100)
+    live = LiveScheduler(eng, sc, buckets=[B], depth=S)
+    try:
+        synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=9)
+        for rows in (1, 300, 1024):
+            req = synth.serialized(rows, raw=True)
+            r = pb.PredictRequest.FromString(req)
+            ids = torch.from_numpy(T.to_ndarray(r.inputs["feat_ids"])).to(cuda)
+            wts = torch.from_numpy(T.to_ndarray(r.inputs["feat_wts"])).to(cuda)
+            want = m(ids, wts).float().cpu()
+            resp = pb.PredictResponse.FromString(live.predict_bytes(req, 30.0))
+            got = torch.from_numpy(T.to_ndarray(resp.outputs["prediction_node"]))
+            assert got.shape == (rows,)
+            assert (got - want).abs().max().item() < 1e-5
+    finally:
+        live.close()
