@@ -59,7 +59,7 @@ from distributed_tf_serving_amd.parallel.fanout import FanoutEngine  # noqa: E40
 from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E402
 from distributed_tf_serving_amd.serving.arena import ArenaLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.live import LiveScheduler  # noqa: E402
-from distributed_tf_serving_amd.serving.packing import PackedLayout  # noqa: E402
+from distributed_tf_serving_amd.serving.packing import PackedLayout, layout_for  # noqa: E402
 from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
 from distributed_tf_serving_amd.utils.gc_tuning import tune_for_serving  # noqa: E402
@@ -103,6 +103,12 @@ def parse_args():
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--shard-tables", action="store_true",
                     help="dlrm: shard the tables even on one GPU (exercises the embedding-exchange step program)")
+    ap.add_argument("--small-buckets", default="2048",
+                    help="N=1 (no lockstep): extra padding buckets below the full step, so a lightly loaded "
+                         "server runs a step sized to what is queued (TF-Serving allowed_batch_sizes); '' = only "
+                         "the full step. 2048: bench/bucket_cost.py on MI355X - a 512- or 1024-row step costs "
+                         "64-66 us pipelined (launch-chain bound), a 2048-row one 79 us, so smaller buckets only "
+                         "saturate at 20k QPS of 512-row requests")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight)")
     ap.add_argument("--batch-timeout-us", type=int, default=200)
@@ -153,12 +159,19 @@ def build(a, ctx):
     if sharded and a.mode != "local":
         raise SystemExit("dlrm with sharded tables runs --mode local (the embedding exchange is the fan-out)")
     mode = a.mode if world > 1 else ("alltoall" if a.force_fanout else "local")
-    ex = ShardExecutor(model, PackedLayout(F), [B], dev, use_graphs=not a.no_graphs, slots=a.slots)
+    # lockstep jobs (collectives in the step) always run the full bucket on every rank
+    small = [int(x) for x in a.small_buckets.split(",") if x.strip()] if a.small_buckets else []
+    lock = world > 1 and (mode != "local" or sharded)
+    buckets = sorted({b for b in small if 0 < b < B} | {B}) if not lock and mode == "local" else [B]
+    # fan-out rows travel narrow (int32 table rows + bf16 weights: half the xGMI bytes)
+    layout = layout_for(cfg, mode != "local" and not a.no_narrow) if mode != "local" else PackedLayout(F)
+    ex = ShardExecutor(model, layout, buckets, dev, use_graphs=not a.no_graphs, slots=a.slots)
     rows_in_max = B * (world if mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
                        native_fanout=not a.no_native_fanout)
-    eng.prepare(B)
+    for b in buckets:
+        eng.prepare(b)
     if eng.program_active:
         # one synthetic step of the native step program vs the eager forward (collective)
         if not eng.self_check(B, seed=rank):
@@ -219,9 +232,10 @@ def run_live(a, ctx, cfg, model, eng, B):
     # lockstep (fan-out): every rank launches exactly this many steps, empty
     # ones included, so the collectives of the last steps always pair up
     max_steps = a.warmup + a.steps + -(-conc // max(1, n_req)) + 4 if lockstep else -1
-    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=(B,), batch_timeout_us=a.batch_timeout_us,
+    buckets = list(eng.ex.buckets)
+    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=tuple(buckets), batch_timeout_us=a.batch_timeout_us,
                        max_queued_rows=1 << 24, max_request_rows=1 << 20)
-    live = LiveScheduler(eng, sc, buckets=[B], depth=a.slots, lockstep=lockstep, max_steps=max_steps,
+    live = LiveScheduler(eng, sc, buckets=buckets, depth=a.slots, lockstep=lockstep, max_steps=max_steps,
                          step_timeout_s=a.step_timeout_s, start_paused=lockstep, narrow=not a.no_narrow)
     extra = {}
     if world == 1 and pool:
@@ -394,7 +408,9 @@ def main():
                                               "one independent replica per GPU, no collectives") + ")"
         else:
             par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
-                   + (", native C++ step" if eng.native_fanout_active else ", torch.distributed") + ")")
+                   + (", native C++ step" if eng.native_fanout_active else ", torch.distributed")
+                   + (f", {eng.layout.row_bytes} B rows: int32 table rows + bf16 weights" if eng.layout.narrow
+                      else f", {eng.layout.row_bytes} B rows: raw int64 ids + fp32 weights") + ")")
         if hasattr(model, "plan"):
             par += (f" + embedding-mp{model.plan.world} ({len(model.plan.row_wise())} row-wise tables, all-to-all; "
                     + ("native two-lane step program" if eng.program_active else "eager torch.distributed") + ")")
@@ -416,6 +432,7 @@ def main():
                 "global_batch": world * B,
                 "request_rows": a.request_rows,
                 "requests_per_gpu_per_step": a.requests_per_gpu,
+                "buckets": list(eng.ex.buckets),
                 "seq_len": None,
                 "parallelism": par,
                 "encoding": a.encoding,

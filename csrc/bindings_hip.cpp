@@ -105,9 +105,10 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
     TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]: ids are hashed onto rows");
   }
   if (wts) {
-    TORCH_CHECK(wts->is_cuda() && wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->size(0) == B &&
-                    wts->size(1) == F && wts->stride(1) == 1 && wts->stride(0) >= F,
-                "wts must be fp32 [B, F] with contiguous rows");
+    TORCH_CHECK(wts->is_cuda() && (wts->scalar_type() == torch::kFloat32 || wts->scalar_type() == torch::kBFloat16) &&
+                    wts->dim() == 2 && wts->size(0) == B && wts->size(1) == F && wts->stride(1) == 1 &&
+                    wts->stride(0) >= F,
+                "wts must be fp32 / bf16 [B, F] with contiguous rows");
     check_same_dev(table, *wts, "wts");
   }
   if (lin) {
@@ -132,7 +133,8 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
   a.ids = ids.data_ptr();
   a.ids64 = ids.scalar_type() == torch::kInt64;
   a.ids_ld = ids.stride(0);
-  a.wts = wts ? wts->data_ptr<float>() : nullptr;
+  a.wts = wts ? wts->data_ptr() : nullptr;
+  a.wts16 = wts && wts->scalar_type() == torch::kBFloat16;
   a.wts_ld = wts ? wts->stride(0) : 0;
   a.B = int(B);
   a.F = int(F);
@@ -499,18 +501,19 @@ torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, in
 }
 
 // ---------------------------------------------------------------- K0 ingest
-void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields) {
+void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields, int64_t narrow_modulo) {
   check_dev(arena, "arena");
   check_dev(packed, "packed");
   check_same_dev(arena, packed, "packed");
   TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.numel() > dtfs::kArenaPayloadOff, "arena: uint8 [cap]");
   TORCH_CHECK(packed.scalar_type() == torch::kInt64 && packed.dim() == 2, "packed must be int64 [B, W]");
-  TORCH_CHECK(packed.size(1) * 8 >= 12 * fields, "packed rows too narrow for the field count");
+  TORCH_CHECK(packed.size(1) * 8 >= (narrow_modulo > 0 ? 6 : 12) * fields, "packed rows too narrow for the field count");
+  TORCH_CHECK(narrow_modulo >= 0 && narrow_modulo < (int64_t(1) << 31), "narrow_modulo must fit int32 rows");
   c10::DeviceGuard g(arena.device());
   // descriptor offsets come from the (validated) host parse of this arena; the
   // kernel additionally bounds n_req by the descriptor capacity
   check_hip(dtfs::launch_unpack_arena(arena.data_ptr(), packed.data_ptr<int64_t>(), int(packed.size(0)), int(fields),
-                                      int(packed.size(1)), dtfs::kArenaMaxRequests, cur_stream(arena)),
+                                      int(packed.size(1)), dtfs::kArenaMaxRequests, cur_stream(arena), narrow_modulo),
             "unpack_arena");
 }
 
@@ -875,7 +878,8 @@ PYBIND11_MODULE(_hip, m) {
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
-  m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"));
+  m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"),
+        py::arg("narrow_modulo") = 0);
   m.def("arena_varint_decode", &arena_varint_decode, py::arg("arena"), py::arg("blocks") = 256);
   m.def("pull_host", &pull_host, py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("blocks") = 128);
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);

@@ -84,6 +84,13 @@ __device__ __forceinline__ float fm_row_logit(const float (&s)[8], const float (
   return wave_sum(part);
 }
 
+// feature weight: fp32, or bf16 rows (narrow packed rows of the fan-out); 1 without weights
+__device__ __forceinline__ float load_weight(const EmbedArgs& a, int64_t i) {
+  if (!a.wts) return 1.f;
+  if (a.wts16) return __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.wts)[i]) << 16);
+  return static_cast<const float*>(a.wts)[i];
+}
+
 template <int D, typename IdT, bool ARENA>
 __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
   constexpr int LPR = D / 8;          // lanes per table row (16 B each)
@@ -118,7 +125,7 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
         if (arow.ids) arena_feature(arow, fl, id, w_in);
       } else {
         id = int64_t(ids[int64_t(b) * a.ids_ld + fl]);
-        w_in = a.wts ? a.wts[int64_t(b) * a.wts_ld + fl] : 1.f;
+        w_in = load_weight(a, int64_t(b) * a.wts_ld + fl);
       }
       const int64_t m = a.modulo_f ? a.modulo_f[fl] : a.modulo;
       int64_t g = hash_row(id, m);
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
       if (ar.ids) arena_feature(ar, lane, id, w);
     } else {
       id = int64_t(static_cast<const IdT*>(a.ids)[int64_t(r) * a.ids_ld + lane]);
-      w = a.wts ? a.wts[int64_t(r) * a.wts_ld + lane] : 1.f;
+      w = load_weight(a, int64_t(r) * a.wts_ld + lane);
     }
   };
   // stage 2: hash -> table row (clamped), weight (0 for rows another shard owns)

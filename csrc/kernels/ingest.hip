@@ -60,6 +60,33 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
   }
 }
 
+// Narrow output (the candidate fan-out's exchange rows, serving/packing.py
+// PackedLayout(narrow_modulo=m)): [int32 table rows x F | bf16 weights x F |
+// pad], 6 bytes per field instead of 12, so the all-to-all moves half the
+// bytes. Raw ids are hashed (id mod m) here; host-narrowed rows already are.
+__global__ void __launch_bounds__(256) unpack_arena_narrow_kernel(const uint8_t* __restrict__ arena,
+                                                                  int64_t* __restrict__ packed, int B, int F, int W,
+                                                                  int64_t modulo) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const ArenaRow src = arena_row(arena, kArenaPayloadOff, r);
+  int32_t* ids = reinterpret_cast<int32_t*>(packed + int64_t(r) * W);
+  uint16_t* wts = reinterpret_cast<uint16_t*>(ids + F);
+  for (int f = lane; f < F; f += 64) {
+    int64_t id = 0;
+    float w = 0.f;  // padding rows (no request): row 0, weight 0
+    if (src.ids) arena_feature(src, f, id, w);
+    ids[f] = int32_t(src.narrow ? id : hash_row(id, modulo));
+    const bf16 wb = f2bf(w);  // round to nearest even, as torch's fp32 -> bf16
+    wts[f] = *reinterpret_cast<const uint16_t*>(&wb);
+  }
+  // zero the row's pad bytes (fixed-size rows travel whole)
+  const int used = 6 * F, total = 8 * W;
+  uint8_t* row = reinterpret_cast<uint8_t*>(ids);
+  for (int c = used + lane; c < total; c += 64) row[c] = 0;
+}
+
 // H2D by the GPU itself: waves read the pinned request arena over PCIe and
 // write device memory. Replaces the SDMA copy of the serving step: an SDMA
 // command costs 10-17 us of idle engine time between back-to-back copies
@@ -215,9 +242,15 @@ hipError_t launch_pull_host(void* dst, const void* src, int64_t nbytes, int bloc
 }
 
 hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
-                               hipStream_t st) {
+                               hipStream_t st, int64_t narrow_modulo) {
   (void)max_req;  // rows are located through the row table, not the descriptors
   if (B == 0) return hipSuccess;
+  if (narrow_modulo > 0) {
+    if (W * 8 < 6 * F || narrow_modulo >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern::unpack_arena_narrow_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
+                       static_cast<const uint8_t*>(arena), packed, B, F, W, narrow_modulo);
+    return hipGetLastError();
+  }
   if (W * 8 < 12 * F) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern::unpack_arena_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
                      static_cast<const uint8_t*>(arena), packed, B, F, W);

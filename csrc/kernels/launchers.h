@@ -25,8 +25,9 @@ struct EmbedArgs {
   const void* ids = nullptr;       // int32/int64 [B, ids_ld] (first F used)
   bool ids64 = true;
   int64_t ids_ld = 0;
-  const float* wts = nullptr;      // fp32 [B, wts_ld] (optional)
+  const void* wts = nullptr;       // fp32 (or bf16 with wts16) [B, wts_ld] (optional)
   int64_t wts_ld = 0;
+  bool wts16 = false;
   int B = 0, F = 0, D = 0;
   int64_t V = 0;                   // table rows (rows are clamped into [0, V))
   int64_t modulo = 0;              // shared-table hashing
@@ -56,8 +57,9 @@ void set_embed_wave_cap(int waves, int rows_in_flight = 1);
 // rows [B, W] int64 (serving/arena.py, csrc/runtime/arena.h share the layout).
 constexpr int kArenaPayloadOff = 64 + 32 * 1024;  // descriptors: up to 1024 requests
 constexpr int kArenaMaxRequests = 1024;
+// narrow_modulo > 0: narrow rows [int32 (id mod m) x F | bf16 weights x F | pad].
 hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
-                               hipStream_t st);
+                               hipStream_t st, int64_t narrow_modulo = 0);
 // Packed varint ids of a built arena -> its device-only int64 id region
 // (csrc/runtime/arena.h VarintChunk); blocks loop over the chunk table.
 hipError_t launch_arena_varint(void* arena, int blocks, hipStream_t st);

@@ -204,7 +204,7 @@ class FanoutEngine:
         from ..ops import hip
 
         self.arena.decode_varints(arena_dev)
-        hip().unpack_arena(arena_dev, packed, self.layout.fields)
+        hip().unpack_arena(arena_dev, packed, self.layout.fields, self.layout.narrow_modulo)
 
     def _dev(self, store, key, shape, dtype):
         t = store.get(key)
@@ -386,11 +386,12 @@ class FanoutEngine:
             else:
                 buf = self.host_in(B, slot)
                 if rows:
-                    self.layout.ids(buf)[:rows].copy_(ids)
-                    self.layout.wts(buf)[:rows].copy_(wts)
+                    self.layout.pack(ids, wts, out=buf[:rows])
                 h = self.launch(B, slot, nbytes=0 if self.ingest == "arena" else None)
             got = h.wait().clone()
             if rows:
+                if self.layout.narrow:  # the exchanged rows carry bf16 weights
+                    wts = wts.to(torch.bfloat16).float()
                 want = self.ex.model(ids.to(self.dev), wts.to(self.dev)).float().cpu()
                 diff = (got - want).abs().max().item()
                 ok = bool(diff <= atol)
@@ -592,7 +593,14 @@ class FanoutEngine:
             if arena_mode:  # host reference of the GPU unpack
                 packed = self.host_in(B, slot)
                 if rows:
-                    self.arena.unpack_cpu(h_in, packed[:rows])
+                    if self.layout.narrow:  # wide unpack, then the narrow row form
+                        from ..serving.packing import PackedLayout
+
+                        wide = PackedLayout(self.layout.fields)
+                        tmp = self.arena.unpack_cpu(h_in, wide.alloc(rows))
+                        self.layout.pack(wide.ids(tmp), wide.wts(tmp), out=packed[:rows])
+                    else:
+                        self.arena.unpack_cpu(h_in, packed[:rows])
                 h_in = packed
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
         if self.program_active:

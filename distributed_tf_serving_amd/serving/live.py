@@ -33,8 +33,7 @@ from .errors import Code, ServingError
 log = logging.getLogger(__name__)
 
 
-# families whose forward hashes every id with one modulo (cfg.vocab_size)
-NARROW_FAMILIES = ("wdl", "deepfm", "dcn", "dcn_v2")
+from .packing import NARROW_FAMILIES  # noqa: E402  (single-modulo families)
 
 
 def _code(c: int) -> Code:

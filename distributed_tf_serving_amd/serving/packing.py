@@ -20,12 +20,24 @@ import torch
 
 @dataclass(frozen=True)
 class PackedLayout:
+    """``narrow_modulo`` > 0: the narrow row [int32 table rows x F | bf16
+    weights x F | pad to 8 bytes] - ids already hashed (id mod m, the model's
+    table size) and weights rounded to bf16, 6 bytes per field instead of 12.
+    The candidate fan-out exchanges rows in this form (half the xGMI bytes,
+    SURVEY.md §2.5 C1: "narrow ids to int32 and wts to bf16 first"); the
+    gather reads int32 rows and bf16 weights in place."""
+
     fields: int
+    narrow_modulo: int = 0
+
+    @property
+    def narrow(self) -> bool:
+        return self.narrow_modulo > 0
 
     @property
     def row_bytes(self) -> int:
-        b = 12 * self.fields
-        return b + (b % 8)
+        b = (6 if self.narrow else 12) * self.fields
+        return (b + 7) // 8 * 8
 
     @property
     def words(self) -> int:
@@ -36,16 +48,35 @@ class PackedLayout:
         return t
 
     def ids(self, buf: torch.Tensor) -> torch.Tensor:
-        """int64 [rows, F] row view."""
+        """int64 [rows, F] row view (narrow: int32 table rows)."""
+        if self.narrow:
+            return buf.view(torch.int32)[:, : self.fields]
         return buf[:, : self.fields]
 
     def wts(self, buf: torch.Tensor) -> torch.Tensor:
-        """fp32 [rows, F] row view."""
+        """fp32 [rows, F] row view (narrow: bf16)."""
+        if self.narrow:
+            return buf.view(torch.bfloat16)[:, 2 * self.fields: 3 * self.fields]
         return buf.view(torch.float32)[:, 2 * self.fields: 3 * self.fields]
 
     def pack(self, ids: torch.Tensor, wts: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         rows = ids.shape[0]
         buf = self.alloc(rows, device=ids.device) if out is None else out
+        if self.narrow:
+            ids = torch.remainder(ids.long(), self.narrow_modulo).to(torch.int32)
+            wts = wts.to(torch.bfloat16)
         self.ids(buf)[:rows].copy_(ids)
         self.wts(buf)[:rows].copy_(wts)
         return buf
+
+
+# families whose forward hashes every id with ONE modulo (cfg.vocab_size) and
+# reads ids / weights only in the embedding gather
+NARROW_FAMILIES = ("wdl", "deepfm", "dcn", "dcn_v2")
+
+
+def layout_for(cfg, fanout: bool) -> PackedLayout:
+    """Packed rows a shard backend uses: narrow when the rows are exchanged
+    between GPUs (candidate fan-out) and the model allows it."""
+    narrow = fanout and cfg.family in NARROW_FAMILIES and 0 < int(getattr(cfg, "vocab_size", 0)) < (1 << 31)
+    return PackedLayout(cfg.num_fields, int(cfg.vocab_size) if narrow else 0)

@@ -27,7 +27,7 @@ from .batching import BatchingScheduler
 from .executor import ShardExecutor
 from .live import LiveScheduler
 from .monitoring import ServingMetrics
-from .packing import PackedLayout
+from .packing import PackedLayout, layout_for
 from .registry import ModelRegistry, Servable, Signature
 from .service import PredictionServiceImpl
 
@@ -66,12 +66,14 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
     dev = torch.device(device) if device is not None else (ctx.device if ctx is not None else pick_device(sc.device))
     ctx = ctx or DistContext(device=dev)
     model = build_parallel_model(cfg.model, dev, ctx)
-    layout = PackedLayout(cfg.model.num_fields)
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
     use_graphs = sc.use_graphs
     live = live_enabled(cfg, mode, model)
     if live and dev.type == "cuda" and not use_graphs:
         live = False  # the native step replays captured graphs
+    # rows exchanged between GPUs travel narrow (int32 rows + bf16 weights)
+    fanout = live and mode != "local" and ctx.is_distributed
+    layout = layout_for(cfg.model, fanout) if fanout else PackedLayout(cfg.model.num_fields)
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=use_graphs, slots=slots)
     if live:
         eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena",

@@ -398,6 +398,32 @@ def test_unpack_arena_gpu_matches_cpu(cuda):
     assert torch.equal(got.cpu(), ref)  # rows past total_rows are zeroed too
 
 
+def test_unpack_arena_narrow_matches_cpu(cuda):
+    """Narrow fan-out rows: [int32 id mod m | bf16 weight | pad] from raw,
+    varint and host-narrowed arena rows vs the wide CPU unpack + narrowing."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    m = 999_983
+    A, W, N = ArenaLayout(43, 2048), PackedLayout(43), PackedLayout(43, m)
+    assert N.row_bytes == 264 and W.row_bytes == 520
+    ar = A.alloc()
+    s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=6)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, False), (64, True))]
+    ab = A.build(ar, A.place(ar, reqs))
+    assert not any(ab.errors)
+    dev = ar.to(cuda)
+    wide = A.unpack_cpu(ar, W.alloc(512))
+    ref = N.pack(W.ids(wide), W.wts(wide))
+    got = N.alloc(512, device=cuda)
+    got.fill_(-1)
+    A.decode_varints(dev)
+    ops.hip().unpack_arena(dev, got, 43, m)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref)
+
+
 @pytest.mark.parametrize("family", ["deepfm", "wdl", "dcn", "dcn_v2"])
 def test_forward_arena_matches_packed(cuda, family):
     # K0 fused into K1: the gather reads ids / weights from the raw request bytes

@@ -86,11 +86,13 @@ def test_native_serving_loop(cuda, mode, raw):
 
 
 @pytest.mark.parametrize("mode", ["alltoall", "scatter"])
-@pytest.mark.parametrize("ingest", ["packed", "arena"])
+@pytest.mark.parametrize("ingest", ["packed", "arena", "arena-narrow"])
 def test_native_fanout_step_matches_local(cuda, mode, ingest):
     cfg = ModelConfig(family="deepfm", vocab_size=50_000)
     m = build_model(cfg, cuda)
-    L = PackedLayout(cfg.num_fields)
+    narrow = ingest == "arena-narrow"
+    ingest = "arena" if narrow else ingest
+    L = PackedLayout(cfg.num_fields, cfg.vocab_size if narrow else 0)
     B = 1024
     ex = ShardExecutor(m, L, [B], cuda, slots=3)
     eng = FanoutEngine(ex, DistContext(device=cuda), mode=mode, ingest=ingest,
