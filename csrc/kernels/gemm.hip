@@ -776,6 +776,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   const int lr = lane >> 3, ls = lane & 7;
   const int fr = lane & 15, fq = lane >> 4;
 
+  const int nk = (K * EB) / 128;
   // staging geometry: quarter q of A / B = 16 groups of 8 contiguous LDS rows;
   // this wave stages groups wid and wid + 8 of every quarter
   auto a_row = [&](int qm, int g) { return (g < 8 ? 0 : 128) + 64 * qm + 8 * (g & 7); };
@@ -794,9 +795,11 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
       a_dst[q][j] = ra * 128;
       b_dst[q][j] = BM * 128 + rb * 128;
     }
+  // tiles past the end (the loop stages unconditionally, see below) re-load
+  // the last tile into the buffer nobody reads any more
   auto stage_a = [&](int q, int kt) {
     uint8_t* base = smem + (kt & 1) * BUF;
-    const int64_t kb = int64_t(kt) * 128;
+    const int64_t kb = int64_t(min(kt, nk - 1)) * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(A + a_src[q][j] + kb),
@@ -804,7 +807,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   };
   auto stage_b = [&](int q, int kt) {
     uint8_t* base = smem + (kt & 1) * BUF;
-    const int64_t kb = int64_t(kt) * 128;
+    const int64_t kb = int64_t(min(kt, nk - 1)) * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(W + b_src[q][j] + kb),
@@ -817,7 +820,6 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K * EB) / 128;
   // prologue: tile 0 whole + tile 1's Aq0, Bq0 (staged at phases -2, -1 of the
   // steady-state schedule below)
   stage_a(0, 0);
@@ -866,9 +868,14 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     }
   };
   // one quadrant: 4 x 2 output tiles (transposed MFMA: D = W . A^T, see store_acc_t)
+  // sched_barrier(0) pins the quadrant's MFMAs inside their phase: without it
+  // the scheduler sinks every (register-only) scaled fp8 MFMA of the K tile
+  // past the phase barriers to the end of the iteration (seen in the gfx950
+  // ISA), which serialises the two wave groups instead of overlapping them
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -882,66 +889,60 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[kk][i], c, 0, 0, 0);
         }
       }
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
   };
   auto barrier = [] {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // Wait so that the quarter staged 4 phases ago has landed: keep the
-  // quarters staged at phases phi-3..phi (2 DMA instructions each) in flight.
-  // Quarter staging phases: Aq0(u) 4u-6, Bq0(u) 4u-5, Bq1(u) 4u-4, Aq1(u) 4u-3
-  // (u < nk), so the last one is at 4nk-7.
-  const int last_stage = 4 * nk - 7;
-  auto wait_dma = [&](int phi) {
-    const int hi = min(phi, last_stage), lo = max(phi - 3, -2);
-    const int keep = hi >= lo ? hi - lo + 1 : 0;
-    if (keep >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (keep == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (keep == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (keep == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
   // Phase = reads | stage one quarter | counted wait | barrier | MFMAs | barrier
   //   p0: read A[qm0] B[qn0], stage Bq1(t+1)      p1: read B[qn1], stage Aq1(t+1)
   //   p2: read A[qm1],        stage Aq0(t+2)      p3: (no reads), stage Bq0(t+2)
   // WAR: each quarter is restaged >= 2 phases after its last read (Aq0, Bq0 at
   // p0; Bq1 p1; Aq1 p2). RAW: a quarter staged at phase s is retired by the
-  // wait of phase s+4 and first read at phase >= s+5.
+  // wait of phase s+4 (vmcnt(8): the 4 most recent quarters, 2 DMA
+  // instructions each, stay in flight) and first read at phase >= s+5.
+  // The loop body is branch-free: the stages of tiles nk and nk+1 are issued
+  // too (re-loading the last tile, into buffers no later phase reads; same WAR
+  // spacing as every other stage), so every wait is the same vmcnt(8) and the
+  // whole K tile is ONE basic block. With per-phase branches the scheduler
+  // sank every scaled fp8 MFMA of the tile past the phase barriers into the
+  // loop latch (gfx950 ISA), serialising the two wave groups;
+  // sched_barrier(0) in mma() then pins each quadrant inside its phase.
+  auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
   for (int t = 0; t < nk; ++t) {
     const uint8_t* buf = smem + (t & 1) * BUF;
-    const bool s1 = t + 1 < nk, s2 = t + 2 < nk;
-    const int phi = 4 * t;
     // p0
     read_a(buf, 0);
     read_b(buf, 0);
-    if (s1) stage_b(1, t + 1);
-    wait_dma(phi);
+    stage_b(1, t + 1);
+    wait_dma();
     barrier();
     mma(0, 0);
     barrier();
     // p1
     read_b(buf, 1);
-    if (s1) stage_a(1, t + 1);
-    wait_dma(phi + 1);
+    stage_a(1, t + 1);
+    wait_dma();
     barrier();
     mma(0, 1);
     barrier();
     // p2
     read_a(buf, 1);
-    if (s2) stage_a(0, t + 2);
-    wait_dma(phi + 2);
+    stage_a(0, t + 2);
+    wait_dma();
     barrier();
     mma(1, 1);
     barrier();
     // p3
-    if (s2) stage_b(0, t + 2);
-    wait_dma(phi + 3);
+    stage_b(0, t + 2);
+    wait_dma();
     barrier();
     mma(1, 0);
     barrier();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing stages land before the waves exit
   if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
   DTFS_STAMP(2);
 
