@@ -625,7 +625,7 @@ dtfs::runtime::FanoutStep make_fanout_step(torch::Tensor h2d_dst, uintptr_t ingr
 // {"h2d_dst": tensor, "h2d_lane": int, "ops": [dict, ...]} with op dicts
 //   {"kind": "kernels", "lane": l, "seq": KernelSequence | None, "graph_exec": int}
 //   {"kind": "alltoall" | "allgather" | "reduce_scatter", "lane": l, "comm": RcclComm, "send": t, "recv": t}
-//   {"kind": "record" | "wait", "lane": l, "event": k}
+//   {"kind": "record" | "wait" | "wait_prev", "lane": l, "event": k}
 // Message sizes come from the tensors (validated here, once).
 dtfs::runtime::StepProgram program_from(const py::dict& d, std::vector<py::object>* keep) {
   keep->push_back(d);
@@ -643,8 +643,10 @@ dtfs::runtime::StepProgram program_from(const py::dict& d, std::vector<py::objec
       op.kind = dtfs::runtime::ProgOp::kKernels;
       if (o.contains("seq") && !o["seq"].is_none()) op.seq = &o["seq"].cast<dtfs::runtime::KernelSequence&>();
       if (o.contains("graph_exec")) op.graph = reinterpret_cast<hipGraphExec_t>(o["graph_exec"].cast<uintptr_t>());
-    } else if (kind == "record" || kind == "wait") {
-      op.kind = kind == "record" ? dtfs::runtime::ProgOp::kRecord : dtfs::runtime::ProgOp::kWait;
+    } else if (kind == "record" || kind == "wait" || kind == "wait_prev") {
+      op.kind = kind == "record" ? dtfs::runtime::ProgOp::kRecord
+                : kind == "wait" ? dtfs::runtime::ProgOp::kWait
+                                 : dtfs::runtime::ProgOp::kWaitPrev;
       op.event = o["event"].cast<int>();
     } else {
       auto& c = o["comm"].cast<dtfs::comm::RcclComm&>();
@@ -782,7 +784,7 @@ class GpuBackend : public dtfs::runtime::StepBackend {
     const int64_t nbytes = batch.used_bytes;
     if (s.program) {
       if (nbytes > s.h2d_cap) throw std::runtime_error("batch larger than the device arena");
-      runner_->launch_program(slot, s.prog, arena, nbytes);
+      runner_->launch_program(slot, s.prog, arena, nbytes, batch.n_gpu_varint == 0);
     } else if (s.fanout) {
       dtfs::runtime::FanoutStep f = s.fan;
       f.h2d_src = arena;

@@ -175,7 +175,7 @@ LoopStats ServingLoop::run(int64_t n, bool record) {
       const LoopSlot& s = slots_[size_t(slot)];
       const int64_t nbytes = b.n_valid > 0 ? b.used_bytes : 0;
       if (s.program) {
-        runner_->launch_program(slot, s.prog, in.arena, nbytes);
+        runner_->launch_program(slot, s.prog, in.arena, nbytes, b.n_gpu_varint == 0);
       } else if (s.fanout) {
         FanoutStep f = s.fan;
         f.h2d_src = in.arena;

@@ -176,6 +176,7 @@ void StepProgram::validate() const {
         break;
       case ProgOp::kRecord:
       case ProgOp::kWait:
+      case ProgOp::kWaitPrev:
         if (o.event < 0 || o.event >= kProgEvents) throw std::invalid_argument("program: event index out of range");
         break;
       default:
@@ -187,20 +188,25 @@ void StepProgram::validate() const {
     } else if (o.kind == ProgOp::kWait) {
       if (!recorded[o.event]) throw std::invalid_argument("program: event waited before it is recorded");
       if (o.lane == 0) joined = std::max(joined, covers[o.event]);
-    } else if (o.lane == 1) {
+    } else if (o.kind != ProgOp::kWaitPrev && o.lane == 1) {
       ++aux_ops;
     }
   }
   if (joined < aux_ops) throw std::invalid_argument("program: aux-lane work is not joined into the compute lane");
 }
 
-void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes) {
+void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes,
+                                bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
   ensure_fanout_streams();  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
-    for (auto& e : prog_ev_) ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(program)");
+    // lane-to-lane dependencies stay on the device: no system-scope release
+    // (a system-fenced marker between two kernels of a step measured a 7-22 us
+    // bubble on MI355X, bench/step_timeline.py)
+    for (auto& e : prog_ev_)
+      ck(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate(program)");
   }
   hipStream_t lanes[2] = {compute_, ingress_};
   // WAR on the slot's buffers + the H2D of the request bytes (one copy stream:
@@ -211,7 +217,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
     hipStream_t st = lanes[o.lane];
     switch (o.kind) {
       case ProgOp::kKernels:
-        if (o.seq) o.seq->launch(st);
+        if (o.seq) o.seq->launch(st, nullptr, false, skip_varint);
         else ck(hipGraphLaunch(o.graph, st), "hipGraphLaunch(program)");
         break;
       case ProgOp::kAllToAll:
@@ -229,10 +235,18 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
       case ProgOp::kWait:
         ck(hipStreamWaitEvent(st, ev[o.event], 0), "hipStreamWaitEvent(program)");
         break;
+      case ProgOp::kWaitPrev:
+        // the previous step recorded this event before this launch (the host
+        // launches steps in order), and its slot is not reused before this one
+        if (last_prog_slot_ >= 0)
+          ck(hipStreamWaitEvent(st, prog_ev_[size_t(last_prog_slot_) * kProgEvents + o.event], 0),
+             "hipStreamWaitEvent(program prev)");
+        break;
     }
   }
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
   used_[slot] = 1;
+  last_prog_slot_ = slot;
 }
 
 void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph) {

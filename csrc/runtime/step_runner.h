@@ -72,6 +72,10 @@ struct ProgOp {
     kReduceScatter = 3,  // comm: bf16 sum, send (W x elems) -> recv (`bytes` = elems)
     kRecord = 4,         // record per-slot event `event` on the lane
     kWait = 5,           // lane waits for per-slot event `event`
+    kWaitPrev = 6,       // lane waits for event `event` of the PREVIOUS programmed step (any slot;
+                         // no-op for the first): cross-step overlap, e.g. step k+1's gather
+                         // starts when step k's first GEMM is done, so it shares the CUs with
+                         // step k's smaller GEMMs instead of delaying the big one
   };
   int kind = kKernels;
   int lane = 0;  // 0 compute, 1 aux
@@ -112,7 +116,9 @@ class StepRunner {
   // Enqueue one fan-out step (see FanoutStep).
   void launch_fanout(int slot, const FanoutStep& s);
   // Enqueue one programmed step (see StepProgram).
-  void launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes);
+  // skip_varint: no request of the step has packed varint ids (see launch_seq)
+  void launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes,
+                      bool skip_varint = false);
   // Block until the slot's last step has finished (scores are on the host).
   void wait(int slot);
   // Bounded wait: false when the step has not finished within timeout_us or a
@@ -145,6 +151,7 @@ class StepRunner {
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
   std::vector<hipEvent_t> prog_ev_;  // [slot * kProgEvents + k], created on first program launch
+  int last_prog_slot_ = -1;
   // H2D gate (DTFS_H2D_GATE = k, default 0 = off): step k+1's H2D waits until
   // step k's first k kernels (the embedding gather) have run, so the DMA
   // overlaps the GEMMs instead of the latency-bound gather it slows ~2x

@@ -91,6 +91,39 @@ class CTRModel(nn.Module):
             raise NotImplementedError(f"{self.family} reads dense features; unpack the arena first")
         return self._forward(ops.ArenaRows(arena, int(B), self.cfg.num_fields), None, out)
 
+    # families whose step is "gather (+ FM / wide terms) -> MLP -> head" can run
+    # as a two-lane program that overlaps consecutive steps (local_step_program)
+    supports_overlap = False
+
+    def local_step_program(self, arena: torch.Tensor, B: int, out: torch.Tensor, decode, state: dict):
+        """One local (no fan-out) step as a two-lane program
+        (parallel/step_program.py): the gather - K0 fused into K1, reading the
+        request arena - on the aux lane, the MLP GEMMs + head on the compute
+        lane. Step k+1's gather waits for step k's FIRST GEMM only, so it runs
+        on the CUs next to step k's smaller GEMMs and head (the big GEMM holds
+        every CU's registers; the gather is memory-latency bound) instead of
+        after them. ``decode`` runs the arena's GPU varint decode."""
+        from ..parallel import step_program as sp
+
+        rows = ops.ArenaRows(arena, int(B), self.cfg.num_fields)
+        mlp = self.mlp
+
+        def front():
+            decode()
+            state["x"], state["extra"] = self._front(rows, None)
+
+        def back1():
+            state["h"] = mlp.layers[0](state["x"])
+
+        def back2():
+            state["scores"] = mlp.forward_head(state["h"], self.head_w, self.head_b, extra=state["extra"], out=out,
+                                               start=1)
+
+        return [sp.Sync("wait_prev", sp.AUX, 1), sp.Kernels(sp.AUX, front, "gather"),
+                sp.Sync("record", sp.AUX, 0), sp.Sync("wait", sp.COMPUTE, 0),
+                sp.Kernels(sp.COMPUTE, back1, "gemm1"), sp.Sync("record", sp.COMPUTE, 1),
+                sp.Kernels(sp.COMPUTE, back2, "mlp+head")]
+
 
 class WideDeep(CTRModel):
     family = "wdl"
@@ -107,9 +140,14 @@ class WideDeep(CTRModel):
                                    requires_grad=False)
         self.head_b = 0.0
 
+    supports_overlap = True
+
+    def _front(self, ids, wts):
+        return ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
+                         want_x=True, want_fm=True, fm2=False)
+
     def _forward(self, ids, wts, out=None):
-        x, wide = ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
-                            want_x=True, want_fm=True, fm2=False)
+        x, wide = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide, out=out)
 
 
@@ -128,9 +166,14 @@ class DeepFM(CTRModel):
                                    requires_grad=False)
         self.head_b = 0.0
 
+    supports_overlap = True
+
+    def _front(self, ids, wts):
+        return ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
+                         want_x=True, want_fm=True, fm2=True)
+
     def _forward(self, ids, wts, out=None):
-        x, fm = ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
-                          want_x=True, want_fm=True, fm2=True)
+        x, fm = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm, out=out)
 
 

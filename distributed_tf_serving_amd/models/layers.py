@@ -137,14 +137,16 @@ class MLP(nn.Module):
 
     def forward_head(self, x: torch.Tensor, head_w: torch.Tensor, head_b: float,
                      extra: Optional[torch.Tensor] = None, sigmoid: bool = True,
-                     out: Optional[torch.Tensor] = None, xq=None) -> torch.Tensor:
+                     out: Optional[torch.Tensor] = None, xq=None, start: int = 0) -> torch.Tensor:
         """MLP then CTR head. On the GPU the last layer and the head run as one
         kernel (ops.linear_head) whenever its shape allows; it writes ``out``
         (device or pinned host memory) directly. (Fusing the last TWO layers
         as well streams both weights through every 64-row block: measured
         48.0 us vs 34.5 us for GEMM + fused head at 16384 rows on MI355X -
-        weight-load latency bound - so that fusion is not used.)"""
-        for k, layer in enumerate(self.layers[:-1]):
+        weight-load latency bound - so that fusion is not used.)
+        ``start``: x is already the output of layers[:start] (a step split
+        after its first GEMM, CTRModel.local_step_program)."""
+        for k, layer in enumerate(self.layers[start:-1], start):
             x = layer(x, xq if k == 0 else None)
         last = self.layers[-1]
         if x.is_cuda and not last.fp8 and last.act in ("relu", "none") and ops.linear_head_ok(x, last.weight):

@@ -101,7 +101,7 @@ class StepHandle:
 class FanoutEngine:
     def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
                  step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None,
-                 native_fanout: bool = True, force_fanout: bool = False):
+                 native_fanout: bool = True, force_fanout: bool = False, overlap: Optional[bool] = None):
         """``ingest="packed"``: the host decodes into packed rows (host_in) and
         the H2D moves rows. ``ingest="arena"``: the host only parses request
         framing into a request arena (serving/arena.py); the H2D moves the raw
@@ -135,6 +135,12 @@ class FanoutEngine:
         self._programs: Dict[Tuple[int, int], object] = {}
         self._prog_bufs: Dict[Tuple[int, int], dict] = {}
         self.program_active = False
+        # local steps as cross-step overlapped two-lane programs (CTRModel.
+        # local_step_program). Opt-in (DTFS_OVERLAP=1): interleaved A/B on one
+        # MI355X (bench/step_timeline.py) - step k+1's gather co-running with
+        # step k's smaller GEMMs slows the fused head 12.6 -> 61 us, so the step
+        # period is 176-182 us vs 174-175 us serial (profiles/step_overlap.md)
+        self.overlap = (os.environ.get("DTFS_OVERLAP", "0") == "1") if overlap is None else bool(overlap)
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
@@ -250,9 +256,14 @@ class FanoutEngine:
 
     # -- programmed steps (embedding-parallel models) ------------------------------
     def _program_enabled(self) -> bool:
-        return (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"
-                and getattr(self.ex.model, "supports_program", False)
-                and os.environ.get("DTFS_STEP_PROGRAM", "1") != "0")
+        if not (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"):
+            return False
+        m = self.ex.model
+        if getattr(m, "supports_program", False):  # embedding-parallel: the exchange is the program
+            return os.environ.get("DTFS_STEP_PROGRAM", "1") != "0"
+        # cross-step overlap of gather and GEMMs (CTRModel.local_step_program)
+        return (self.overlap and getattr(m, "supports_overlap", False) and self.ex.use_graphs
+                and os.environ.get("DTFS_ARENA_UNPACK", "0") != "1")
 
     def _capture_program(self, B: int, slot: int) -> None:
         """Build and capture the step program of one (bucket, slot): GPU unpack
@@ -267,10 +278,15 @@ class FanoutEngine:
         buf = self.ex.input_buffer(B, slot)
         arena_dev = self.dev_arena(slot)
         h_out = self.host_out(B, slot)
-        bufs = self._prog_bufs[key] = model.alloc(B)
+        bufs = self._prog_bufs[key] = model.alloc(B) if hasattr(model, "alloc") else {}
         state: dict = {}
-        ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
-        ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B], state=state)
+        if getattr(model, "supports_program", False):
+            ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
+            ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B],
+                                       state=state)
+        else:
+            ops = model.local_step_program(arena_dev, B, h_out[:B], lambda: self.arena.decode_varints(arena_dev),
+                                           state)
         # warm-up: one eager run (collective on every rank, like the capture below)
         sp.run_eager(ops, self.group)
         torch.cuda.synchronize(self.dev)

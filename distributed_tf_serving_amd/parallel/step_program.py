@@ -52,7 +52,7 @@ class Coll:
 
 @dataclass
 class Sync:
-    kind: str  # "record" | "wait"
+    kind: str  # "record" | "wait" | "wait_prev" (the event of the previous step, any slot)
     lane: int
     event: int
 
@@ -75,7 +75,7 @@ def validate(ops: Sequence[Op]) -> None:
                     raise ValueError("event waited before it is recorded")
                 if o.lane == COMPUTE:
                     joined = max(joined, covers[o.event])
-            else:
+            elif o.kind != "wait_prev":
                 raise ValueError(f"unknown sync {o.kind!r}")
         elif o.lane == AUX:
             aux_ops += 1
