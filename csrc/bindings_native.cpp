@@ -648,6 +648,7 @@ PYBIND11_MODULE(_native, m) {
     dtfs_live::def_live_methods(c);
   }
   m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
+  m.attr("STATUS_CALLER_PATH") = int(runtime::kCallerPath);
   m.def(
       "narrow_ids",
       [](torch::Tensor ids, int64_t modulo) {

@@ -32,6 +32,7 @@ inline LiveConfig live_config_from(const py::dict& d) {
   if (get("model_name")) c.model_name = d["model_name"].cast<std::string>();
   if (get("signature_name")) c.signature_name = d["signature_name"].cast<std::string>();
   if (get("output_key")) c.output_key = d["output_key"].cast<std::string>();
+  if (get("caller_outputs")) c.caller_outputs = d["caller_outputs"].cast<std::vector<std::string>>();
   if (get("version")) c.version = d["version"].cast<int64_t>();
   if (get("max_batch_rows")) c.max_batch_rows = d["max_batch_rows"].cast<int64_t>();
   if (get("batch_timeout_us")) c.batch_timeout_us = d["batch_timeout_us"].cast<int64_t>();

@@ -101,8 +101,12 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   if (!v.signature_name.empty() && v.signature_name != cfg_.signature_name)
     return reject(kInvalidArgument, "Serving signature name: \"" + v.signature_name +
                                         "\" not found in signature def of model " + cfg_.model_name);
-  for (const auto& k : v.output_filter)
-    if (k != cfg_.output_key) return reject(kInvalidArgument, "output tensor alias not found in signature: " + k);
+  for (const auto& k : v.output_filter) {
+    if (k == cfg_.output_key) continue;
+    if (std::find(cfg_.caller_outputs.begin(), cfg_.caller_outputs.end(), k) != cfg_.caller_outputs.end())
+      return reject(kCallerPath, "output " + k + " is produced by the general path");
+    return reject(kInvalidArgument, "output tensor alias not found in signature: " + k);
+  }
   const wire::TensorView* ti = v.find(cfg_.ids_key);
   const wire::TensorView* tw = v.find(cfg_.wts_key);
   if (!ti || !tw)

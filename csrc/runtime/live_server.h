@@ -51,6 +51,10 @@ enum StatusCode : int {
   // not a gRPC code: the request has more rows than one batch holds; the
   // caller may split it and resubmit the parts (serving/batching.py does)
   kOversize = 1000,
+  // not a gRPC code: the request asks for an output the fast path does not
+  // produce (LiveConfig::caller_outputs, e.g. the ranked outputs); the
+  // caller's general path serves it (serving/service.py)
+  kCallerPath = 1001,
 };
 
 struct Reply {
@@ -108,6 +112,10 @@ struct LiveConfig {
   // ids -> int32 rows (id mod narrow_modulo: the model's table size), weights
   // -> bf16. Halves the H2D bytes; other encodings travel raw.
   int64_t narrow_modulo = 0;
+  // output keys the signature has besides output_key that only the caller's
+  // general path produces: a request naming one in output_filter gets
+  // kCallerPath instead of INVALID_ARGUMENT
+  std::vector<std::string> caller_outputs;
 };
 
 struct LiveStats {

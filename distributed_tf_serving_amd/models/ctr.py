@@ -54,7 +54,9 @@ class CTRModel(nn.Module):
         F = self.cfg.num_fields
         return {
             "inputs": {"feat_ids": ("DT_INT64", [-1, F]), "feat_wts": ("DT_FLOAT", [-1, F])},
-            "outputs": {"prediction_node": ("DT_FLOAT", [-1])},
+            # ranked outputs: produced when named in output_filter (serving/service.py)
+            "outputs": {"prediction_node": ("DT_FLOAT", [-1]), "sorted_prediction": ("DT_FLOAT", [-1]),
+                        "sorted_index": ("DT_INT64", [-1])},
             "method_name": "tensorflow/serving/predict",
         }
 

@@ -85,7 +85,8 @@ class LiveScheduler:
             depth=depth, varint_chunks=self.layout.varint_chunks,
             max_pending=max(64, sc.max_queued_rows // max(1, min(self.buckets))),
             lockstep=lockstep, max_steps=max_steps, step_timeout_us=int(step_timeout_s * 1e6),
-            start_paused=start_paused, narrow_modulo=self.narrow_modulo)
+            start_paused=start_paused, narrow_modulo=self.narrow_modulo,
+            caller_outputs=["sorted_prediction", "sorted_index"])  # service.RANKED_OUTPUTS
         if engine.cuda:
             from ..ops import hip
 
@@ -102,6 +103,7 @@ class LiveScheduler:
             self.srv = native().LiveServer(self.config, self.step_rows, scores, self.arenas, forward)
         self.max_rows = int(self.srv.max_rows)
         self.OVERSIZE = int(native().STATUS_OVERSIZE)
+        self.CALLER_PATH = int(native().STATUS_CALLER_PATH)
 
     # -- fast path: serialized request in, serialized response out -------------
     def predict_raw(self, data: bytes, timeout_s: Optional[float] = None):

@@ -3,7 +3,12 @@
 All five RPCs are implemented against the model registry:
 
 ``Predict``          inputs feat_ids / feat_wts [B, F] -> outputs prediction_node [B]
-                     (the only RPC the reference client calls, DCNClient.java:111-112)
+                     (the only RPC the reference client calls, DCNClient.java:111-112);
+                     on request (output_filter) also the RANKED outputs
+                     sorted_prediction [B] (ascending, the reference client's
+                     Collections.sort, DCNClient.java:195) and sorted_index [B]
+                     (the candidate permutation the reference loses), computed
+                     by the K7 bitonic sort kernel on the servable's GPU
 ``Classify``         tf.Example list -> per example {label "click", score}
 ``Regress``          tf.Example list -> per example CTR value
 ``MultiInference``   several classify/regress tasks over one Example list
@@ -29,6 +34,11 @@ from .errors import Code, ServingError
 from .registry import CLASSIFY_METHOD, PREDICT_METHOD, REGRESS_METHOD, ModelRegistry, Servable
 
 CLICK_LABEL = "click"
+# ranked outputs: produced only when named in output_filter (an empty filter
+# returns prediction_node alone - unlike TF's "all outputs" - so the hot path
+# never pays for a sort)
+SORTED_SCORES, SORTED_INDEX = "sorted_prediction", "sorted_index"
+RANKED_OUTPUTS = (SORTED_SCORES, SORTED_INDEX)
 
 
 def _dt(name: str) -> int:
@@ -64,8 +74,28 @@ class PredictionServiceImpl:
 
     def _check_filter(self, s: Servable, flt) -> None:
         for k in flt:
-            if k != s.output_key:
+            if k != s.output_key and k not in RANKED_OUTPUTS:
                 raise ServingError(Code.INVALID_ARGUMENT, f"output tensor alias not found in signature: {k}")
+
+    def _outputs(self, s: Servable, flt, scores: torch.Tensor) -> List[Tuple[str, torch.Tensor]]:
+        """(key, tensor) pairs of a Predict response: prediction_node unless the
+        filter names only other outputs, plus the requested ranked outputs
+        (K7 on the servable's device: ops.sort_scores)."""
+        flt = list(flt)
+        out = []
+        if not flt or s.output_key in flt:
+            out.append((s.output_key, scores))
+        if any(k in RANKED_OUTPUTS for k in flt):
+            from .. import ops
+
+            dev = getattr(getattr(s.model, "device_", None), "type", "cpu")
+            src = scores.to(s.model.device_) if dev == "cuda" else scores
+            srt, perm = ops.sort_scores(src.float())
+            if SORTED_SCORES in flt:
+                out.append((SORTED_SCORES, srt.cpu()))
+            if SORTED_INDEX in flt:
+                out.append((SORTED_INDEX, perm.cpu().to(torch.int64)))
+        return out
 
     # ------------------------------------------------------------------ Predict (bytes, native codec)
     def predict_async_bytes(self, data: bytes, timeout_s: Optional[float] = None) -> Tuple[cf.Future, object]:
@@ -91,17 +121,20 @@ class PredictionServiceImpl:
             raise ServingError(Code.INVALID_ARGUMENT, f"{s.ids_key} must be DT_INT64 or DT_INT32")
         rows = int(shape[0])
 
+        flt = list(req.output_filter)
+
         def fill(ids_v, wts_v, req=req, s=s):
             req.decode_into(s.ids_key, ids_v, 0, 0)
             req.decode_into(s.wts_key, wts_v, 0, 0)
 
         fut = s.scheduler.submit(rows, fill, self._deadline_us(timeout_s))
-        return fut, (s, req.signature_name)
+        return fut, (s, req.signature_name, flt)
 
     def encode_predict(self, ctx, scores: torch.Tensor, raw: bool = False) -> bytes:
-        s, sig = ctx
+        s, sig = ctx[0], ctx[1]
+        flt = ctx[2] if len(ctx) > 2 else ()
         return self.nat.encode_predict_response(s.name, sig or "serving_default", s.version,
-                                                [(s.output_key, scores.contiguous())], raw)
+                                                [(k, t.contiguous()) for k, t in self._outputs(s, flt, scores)], raw)
 
     def _live_fast(self):
         """The live scheduler when exactly one servable is loaded (the common
@@ -118,8 +151,8 @@ class PredictionServiceImpl:
             code, msg, resp = live.predict_raw(data, t)
             if code == 0:
                 return resp
-            # NOT_FOUND / oversize: the general path resolves or splits
-            if code not in (Code.NOT_FOUND, live.OVERSIZE):
+            # NOT_FOUND / oversize / ranked outputs: the general path resolves, splits or sorts
+            if code not in (Code.NOT_FOUND, live.OVERSIZE, live.CALLER_PATH):
                 raise ServingError(Code(code) if code in Code._value2member_map_ else Code.UNKNOWN, msg)
         fut, ctx = self.predict_async_bytes(data, timeout_s)
         return self.encode_predict(ctx, self._wait(fut, timeout_s))
@@ -139,7 +172,8 @@ class PredictionServiceImpl:
         scores = self._score(s, ids, wts, timeout_s)
         resp = pb.PredictResponse()
         self._spec_out(resp.model_spec, s, request.model_spec.signature_name)
-        resp.outputs[s.output_key].CopyFrom(T.make_tensor_proto(scores.numpy()))
+        for key, t in self._outputs(s, request.output_filter, scores):
+            resp.outputs[key].CopyFrom(T.make_tensor_proto(t.numpy()))
         return resp
 
     def _score(self, s: Servable, ids: np.ndarray, wts: np.ndarray, timeout_s=None) -> torch.Tensor:

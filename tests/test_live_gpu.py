@@ -99,3 +99,20 @@ def test_deadline_exceeded_reported(server):
     synth = SyntheticRequests(fields=F, seed=1)
     code, msg, _ = live.predict_raw(synth.serialized(64), 1e-6)
     assert code in (0, Code.DEADLINE_EXCEEDED)
+
+
+def test_ranked_outputs_use_gpu_sort(server):
+    """A request naming the ranked outputs leaves the live fast path and is
+    served with the K7 bitonic sort on the GPU: sorted scores ascending and
+    the candidate permutation, consistent with prediction_node."""
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=8)
+    ids, wts = synth.arrays(1500)  # the reference request size
+    data = native().encode_predict_request("DCN", "serving_default", None,
+                                           [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                           True, ["prediction_node", "sorted_prediction", "sorted_index"])
+    resp = pb.PredictResponse.FromString(server.service.predict_bytes(data, 30.0))
+    got = T.to_ndarray(resp.outputs["prediction_node"])
+    srt = T.to_ndarray(resp.outputs["sorted_prediction"])
+    perm = T.to_ndarray(resp.outputs["sorted_index"])
+    assert got.shape == (1500,) and sorted(perm.tolist()) == list(range(1500))
+    assert np.all(np.diff(srt) >= 0) and np.array_equal(srt, got[perm])

@@ -244,3 +244,45 @@ def test_prometheus_metrics(server):
     assert val(':tensorflow:serving:request_latency_count{API="Predict"}') >= 2
     assert val(':tensorflow:serving:rows_served_total{model_name="DCN",version="1"}') >= 1
     assert val(':tensorflow:serving:batching_avg_batch_rows{model_name="DCN",version="1"}') > 0
+
+
+def test_predict_ranked_outputs(server):
+    """output_filter naming the ranked outputs: sorted_prediction ascending
+    (the reference client's Collections.sort, DCNClient.java:195) and the
+    candidate permutation it loses, over gRPC (bytes path) and in-process
+    (message path); the live fast path routes such requests to the general
+    path; unknown outputs stay INVALID_ARGUMENT."""
+    srv, port = server
+    rng = np.random.default_rng(3)
+    ids = rng.integers(0, 1 << 40, (37, 43))
+    wts = rng.random((37, 43), dtype=np.float32)
+    req = pb.PredictRequest()
+    req.model_spec.name = "DCN"
+    req.inputs["feat_ids"].CopyFrom(T.make_tensor_proto(ids))
+    req.inputs["feat_wts"].CopyFrom(T.make_tensor_proto(wts))
+    want = _expected(srv, ids, wts).numpy()
+    req.output_filter.extend(["prediction_node", "sorted_prediction", "sorted_index"])
+    be = GrpcBackend(f"127.0.0.1:{port}")
+    try:
+        for resp in (pb.PredictResponse.FromString(be.predict(req.SerializeToString(), 30)),
+                     srv.service.predict(req)):
+            got = T.to_ndarray(resp.outputs["prediction_node"])
+            srt = T.to_ndarray(resp.outputs["sorted_prediction"])
+            perm = T.to_ndarray(resp.outputs["sorted_index"])
+            assert np.allclose(got, want, atol=1e-6)
+            assert perm.dtype == np.int64 and sorted(perm.tolist()) == list(range(37))
+            assert np.all(np.diff(srt) >= 0) and np.array_equal(srt, got[perm])
+        only = pb.PredictRequest()
+        only.CopyFrom(req)
+        del only.output_filter[:]
+        only.output_filter.append("sorted_index")
+        resp = pb.PredictResponse.FromString(be.predict(only.SerializeToString(), 30))
+        assert list(resp.outputs.keys()) == ["sorted_index"]
+        bad = pb.PredictRequest()
+        bad.CopyFrom(req)
+        bad.output_filter.append("nope")
+        with pytest.raises(grpc.RpcError) as ei:
+            be.predict(bad.SerializeToString(), 30)
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    finally:
+        be.close()
