@@ -47,13 +47,17 @@ class ModelConfig:
     num_dense: int = 13               # dlrm: leading fields carried as dense values
     bottom_mlp: Tuple[int, ...] = (512, 256, 64)   # dlrm bottom MLP (last = embed_dim)
     table_rows: int = 1_000_000       # dlrm: rows per sparse table
+    multi_hot: int = 1                # dlrm: ids per sparse table (> 1: weighted sum-pooled bag, K1b)
     param_dtype: str = "bf16"         # storage dtype of embeddings + dense weights
     gemm_dtype: str = "bf16"          # bf16 | fp8 (dcn_v2 towers on CDNA4 fp8 MFMA)
     seed: int = 1234
 
     @property
     def num_sparse(self) -> int:
-        return self.num_fields - self.num_dense if self.family == "dlrm" else self.num_fields
+        """Sparse tables (dlrm: the fields after the dense ones, ``multi_hot`` per table)."""
+        if self.family == "dlrm":
+            return (self.num_fields - self.num_dense) // max(1, self.multi_hot)
+        return self.num_fields
 
 
 @dataclass

@@ -309,10 +309,16 @@ class DLRM(CTRModel):
                                    requires_grad=False)
         self.head_b = 0.0
         rows = cfg.table_rows
+        self.hot = max(1, int(cfg.multi_hot))
+        if cfg.num_dense + T * self.hot != cfg.num_fields:
+            raise ValueError(f"dlrm: {cfg.num_fields} fields != {cfg.num_dense} dense + {T} tables x {self.hot} ids")
         self.register_buffer("modulo_f", torch.full((T,), rows, dtype=torch.int64, device=self.device_),
                              persistent=False)
         self.register_buffer("offset_f", torch.arange(T, dtype=torch.int64, device=self.device_) * rows,
                              persistent=False)
+        # multi-hot: per id column (table t owns columns t*hot .. t*hot + hot - 1)
+        self.register_buffer("col_mod", self.modulo_f.repeat_interleave(self.hot), persistent=False)
+        self.register_buffer("col_off", self.offset_f.repeat_interleave(self.hot), persistent=False)
         self.emb = None
         if materialize_tables:
             t = torch.empty(T * rows, D, dtype=self.dtype, device=self.device_)
@@ -333,11 +339,23 @@ class DLRM(CTRModel):
     def sparse_ids(self, ids: torch.Tensor) -> torch.Tensor:
         return ids[:, self.cfg.num_dense:].contiguous()
 
-    def lookup(self, ids: torch.Tensor) -> torch.Tensor:
-        """Local (single-process) lookup of every sparse field -> [B, T, D]."""
+    def lookup(self, ids: torch.Tensor, wts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Local (single-process) lookup of every sparse table -> [B, T, D].
+        One-hot: the K1 gather. Multi-hot (``cfg.multi_hot`` ids per table):
+        ids hashed onto global table rows (K0), then the K1b bag kernel sums
+        each table's ``hot`` rows weighted by their feat_wts."""
+        B = ids.shape[0]
         sp = self.sparse_ids(ids)
-        x, _ = ops.embed(self.emb, sp, None, modulo_f=self.modulo_f, offset_f=self.offset_f, want_x=True)
-        return x.view(ids.shape[0], self.T, self.cfg.embed_dim)
+        if self.hot == 1:
+            x, _ = ops.embed(self.emb, sp, None, modulo_f=self.modulo_f, offset_f=self.offset_f, want_x=True)
+            return x.view(B, self.T, self.cfg.embed_dim)
+        rows = ops.pack_ids(sp, modulo_f=self.col_mod, offset_f=self.col_off)  # int32 [B, T*hot]
+        w = None
+        if wts is not None:
+            w = wts[:, self.cfg.num_dense:].float().contiguous().view(-1)
+        offsets = torch.arange(0, B * self.T * self.hot + 1, self.hot, dtype=torch.int64, device=rows.device)
+        pooled = ops.embedding_bag(self.emb, rows.view(-1), offsets, per_sample_weights=w, out_bf16=True)
+        return pooled.view(B, self.T, self.cfg.embed_dim)
 
     def interact_and_top(self, dense_out: torch.Tensor, emb: torch.Tensor, out=None) -> torch.Tensor:
         z = ops.dot_interaction(dense_out, emb, self.inter_cols)
@@ -345,7 +363,7 @@ class DLRM(CTRModel):
 
     def _forward(self, ids, wts, out=None):
         dense_out = self.bottom(self.dense_input(wts))
-        emb = self.lookup(ids)
+        emb = self.lookup(ids, wts)
         return self.interact_and_top(dense_out, emb, out=out)
 
 

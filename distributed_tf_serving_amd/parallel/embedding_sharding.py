@@ -366,6 +366,8 @@ class ShardedDLRM(nn.Module):
                  policy: str = "auto", budget_bytes: int = int(0.8 * MI355X_HBM_BYTES), group=None):
         super().__init__()
         self.cfg, self.ctx, self.group = cfg, ctx, group
+        if int(getattr(cfg, "multi_hot", 1)) != 1:
+            raise NotImplementedError("sharded DLRM tables are one-hot (multi-hot bags run unsharded)")
         world = ctx.world if ctx.is_distributed else 1
         self.plan = plan or plan_sharding(dlrm_tables(cfg), world, budget_bytes, policy)
         self.dense = DLRM(cfg, device=device, materialize_tables=False)

@@ -85,3 +85,28 @@ def test_sharded_dlrm_one_rank_cpu(policy):
         assert kinds == ["allgather", "reduce_scatter"]
     else:
         assert kinds == ["alltoall", "allgather", "alltoall", "reduce_scatter"]
+
+
+def test_dlrm_multi_hot_bag_matches_manual_pooling():
+    """Multi-hot DLRM (K1b): table t's `hot` ids are hashed onto its rows and
+    sum-pooled with their feat_wts; checked against explicit row gathers."""
+    cfg = ModelConfig(family="dlrm", num_fields=13 + 15 * 2, num_dense=13, table_rows=1009, embed_dim=64,
+                      multi_hot=2, bottom_mlp=(32, 64), mlp_dims=(64, 32))
+    m = build_model(cfg)
+    assert m.T == 15 and m.hot == 2
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 10 ** 12, (6, cfg.num_fields), generator=g)
+    wts = torch.rand(6, cfg.num_fields, generator=g)
+    got = m.lookup(ids, wts).float()
+    want = torch.zeros(6, 15, 64)
+    for b in range(6):
+        for t in range(15):
+            for h in range(2):
+                c = 13 + 2 * t + h
+                row = t * 1009 + int(ids[b, c]) % 1009
+                want[b, t] += m.emb[row].float() * wts[b, c]
+    assert (got - want).abs().max().item() < 2e-2  # bf16 pooled output
+    y = m(ids, wts)
+    assert y.shape == (6,) and torch.isfinite(y).all()
+    with pytest.raises(ValueError):
+        build_model(ModelConfig(family="dlrm", num_fields=42, num_dense=13, multi_hot=2))

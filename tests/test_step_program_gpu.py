@@ -129,3 +129,18 @@ def test_local_overlap_program(cuda, family):
     for k in range(7):
         B = (512, 2048)[k % 2]
         assert eng.self_check(B, seed=k, slot=k % S)
+
+
+def test_dlrm_multi_hot_gpu_matches_cpu(cuda):
+    """K1b bag kernel inside the multi-hot DLRM forward: GPU vs the fp32 CPU
+    model with the same weights."""
+    cfg = ModelConfig(family="dlrm", num_fields=13 + 15 * 2, num_dense=13, table_rows=50_021, embed_dim=64,
+                      multi_hot=2, bottom_mlp=(512, 256, 64), mlp_dims=(1024, 512, 256))
+    gm, cm = build_model(cfg, cuda), build_model(cfg, "cpu")
+    cm.load_state_dict({k: v.detach().cpu() for k, v in gm.state_dict().items()})  # device RNG streams differ
+    g = torch.Generator().manual_seed(6)
+    ids = torch.randint(0, 1 << 40, (513, cfg.num_fields), generator=g)
+    wts = torch.rand(513, cfg.num_fields, generator=g)
+    got = gm(ids.to(cuda), wts.to(cuda)).float().cpu()
+    want = cm(ids, wts).float()
+    assert (got - want).abs().max().item() < 2e-2
