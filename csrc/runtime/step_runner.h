@@ -141,6 +141,7 @@ class StepRunner {
            bool gated = false);
   int n_copy_ = 1;
   bool copy_wait_always_ = false;
+  bool host_wait_h2d_ = true;  // DTFS_H2D_HOST_WAIT (default 1): local steps wait for their H2D on the host
   bool spin_wait_ = false;
   std::vector<hipStream_t> extra_copy_;  // more H2D streams, used round-robin with copy_
   uint64_t n_h2d_ = 0;
