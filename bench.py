@@ -260,8 +260,11 @@ def run_live(a, ctx, cfg, model, eng, B):
         live.close()  # finishes the fixed-length run (empty steps until max_steps)
     sync()
     window_s = r["window_us"] * 1e-6
-    if r["errors"] and rank == 0:
-        print(f"warning: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr)
+    if r["errors"]:
+        # a failed request means the server broke mid-run: the window no longer
+        # measures served scores, so no number is reported
+        print(f"rank {rank}: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr, flush=True)
+        raise SystemExit(3)
     lat = r["latency_us"]
     extra["p50_request_ms"], extra["p99_request_ms"] = pct(lat, 50), pct(lat, 99)
     extra["requests_failed"] = int(r["errors"])

@@ -21,6 +21,8 @@
 //     W panel run on one L2.
 // Epilogues: bias, ReLU, sigmoid, DCN-v2 cross (x0 * (acc + b) + xl), written
 // as bf16 or fp32.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -755,7 +757,7 @@ __device__ unsigned long long g_8ph_stamps[4096][8][4];
   } while (0)
 #endif
 
-template <bool FP8, typename OutT>
+template <bool FP8, typename OutT, bool PRE = false>
 __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
@@ -840,20 +842,28 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
 
   // fragments (bf16: [kk][tile] 8 x bf16, fp8: [tile] 32 x e4m3); both B
   // column halves stay in registers for the whole K tile (no B re-read)
-  bf16x8 fa[2][4], fb[2][2][2];
-  i32x8 xa[4], xb[2][2];
-  auto read_a = [&](const uint8_t* buf, int qm) {
+  // PRE: two A fragment sets - [0] holds A[qm0], [1] A[qm1] - and A[qm0] of
+  // the NEXT K tile is read in phase 3 (which reads nothing otherwise), so the
+  // LDS reads per phase are 4 / 4 / 8 / 8 instead of 12 / 4 / 8 / 0. Next
+  // tile's Aq0 was staged 5 phases before p3 and retired by p2's wait (RAW
+  // s + 5 holds); its restage (tile t + 3) is 3 phases after this read.
+  constexpr int NA = PRE ? 2 : 1;
+  bf16x8 fa[NA][2][4], fb[2][2][2];
+  i32x8 xa[NA][4], xb[2][2];
+  auto read_a_into = [&](const uint8_t* buf, int qm, int set) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 128 * wr + 64 * qm + 16 * i + fr;
       if constexpr (FP8) {
-        xa[i] = mx_frag(buf, row, fq);
+        xa[set][i] = mx_frag(buf, row, fq);
       } else {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
+        for (int kk = 0; kk < 2; ++kk)
+          fa[set][kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
       }
     }
   };
+  auto read_a = [&](const uint8_t* buf, int qm) { read_a_into(buf, qm, PRE ? qm : 0); };
   auto read_b = [&](const uint8_t* buf, int qn) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -876,17 +886,18 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
     __builtin_amdgcn_sched_barrier(0);
+    const int set = PRE ? qm : 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4& c = acc[4 * qm + i][2 * qn + j];
         if constexpr (FP8) {
-          c = mx_mfma(xb[qn][j], xa[i], c);
+          c = mx_mfma(xb[qn][j], xa[set][i], c);
         } else {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[kk][i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[set][kk][i], c, 0, 0, 0);
         }
       }
     __builtin_amdgcn_sched_barrier(0);
@@ -911,10 +922,11 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   // loop latch (gfx950 ISA), serialising the two wave groups;
   // sched_barrier(0) in mma() then pins each quadrant inside its phase.
   auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  if constexpr (PRE) read_a(smem, 0);  // tile 0's A[qm0] (landed: the prologue's wait + barrier)
   for (int t = 0; t < nk; ++t) {
     const uint8_t* buf = smem + (t & 1) * BUF;
     // p0
-    read_a(buf, 0);
+    if constexpr (!PRE) read_a(buf, 0);
     read_b(buf, 0);
     stage_b(1, t + 1);
     wait_dma();
@@ -936,6 +948,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     mma(1, 1);
     barrier();
     // p3
+    if constexpr (PRE) read_a(smem + ((t + 1) & 1) * BUF, 0);  // next tile's A[qm0] (dead data after the last)
     stage_b(0, t + 2);
     wait_dma();
     barrier();
@@ -950,12 +963,12 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   DTFS_STAMP(3);
 }
 
-template <bool FP8, typename OutT>
+template <bool FP8, typename OutT, bool PRE = false>
 static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, OutT* C, int64_t ldc, const bf16* X0, const bf16* XL, int64_t ldx, int M,
                        int N, int K, int epi, hipStream_t st) {
   const int grid = ((M + 255) / 256) * ((N + 255) / 256);
-  hipLaunchKernelGGL((gemm_8ph_kernel<FP8, OutT>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(A), lda,
+  hipLaunchKernelGGL((gemm_8ph_kernel<FP8, OutT, PRE>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(A), lda,
                      static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi);
 }
 
@@ -1145,6 +1158,7 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     return;
   }
   }
+  const bool pre_from_dispatch = variant == 0;  // an explicit 17 keeps the plain kernel (A/B, tests)
   if (variant == 0 && glds_ok) {
     // The five tile variants kept (round-1/2 interleaved A/B sweeps, bench/
     // microbench.py --variants; 11 other tilings measured slower everywhere were
@@ -1177,8 +1191,18 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     return;
   }
   // 256x256 8-phase (staggered wave groups, counted vmcnt)
-  if (variant == 17 && glds_ok) {
-    launch_8ph<FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+  // 17: the 8-phase kernel; 18: the same with the next tile's A[qm0] read in
+  // phase 3 (LDS reads per phase 4/4/8/8 instead of 12/4/8/0): 16384x1024x2752
+  // bf16 76.2-76.9 us vs 80.9-81.9 (interleaved, MI355X), so the default
+  // 8-phase pick (variant 0 -> 17) runs it unless DTFS_8PH_PRE=0
+  if ((variant == 17 || variant == 18) && glds_ok) {
+    static const bool pre_default = [] {
+      const char* e = std::getenv("DTFS_8PH_PRE");
+      return !(e && e[0] == '0');
+    }();
+    const bool pre = variant == 18 || (variant == 17 && pre_from_dispatch && pre_default);
+    if (pre) launch_8ph<FP8, OutT, true>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
+    else launch_8ph<FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;
   }
   if (variant == 14 && glds_ok) {

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -118,7 +119,21 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
   if (used_[slot] && (copy_wait_always_ || !observed_[slot].load(std::memory_order_acquire)))
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
   if (gated && last_gate_slot_ >= 0) ck(hipStreamWaitEvent(st, gate_[last_gate_slot_], 0), "hipStreamWaitEvent(gate)");
-  if (nbytes > 0) ck(hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, st), "hipMemcpyAsync(H2D)");
+  if (nbytes > 0) {
+    hipError_t e = hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, st);
+    if (e == hipErrorInvalidMemcpyDirection) {
+      // Seen once on MI355X (ROCm 7.2) after thousands of identical copies from
+      // the same pinned arena into the same device buffer: the runtime's
+      // pointer classification rejected the direction. Let it infer the
+      // direction from the pointers instead of failing the whole server.
+      (void)hipGetLastError();
+      static std::atomic<bool> warned{false};
+      if (!warned.exchange(true))
+        std::fprintf(stderr, "[step_runner] hipMemcpyAsync(H2D) returned invalid direction; retrying as hipMemcpyDefault\n");
+      e = hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyDefault, st);
+    }
+    ck(e, "hipMemcpyAsync(H2D)");
+  }
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
   if (host_wait_h2d_ && consumer == compute_ && nbytes > 0) {
     // The launcher thread waits for the copy instead of the compute queue:

@@ -131,7 +131,7 @@ def test_gemm_bf16(cuda, M, N, K, act):
     _close(yb, ref, 1e-2, 1e-2, "gemm bf16 out")
 
 
-@pytest.mark.parametrize("variant", [4, 8, 10, 14, 17])
+@pytest.mark.parametrize("variant", [4, 8, 10, 14, 17, 18])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 128), (8192, 1024, 2752), (1000, 2752, 2752),
                                    (16384, 512, 1024), (513, 1024, 192)])
 def test_gemm_variants_bf16(cuda, variant, M, N, K):
@@ -145,17 +145,18 @@ def test_gemm_variants_bf16(cuda, variant, M, N, K):
         _close(y, ops.linear(x, W, b, "relu", out_f32=True), 2e-3, 2e-3, f"v{variant} {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("variant", [17, 18])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (8192, 2752, 2752), (700, 1024, 2816)])
-def test_gemm_8phase_fp8(cuda, M, N, K):
+def test_gemm_8phase_fp8(cuda, M, N, K, variant):
     g = torch.Generator().manual_seed(M + N)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16)
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
     xq, sx = ops.quant_rows_fp8(x.to(cuda), ops.FP8_K_PAD)
     wq, sw = ops.quant_rows_fp8(W.to(cuda), ops.FP8_K_PAD)
     b = torch.randn(N, generator=g) * 0.1
-    y = ops.hip().gemm(xq, wq, b.to(cuda), 1, None, None, True, sx, sw, None, 17)
+    y = ops.hip().gemm(xq, wq, b.to(cuda), 1, None, None, True, sx, sw, None, variant)
     ref = ops.linear_fp8(xq.cpu(), sx.cpu(), wq.cpu(), sw.cpu(), b, "relu", out_f32=True)
-    _close(y, ref, 2e-3, 2e-3, "fp8 8-phase")
+    _close(y, ref, 2e-3, 2e-3, f"fp8 8-phase v{variant}")
 
 
 def test_gemm_layout_asymmetric(cuda):
