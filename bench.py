@@ -261,10 +261,7 @@ def run_live(a, ctx, cfg, model, eng, B):
     sync()
     window_s = r["window_us"] * 1e-6
     if r["errors"]:
-        # a failed request means the server broke mid-run: the window no longer
-        # measures served scores, so no number is reported
         print(f"rank {rank}: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr, flush=True)
-        raise SystemExit(3)
     lat = r["latency_us"]
     extra["p50_request_ms"], extra["p99_request_ms"] = pct(lat, 50), pct(lat, 99)
     extra["requests_failed"] = int(r["errors"])
@@ -399,10 +396,18 @@ def main():
     else:
         el, extra = run_replay(a, ctx, cfg, model, eng, B)
 
-    t = torch.tensor([el], dtype=torch.float64, device=dev if ctx.backend == "nccl" else "cpu")
+    t = torch.tensor([el, float(extra.get("requests_failed", 0))], dtype=torch.float64,
+                     device=dev if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el_max = float(t.item())
+    el_max, failed = float(t[0].item()), int(t[1].item())
+    if failed:
+        # a failed request means a server broke mid-run: the window no longer
+        # measures served scores, so no number is reported (every rank agrees)
+        if rank == 0:
+            print(f"error: requests failed during the timed run; no result", file=sys.stderr, flush=True)
+        shutdown()
+        raise SystemExit(3)
     total_scores = world * B * a.steps
     value = total_scores / el_max if el_max > 0 else 0.0
     if rank == 0:
