@@ -1050,6 +1050,44 @@ PYBIND11_MODULE(_hip, m) {
             c.allgather(send.data_ptr(), recv.data_ptr(), send.nbytes(), cur_stream(send));
           },
           py::arg("send"), py::arg("recv"))
+      .def(
+          "gather",
+          [](dtfs::comm::RcclComm& c, torch::Tensor send, torch::Tensor recv, int root) {
+            TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+                        "contiguous GPU tensors");
+            TORCH_CHECK(root >= 0 && root < c.nranks(), "bad root");
+            TORCH_CHECK(c.rank() != root || recv.nbytes() == send.nbytes() * c.nranks(), "root recv must be world x send");
+            c10::DeviceGuard g(send.device());
+            c.gather(send.data_ptr(), recv.data_ptr(), send.nbytes(), root, cur_stream(send));
+          },
+          py::arg("send"), py::arg("recv"), py::arg("root") = 0)
+      .def(
+          "scatter",
+          [](dtfs::comm::RcclComm& c, torch::Tensor send, torch::Tensor recv, int root) {
+            TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+                        "contiguous GPU tensors");
+            TORCH_CHECK(root >= 0 && root < c.nranks(), "bad root");
+            TORCH_CHECK(c.rank() != root || send.nbytes() == recv.nbytes() * c.nranks(), "root send must be world x recv");
+            c10::DeviceGuard g(recv.device());
+            c.scatter(send.data_ptr(), recv.data_ptr(), recv.nbytes(), root, cur_stream(recv));
+          },
+          py::arg("send"), py::arg("recv"), py::arg("root") = 0)
+      .def(
+          "peer_prepare", [](dtfs::comm::RcclComm& c, uint64_t cap) { return py::bytes(c.peer_prepare(cap)); },
+          py::arg("cap"),
+          "Allocate and export this rank's one-shot exchange mailbox (collective setup, step 1); returns its IPC handle")
+      .def(
+          "peer_enable",
+          [](dtfs::comm::RcclComm& c, std::vector<py::bytes> handles, double timeout_s) {
+            std::vector<std::string> h;
+            for (auto& b : handles) h.emplace_back(std::string(b));
+            c.peer_enable(h, timeout_s);
+          },
+          py::arg("handles"), py::arg("timeout_s") = 5.0,
+          "Map every rank's mailbox (handles in rank order); messages <= cap then bypass RCCL")
+      .def_property_readonly("peer_enabled", &dtfs::comm::RcclComm::peer_enabled)
+      .def_property_readonly("peer_cap", &dtfs::comm::RcclComm::peer_cap)
+      .def_property_readonly("peer_exchanges", &dtfs::comm::RcclComm::peer_exchanges)
       .def("async_error", &dtfs::comm::RcclComm::async_error)
       .def("abort", &dtfs::comm::RcclComm::abort)
       .def_property_readonly("aborted", &dtfs::comm::RcclComm::aborted);

@@ -16,7 +16,9 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <vector>
 
 namespace dtfs {
 namespace comm {
@@ -50,6 +52,18 @@ class RcclComm {
   // rank contributes a non-zero row, so the bf16 sum is exact.
   void reduce_scatter_bf16(const void* send, void* recv, size_t elems, hipStream_t st);
 
+  // One-shot peer exchange (csrc/kernels/peer.hip): alltoall / scatter /
+  // gather / allgather messages of at most `cap` bytes per peer go through
+  // IPC-mapped mailboxes in ONE kernel per rank instead of RCCL. Setup is
+  // collective: every rank calls peer_prepare (allocates and exports its
+  // mailbox), the handles are exchanged out of band (torch.distributed), then
+  // every rank calls peer_enable with all handles in rank order.
+  std::string peer_prepare(uint64_t cap);
+  void peer_enable(const std::vector<std::string>& handles, double timeout_s);
+  bool peer_enabled() const { return peer_ && peer_->enabled; }
+  uint64_t peer_cap() const { return peer_ ? peer_->cap : 0; }
+  uint64_t peer_exchanges() const { return peer_ ? peer_->count : 0; }
+
   // "" when healthy, else the asynchronous RCCL error (failure detection).
   std::string async_error();
   // Abort in-flight operations (a peer died / a deadline passed); the
@@ -59,6 +73,23 @@ class RcclComm {
 
  private:
   void check(ncclResult_t r, const char* what);
+  struct Peer {
+    uint64_t cap = 0;
+    bool enabled = false;
+    uint64_t count = 0;
+    double timeout_s = 5.0;
+    uint8_t* box = nullptr;               // own mailbox
+    std::vector<uint8_t*> boxes;          // every rank's, mapped (own one local)
+    std::vector<bool> opened;             // which were opened from an IPC handle
+    void* ctl = nullptr;                  // PeerCtl, device memory
+    int* err_host = nullptr;              // mapped pinned word set by a timed-out kernel
+    int* err_dev = nullptr;
+  };
+  // true when the exchange went through the mailboxes
+  bool peer_run(const void* const* src, void* const* dst, const uint64_t* send_bytes, const uint64_t* recv_bytes,
+                hipStream_t st);
+  void peer_release();
+  std::unique_ptr<Peer> peer_;
   ncclComm_t comm_ = nullptr;
   int nranks_ = 1, rank_ = 0, device_ = 0;
   bool aborted_ = false;

@@ -6,6 +6,7 @@ after that the fan-out collectives are issued from C++ by the StepRunner
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -15,20 +16,51 @@ from ..ops import hip
 from .dist import DistContext
 
 
-def create_comm(ctx: DistContext, group=None):
+def peer_cap_from_env() -> int:
+    """``DTFS_PEER_COMM``: 0 / unset = RCCL only; 1 = one-shot peer exchange for
+    messages up to 64 KiB per peer; N > 1 = up to N bytes per peer."""
+    v = int(os.environ.get("DTFS_PEER_COMM", "0") or 0)
+    return 0 if v <= 0 else (64 << 10 if v == 1 else v)
+
+
+def create_comm(ctx: DistContext, group=None, peer_cap: Optional[int] = None, peer_timeout_s: float = 5.0):
     """A new RcclComm over the ranks of ``group`` (default: the world).
+
+    ``peer_cap`` > 0 (default: ``peer_cap_from_env()``) also sets up the
+    one-shot peer exchange (csrc/kernels/peer.hip): messages of at most that
+    many bytes per peer then go through IPC-mapped mailboxes in one kernel
+    instead of RCCL (latency-bound score gathers).
 
     Collective: every rank of the group must call it, in the same order."""
     h = hip()
     dev = ctx.device.index if ctx.device.index is not None else torch.cuda.current_device()
+    cap = peer_cap_from_env() if peer_cap is None else int(peer_cap)
     if not (ctx.world > 1 and dist.is_initialized()):
-        return h.RcclComm(h.rccl_unique_id(), 1, 0, dev)
+        c = h.RcclComm(h.rccl_unique_id(), 1, 0, dev)
+        if cap > 0:
+            c.peer_enable([c.peer_prepare(cap)], peer_timeout_s)
+        return c
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     obj = [h.rccl_unique_id() if rank == 0 else None]
     src = 0 if group is None else dist.get_global_rank(group, 0)
     dist.broadcast_object_list(obj, src=src, group=group)
-    return h.RcclComm(obj[0], world, rank, dev)
+    c = h.RcclComm(obj[0], world, rank, dev)
+    if cap > 0:
+        enable_peer(c, cap, group, peer_timeout_s)
+    return c
+
+
+def enable_peer(comm, cap: int, group=None, timeout_s: float = 5.0) -> None:
+    """Collective: export every rank's mailbox, exchange the IPC handles over
+    torch.distributed, map them. After it, every rank's exchanges of at most
+    ``cap`` bytes per peer run as one peer.hip kernel."""
+    mine = comm.peer_prepare(int(cap))
+    handles = [None] * comm.nranks
+    dist.all_gather_object(handles, mine, group=group)
+    comm.peer_enable(handles, timeout_s)
+    # every rank has mapped every mailbox before anyone pushes into one
+    dist.barrier(group=group)
 
 
 def check_comms(*comms) -> Optional[str]:
