@@ -417,6 +417,8 @@ def main():
         else:
             par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
                    + (", native C++ step" if eng.native_fanout_active else ", torch.distributed")
+                   + (f", one-shot peer exchange for messages <= {eng._cin.peer_cap} B per peer"
+                      if getattr(eng, "_cin", None) is not None and eng._cin.peer_enabled else "")
                    + (f", {eng.layout.row_bytes} B rows: int32 table rows + bf16 weights" if eng.layout.narrow
                       else f", {eng.layout.row_bytes} B rows: raw int64 ids + fp32 weights") + ")")
         if hasattr(model, "plan"):
