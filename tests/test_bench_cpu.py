@@ -20,7 +20,7 @@ def _free_port() -> int:
 
 
 def _run_bench(n: int, extra=()):
-    args = ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--requests-per-gpu", "1",
+    args = ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--prime-steps", "0", "--requests-per-gpu", "1",
             "--request-rows", "64", "--pool", "2", "--client-threads", "2", *extra]
     if n == 1:
         cmd = [sys.executable, *args]

@@ -22,15 +22,19 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,mode", [(2, "alltoall"), (3, "alltoall"), (2, "scatter"), (2, "local")])
-def test_bench_ranks_sharing_one_gpu(n, mode):
+@pytest.mark.parametrize("n,mode,peer", [(2, "alltoall", 0), (3, "alltoall", 0), (2, "scatter", 0), (2, "local", 0),
+                                         (3, "alltoall", 262144), (2, "scatter", 262144)])
+def test_bench_ranks_sharing_one_gpu(n, mode, peer):
+    """peer > 0: the fan-out's exchanges of at most that many bytes per peer go
+    through the one-shot peer kernel (csrc/kernels/peer.hip) instead of RCCL."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
-           "--steps", "20", "--warmup", "4", "--requests-per-gpu", "4", "--request-rows", "96", "--mode", mode,
+           "--steps", "20", "--warmup", "4", "--prime-steps", "10", "--requests-per-gpu", "4", "--request-rows", "96", "--mode", mode,
            "--pool", "8", "--client-threads", "2", "--qps", "0", "--step-timeout-s", "20"]
-    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
+               DTFS_PEER_COMM=str(peer))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -39,10 +43,11 @@ def test_bench_ranks_sharing_one_gpu(n, mode):
     assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
     if mode != "local":
         assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
+        assert ("one-shot peer exchange" in out["config"]["parallelism"]) == (peer > 0), out["config"]["parallelism"]
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n):
+@pytest.mark.parametrize("n,peer", [(2, 0), (3, 0), (3, 1 << 20)])
+def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
     """BASELINE config 4 shape on N ranks: DLRM tables sharded table-wise over
     the ranks, every step a native two-lane step program (ids all-to-all ->
     owner gather -> embeddings all-to-all on the aux lane, bottom MLP on the
@@ -51,10 +56,11 @@ def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n):
         pytest.skip("no GPU")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
-           "--model", "dlrm", "--table-rows", "1000000", "--steps", "20", "--warmup", "4",
+           "--model", "dlrm", "--table-rows", "1000000", "--steps", "20", "--warmup", "4", "--prime-steps", "10",
            "--requests-per-gpu", "4", "--request-rows", "96", "--pool", "8", "--client-threads", "2",
            "--qps", "0", "--step-timeout-s", "20"]
-    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
+               DTFS_PEER_COMM=str(peer))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -63,3 +69,4 @@ def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n):
     assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
     par = out["config"]["parallelism"]
     assert f"embedding-mp{n}" in par and "native two-lane step program" in par, par
+    assert ("one-shot peer exchange" in par) == (peer > 0), par
