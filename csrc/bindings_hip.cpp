@@ -552,6 +552,44 @@ std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x, int64_t k_pad) {
   return {q, s};
 }
 
+// z = x0 * y + xl (+ fp8 quantisation of z, + head dot): the split DCN-v2 cross layer's combine pass
+std::vector<torch::Tensor> cross_combine(torch::Tensor y, torch::Tensor x0, torch::Tensor xl, bool want_z,
+                                         int64_t k_pad, c10::optional<torch::Tensor> head_w) {
+  check_dev(y, "y");
+  for (auto* t : {&y, &x0, &xl})
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->dim() == 2 && t->is_contiguous() &&
+                    t->sizes() == y.sizes() && t->device() == y.device(),
+                "y, x0, xl must be contiguous bf16 [M, N] on one device");
+  const int64_t M = y.size(0), N = y.size(1);
+  TORCH_CHECK(N % 8 == 0 && N <= 4096, "N must be a multiple of 8 and <= 4096");
+  TORCH_CHECK(k_pad >= 0 && k_pad <= 256, "k_pad must be in [0, 256] (0 = no quantisation)");
+  c10::DeviceGuard g(y.device());
+  torch::Tensor z, q, s, dot;
+  if (want_z) z = torch::empty({M, N}, y.options());
+  int64_t Kq = 0;
+  if (k_pad > 0) {
+    Kq = (N + k_pad - 1) / k_pad * k_pad;
+    TORCH_CHECK(Kq % 16 == 0, "padded K must be a multiple of 16");
+    q = torch::empty({M, Kq}, y.options().dtype(torch::kFloat8_e4m3fn));
+    s = torch::empty({M}, y.options().dtype(torch::kFloat32));
+  }
+  const float* hw = nullptr;
+  if (head_w && head_w->defined()) {
+    TORCH_CHECK(head_w->scalar_type() == torch::kFloat32 && head_w->numel() == N && head_w->is_contiguous() &&
+                    head_w->device() == y.device(),
+                "head_w must be fp32 [N] on y's device");
+    hw = head_w->data_ptr<float>();
+    dot = torch::empty({M}, y.options().dtype(torch::kFloat32));
+  }
+  TORCH_CHECK(want_z || k_pad > 0 || hw, "nothing to produce");
+  check_hip(dtfs::launch_cross_combine(y.data_ptr(), x0.data_ptr(), xl.data_ptr(), N, int(M), int(N),
+                                       want_z ? z.data_ptr() : nullptr, N, k_pad > 0 ? q.data_ptr() : nullptr, Kq,
+                                       k_pad > 0 ? s.data_ptr<float>() : nullptr, int(Kq), hw,
+                                       hw ? dot.data_ptr<float>() : nullptr, cur_stream(y)),
+            "cross_combine");
+  return {z, q, s, dot};
+}
+
 // ---------------------------------------------------------------- K7
 std::vector<torch::Tensor> sort_scores(torch::Tensor s, bool descending, int64_t k) {
   check_dev(s, "scores");
@@ -880,6 +918,9 @@ PYBIND11_MODULE(_hip, m) {
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
+  m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,
+        py::arg("k_pad") = 0, py::arg("head_w") = py::none(),
+        "split DCN-v2 cross layer: z = x0*y + xl, optionally quantised (e4m3 + row scale) and/or dotted with head_w");
   m.def("unpack_arena", &unpack_arena, py::arg("arena"), py::arg("packed"), py::arg("fields"),
         py::arg("narrow_modulo") = 0);
   m.def("arena_varint_decode", &arena_varint_decode, py::arg("arena"), py::arg("blocks") = 256);

@@ -1173,7 +1173,10 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     //  *  4: otherwise (narrow N): 64x64 LDS-DMA
     // K not a multiple of one 128-byte K tile: the register-staged gemm_kernel.
     if (M <= 1024) variant = 8;
-    else if (blocks(256, 256) >= 256 && N % 256 == 0) variant = 17;
+    // ragged N (2752) with a PLAIN fp8 epilogue (the split DCN-v2 cross GEMM):
+    // 8-phase 124.7 us vs 147.6 us for 14 at 16384 x 2752 x 2816 (81.6 vs 84.0
+    // at 8192 rows, bench/cross_split.py); with the cross epilogue 14 stays ahead
+    else if (blocks(256, 256) >= 256 && (N % 256 == 0 || (FP8 && (epi & 15) != EPI_CROSS))) variant = 17;
     else if (blocks(128, 128) >= 512) variant = 14;
     else if (blocks(128, 64) >= 512) variant = 10;  // 8192 x 512: 15.5 us vs 16.9 (64x64)
     else variant = 4;

@@ -200,9 +200,106 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const bf16* __restrict_
   }
 }
 
+// DCN-v2 cross combine, the second half of a split cross layer: the GEMM
+// writes y = xl W^T + b (plain bf16 epilogue, so the big 8-phase tile can run
+// it), then one wave per row computes z = x0 * y + xl (fp32, rounded to bf16)
+// and, in the same pass over the row,
+//   * writes z (the next layer's xl) and/or
+//   * quantises z to e4m3 with a per-row scale (the next layer's fp8 operand,
+//     zero-padded to Kq columns; same rounding as quant_rows_kernel) and/or
+//   * reduces dot[m] = z . head_w (the last layer: z never reaches memory).
+// Measured at 16384 x 2752 x 2816 fp8 (bench/cross_split.py, MI355X): fused
+// cross epilogue 215.6 us + quant_rows 22.8 us vs plain 8-phase GEMM 124.7 us
+// + a 360 MB elementwise pass ~63 us.
+template <int MAXC>
+__global__ void __launch_bounds__(256) cross_combine_kernel(const bf16* __restrict__ y, const bf16* __restrict__ x0,
+                                                            const bf16* __restrict__ xl, int64_t ld, int M, int N,
+                                                            bf16* __restrict__ z, int64_t ldz, uint8_t* __restrict__ q,
+                                                            int64_t ldq, float* __restrict__ scale, int Kq,
+                                                            const float* __restrict__ head_w, float* __restrict__ dot) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int nch = N / 8;
+  float v[MAXC][8];
+  float amax = 0.f, acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      const int64_t o = int64_t(m) * ld + ch * 8;
+      const bf16x8 ty = *reinterpret_cast<const bf16x8*>(y + o);
+      const bf16x8 t0 = *reinterpret_cast<const bf16x8*>(x0 + o);
+      const bf16x8 tl = *reinterpret_cast<const bf16x8*>(xl + o);
+      bf16x8 tz;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        tz[j] = f2bf(bf2f(t0[j]) * bf2f(ty[j]) + bf2f(tl[j]));
+        v[c][j] = bf2f(tz[j]);  // quantise / reduce exactly what the next layer would read back
+        amax = fmaxf(amax, fabsf(v[c][j]));
+      }
+      if (z) *reinterpret_cast<bf16x8*>(z + int64_t(m) * ldz + ch * 8) = tz;
+      if (head_w) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(head_w + ch * 8);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(head_w + ch * 8 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += v[c][j] * w0[j] + v[c][j + 4] * w1[j];
+      }
+    }
+  }
+  if (head_w) {
+    acc = wave_sum(acc);
+    if (lane == 0) dot[m] = acc;
+  }
+  if (!q) return;
+  for (int ch = nch + lane; ch < Kq / 8; ch += 64) *reinterpret_cast<int2*>(q + m * ldq + ch * 8) = make_int2(0, 0);
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (lane == 0) scale[m] = s;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      int lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * inv, v[c][1] * inv, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * inv, v[c][3] * inv, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4] * inv, v[c][5] * inv, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][6] * inv, v[c][7] * inv, hi, true);
+      *reinterpret_cast<int2*>(q + m * ldq + ch * 8) = make_int2(lo, hi);
+    }
+  }
+}
+
 }  // namespace kern
 
 using namespace kern;
+
+hipError_t launch_cross_combine(const void* y, const void* x0, const void* xl, int64_t ld, int M, int N, void* z,
+                                int64_t ldz, void* q, int64_t ldq, float* scale, int Kq, const float* head_w,
+                                float* dot, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (N % 8 || ld < N || (z && ldz < N) || (q && (Kq % 8 || Kq < N || ldq < Kq || !scale)) || (head_w && !dot))
+    return hipErrorInvalidValue;
+  const int chunks = (N / 8 + 63) / 64;
+  dim3 grid((M + 3) / 4), block(256);
+  const bf16* yi = static_cast<const bf16*>(y);
+  const bf16* x0i = static_cast<const bf16*>(x0);
+  const bf16* xli = static_cast<const bf16*>(xl);
+  bf16* zo = static_cast<bf16*>(z);
+  uint8_t* qo = static_cast<uint8_t*>(q);
+#define CC_CASE(C)                                                                                              \
+  case C:                                                                                                      \
+    hipLaunchKernelGGL(cross_combine_kernel<C>, grid, block, 0, st, yi, x0i, xli, ld, M, N, zo, ldz, qo, ldq, scale, \
+                       Kq, head_w, dot);                                                                       \
+    break;
+  switch (chunks) {
+    CC_CASE(1) CC_CASE(2) CC_CASE(3) CC_CASE(4) CC_CASE(5) CC_CASE(6) CC_CASE(7) CC_CASE(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef CC_CASE
+  return hipGetLastError();
+}
 
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
                            void* out_x, int64_t ldo, const float* head_w, float* out_dot, hipStream_t st) {

@@ -123,6 +123,13 @@ hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, c
 hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void* q, int64_t ldq, float* scale,
                                  hipStream_t st, int Kq = 0);
 
+// K3b split: z = x0 * y + xl per row (bf16 [M, N], row stride ld), optionally
+// written (z), quantised to e4m3 + per-row scale with zero K padding to Kq (q,
+// scale), and/or reduced against head_w (dot[m] = z . head_w).
+hipError_t launch_cross_combine(const void* y, const void* x0, const void* xl, int64_t ld, int M, int N, void* z,
+                                int64_t ldz, void* q, int64_t ldq, float* scale, int Kq, const float* head_w,
+                                float* dot, hipStream_t st);
+
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();
 hipError_t launch_sort_scores(const float* in, int n, bool descending, float* out, int64_t* perm, int k_out,

@@ -246,6 +246,12 @@ class DCNv2(CTRModel):
         # (profiles/dcn_v2_mx_chain.md) - the 22 us quant pass it removes costs
         # less than the block-scale epilogue + MX operand path it adds.
         self.mx_chain = os.environ.get("DTFS_MX_CHAIN", "0") == "1"
+        # Split cross layers (fp8 full rank): plain-epilogue GEMM y = xl W^T + b
+        # (the 8-phase tile runs it) + one combine pass that writes z = x0*y + xl,
+        # quantises it for the next layer and, for the last layer, reduces the
+        # cross logit instead of writing z (ops.cross_combine). DTFS_CROSS_SPLIT=0:
+        # fused cross epilogue + separate quant_rows / head passes.
+        self.cross_split = os.environ.get("DTFS_CROSS_SPLIT", "1") == "1"
 
     def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None, emit_mx: int = 0):
         """One cross layer. fp8: ``xq`` = (q, row scales | None, MX block scales
@@ -273,17 +279,28 @@ class DCNv2(CTRModel):
         q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
         nq = -(-self.d // ops.FP8_K_PAD) * ops.FP8_K_PAD
         chain = fp8_full and self.mx_chain and self.d % ops.MX_BLOCK == 0 and nq <= ops.MX_MAX_K
-        xl, xq = x0, ((*q0, None) if q0 is not None else None)
         L = self.cfg.num_cross_layers
-        for i in range(L):
-            emit = nq if (chain and i < L - 1) else 0
-            r = self._cross_layer(i, x0, xl, xq, emit)
-            if emit:
-                xl, q, sq = r
-                xq = (q, None, sq)
-            else:
-                xl, xq = r, None
-        cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
+        if fp8_full and self.cross_split and not chain and self.d % 8 == 0 and L > 0:
+            xl, (q, sx) = x0, q0
+            for i in range(L):
+                layer = self.cross[i]
+                y = ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias)  # plain bf16 epilogue
+                last = i == L - 1
+                z, q, sx, cross_logit = ops.cross_combine(y, x0, xl, want_z=not last,
+                                                          k_pad=0 if last else ops.FP8_K_PAD,
+                                                          head_w=self.head_wc if last else None)
+                xl = z
+        else:
+            xl, xq = x0, ((*q0, None) if q0 is not None else None)
+            for i in range(L):
+                emit = nq if (chain and i < L - 1) else 0
+                r = self._cross_layer(i, x0, xl, xq, emit)
+                if emit:
+                    xl, q, sq = r
+                    xq = (q, None, sq)
+                else:
+                    xl, xq = r, None
+            cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
         mlp_q = q0 if (q0 is not None and self.mlp.layers[0].fp8 and self.mlp.layers[0].k == x0.shape[1]) else None
         return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out, xq=mlp_q)
 

@@ -237,6 +237,27 @@ def dequant_mx_fp8(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     return q.float() * torch.exp2(s.float() - 127).repeat_interleave(MX_BLOCK, dim=1)
 
 
+def cross_combine(y: torch.Tensor, x0: torch.Tensor, xl: torch.Tensor, want_z: bool = True, k_pad: int = 0,
+                  head_w: Optional[torch.Tensor] = None):
+    """Split DCN-v2 cross layer, second half: z = x0 * y + xl (bf16), in one pass
+    over the rows also quantised (``k_pad`` > 0: e4m3 + per-row scale, zero
+    padded to a multiple of k_pad - the next layer's fp8 operand) and/or dotted
+    with ``head_w`` (the last layer's cross logit). Returns (z, q, scale, dot),
+    None for what was not asked."""
+    if y.is_cuda:
+        z, q, s, d = hip().cross_combine(y.contiguous(), x0.contiguous(), xl.contiguous(), want_z, int(k_pad),
+                                         head_w)
+        return (z if want_z else None, q if k_pad else None, s if k_pad else None,
+                d if head_w is not None else None)
+    zb = (x0.float() * y.float() + xl.float()).to(torch.bfloat16)
+    q = s = d = None
+    if k_pad:
+        q, s = quant_rows_fp8(zb, k_pad)
+    if head_w is not None:
+        d = zb.float() @ head_w.float()
+    return (zb if want_z else None, q, s, d)
+
+
 def linear_fp8(xq: torch.Tensor, sx: Optional[torch.Tensor], Wq: torch.Tensor, sw: torch.Tensor,
                b: Optional[torch.Tensor] = None, act: str = "none", out_f32: bool = False,
                x0: Optional[torch.Tensor] = None, xl: Optional[torch.Tensor] = None,

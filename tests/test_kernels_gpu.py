@@ -270,6 +270,48 @@ def test_dcn_v2_fp8_mx_chain_matches_row_requant(cuda, monkeypatch):
     assert (a - b).abs().max().item() < 0.02
 
 
+@pytest.mark.parametrize("M,N", [(1, 8), (37, 264), (1000, 2752), (4099, 2752)])
+def test_cross_combine(cuda, M, N):
+    """Split cross layer combine pass: z = x0*y + xl, its e4m3 quantisation and
+    the head dot, against the CPU reference of the same op."""
+    g = torch.Generator().manual_seed(M + N)
+    y, x0, xl = (torch.randn(M, N, generator=g).to(torch.bfloat16) for _ in range(3))
+    hw = torch.randn(N, generator=g) * 0.05
+    z, q, s, d = ops.cross_combine(y.to(cuda), x0.to(cuda), xl.to(cuda), True, ops.FP8_K_PAD, hw.to(cuda))
+    zr, qr, sr, dr = ops.cross_combine(y, x0, xl, True, ops.FP8_K_PAD, hw)
+    torch.cuda.synchronize()
+    assert torch.equal(z.cpu(), zr)
+    _close(s, sr, 1e-6, 0, "scale")
+    assert q.shape == qr.shape
+    # x * (1/s) on the GPU vs x / s on the CPU: at most 1 e4m3 ulp apart (<= 1/8 relative)
+    _close(q.float(), qr.float(), 0.126, 1e-3, "q")
+    _close(d, dr, 1e-4, 1e-3, "dot")
+    # head-only form writes nothing else
+    z2, q2, s2, d2 = ops.cross_combine(y.to(cuda), x0.to(cuda), xl.to(cuda), False, 0, hw.to(cuda))
+    assert z2 is None and q2 is None and s2 is None
+    _close(d2, dr, 1e-4, 1e-3, "dot only")
+
+
+def test_dcn_v2_split_cross_matches_fused(cuda, monkeypatch):
+    """DCN-v2 fp8: split cross layers (plain GEMM + combine/quant/head pass) vs
+    the fused cross epilogue + quant_rows + head, same weights."""
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
+
+    cfg = ModelConfig(family="dcn_v2", vocab_size=20000, embed_dim=64, num_fields=43, mlp_dims=(1024, 512, 256),
+                      num_cross_layers=3, gemm_dtype="fp8")
+    m = build_model(cfg, cuda)
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 1 << 30, (4096, 43), generator=g).to(cuda)
+    wts = torch.rand(4096, 43, generator=g).to(cuda)
+    m.cross_split = True
+    a = m(ids, wts)
+    m.cross_split = False
+    b = m(ids, wts)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() < 0.02
+
+
 def test_cross_v2_epilogue(cuda):
     M, d = 130, 256
     x0 = torch.randn(M, d).to(torch.bfloat16)
