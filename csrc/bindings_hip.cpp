@@ -57,11 +57,27 @@ torch::Tensor pack_ids(torch::Tensor ids, int64_t modulo, c10::optional<torch::T
 }
 
 // ---------------------------------------------------------------- K1
+// k_pad > 0: the gather also writes x as e4m3 [B, K rounded up to k_pad] + a
+// per-row scale (the fp8 towers' first operand; replaces quant_rows_fp8(x)).
+static void embed_fp8_out(dtfs::EmbedArgs& a, const torch::Tensor& table, int64_t B, int64_t K, int64_t k_pad,
+                          torch::Tensor& q, torch::Tensor& qs) {
+  if (k_pad <= 0) return;
+  TORCH_CHECK(k_pad <= 256, "k_pad must be in [0, 256]");
+  const int64_t Kq = (K + k_pad - 1) / k_pad * k_pad;
+  TORCH_CHECK(Kq % 16 == 0 && a.F <= 64, "fp8 x needs F <= 64 and a padded K that is a multiple of 16");
+  q = torch::empty({B, Kq}, table.options().dtype(torch::kFloat8_e4m3fn));
+  qs = torch::empty({B}, table.options().dtype(torch::kFloat32));
+  a.out_q = q.data_ptr();
+  a.q_ld = Kq;
+  a.out_qs = qs.data_ptr<float>();
+}
+
 std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor ids,
                                  c10::optional<torch::Tensor> wts, int64_t modulo, c10::optional<torch::Tensor> modulo_f,
                                  c10::optional<torch::Tensor> offset_f, double bias, bool want_x, bool want_fm,
                                  bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables,
-                                 c10::optional<torch::Tensor> shard_lo_f, c10::optional<torch::Tensor> shard_n_f) {
+                                 c10::optional<torch::Tensor> shard_lo_f, c10::optional<torch::Tensor> shard_n_f,
+                                 int64_t k_pad) {
   check_dev(table, "table");
   TORCH_CHECK(ids.is_cuda(), "ids must be a GPU tensor");
   TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
@@ -150,15 +166,17 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
   a.x_ld = F * D;
   a.out_fm = want_fm ? fm.data_ptr<float>() : nullptr;
   a.fm2 = fm2 ? 1 : 0;
+  torch::Tensor q, qs;
+  embed_fp8_out(a, table, B, F * D, k_pad, q, qs);
   check_hip(dtfs::launch_embed(a, cur_stream(ids)), "embed");
-  return {x, fm};
+  return {x, fm, q, qs};
 }
 
 // K0+K1(+K2): the gather reads ids / weights straight from a device request
 // arena (csrc/runtime/arena.h) - no separate unpack kernel, no packed rows.
 std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor arena,
                                        int64_t B, int64_t F, int64_t modulo, double bias, bool want_x, bool want_fm,
-                                       bool fm2, c10::optional<torch::Tensor> out_x) {
+                                       bool fm2, c10::optional<torch::Tensor> out_x, int64_t k_pad) {
   check_dev(table, "table");
   check_dev(arena, "arena");
   check_same_dev(table, arena, "arena");
@@ -200,8 +218,10 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
   a.x_ld = F * D;
   a.out_fm = want_fm ? fm.data_ptr<float>() : nullptr;
   a.fm2 = fm2 ? 1 : 0;
+  torch::Tensor q, qs;
+  embed_fp8_out(a, table, B, F * D, k_pad, q, qs);
   check_hip(dtfs::launch_embed(a, cur_stream(table)), "embed_arena");
-  return {x, fm};
+  return {x, fm, q, qs};
 }
 
 // ---------------------------------------------------------------- K1b
@@ -892,10 +912,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("embed", &embed, py::arg("table"), py::arg("lin"), py::arg("ids"), py::arg("wts"), py::arg("modulo"),
         py::arg("modulo_f") = py::none(), py::arg("offset_f") = py::none(), py::arg("bias") = 0.0,
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
-        py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none());
+        py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none(),
+        py::arg("k_pad") = 0);
   m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
         py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
-        py::arg("fm2") = false, py::arg("out_x") = py::none());
+        py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0);
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
         py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
         py::arg("out_bf16") = false);

@@ -336,9 +336,12 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
       float s[8], q[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+      float amax = 0.f;
+      bf16x8 ox[MAXG];
 #pragma unroll
       for (int g = 0; g < MAXG; ++g) {
         const int f = g * FPI + sub;
+        ox[g] = bf16x8{};
         if (f < F) {
           bf16x8 o;
 #pragma unroll
@@ -347,9 +350,32 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
             s[j] += e;
             q[j] += e * e;
             o[j] = f2bf(e);
+            amax = fmaxf(amax, fabsf(bf2f(o[j])));
           }
+          ox[g] = o;
           if (out_x) *reinterpret_cast<bf16x8*>(out_x + int64_t(bk) * a.x_ld + int64_t(f) * D + dl) = o;
         }
+      }
+      if (a.out_q) {  // wave-uniform: the whole row is in this wave's registers
+        uint8_t* qrow = static_cast<uint8_t*>(a.out_q) + int64_t(bk) * a.q_ld;
+        amax = wave_max(amax);
+        const float sc = amax > 0.f ? amax / 448.f : 1.f;
+        const float inv = 1.f / sc;
+        if (lane == 0) a.out_qs[bk] = sc;
+#pragma unroll
+        for (int g = 0; g < MAXG; ++g) {
+          const int f = g * FPI + sub;
+          if (f < F) {
+            int lo = 0, hi = 0;
+            lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(ox[g][0]) * inv, bf2f(ox[g][1]) * inv, lo, false);
+            lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(ox[g][2]) * inv, bf2f(ox[g][3]) * inv, lo, true);
+            hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(ox[g][4]) * inv, bf2f(ox[g][5]) * inv, hi, false);
+            hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(ox[g][6]) * inv, bf2f(ox[g][7]) * inv, hi, true);
+            *reinterpret_cast<int2*>(qrow + int64_t(f) * D + dl) = make_int2(lo, hi);
+          }
+        }
+        for (int64_t c = int64_t(F) * D / 8 + lane; c < a.q_ld / 8; c += kWave)
+          *reinterpret_cast<int2*>(qrow + c * 8) = make_int2(0, 0);
       }
       if (a.out_fm) {
         const float logit = fm_row_logit<LPR>(s, q, lin_w[k], a.fm2 != 0, lane);
@@ -482,6 +508,7 @@ static void embed_pipe_dispatch(const EmbedArgs& a, dim3 grid, dim3 block, uint6
 template <int D>
 static void embed_dispatch(const EmbedArgs& a, hipStream_t st) {
   const int rows_per_block = 4;
+  if (a.out_q && !(a.F <= kWave && g_embed_waves > 0)) return;  // launch_embed rejects it first
   if (a.F <= kWave && g_embed_waves > 0) {
     const int waves = std::min((a.B + g_embed_rows - 1) / g_embed_rows, std::max(g_embed_waves, rows_per_block));
     dim3 grid((waves + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
@@ -499,6 +526,9 @@ static void embed_dispatch(const EmbedArgs& a, hipStream_t st) {
 
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st) {
   if (a.B == 0) return hipSuccess;
+  // fp8 x: pipelined kernel only (F <= 64), whole 8-byte chunks, room for F*D columns
+  if (a.out_q && (a.F > kWave || g_embed_waves <= 0 || !a.out_qs || a.q_ld < int64_t(a.F) * a.D || a.q_ld % 8))
+    return hipErrorInvalidValue;
   switch (a.D) {
     case 8: embed_dispatch<8>(a, st); break;
     case 16: embed_dispatch<16>(a, st); break;

@@ -47,6 +47,12 @@ struct EmbedArgs {
   int64_t x_ld = 0;
   float* out_fm = nullptr;         // fp32 [B]
   int fm2 = 0;
+  // fp8 copy of x for the fp8 towers (pipelined kernel, F <= 64 only): per-row
+  // e4m3 of the bf16-rounded x with scale amax / 448 (quant_rows_fp8's
+  // rounding), columns [F*D, q_ld) zeroed - saves a separate quant pass
+  void* out_q = nullptr;           // e4m3 [B, q_ld]
+  int64_t q_ld = 0;
+  float* out_qs = nullptr;         // fp32 [B]
 };
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 // Pipelined K1 kernel geometry: resident-wave cap (0 = one row per wave) and

@@ -106,7 +106,17 @@ void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool ski
       const hipMemcpy3DParms& c = op.mc;
       const char* src = static_cast<const char*>(c.srcPtr.ptr) + c.srcPos.x;
       char* dst = static_cast<char*>(c.dstPtr.ptr) + c.dstPos.x;
-      ck(hipMemcpyAsync(dst, src, c.extent.width, c.kind, st), "hipMemcpyAsync");
+      hipError_t e = hipMemcpyAsync(dst, src, c.extent.width, c.kind, st);
+      if (e == hipErrorInvalidMemcpyDirection && c.kind != hipMemcpyDefault) {
+        // Seen intermittently on MI355X (ROCm 7.2) under load for the same
+        // captured copy that succeeded thousands of times before (the runtime's
+        // pointer classification rejects the recorded direction; also seen on
+        // the step runner's H2D): let the runtime infer the direction from
+        // the pointers instead of failing every request of the server.
+        (void)hipGetLastError();
+        e = hipMemcpyAsync(dst, src, c.extent.width, hipMemcpyDefault, st);
+      }
+      ck(e, "hipMemcpyAsync");
     } else {
       const hipMemsetParams& m = op.ms;
       if (m.elementSize == 1) ck(hipMemsetD8Async(hipDeviceptr_t(m.dst), uint8_t(m.value), m.width, st), "memset");

@@ -183,8 +183,14 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   ck(hipStreamWaitEvent(egress_, fwd_done_[slot], 0), "hipStreamWaitEvent(egress)");
   if (s.mode == 0) s.cout->alltoall(s.scores, s.back, s.out_bytes, egress_);
   else s.cout->gather(s.scores, s.back, s.out_bytes, 0, egress_);
-  if (s.d2h_bytes > 0)
-    ck(hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_), "hipMemcpyAsync(D2H)");
+  if (s.d2h_bytes > 0) {
+    hipError_t e = hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_);
+    if (e == hipErrorInvalidMemcpyDirection) {  // the runtime quirk handled in h2d() above
+      (void)hipGetLastError();
+      e = hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDefault, egress_);
+    }
+    ck(e, "hipMemcpyAsync(D2H)");
+  }
   ck(hipEventRecord(done_[slot], egress_), "hipEventRecord(done)");
   used_[slot] = 1;
 }

@@ -252,6 +252,8 @@ class DCNv2(CTRModel):
         # cross logit instead of writing z (ops.cross_combine). DTFS_CROSS_SPLIT=0:
         # fused cross epilogue + separate quant_rows / head passes.
         self.cross_split = os.environ.get("DTFS_CROSS_SPLIT", "1") == "1"
+        # x0's fp8 copy written by the gather (DTFS_GATHER_QUANT=0: quant_rows pass)
+        self.gather_quant = os.environ.get("DTFS_GATHER_QUANT", "1") == "1"
 
     def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None, emit_mx: int = 0):
         """One cross layer. fp8: ``xq`` = (q, row scales | None, MX block scales
@@ -270,13 +272,16 @@ class DCNv2(CTRModel):
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
     def _forward(self, ids, wts, out=None):
-        x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
         # fp8 towers: x0 is quantised once, for the first cross layer AND the
-        # first MLP layer (both read it); each cross layer's epilogue hands the
-        # next one its output already in MX-fp8 (e4m3 + per-32 E8M0 scales), so
-        # the chain has no separate quantisation pass.
+        # first MLP layer (both read it) - by the gather itself, which holds each
+        # row in one wave's registers (ops.embed_fp8; no separate quant pass)
         fp8_full = self.fp8 and not self.low_rank
-        q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
+        if fp8_full and self.gather_quant and self.cfg.num_fields <= 64:
+            x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
+            q0 = tuple(q0)
+        else:
+            x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
+            q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
         nq = -(-self.d // ops.FP8_K_PAD) * ops.FP8_K_PAD
         chain = fp8_full and self.mx_chain and self.d % ops.MX_BLOCK == 0 and nq <= ops.MX_MAX_K
         L = self.cfg.num_cross_layers

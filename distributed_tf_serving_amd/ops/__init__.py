@@ -99,14 +99,14 @@ def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = 
             raise ValueError("arena rows support the shared-table gather only")
         if ids.arena.is_cuda:
             m = int(modulo) if modulo > 0 else table.shape[0]
-            x, fm = hip().embed_arena(table, lin, ids.arena, int(ids.B), int(ids.F), m, float(bias), want_x,
-                                      want_fm, fm2, out_x)
+            x, fm, _, _ = hip().embed_arena(table, lin, ids.arena, int(ids.B), int(ids.F), m, float(bias), want_x,
+                                            want_fm, fm2, out_x)
             return (x if want_x else None), (fm if want_fm else None)
         ids, wts = _arena_unpack_host(ids)
     if ids.is_cuda:
         if modulo_f is None and modulo <= 0:
             modulo = table.shape[0]
-        x, fm = hip().embed(table, lin, _rows(ids), None if wts is None else _rows(wts), int(modulo),
+        x, fm, _, _ = hip().embed(table, lin, _rows(ids), None if wts is None else _rows(wts), int(modulo),
                             modulo_f, offset_f, float(bias), want_x, want_fm, fm2, out_x, False, shard_lo_f, shard_n_f)
         return (x if want_x else None), (fm if want_fm else None)
     if shard_lo_f is not None:
@@ -139,6 +139,26 @@ def embed(table: torch.Tensor, ids: torch.Tensor, wts: Optional[torch.Tensor] = 
 
 
 # ------------------------------------------------------------------ K1b
+def embed_fp8(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: int, k_pad: int):
+    """Weighted gather that also returns x as the fp8 towers' first operand:
+    (x bf16 [B, F*D], q e4m3 [B, K padded to k_pad], per-row scale [B]) - the
+    same values as ``quant_rows_fp8(x, k_pad)``, written by the gather itself
+    (shared-table gather, F <= 64)."""
+    m = int(modulo) if modulo > 0 else table.shape[0]
+    if isinstance(ids, ArenaRows):
+        if ids.arena.is_cuda:
+            x, _, q, s = hip().embed_arena(table, None, ids.arena, int(ids.B), int(ids.F), m, 0.0, True, False,
+                                           False, None, int(k_pad))
+            return x, q, s
+    elif ids.is_cuda:
+        x, _, q, s = hip().embed(table, None, _rows(ids), None if wts is None else _rows(wts), m,
+                                 None, None, 0.0, True, False, False, None, False, None, None, int(k_pad))
+        return x, q, s
+    x, _ = embed(table, ids, wts, modulo=m, want_x=True)
+    q, s = quant_rows_fp8(x, k_pad)
+    return x, q, s
+
+
 def embedding_bag(table: torch.Tensor, indices: torch.Tensor, offsets: torch.Tensor,
                   per_sample_weights: Optional[torch.Tensor] = None, modulo: int = 0, mean: bool = False,
                   out_bf16: bool = False) -> torch.Tensor:

@@ -292,6 +292,23 @@ def test_cross_combine(cuda, M, N):
     _close(d2, dr, 1e-4, 1e-3, "dot only")
 
 
+@pytest.mark.parametrize("B,F,D", [(1, 43, 64), (4099, 43, 64), (300, 13, 32), (77, 64, 16)])
+def test_embed_fp8_matches_quant_rows(cuda, B, F, D):
+    """The gather's own e4m3 copy of x == quant_rows_fp8(x) (same rounding,
+    same K padding) and x itself is unchanged."""
+    g = torch.Generator().manual_seed(B + F + D)
+    table = torch.randn(5000, D, generator=g).to(torch.bfloat16).to(cuda)
+    ids = torch.randint(0, 1 << 40, (B, F), generator=g).to(cuda)
+    wts = torch.rand(B, F, generator=g).to(cuda)
+    x, q, sc = ops.embed_fp8(table, ids, wts, 5000, ops.FP8_K_PAD)
+    xr, _ = ops.embed(table, ids, wts, modulo=5000, want_x=True)
+    qr, sr = ops.quant_rows_fp8(xr, ops.FP8_K_PAD)
+    torch.cuda.synchronize()
+    assert torch.equal(x, xr)
+    assert torch.equal(sc, sr)
+    assert q.shape == qr.shape and torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+
+
 def test_dcn_v2_split_cross_matches_fused(cuda, monkeypatch):
     """DCN-v2 fp8: split cross layers (plain GEMM + combine/quant/head pass) vs
     the fused cross epilogue + quant_rows + head, same weights."""
