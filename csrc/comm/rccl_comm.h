@@ -58,6 +58,9 @@ class RcclComm {
   // collective: every rank calls peer_prepare (allocates and exports its
   // mailbox), the handles are exchanged out of band (torch.distributed), then
   // every rank calls peer_enable with all handles in rank order.
+  // Like the RCCL collectives, one communicator's exchanges must be issued in
+  // the same order on every rank and stream-ordered (one stream per
+  // communicator): the sequence number advances kernel by kernel.
   std::string peer_prepare(uint64_t cap);
   void peer_enable(const std::vector<std::string>& handles, double timeout_s);
   bool peer_enabled() const { return peer_ && peer_->enabled; }
