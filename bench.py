@@ -92,6 +92,9 @@ def parse_args():
     ap.add_argument("--request-rows", type=int, default=512, help="candidates per client request (config batch)")
     ap.add_argument("--requests-per-gpu", type=int, default=32,
                     help="requests per GPU batch (32 x 512 = 16384 rows = the preset's max batch)")
+    ap.add_argument("--peer-comm", type=int, default=None,
+                    help="one-shot peer exchange (csrc/kernels/peer.hip) for fan-out / step-program messages of at "
+                         "most this many bytes per peer (1 = 64 KiB, 0 = RCCL only; default: $DTFS_PEER_COMM or 0)")
     ap.add_argument("--mode", default=None, choices=["alltoall", "scatter", "local"],
                     help="N > 1: alltoall = every request fanned out over all GPUs (config 3, default); local = "
                          "one independent replica per GPU (default for dlrm: its tables are sharded instead and "
@@ -389,6 +392,8 @@ def main():
 
         faulthandler.dump_traceback_later(float(os.environ["DTFS_HANG_DUMP_S"]), exit=True)
     os.environ.setdefault("DTFS_HOST_THREADS", str(max(1, a.decode_threads)))
+    if a.peer_comm is not None:
+        os.environ["DTFS_PEER_COMM"] = str(max(0, a.peer_comm))  # read by parallel/native_comm.create_comm
     ctx = init_from_env()
     world, rank = ctx.world, ctx.rank
     if world != a.gpus and rank == 0:

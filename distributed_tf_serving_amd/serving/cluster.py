@@ -239,7 +239,12 @@ def main(argv=None):
                     help="a GPU step not finished this long breaks the cluster (UNAVAILABLE)")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="leave CPython's cyclic GC at its defaults (utils/gc_tuning.py)")
+    ap.add_argument("--peer-comm", type=int, default=None,
+                    help="one-shot peer exchange for fan-out messages of at most this many bytes per peer "
+                         "(1 = 64 KiB, 0 = RCCL only; default: $DTFS_PEER_COMM or 0)")
     a = ap.parse_args(argv)
+    if a.peer_comm is not None:
+        os.environ["DTFS_PEER_COMM"] = str(max(0, a.peer_comm))
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     ctx = init_from_env(timeout_s=max(60.0, a.control_timeout_s))
     srv = ClusterServer(load_preset(a.preset), ctx, control_timeout_s=a.control_timeout_s,
