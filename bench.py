@@ -84,7 +84,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--prime-steps", type=int, default=100,
+    ap.add_argument("--prime-steps", type=int, default=1000,
                     help="server start-up load: untimed steps of the same continuous closed loop run BEFORE the "
                          "--warmup steps (clocks, caches and host threads reach steady state, as in a server that "
                          "has been up for a while); the timed window is still exactly --steps steps")
