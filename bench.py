@@ -111,23 +111,26 @@ def parse_args():
     ap.add_argument("--shard-tables", action="store_true",
                     help="dlrm: shard the tables even on one GPU (exercises the embedding-exchange step program)")
     ap.add_argument("--small-buckets", default="2048",
-                    help="N=1 (no lockstep): extra padding buckets below the full step, so a lightly loaded "
-                         "server runs a step sized to what is queued (TF-Serving allowed_batch_sizes); '' = only "
-                         "the full step. 2048: bench/bucket_cost.py on MI355X - a 512- or 1024-row step costs "
-                         "64-66 us pipelined (launch-chain bound), a 2048-row one 79 us, so smaller buckets only "
-                         "saturate at 20k QPS of 512-row requests")
+                    help="extra padding buckets (rows per GPU) below the full step, so a lightly loaded server "
+                         "runs a step sized to what is queued (TF-Serving allowed_batch_sizes; at N > 1 every "
+                         "rank agrees on the largest bucket any rank needs); '' = only the full step. 2048: "
+                         "bench/bucket_cost.py on MI355X - a 512- or 1024-row step costs 64-66 us pipelined "
+                         "(launch-chain bound), a 2048-row one 79 us, so smaller buckets only saturate at 20k QPS "
+                         "of 512-row requests")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight)")
     ap.add_argument("--batch-timeout-us", type=int, default=200)
     ap.add_argument("--qps", type=float, default=20000.0,
-                    help="N=1: offered load of the fixed-QPS latency run (requests/s; 0 = skip)")
+                    help="offered load of the fixed-QPS latency run, whole node (requests/s; 0 = skip); at N > 1 "
+                         "split evenly over the front-door ranks")
     ap.add_argument("--qps-seconds", type=float, default=1.0)
     ap.add_argument("--loop", default="live", choices=["live", "replay", "python"],
                     help="live: the served path (default); replay / python: engine-only diagnostics (round 1)")
     ap.add_argument("--force-fanout", action="store_true",
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--no-native-fanout", action="store_true",
-                    help="N>1: issue collectives through torch.distributed instead of the C++ StepRunner")
+                    help="N>1 on GPU: issue collectives through torch.distributed instead of the C++ StepRunner "
+                         "(diagnostic; the live server then needs --loop replay/python)")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a step not finished by then fails the run instead of hanging it")
     ap.add_argument("--no-narrow", action="store_true",
@@ -157,7 +160,11 @@ def build(a, ctx):
                       file=sys.stderr)
             rows = fit
         cfg.table_rows = rows
-    model = build_parallel_model(cfg, dev, ctx, shard_tables="on" if a.shard_tables else "auto")
+    # CPU (gloo): the step's collectives run on the live server's launcher
+    # thread, so they get a group of their own (the main thread syncs phases
+    # on the default group)
+    step_group = dist.new_group(backend="gloo") if (world > 1 and dev.type != "cuda") else None
+    model = build_parallel_model(cfg, dev, ctx, shard_tables="on" if a.shard_tables else "auto", group=step_group)
     F = cfg.num_fields
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
     sharded = getattr(model, "has_collectives", False) or (a.model == "dlrm" and a.shard_tables)
@@ -166,27 +173,28 @@ def build(a, ctx):
     if sharded and a.mode != "local":
         raise SystemExit("dlrm with sharded tables runs --mode local (the embedding exchange is the fan-out)")
     mode = a.mode if world > 1 else ("alltoall" if a.force_fanout else "local")
-    # lockstep jobs (collectives in the step) always run the full bucket on every rank
     small = [int(x) for x in a.small_buckets.split(",") if x.strip()] if a.small_buckets else []
-    lock = world > 1 and (mode != "local" or sharded)
-    buckets = sorted({b for b in small if 0 < b < B} | {B}) if not lock and mode == "local" else [B]
+    # an all-to-all splits every rank's rows evenly over the GPUs
+    small = [b for b in small if mode != "alltoall" or b % world == 0]
+    buckets = sorted({b for b in small if 0 < b < B} | {B})
     # fan-out rows travel narrow (int32 table rows + bf16 weights: half the xGMI bytes)
     layout = layout_for(cfg, mode != "local" and not a.no_narrow) if mode != "local" else PackedLayout(F)
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=not a.no_graphs, slots=a.slots)
     rows_in_max = B * (world if mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
-                       native_fanout=not a.no_native_fanout)
+                       native_fanout=not a.no_native_fanout, group=step_group)
     for b in buckets:
         eng.prepare(b)
-    if eng.program_active:
-        # one synthetic step of the native step program vs the eager forward (collective)
-        if not eng.self_check(B, seed=rank):
-            raise SystemExit(f"rank {rank}: the step program's scores differ from the eager forward")
-    elif eng.mode != "local":
-        # one synthetic step checked against a local forward on every rank; a
-        # failure anywhere switches every rank to the torch.distributed path
-        eng.self_check(B, seed=rank)
+    if eng.program_active or eng.mode != "local":
+        # one synthetic step of every bucket checked against a local / eager
+        # forward on every rank (collective): a fan-out that scores wrong is
+        # a failed run, not a silent fallback
+        for b in buckets:
+            if not eng.self_check(b, seed=rank):
+                raise SystemExit(f"rank {rank}: the fan-out step's scores differ from a local forward (bucket {b})")
+        if dev.type == "cuda" and eng.mode != "local" and not eng.native_fanout_active:
+            raise SystemExit(f"rank {rank}: the native fan-out step is not active")
     return cfg, model, eng, B
 
 
@@ -232,41 +240,47 @@ def pct(lat_us, q):
 def run_live(a, ctx, cfg, model, eng, B):
     world, rank, dev = ctx.world, ctx.rank, ctx.device
     F = cfg.num_fields
-    R = a.requests_per_gpu
     pool, n_req = request_pool(a, ctx, eng, B, F)
-    lockstep = eng.lockstep
     conc = (a.slots + 2) * max(1, n_req)
-    # lockstep (fan-out): every rank launches exactly this many steps, empty
-    # ones included, so the collectives of the last steps always pair up
     untimed = a.prime_steps + a.warmup  # one continuous run: prime, then warmup, then the K timed steps
-    max_steps = untimed + a.steps + -(-conc // max(1, n_req)) + 4 if lockstep else -1
     buckets = list(eng.ex.buckets)
     sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=tuple(buckets), batch_timeout_us=a.batch_timeout_us,
                        max_queued_rows=1 << 24, max_request_rows=1 << 20)
-    live = LiveScheduler(eng, sc, buckets=buckets, depth=a.slots, lockstep=lockstep, max_steps=max_steps,
-                         step_timeout_s=a.step_timeout_s, start_paused=lockstep, narrow=not a.no_narrow)
+    # steps with collectives are agreed with the other ranks through the
+    # shared-memory step control: launched only when some rank has requests,
+    # at the smallest bucket that holds every rank's batch
+    control = None
+    if eng.lockstep and world > 1:
+        from distributed_tf_serving_amd.ops import hip
+        from distributed_tf_serving_amd.parallel.control import control_for_job
+
+        control = control_for_job(hip() if dev.type == "cuda" else native(), ctx, "bench")
+    live = LiveScheduler(eng, sc, buckets=buckets, depth=a.slots, control=control, step_timeout_s=a.step_timeout_s,
+                         start_paused=control is not None, narrow=not a.no_narrow, peer_timeout_s=a.step_timeout_s)
     extra = {}
     if world == 1 and pool:
         extra["fp32_check"] = fp32_check(cfg, model, live, pool[0])
+    # phase barriers of the main thread: a CPU group of their own (the step's
+    # collectives, if any, run on the launcher thread on other communicators)
+    phase = dist.new_group(backend="gloo") if ctx.is_distributed else None
 
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         if ctx.is_distributed:
-            dist.barrier()
+            dist.barrier(group=phase)
 
     tune_for_serving()  # same process tuning as the gRPC server (utils/gc_tuning.py)
     sync()
-    if lockstep:
-        live.resume()  # every rank is past its start-up collectives: the step cadence may begin
+    if control is not None:
+        live.resume()  # every rank is past its start-up collectives: steps may begin
+    timeout_us = int(a.step_timeout_s * 1e6)
     if pool:
         r = live.run_load(pool, warmup=untimed * n_req, count=a.steps * n_req, concurrency=conc,
-                          threads=a.client_threads, timeout_us=int(a.step_timeout_s * 1e6))
-    else:  # a rank without requests (scatter followers): its steps run in lockstep with rank 0's
+                          threads=a.client_threads, timeout_us=timeout_us)
+    else:  # a rank without requests (scatter followers): its live server joins rank 0's steps
         r = {"window_us": 0.0, "latency_us": [], "errors": 0, "ok": 0}
-    if lockstep:
-        live.close()  # finishes the fixed-length run (empty steps until max_steps)
-    sync()
+    st_load = live.stats()
     window_s = r["window_us"] * 1e-6
     if r["errors"]:
         print(f"rank {rank}: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr, flush=True)
@@ -274,33 +288,52 @@ def run_live(a, ctx, cfg, model, eng, B):
     extra["p50_request_ms"], extra["p99_request_ms"] = pct(lat, 50), pct(lat, 99)
     extra["requests_failed"] = int(r["errors"])
 
-    if world == 1 and pool and not lockstep:
-        if a.qps > 0:
-            n = max(200, int(a.qps * a.qps_seconds))
-            q = live.run_load(pool, warmup=n // 10, count=n, qps=a.qps, threads=a.client_threads,
-                              timeout_us=int(a.step_timeout_s * 1e6))
-            extra["fixed_qps"] = {"qps": a.qps, "request_rows": a.request_rows,
-                                  "scores_per_s": round(a.qps * a.request_rows, 1),
-                                  "p50_ms": pct(q["latency_us"], 50), "p99_ms": pct(q["latency_us"], 99),
-                                  "errors": int(q["errors"])}
-            extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
-        # BASELINE config 2 literally: one 512-candidate request at a time
-        c1 = live.run_load(pool, warmup=20, count=300, concurrency=1, threads=1,
-                           timeout_us=int(a.step_timeout_s * 1e6))
+    # fixed offered load (whole node), split over the front-door ranks
+    fronts = world if eng.contrib_rows(B) and eng.mode != "scatter" else 1
+    if a.qps > 0:
+        sync()
+        q = {"latency_us": [], "errors": 0}
+        if pool:
+            n = max(200, int(a.qps / fronts * a.qps_seconds))
+            q = live.run_load(pool, warmup=n // 10, count=n, qps=a.qps / fronts, threads=a.client_threads,
+                              timeout_us=timeout_us)
+        p50, p99 = pct(q["latency_us"], 50), pct(q["latency_us"], 99)
+        red = torch.tensor([p50 or 0.0, p99 or 0.0, float(q["errors"])], dtype=torch.float64)
+        if ctx.is_distributed:  # the slowest front door's percentiles
+            dist.all_reduce(red, op=dist.ReduceOp.MAX, group=phase)
+        extra["fixed_qps"] = {"qps": a.qps, "front_doors": fronts, "request_rows": a.request_rows,
+                              "scores_per_s": round(a.qps * a.request_rows, 1),
+                              "p50_ms": round(float(red[0]), 3), "p99_ms": round(float(red[1]), 3),
+                              "errors": int(red[2])}
+        extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
+    # BASELINE config 2 literally: one 512-candidate request at a time (at N > 1
+    # fanned out over every GPU: the reference's topology inside one node)
+    sync()
+    if rank == 0 and pool:
+        c1 = live.run_load(pool, warmup=20, count=300, concurrency=1, threads=1, timeout_us=timeout_us)
         w = c1["window_us"] * 1e-6
         extra["config2_batch512"] = {"concurrency": 1, "p50_ms": pct(c1["latency_us"], 50),
                                      "p99_ms": pct(c1["latency_us"], 99),
                                      "scores_per_s": round(300 * a.request_rows / w, 1) if w > 0 else None}
+    sync()
     st = live.stats()
-    extra["server"] = {k: st[k] for k in ("steps", "full_steps", "timeout_steps", "eager_steps", "empty_steps",
-                                          "blocked_submits", "narrowed")}
-    extra["ingest"] = ("host-narrowed int32 rows + bf16 weights (K0 on the submitting thread)" if live.narrow_modulo
+    keys = ("steps", "full_steps", "timeout_steps", "eager_steps", "empty_steps", "proposed_steps", "joined_steps",
+            "blocked_submits", "narrowed")
+    extra["server"] = {k: st[k] for k in keys}
+    extra["server"]["steps_in_throughput_run"] = st_load["steps"]
+    if control is not None:
+        # an idle cluster launches nothing: no step between the phases' ends
+        t0 = st["steps"]
+        time.sleep(0.05)
+        extra["server"]["idle_steps_per_s"] = round((live.stats()["steps"] - t0) / 0.05, 1)
+    extra["ingest"] = ("host-narrowed int32 rows + fp32 weights (K0 on the submitting thread)" if live.narrow_modulo
                        else "raw request bytes, unpacked on the GPU")
     if a.json_extra and rank == 0:
         per = {k: round(st[k] / max(1, st["steps"]), 1) for k in ("copy_us", "build_us", "launch_us", "wait_us",
                                                                   "encode_us")}
         print(json.dumps({"server_us_per_step": per, "stats": st}), file=sys.stderr, flush=True)
-    live.close()
+    live.close()  # cluster: returns once every rank has closed
+    sync()
     return window_s, extra
 
 
@@ -429,7 +462,7 @@ def main():
                    + (", native C++ step" if eng.native_fanout_active else ", torch.distributed")
                    + (f", one-shot peer exchange for messages <= {eng._cin.peer_cap} B per peer"
                       if getattr(eng, "_cin", None) is not None and eng._cin.peer_enabled else "")
-                   + (f", {eng.layout.row_bytes} B rows: int32 table rows + bf16 weights" if eng.layout.narrow
+                   + (f", {eng.layout.row_bytes} B rows: int32 table rows + fp32 weights" if eng.layout.narrow
                       else f", {eng.layout.row_bytes} B rows: raw int64 ids + fp32 weights") + ")")
         if hasattr(model, "plan"):
             par += (f" + embedding-mp{model.plan.world} ({len(model.plan.row_wise())} row-wise tables, all-to-all; "

@@ -527,7 +527,7 @@ void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields, int
   check_same_dev(arena, packed, "packed");
   TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.numel() > dtfs::kArenaPayloadOff, "arena: uint8 [cap]");
   TORCH_CHECK(packed.scalar_type() == torch::kInt64 && packed.dim() == 2, "packed must be int64 [B, W]");
-  TORCH_CHECK(packed.size(1) * 8 >= (narrow_modulo > 0 ? 6 : 12) * fields, "packed rows too narrow for the field count");
+  TORCH_CHECK(packed.size(1) * 8 >= (narrow_modulo > 0 ? 8 : 12) * fields, "packed rows too narrow for the field count");
   TORCH_CHECK(narrow_modulo >= 0 && narrow_modulo < (int64_t(1) << 31), "narrow_modulo must fit int32 rows");
   c10::DeviceGuard g(arena.device());
   // descriptor offsets come from the (validated) host parse of this arena; the
@@ -882,8 +882,10 @@ struct PyGpuLive {
 };
 
 // buckets: [(rows, [slot dict per slot]), ...] ascending.
-PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, py::list arenas) {
+PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, py::list arenas,
+                         py::object control) {
   auto* p = new PyGpuLive();
+  dtfs::runtime::StepControl* ctl = dtfs_live::control_from(control, &p->keep);
   p->keep.push_back(runner_obj);
   auto& runner = runner_obj.cast<dtfs::runtime::StepRunner&>();
   std::vector<int64_t> rows;
@@ -899,7 +901,7 @@ PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, 
   auto ar = dtfs_live::arenas_from(arenas, true, &p->keep);
   p->backend = std::make_unique<GpuBackend>(&runner, std::move(rows), std::move(slots));
   p->srv = std::make_unique<dtfs::runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg),
-                                                       std::move(ar));
+                                                       std::move(ar), ctl);
   return p;
 }
 
@@ -1076,9 +1078,11 @@ PYBIND11_MODULE(_hip, m) {
     py::class_<PyGpuLive> c(m, "LiveServer",
                             "Live serving core (csrc/runtime/live_server.h) on this GPU: requests are batched into "
                             "pinned arenas and run as captured step kernels (or the fan-out step)");
-    c.def(py::init(&make_gpu_live), py::arg("runner"), py::arg("config"), py::arg("buckets"), py::arg("arenas"));
+    c.def(py::init(&make_gpu_live), py::arg("runner"), py::arg("config"), py::arg("buckets"), py::arg("arenas"),
+          py::arg("control") = py::none());
     dtfs_live::def_live_methods(c);
   }
+  dtfs_live::def_step_control(m);
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });

@@ -474,8 +474,9 @@ struct PyCpuLive {
 };
 
 PyCpuLive* make_cpu_live(py::dict cfg, std::vector<int64_t> buckets, py::list scores, py::list arenas,
-                         py::function fwd) {
+                         py::function fwd, py::object control) {
   auto* p = new PyCpuLive();
+  runtime::StepControl* ctl = dtfs_live::control_from(control, &p->keep);
   auto ar = dtfs_live::arenas_from(arenas, false, &p->keep);
   std::vector<const uint8_t*> bases;
   for (auto& a : ar) bases.push_back(a.first);
@@ -487,7 +488,8 @@ PyCpuLive* make_cpu_live(py::dict cfg, std::vector<int64_t> buckets, py::list sc
   }
   p->keep.push_back(scores);
   p->backend = std::make_unique<PyCpuBackend>(std::move(buckets), std::move(sc), std::move(bases), fwd);
-  p->srv = std::make_unique<runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg), std::move(ar));
+  p->srv = std::make_unique<runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg), std::move(ar),
+                                                 ctl);
   return p;
 }
 
@@ -644,9 +646,10 @@ PYBIND11_MODULE(_native, m) {
                             "Live serving core (csrc/runtime/live_server.h) with a CPU backend: a Python "
                             "forward(arena_index, slot, bucket_index) scores each batch");
     c.def(py::init(&make_cpu_live), py::arg("config"), py::arg("buckets"), py::arg("scores"), py::arg("arenas"),
-          py::arg("forward"));
+          py::arg("forward"), py::arg("control") = py::none());
     dtfs_live::def_live_methods(c);
   }
+  dtfs_live::def_step_control(m);
   m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
   m.attr("STATUS_CALLER_PATH") = int(runtime::kCallerPath);
   m.def(
@@ -661,17 +664,6 @@ PYBIND11_MODULE(_native, m) {
         return out;
       },
       py::arg("ids"), py::arg("modulo"), "Host K0: int64 ids -> int32 rows (python-style id mod modulo).");
-  m.def(
-      "narrow_wts",
-      [](torch::Tensor w) {
-        TORCH_CHECK(w.device().is_cpu() && w.scalar_type() == torch::kFloat32, "weights must be CPU fp32");
-        auto src = w.contiguous();
-        auto out = torch::empty(src.sizes(), torch::kBFloat16);
-        runtime::narrow_wts(reinterpret_cast<const uint8_t*>(src.data_ptr()),
-                            reinterpret_cast<uint16_t*>(out.data_ptr()), src.numel());
-        return out;
-      },
-      py::arg("wts"), "Host K0: fp32 weights -> bf16 (round to nearest even).");
   m.def("now_us", &runtime::now_us);
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));

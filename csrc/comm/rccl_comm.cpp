@@ -115,7 +115,7 @@ void RcclComm::check(ncclResult_t r, const char* what) {
 }
 
 void RcclComm::alltoall(const void* send, void* recv, size_t bytes, hipStream_t st) {
-  if (aborted_) throw std::runtime_error("communicator aborted");
+  check_usable();
   if (peer_enabled() && bytes <= peer_->cap) {
     const void* src[kPeerMaxRanks];
     void* dst[kPeerMaxRanks];
@@ -131,7 +131,7 @@ void RcclComm::alltoall(const void* send, void* recv, size_t bytes, hipStream_t 
 }
 
 void RcclComm::scatter(const void* send, void* recv, size_t bytes, int root, hipStream_t st) {
-  if (aborted_) throw std::runtime_error("communicator aborted");
+  check_usable();
   if (peer_enabled() && bytes <= peer_->cap) {
     const void* src[kPeerMaxRanks] = {};
     void* dst[kPeerMaxRanks] = {};
@@ -155,7 +155,7 @@ void RcclComm::scatter(const void* send, void* recv, size_t bytes, int root, hip
 }
 
 void RcclComm::gather(const void* send, void* recv, size_t bytes, int root, hipStream_t st) {
-  if (aborted_) throw std::runtime_error("communicator aborted");
+  check_usable();
   if (peer_enabled() && bytes <= peer_->cap) {
     const void* src[kPeerMaxRanks] = {};
     void* dst[kPeerMaxRanks] = {};
@@ -179,7 +179,7 @@ void RcclComm::gather(const void* send, void* recv, size_t bytes, int root, hipS
 }
 
 void RcclComm::allgather(const void* send, void* recv, size_t bytes, hipStream_t st) {
-  if (aborted_) throw std::runtime_error("communicator aborted");
+  check_usable();
   if (peer_enabled() && bytes <= peer_->cap) {
     const void* src[kPeerMaxRanks];
     void* dst[kPeerMaxRanks];
@@ -195,8 +195,16 @@ void RcclComm::allgather(const void* send, void* recv, size_t bytes, hipStream_t
 }
 
 void RcclComm::reduce_scatter_bf16(const void* send, void* recv, size_t elems, hipStream_t st) {
-  if (aborted_) throw std::runtime_error("communicator aborted");
+  check_usable();
   check(api().ReduceScatter(send, recv, elems, ncclBfloat16, ncclSum, comm_, st), "ncclReduceScatter");
+}
+
+void RcclComm::check_usable() const {
+  if (aborted_) throw std::runtime_error("communicator aborted");
+  // a timed-out peer exchange is sticky (its sequence numbers no longer match
+  // the peers'): launching more would move no data and report success
+  if (peer_ && peer_->err_host && __atomic_load_n(peer_->err_host, __ATOMIC_ACQUIRE))
+    throw std::runtime_error("communicator broken: a peer exchange timed out (a peer rank stopped answering)");
 }
 
 std::string RcclComm::async_error() {

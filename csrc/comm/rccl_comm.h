@@ -69,6 +69,8 @@ class RcclComm {
 
   // "" when healthy, else the asynchronous RCCL error (failure detection).
   std::string async_error();
+  // throws if the communicator is aborted or its peer exchange timed out
+  void check_usable() const;
   // Abort in-flight operations (a peer died / a deadline passed); the
   // communicator is unusable afterwards.
   void abort();

@@ -78,10 +78,10 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* p) {
 // Request-arena header (csrc/runtime/arena.h): n_req @0, total_rows @8,
 // row_table_off @16 ({ids_off, wts_off} int32 per row, payload-relative).
 // A row whose ids_off has bit 31 set was narrowed by the host while it copied
-// the request (runtime/narrow.h): int32 table rows + bf16 weights, aligned.
+// the request (runtime/narrow.h): int32 table rows + fp32 weights, aligned.
 struct ArenaRow {
   const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: 4 * F of int32 rows), or nullptr (padding row)
-  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 2 * F of bf16)
+  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 4-byte aligned)
   bool narrow;
 };
 
@@ -103,7 +103,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
 __device__ __forceinline__ void arena_feature(const ArenaRow& ar, int f, int64_t& id, float& w) {
   if (ar.narrow) {
     id = int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
-    w = __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(ar.wts)[f]) << 16);
+    w = reinterpret_cast<const float*>(ar.wts)[f];
   } else {
     id = int64_t(load_u64_unaligned(ar.ids + 8 * f));
     w = __uint_as_float(load_u32_unaligned(ar.wts + 4 * f));

@@ -28,16 +28,16 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
   if (r >= B) return;
   const ArenaRow src = arena_row(arena, kArenaPayloadOff, r);
   int64_t* dst = packed + int64_t(r) * W;
-  if (src.narrow) {  // host-narrowed row: int32 rows -> int64, bf16 -> fp32 (packed as 2 per word)
+  if (src.narrow) {  // host-narrowed row: int32 rows -> int64, fp32 weights (packed as 2 per word)
     for (int c = lane; c < W; c += 64) {
       uint64_t v = 0;
       if (c < F) {
         v = uint64_t(int64_t(reinterpret_cast<const int32_t*>(src.ids)[c]));
       } else {
         const int f0 = 2 * (c - F);
-        const uint16_t* wb = reinterpret_cast<const uint16_t*>(src.wts);
-        const uint32_t lo = f0 < F ? uint32_t(wb[f0]) << 16 : 0u;
-        const uint32_t hi = f0 + 1 < F ? uint32_t(wb[f0 + 1]) << 16 : 0u;
+        const uint32_t* wb = reinterpret_cast<const uint32_t*>(src.wts);
+        const uint32_t lo = f0 < F ? wb[f0] : 0u;
+        const uint32_t hi = f0 + 1 < F ? wb[f0 + 1] : 0u;
         v = (uint64_t(hi) << 32) | lo;
       }
       dst[c] = int64_t(v);
@@ -61,9 +61,9 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
 }
 
 // Narrow output (the candidate fan-out's exchange rows, serving/packing.py
-// PackedLayout(narrow_modulo=m)): [int32 table rows x F | bf16 weights x F |
-// pad], 6 bytes per field instead of 12, so the all-to-all moves half the
-// bytes. Raw ids are hashed (id mod m) here; host-narrowed rows already are.
+// PackedLayout(narrow_modulo=m)): [int32 table rows x F | fp32 weights x F],
+// 8 bytes per field instead of 12, so the all-to-all moves 2/3 of the bytes.
+// Raw ids are hashed (id mod m) here; host-narrowed rows already are.
 __global__ void __launch_bounds__(256) unpack_arena_narrow_kernel(const uint8_t* __restrict__ arena,
                                                                   int64_t* __restrict__ packed, int B, int F, int W,
                                                                   int64_t modulo) {
@@ -72,17 +72,16 @@ __global__ void __launch_bounds__(256) unpack_arena_narrow_kernel(const uint8_t*
   if (r >= B) return;
   const ArenaRow src = arena_row(arena, kArenaPayloadOff, r);
   int32_t* ids = reinterpret_cast<int32_t*>(packed + int64_t(r) * W);
-  uint16_t* wts = reinterpret_cast<uint16_t*>(ids + F);
+  float* wts = reinterpret_cast<float*>(ids + F);
   for (int f = lane; f < F; f += 64) {
     int64_t id = 0;
     float w = 0.f;  // padding rows (no request): row 0, weight 0
     if (src.ids) arena_feature(src, f, id, w);
     ids[f] = int32_t(src.narrow ? id : hash_row(id, modulo));
-    const bf16 wb = f2bf(w);  // round to nearest even, as torch's fp32 -> bf16
-    wts[f] = *reinterpret_cast<const uint16_t*>(&wb);
+    wts[f] = w;
   }
   // zero the row's pad bytes (fixed-size rows travel whole)
-  const int used = 6 * F, total = 8 * W;
+  const int used = 8 * F, total = 8 * W;
   uint8_t* row = reinterpret_cast<uint8_t*>(ids);
   for (int c = used + lane; c < total; c += 64) row[c] = 0;
 }
@@ -246,7 +245,7 @@ hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F,
   (void)max_req;  // rows are located through the row table, not the descriptors
   if (B == 0) return hipSuccess;
   if (narrow_modulo > 0) {
-    if (W * 8 < 6 * F || narrow_modulo >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+    if (W * 8 < 8 * F || narrow_modulo >= (int64_t(1) << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern::unpack_arena_narrow_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
                        static_cast<const uint8_t*>(arena), packed, B, F, W, narrow_modulo);
     return hipGetLastError();

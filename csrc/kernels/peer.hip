@@ -22,9 +22,11 @@
 // The sequence number lives in device memory (ctl->seq) and is advanced by the
 // last block of each exchange, so the launch is graph-capturable and needs no
 // host bookkeeping. Every spin is bounded (s_memrealtime, 100 MHz): a peer that
-// never answers makes the kernel record an error word in mapped host memory
-// and exit, so the grid always drains; the host reports it through
-// RcclComm::async_error() and the step runner aborts the step.
+// never answers makes the kernel record an error word in mapped host memory,
+// fill the receive buffers it could not deliver with all-ones (NaN scores) and
+// exit, so the grid always drains; the host reports it through
+// RcclComm::async_error(), which the step wait checks once more before it
+// declares a step done, and further exchanges on the communicator throw.
 #include "common.h"
 #include "peer_exchange.h"
 
@@ -118,6 +120,19 @@ __global__ void __launch_bounds__(256) peer_exchange_kernel(PeerExchangeArgs a) 
     }
   }
   __syncthreads();
+  if (!s_ok && a.dst[p] && a.recv_bytes[p]) {
+    // poison what this block should have delivered (all-ones: NaN as fp32
+    // scores, -1 as int32 rows - which the gather clamps): a host that misses
+    // the error word cannot hand out plausible-looking scores from stale data
+    uint8_t* d = a.dst[p];
+    const uint64_t n = a.recv_bytes[p];
+    if ((reinterpret_cast<uintptr_t>(d) & 3) == 0) {
+      for (uint64_t i = threadIdx.x; i < (n >> 2); i += blockDim.x) reinterpret_cast<uint32_t*>(d)[i] = 0xffffffffu;
+      for (uint64_t i = ((n >> 2) << 2) + threadIdx.x; i < n; i += blockDim.x) d[i] = 0xff;
+    } else {
+      for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = 0xff;
+    }
+  }
   if (threadIdx.x == 0) {
     if (!s_ok) {
       a.ctl->broken = 1;

@@ -15,6 +15,7 @@
 #include "runtime/batcher.h"
 #include "runtime/live_server.h"
 #include "runtime/loadgen.h"
+#include "runtime/step_control.h"
 
 namespace dtfs_live {
 
@@ -22,6 +23,71 @@ namespace py = pybind11;
 using dtfs::runtime::LiveConfig;
 using dtfs::runtime::LiveServer;
 using dtfs::runtime::Reply;
+using dtfs::runtime::StepControl;
+
+// StepControl (runtime/step_control.h) of this module; module-local, so the
+// CPU (_native) and GPU (_hip) modules each own one binding of the type.
+inline void def_step_control(py::module& m) {
+  py::class_<StepControl>(m, "StepControl", py::module_local(),
+                          "Shared-memory step agreement of a multi-rank live server (one node)")
+      .def(py::init<std::string, int, int, bool>(), py::arg("name"), py::arg("world"), py::arg("rank"),
+           py::arg("create"))
+      .def_property_readonly("world", &StepControl::world)
+      .def_property_readonly("rank", &StepControl::rank)
+      .def_property_readonly("name", &StepControl::name)
+      .def_property_readonly("proposed", &StepControl::proposed)
+      .def("propose", &StepControl::propose, py::arg("step"))
+      .def("post", &StepControl::post, py::arg("step"), py::arg("bucket"))
+      .def(
+          "gather",
+          [](StepControl& c, uint64_t k, double timeout_s) {
+            std::string err;
+            int b;
+            {
+              py::gil_scoped_release nogil;
+              b = c.gather(k, int64_t(timeout_s * 1e6), &err);
+            }
+            return py::make_tuple(b, err);
+          },
+          py::arg("step"), py::arg("timeout_s"))
+      .def("heartbeat", &StepControl::heartbeat)
+      .def(
+          "silent_peer", [](const StepControl& c, double timeout_s) { return c.silent_peer(int64_t(timeout_s * 1e6)); },
+          py::arg("timeout_s"))
+      .def("set_closing", &StepControl::set_closing, py::arg("closing"))
+      .def_property_readonly("all_closing", &StepControl::all_closing)
+      .def("request_stop", &StepControl::request_stop)
+      .def_property_readonly("stop_requested", &StepControl::stop_requested)
+      .def("mark_broken", &StepControl::mark_broken, py::arg("by_rank"))
+      .def_property_readonly("broken_by", &StepControl::broken_by)
+      .def_property_readonly("epoch", &StepControl::epoch)
+      .def("bump_epoch", &StepControl::bump_epoch)
+      .def(
+          "wait_event",
+          [](StepControl& c, double timeout_s) {
+            // block until a stop request, a broken cluster, an epoch change or
+            // the timeout; heartbeats while waiting (a follower's main thread)
+            py::gil_scoped_release nogil;
+            const int64_t end = dtfs::runtime::now_us() + int64_t(timeout_s * 1e6);
+            const uint32_t ep = c.epoch();
+            for (;;) {
+              const uint32_t seen = c.bell();
+              c.heartbeat();
+              if (c.stop_requested() || c.broken_by() >= 0 || c.epoch() != ep) return true;
+              const int64_t left = end - dtfs::runtime::now_us();
+              if (left <= 0) return false;
+              c.wait_bell(seen, std::min<int64_t>(left, 20000));
+            }
+          },
+          py::arg("timeout_s"))
+      .def("unlink", &StepControl::unlink);
+}
+
+inline StepControl* control_from(const py::object& o, std::vector<py::object>* keep) {
+  if (o.is_none()) return nullptr;
+  keep->push_back(o);
+  return &o.cast<StepControl&>();
+}
 
 inline LiveConfig live_config_from(const py::dict& d) {
   LiveConfig c;
@@ -40,8 +106,8 @@ inline LiveConfig live_config_from(const py::dict& d) {
   if (get("varint_chunks")) c.varint_chunks = d["varint_chunks"].cast<int64_t>();
   if (get("max_pending")) c.max_pending = d["max_pending"].cast<int64_t>();
   if (get("eager_when_idle")) c.eager_when_idle = d["eager_when_idle"].cast<bool>();
-  if (get("lockstep")) c.lockstep = d["lockstep"].cast<bool>();
-  if (get("max_steps")) c.max_steps = d["max_steps"].cast<int64_t>();
+  if (get("peer_timeout_us")) c.peer_timeout_us = d["peer_timeout_us"].cast<int64_t>();
+  if (get("heartbeat_us")) c.heartbeat_us = d["heartbeat_us"].cast<int64_t>();
   if (get("step_timeout_us")) c.step_timeout_us = d["step_timeout_us"].cast<int64_t>();
   if (get("start_paused")) c.start_paused = d["start_paused"].cast<bool>();
   if (get("narrow_modulo")) c.narrow_modulo = d["narrow_modulo"].cast<int64_t>();
@@ -164,6 +230,8 @@ void def_live_methods(py::class_<H>& c) {
             o["eager_steps"] = s.eager_steps;
             o["blocked_submits"] = s.blocked_submits;
             o["narrowed"] = s.narrowed;
+            o["proposed_steps"] = s.proposed_steps;
+            o["joined_steps"] = s.joined_steps;
             o["copy_us"] = s.copy_us;
             o["build_us"] = s.build_us;
             o["launch_us"] = s.launch_us;

@@ -83,10 +83,10 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
     const ArenaItem& it = items[i];
     if (it.narrow) {
       const int64_t ne = it.rows * fields;
-      if (it.rows < 0 || it.ids_off < 0 || it.wts_off < 0 || it.ids_off % 4 || it.wts_off % 2 ||
-          it.ids_off + 4 * ne > cap || it.wts_off + 2 * ne > cap)
+      if (it.rows < 0 || it.ids_off < 0 || it.wts_off < 0 || it.ids_off % 4 || it.wts_off % 4 ||
+          it.ids_off + 4 * ne > cap || it.wts_off + 4 * ne > cap)
         throw std::invalid_argument("narrow request outside arena");
-      end = std::max(end, std::max(it.ids_off + 4 * ne, it.wts_off + 2 * ne));
+      end = std::max(end, std::max(it.ids_off + 4 * ne, it.wts_off + 4 * ne));
       continue;
     }
     spans[i] = {it.off, it.len};
@@ -309,7 +309,7 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
       const int64_t ni = io & ~kNarrowFlag;
       for (int64_t r = 0; r < rows; ++r) {
         tab[2 * (r0 + r) + 0] = int32_t(uint32_t(ni + r * 4 * fields) | 0x80000000u);
-        tab[2 * (r0 + r) + 1] = int32_t(wo + r * 2 * fields);
+        tab[2 * (r0 + r) + 1] = int32_t(wo + r * 4 * fields);
       }
       continue;
     }
@@ -342,19 +342,16 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
     for (int64_t r = 0; r < desc[4 * i + 2]; ++r) {
       const int64_t row = desc[4 * i + 3] + r;
       if (row >= B) break;
-      if (narrow) {  // int32 rows -> int64, bf16 -> fp32
+      if (narrow) {  // int32 rows -> int64, fp32 weights as they are
         const uint8_t* ip = payload + (desc[4 * i + 0] & ~kNarrowFlag) + r * 4 * fields;
-        const uint8_t* wp = payload + desc[4 * i + 1] + r * 2 * fields;
+        const uint8_t* wp = payload + desc[4 * i + 1] + r * 4 * fields;
         for (int64_t f = 0; f < fields; ++f) {
           int32_t id;
-          uint16_t h;
           std::memcpy(&id, ip + 4 * f, 4);
-          std::memcpy(&h, wp + 2 * f, 2);
           const int64_t id64 = id;
-          const uint32_t bits = uint32_t(h) << 16;
           std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
-          std::memcpy(dst + row * W * 8 + 8 * fields + 4 * f, &bits, 4);
         }
+        std::memcpy(dst + row * W * 8 + 8 * fields, wp, size_t(4 * fields));
         continue;
       }
       std::memcpy(dst + row * W * 8, payload + desc[4 * i + 0] + r * 8 * fields, size_t(8 * fields));

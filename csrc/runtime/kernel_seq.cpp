@@ -5,6 +5,8 @@
 #include "../kernels/launchers.h"
 
 #include <map>
+#include <cstdio>
+#include <cstring>
 #include <stdexcept>
 
 namespace dtfs {
@@ -106,17 +108,23 @@ void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool ski
       const hipMemcpy3DParms& c = op.mc;
       const char* src = static_cast<const char*>(c.srcPtr.ptr) + c.srcPos.x;
       char* dst = static_cast<char*>(c.dstPtr.ptr) + c.dstPos.x;
-      hipError_t e = hipMemcpyAsync(dst, src, c.extent.width, c.kind, st);
-      if (e == hipErrorInvalidMemcpyDirection && c.kind != hipMemcpyDefault) {
-        // Seen intermittently on MI355X (ROCm 7.2) under load for the same
-        // captured copy that succeeded thousands of times before (the runtime's
-        // pointer classification rejects the recorded direction; also seen on
-        // the step runner's H2D): let the runtime infer the direction from
-        // the pointers instead of failing every request of the server.
+      const hipError_t e = hipMemcpyAsync(dst, src, c.extent.width, c.kind, st);
+      if (e != hipSuccess) {
+        // fail with what HIP thinks both pointers are (never retried with
+        // another direction: that would hide the cause)
         (void)hipGetLastError();
-        e = hipMemcpyAsync(dst, src, c.extent.width, hipMemcpyDefault, st);
+        hipPointerAttribute_t ad, as;
+        std::memset(&ad, 0, sizeof(ad));
+        std::memset(&as, 0, sizeof(as));
+        const hipError_t qd = hipPointerGetAttributes(&ad, dst), qs = hipPointerGetAttributes(&as, src);
+        (void)hipGetLastError();
+        char buf[256];
+        std::snprintf(buf, sizeof(buf), "replayed hipMemcpyAsync(kind %d, %zu B): %s; dst %p type %d (%s), src %p type %d (%s)",
+                      int(c.kind), size_t(c.extent.width), hipGetErrorString(e), static_cast<void*>(dst), int(ad.type),
+                      hipGetErrorString(qd), static_cast<const void*>(src), int(as.type), hipGetErrorString(qs));
+        std::fprintf(stderr, "[kernel_seq] %s\n", buf);
+        throw std::runtime_error(buf);
       }
-      ck(e, "hipMemcpyAsync");
     } else {
       const hipMemsetParams& m = op.ms;
       if (m.elementSize == 1) ck(hipMemsetD8Async(hipDeviceptr_t(m.dst), uint8_t(m.value), m.width, st), "memset");

@@ -25,8 +25,9 @@ std::string shape_str(const std::vector<int64_t>& s) {
 }
 }  // namespace
 
-LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas)
-    : backend_(backend), cfg_(std::move(cfg)) {
+LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas,
+                       StepControl* ctl)
+    : backend_(backend), cfg_(std::move(cfg)), ctl_(ctl) {
   if (!backend_) throw std::invalid_argument("null StepBackend");
   const auto& bk = backend_->buckets();
   if (bk.empty() || !std::is_sorted(bk.begin(), bk.end()) || bk.front() <= 0)
@@ -53,9 +54,14 @@ LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pa
     free_.push_back(int(i));
   }
   slot_busy_.assign(size_t(S), 0);
+  if (bk.size() > 0xffff) throw std::invalid_argument("too many buckets");
+  // narrow_ids' AVX2 path multiplies with the low 32 bits of the modulo
+  if (cfg_.narrow_modulo < 0 || cfg_.narrow_modulo >= (int64_t(1) << 31))
+    throw std::invalid_argument("narrow_modulo must be in [0, 2^31)");
   paused_ = cfg_.start_paused;
   launcher_ = std::thread([this] { launcher_loop(); });
   completer_ = std::thread([this] { completer_loop(); });
+  if (ctl_) watcher_ = std::thread([this] { watcher_loop(); });
 }
 
 LiveServer::~LiveServer() {
@@ -74,7 +80,6 @@ int64_t LiveServer::need_of(int64_t len, int64_t rows) const {
 
 int LiveServer::bucket_for(int64_t rows) const {
   const auto& bk = backend_->buckets();
-  if (cfg_.lockstep) return int(bk.size()) - 1;
   for (size_t i = 0; i < bk.size(); ++i)
     if (bk[i] >= rows) return int(i);
   return int(bk.size()) - 1;
@@ -145,7 +150,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
       wts_src = tw->packed[0].p;
   }
   const bool narrow = ids_src && wts_src;
-  const int64_t need = narrow ? align64(4 * ne) + align64(2 * ne) + 8 * rows + 256 : need_of(int64_t(n), rows);
+  const int64_t need = narrow ? align64(4 * ne) + align64(4 * ne) + 8 * rows + 256 : need_of(int64_t(n), rows);
   if (need > arena_budget_) return reject(kOversize, "request does not fit one arena");
 
   const int64_t t0 = now_us();
@@ -210,7 +215,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
       p.narrow = true;
       p.ids_off = align64(o.used);
       p.wts_off = align64(p.ids_off + 4 * ne);
-      o.used = p.wts_off + 2 * ne;
+      o.used = p.wts_off + 4 * ne;
       ++st_.narrowed;
     } else {
       off = p.off = o.used;
@@ -238,7 +243,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   uint8_t* payload = arenas_[size_t(a)].base + kArenaPayloadOff;
   if (narrow) {  // ... narrowed on the way (K0 on the host)
     narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
-    narrow_wts(wts_src, reinterpret_cast<uint16_t*>(payload + pend_wts), ne);
+    std::memcpy(payload + pend_wts, wts_src, size_t(4 * ne));  // fp32 weights travel as they are
   } else {
     std::memcpy(payload + off, data, n);
   }
@@ -327,6 +332,9 @@ void LiveServer::launcher_loop() {
   const int nb = int(backend_->buckets().size());
   for (;;) {
     int a = -1, slot = -1;
+    uint64_t k = 0;            // cluster mode: the step index (identical on every rank)
+    bool remote = false;       // cluster mode: another rank proposed the step
+    int64_t arena_rows = 0;
     std::vector<Pending> pend;
     bool stop = false;
     {
@@ -334,75 +342,147 @@ void LiveServer::launcher_loop() {
       // a free slot first: while the device is busy, requests keep filling the
       // open batch (fuller steps under load)
       auto slot_free = [&] { return inflight_ < cfg_.depth && !slot_busy_[size_t(next_slot_)]; };
-      auto drained = [&] {
-        const bool fixed_run = cfg_.lockstep && cfg_.max_steps >= 0 && steps_launched_ < cfg_.max_steps;
-        return closing_ && !fixed_run && sealed_.empty() && (open_ < 0 || arenas_[size_t(open_)].pend.empty());
-      };
-      cv_launch_.wait(lk, [&] { return broken_ || (!paused_ && (drained() || slot_free())) || (paused_ && closing_); });
-      if (paused_ && closing_) break;  // never started: nothing was launched
-      if (broken_ || !slot_free()) break;
+      auto drained = [&] { return closing_ && sealed_.empty() && (open_ < 0 || arenas_[size_t(open_)].pend.empty()); };
+      if (!ctl_) {
+        cv_launch_.wait(lk, [&] { return broken_ || (!paused_ && (drained() || slot_free())) || (paused_ && closing_); });
+        if (paused_ && closing_) break;  // never started: nothing was launched
+        if (broken_ || !slot_free()) break;
+      }
       for (;;) {
-        if (cfg_.max_steps >= 0 && steps_launched_ >= cfg_.max_steps) {
-          stop = true;
-          break;
-        }
-        if (!sealed_.empty()) {
-          a = sealed_.front();
-          sealed_.pop_front();
-          ++st_.full_steps;
-          break;
+        if (broken_) break;
+        if (paused_) {
+          if (closing_) {  // never started: nothing was launched
+            stop = true;
+            break;
+          }
+          cv_launch_.wait(lk);
+          continue;
         }
         const int64_t now = now_us();
         int64_t wake = 0;
-        if (open_ >= 0 && !arenas_[size_t(open_)].pend.empty()) {
+        // does this rank have a batch to run now?
+        bool local = !sealed_.empty();
+        if (!local && open_ >= 0 && !arenas_[size_t(open_)].pend.empty()) {
           const Arena& o = arenas_[size_t(open_)];
-          const bool idle = cfg_.eager_when_idle && !cfg_.lockstep && inflight_ == 0;
-          if (closing_ || idle || now >= o.t_first + cfg_.batch_timeout_us) {
+          const bool idle = cfg_.eager_when_idle && inflight_ == 0;
+          if (closing_ || idle || now >= o.t_first + cfg_.batch_timeout_us) local = true;
+          else wake = o.t_first + cfg_.batch_timeout_us;
+        }
+        if (!ctl_) {
+          if (!sealed_.empty()) {
+            a = sealed_.front();
+            sealed_.pop_front();
+            ++st_.full_steps;
+            break;
+          }
+          if (local) {
+            const bool idle = cfg_.eager_when_idle && inflight_ == 0;
             a = open_;
             open_ = -1;
             ++(idle ? st_.eager_steps : st_.timeout_steps);
             break;
           }
-          wake = o.t_first + cfg_.batch_timeout_us;
-        } else if (closing_ && !(cfg_.lockstep && cfg_.max_steps >= 0)) {
-          // (a fixed-length lockstep run keeps launching empty steps until
-          // max_steps: the other ranks' steps pair with them)
-          stop = true;
-          break;
-        } else if (cfg_.lockstep) {
-          // fan-out: the other ranks launch this step too, requests or not
-          if (now >= last_launch_us_ + cfg_.batch_timeout_us) {
-            if (open_ >= 0) {
+          if (closing_) {  // drained
+            stop = true;
+            break;
+          }
+        } else {
+          // cluster mode: launch step k when this rank has a batch for it or
+          // another rank proposed it; leave once every rank is closing and no
+          // step is pending (read closing flags BEFORE `proposed`: a rank
+          // proposes its last step before it raises its closing flag)
+          k = uint64_t(steps_launched_);
+          if (drained() && !closing_posted_) {
+            closing_posted_ = true;
+            ctl_->set_closing(true);
+          }
+          if (closing_posted_ && ctl_->all_closing() && ctl_->proposed() <= k) {
+            stop = true;
+            break;
+          }
+          remote = ctl_->proposed() > k;
+          if ((remote || local) && slot_free()) {
+            if (!sealed_.empty()) {
+              a = sealed_.front();
+              sealed_.pop_front();
+              ++st_.full_steps;
+            } else if (open_ >= 0 && !arenas_[size_t(open_)].pend.empty()) {
               a = open_;
               open_ = -1;
-            } else if (!free_.empty()) {
-              a = free_.front();
-              free_.pop_front();
+              ++(local ? st_.timeout_steps : st_.joined_steps);
+            } else if (!free_.empty() || open_ >= 0) {
+              // nothing queued here: an empty contribution to another rank's step
+              if (open_ >= 0) {
+                a = open_;
+                open_ = -1;
+              } else {
+                a = free_.front();
+                free_.pop_front();
+              }
+              ++st_.empty_steps;
             }
             if (a >= 0) {
-              ++st_.empty_steps;
+              if (!remote) ++st_.proposed_steps;
               break;
             }
-          } else {
-            wake = last_launch_us_ + cfg_.batch_timeout_us;
           }
         }
-        if (broken_) break;
-        if (wake > 0) cv_launch_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
-        else cv_launch_.wait(lk);
-        if (broken_) break;
+        // nothing to launch yet: sleep until a submit / slot release / the
+        // batch timeout, or (cluster) a proposal, which the watcher relays
+        if (ctl_ && !(remote || local)) {
+          launcher_idle_.store(true, std::memory_order_seq_cst);
+          ctl_->set_idle(true);
+          // re-check after announcing idleness (seq_cst against propose())
+          if (ctl_->proposed() <= k && !broken_) {
+            if (wake > 0) cv_launch_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
+            else cv_launch_.wait_for(lk, std::chrono::microseconds(cfg_.heartbeat_us));
+          }
+          ctl_->set_idle(false);
+          launcher_idle_.store(false, std::memory_order_seq_cst);
+        } else if (ctl_) {
+          // a step to launch but no free slot / arena yet: release() notifies
+          cv_launch_.wait_for(lk, std::chrono::microseconds(cfg_.heartbeat_us));
+        } else if (wake > 0) {
+          cv_launch_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
+        } else {
+          cv_launch_.wait(lk);
+        }
       }
       if (broken_ || stop) break;
       // writers that reserved space in this batch finish their copies first
       cv_launch_.wait(lk, [&] { return arenas_[size_t(a)].writers == 0; });
       pend = std::move(arenas_[size_t(a)].pend);
       arenas_[size_t(a)].pend.clear();
+      arena_rows = arenas_[size_t(a)].rows;
       slot = next_slot_;
       slot_busy_[size_t(slot)] = 1;
       next_slot_ = (next_slot_ + 1) % S;
       ++inflight_;
       ++steps_launched_;
-      last_launch_us_ = now_us();
+    }
+    int agreed = -1;
+    if (ctl_) {
+      // agree on step k's bucket with every rank (step_control.h)
+      const int mine = arena_rows > 0 ? bucket_for(arena_rows) : 0;
+      std::string gerr;
+      int b = -1;
+      try {
+        trace::Range tr("live_agree");
+        if (!remote) ctl_->propose(k);
+        ctl_->post(k, mine);
+        b = ctl_->gather(k, cfg_.step_timeout_us, &gerr);
+      } catch (const std::exception& e) {
+        gerr = e.what();
+      }
+      if (b < 0 || b >= nb) {
+        const std::string why = "step agreement failed: " + (b >= nb ? std::string("bucket out of range") : gerr);
+        fail_all(pend, kUnavailable, "server unavailable: " + why);
+        release(a, slot);
+        ctl_->mark_broken(ctl_->rank());
+        go_broken(why);
+        break;
+      }
+      agreed = b;
     }
     // requests whose deadline passed while queued are answered, not computed
     const int64_t t0 = now_us();
@@ -429,6 +509,13 @@ void LiveServer::launcher_loop() {
                                 cfg_.varint_chunks);
     } catch (const std::exception& e) {
       fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
+      if (ctl_) {  // the other ranks launch step k: this rank cannot skip it
+        const std::string why = std::string("batch build failed in a cluster step: ") + e.what();
+        release(a, slot);
+        ctl_->mark_broken(ctl_->rank());
+        go_broken(why);
+        break;
+      }
       {
         std::lock_guard<std::mutex> lk(mu_);
         --steps_launched_;
@@ -437,7 +524,7 @@ void LiveServer::launcher_loop() {
       continue;
     }
     const int64_t t1 = now_us();
-    if (batch.n_valid == 0 && !cfg_.lockstep) {
+    if (batch.n_valid == 0 && !ctl_) {
       // nothing to compute: every request was malformed (or none left)
       for (size_t i = 0; i < live.size(); ++i)
         if (live[i].done) live[i].done(Reply{kInvalidArgument, batch.errors[i], std::string()});
@@ -450,7 +537,7 @@ void LiveServer::launcher_loop() {
       release(a, slot);
       continue;
     }
-    const int b = bucket_for(batch.total_rows);
+    const int b = ctl_ ? agreed : bucket_for(batch.total_rows);
     try {
       trace::Range tr("live_launch");
       backend_->launch(slot, b, ar.base, batch);
@@ -458,6 +545,7 @@ void LiveServer::launcher_loop() {
       const std::string why = std::string("step launch failed: ") + e.what();
       fail_all(live, kUnavailable, why);
       release(a, slot);
+      if (ctl_) ctl_->mark_broken(ctl_->rank());
       go_broken(why);
       break;
     }
@@ -478,6 +566,7 @@ void LiveServer::launcher_loop() {
     cv_done_.notify_all();
     cv_space_.notify_all();
   }
+  if (ctl_ && !closing_posted_) ctl_->set_closing(true);
   // whatever is still queued will not be launched
   std::vector<Pending> orphans;
   {
@@ -493,6 +582,32 @@ void LiveServer::launcher_loop() {
   }
   if (!orphans.empty())
     fail_all(orphans, kUnavailable, broken_ ? "server unavailable: " + error_ : "server stopped before the request ran");
+}
+
+void LiveServer::watcher_loop() {
+  for (;;) {
+    const uint32_t seen = ctl_->bell();
+    ctl_->heartbeat();
+    if (!broken_) {
+      const int by = ctl_->broken_by();
+      if (by >= 0 && by != ctl_->rank()) {
+        go_broken("rank " + std::to_string(by) + " gave up on the cluster");
+      } else {
+        const int silent = ctl_->silent_peer(cfg_.peer_timeout_us);
+        if (silent >= 0) {
+          ctl_->mark_broken(ctl_->rank());
+          go_broken("rank " + std::to_string(silent) + " stopped answering (no heartbeat for " +
+                    std::to_string(cfg_.peer_timeout_us / 1000) + " ms)");
+        }
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (watcher_stop_) break;
+      if (launcher_idle_.load(std::memory_order_seq_cst) || broken_) cv_launch_.notify_all();
+    }
+    ctl_->wait_bell(seen, cfg_.heartbeat_us);
+  }
 }
 
 void LiveServer::completer_loop() {
@@ -572,7 +687,6 @@ void LiveServer::completer_loop() {
 void LiveServer::resume() {
   std::lock_guard<std::mutex> lk(mu_);
   paused_ = false;
-  last_launch_us_ = now_us();
   cv_launch_.notify_all();
 }
 
@@ -583,8 +697,18 @@ void LiveServer::close() {
     cv_launch_.notify_all();
     cv_space_.notify_all();
   }
+  // cluster mode: the launcher keeps joining the other ranks' steps until
+  // every rank is closing (the watcher keeps the heartbeat going meanwhile)
   if (launcher_.joinable()) launcher_.join();
   if (completer_.joinable()) completer_.join();
+  if (watcher_.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      watcher_stop_ = true;
+    }
+    ctl_->ring();
+    watcher_.join();
+  }
 }
 
 LiveStats LiveServer::stats() const {

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "arena.h"
+#include "step_control.h"
 
 namespace dtfs {
 namespace runtime {
@@ -95,17 +96,16 @@ struct LiveConfig {
   int64_t varint_chunks = 0;       // GPU varint decode capacity (arena.h)
   int64_t max_pending = 1 << 16;   // admitted, unfinished requests; beyond: RESOURCE_EXHAUSTED
   bool eager_when_idle = true;     // no step in flight: launch what is queued right away
-  // Fan-out (collectives inside the step): every rank must launch the same
-  // steps, so every step uses the largest bucket and an empty step is
-  // launched after batch_timeout_us without requests. max_steps >= 0 stops
-  // launching after that many steps (a fixed-length run on every rank).
-  bool lockstep = false;
-  int64_t max_steps = -1;
   int64_t step_timeout_us = 10'000'000;  // a GPU step taking longer = the device / a peer is gone
-  // Launch nothing until resume() (requests are admitted and queue). A
-  // lockstep server whose step issues torch.distributed collectives from the
-  // launcher thread must not start its empty-step cadence before every rank
-  // has finished its own start-up collectives.
+  // Cluster mode (a StepControl is given: collectives inside the step): steps
+  // are agreed with the other ranks (step_control.h). A peer whose heartbeat
+  // is older than peer_timeout_us breaks the cluster; heartbeat_us is the
+  // watcher's period.
+  int64_t peer_timeout_us = 5'000'000;
+  int64_t heartbeat_us = 20'000;
+  // Launch nothing until resume() (requests are admitted and queue): a server
+  // whose step issues torch.distributed collectives from the launcher thread
+  // must not launch before every rank has finished its start-up collectives.
   bool start_paused = false;
   // > 0: requests with raw tensor_content int64 ids + fp32 weights are
   // narrowed by the submitting thread while it copies them (runtime/narrow.h):
@@ -122,6 +122,9 @@ struct LiveStats {
   int64_t submitted = 0, rejected = 0, completed = 0, failed = 0, expired = 0;
   int64_t steps = 0, rows = 0, padded_rows = 0, empty_steps = 0;
   int64_t full_steps = 0, timeout_steps = 0, eager_steps = 0, blocked_submits = 0, narrowed = 0;
+  // cluster mode: steps this rank proposed / joined with a batch of its own /
+  // joined with nothing queued (empty_steps counts those too)
+  int64_t proposed_steps = 0, joined_steps = 0;
   double copy_us = 0, build_us = 0, launch_us = 0, wait_us = 0, encode_us = 0;
   bool broken = false;
   std::string error;
@@ -130,7 +133,9 @@ struct LiveStats {
 class LiveServer {
  public:
   // arenas: pinned host buffers of ArenaLayout capacity (>= 2 + depth of them).
-  LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas);
+  // ctl: cluster mode (every step agreed with the other ranks), or null.
+  LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas,
+             StepControl* ctl = nullptr);
   ~LiveServer();
   LiveServer(const LiveServer&) = delete;
   LiveServer& operator=(const LiveServer&) = delete;
@@ -176,6 +181,7 @@ class LiveServer {
 
   void launcher_loop();
   void completer_loop();
+  void watcher_loop();  // cluster mode: heartbeats, peer liveness, wakes an idle launcher
   int bucket_for(int64_t rows) const;
   int64_t need_of(int64_t len, int64_t rows) const;
   void fail_all(std::vector<Pending>& ps, int code, const std::string& msg);
@@ -184,6 +190,7 @@ class LiveServer {
 
   StepBackend* backend_;
   LiveConfig cfg_;
+  StepControl* ctl_ = nullptr;
   int64_t max_rows_ = 0;
   int64_t arena_budget_ = 0;  // payload bytes a batch may plan for (see need_of)
 
@@ -198,14 +205,16 @@ class LiveServer {
   int next_slot_ = 0;
   int inflight_ = 0;
   int64_t pending_ = 0;
-  int64_t steps_launched_ = 0, last_launch_us_ = 0;
+  int64_t steps_launched_ = 0;
+  bool closing_posted_ = false, watcher_stop_ = false;
+  std::atomic<bool> launcher_idle_{false};
   std::deque<InFlight> q_done_;
   bool closing_ = false, launcher_exited_ = false, paused_ = false;
   std::atomic<bool> broken_{false};
   std::string error_;
   LiveStats st_;
 
-  std::thread launcher_, completer_;
+  std::thread launcher_, completer_, watcher_;
 };
 
 }  // namespace runtime

@@ -15,24 +15,11 @@ inline int32_t mod_scalar(int64_t v, int64_t m) {
   return int32_t(r);
 }
 
-inline uint16_t bf16_scalar(uint32_t u) {
-  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x0040u);  // quiet NaN, sign kept
-  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
-
 void narrow_ids_scalar(const uint8_t* src, int32_t* dst, int64_t n, int64_t m) {
   for (int64_t i = 0; i < n; ++i) {
     int64_t v;
     std::memcpy(&v, src + 8 * i, 8);
     dst[i] = mod_scalar(v, m);
-  }
-}
-
-void narrow_wts_scalar(const uint8_t* src, uint16_t* dst, int64_t n) {
-  for (int64_t i = 0; i < n; ++i) {
-    uint32_t u;
-    std::memcpy(&u, src + 4 * i, 4);
-    dst[i] = bf16_scalar(u);
   }
 }
 
@@ -76,30 +63,6 @@ __attribute__((target("avx2,fma"))) void narrow_ids_avx2(const uint8_t* src, int
   narrow_ids_scalar(src + 8 * i, dst + i, n - i, m);
 }
 
-__attribute__((target("avx2"))) void narrow_wts_avx2(const uint8_t* src, uint16_t* dst, int64_t n) {
-  const __m256i one = _mm256_set1_epi32(1);
-  const __m256i bias = _mm256_set1_epi32(0x7fff);
-  const __m256i absmask = _mm256_set1_epi32(0x7fffffff);
-  const __m256i inf = _mm256_set1_epi32(0x7f800000);
-  const __m256i qnan = _mm256_set1_epi32(0x00400000);
-  int64_t i = 0;
-  for (; i + 16 <= n; i += 16) {
-    __m256i out[2];
-    for (int h = 0; h < 2; ++h) {
-      const __m256i u = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 4 * (i + 8 * h)));
-      const __m256i rnd = _mm256_add_epi32(bias, _mm256_and_si256(_mm256_srli_epi32(u, 16), one));
-      __m256i r = _mm256_srli_epi32(_mm256_add_epi32(u, rnd), 16);
-      const __m256i nan = _mm256_cmpgt_epi32(_mm256_and_si256(u, absmask), inf);
-      const __m256i keep = _mm256_srli_epi32(_mm256_or_si256(u, qnan), 16);
-      out[h] = _mm256_blendv_epi8(r, keep, nan);
-    }
-    // 2 x 8 dwords (each < 2^16) -> 16 words in order
-    const __m256i packed = _mm256_permute4x64_epi64(_mm256_packus_epi32(out[0], out[1]), 0xD8);
-    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + i), packed);
-  }
-  narrow_wts_scalar(src + 4 * i, dst + i, n - i);
-}
-
 const bool g_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
 
 }  // namespace
@@ -107,11 +70,6 @@ const bool g_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fm
 void narrow_ids(const uint8_t* src, int32_t* dst, int64_t n, int64_t modulo) {
   if (g_avx2) narrow_ids_avx2(src, dst, n, modulo);
   else narrow_ids_scalar(src, dst, n, modulo);
-}
-
-void narrow_wts(const uint8_t* src, uint16_t* dst, int64_t n) {
-  if (g_avx2) narrow_wts_avx2(src, dst, n);
-  else narrow_wts_scalar(src, dst, n);
 }
 
 }  // namespace runtime

@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -99,6 +100,35 @@ void StepRunner::ensure_fanout_streams() {
   }
 }
 
+// An async copy that fails is a server error, never retried with another
+// direction: the failure record says which memory HIP saw (the round-2 retry of
+// hipErrorInvalidMemcpyDirection as hipMemcpyDefault hid the cause).
+void StepRunner::copy_checked(void* dst, const void* src, int64_t nbytes, hipMemcpyKind kind, hipStream_t st,
+                              int slot, const char* what) {
+  const hipError_t e = hipMemcpyAsync(dst, src, size_t(nbytes), kind, st);
+  if (e == hipSuccess) return;
+  (void)hipGetLastError();
+  auto describe = [](const void* p) {
+    hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof(at));
+    const hipError_t q = hipPointerGetAttributes(&at, p);
+    char buf[160];
+    if (q != hipSuccess) {
+      std::snprintf(buf, sizeof(buf), "%p (no HIP attributes: %s)", p, hipGetErrorString(q));
+    } else {
+      std::snprintf(buf, sizeof(buf), "%p (type %d, device %d, host %p, dev %p)", p, int(at.type), at.device,
+                    at.hostPointer, at.devicePointer);
+    }
+    (void)hipGetLastError();
+    return std::string(buf);
+  };
+  const std::string msg = std::string("hipMemcpyAsync(") + what + ", slot " + std::to_string(slot) + ", " +
+                          std::to_string(nbytes) + " B): " + hipGetErrorString(e) + "; dst " + describe(dst) +
+                          ", src " + describe(src);
+  std::fprintf(stderr, "[step_runner] %s\n", msg.c_str());
+  throw std::runtime_error(msg);
+}
+
 void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
                      bool gated) {
   hipStream_t st = copy_;
@@ -119,21 +149,7 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
   if (used_[slot] && (copy_wait_always_ || !observed_[slot].load(std::memory_order_acquire)))
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
   if (gated && last_gate_slot_ >= 0) ck(hipStreamWaitEvent(st, gate_[last_gate_slot_], 0), "hipStreamWaitEvent(gate)");
-  if (nbytes > 0) {
-    hipError_t e = hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyHostToDevice, st);
-    if (e == hipErrorInvalidMemcpyDirection) {
-      // Seen once on MI355X (ROCm 7.2) after thousands of identical copies from
-      // the same pinned arena into the same device buffer: the runtime's
-      // pointer classification rejected the direction. Let it infer the
-      // direction from the pointers instead of failing the whole server.
-      (void)hipGetLastError();
-      static std::atomic<bool> warned{false};
-      if (!warned.exchange(true))
-        std::fprintf(stderr, "[step_runner] hipMemcpyAsync(H2D) returned invalid direction; retrying as hipMemcpyDefault\n");
-      e = hipMemcpyAsync(dst, src, size_t(nbytes), hipMemcpyDefault, st);
-    }
-    ck(e, "hipMemcpyAsync(H2D)");
-  }
+  if (nbytes > 0) copy_checked(dst, src, nbytes, hipMemcpyHostToDevice, st, slot, "H2D");
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
   if (host_wait_h2d_ && consumer == compute_ && nbytes > 0) {
     // The launcher thread waits for the copy instead of the compute queue:
@@ -183,14 +199,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   ck(hipStreamWaitEvent(egress_, fwd_done_[slot], 0), "hipStreamWaitEvent(egress)");
   if (s.mode == 0) s.cout->alltoall(s.scores, s.back, s.out_bytes, egress_);
   else s.cout->gather(s.scores, s.back, s.out_bytes, 0, egress_);
-  if (s.d2h_bytes > 0) {
-    hipError_t e = hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_);
-    if (e == hipErrorInvalidMemcpyDirection) {  // the runtime quirk handled in h2d() above
-      (void)hipGetLastError();
-      e = hipMemcpyAsync(s.h_out, s.back, s.d2h_bytes, hipMemcpyDefault, egress_);
-    }
-    ck(e, "hipMemcpyAsync(D2H)");
-  }
+  if (s.d2h_bytes > 0) copy_checked(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_, slot, "D2H");
   ck(hipEventRecord(done_[slot], egress_), "hipEventRecord(done)");
   used_[slot] = 1;
 }
@@ -361,6 +370,16 @@ bool StepRunner::wait_for(int slot, int64_t timeout_us, const std::vector<comm::
       }
       if (el < 2000) std::this_thread::yield();
       else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+  // the step finished - but a peer exchange that timed out also finishes
+  // (its kernel exits), so a step is only done if no communicator failed
+  for (auto* c : comms) {
+    if (!c) continue;
+    std::string ce = c->async_error();
+    if (!ce.empty()) {
+      *err = "RCCL: " + ce;
+      return false;
     }
   }
   observed_[slot].store(true, std::memory_order_release);

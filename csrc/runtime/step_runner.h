@@ -137,6 +137,8 @@ class StepRunner {
   int device_;
   int event_mode_ = 0;
   unsigned done_flags() const;
+  void copy_checked(void* dst, const void* src, int64_t nbytes, hipMemcpyKind kind, hipStream_t st, int slot,
+                    const char* what);
   void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
            bool gated = false);
   int n_copy_ = 1;

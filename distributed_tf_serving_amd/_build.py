@@ -42,12 +42,14 @@ NATIVE_SOURCES = [
     "runtime/live_server.cpp",
     "runtime/loadgen.cpp",
     "runtime/narrow.cpp",
+    "runtime/step_control.cpp",
 ]
 HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp", "runtime/serving_loop.cpp",
                     "runtime/kernel_seq.cpp",
                     # shared with _native (the loop parses arenas / encodes responses itself)
                     "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp", "runtime/trace.cpp",
-                    "runtime/batcher.cpp", "runtime/live_server.cpp", "runtime/loadgen.cpp", "runtime/narrow.cpp"]
+                    "runtime/batcher.cpp", "runtime/live_server.cpp", "runtime/loadgen.cpp", "runtime/narrow.cpp",
+                    "runtime/step_control.cpp"]
 
 
 def _torch_paths():

@@ -406,8 +406,6 @@ class FanoutEngine:
                 h = self.launch(B, slot, nbytes=0 if self.ingest == "arena" else None)
             got = h.wait().clone()
             if rows:
-                if self.layout.narrow:  # the exchanged rows carry bf16 weights
-                    wts = wts.to(torch.bfloat16).float()
                 want = self.ex.model(ids.to(self.dev), wts.to(self.dev)).float().cpu()
                 diff = (got - want).abs().max().item()
                 ok = bool(diff <= atol)

@@ -1,13 +1,22 @@
-"""Multi-GPU model server: one front door fanning candidates out to every GPU.
+"""Multi-GPU model server: requests fanned out over every GPU of the node.
 
 The reference client fans each request's candidates out to N TF-Serving hosts
 itself (reference DCNClient.java:46-74 split, :146-164 dispatch + join). Here
-that fan-out moves inside one node: rank 0 runs the PredictionService front
-door (gRPC and/or in-process) and the dynamic batcher; every batch of world x B
-candidate rows is scattered over the GPUs by RCCL (parallel/fanout.py, scatter
-mode), each GPU scores its B rows, and the scores are gathered back. Ranks > 0
-run :func:`ClusterServer.serve_follower`: per step they receive the step's
-(bucket, slot) over a small gloo control channel and join its collectives.
+that fan-out moves inside one node, onto the native live server of every rank
+(csrc/runtime/live_server.cpp):
+
+``scatter``   rank 0 runs the PredictionService front door (gRPC and/or
+              in-process); each batch of up to world x B candidate rows is
+              scattered over the GPUs (RCCL / the one-shot peer kernel), each
+              GPU scores its share, the scores are gathered back to rank 0.
+``alltoall``  every rank is a front door (gRPC port + rank); each rank's rows
+              are split over all GPUs and the scores return to it.
+
+Steps are agreed through a shared-memory step control (parallel/control.py,
+csrc/runtime/step_control.h): a step runs only when some rank has requests
+(an idle cluster launches nothing), at the smallest padding bucket that holds
+every rank's batch, so a lone request costs a small step, not a full one.
+No Python runs per step or per request on any rank.
 
     torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m distributed_tf_serving_amd.serving.cluster \\
         --preset deepfm_fanout4 --port 9999
@@ -15,34 +24,34 @@ run :func:`ClusterServer.serve_follower`: per step they receive the step's
 Failure handling (the reference has none: a failed shard kills the requester
 thread, reference DCNClient.java:158-159, :185-188):
 
-* every GPU step wait is bounded (``FanoutEngine.step_timeout_s``) and polls
-  the RCCL communicators' asynchronous errors; a step that does not finish
-  marks rank 0's scheduler BROKEN: in-flight and queued requests fail
-  UNAVAILABLE, later ones immediately, the communicators are aborted and the
-  followers are told to stop (best effort);
-* a launch that fails after the followers were told about the step also
-  breaks the cluster (the ranks' collective sequences no longer match);
-* rank 0 sends a heartbeat on the control channel when idle; a follower that
-  hears nothing for ``control_timeout_s`` (rank 0 is gone) exits non-zero;
-  a follower that loses its peers fails its step wait and exits non-zero;
-* a watchdog thread on rank 0 polls :meth:`ClusterServer.health`.
+* every GPU step wait is bounded and polls the communicators' asynchronous
+  errors; a rank whose step does not finish, or that cannot agree a step with
+  its peers within the step timeout, breaks the cluster (a sticky flag in the
+  shared segment): in-flight and queued requests fail UNAVAILABLE, later ones
+  immediately, and the communicators are aborted so no peer hangs;
+* every rank's watcher thread heartbeats into the segment; a rank silent for
+  ``peer_timeout_s`` (a dead process) breaks the cluster the same way;
+* with ``recover=True`` rank 0 then rebuilds the cluster over the surviving
+  ranks (fresh step control and communicators, candidates re-split over the
+  survivors, same processes) and resumes serving: the requests in flight when
+  the rank died fail UNAVAILABLE once, later ones succeed.
 """
 from __future__ import annotations
 
 import argparse
-import collections
 import datetime
 import logging
 import os
 import signal
 import threading
 import time
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..config import Config, load_preset
+from ..parallel.control import create_control, default_store
 from ..parallel.dist import DistContext, init_from_env, shutdown
 from ..utils.gc_tuning import tune_for_serving
 from .registry import ModelRegistry
@@ -51,125 +60,135 @@ from .service import PredictionServiceImpl
 
 log = logging.getLogger(__name__)
 
-STOP = -1
-HEARTBEAT = 0  # bucket 0: no step, rank 0 is alive
-
-
-class StepControl:
-    """Rank 0 -> followers: (bucket, slot) of every step, over a CPU gloo group
-    (a 16-byte broadcast per step; the data itself moves over RCCL). Rank 0
-    sends heartbeats while idle, so a follower can tell an idle server from a
-    dead one within ``timeout_s``."""
-
-    def __init__(self, ctx: DistContext, timeout_s: float = 30.0, heartbeat_s: float = 1.0):
-        self.ctx = ctx
-        self.timeout_s = timeout_s
-        self.heartbeat_s = heartbeat_s
-        self.group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
-        self._buf = torch.zeros(2, dtype=torch.int64)
-        self._lock = threading.Lock()
-        self._last_send = time.monotonic()
-        self._hb: Optional[threading.Thread] = None
-        self._stop = threading.Event()
-
-    def send(self, B: int, slot: int) -> None:
-        with self._lock:
-            self._buf[0], self._buf[1] = int(B), int(slot)
-            dist.broadcast(self._buf, src=0, group=self.group)
-            self._last_send = time.monotonic()
-
-    def recv(self):
-        dist.broadcast(self._buf, src=0, group=self.group)
-        return int(self._buf[0]), int(self._buf[1])
-
-    def start_heartbeat(self) -> None:
-        def run():
-            while not self._stop.wait(self.heartbeat_s / 2):
-                if time.monotonic() - self._last_send >= self.heartbeat_s:
-                    try:
-                        self.send(HEARTBEAT, 0)
-                    except Exception as e:  # noqa: BLE001 - a follower is gone
-                        log.error("control heartbeat failed: %s", e)
-                        return
-
-        self._hb = threading.Thread(target=run, name="dtfs-heartbeat", daemon=True)
-        self._hb.start()
-
-    def stop(self) -> None:
-        self._stop.set()
-        if self._hb is not None:
-            self._hb.join(timeout=5)
-        self.send(STOP, 0)
-
 
 class ClusterServer:
-    """Every rank constructs one (collective); rank 0 serves, the rest follow."""
+    """Every rank constructs one (collective at start-up); the front-door
+    rank(s) serve, the others follow until ``stop``."""
 
     def __init__(self, cfg: Config, ctx: DistContext, slots: int = 3, self_check: bool = True,
                  control_timeout_s: float = 30.0, step_timeout_s: Optional[float] = None,
-                 follower_fault: Optional[dict] = None):
+                 follower_fault: Optional[dict] = None, mode: str = "scatter", recover: bool = False):
         self.cfg, self.ctx = cfg, ctx
         self.rank = ctx.rank if ctx.is_distributed else 0
-        mode = "scatter" if ctx.is_distributed else "local"
-        self.engine = build_engine(cfg, ctx.device, slots, ctx=ctx, mode=mode)
+        self.world = ctx.world if ctx.is_distributed else 1
+        self.mode = mode if self.world > 1 else "local"
+        if self.mode not in ("scatter", "alltoall", "local"):
+            raise ValueError("mode must be scatter, alltoall or local")
         if step_timeout_s is not None:
-            self.engine.step_timeout_s = step_timeout_s
-        if self_check and mode != "local":
-            B = self.engine.ex.buckets[-1]
-            if not self.engine.self_check(B):
-                log.warning("fan-out self-check failed on some rank; serving on the torch.distributed path")
-        self.ctrl = StepControl(ctx, timeout_s=control_timeout_s) if ctx.is_distributed else None
-        self.depth = max(1, slots - 1)
+            cfg.serving.step_timeout_s = float(step_timeout_s)
+        cfg.serving.peer_timeout_s = float(control_timeout_s)
+        self.slots = slots
+        self.self_check_on = self_check
+        self.follower_fault = follower_fault or {}
+        self.recover_on = recover
+        self.epoch = 0
+        self.members: List[int] = list(range(self.world))  # original ranks serving in this epoch
         self.registry: Optional[ModelRegistry] = None
         self.service: Optional[PredictionServiceImpl] = None
         self.front = None
         self.metrics = None
-        self.steps_followed = 0
-        self.follower_fault = follower_fault or {}
-        self._watchdog: Optional[threading.Thread] = None
         self._stopping = threading.Event()
-        self.sched = None
-        if self.rank == 0:
-            on_launch = self.ctrl.send if self.ctrl is not None else None
-            self.registry = ModelRegistry()
-            servable = build_servable(cfg, slots=slots, engine=self.engine, on_launch=on_launch)
-            self.sched = servable.scheduler
-            if hasattr(self.sched, "on_broken"):
-                self.sched.on_broken = self._on_broken
-            self.registry.load(servable)
-            self.service = PredictionServiceImpl(self.registry, cfg.serving.request_timeout_s)
-            if self.ctrl is not None:
-                self.ctrl.start_heartbeat()
-                self._watchdog = threading.Thread(target=self._watch, name="dtfs-watchdog", daemon=True)
-                self._watchdog.start()
+        self._lock = threading.RLock()
+        self.recoveries = 0
+        self.engine = self.ctl = self.sched = None
+        self._build(ctx, first=True)
+        if self.serves and self.world > 1:
+            self._watchdog = threading.Thread(target=self._watch, name="dtfs-watchdog", daemon=True)
+            self._watchdog.start()
 
-    # -- failure handling (rank 0) ----------------------------------------------
-    def _on_broken(self, reason: str) -> None:
-        log.error("cluster broken: %s - aborting communicators, stopping followers", reason)
-        try:
-            self.engine.abort()
-        except Exception:  # noqa: BLE001
-            log.exception("communicator abort failed")
+    # -- construction -------------------------------------------------------------
+    @property
+    def serves(self) -> bool:
+        """This rank is a front door (rank 0; every rank in alltoall mode)."""
+        return self.rank == 0 or self.mode == "alltoall"
 
-    def _watch(self, period_s: float = 0.5) -> None:
+    def _module(self):
+        from ..ops import hip, native
+
+        return hip() if self.ctx.device.type == "cuda" else native()
+
+    def _build(self, ctx: DistContext, first: bool, store=None) -> None:
+        """Engine + step control + live server of this rank for ``ctx`` (the
+        original job, or the survivors after a rebuild)."""
+        world = ctx.world if ctx.is_distributed else 1
+        mode = self.mode if world > 1 else "local"
+        group = None
+        if world > 1 and ctx.device.type != "cuda":
+            # the step's gloo collectives run on the live server's launcher
+            # thread: their own group, never interleaved with other traffic
+            group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=self.cfg.serving.step_timeout_s))
+        eng = build_engine(self.cfg, ctx.device, self.slots, ctx=ctx, mode=mode, group=group)
+        eng.step_timeout_s = self.cfg.serving.step_timeout_s
+        if self.self_check_on and mode != "local":
+            B = eng.ex.buckets[-1]
+            if not eng.self_check(B, seed=self.epoch):
+                raise RuntimeError("fan-out self-check failed: the native step's scores differ from a local forward")
+        ctl = None
+        if world > 1 and eng.lockstep:
+            ctl = create_control(self._module(), world, ctx.rank, store=store,
+                                 prefix=f"dtfs/ctl/cluster/{self.epoch}")
+        servable = build_servable(self.cfg, slots=self.slots, engine=eng, control=ctl)
+        with self._lock:
+            self.engine, self.ctl, self.sched, self.ctx = eng, ctl, servable.scheduler, ctx
+            if self.serves:
+                if self.registry is None:
+                    self.registry = ModelRegistry()
+                    self.registry.load(servable)
+                    self.service = PredictionServiceImpl(self.registry, self.cfg.serving.request_timeout_s)
+                else:
+                    self.registry.replace(servable)
+        if ctl is not None:
+            if world > 1 and dist.is_initialized() and first:
+                dist.barrier(group=group)  # every rank finished its start-up collectives
+            servable.scheduler.resume()
+
+    # -- failure handling -----------------------------------------------------------
+    def _watch(self, period_s: float = 0.05) -> None:
+        """Front door: turn an asynchronous communicator error into a broken
+        cluster, and (``recover``) rebuild over the survivors."""
         while not self._stopping.wait(period_s):
             err = self.health()
-            if err and self.sched is not None and hasattr(self.sched, "mark_broken"):
-                self.sched.mark_broken(f"communicator error: {err}")
-                return
+            if err and self.ctl is not None and self.ctl.broken_by < 0:
+                log.error("communicator error on rank %d: %s", self.rank, err)
+                self.ctl.mark_broken(self.rank)
+            if self.broken and self.recover_on and self.rank == 0 and not self._stopping.is_set():
+                try:
+                    self._recover_leader()
+                except Exception:  # noqa: BLE001
+                    log.exception("cluster recovery failed; staying unavailable")
+                    return
 
     @property
     def broken(self) -> Optional[str]:
-        return getattr(self.sched, "broken", None)
+        s = self.sched
+        if s is None or not getattr(s, "broken", False):
+            return None
+        return s.stats().get("error") or "broken"
 
-    # -- rank 0 -------------------------------------------------------------------
+    def health(self) -> Optional[str]:
+        """First asynchronous communicator error of this rank (None = healthy)."""
+        return self.engine.comm_error() if self.engine is not None and self.engine.native_fanout_active else None
+
+    # -- recovery (serving/cluster.py docstring; SURVEY.md §5.3) ----------------------
+    def _survivors(self, ctl, wait_s: float) -> List[int]:
+        """Ranks of the current epoch whose heartbeat is fresh (index order)."""
+        alive = []
+        for r in range(ctl.world):
+            if r == ctl.rank or ctl.peer_alive(r, wait_s):
+                alive.append(r)
+        return alive
+
+    def _recover_leader(self) -> None:
+        raise NotImplementedError
+
+    # -- front door ---------------------------------------------------------------------
     def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32,
                    monitoring_port: Optional[int] = None) -> int:
         """monitoring_port: also serve Prometheus metrics (serving/monitoring.py)."""
         from .grpc_server import GrpcFrontDoor
         from .monitoring import ServingMetrics
 
-        assert self.rank == 0, "only rank 0 is a front door"
+        assert self.serves, "this rank is not a front door"
         self.metrics = ServingMetrics(self.registry)
         self.front = GrpcFrontDoor(self.service, port=port, host=host, max_workers=max_workers,
                                    metrics=self.metrics).start()
@@ -177,66 +196,62 @@ class ClusterServer:
             self.metrics.serve_http(monitoring_port, host)
         return self.front.port
 
-    # -- ranks > 0 ----------------------------------------------------------------
+    # -- followers ----------------------------------------------------------------------
     def serve_follower(self) -> int:
-        """Join every step rank 0 launches until it sends STOP; returns steps
-        served. Raises when rank 0 goes silent or a step cannot finish."""
-        assert self.rank != 0 and self.ctrl is not None
-        inflight = collections.deque()
+        """A rank without a front door: its live server joins every step the
+        front door proposes. Returns the steps served once the front door
+        stops the cluster; raises when the cluster breaks."""
+        if self.ctl is None:
+            return 0
         fault_after = int(self.follower_fault.get("after", -1))
-        launched = 0
         while True:
-            B, slot = self.ctrl.recv()  # times out (raises) if rank 0 is gone
-            if B == STOP:
-                break
-            if B == HEARTBEAT:
-                continue
-            if fault_after >= 0 and launched >= fault_after:
-                log.error("fault injection: follower rank %d exits before step %d", self.rank, launched)
-                os._exit(int(self.follower_fault.get("code", 17)))
-            inflight.append(self.engine.launch(B, slot, nbytes=0 if self.engine.ingest == "arena" else None))
-            launched += 1
-            if len(inflight) >= self.depth:
-                inflight.popleft().wait()  # bounded (engine.step_timeout_s)
-                self.steps_followed += 1
-        while inflight:
-            inflight.popleft().wait()
-            self.steps_followed += 1
-        return self.steps_followed
+            ctl, sched = self.ctl, self.sched
+            if fault_after >= 0:
+                if sched.stats()["steps"] >= fault_after:
+                    log.error("fault injection: follower rank %d exits after %d steps", self.rank, fault_after)
+                    os._exit(int(self.follower_fault.get("code", 17)))
+                ctl.wait_event(0.002)
+            else:
+                ctl.wait_event(1.0)
+            if ctl.stop_requested:
+                steps = sched.stats()["steps"]
+                sched.close()
+                return steps
+            if ctl.broken_by >= 0 or sched.broken:
+                raise RuntimeError(f"cluster broken: {self.broken or f'rank {ctl.broken_by} gave up'}")
 
-    def health(self) -> Optional[str]:
-        """First asynchronous communicator error of this rank (None = healthy)."""
-        return self.engine.comm_error() if self.engine.native_fanout_active else None
-
+    # -- shutdown ---------------------------------------------------------------------------
     def stop(self) -> None:
         self._stopping.set()
-        if self.rank == 0:
-            if self.metrics is not None:
-                self.metrics.stop()
-            if self.front is not None:
-                self.front.stop()
-                self.front = None
-            if self.registry is not None:
-                self.registry.close()  # drains the batcher: every launched step completes
-            if self.ctrl is not None and not self.broken:
-                try:
-                    self.ctrl.stop()
-                except Exception as e:  # noqa: BLE001 - followers already gone
-                    log.warning("could not stop the followers: %s", e)
+        if self.metrics is not None:
+            self.metrics.stop()
+        if self.front is not None:
+            self.front.stop()
+            self.front = None
+        if self.ctl is not None and self.rank == 0:
+            self.ctl.request_stop()  # followers close their live servers too
+        if self.registry is not None:
+            self.registry.close()  # drains this rank's live server: every launched step completes
+        elif self.sched is not None:
+            self.sched.close()
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description="multi-GPU CTR model server (rank 0 = PredictionService front door)")
     ap.add_argument("--preset", default="deepfm_fanout4")
+    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall"],
+                    help="scatter: rank 0 is the only front door; alltoall: every rank serves on port + rank")
     ap.add_argument("--port", type=int, default=9999)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--grpc-workers", type=int, default=32)
     ap.add_argument("--monitoring-port", type=int, default=None,
                     help="serve Prometheus metrics over HTTP on this port (rank 0)")
-    ap.add_argument("--control-timeout-s", type=float, default=30.0,
-                    help="a follower that hears nothing from rank 0 this long exits")
+    ap.add_argument("--control-timeout-s", type=float, default=5.0,
+                    help="a rank silent (no heartbeat) this long breaks the cluster")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a GPU step not finished this long breaks the cluster (UNAVAILABLE)")
+    ap.add_argument("--recover", action="store_true",
+                    help="after a rank dies, rebuild the cluster over the survivors and keep serving")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="leave CPython's cyclic GC at its defaults (utils/gc_tuning.py)")
     ap.add_argument("--peer-comm", type=int, default=None,
@@ -248,14 +263,15 @@ def main(argv=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     ctx = init_from_env(timeout_s=max(60.0, a.control_timeout_s))
     srv = ClusterServer(load_preset(a.preset), ctx, control_timeout_s=a.control_timeout_s,
-                        step_timeout_s=a.step_timeout_s)
+                        step_timeout_s=a.step_timeout_s, mode=a.mode, recover=a.recover)
     rc = 0
     try:
-        if not a.no_gc_freeze:  # every rank, after warm-up, before traffic: a GC pause on a
-            tune_for_serving()  # follower stalls the step's collectives too
-        if srv.rank == 0:
-            port = srv.start_grpc(a.port, a.host, a.grpc_workers, a.monitoring_port)
-            print(f"serving on port {port} over {ctx.world} GPU(s)", flush=True)
+        if not a.no_gc_freeze:  # every rank, after warm-up, before traffic
+            tune_for_serving()
+        if srv.serves:
+            port = srv.start_grpc(a.port + (srv.rank if a.mode == "alltoall" else 0), a.host, a.grpc_workers,
+                                  a.monitoring_port if srv.rank == 0 else None)
+            print(f"rank {srv.rank}: serving on port {port} over {ctx.world} GPU(s) ({a.mode})", flush=True)
             signal.signal(signal.SIGTERM, lambda *_: srv.front.stop() if srv.front else None)
             try:
                 srv.front.wait()
@@ -263,7 +279,7 @@ def main(argv=None):
                 pass
         else:
             srv.serve_follower()
-    except Exception:  # noqa: BLE001 - a follower that lost rank 0 / its peers
+    except Exception:  # noqa: BLE001 - a follower that lost its peers
         log.exception("rank %d failed", srv.rank)
         rc = 3
     finally:

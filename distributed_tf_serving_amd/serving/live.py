@@ -47,9 +47,13 @@ class LiveScheduler:
     """The servable's batching scheduler, backed by the native live server."""
 
     def __init__(self, engine, serving_cfg, buckets: Optional[Sequence[int]] = None, n_arenas: Optional[int] = None,
-                 depth: Optional[int] = None, lockstep: bool = False, max_steps: int = -1,
-                 step_timeout_s: float = 10.0, model_name: Optional[str] = None, version: Optional[int] = None,
-                 start_paused: bool = False, narrow: Optional[bool] = None):
+                 depth: Optional[int] = None, control=None, step_timeout_s: float = 10.0,
+                 model_name: Optional[str] = None, version: Optional[int] = None, start_paused: bool = False,
+                 narrow: Optional[bool] = None, peer_timeout_s: float = 5.0):
+        """``control``: the job's StepControl (parallel/control.py) when the
+        step has collectives (fan-out, sharded tables): every step is then
+        agreed with the other ranks - launched only when some rank has work,
+        at the largest bucket any rank needs (csrc/runtime/step_control.h)."""
         if engine.ingest != "arena":
             raise ValueError("the live server needs an arena-ingest FanoutEngine")
         sc = serving_cfg
@@ -84,14 +88,14 @@ class LiveScheduler:
             batch_timeout_us=sc.batch_timeout_us,
             depth=depth, varint_chunks=self.layout.varint_chunks,
             max_pending=max(64, sc.max_queued_rows // max(1, min(self.buckets))),
-            lockstep=lockstep, max_steps=max_steps, step_timeout_us=int(step_timeout_s * 1e6),
+            step_timeout_us=int(step_timeout_s * 1e6), peer_timeout_us=int(peer_timeout_s * 1e6),
             start_paused=start_paused, narrow_modulo=self.narrow_modulo,
             caller_outputs=["sorted_prediction", "sorted_index"])  # service.RANKED_OUTPUTS
         if engine.cuda:
             from ..ops import hip
 
             spec = [(R, engine.loop_slots(B)) for B, R in zip(self.buckets, self.step_rows)]
-            self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas)
+            self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas, control)
         else:
             slots = self.ex.slots
             scores = [[engine.host_out(B, s) for B in self.buckets] for s in range(slots)]
@@ -100,7 +104,8 @@ class LiveScheduler:
             def forward(ai: int, slot: int, b: int) -> None:
                 engine.launch(buckets[b], slot, src=self.arenas[ai], nbytes=self.layout.capacity).wait()
 
-            self.srv = native().LiveServer(self.config, self.step_rows, scores, self.arenas, forward)
+            self.srv = native().LiveServer(self.config, self.step_rows, scores, self.arenas, forward, control)
+        self.control = control
         self.max_rows = int(self.srv.max_rows)
         self.OVERSIZE = int(native().STATUS_OVERSIZE)
         self.CALLER_PATH = int(native().STATUS_CALLER_PATH)

@@ -20,12 +20,13 @@ import torch
 
 @dataclass(frozen=True)
 class PackedLayout:
-    """``narrow_modulo`` > 0: the narrow row [int32 table rows x F | bf16
-    weights x F | pad to 8 bytes] - ids already hashed (id mod m, the model's
-    table size) and weights rounded to bf16, 6 bytes per field instead of 12.
-    The candidate fan-out exchanges rows in this form (half the xGMI bytes,
-    SURVEY.md §2.5 C1: "narrow ids to int32 and wts to bf16 first"); the
-    gather reads int32 rows and bf16 weights in place."""
+    """``narrow_modulo`` > 0: the narrow row [int32 table rows x F | fp32
+    weights x F] - ids already hashed (id mod m, the model's table size), 8
+    bytes per field instead of 12. The candidate fan-out exchanges rows in
+    this form (2/3 of the xGMI bytes); the gather reads
+    int32 rows and fp32 weights in place. Weights stay fp32 (not bf16): a
+    request's scores must not depend on its wire encoding or on the path it
+    took through the server."""
 
     fields: int
     narrow_modulo: int = 0
@@ -36,7 +37,7 @@ class PackedLayout:
 
     @property
     def row_bytes(self) -> int:
-        b = (6 if self.narrow else 12) * self.fields
+        b = (8 if self.narrow else 12) * self.fields
         return (b + 7) // 8 * 8
 
     @property
@@ -54,9 +55,9 @@ class PackedLayout:
         return buf[:, : self.fields]
 
     def wts(self, buf: torch.Tensor) -> torch.Tensor:
-        """fp32 [rows, F] row view (narrow: bf16)."""
+        """fp32 [rows, F] row view."""
         if self.narrow:
-            return buf.view(torch.bfloat16)[:, 2 * self.fields: 3 * self.fields]
+            return buf.view(torch.float32)[:, self.fields: 2 * self.fields]
         return buf.view(torch.float32)[:, 2 * self.fields: 3 * self.fields]
 
     def pack(self, ids: torch.Tensor, wts: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
@@ -64,7 +65,6 @@ class PackedLayout:
         buf = self.alloc(rows, device=ids.device) if out is None else out
         if self.narrow:
             ids = torch.remainder(ids.long(), self.narrow_modulo).to(torch.int32)
-            wts = wts.to(torch.bfloat16)
         self.ids(buf)[:rows].copy_(ids)
         self.wts(buf)[:rows].copy_(wts)
         return buf

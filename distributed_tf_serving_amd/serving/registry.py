@@ -57,6 +57,15 @@ class ModelRegistry:
         with self._lock:
             self._models.setdefault(servable.name, {})[servable.version] = servable
 
+    def replace(self, servable: Servable) -> Optional[Servable]:
+        """Swap in a servable for the same (name, version); the previous one is
+        returned, not closed (the caller drains it)."""
+        with self._lock:
+            vs = self._models.setdefault(servable.name, {})
+            old = vs.get(servable.version)
+            vs[servable.version] = servable
+            return old
+
     def unload(self, name: str, version: Optional[int] = None) -> None:
         with self._lock:
             vs = self._models.get(name, {})

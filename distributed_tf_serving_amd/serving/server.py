@@ -42,62 +42,67 @@ def pick_device(pref: str = "auto") -> torch.device:
     return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
 
 
-def live_enabled(cfg: Config, mode: str = "local", model=None) -> bool:
-    """The native live server serves local (one-rank) servables whose step can
-    be replayed natively: a CPU model, or a GPU model with HIP graphs and no
-    collectives inside its forward."""
+def live_enabled(cfg: Config, device: torch.device) -> bool:
+    """Servables run on the native live server: a CPU model (Python forward
+    behind the C++ core), or a GPU model whose step replays captured graphs."""
     sc = cfg.serving
-    if not sc.live or mode != "local":
-        return False
-    if model is not None and getattr(model, "has_collectives", False):
-        return False
-    return True
+    return bool(sc.live) and (device.type != "cuda" or sc.use_graphs)
 
 
 def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistContext] = None,
-                 mode: str = "local") -> FanoutEngine:
+                 mode: str = "local", group=None) -> FanoutEngine:
     """Model + executor + fan-out engine of one rank, every bucket prepared
     (HIP graphs captured). With ``ctx`` of a multi-rank job, DLRM tables are
-    sharded over the ranks (parallel/embedding_sharding.py). A servable of the
-    live server ingests request arenas (the GPU unpacks raw request bytes)."""
+    sharded over the ranks (parallel/embedding_sharding.py) and ``mode``
+    scatter / alltoall fans every batch out over the ranks. A servable of the
+    live server ingests request arenas (the GPU unpacks raw request bytes).
+    ``group``: process group of the step's collectives (CPU: a dedicated gloo
+    group, since they run on the live server's launcher thread)."""
     from ..parallel.embedding_sharding import build_parallel_model
 
     sc = cfg.serving
     dev = torch.device(device) if device is not None else (ctx.device if ctx is not None else pick_device(sc.device))
     ctx = ctx or DistContext(device=dev)
     model = build_parallel_model(cfg.model, dev, ctx)
+    world = ctx.world if ctx.is_distributed else 1
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
+    if mode == "alltoall" and world > 1:  # every rank's rows split evenly over the GPUs
+        buckets = [b for b in buckets if b % world == 0] or [sc.max_batch_rows * world]
     use_graphs = sc.use_graphs
-    live = live_enabled(cfg, mode, model)
-    if live and dev.type == "cuda" and not use_graphs:
-        live = False  # the native step replays captured graphs
+    live = live_enabled(cfg, dev)
     # rows exchanged between GPUs travel narrow (int32 rows + bf16 weights)
-    fanout = live and mode != "local" and ctx.is_distributed
+    fanout = live and mode != "local" and world > 1
     layout = layout_for(cfg.model, fanout) if fanout else PackedLayout(cfg.model.num_fields)
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=use_graphs, slots=slots)
     if live:
-        eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena",
-                           arena=ArenaLayout(cfg.model.num_fields, max_rows=max(buckets)))
+        rows_in = max(buckets) * (world if mode == "scatter" else 1)
+        eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", group=group,
+                           arena=ArenaLayout(cfg.model.num_fields, max_rows=rows_in))
     else:
-        eng = FanoutEngine(ex, ctx, mode=mode)
+        eng = FanoutEngine(ex, ctx, mode=mode, group=group)
     for B in buckets:
         eng.prepare(B)
     return eng
 
 
 def build_servable(cfg: Config, device=None, version: Optional[int] = None, slots: int = 3,
-                   engine: Optional[FanoutEngine] = None, on_launch=None) -> Servable:
+                   engine: Optional[FanoutEngine] = None, control=None) -> Servable:
+    """``control``: the job's StepControl (parallel/control.py) when the
+    engine's step has collectives (every rank's live server agrees on it)."""
     sc = cfg.serving
     eng = engine or build_engine(cfg, device, slots)
     model = eng.ex.model
     world = eng.world if eng.mode == "scatter" else 1
-    if eng.ingest == "arena" and eng.mode == "local" and on_launch is None:
+    if eng.ingest == "arena":
+        if eng.lockstep and eng.world > 1 and control is None:
+            raise ValueError("a multi-rank engine with collectives in its step needs a StepControl")
         sched = LiveScheduler(eng, sc, version=sc.version if version is None else version,
-                              step_timeout_s=sc.step_timeout_s)
+                              step_timeout_s=sc.step_timeout_s, control=control,
+                              peer_timeout_s=getattr(sc, "peer_timeout_s", 5.0), start_paused=control is not None)
     else:
         sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
                                   max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name,
-                                  fanout_world=world, on_launch=on_launch, max_request_rows=sc.max_request_rows)
+                                  fanout_world=world, max_request_rows=sc.max_request_rows)
     sig = model.signature()
     sigs = {sc.signature_name: Signature(inputs=sig["inputs"], outputs=sig["outputs"], method_name=sig["method_name"])}
     return Servable(name=sc.model_name, version=sc.version if version is None else version, model=model,

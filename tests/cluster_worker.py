@@ -1,0 +1,114 @@
+"""One rank of a multi-rank ClusterServer rehearsal (launched by
+torch.distributed.run from tests/test_cluster_server.py on CPU / gloo and from
+tests/test_multirank_gpu.py on the GPU box, ranks sharing its one GPU).
+
+Every front-door rank sends requests of assorted sizes concurrently through
+the in-process PredictionService (and, with --grpc, through the gRPC front
+door), compares every request's scores with a local forward of the same
+weights, and checks that an idle cluster launches no steps. Each rank writes
+``<out>/rank<r>.json``.
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall"])
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--grpc-port", type=int, default=0, help="> 0: also serve gRPC on port + rank and query it")
+    ap.add_argument("--requests", type=int, default=24)
+    ap.add_argument("--kill-rank", type=int, default=-1, help="this rank exits abruptly after --kill-after steps")
+    ap.add_argument("--kill-after", type=int, default=3)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.config import load_preset
+    from distributed_tf_serving_amd.ops import native
+    from distributed_tf_serving_amd.parallel.dist import init_from_env
+    from distributed_tf_serving_amd.serving.cluster import ClusterServer
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
+
+    ctx = init_from_env(timeout_s=120)
+    rank = ctx.rank
+    gpu = ctx.device.type == "cuda"
+    cfg = load_preset("deepfm_1gpu")
+    cfg.model.vocab_size = 100_000
+    if not gpu:  # small enough for gloo on a CPU test box
+        cfg.model.embed_dim, cfg.model.mlp_dims = 16, (32, 16)
+    cfg.serving.device = "cuda" if gpu else "cpu"
+    cfg.serving.max_batch_rows = 768
+    cfg.serving.allowed_batch_sizes = (96, 768)  # divisible by 1, 2, 3
+    cfg.serving.batch_timeout_us = 300
+    phase = dist.new_group(backend="gloo")
+    fault = {"after": a.kill_after} if rank == a.kill_rank else None
+    srv = ClusterServer(cfg, ctx, mode=a.mode, control_timeout_s=20, step_timeout_s=20, follower_fault=fault)
+    res = {"rank": rank, "serves": srv.serves}
+    if srv.serves:
+        model = srv.registry.resolve("DCN").model
+        synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=100 + rank)
+        reqs = []
+        for i in range(a.requests):
+            rows = [1, 37, 200, 96, 500, 7][i % 6]
+            ids, wts = synth.arrays(rows)
+            raw = i % 3 != 2  # raw tensor_content and packed typed fields
+            data = native().encode_predict_request("DCN", "serving_default", None,
+                                                   [("feat_ids", torch.from_numpy(ids)),
+                                                    ("feat_wts", torch.from_numpy(wts))], raw)
+            reqs.append((data, ids, wts))
+        steps0 = srv.sched.stats()["steps"]
+        with cf.ThreadPoolExecutor(8) as pool:
+            outs = list(pool.map(lambda r: srv.service.predict_bytes(r[0], 60.0), reqs))
+        diffs = []
+        for (data, ids, wts), resp in zip(reqs, outs):
+            got = T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+            want = model(torch.from_numpy(ids).to(ctx.device), torch.from_numpy(wts).to(ctx.device)).float().cpu()
+            diffs.append(float(np.abs(got - want.numpy()).max()))
+        res["max_diff"] = max(diffs)
+        res["n_checked"] = len(diffs)
+        res["steps_used"] = srv.sched.stats()["steps"] - steps0
+        if a.grpc_port:
+            from distributed_tf_serving_amd.client.backends import GrpcBackend
+
+            port = srv.start_grpc(a.grpc_port + (rank if a.mode == "alltoall" else 0), host="127.0.0.1")
+            be = GrpcBackend(f"127.0.0.1:{port}")
+            gd = []
+            for data, ids, wts in reqs[:4]:
+                resp = pb.PredictResponse.FromString(be.predict(data, timeout_s=60.0))
+                got = T.to_ndarray(resp.outputs["prediction_node"])
+                want = model(torch.from_numpy(ids).to(ctx.device), torch.from_numpy(wts).to(ctx.device)).float().cpu()
+                gd.append(float(np.abs(got - want.numpy()).max()))
+            be.close()
+            res["grpc_max_diff"] = max(gd)
+    dist.barrier(group=phase)  # every front door is done: the cluster is idle now
+    st0 = srv.sched.stats()["steps"]
+    time.sleep(0.3)
+    res["idle_steps"] = srv.sched.stats()["steps"] - st0
+    res["stats"] = {k: v for k, v in srv.sched.stats().items() if isinstance(v, (int, float))}
+    dist.barrier(group=phase)
+    if srv.serves:
+        srv.stop()
+    else:
+        res["followed"] = srv.serve_follower()
+        srv.stop()
+    res["broken"] = bool(srv.broken)
+    with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier(group=phase)
+
+
+if __name__ == "__main__":
+    main()

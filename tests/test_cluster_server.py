@@ -174,3 +174,39 @@ def test_cluster_dead_follower_fails_requests_instead_of_hanging():
     assert t_fail is not None and t_fail < 20, t_fail
     assert procs[die_rank].exitcode == 17
     assert res[1][1] in ("raised", "stopped"), res[1]
+
+
+def _run_worker(n, mode, out, extra=(), env_extra=None, timeout=240):
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "tests/cluster_worker.py",
+           "--mode", mode, "--out", str(out), *extra]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               DTFS_HOST_THREADS="1", **(env_extra or {}))
+    return subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world,mode", [(2, "alltoall"), (3, "scatter"), (3, "alltoall")])
+def test_native_cluster_serves_exact_scores_and_idles(tmp_path, world, mode):
+    """The ClusterServer on the native live server in both fan-out modes: every
+    front door's concurrent requests (raw and packed encodings, sizes that do
+    not divide by the world) score exactly like a local forward, over the
+    in-process service and the gRPC front door; an idle cluster launches no
+    step (the step control proposes steps only for queued work)."""
+    import json
+
+    p = _run_worker(world, mode, tmp_path, ("--grpc-port", str(_free_port())))
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    fronts = [r for r in res if r["serves"]]
+    assert len(fronts) == (world if mode == "alltoall" else 1)
+    for r in fronts:
+        assert r["max_diff"] < 1e-5 and r["grpc_max_diff"] < 1e-5, r
+        assert r["steps_used"] < r["n_checked"]  # requests were batched
+    for r in res:
+        assert r["idle_steps"] == 0 and not r["broken"], r
+    # every rank ran the same steps (each collective paired up)
+    assert len({r["stats"]["steps"] for r in res}) == 1, [r["stats"]["steps"] for r in res]

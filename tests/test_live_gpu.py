@@ -60,9 +60,7 @@ def test_concurrent_served_requests_match_eager_forward(server, raw):
     live = server.registry.resolve("DCN").scheduler
     for (data, ids, wts), resp in zip(reqs, outs):
         got = _scores(resp)
-        w = torch.from_numpy(wts).cuda()
-        if raw and live.narrow_modulo:  # host-narrowed ingest: weights arrive as bf16
-            w = w.to(torch.bfloat16).float()
+        w = torch.from_numpy(wts).cuda()  # every encoding keeps fp32 weights
         want = model(torch.from_numpy(ids).cuda(), w).float().cpu().numpy()
         np.testing.assert_allclose(got, want, atol=2e-5)
     st = live.stats()
@@ -78,7 +76,7 @@ def test_oversize_request_split(server):
     data = native().encode_predict_request("DCN", "", None, [("feat_ids", torch.from_numpy(ids)),
                                                              ("feat_wts", torch.from_numpy(wts))], True)
     got = _scores(server.service.predict_bytes(data, 30.0))
-    w = torch.from_numpy(wts).cuda().to(torch.bfloat16).float()  # split parts travel raw -> narrowed
+    w = torch.from_numpy(wts).cuda()  # split parts travel raw -> narrowed ids, fp32 weights
     want = model(torch.from_numpy(ids).cuda(), w).float().cpu().numpy()
     np.testing.assert_allclose(got, want, atol=2e-5)
 

@@ -32,7 +32,8 @@ def test_bench_ranks_sharing_one_gpu(n, mode, peer):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
            "--steps", "20", "--warmup", "4", "--prime-steps", "10", "--requests-per-gpu", "4", "--request-rows", "96", "--mode", mode,
-           "--pool", "8", "--client-threads", "2", "--qps", "0", "--step-timeout-s", "20"]
+           "--pool", "8", "--client-threads", "2", "--qps", "500", "--qps-seconds", "0.4", "--small-buckets", "96",
+           "--step-timeout-s", "20"]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
                DTFS_PEER_COMM=str(peer))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
@@ -41,7 +42,11 @@ def test_bench_ranks_sharing_one_gpu(n, mode, peer):
     assert len(line) == 1, p.stdout
     out = json.loads(line[0])
     assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    # the BASELINE's second metric at every N, and load-proportional stepping
+    assert out["p50_at_fixed_qps_ms"] > 0 and out["fixed_qps"]["errors"] == 0, out.get("fixed_qps")
+    assert out["config2_batch512"]["p50_ms"] > 0
     if mode != "local":
+        assert out["server"]["idle_steps_per_s"] == 0, out["server"]
         assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
         assert ("one-shot peer exchange" in out["config"]["parallelism"]) == (peer > 0), out["config"]["parallelism"]
 
@@ -70,3 +75,26 @@ def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
     par = out["config"]["parallelism"]
     assert f"embedding-mp{n}" in par and "native two-lane step program" in par, par
     assert ("one-shot peer exchange" in par) == (peer > 0), par
+
+
+@pytest.mark.parametrize("n,mode", [(2, "scatter"), (3, "alltoall")])
+def test_native_cluster_server_ranks_sharing_one_gpu(tmp_path, n, mode):
+    """serving/cluster.py on N ranks over RCCL: every front door's concurrent
+    requests (in-process and gRPC) score like a local forward of the same
+    weights, every rank runs the same steps, and an idle cluster runs none."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tests/cluster_worker.py",
+           "--mode", mode, "--out", str(tmp_path), "--grpc-port", str(_port())]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
+    fronts = [r for r in res if r["serves"]]
+    assert len(fronts) == (n if mode == "alltoall" else 1)
+    for r in fronts:
+        assert r["max_diff"] < 1e-4 and r["grpc_max_diff"] < 1e-4, r
+    for r in res:
+        assert r["idle_steps"] == 0 and not r["broken"], r
+    assert len({r["stats"]["steps"] for r in res}) == 1
