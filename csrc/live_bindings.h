@@ -54,6 +54,9 @@ inline void def_step_control(py::module& m) {
       .def(
           "silent_peer", [](const StepControl& c, double timeout_s) { return c.silent_peer(int64_t(timeout_s * 1e6)); },
           py::arg("timeout_s"))
+      .def(
+          "heartbeat_age", [](const StepControl& c, int r) { return double(c.heartbeat_age_us(r)) * 1e-6; },
+          py::arg("rank"), "seconds since the rank's last heartbeat")
       .def("set_closing", &StepControl::set_closing, py::arg("closing"))
       .def_property_readonly("all_closing", &StepControl::all_closing)
       .def("request_stop", &StepControl::request_stop)

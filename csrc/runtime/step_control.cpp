@@ -175,6 +175,13 @@ int StepControl::gather(uint64_t k, int64_t timeout_us, std::string* err) {
 
 void StepControl::heartbeat() { s_->ranks[rank_].heartbeat_us.store(now_us(), std::memory_order_release); }
 
+int64_t StepControl::heartbeat_age_us(int r) const {
+  if (r < 0 || r >= world_) throw std::out_of_range("step control: rank out of range");
+  int64_t hb = s_->ranks[r].heartbeat_us.load(std::memory_order_acquire);
+  if (hb == 0) hb = attach_us_;
+  return now_us() - hb;
+}
+
 int StepControl::silent_peer(int64_t timeout_us) const {
   const int64_t now = now_us();
   for (int r = 0; r < world_; ++r) {

@@ -95,6 +95,8 @@ class StepControl {
   // First peer whose heartbeat is older than timeout_us (-1: all alive). A peer
   // that never started is judged from `since_us` (this rank's attach time).
   int silent_peer(int64_t timeout_us) const;
+  // Microseconds since rank r's last heartbeat (its attach time if it never beat).
+  int64_t heartbeat_age_us(int r) const;
 
   void set_closing(bool v);
   bool all_closing() const;

@@ -71,6 +71,8 @@ class ClusterServer:
         self.cfg, self.ctx = cfg, ctx
         self.rank = ctx.rank if ctx.is_distributed else 0
         self.world = ctx.world if ctx.is_distributed else 1
+        self.orig_rank = self.rank  # rank in the original job (the current epoch's rank is self.rank)
+        self._store = default_store() if self.world > 1 else None
         self.mode = mode if self.world > 1 else "local"
         if self.mode not in ("scatter", "alltoall", "local"):
             raise ValueError("mode must be scatter, alltoall or local")
@@ -91,7 +93,7 @@ class ClusterServer:
         self._lock = threading.RLock()
         self.recoveries = 0
         self.engine = self.ctl = self.sched = None
-        self._build(ctx, first=True)
+        self._build(ctx, first=True, store=self._store)
         if self.serves and self.world > 1:
             self._watchdog = threading.Thread(target=self._watch, name="dtfs-watchdog", daemon=True)
             self._watchdog.start()
@@ -107,7 +109,7 @@ class ClusterServer:
 
         return hip() if self.ctx.device.type == "cuda" else native()
 
-    def _build(self, ctx: DistContext, first: bool, store=None) -> None:
+    def _build(self, ctx: DistContext, first: bool, store=None, model=None) -> None:
         """Engine + step control + live server of this rank for ``ctx`` (the
         original job, or the survivors after a rebuild)."""
         world = ctx.world if ctx.is_distributed else 1
@@ -117,7 +119,7 @@ class ClusterServer:
             # the step's gloo collectives run on the live server's launcher
             # thread: their own group, never interleaved with other traffic
             group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=self.cfg.serving.step_timeout_s))
-        eng = build_engine(self.cfg, ctx.device, self.slots, ctx=ctx, mode=mode, group=group)
+        eng = build_engine(self.cfg, ctx.device, self.slots, ctx=ctx, mode=mode, group=group, model=model)
         eng.step_timeout_s = self.cfg.serving.step_timeout_s
         if self.self_check_on and mode != "local":
             B = eng.ex.buckets[-1]
@@ -130,6 +132,7 @@ class ClusterServer:
         servable = build_servable(self.cfg, slots=self.slots, engine=eng, control=ctl)
         with self._lock:
             self.engine, self.ctl, self.sched, self.ctx = eng, ctl, servable.scheduler, ctx
+            self.rank, self.world = (ctx.rank, world) if world > 1 else (0, 1)
             if self.serves:
                 if self.registry is None:
                     self.registry = ModelRegistry()
@@ -138,7 +141,7 @@ class ClusterServer:
                 else:
                     self.registry.replace(servable)
         if ctl is not None:
-            if world > 1 and dist.is_initialized() and first:
+            if world > 1 and dist.is_initialized():
                 dist.barrier(group=group)  # every rank finished its start-up collectives
             servable.scheduler.resume()
 
@@ -151,9 +154,12 @@ class ClusterServer:
             if err and self.ctl is not None and self.ctl.broken_by < 0:
                 log.error("communicator error on rank %d: %s", self.rank, err)
                 self.ctl.mark_broken(self.rank)
-            if self.broken and self.recover_on and self.rank == 0 and not self._stopping.is_set():
+            if self.broken and self.recover_on and not self._stopping.is_set():
                 try:
-                    self._recover_leader()
+                    if self.rank == 0:
+                        self._recover_leader()
+                    elif not self._rejoin():
+                        return
                 except Exception:  # noqa: BLE001
                     log.exception("cluster recovery failed; staying unavailable")
                     return
@@ -170,16 +176,65 @@ class ClusterServer:
         return self.engine.comm_error() if self.engine is not None and self.engine.native_fanout_active else None
 
     # -- recovery (serving/cluster.py docstring) ----------------------
-    def _survivors(self, ctl, wait_s: float) -> List[int]:
-        """Ranks of the current epoch whose heartbeat is fresh (index order)."""
-        alive = []
-        for r in range(ctl.world):
-            if r == ctl.rank or ctl.peer_alive(r, wait_s):
-                alive.append(r)
-        return alive
+    def _survivors(self) -> List[int]:
+        """Current-epoch ranks whose heartbeat is fresh. A dead process stops
+        beating; a live one beats every few ms even while its step is stuck."""
+        ctl, lim = self.ctl, self.cfg.serving.peer_timeout_s
+        return [r for r in range(ctl.world) if r == ctl.rank or ctl.heartbeat_age(r) < lim]
 
     def _recover_leader(self) -> None:
-        raise NotImplementedError
+        """Rank 0 of a broken cluster: publish the survivors as the next
+        epoch's members (job store), wake the followers, rebuild."""
+        deadline = time.monotonic() + self.cfg.serving.peer_timeout_s
+        alive = self._survivors()
+        while len(alive) == self.ctl.world and time.monotonic() < deadline:
+            time.sleep(0.05)  # a stuck step before the heartbeat went stale
+            alive = self._survivors()
+        members = [self.members[r] for r in alive]
+        e = self.epoch + 1
+        log.warning("rebuilding the cluster over ranks %s (epoch %d)", members, e)
+        self._store.set(f"dtfs/recover/{e}", ",".join(str(m) for m in members))
+        self.ctl.bump_epoch()  # followers blocked on the old segment wake up
+        self._rebuild(e, members)
+
+    def _rejoin(self) -> bool:
+        """A non-leader rank of a broken cluster: wait for the next epoch's
+        members; rebuild if this rank is one (False: it was left out)."""
+        e = self.epoch + 1
+        key = f"dtfs/recover/{e}"
+        self._store.wait([key], datetime.timedelta(seconds=max(30.0, 4 * self.cfg.serving.step_timeout_s)))
+        members = [int(x) for x in self._store.get(key).decode().split(",")]
+        if self.orig_rank not in members:
+            log.error("rank %d was left out of epoch %d", self.orig_rank, e)
+            return False
+        self._rebuild(e, members)
+        return True
+
+    def _rebuild(self, epoch: int, members: List[int]) -> None:
+        """Fresh process group, communicators, step control and live server
+        over ``members`` (original ranks), in this same process; the model's
+        weights are kept. Requests that reach the old servable meanwhile fail
+        UNAVAILABLE; the registry swaps in the new one at the end."""
+        old_sched, old_eng = self.sched, self.engine
+        try:
+            old_eng.abort()  # the old communicators: nobody waits on a dead peer
+        except Exception:  # noqa: BLE001
+            log.exception("communicator abort failed")
+        old_sched.close()  # launcher / completer drain (failed steps answer UNAVAILABLE)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        world, rank = len(members), members.index(self.orig_rank)
+        if world > 1:
+            # control plane only (gloo): the data path is the native communicators
+            dist.init_process_group("gloo", store=dist.PrefixStore(f"dtfs/pg/{epoch}", self._store), rank=rank,
+                                    world_size=world,
+                                    timeout=datetime.timedelta(seconds=max(60.0, self.cfg.serving.step_timeout_s)))
+        ctx = DistContext(rank=rank, world=world, local_rank=self.ctx.local_rank, device=self.ctx.device,
+                          backend="gloo" if world > 1 else "none")
+        self.epoch, self.members = epoch, list(members)
+        self._build(ctx, first=False, store=self._store, model=old_eng.ex.model)
+        self.recoveries += 1
+        log.warning("rank %d serving again as rank %d of %d (epoch %d)", self.orig_rank, rank, world, epoch)
 
     # -- front door ---------------------------------------------------------------------
     def start_grpc(self, port: int = 9999, host: str = "0.0.0.0", max_workers: int = 32,
@@ -206,6 +261,8 @@ class ClusterServer:
         fault_after = int(self.follower_fault.get("after", -1))
         while True:
             ctl, sched = self.ctl, self.sched
+            if ctl is None:  # rebuilt as a one-rank cluster (nothing to follow)
+                return sched.stats()["steps"]
             if fault_after >= 0:
                 if sched.stats()["steps"] >= fault_after:
                     log.error("fault injection: follower rank %d exits after %d steps", self.rank, fault_after)
@@ -217,7 +274,9 @@ class ClusterServer:
                 steps = sched.stats()["steps"]
                 sched.close()
                 return steps
-            if ctl.broken_by >= 0 or sched.broken:
+            if ctl.broken_by >= 0 or sched.broken or ctl.epoch > 0:
+                if self.recover_on and self._rejoin():
+                    continue
                 raise RuntimeError(f"cluster broken: {self.broken or f'rank {ctl.broken_by} gave up'}")
 
     # -- shutdown ---------------------------------------------------------------------------

@@ -50,20 +50,22 @@ def live_enabled(cfg: Config, device: torch.device) -> bool:
 
 
 def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistContext] = None,
-                 mode: str = "local", group=None) -> FanoutEngine:
+                 mode: str = "local", group=None, model=None) -> FanoutEngine:
     """Model + executor + fan-out engine of one rank, every bucket prepared
     (HIP graphs captured). With ``ctx`` of a multi-rank job, DLRM tables are
     sharded over the ranks (parallel/embedding_sharding.py) and ``mode``
     scatter / alltoall fans every batch out over the ranks. A servable of the
     live server ingests request arenas (the GPU unpacks raw request bytes).
     ``group``: process group of the step's collectives (CPU: a dedicated gloo
-    group, since they run on the live server's launcher thread)."""
+    group, since they run on the live server's launcher thread). ``model``:
+    reuse a built replica (a cluster rebuilt over fewer ranks keeps its weights)."""
     from ..parallel.embedding_sharding import build_parallel_model
 
     sc = cfg.serving
     dev = torch.device(device) if device is not None else (ctx.device if ctx is not None else pick_device(sc.device))
     ctx = ctx or DistContext(device=dev)
-    model = build_parallel_model(cfg.model, dev, ctx)
+    if model is None or getattr(model, "has_collectives", False):  # sharded tables re-shard over the new world
+        model = build_parallel_model(cfg.model, dev, ctx, group=group)
     world = ctx.world if ctx.is_distributed else 1
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
     if mode == "alltoall" and world > 1:  # every rank's rows split evenly over the GPUs

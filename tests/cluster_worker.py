@@ -55,6 +55,45 @@ def main():
     cfg.serving.batch_timeout_us = 300
     phase = dist.new_group(backend="gloo")
     fault = {"after": a.kill_after} if rank == a.kill_rank else None
+    if a.kill_rank >= 0:
+        # recovery rehearsal: rank a.kill_rank dies after a few steps; rank 0
+        # keeps sending requests until the rebuilt cluster served 5 in a row
+        srv = ClusterServer(cfg, ctx, mode="scatter", control_timeout_s=3, step_timeout_s=5, follower_fault=fault,
+                            recover=True)
+        res = {"rank": rank}
+        if rank == 0:
+            from distributed_tf_serving_amd.serving.errors import ServingError
+
+            model = srv.registry.resolve("DCN").model
+            synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=7)
+            outcomes, diffs = [], []
+            t_end = time.monotonic() + 70
+            while time.monotonic() < t_end:
+                ids, wts = synth.arrays(300)
+                data = native().encode_predict_request("DCN", "serving_default", None,
+                                                       [("feat_ids", torch.from_numpy(ids)),
+                                                        ("feat_wts", torch.from_numpy(wts))], True)
+                try:
+                    resp = srv.service.predict_bytes(data, 30.0)
+                    got = T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+                    want = model(torch.from_numpy(ids).to(ctx.device), torch.from_numpy(wts).to(ctx.device))
+                    diffs.append(float(np.abs(got - want.float().cpu().numpy()).max()))
+                    outcomes.append("ok")
+                except ServingError as e:
+                    outcomes.append(e.code.name)
+                    time.sleep(0.05)
+                if srv.recoveries and outcomes[-5:] == ["ok"] * 5:
+                    break
+            res.update(outcomes=outcomes, max_diff=max(diffs) if diffs else None, recoveries=srv.recoveries,
+                       world_after=srv.world)
+            srv.stop()
+        else:
+            res["followed"] = srv.serve_follower()
+            res.update(recoveries=srv.recoveries, world_after=srv.world)
+            srv.stop()
+        with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+        return
     srv = ClusterServer(cfg, ctx, mode=a.mode, control_timeout_s=20, step_timeout_s=20, follower_fault=fault)
     res = {"rank": rank, "serves": srv.serves}
     if srv.serves:

@@ -210,3 +210,124 @@ def test_native_cluster_serves_exact_scores_and_idles(tmp_path, world, mode):
         assert r["idle_steps"] == 0 and not r["broken"], r
     # every rank ran the same steps (each collective paired up)
     assert len({r["stats"]["steps"] for r in res}) == 1, [r["stats"]["steps"] for r in res]
+
+
+def _recover_worker(rank, world, port, q, die_rank, die_after):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import time
+
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.parallel.dist import init_from_env
+    from distributed_tf_serving_amd.serving.cluster import ClusterServer
+    from distributed_tf_serving_amd.serving.errors import ServingError
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire.tensor import make_tensor_proto, to_ndarray
+
+    try:
+        ctx = init_from_env(device="cpu", timeout_s=20)
+        fault = {"after": die_after} if rank == die_rank else None
+        cfg = _cfg()
+        srv = ClusterServer(cfg, ctx, control_timeout_s=2, step_timeout_s=3, follower_fault=fault, recover=True)
+        if rank == 0:
+            ref = build_model(cfg.model)
+            rng = np.random.default_rng(1)
+            outcomes, diffs = [], []
+            t_end = time.monotonic() + 90
+            while time.monotonic() < t_end:
+                ids = rng.integers(0, 1 << 40, size=(50, 43), dtype=np.int64)
+                wts = rng.random((50, 43), dtype=np.float32)
+                req = pb.PredictRequest()
+                req.model_spec.name = "DCN"
+                req.inputs["feat_ids"].CopyFrom(make_tensor_proto(ids))
+                req.inputs["feat_wts"].CopyFrom(make_tensor_proto(wts))
+                try:
+                    resp = srv.service.predict(req, timeout_s=20)
+                    outcomes.append("ok")
+                    got = to_ndarray(resp.outputs["prediction_node"])
+                    diffs.append(float(np.abs(got - ref(torch.from_numpy(ids), torch.from_numpy(wts)).numpy()).max()))
+                except ServingError as e:
+                    outcomes.append(e.code.name)
+                    time.sleep(0.05)
+                if srv.recoveries and outcomes[-5:] == ["ok"] * 5:
+                    break
+            q.put((rank, outcomes, diffs, srv.recoveries, srv.world))
+            srv.stop()
+        else:
+            n = srv.serve_follower()
+            q.put((rank, "stopped", n, srv.recoveries, srv.world))
+            srv.stop()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def test_cluster_recovers_over_surviving_ranks():
+    """SURVEY §5.3 degraded mode: a follower dies mid-stream; the requests in
+    flight fail UNAVAILABLE, rank 0 rebuilds the cluster over the two
+    survivors (fresh process group, step control and fan-out, same processes,
+    same weights) and later requests are served correctly at world 2."""
+    world, die_rank = 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_recover_worker, args=(r, world, port, q, die_rank, 3)) for r in range(world)]
+    [p.start() for p in procs]
+    res = {}
+    for _ in range(world - 1):
+        item = q.get(timeout=240)
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert 0 in res and isinstance(res[0][1], list), res
+    outcomes, diffs, recoveries, world_after = res[0][1:]
+    assert outcomes[0] == "ok" and "UNAVAILABLE" in outcomes, outcomes
+    assert outcomes[-5:] == ["ok"] * 5, outcomes
+    assert recoveries == 1 and world_after == 2
+    assert max(diffs) < 1e-5
+    assert res[1][1] == "stopped" and res[1][3] == 1 and res[1][4] == 2, res[1]
+    assert procs[die_rank].exitcode == 17
+
+
+def spawn_ranks(n, args, env_extra, timeout):
+    """Start n worker processes directly (RANK / WORLD_SIZE / MASTER_* in the
+    environment, rank 0 hosts the store): unlike torch.distributed.run's agent,
+    nothing tears the survivors down when one rank dies."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_RANK=str(r), **env_extra)
+        procs.append(subprocess.Popen([sys.executable, "tests/cluster_worker.py", *args], cwd=repo, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            outs.append(p.communicate()[0])
+    return procs, outs
+
+
+def test_cluster_worker_recovery_rehearsal_cpu(tmp_path):
+    """The GPU recovery rehearsal's worker (tests/cluster_worker.py) on gloo."""
+    import json
+
+    procs, outs = spawn_ranks(3, ["--out", str(tmp_path), "--kill-rank", "2", "--kill-after", "3"],
+                              dict(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+                                   DTFS_HOST_THREADS="1"), timeout=200)
+    r0 = json.load(open(tmp_path / "rank0.json")) if (tmp_path / "rank0.json").exists() else None
+    assert r0 is not None, [o[-2000:] for o in outs]
+    assert procs[2].returncode == 17
+    out = r0["outcomes"]
+    assert out[0] == "ok" and "UNAVAILABLE" in out and out[-5:] == ["ok"] * 5, out
+    assert r0["recoveries"] == 1 and r0["world_after"] == 2 and r0["max_diff"] < 1e-5

@@ -98,3 +98,24 @@ def test_native_cluster_server_ranks_sharing_one_gpu(tmp_path, n, mode):
     for r in res:
         assert r["idle_steps"] == 0 and not r["broken"], r
     assert len({r["stats"]["steps"] for r in res}) == 1
+
+
+def test_cluster_recovers_over_surviving_ranks_sharing_one_gpu(tmp_path):
+    """SURVEY §5.3 on hardware: of 3 ranks (RCCL, one shared GPU) rank 2 dies
+    after 3 steps; rank 0 answers the affected requests UNAVAILABLE, rebuilds
+    the cluster over ranks 0-1 (new communicators, step control, fan-out; same
+    processes and weights) and serves correct scores again."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_cluster_server import spawn_ranks  # direct processes: no agent tears the survivors down
+
+    procs, outs = spawn_ranks(3, ["--out", str(tmp_path), "--kill-rank", "2", "--kill-after", "3"],
+                              dict(DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100"), timeout=110)
+    r0 = json.load(open(tmp_path / "rank0.json")) if (tmp_path / "rank0.json").exists() else None
+    assert r0 is not None, [o[-3000:] for o in outs]
+    assert procs[2].returncode == 17
+    out = r0["outcomes"]
+    assert out[0] == "ok" and "UNAVAILABLE" in out and out[-5:] == ["ok"] * 5, out
+    assert r0["recoveries"] == 1 and r0["world_after"] == 2 and r0["max_diff"] < 1e-4, r0
+    r1 = json.load(open(tmp_path / "rank1.json"))
+    assert r1["recoveries"] == 1 and r1["world_after"] == 2, r1
