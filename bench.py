@@ -29,8 +29,7 @@ the literal config-2 point (one 512-candidate request per step, concurrency 1).
 
 Launch: ``python bench.py`` (1 GPU) or, for N GPUs,
 ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
-127.0.0.1 --master-port P bench.py --gpus N``. ``--loop replay`` runs the
-engine-only replay loop of round 1 (diagnostic, not the served path).
+127.0.0.1 --master-port P bench.py --gpus N``.
 """
 from __future__ import annotations
 
@@ -60,7 +59,6 @@ from distributed_tf_serving_amd.serving.executor import ShardExecutor  # noqa: E
 from distributed_tf_serving_amd.serving.arena import ArenaLayout  # noqa: E402
 from distributed_tf_serving_amd.serving.live import LiveScheduler  # noqa: E402
 from distributed_tf_serving_amd.serving.packing import PackedLayout, layout_for  # noqa: E402
-from distributed_tf_serving_amd.serving.pipeline import StepPipeline  # noqa: E402
 from distributed_tf_serving_amd.client.synth import SyntheticRequests  # noqa: E402
 from distributed_tf_serving_amd.utils.gc_tuning import tune_for_serving  # noqa: E402
 
@@ -124,13 +122,8 @@ def parse_args():
                     help="offered load of the fixed-QPS latency run, whole node (requests/s; 0 = skip); at N > 1 "
                          "split evenly over the front-door ranks")
     ap.add_argument("--qps-seconds", type=float, default=1.0)
-    ap.add_argument("--loop", default="live", choices=["live", "replay", "python"],
-                    help="live: the served path (default); replay / python: engine-only diagnostics (round 1)")
     ap.add_argument("--force-fanout", action="store_true",
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
-    ap.add_argument("--no-native-fanout", action="store_true",
-                    help="N>1 on GPU: issue collectives through torch.distributed instead of the C++ StepRunner "
-                         "(diagnostic; the live server then needs --loop replay/python)")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a step not finished by then fails the run instead of hanging it")
     ap.add_argument("--no-narrow", action="store_true",
@@ -183,7 +176,7 @@ def build(a, ctx):
     rows_in_max = B * (world if mode == "scatter" else 1)
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
-                       native_fanout=not a.no_native_fanout, group=step_group)
+                       group=step_group)
     for b in buckets:
         eng.prepare(b)
     if eng.program_active or eng.mode != "local":
@@ -337,87 +330,6 @@ def run_live(a, ctx, cfg, model, eng, B):
     return window_s, extra
 
 
-def run_replay(a, ctx, cfg, model, eng, B):
-    """Round-1 engine-only loop (diagnostic): pre-placed arenas replayed by the
-    C++ ServingLoop or the Python StepPipeline. Not the served path."""
-    world, rank, dev = ctx.world, ctx.rank, ctx.device
-    F = cfg.num_fields
-    pool, n_req = request_pool(a, ctx, eng, B, F)
-    pool = [pool[i * n_req:(i + 1) * n_req] for i in range(max(1, len(pool) // max(1, n_req)))] if n_req else [[]]
-    arena_layout = eng.arena
-    nat = native()
-    arenas, spans = [], []
-    for reqs in pool:
-        ar = arena_layout.alloc(pin=dev.type == "cuda")
-        spans.append(arena_layout.place(ar, reqs) if reqs else [])
-        arenas.append(ar)
-
-    def decode(k: int, slot: int):
-        if not pool[k % len(pool)]:
-            return None
-        ab = arena_layout.build(arenas[k % len(pool)], spans[k % len(pool)])
-        errs = [e for e in ab.errors if e]
-        if errs:
-            raise RuntimeError(errs[0])
-        return (ab, arenas[k % len(pool)])
-
-    def launch(k: int, slot: int, ctx_k):
-        if ctx_k is not None:
-            ab, ar = ctx_k
-            return eng.launch(B, slot, src=ar, nbytes=ab.used_bytes)
-        return eng.launch(B, slot, nbytes=0)
-
-    def encode(pb_, scores):
-        if pb_ is None:
-            return []
-        ab = pb_[0]
-        return nat.encode_batch_responses("DCN", "serving_default", 1, "prediction_node", scores, list(ab.rows),
-                                          list(ab.offsets))
-
-    if a.loop == "replay" and dev.type == "cuda" and not a.no_graphs:
-        from distributed_tf_serving_amd.ops import hip
-
-        nloop = hip().ServingLoop(eng.runner(), dict(depth=a.slots - 1, fields=F, max_rows=arena_layout.max_rows,
-                                                     varint_chunks=arena_layout.varint_chunks, version=1),
-                                  eng.loop_slots(B))
-        for ar, sp in zip(arenas, spans):
-            nloop.add_input(ar, sp)
-        lat = []
-
-        def run(n_steps, record):
-            st = nloop.run(n_steps, record)
-            if st["errors"]:
-                raise RuntimeError(f"{st['errors']} requests failed in the native loop")
-            if record:
-                lat.extend(st["latency_us"])
-    else:
-        pipe = StepPipeline(eng, B, slots=a.slots, depth=a.slots - 1, produce=decode,
-                            consume=lambda k, pb_, scores: encode(pb_, scores), launch=launch)
-        lat = pipe.latencies
-
-        def run(n_steps, record):
-            pipe.run(n_steps, record=record)
-
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        if ctx.is_distributed:
-            dist.barrier()
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-
-    tune_for_serving()
-    run(max(1, a.warmup), record=False)
-    sync()
-    t0 = time.perf_counter()
-    run(a.steps, record=True)
-    sync()
-    el = time.perf_counter() - t0
-    lat_us = [x if a.loop == "replay" else x * 1e6 for x in lat]
-    return el, {"p50_request_ms": pct(lat_us, 50), "p99_request_ms": pct(lat_us, 99),
-                "note": "engine-only replay loop (diagnostic), not the served path"}
-
-
 def main():
     a = parse_args()
     if os.environ.get("DTFS_HANG_DUMP_S"):  # debugging aid: every thread's stack, then exit
@@ -434,10 +346,7 @@ def main():
     dev = ctx.device
     torch.manual_seed(1234)
     cfg, model, eng, B = build(a, ctx)
-    if a.loop == "live":
-        el, extra = run_live(a, ctx, cfg, model, eng, B)
-    else:
-        el, extra = run_replay(a, ctx, cfg, model, eng, B)
+    el, extra = run_live(a, ctx, cfg, model, eng, B)
 
     t = torch.tensor([el, float(extra.get("requests_failed", 0))], dtype=torch.float64,
                      device=dev if ctx.backend == "nccl" else "cpu")
@@ -459,7 +368,7 @@ def main():
                                               "one independent replica per GPU, no collectives") + ")"
         else:
             par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
-                   + (", native C++ step" if eng.native_fanout_active else ", torch.distributed")
+                   + (", native C++ step" if eng.native_fanout_active else ", gloo (CPU)")
                    + (f", one-shot peer exchange for messages <= {eng._cin.peer_cap} B per peer"
                       if getattr(eng, "_cin", None) is not None and eng._cin.peer_enabled else "")
                    + (f", {eng.layout.row_bytes} B rows: int32 table rows + fp32 weights" if eng.layout.narrow
@@ -493,7 +402,7 @@ def main():
                 "parallelism": par,
                 "encoding": a.encoding,
                 "path": ("served: native live server (batching, arena copy, parse, step, encode) driven by "
-                         "in-process native client threads") if a.loop == "live" else f"engine-only {a.loop} loop",
+                         "in-process native client threads"),
             },
         }
         out.update(extra)

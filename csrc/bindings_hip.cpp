@@ -12,7 +12,6 @@
 
 #include "kernels/launchers.h"
 #include "comm/rccl_comm.h"
-#include "runtime/serving_loop.h"
 #include "live_bindings.h"
 #include "runtime/step_runner.h"
 
@@ -744,12 +743,6 @@ dtfs::runtime::StepProgram program_from(const py::dict& d, std::vector<py::objec
   return p;
 }
 
-// ServingLoop + the Python objects whose memory it points into.
-struct PyServingLoop {
-  std::unique_ptr<dtfs::runtime::ServingLoop> loop;
-  std::vector<py::object> keep;
-};
-
 // One native loop slot from its Python description (FanoutEngine.loop_slots).
 dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object>* keep) {
   keep->push_back(d);
@@ -786,27 +779,6 @@ dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object
     TORCH_CHECK(s.graph != nullptr || s.seq != nullptr, "slot needs a step graph or kernel sequence");
   }
   return s;
-}
-
-PyServingLoop* make_serving_loop(py::object runner_obj, py::dict cfg, py::list slots) {
-  auto* p = new PyServingLoop();
-  p->keep.push_back(runner_obj);
-  auto& runner = runner_obj.cast<dtfs::runtime::StepRunner&>();
-  dtfs::runtime::LoopConfig c;
-  c.depth = cfg.contains("depth") ? cfg["depth"].cast<int>() : 3;
-  c.fields = cfg["fields"].cast<int64_t>();
-  c.max_rows = cfg["max_rows"].cast<int64_t>();
-  if (cfg.contains("varint_chunks")) c.varint_chunks = cfg["varint_chunks"].cast<int64_t>();
-  if (cfg.contains("ids_key")) c.ids_key = cfg["ids_key"].cast<std::string>();
-  if (cfg.contains("wts_key")) c.wts_key = cfg["wts_key"].cast<std::string>();
-  if (cfg.contains("model_name")) c.model_name = cfg["model_name"].cast<std::string>();
-  if (cfg.contains("signature_name")) c.signature_name = cfg["signature_name"].cast<std::string>();
-  if (cfg.contains("output_key")) c.output_key = cfg["output_key"].cast<std::string>();
-  if (cfg.contains("version") && !cfg["version"].is_none()) c.version = cfg["version"].cast<int64_t>();
-  std::vector<dtfs::runtime::LoopSlot> ls;
-  for (auto item : slots) ls.push_back(loop_slot_from(item.cast<py::dict>(), &p->keep));
-  p->loop = std::make_unique<dtfs::runtime::ServingLoop>(&runner, c, std::move(ls));
-  return p;
 }
 
 // ---------------------------------------------------------------- live server (GPU backend)
@@ -1014,7 +986,6 @@ PYBIND11_MODULE(_hip, m) {
           "Bounded wait for the slot's step: (ok, error). Also polls the communicators' async errors.")
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
-      .def_property_readonly("event_mode", &dtfs::runtime::StepRunner::event_mode)
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
 
@@ -1034,45 +1005,6 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("stream") = 0)
       .def_property_readonly("size", &dtfs::runtime::KernelSequence::size)
       .def("describe", &dtfs::runtime::KernelSequence::describe);
-
-  py::class_<PyServingLoop>(m, "ServingLoop",
-                            "Native per-rank serving loop: parse -> H2D + step graph (or fan-out) -> encode")
-      .def(py::init(&make_serving_loop), py::arg("runner"), py::arg("config"), py::arg("slots"))
-      .def(
-          "add_input",
-          [](PyServingLoop& p, torch::Tensor arena, const std::vector<std::pair<int64_t, int64_t>>& spans) {
-            TORCH_CHECK(arena.device().is_cpu() && arena.is_pinned() && arena.is_contiguous() &&
-                            arena.scalar_type() == torch::kUInt8,
-                        "arena must be a pinned contiguous uint8 tensor");
-            p.keep.push_back(py::cast(arena));
-            p.loop->add_input(arena.data_ptr<uint8_t>(), arena.numel(), spans);
-          },
-          py::arg("arena"), py::arg("spans"))
-      .def(
-          "run",
-          [](PyServingLoop& p, int64_t n, bool record) {
-            dtfs::runtime::LoopStats s;
-            {
-              py::gil_scoped_release nogil;
-              s = p.loop->run(n, record);
-            }
-            py::dict d;
-            d["latency_us"] = s.latency_us;
-            d["score_sum"] = s.score_sum;
-            d["steps"] = s.steps;
-            d["requests"] = s.requests;
-            d["rows"] = s.rows;
-            d["errors"] = s.errors;
-            d["response_bytes"] = s.response_bytes;
-            d["parse_us"] = s.parse_us;
-            d["launch_us"] = s.launch_us;
-            d["wait_us"] = s.wait_us;
-            d["encode_us"] = s.encode_us;
-            d["wall_us"] = s.wall_us;
-            return d;
-          },
-          py::arg("n_steps"), py::arg("record") = true)
-      .def_property_readonly("slots", [](const PyServingLoop& p) { return p.loop->slots(); });
 
   {
     py::class_<PyGpuLive> c(m, "LiveServer",

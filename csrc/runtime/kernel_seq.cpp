@@ -82,19 +82,11 @@ KernelSequence::KernelSequence(hipGraph_t graph) {
   }
 }
 
-void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool skip_varint, hipEvent_t gate,
-                            int gate_after) const {
+void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool skip_varint) const {
   const bool bind_last = done && bind && !ops_.empty() && ops_.back().kind == 0;
-  int kernels = 0;
-  bool gated = false;
   for (size_t i = 0; i < ops_.size(); ++i) {
     const Op& op = ops_[i];
     if (skip_varint && op.varint && i + 1 < ops_.size()) continue;
-    if (gate && !gated && kernels >= gate_after && gate_after > 0) {
-      ck(hipEventRecord(gate, st), "hipEventRecord(gate)");
-      gated = true;
-    }
-    if (op.kind == 0 && !op.varint) ++kernels;
     if (op.kind == 0) {
       if (bind_last && i + 1 == ops_.size())
         ck(hipExtLaunchKernel(op.k.func, op.k.gridDim, op.k.blockDim, op.k.kernelParams, op.k.sharedMemBytes, st,
@@ -133,7 +125,6 @@ void KernelSequence::launch(hipStream_t st, hipEvent_t done, bool bind, bool ski
       else ck(hipMemsetD32Async(hipDeviceptr_t(m.dst), int(m.value), m.width, st), "memset");
     }
   }
-  if (gate && !gated) ck(hipEventRecord(gate, st), "hipEventRecord(gate)");
   if (done && !bind_last) ck(hipEventRecord(done, st), "hipEventRecord");
 }
 

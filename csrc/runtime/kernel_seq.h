@@ -30,11 +30,7 @@ class KernelSequence {
   // kernel, otherwise recorded after it.
   // skip_varint: leave out the arena varint-decode kernel (the host parse
   // found no packed varint ids in this step's requests).
-  // gate / gate_after > 0: record `gate` right after the gate_after-th kernel
-  // launched (the step's first stage; StepRunner holds the next step's H2D
-  // behind it).
-  void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false, bool skip_varint = false,
-              hipEvent_t gate = nullptr, int gate_after = 0) const;
+  void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false, bool skip_varint = false) const;
   int size() const { return int(ops_.size()); }
   std::string describe() const;
 

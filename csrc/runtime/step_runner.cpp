@@ -18,42 +18,20 @@ void ck(hipError_t e, const char* what) {
 }
 }  // namespace
 
-// How the compute stream signals "step done" (bench/wait_gap.py: an event
-// recorded after the last kernel costs ~6 us of idle GPU before the next
-// kernel - the marker's system-scope release writes back and invalidates L2):
-//   0  hipEventRecord marker, default (system-scope) fence
-//   1  hipEventRecord marker, device-scope release
-//   2  event bound to the last kernel's dispatch (hipExtLaunchKernel stop event)
-//   3  2 + no system fence (the scores reach the host through uncached
-//      pinned-memory stores the kernel itself issued)
-// DTFS_EVENT_MODE overrides the default.
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  if (e && *e) return std::atoi(e);
-  return dflt;
-}
-static int event_mode() { return env_int("DTFS_EVENT_MODE", 0); }
-
-StepRunner::StepRunner(int device, int slots) : device_(device), event_mode_(event_mode()) {
+// Step completion is an ordinary hipEventRecord marker after the step's last
+// kernel. (Round 2 measured the alternatives - device-scope release, an event
+// bound to the last dispatch, no system fence - in bench/wait_gap.py; none
+// paid on the served step.)
+StepRunner::StepRunner(int device, int slots) : device_(device) {
   if (slots < 1) slots = 1;
   ck(hipSetDevice(device), "hipSetDevice");
+  // Local steps alternate their H2D copies over two copy streams: back-to-back
+  // SDMA copies on one stream leave the engine idle ~15 us between commands;
+  // on two streams one copy's setup overlaps the other's transfer (8.6 MB per
+  // step every ~153 us instead of ~173 us, bench/copy_pipe.py on MI355X). A
+  // fan-out runner keeps one (its ingress / egress streams take the other
+  // hardware queues).
   ck(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking), "hipStreamCreate(copy)");
-  // Consecutive steps' H2D copies alternate over DTFS_H2D_STREAMS copy
-  // streams (default 2). Back-to-back SDMA copies on one stream leave the
-  // engine idle ~15 us between commands; on two streams one copy's setup
-  // overlaps the other's transfer: 8.6 MB per step every ~153 us instead of
-  // ~173 us (bench/copy_pipe.py on MI355X). DTFS_COPY_WAIT=1 keeps the copy
-  // stream's WAR wait on the slot's previous step even when the host has
-  // already seen it complete.
-  // The extra streams are created on first use, so a fan-out runner (one copy
-  // stream) never holds them.
-  n_copy_ = std::max(1, std::min(4, env_int("DTFS_H2D_STREAMS", 2)));
-  copy_wait_always_ = env_int("DTFS_COPY_WAIT", 0) != 0;
-  // default on: +3.6 % on the served DeepFM step (3 interleaved rounds, one
-  // box: 97.3 vs 93.6 M scores/s); the host having seen the copy complete
-  // before it enqueues the kernels is HIP's ordinary copy-then-launch pattern
-  host_wait_h2d_ = env_int("DTFS_H2D_HOST_WAIT", 1) != 0;
-  spin_wait_ = env_int("DTFS_SPIN_WAIT", 0) != 0;
   ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
   h2d_done_.resize(slots);
   done_.resize(slots);
@@ -62,30 +40,18 @@ StepRunner::StepRunner(int device, int slots) : device_(device), event_mode_(eve
   for (int i = 0; i < slots; ++i) observed_[i].store(false);
   for (int i = 0; i < slots; ++i) {
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
-    ck(hipEventCreateWithFlags(&done_[i], done_flags()), "hipEventCreate");
+    ck(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming), "hipEventCreate");
   }
-  gate_after_ = std::max(0, env_int("DTFS_H2D_GATE", 0));
-  gate_.resize(slots);
-  for (int i = 0; i < slots; ++i) ck(hipEventCreateWithFlags(&gate_[i], hipEventDisableTiming), "hipEventCreate");
-}
-
-unsigned StepRunner::done_flags() const {
-  unsigned f = hipEventDisableTiming;
-  if (event_mode_ == 1) f |= hipEventReleaseToDevice;
-  if (event_mode_ == 3) f |= hipEventDisableSystemFence;
-  return f;
 }
 
 StepRunner::~StepRunner() {
   hipSetDevice(device_);
-  for (hipStream_t s : {compute_, copy_, ingress_, egress_})
+  for (hipStream_t s : {compute_, copy_, copy2_, ingress_, egress_})
     if (s) hipStreamSynchronize(s);
-  for (hipStream_t s : extra_copy_) hipStreamSynchronize(s);
-  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_, &gate_, &prog_ev_})
+  for (auto* v : {&h2d_done_, &done_, &in_done_, &fwd_done_, &prog_ev_})
     for (auto e : *v) hipEventDestroy(e);
-  for (hipStream_t s : {compute_, copy_, ingress_, egress_})
+  for (hipStream_t s : {compute_, copy_, copy2_, ingress_, egress_})
     if (s) hipStreamDestroy(s);
-  for (hipStream_t s : extra_copy_) hipStreamDestroy(s);
 }
 
 void StepRunner::ensure_fanout_streams() {
@@ -96,7 +62,7 @@ void StepRunner::ensure_fanout_streams() {
   fwd_done_.resize(done_.size());
   for (size_t i = 0; i < done_.size(); ++i) {
     ck(hipEventCreateWithFlags(&in_done_[i], hipEventDisableTiming), "hipEventCreate");
-    ck(hipEventCreateWithFlags(&fwd_done_[i], done_flags()), "hipEventCreate");
+    ck(hipEventCreateWithFlags(&fwd_done_[i], hipEventDisableTiming), "hipEventCreate");
   }
 }
 
@@ -129,35 +95,27 @@ void StepRunner::copy_checked(void* dst, const void* src, int64_t nbytes, hipMem
   throw std::runtime_error(msg);
 }
 
-void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
-                     bool gated) {
+void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate) {
   hipStream_t st = copy_;
-  if (alternate && n_copy_ > 1 && extra_copy_.empty()) {
-    for (int i = 1; i < n_copy_; ++i) {
-      hipStream_t x;
-      ck(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate(copy2)");
-      extra_copy_.push_back(x);
-    }
-  }
-  if (alternate && !extra_copy_.empty()) {
-    const size_t i = size_t(n_h2d_++ % uint64_t(extra_copy_.size() + 1));
-    if (i) st = extra_copy_[i - 1];
+  if (alternate) {
+    if (!copy2_) ck(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking), "hipStreamCreate(copy2)");
+    if (n_h2d_++ & 1) st = copy2_;
   }
   // WAR on the slot's buffers: its previous step must have finished reading
-  // them. Skipped when the host already saw that step complete (the serving
-  // loop waits for step k-3 before launching k).
-  if (used_[slot] && (copy_wait_always_ || !observed_[slot].load(std::memory_order_acquire)))
+  // them. Skipped when the host already saw that step complete (the live
+  // server waits for step k - depth before it launches k).
+  if (used_[slot] && !observed_[slot].load(std::memory_order_acquire))
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
-  if (gated && last_gate_slot_ >= 0) ck(hipStreamWaitEvent(st, gate_[last_gate_slot_], 0), "hipStreamWaitEvent(gate)");
   if (nbytes > 0) copy_checked(dst, src, nbytes, hipMemcpyHostToDevice, st, slot, "H2D");
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
-  if (host_wait_h2d_ && consumer == compute_ && nbytes > 0) {
+  if (consumer == compute_ && nbytes > 0) {
     // The launcher thread waits for the copy instead of the compute queue:
     // a cross-queue barrier packet in front of every step costs ~5-7 us of
     // idle GPU at the step boundary (bench/step_timeline.py, MI355X), while
     // the launcher runs ~3 steps (~500 us) ahead of the GPU, so waiting the
-    // ~100 us copy on the host costs nothing. Kernels are enqueued after the
-    // copy completed, so stream order alone is enough.
+    // ~100 us copy on the host costs nothing (+3.6 % served DeepFM, round 2).
+    // Kernels are enqueued after the copy completed, so stream order alone is
+    // enough.
     for (;;) {
       const hipError_t e = hipEventQuery(h2d_done_[slot]);
       if (e == hipSuccess) break;
@@ -190,7 +148,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   // compute: the forward graph
   ck(hipStreamWaitEvent(compute_, in_done_[slot], 0), "hipStreamWaitEvent(compute)");
   if (s.forward_seq) {
-    s.forward_seq->launch(compute_, fwd_done_[slot], event_mode_ >= 2);
+    s.forward_seq->launch(compute_, fwd_done_[slot]);
   } else {
     ck(hipGraphLaunch(s.forward, compute_), "hipGraphLaunch(forward)");
     ck(hipEventRecord(fwd_done_[slot], compute_), "hipEventRecord(fwd)");
@@ -312,28 +270,14 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
-  h2d(slot, dst, src, nbytes, compute_, true, true);
-  seq->launch(compute_, done_[slot], event_mode_ >= 2, skip_varint, gate_after_ > 0 ? gate_[slot] : nullptr,
-              gate_after_);
-  last_gate_slot_ = gate_after_ > 0 ? slot : -1;
+  h2d(slot, dst, src, nbytes, compute_, true);
+  seq->launch(compute_, done_[slot], false, skip_varint);
   used_[slot] = 1;
 }
 
 void StepRunner::wait(int slot) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
-  if (used_[slot]) {
-    if (spin_wait_) {
-      // poll instead of blocking in the runtime (DTFS_SPIN_WAIT=1)
-      for (;;) {
-        const hipError_t e = hipEventQuery(done_[slot]);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) ck(e, "hipEventQuery");
-        std::this_thread::yield();
-      }
-    } else {
-      ck(hipEventSynchronize(done_[slot]), "hipEventSynchronize");
-    }
-  }
+  if (used_[slot]) ck(hipEventSynchronize(done_[slot]), "hipEventSynchronize");
   observed_[slot].store(true, std::memory_order_release);
 }
 

@@ -99,6 +99,22 @@ struct StepProgram {
   void validate() const;
 };
 
+// What one (bucket, slot) of a live server launches: a local step (direct
+// launches of the captured step, or its graph), a fan-out step, or a
+// programmed step; plus the pinned host scores it produces.
+struct LoopSlot {
+  void* h2d_dst = nullptr;           // device arena of the slot (local launch)
+  int64_t h2d_cap = 0;               // its size in bytes
+  hipGraphExec_t graph = nullptr;    // local: unpack + forward + scores -> h_out
+  const KernelSequence* seq = nullptr;  // local, preferred: the same step as direct launches
+  bool fanout = false;
+  FanoutStep fan;                    // fan-out: everything but h2d_src / h2d_bytes
+  bool program = false;
+  StepProgram prog;                  // programmed step (embedding-parallel models)
+  const float* h_out = nullptr;      // pinned scores of the slot
+  int64_t h_out_len = 0;
+};
+
 class StepRunner {
  public:
   StepRunner(int device, int slots);
@@ -129,23 +145,15 @@ class StepRunner {
   bool query(int slot);
   // Microseconds between the slot's last H2D start and compute end (diagnostic).
   int slots() const { return int(done_.size()); }
-  int event_mode() const { return event_mode_; }
   hipStream_t compute_stream() const { return compute_; }
   hipStream_t copy_stream() const { return copy_; }
 
  private:
   int device_;
-  int event_mode_ = 0;
-  unsigned done_flags() const;
   void copy_checked(void* dst, const void* src, int64_t nbytes, hipMemcpyKind kind, hipStream_t st, int slot,
                     const char* what);
-  void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate,
-           bool gated = false);
-  int n_copy_ = 1;
-  bool copy_wait_always_ = false;
-  bool host_wait_h2d_ = true;  // DTFS_H2D_HOST_WAIT (default 1): local steps wait for their H2D on the host
-  bool spin_wait_ = false;
-  std::vector<hipStream_t> extra_copy_;  // more H2D streams, used round-robin with copy_
+  void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
+  hipStream_t copy2_ = nullptr;  // second H2D stream, alternated with copy_ by local steps
   uint64_t n_h2d_ = 0;
   // host saw the slot's last step complete (set by wait/query, possibly from
   // another thread than the launcher)
@@ -155,14 +163,6 @@ class StepRunner {
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
   std::vector<hipEvent_t> prog_ev_;  // [slot * kProgEvents + k], created on first program launch
   int last_prog_slot_ = -1;
-  // H2D gate (DTFS_H2D_GATE = k, default 0 = off): step k+1's H2D waits until
-  // step k's first k kernels (the embedding gather) have run, so the DMA
-  // overlaps the GEMMs instead of the latency-bound gather it slows ~2x
-  // (profiles/kernel_counters.md). Measured on MI355X it costs 2-13 % (the
-  // serialised H2D outweighs the faster gather: profiles/ingest_ab.md).
-  std::vector<hipEvent_t> gate_;
-  int gate_after_ = 0;
-  int last_gate_slot_ = -1;
   std::vector<char> used_;  // not vector<bool>: written by the launcher, read by the waiter
 };
 

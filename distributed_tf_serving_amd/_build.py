@@ -44,7 +44,7 @@ NATIVE_SOURCES = [
     "runtime/narrow.cpp",
     "runtime/step_control.cpp",
 ]
-HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp", "runtime/serving_loop.cpp",
+HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp",
                     "runtime/kernel_seq.cpp",
                     # shared with _native (the loop parses arenas / encodes responses itself)
                     "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp", "runtime/trace.cpp",

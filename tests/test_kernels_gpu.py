@@ -459,15 +459,15 @@ def test_unpack_arena_gpu_matches_cpu(cuda):
 
 
 def test_unpack_arena_narrow_matches_cpu(cuda):
-    """Narrow fan-out rows: [int32 id mod m | bf16 weight | pad] from raw,
-    varint and host-narrowed arena rows vs the wide CPU unpack + narrowing."""
+    """Narrow fan-out rows: [int32 id mod m | fp32 weight] from raw, varint
+    and host-narrowed arena rows vs the wide CPU unpack + narrowing."""
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.serving.arena import ArenaLayout
     from distributed_tf_serving_amd.serving.packing import PackedLayout
 
     m = 999_983
     A, W, N = ArenaLayout(43, 2048), PackedLayout(43), PackedLayout(43, m)
-    assert N.row_bytes == 264 and W.row_bytes == 520
+    assert N.row_bytes == 344 and W.row_bytes == 520
     ar = A.alloc()
     s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=6)
     reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (250, False), (64, True))]

@@ -38,51 +38,52 @@ def test_rccl_comm_single_rank(cuda):
 
 @pytest.mark.parametrize("mode,raw", [("local", True), ("local", False), ("alltoall", True), ("alltoall", False),
                                       ("scatter", True)])
-def test_native_serving_loop(cuda, mode, raw):
-    """The C++ ServingLoop (parse -> H2D + step graph / fan-out -> encode) over a
-    ring of request arenas; the last step's scores match a local forward.
-    raw=False: packed varint requests, decoded on the GPU (the local replay
-    skips the varint kernel for steps without any)."""
+def test_live_server_every_step_kind(cuda, mode, raw):
+    """The GPU live server (parse -> H2D + step kernels / fan-out step ->
+    encode) on one rank for each step kind - local direct launches, the native
+    fan-out step (RCCL all-to-all / scatter+gather with the rank itself) - with
+    raw and packed-varint requests (the latter decoded on the GPU): every
+    request's scores match a local forward."""
+    import concurrent.futures as cf
+
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
-    from distributed_tf_serving_amd.ops import hip, native
+    from distributed_tf_serving_amd.config import ServingConfig
+    from distributed_tf_serving_amd.ops import native
+    from distributed_tf_serving_amd.serving.live import LiveScheduler
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
 
     cfg = ModelConfig(family="deepfm", vocab_size=50_000)
     m = build_model(cfg, cuda)
     F = cfg.num_fields
-    L = PackedLayout(F)
-    B, S, R = 1024, 4, 4
-    ex = ShardExecutor(m, L, [B], cuda, slots=S)
+    B, S = 1024, 4
+    narrow = mode != "local"
+    L = PackedLayout(F, cfg.vocab_size if narrow else 0)
+    ex = ShardExecutor(m, L, [256, B], cuda, slots=S)
     AL = ArenaLayout(F, max_rows=B)
     eng = FanoutEngine(ex, DistContext(device=cuda), mode="alltoall" if mode == "local" else mode, ingest="arena",
                        arena=AL, force_fanout=mode != "local")
-    loop = hip().ServingLoop(eng.runner(), dict(depth=S - 1, fields=F, max_rows=B, version=1,
-                                                        varint_chunks=AL.varint_chunks), eng.loop_slots(B))
+    for b in (256, B):
+        eng.prepare(b)
+    assert eng.native_fanout_active == (mode != "local")
+    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=(256, B), batch_timeout_us=300)
+    live = LiveScheduler(eng, sc, depth=S - 1, step_timeout_s=20)
     synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=5)
-    inputs = []
-    for p in range(5):
-        ids, wts = synth.arrays(B)
-        ids, wts = torch.from_numpy(ids), torch.from_numpy(wts)
-        reqs = [native().encode_predict_request("DCN", "serving_default", None,
-                                                [("feat_ids", ids[i:i + B // R]), ("feat_wts", wts[i:i + B // R])],
-                                                raw or p == 1)
-                for i in range(0, B, B // R)]
-        ar = AL.alloc(pin=True)
-        loop.add_input(ar, AL.place(ar, reqs))
-        inputs.append((ids, wts))
-    n = 11
-    st = loop.run(n, True)
-    assert st["errors"] == 0 and st["requests"] == n * R and st["rows"] == n * B
-    assert st["response_bytes"] > n * B * 4 and len(st["latency_us"]) == n
-    # every step's scores as the encoder read them: replays of one input agree
-    sums = st["score_sum"]
-    assert len(sums) == n
-    for k in range(len(inputs), n):
-        assert abs(sums[k] - sums[k - len(inputs)]) <= 1e-6 * max(1.0, abs(sums[k])), (k, sums)
-    last = n - 1
-    ids, wts = inputs[last % len(inputs)]
-    got = eng.host_out(B, last % S)[:B].clone()
-    want = m(ids.to(cuda), wts.to(cuda)).float().cpu()
-    assert (got - want).abs().max().item() < 1e-5
+    reqs = []
+    for i in range(24):
+        ids, wts = synth.arrays([1, 200, 37, 512][i % 4])
+        reqs.append((native().encode_predict_request("DCN", "serving_default", None,
+                                                     [("feat_ids", torch.from_numpy(ids)),
+                                                      ("feat_wts", torch.from_numpy(wts))], raw), ids, wts))
+    with cf.ThreadPoolExecutor(8) as pool:
+        outs = list(pool.map(lambda r: live.predict_bytes(r[0], 30.0), reqs))
+    for (data, ids, wts), resp in zip(reqs, outs):
+        got = T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+        want = m(torch.from_numpy(ids).to(cuda), torch.from_numpy(wts).to(cuda)).float().cpu().numpy()
+        assert abs(got - want).max() < 2e-5
+    st = live.stats()
+    assert st["steps"] < len(reqs) and not st["broken"]
+    live.close()
 
 
 @pytest.mark.parametrize("mode", ["alltoall", "scatter"])

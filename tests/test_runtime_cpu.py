@@ -14,7 +14,6 @@ from distributed_tf_serving_amd.parallel.dist import DistContext, reference_part
 from distributed_tf_serving_amd.parallel.fanout import FanoutEngine
 from distributed_tf_serving_amd.serving.executor import ShardExecutor
 from distributed_tf_serving_amd.serving.packing import PackedLayout
-from distributed_tf_serving_amd.serving.pipeline import StepPipeline
 
 
 # ------------------------------------------------------------------ batcher
@@ -198,30 +197,3 @@ def test_executor_and_local_engine_cpu():
     out = h.wait()
     assert torch.allclose(out, m(ids, wts), atol=1e-6)
     assert torch.allclose(ex.run_rows(ids[:5], wts[:5]), m(ids[:5], wts[:5]), atol=1e-6)
-
-
-def test_step_pipeline_cpu():
-    m = build_model(small_cfg("wdl"))
-    L = PackedLayout(43)
-    B = 8
-    ex = ShardExecutor(m, L, [B], "cpu", slots=4)
-    eng = FanoutEngine(ex, DistContext(), mode="local")
-    data = {k: (torch.randint(0, 10**9, (B, 43)), torch.rand(B, 43)) for k in range(9)}
-    got = {}
-
-    def produce(k, slot):
-        buf = eng.host_in(B, slot)
-        L.ids(buf).copy_(data[k][0])
-        L.wts(buf).copy_(data[k][1])
-        return k
-
-    def consume(k, ctx, scores):
-        got[k] = scores.clone()
-
-    pipe = StepPipeline(eng, B, slots=4, depth=3, produce=produce, consume=consume)
-    pipe.run(9)
-    pipe.close()
-    assert sorted(got) == list(range(9)) and len(pipe.latencies) == 9
-    for k in range(9):
-        assert torch.allclose(got[k], m(*data[k]), atol=1e-6)
-
