@@ -1197,13 +1197,9 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
   // 17: the 8-phase kernel; 18: the same with the next tile's A[qm0] read in
   // phase 3 (LDS reads per phase 4/4/8/8 instead of 12/4/8/0): 16384x1024x2752
   // bf16 76.2-76.9 us vs 80.9-81.9 (interleaved, MI355X), so the default
-  // 8-phase pick (variant 0 -> 17) runs it unless DTFS_8PH_PRE=0
+  // 8-phase pick (variant 0 -> 17) runs it
   if ((variant == 17 || variant == 18) && glds_ok) {
-    static const bool pre_default = [] {
-      const char* e = std::getenv("DTFS_8PH_PRE");
-      return !(e && e[0] == '0');
-    }();
-    const bool pre = variant == 18 || (variant == 17 && pre_from_dispatch && pre_default);
+    const bool pre = variant == 18 || (variant == 17 && pre_from_dispatch);
     if (pre) launch_8ph<FP8, OutT, true>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     else launch_8ph<FP8>(A, lda, W, ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi, st);
     return;

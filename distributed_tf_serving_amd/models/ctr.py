@@ -26,7 +26,6 @@ dlrm         sigmoid(head(topMLP(dot(botMLP(dense), emb_t))))
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, Optional
 
 import torch
@@ -93,39 +92,6 @@ class CTRModel(nn.Module):
             raise NotImplementedError(f"{self.family} reads dense features; unpack the arena first")
         return self._forward(ops.ArenaRows(arena, int(B), self.cfg.num_fields), None, out)
 
-    # families whose step is "gather (+ FM / wide terms) -> MLP -> head" can run
-    # as a two-lane program that overlaps consecutive steps (local_step_program)
-    supports_overlap = False
-
-    def local_step_program(self, arena: torch.Tensor, B: int, out: torch.Tensor, decode, state: dict):
-        """One local (no fan-out) step as a two-lane program
-        (parallel/step_program.py): the gather - K0 fused into K1, reading the
-        request arena - on the aux lane, the MLP GEMMs + head on the compute
-        lane. Step k+1's gather waits for step k's FIRST GEMM only, so it runs
-        on the CUs next to step k's smaller GEMMs and head (the big GEMM holds
-        every CU's registers; the gather is memory-latency bound) instead of
-        after them. ``decode`` runs the arena's GPU varint decode."""
-        from ..parallel import step_program as sp
-
-        rows = ops.ArenaRows(arena, int(B), self.cfg.num_fields)
-        mlp = self.mlp
-
-        def front():
-            decode()
-            state["x"], state["extra"] = self._front(rows, None)
-
-        def back1():
-            state["h"] = mlp.layers[0](state["x"])
-
-        def back2():
-            state["scores"] = mlp.forward_head(state["h"], self.head_w, self.head_b, extra=state["extra"], out=out,
-                                               start=1)
-
-        return [sp.Sync("wait_prev", sp.AUX, 1), sp.Kernels(sp.AUX, front, "gather"),
-                sp.Sync("record", sp.AUX, 0), sp.Sync("wait", sp.COMPUTE, 0),
-                sp.Kernels(sp.COMPUTE, back1, "gemm1"), sp.Sync("record", sp.COMPUTE, 1),
-                sp.Kernels(sp.COMPUTE, back2, "mlp+head")]
-
 
 class WideDeep(CTRModel):
     family = "wdl"
@@ -141,8 +107,6 @@ class WideDeep(CTRModel):
         self.head_w = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
                                    requires_grad=False)
         self.head_b = 0.0
-
-    supports_overlap = True
 
     def _front(self, ids, wts):
         return ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
@@ -167,8 +131,6 @@ class DeepFM(CTRModel):
         self.head_w = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
                                    requires_grad=False)
         self.head_b = 0.0
-
-    supports_overlap = True
 
     def _front(self, ids, wts):
         return ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
@@ -238,8 +200,8 @@ class DCNv2(CTRModel):
         # the FLOPs; the small tail layers stay bf16 so the last layer + head run as
         # one fused kernel writing the scores to pinned memory (fp8 there needs two
         # quant passes, a separate head and a D2H copy: 53 us vs ~37 us per
-        # 16384-row step). DTFS_FP8_MLP_TAIL=1 keeps every MLP layer fp8.
-        if self.fp8 and os.environ.get("DTFS_FP8_MLP_TAIL", "0") != "1":
+        # 16384-row step, round 2)
+        if self.fp8:
             for layer in self.mlp.layers[1:]:
                 layer.fp8 = False
         self.head_wc = nn.Parameter(init_uniform_(torch.empty(d, device=self.device_), 0.5 / math.sqrt(d), self.gen),
@@ -247,26 +209,10 @@ class DCNv2(CTRModel):
         self.head_wd = nn.Parameter(init_uniform_(torch.empty(self.mlp.out_dim, device=self.device_), 0.05, self.gen),
                                     requires_grad=False)
         self.head_b = 0.0
-        # MX-fp8 cross chain (each cross epilogue emits the next layer's e4m3 +
-        # E8M0 block-scaled operand) vs per-row re-quantisation between layers.
-        # Opt-in (DTFS_MX_CHAIN=1): interleaved A/B on one MI355X, bench.py
-        # --model dcn_v2: 0.973 ms/step chained vs 0.914 re-quantised
-        # (profiles/dcn_v2_mx_chain.md) - the 22 us quant pass it removes costs
-        # less than the block-scale epilogue + MX operand path it adds.
-        self.mx_chain = os.environ.get("DTFS_MX_CHAIN", "0") == "1"
-        # Split cross layers (fp8 full rank): plain-epilogue GEMM y = xl W^T + b
-        # (the 8-phase tile runs it) + one combine pass that writes z = x0*y + xl,
-        # quantises it for the next layer and, for the last layer, reduces the
-        # cross logit instead of writing z (ops.cross_combine). DTFS_CROSS_SPLIT=0:
-        # fused cross epilogue + separate quant_rows / head passes.
-        self.cross_split = os.environ.get("DTFS_CROSS_SPLIT", "1") == "1"
-        # x0's fp8 copy written by the gather (DTFS_GATHER_QUANT=0: quant_rows pass)
-        self.gather_quant = os.environ.get("DTFS_GATHER_QUANT", "1") == "1"
 
-    def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None, emit_mx: int = 0):
-        """One cross layer. fp8: ``xq`` = (q, row scales | None, MX block scales
-        | None) of xl; ``emit_mx`` > 0 also returns this layer's output as the
-        next layer's MX-fp8 operand (q, block scales)."""
+    def _cross_layer(self, i: int, x0: torch.Tensor, xl: torch.Tensor, xq=None):
+        """One cross layer with the cross epilogue fused into its GEMM. fp8:
+        ``xq`` = (q, row scales) of xl."""
         if self.low_rank:
             # x0 * (U (V xl) + b) + xl : the cross epilogue rides on the U GEMM
             v = self.cross_v[i](xl)
@@ -274,9 +220,8 @@ class DCNv2(CTRModel):
             return ops.cross_v2(x0, xl, u.weight, u.bias, a=v)
         layer = self.cross[i]
         if self.fp8:
-            q, sx, sblk = xq if xq is not None else (*ops.quant_rows_fp8(xl, ops.FP8_K_PAD), None)
-            return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl, sx_blk=sblk,
-                                  emit_mx=emit_mx)
+            q, sx = xq if xq is not None else ops.quant_rows_fp8(xl, ops.FP8_K_PAD)
+            return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
     def _forward(self, ids, wts, out=None):
@@ -284,16 +229,18 @@ class DCNv2(CTRModel):
         # first MLP layer (both read it) - by the gather itself, which holds each
         # row in one wave's registers (ops.embed_fp8; no separate quant pass)
         fp8_full = self.fp8 and not self.low_rank
-        if fp8_full and self.gather_quant and self.cfg.num_fields <= 64:
+        if fp8_full and self.cfg.num_fields <= 64:
             x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
             q0 = tuple(q0)
         else:
             x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
             q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
-        nq = -(-self.d // ops.FP8_K_PAD) * ops.FP8_K_PAD
-        chain = fp8_full and self.mx_chain and self.d % ops.MX_BLOCK == 0 and nq <= ops.MX_MAX_K
         L = self.cfg.num_cross_layers
-        if fp8_full and self.cross_split and not chain and self.d % 8 == 0 and L > 0:
+        if fp8_full and self.d % 8 == 0 and L > 0:
+            # split cross layers: plain-epilogue GEMM y = xl W^T + b (the
+            # 8-phase tile runs it) + one combine pass that writes z = x0*y + xl,
+            # quantises it for the next layer and, for the last layer, reduces
+            # the cross logit instead of writing z (profiles/dcn_v2_split_kernels.md)
             xl, (q, sx) = x0, q0
             for i in range(L):
                 layer = self.cross[i]
@@ -304,15 +251,9 @@ class DCNv2(CTRModel):
                                                           head_w=self.head_wc if last else None)
                 xl = z
         else:
-            xl, xq = x0, ((*q0, None) if q0 is not None else None)
+            xl, xq = x0, q0
             for i in range(L):
-                emit = nq if (chain and i < L - 1) else 0
-                r = self._cross_layer(i, x0, xl, xq, emit)
-                if emit:
-                    xl, q, sq = r
-                    xq = (q, None, sq)
-                else:
-                    xl, xq = r, None
+                xl, xq = self._cross_layer(i, x0, xl, xq), None
             cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
         mlp_q = q0 if (q0 is not None and self.mlp.layers[0].fp8 and self.mlp.layers[0].k == x0.shape[1]) else None
         return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out, xq=mlp_q)

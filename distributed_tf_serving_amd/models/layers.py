@@ -144,8 +144,7 @@ class MLP(nn.Module):
         as well streams both weights through every 64-row block: measured
         48.0 us vs 34.5 us for GEMM + fused head at 16384 rows on MI355X -
         weight-load latency bound - so that fusion is not used.)
-        ``start``: x is already the output of layers[:start] (a step split
-        after its first GEMM, CTRModel.local_step_program)."""
+        ``start``: x is already the output of layers[:start]."""
         for k, layer in enumerate(self.layers[start:-1], start):
             x = layer(x, xq if k == 0 else None)
         last = self.layers[-1]

@@ -43,11 +43,6 @@ def hip():
                         "gfx950 kernels (_hip) are not built: run `python -m distributed_tf_serving_amd._build`"
                     ) from e
             _hip_mod.rccl_set_library(_torch_rccl_path())
-            # pipelined gather geometry override (tuning A/Bs; kernels captured
-            # afterwards use it): DTFS_EMBED_WAVES=<resident-wave cap>, DTFS_EMBED_ROWS=1|2
-            if os.environ.get("DTFS_EMBED_WAVES") or os.environ.get("DTFS_EMBED_ROWS"):
-                _hip_mod.set_embed_wave_cap(int(os.environ.get("DTFS_EMBED_WAVES", "4096")),
-                                            int(os.environ.get("DTFS_EMBED_ROWS", "1")))
     return _hip_mod
 
 

@@ -101,7 +101,7 @@ class StepHandle:
 class FanoutEngine:
     def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
                  step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None,
-                 native_fanout: bool = True, force_fanout: bool = False, overlap: Optional[bool] = None):
+                 native_fanout: bool = True, force_fanout: bool = False):
         """``ingest="packed"``: the host decodes into packed rows (host_in) and
         the H2D moves rows. ``ingest="arena"``: the host only parses request
         framing into a request arena (serving/arena.py); the H2D moves the raw
@@ -135,12 +135,6 @@ class FanoutEngine:
         self._programs: Dict[Tuple[int, int], object] = {}
         self._prog_bufs: Dict[Tuple[int, int], dict] = {}
         self.program_active = False
-        # local steps as cross-step overlapped two-lane programs (CTRModel.
-        # local_step_program). Opt-in (DTFS_OVERLAP=1): interleaved A/B on one
-        # MI355X (bench/step_timeline.py) - step k+1's gather co-running with
-        # step k's smaller GEMMs slows the fused head 12.6 -> 61 us, so the step
-        # period is 176-182 us vs 174-175 us serial (profiles/step_overlap.md)
-        self.overlap = (os.environ.get("DTFS_OVERLAP", "0") == "1") if overlap is None else bool(overlap)
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
@@ -258,12 +252,10 @@ class FanoutEngine:
     def _program_enabled(self) -> bool:
         if not (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"):
             return False
-        m = self.ex.model
-        if getattr(m, "supports_program", False):  # embedding-parallel: the exchange is the program
-            return os.environ.get("DTFS_STEP_PROGRAM", "1") != "0"
-        # cross-step overlap of gather and GEMMs (CTRModel.local_step_program)
-        return (self.overlap and getattr(m, "supports_overlap", False) and self.ex.use_graphs
-                and os.environ.get("DTFS_ARENA_UNPACK", "0") != "1")
+        # embedding-parallel models: the exchange is the program. (Local
+        # steps stay serial: a cross-step overlapped gather slowed the fused
+        # head 12.6 -> 61 us, 176-182 vs 174-175 us per step, profiles/step_overlap.md)
+        return bool(getattr(self.ex.model, "supports_program", False))
 
     def _capture_program(self, B: int, slot: int) -> None:
         """Build and capture the step program of one (bucket, slot): GPU unpack
@@ -280,20 +272,14 @@ class FanoutEngine:
         h_out = self.host_out(B, slot)
         bufs = self._prog_bufs[key] = model.alloc(B) if hasattr(model, "alloc") else {}
         state: dict = {}
-        if getattr(model, "supports_program", False):
-            ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
-            ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B],
-                                       state=state)
-        else:
-            ops = model.local_step_program(arena_dev, B, h_out[:B], lambda: self.arena.decode_varints(arena_dev),
-                                           state)
+        ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
+        ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B], state=state)
         # warm-up: one eager run (collective on every rank, like the capture below)
         sp.run_eager(ops, self.group)
         torch.cuda.synchronize(self.dev)
         pools = {lane: torch.cuda.graph_pool_handle() for lane in (sp.COMPUTE, sp.AUX)}
         streams = {lane: torch.cuda.Stream(self.dev) for lane in (sp.COMPUTE, sp.AUX)}
-        direct = os.environ.get("DTFS_STEP_LAUNCH", "direct") != "graph"
-        prog = sp.capture_native(ops, arena_dev, self._cprog, pools, streams, direct=direct)
+        prog = sp.capture_native(ops, arena_dev, self._cprog, pools, streams, direct=True)
         prog.state = state  # the captured graphs' intermediate tensors live here
         self._programs[key] = prog
 
@@ -439,21 +425,19 @@ class FanoutEngine:
         return self._runner
 
     def loop_slots(self, B: int):
-        """Per-slot launch descriptions for the native ServingLoop
-        (csrc/runtime/serving_loop.cpp): a local step graph, or a fan-out step."""
+        """Per-slot launch descriptions for the GPU live server
+        (csrc/runtime/step_runner.h LoopSlot): a local step, a fan-out step or a
+        programmed step."""
         if not self.cuda or self.ingest != "arena":
             raise RuntimeError("the native serving loop needs a GPU and arena ingest")
-        import os
-
         from ..ops import hip
 
         self.prepare(B)
-        # direct kernel launches instead of hipGraphLaunch (runtime/kernel_seq.h:
-        # ~8-14 us less idle per step); DTFS_STEP_LAUNCH=graph restores graphs
-        direct = os.environ.get("DTFS_STEP_LAUNCH", "direct") != "graph"
 
+        # direct kernel launches instead of hipGraphLaunch (runtime/kernel_seq.h:
+        # ~8-14 us less idle per step)
         def seq(g):
-            if not direct or g is None:
+            if g is None:
                 return None
             k = id(g)
             if k not in self._seqs:
@@ -525,8 +509,7 @@ class FanoutEngine:
         buf = self.ex.input_buffer(B, slot)
         arena_dev = self.dev_arena(slot) if self.ingest == "arena" else None
 
-        fused_ingest = (arena_dev is not None and getattr(self.ex.model, "supports_arena", False)
-                        and os.environ.get("DTFS_ARENA_UNPACK", "0") != "1")
+        fused_ingest = arena_dev is not None and getattr(self.ex.model, "supports_arena", False)
 
         def body():
             # the head kernel writes the scores straight into pinned host memory

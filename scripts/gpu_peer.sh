@@ -1,7 +1,7 @@
 set -o pipefail
 export DTFS_SHARE_GPU=1 DTFS_HOST_THREADS=2
 mkdir -p gpurun_out
-timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29611 -m distributed_tf_serving_amd.bench.peer_exchange --iters 300 > gpurun_out/peer_x2.log 2>&1 || { tail -30 gpurun_out/peer_x2.log; exit 1; }
+timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29611 -m tools.studies.peer_exchange --iters 300 > gpurun_out/peer_x2.log 2>&1 || { tail -30 gpurun_out/peer_x2.log; exit 1; }
 grep '^{' gpurun_out/peer_x2.log
 for pc in 0 262144 0 262144; do
  for mode in alltoall scatter; do

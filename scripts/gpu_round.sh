@@ -25,7 +25,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
     -- python3 bench.py ${PROF_ARGS:---steps 100 --warmup 10 --qps 0} > gpurun_out/prof.log 2>&1 \
     || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
   db=$(find gpurun_out/prof -name '*.db' | head -1)
-  python -m distributed_tf_serving_amd.bench.prof_summary "$db" --steps ${PROF_STEPS:-110} \
+  python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} \
     --title "${PROF_TITLE:-bench.py live path (DeepFM, 32 x 512-candidate requests per step), 1 MI355X}" \
     > gpurun_out/prof_summary.md && cat gpurun_out/prof_summary.md
 fi

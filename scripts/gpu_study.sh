@@ -26,15 +26,15 @@ counters() {
     for pass in "$PASS_SQ" "$PASS_FETCH" "$PASS_WRITE"; do
       i=$((i+1))
       timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d $OUT/${model}_p$i -o run \
-        -- python3 -m distributed_tf_serving_amd.bench.kernel_drive --model $model --rows $rows --iters 10 \
+        -- python3 -m tools.studies.kernel_drive --model $model --rows $rows --iters 10 \
         > $OUT/${model}_p$i.log 2>&1 || { echo "pass $i of $model failed"; tail -5 $OUT/${model}_p$i.log; return 1; }
     done
     mkdir -p $OUT/sum_$model && cp -r $OUT/${model}_p* $OUT/sum_$model/ 2>/dev/null
-    python -m distributed_tf_serving_amd.bench.counters_summary $OUT/sum_$model \
+    python -m tools.counters_summary $OUT/sum_$model \
       --title "$model serving-shape forward, 1 MI355X (rocprofv3 --pmc, 3 passes)" > $OUT/summary_$model.md
     cat $OUT/summary_$model.md
   done
-  timeout -k 10 300 python -u -m distributed_tf_serving_amd.bench.microbench --serving > $OUT/microbench.jsonl 2>&1 \
+  timeout -k 10 300 python -u -m tools.studies.microbench --serving > $OUT/microbench.jsonl 2>&1 \
     || { echo "microbench failed"; tail -5 $OUT/microbench.jsonl; return 1; }
   grep '^{' $OUT/microbench.jsonl
 }
@@ -51,7 +51,7 @@ models() {
         --output-format rocpd -- python3 bench.py --model $m --steps 40 --warmup 5 --qps 0 \
         > gpurun_out/models/prof_$m.log 2>&1 || { echo "prof $m failed"; tail -10 gpurun_out/models/prof_$m.log; return 1; }
       local db=$(find gpurun_out/models/prof_$m -name '*.db' | head -1)
-      python -m distributed_tf_serving_amd.bench.prof_summary "$db" --steps 45 \
+      python -m tools.prof_summary "$db" --steps 45 \
         --title "bench.py --model $m (live path), 1 MI355X" > gpurun_out/models/prof_$m.md && head -16 gpurun_out/models/prof_$m.md
     fi
   done
@@ -114,7 +114,7 @@ grpc() {
   for enc in raw packed; do
     [ $enc = packed ] && [ "${PACKED:-1}" != 1 ] && continue
     local flag=""; [ $enc = packed ] && flag=--packed
-    timeout -k 10 240 python -u -m distributed_tf_serving_amd.bench.grpc_ceiling --preset ${PRESET:-deepfm_1gpu} $flag \
+    timeout -k 10 240 python -u -m tools.studies.grpc_ceiling --preset ${PRESET:-deepfm_1gpu} $flag \
       --procs ${PROCS:-1 2 4} --threads 16 --seconds 5 --frontends ${FRONTENDS:-1} --out gpurun_out/grpc/ceiling_$enc.json \
       > gpurun_out/grpc/ceiling_$enc.log 2>&1 || { echo "ceiling $enc failed"; tail -20 gpurun_out/grpc/ceiling_$enc.log; return 1; }
     grep '^{' gpurun_out/grpc/ceiling_$enc.log
@@ -134,22 +134,22 @@ trace() {
 }
 
 embed() {
-  timeout -k 10 200 python -u -m distributed_tf_serving_amd.bench.microbench --embed-study > gpurun_out/embed_study.log 2>&1 \
+  timeout -k 10 200 python -u -m tools.studies.microbench --embed-study > gpurun_out/embed_study.log 2>&1 \
     || { tail -30 gpurun_out/embed_study.log; return 1; }
   grep '^{' gpurun_out/embed_study.log
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "embed" -d gpurun_out/pmc_fetch \
-    -o run -- python3 -m distributed_tf_serving_amd.bench.microbench --embed-study > gpurun_out/pmc1.log 2>&1 \
+    -o run -- python3 -m tools.studies.microbench --embed-study > gpurun_out/pmc1.log 2>&1 \
     || { tail -30 gpurun_out/pmc1.log; return 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
-    --kernel-include-regex "embed" -d gpurun_out/pmc_write -o run -- python3 -m distributed_tf_serving_amd.bench.microbench \
+    --kernel-include-regex "embed" -d gpurun_out/pmc_write -o run -- python3 -m tools.studies.microbench \
     --embed-study > gpurun_out/pmc2.log 2>&1 || { tail -30 gpurun_out/pmc2.log; return 1; }
 }
 
 gemm() {
-  timeout -k 10 300 python -u -m distributed_tf_serving_amd.bench.microbench --gemm-variants > gpurun_out/gemm_variants.log 2>&1 \
+  timeout -k 10 300 python -u -m tools.studies.microbench --gemm-variants > gpurun_out/gemm_variants.log 2>&1 \
     || { echo "gemm variants failed"; tail -30 gpurun_out/gemm_variants.log; return 1; }
   grep '^{' gpurun_out/gemm_variants.log
-  timeout -k 10 200 python -u -m distributed_tf_serving_amd.bench.mx_ab ${MX_ROWS:-16384} > gpurun_out/mx_ab.log 2>&1 \
+  timeout -k 10 200 python -u -m tools.studies.mx_ab ${MX_ROWS:-16384} > gpurun_out/mx_ab.log 2>&1 \
     || { echo "mx_ab failed"; tail -30 gpurun_out/mx_ab.log; return 1; }
   grep '^{' gpurun_out/mx_ab.log
 }

@@ -53,7 +53,7 @@ def test_peer_exchange_single_rank(cuda):
 def _run(n, *extra, timeout=110):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m",
-           "distributed_tf_serving_amd.bench.peer_exchange", *extra]
+           "tools.studies.peer_exchange", *extra]
     env = dict(os.environ, DTFS_SHARE_GPU="1")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])

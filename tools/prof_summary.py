@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 ``--kernel-trace --stats`` run (rocpd SQLite output)
 into a markdown table for ``profiles/``.
 
-    python -m distributed_tf_serving_amd.bench.prof_summary gpurun_out/prof/run_results.db \
+    python -m tools.prof_summary gpurun_out/prof/run_results.db \
         --steps 110 --title "bench.py R=16" > profiles/bench_r16.md
 
 Per kernel: calls, total / mean / min / max us, share of GPU busy time, and

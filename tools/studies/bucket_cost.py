@@ -5,7 +5,7 @@ every slot in flight. Tells which small buckets are worth having: a bucket
 whose step costs nearly as much as the next larger one only adds queueing
 under load (bench.py --small-buckets).
 
-    python -m distributed_tf_serving_amd.bench.bucket_cost --buckets 512,1024,2048,4096,8192,16384
+    python -m tools.studies.bucket_cost --buckets 512,1024,2048,4096,8192,16384
 """
 from __future__ import annotations
 
@@ -16,14 +16,14 @@ import time
 
 import torch
 
-from ..client.synth import SyntheticRequests
-from ..config import ModelConfig
-from ..models import build_model
-from ..parallel.dist import DistContext
-from ..parallel.fanout import FanoutEngine
-from ..serving.arena import ArenaLayout
-from ..serving.executor import ShardExecutor
-from ..serving.packing import PackedLayout
+from distributed_tf_serving_amd.client.synth import SyntheticRequests
+from distributed_tf_serving_amd.config import ModelConfig
+from distributed_tf_serving_amd.models import build_model
+from distributed_tf_serving_amd.parallel.dist import DistContext
+from distributed_tf_serving_amd.parallel.fanout import FanoutEngine
+from distributed_tf_serving_amd.serving.arena import ArenaLayout
+from distributed_tf_serving_amd.serving.executor import ShardExecutor
+from distributed_tf_serving_amd.serving.packing import PackedLayout
 
 
 def main():

@@ -1,8 +1,8 @@
 """Do back-to-back H2D copies on one stream run back-to-back? (run under rocprofv3)
 
     rocprofv3 --kernel-trace --memory-copy-trace -d out -o run -- \\
-        python3 -m distributed_tf_serving_amd.bench.copy_pipe
-    python -m distributed_tf_serving_amd.bench.copy_pipe --analyze out/run_results.db
+        python3 -m tools.studies.copy_pipe
+    python -m tools.studies.copy_pipe --analyze out/run_results.db
 
 The serving step is H2D-paced (8.6 MB of request arena per 16384-row step,
 ~157 us at ~54 GB/s), and the bench trace showed every copy starting 20-55 us
@@ -110,7 +110,7 @@ def run():
                                  0xFFFFFFFF)  # hipStreamWaitValueGte
         work()
     idle()
-    from .. import ops
+    from distributed_tf_serving_amd import ops
 
     h = ops.hip()
     with torch.cuda.stream(cp):  # 6

@@ -6,7 +6,7 @@ Times, at the served shape (M x 2752 x 2816, fp8 operands, interleaved rounds):
   combine - x0 * y + xl as one torch elementwise pass (a stand-in for a fused
             combine + next-layer quantisation kernel), and quant_rows on its output
 
-    python -m distributed_tf_serving_amd.bench.cross_split [M]
+    python -m tools.studies.cross_split [M]
 """
 import json
 import statistics

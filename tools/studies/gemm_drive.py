@@ -2,7 +2,7 @@
 (rocprofv3 --pmc): the bf16 8-phase MLP GEMM, the same shape in fp8, and the
 fp8 DCN-v2 cross layer (16384 x 2752 x 2816, x0 / xl epilogue).
 
-    rocprofv3 --pmc ... -- python3 -m distributed_tf_serving_amd.bench.gemm_drive --form fp8 --variant 17
+    rocprofv3 --pmc ... -- python3 -m tools.studies.gemm_drive --form fp8 --variant 17
 """
 from __future__ import annotations
 
@@ -10,7 +10,7 @@ import argparse
 
 import torch
 
-from .. import ops
+from distributed_tf_serving_amd import ops
 
 
 def main():

@@ -3,7 +3,7 @@ one tile variant, bf16 and fp8 (row-scaled e4m3), and fit t(K) = F + nk * t_tile
 (nk = K tiles of 128 bytes). Separates the prologue / epilogue / tail share
 from the main-loop rate.
 
-    python -m distributed_tf_serving_amd.bench.gemm_kscan [M N variant]
+    python -m tools.studies.gemm_kscan [M N variant]
 """
 import json
 import sys
@@ -11,7 +11,7 @@ import sys
 import numpy as np
 import torch
 
-from .. import ops
+from distributed_tf_serving_amd import ops
 
 
 def _time(fn, iters=30):

@@ -1,12 +1,12 @@
 """Run one GEMM shape/variant N times (for rocprofv3 counter collection).
 
-    python -m distributed_tf_serving_amd.bench.gemm_probe M N K variant [iters] [bf16|fp8]
+    python -m tools.studies.gemm_probe M N K variant [iters] [bf16|fp8]
 """
 import sys
 
 import torch
 
-from .. import ops
+from distributed_tf_serving_amd import ops
 
 
 def main():

@@ -1,7 +1,7 @@
 """Where does the time between two serving steps go? (run under rocprofv3)
 
-    rocprofv3 --kernel-trace -d out -o run -- python3 -m distributed_tf_serving_amd.bench.graph_gap
-    python -m distributed_tf_serving_amd.bench.graph_gap --analyze out/run_results.db
+    rocprofv3 --kernel-trace -d out -o run -- python3 -m tools.studies.graph_gap
+    python -m tools.studies.graph_gap --analyze out/run_results.db
 
 Phases (separated by 20 ms idle gaps in the trace):
   A  the DeepFM step graph replayed back-to-back on one stream
@@ -22,10 +22,10 @@ import time
 def run(B: int = 8192, iters: int = 30):
     import torch
 
-    from ..config import ModelConfig
-    from ..models import build_model
-    from ..serving.executor import ShardExecutor
-    from ..serving.packing import PackedLayout
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.serving.executor import ShardExecutor
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
 
     dev = torch.device("cuda", 0)
     cfg = ModelConfig(family="deepfm")

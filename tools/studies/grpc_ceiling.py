@@ -10,7 +10,7 @@ client-bound curve (rate grows with P) from a server-bound one (flat rate,
 server CPU pinned), and the live server's own batching stats through the
 Prometheus endpoint.
 
-    python -m distributed_tf_serving_amd.bench.grpc_ceiling --preset deepfm_1gpu --procs 1 2 4
+    python -m tools.studies.grpc_ceiling --preset deepfm_1gpu --procs 1 2 4
 """
 from __future__ import annotations
 

@@ -1,7 +1,7 @@
 """Replay one model's serving-shape forward for kernel profiling.
 
     rocprofv3 --pmc SQ_WAVES ... --kernel-trace -d out -- python3 -m \\
-        distributed_tf_serving_amd.bench.kernel_drive --model deepfm --rows 16384 --iters 20
+        tools.studies.kernel_drive --model deepfm --rows 16384 --iters 20
 
 Builds the bench preset of the model (random-init weights), captures the
 forward at ``rows`` candidates (Zipf ids over 2^40, uniform weights) in a HIP
@@ -15,9 +15,9 @@ import argparse
 
 import torch
 
-from ..client.synth import SyntheticRequests
-from ..config import load_preset
-from ..models import build_model
+from distributed_tf_serving_amd.client.synth import SyntheticRequests
+from distributed_tf_serving_amd.config import load_preset
+from distributed_tf_serving_amd.models import build_model
 
 PRESETS = {"deepfm": "deepfm_1gpu", "dcn_v2": "dcn_v2_fp8", "dcn": "reference_dcn", "wdl": "wdl_tiny_cpu"}
 

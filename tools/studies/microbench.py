@@ -1,6 +1,6 @@
 """Kernel micro-benchmarks on one GPU (hot ops vs the library baseline).
 
-    python -m distributed_tf_serving_amd.bench.microbench [--quick]
+    python -m tools.studies.microbench [--quick]
 
 Prints one JSON line per measurement: the op, its shape, mean microseconds
 over interleaved rounds (cdna_hip_programming.md §5.4 rule 24), achieved
@@ -15,7 +15,7 @@ import statistics
 
 import torch
 
-from .. import ops
+from distributed_tf_serving_amd import ops
 
 
 def _time(fn, iters=50, rounds=5):
@@ -99,8 +99,8 @@ def bench_embed(B, F=43, D=64, V=1_000_000, dev="cuda"):
 
 
 def bench_model(family, B, dev="cuda", graphs=True):
-    from ..config import ModelConfig
-    from ..models import build_model
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
 
     cfg = ModelConfig(family=family)
     if family == "dlrm":
@@ -174,7 +174,7 @@ def main():
 
 def embed_study(B=16384, F=43, D=64, V=1_000_000, dev="cuda"):
     """Where the K1 time goes at the bench shape: id distribution, x write, FM terms."""
-    from ..client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
 
     table = torch.randn(V, D, device=dev).to(torch.bfloat16)
     lin = torch.randn(V, device=dev)

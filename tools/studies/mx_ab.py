@@ -2,7 +2,7 @@
 per-row scaled e4m3 A vs OCP MX-fp8 A (E8M0 block scales into the MFMA),
 with and without the MX-fp8 epilogue output. Prints one JSON line per form.
 
-    python -m distributed_tf_serving_amd.bench.mx_ab
+    python -m tools.studies.mx_ab
 """
 import json
 

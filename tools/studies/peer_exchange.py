@@ -26,8 +26,8 @@ import time
 import torch
 import torch.distributed as dist
 
-from ..parallel.dist import init_from_env
-from ..parallel.native_comm import create_comm
+from distributed_tf_serving_amd.parallel.dist import init_from_env
+from distributed_tf_serving_amd.parallel.native_comm import create_comm
 
 
 def payload(rank: int, peer: int, n: int, seed: int, dev) -> torch.Tensor:

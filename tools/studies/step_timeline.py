@@ -4,7 +4,7 @@ start / end relative to the anchor's start, averaged over the last ``--last``
 steps, plus the step period. Shows whether two lanes actually overlap
 (step_program.py) and where the idle gaps are.
 
-    python -m distributed_tf_serving_amd.bench.step_timeline gpurun_out/prof/run_results.db
+    python -m tools.studies.step_timeline gpurun_out/prof/run_results.db
 """
 from __future__ import annotations
 

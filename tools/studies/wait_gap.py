@@ -1,7 +1,7 @@
 """What does a cross-stream dependency cost on the compute queue? (run under rocprofv3)
 
-    rocprofv3 --kernel-trace -d out -o run -- python3 -m distributed_tf_serving_amd.bench.wait_gap
-    python -m distributed_tf_serving_amd.bench.wait_gap --analyze out/run_results.db
+    rocprofv3 --kernel-trace -d out -o run -- python3 -m tools.studies.wait_gap
+    python -m tools.studies.wait_gap --analyze out/run_results.db
 
 The serving step waits for its H2D copy (copy stream) before its first
 kernel. The trace showed a ~10 us idle gap at exactly that point every step
