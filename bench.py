@@ -129,7 +129,22 @@ def parse_args():
     ap.add_argument("--no-narrow", action="store_true",
                     help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed int32 rows / bf16")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
-    return ap.parse_args()
+    ap.add_argument("--reference-workload", action="store_true",
+                    help="the reference's own run instead (DCNClient.java:25-42, 57-74, 205-241): model DCN, requests "
+                         "of 1500 candidates with ids 1..43 and weights 1.0 encoded like the reference client "
+                         "(int64_val / float_val), 6 closed-loop clients x --ref-requests requests; prints the "
+                         "reference's output lines and a JSON summary. At N > 1 rank 0 is the only front door and "
+                         "every request is scattered over the GPUs (the reference's 3-host fan-out, inside a node)")
+    ap.add_argument("--ref-requests", type=int, default=1000, help="requests per client thread (reference: 1000)")
+    ap.add_argument("--ref-clients", type=int, default=6, help="closed-loop client threads (reference: 6)")
+    ap.add_argument("--print-requests", action="store_true",
+                    help="--reference-workload: also print one 'Time cost' line per request, like the reference")
+    a = ap.parse_args()
+    if a.reference_workload:
+        a.model, a.request_rows, a.encoding = "dcn", 1500, "packed"
+        if a.mode is None:
+            a.mode = "scatter"
+    return a
 
 
 def build(a, ctx):
@@ -160,6 +175,13 @@ def build(a, ctx):
     model = build_parallel_model(cfg, dev, ctx, shard_tables="on" if a.shard_tables else "auto", group=step_group)
     F = cfg.num_fields
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
+    if a.reference_workload:
+        # rows per GPU when k of the clients' 1500-candidate requests share a step
+        # (scatter at N > 1: rank 0's batch of k x 1500 rows is split over N GPUs)
+        split = world if (a.mode or "scatter") == "scatter" and world > 1 else 1
+        per = [-(-(k * a.request_rows) // (split * 64)) * 64 for k in range(1, a.ref_clients + 1)]
+        B = per[-1]
+        a.small_buckets = ",".join(str(b) for b in sorted(set(per[:-1])))
     sharded = getattr(model, "has_collectives", False) or (a.model == "dlrm" and a.shard_tables)
     if a.mode is None:
         a.mode = "local" if a.model == "dlrm" else "alltoall"
@@ -194,6 +216,9 @@ def build(a, ctx):
 def request_pool(a, ctx, eng, B, F):
     rows_in = eng.contrib_rows(B)
     n_req = rows_in // a.request_rows
+    if a.reference_workload:  # every candidate ids 1..43, weights 1.0 (DCNClient.java:57-74)
+        synth = SyntheticRequests(fields=F, dist="reference")
+        return ([synth.serialized(a.request_rows, raw=False)] if rows_in else []), n_req
     synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank)
     n = max(1, a.pool) if n_req else 0
     return [synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n)], n_req
@@ -330,6 +355,61 @@ def run_live(a, ctx, cfg, model, eng, B):
     return window_s, extra
 
 
+def run_reference(a, ctx, cfg, model, eng, B):
+    """--reference-workload: the reference client's closed loop against this
+    server (reference DCNClient.java:205-241): ``--ref-clients`` threads x
+    ``--ref-requests`` back-to-back 1500-candidate requests, latency per
+    request from submit to the serialized PredictResponse, average printed
+    in the reference's format."""
+    world, rank, dev = ctx.world, ctx.rank, ctx.device
+    pool, _ = request_pool(a, ctx, eng, B, cfg.num_fields)
+    buckets = list(eng.ex.buckets)
+    sc = ServingConfig(max_batch_rows=B, allowed_batch_sizes=tuple(buckets), batch_timeout_us=a.batch_timeout_us,
+                       max_queued_rows=1 << 24, max_request_rows=1 << 20, model_name="DCN")
+    control = None
+    if eng.lockstep and world > 1:
+        from distributed_tf_serving_amd.ops import hip
+        from distributed_tf_serving_amd.parallel.control import control_for_job
+
+        control = control_for_job(hip() if dev.type == "cuda" else native(), ctx, "bench-ref")
+    live = LiveScheduler(eng, sc, buckets=buckets, depth=a.slots, control=control, step_timeout_s=a.step_timeout_s,
+                         start_paused=control is not None, narrow=not a.no_narrow, peer_timeout_s=a.step_timeout_s)
+    phase = dist.new_group(backend="gloo") if ctx.is_distributed else None
+    tune_for_serving()
+    if ctx.is_distributed:
+        dist.barrier(group=phase)
+    if control is not None:
+        live.resume()
+    out = None
+    if pool:
+        n = a.ref_clients * a.ref_requests
+        r = live.run_load(pool, warmup=10 * a.ref_clients, count=n, concurrency=a.ref_clients,
+                          threads=a.ref_clients, timeout_us=int(a.step_timeout_s * 1e6))
+        lat_ms = [x * 1e-3 for x in r["latency_us"]]
+        if a.print_requests:
+            for i, ms in enumerate(lat_ms):
+                print(f"Thread Thread-{i % a.ref_clients}. Time cost with {a.request_rows} is {ms} ms")
+        avg = sum(lat_ms) / len(lat_ms) if lat_ms else float("nan")
+        print(f"Average time cost with {a.request_rows} is {avg} ms with {len(lat_ms)} requests", flush=True)
+        wall = r["wall_us"] * 1e-6
+        st = live.stats()
+        out = {"metric": "reference workload (DCNClient.java): average request latency", "value": round(avg, 4),
+               "unit": "ms", "higher_is_better": False, "n_gpus": world, "requests": len(lat_ms),
+               "errors": int(r["errors"]), "clients": a.ref_clients, "candidates": a.request_rows,
+               "p50_ms": pct(r["latency_us"], 50), "p99_ms": pct(r["latency_us"], 99),
+               "requests_per_s": round(len(lat_ms) / wall, 1) if wall > 0 else None,
+               "scores_per_s": round(len(lat_ms) * a.request_rows / wall, 1) if wall > 0 else None,
+               "steps": st["steps"], "buckets": buckets,
+               "path": "in-process native clients -> live server" + (f" -> {eng.mode} over {world} GPUs"
+                                                                      if world > 1 else " (1 GPU)"),
+               "model": describe_model(cfg), "encoding": "int64_val / float_val (like the reference client)"}
+    live.close()
+    if ctx.is_distributed:
+        dist.barrier(group=phase)
+    if out is not None and rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse_args()
     if os.environ.get("DTFS_HANG_DUMP_S"):  # debugging aid: every thread's stack, then exit
@@ -346,6 +426,10 @@ def main():
     dev = ctx.device
     torch.manual_seed(1234)
     cfg, model, eng, B = build(a, ctx)
+    if a.reference_workload:
+        run_reference(a, ctx, cfg, model, eng, B)
+        shutdown()
+        return
     el, extra = run_live(a, ctx, cfg, model, eng, B)
 
     t = torch.tensor([el, float(extra.get("requests_failed", 0))], dtype=torch.float64,

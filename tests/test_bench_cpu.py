@@ -78,3 +78,21 @@ def test_bench_sharded_dlrm_world2():
     par = out["config"]["parallelism"]
     assert "embedding-mp2" in par and "candidate-dp2" in par, par
     assert out.get("requests_failed", 0) == 0 and out["config"]["global_batch"] == 128
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_reference_workload(n):
+    """--reference-workload: the reference's closed loop (DCN, 1500 identical
+    candidates, 6 clients) prints the reference's average line; at N = 2 rank
+    0 scatters every request over both ranks."""
+    args = ["bench.py", "--gpus", str(n), "--reference-workload", "--ref-requests", "2", "--decode-threads", "1"]
+    cmd = [sys.executable, *args] if n == 1 else [
+        sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "Average time cost with 1500 is " in p.stdout and " ms with 12 requests" in p.stdout, p.stdout
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["errors"] == 0 and out["requests"] == 12 and out["n_gpus"] == n
