@@ -58,6 +58,28 @@ torch::Tensor pack_ids(torch::Tensor ids, int64_t modulo, c10::optional<torch::T
 // ---------------------------------------------------------------- K1
 // k_pad > 0: the gather also writes x as e4m3 [B, K rounded up to k_pad] + a
 // per-row scale (the fp8 towers' first operand; replaces quant_rows_fp8(x)).
+// DCN v1 cross network inside the gather (embedding.hip): weight rows
+// [w_0 .. w_{L-1}, head_w] fp32 [L+1, F*D] and constants fp32 [L+1]; the
+// gather's fm output becomes the cross logit.
+static void embed_cross_in(dtfs::EmbedArgs& a, const torch::Tensor& table, int64_t F, int64_t D,
+                           const c10::optional<torch::Tensor>& cross_w, const c10::optional<torch::Tensor>& cross_c) {
+  if (!cross_w) return;
+  TORCH_CHECK(cross_c.has_value(), "cross_w needs cross_c");
+  check_same_dev(table, *cross_w, "cross_w");
+  check_same_dev(table, *cross_c, "cross_c");
+  TORCH_CHECK(cross_w->scalar_type() == torch::kFloat32 && cross_w->is_contiguous() && cross_w->dim() == 2 &&
+                  cross_w->size(1) == F * D && cross_w->size(0) >= 1 && cross_w->size(0) <= dtfs::kCrossMax,
+              "cross_w must be contiguous fp32 [L+1 <= 8, F*D]");
+  TORCH_CHECK(cross_c->scalar_type() == torch::kFloat32 && cross_c->is_contiguous() &&
+                  cross_c->numel() == cross_w->size(0),
+              "cross_c must be fp32 [L+1]");
+  TORCH_CHECK(F <= 64 && (F * D) % 4 == 0 && cross_w->numel() * 4 <= 160 * 1024,
+              "cross in the gather: F <= 64 and the weights must fit the LDS");
+  a.cross_w = cross_w->data_ptr<float>();
+  a.cross_c = cross_c->data_ptr<float>();
+  a.cross_n = int(cross_w->size(0));
+}
+
 static void embed_fp8_out(dtfs::EmbedArgs& a, const torch::Tensor& table, int64_t B, int64_t K, int64_t k_pad,
                           torch::Tensor& q, torch::Tensor& qs) {
   if (k_pad <= 0) return;
@@ -76,7 +98,8 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
                                  c10::optional<torch::Tensor> offset_f, double bias, bool want_x, bool want_fm,
                                  bool fm2, c10::optional<torch::Tensor> out_x, bool validate_tables,
                                  c10::optional<torch::Tensor> shard_lo_f, c10::optional<torch::Tensor> shard_n_f,
-                                 int64_t k_pad) {
+                                 int64_t k_pad, c10::optional<torch::Tensor> cross_w,
+                                 c10::optional<torch::Tensor> cross_c) {
   check_dev(table, "table");
   TORCH_CHECK(ids.is_cuda(), "ids must be a GPU tensor");
   TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2, "table must be bf16 [V, D]");
@@ -167,6 +190,8 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
   a.fm2 = fm2 ? 1 : 0;
   torch::Tensor q, qs;
   embed_fp8_out(a, table, B, F * D, k_pad, q, qs);
+  TORCH_CHECK(!cross_w || (want_fm && !modulo_f && !shard_lo_f), "cross: shared table, want_fm");
+  embed_cross_in(a, table, F, D, cross_w, cross_c);
   check_hip(dtfs::launch_embed(a, cur_stream(ids)), "embed");
   return {x, fm, q, qs};
 }
@@ -175,7 +200,8 @@ std::vector<torch::Tensor> embed(torch::Tensor table, c10::optional<torch::Tenso
 // arena (csrc/runtime/arena.h) - no separate unpack kernel, no packed rows.
 std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch::Tensor> lin, torch::Tensor arena,
                                        int64_t B, int64_t F, int64_t modulo, double bias, bool want_x, bool want_fm,
-                                       bool fm2, c10::optional<torch::Tensor> out_x, int64_t k_pad) {
+                                       bool fm2, c10::optional<torch::Tensor> out_x, int64_t k_pad,
+                                       c10::optional<torch::Tensor> cross_w, c10::optional<torch::Tensor> cross_c) {
   check_dev(table, "table");
   check_dev(arena, "arena");
   check_same_dev(table, arena, "arena");
@@ -219,6 +245,8 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
   a.fm2 = fm2 ? 1 : 0;
   torch::Tensor q, qs;
   embed_fp8_out(a, table, B, F * D, k_pad, q, qs);
+  TORCH_CHECK(!cross_w || want_fm, "cross: want_fm");
+  embed_cross_in(a, table, F, D, cross_w, cross_c);
   check_hip(dtfs::launch_embed(a, cur_stream(table)), "embed_arena");
   return {x, fm, q, qs};
 }
@@ -887,10 +915,11 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("modulo_f") = py::none(), py::arg("offset_f") = py::none(), py::arg("bias") = 0.0,
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
         py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none(),
-        py::arg("k_pad") = 0);
+        py::arg("k_pad") = 0, py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none());
   m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
         py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
-        py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0);
+        py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0, py::arg("cross_w") = py::none(),
+        py::arg("cross_c") = py::none());
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
         py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
         py::arg("out_bf16") = false);

@@ -205,13 +205,32 @@ __device__ __forceinline__ int64_t hash_row_magic(int64_t id, int64_t m, uint64_
   return int64_t(r);
 }
 
-template <int D, typename IdT, bool ARENA, int R>
+// K3 in the gather (DCN v1, CROSS): x_{l+1} = x0 (x_l . w_l) + b_l + x_l keeps
+// every x_l in span{x0, b_0 + .. + b_{l-1}}: x_l = alpha_l x0 + beta_l with
+// alpha_0 = 1, beta_0 = 0, so
+//   s_l = x_l . w_l = alpha_l (x0 . w_l) + c_l,   c_l = beta_l . w_l
+//   alpha_{l+1} = alpha_l + s_l,  beta_{l+1} = beta_l + b_l
+//   cross logit = x_L . head_w = alpha_L (x0 . head_w) + c_L
+// with the c_l precomputed once per weight set (models/ctr.py DCN). The whole
+// cross network of a row is L + 1 dot products of x0 - which this wave holds
+// in registers - with weight rows staged in LDS, and L + 1 scalar steps: no
+// x0 re-read, no per-row weight traffic from L2 (round 2's separate cross
+// kernel read 66 KB of fp32 weights per row, ~1.1 GB per 16384-row step).
+template <int D, typename IdT, bool ARENA, int R, bool CROSS = false>
 __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t magic) {
   constexpr int LPR = D / 8;          // lanes per table row (16 B each)
   constexpr int FPI = kWave / LPR;    // fields per wave-wide load
   constexpr int MAXG = kWave / FPI;   // load instructions per row
   const bf16* __restrict__ table = static_cast<const bf16*>(a.table);
   const int F = a.F, B = a.B;
+  extern __shared__ float4 s_cross4[];  // CROSS: [cross_n][F * D] fp32
+  const float* s_cross = reinterpret_cast<const float*>(s_cross4);
+  const int xd = F * D;
+  if constexpr (CROSS) {
+    const int n4 = a.cross_n * xd / 4;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) s_cross4[i] = reinterpret_cast<const float4*>(a.cross_w)[i];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int nwaves = gridDim.x * (blockDim.x >> 6);
   // this wave's rows: b0 + k * nwaves; each iteration has R of them in flight
@@ -336,6 +355,9 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
       float s[8], q[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+      float dots[kCrossMax];
+#pragma unroll
+      for (int l = 0; l < kCrossMax; ++l) dots[l] = 0.f;
       float amax = 0.f;
       bf16x8 ox[MAXG];
 #pragma unroll
@@ -351,6 +373,17 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
             q[j] += e * e;
             o[j] = f2bf(e);
             amax = fmaxf(amax, fabsf(bf2f(o[j])));
+          }
+          if constexpr (CROSS) {  // x0 (as stored: bf16) . w_l for every weight row
+#pragma unroll
+            for (int l = 0; l < kCrossMax; ++l) {
+              if (l < a.cross_n) {
+                const float4* wr = reinterpret_cast<const float4*>(s_cross + l * xd + f * D + dl);
+                const float4 w0 = wr[0], w1 = wr[1];
+                dots[l] += bf2f(o[0]) * w0.x + bf2f(o[1]) * w0.y + bf2f(o[2]) * w0.z + bf2f(o[3]) * w0.w +
+                           bf2f(o[4]) * w1.x + bf2f(o[5]) * w1.y + bf2f(o[6]) * w1.z + bf2f(o[7]) * w1.w;
+              }
+            }
           }
           ox[g] = o;
           if (out_x) *reinterpret_cast<bf16x8*>(out_x + int64_t(bk) * a.x_ld + int64_t(f) * D + dl) = o;
@@ -377,7 +410,17 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
         for (int64_t c = int64_t(F) * D / 8 + lane; c < a.q_ld / 8; c += kWave)
           *reinterpret_cast<int2*>(qrow + c * 8) = make_int2(0, 0);
       }
-      if (a.out_fm) {
+      if constexpr (CROSS) {
+#pragma unroll
+        for (int l = 0; l < kCrossMax; ++l)
+          if (l < a.cross_n) dots[l] = wave_sum(dots[l]);
+        if (lane == 0) {
+          const int L = a.cross_n - 1;
+          float alpha = 1.f;
+          for (int l = 0; l < L; ++l) alpha += alpha * dots[l] + a.cross_c[l];  // alpha_{l+1} = alpha_l + s_l
+          a.out_fm[bk] = alpha * dots[L] + a.cross_c[L];
+        }
+      } else if (a.out_fm) {
         const float logit = fm_row_logit<LPR>(s, q, lin_w[k], a.fm2 != 0, lane);
         if (lane == 0) a.out_fm[bk] = a.bias + logit;
       }
@@ -500,6 +543,13 @@ void set_embed_wave_cap(int waves, int rows_in_flight) {
 
 template <int D, int R>
 static void embed_pipe_dispatch(const EmbedArgs& a, dim3 grid, dim3 block, uint64_t magic, hipStream_t st) {
+  if (a.cross_n > 0) {  // DCN v1: the cross network rides on the gather (weights in LDS)
+    const size_t lds = size_t(a.cross_n) * a.F * D * sizeof(float);
+    if (a.arena) hipLaunchKernelGGL((embed_pipe_kernel<D, int64_t, true, R, true>), grid, block, lds, st, a, magic);
+    else if (a.ids64) hipLaunchKernelGGL((embed_pipe_kernel<D, int64_t, false, R, true>), grid, block, lds, st, a, magic);
+    else hipLaunchKernelGGL((embed_pipe_kernel<D, int32_t, false, R, true>), grid, block, lds, st, a, magic);
+    return;
+  }
   if (a.arena) hipLaunchKernelGGL((embed_pipe_kernel<D, int64_t, true, R>), grid, block, 0, st, a, magic);
   else if (a.ids64) hipLaunchKernelGGL((embed_pipe_kernel<D, int64_t, false, R>), grid, block, 0, st, a, magic);
   else hipLaunchKernelGGL((embed_pipe_kernel<D, int32_t, false, R>), grid, block, 0, st, a, magic);
@@ -526,6 +576,11 @@ static void embed_dispatch(const EmbedArgs& a, hipStream_t st) {
 
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st) {
   if (a.B == 0) return hipSuccess;
+  // cross: pipelined kernel only, weights fit the LDS, out_fm receives the logit
+  if (a.cross_n > 0 &&
+      (a.F > kWave || g_embed_waves <= 0 || a.cross_n > kCrossMax || !a.cross_w || !a.cross_c || !a.out_fm ||
+       (int64_t(a.F) * a.D) % 4 != 0 || int64_t(a.cross_n) * a.F * a.D * 4 > 160 * 1024))
+    return hipErrorInvalidValue;
   // fp8 x: pipelined kernel only (F <= 64), whole 8-byte chunks, room for F*D columns
   if (a.out_q && (a.F > kWave || g_embed_waves <= 0 || !a.out_qs || a.q_ld < int64_t(a.F) * a.D || a.q_ld % 8))
     return hipErrorInvalidValue;

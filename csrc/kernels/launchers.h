@@ -53,7 +53,15 @@ struct EmbedArgs {
   void* out_q = nullptr;           // e4m3 [B, q_ld]
   int64_t q_ld = 0;
   float* out_qs = nullptr;         // fp32 [B]
+  // DCN v1 cross network inside the gather (pipelined kernel, F <= 64 only):
+  // cross_w = [w_0 .. w_{L-1}, head_w] fp32 [cross_n][F*D], cross_c fp32
+  // [cross_n]; out_fm[b] receives the cross half of the head logit (see
+  // embedding.hip, "K3 in the gather")
+  const float* cross_w = nullptr;
+  const float* cross_c = nullptr;
+  int cross_n = 0;                 // L + 1, at most kCrossMax
 };
+constexpr int kCrossMax = 8;
 hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 // Pipelined K1 kernel geometry: resident-wave cap (0 = one row per wave) and
 // rows in flight per wave (1 or 2).

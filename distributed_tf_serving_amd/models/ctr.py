@@ -164,9 +164,27 @@ class DCN(CTRModel):
         self.head_b = 0.0
 
     def _forward(self, ids, wts, out=None):
-        x, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
-        _, cross_logit = ops.cross_v1(x, self.cross_w, self.cross_b, want_x=False, head_w=self.head_wc)
+        # the whole cross network rides on the gather (ops.embed_cross): the
+        # wave holding x0 computes its L + 1 weight dot products
+        on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
+        x, cross_logit = ops.embed_cross(self.emb, ids, wts, self.cfg.vocab_size, self.cross_w, self.cross_b,
+                                         self.head_wc, self._cross_consts() if on_gpu else None)
         return self.mlp.forward_head(x, self.head_wd, self.head_b, extra=cross_logit, out=out)
+
+    def _cross_consts(self):
+        """Folded cross weights (ops.cross_v1_consts), recomputed only when the
+        weights change (load_state_dict): cached tensors stay valid inside
+        captured graphs."""
+        key = (self.cross_w._version, self.cross_b._version, self.head_wc._version, self.cross_w.data_ptr())
+        if getattr(self, "_cc_key", None) != key:
+            rows, c = ops.cross_v1_consts(self.cross_w, self.cross_b, self.head_wc)
+            if getattr(self, "_cc", None) is not None and self._cc[0].shape == rows.shape:
+                self._cc[0].copy_(rows)  # in place: graphs captured earlier read these buffers
+                self._cc[1].copy_(c)
+            else:
+                self._cc = (rows, c)
+            self._cc_key = key
+        return self._cc
 
 
 class DCNv2(CTRModel):

@@ -337,6 +337,40 @@ def cross_v1(x0: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_x: bool = 
     return (xl.to(x0.dtype) if want_x else None), dot
 
 
+def cross_v1_consts(w: torch.Tensor, b: torch.Tensor, head_w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Weights of the DCN v1 cross network folded for the gather (K3 in K1,
+    csrc/kernels/embedding.hip): (rows [w_0..w_{L-1}, head_w] fp32 [L+1, d],
+    c [L+1] with c_l = (b_0 + .. + b_{l-1}) . w_l and c_L = (b_0 + .. + b_{L-1})
+    . head_w). Per row the cross logit is then alpha_L (x0 . head_w) + c_L with
+    alpha_0 = 1, alpha_{l+1} = alpha_l (1 + x0 . w_l) + c_l."""
+    rows = torch.cat([w.float(), head_w.float().view(1, -1)], 0).contiguous()
+    beta = torch.cumsum(torch.cat([torch.zeros_like(b[:1].float()), b.float()], 0), 0)  # beta_0 .. beta_L
+    c = (beta * rows).sum(1).contiguous()
+    return rows, c
+
+
+def embed_cross(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: int, w: torch.Tensor,
+                b: torch.Tensor, head_w: torch.Tensor, consts=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Weighted gather + the whole DCN v1 cross network: (x bf16 [B, F*D],
+    cross logit x_L . head_w fp32 [B]). On the GPU one kernel (the gather wave
+    holds x0; ``consts`` = cross_v1_consts(...), cached by the caller); on the
+    CPU the layer-by-layer reference math."""
+    m = int(modulo) if modulo > 0 else table.shape[0]
+    on_gpu = ids.arena.is_cuda if isinstance(ids, ArenaRows) else ids.is_cuda
+    if on_gpu:
+        rows, c = consts if consts is not None else cross_v1_consts(w, b, head_w)
+        if isinstance(ids, ArenaRows):
+            x, logit, _, _ = hip().embed_arena(table, None, ids.arena, int(ids.B), int(ids.F), m, 0.0, True, True,
+                                               False, None, 0, rows, c)
+        else:
+            x, logit, _, _ = hip().embed(table, None, _rows(ids), None if wts is None else _rows(wts), m, None, None,
+                                         0.0, True, True, False, None, False, None, None, 0, rows, c)
+        return x, logit
+    x, _ = embed(table, ids, wts, modulo=m, want_x=True)
+    _, logit = cross_v1(x, w, b, want_x=False, head_w=head_w)
+    return x, logit
+
+
 # ------------------------------------------------------------------ K5
 def interaction_cols(num_sparse: int, dim: int = 64) -> int:
     used = dim + (num_sparse + 1) * num_sparse // 2

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-3 evidence in one GPU call: GPU tests, smoke, DeepFM / DCN / reference-workload benches, DeepFM
+# kernel profile. Each step under its own time limit; the script stops at the first failure.
+#   SKIP_TESTS=1 MODELS="deepfm dcn" PROFILE=1 bash scripts/gpu_r3.sh
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+    || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
+  grep -v amdgpu.ids gpurun_out/smoke.log
+fi
+for m in ${MODELS:-deepfm}; do
+  timeout -k 10 300 python -u bench.py --model $m --steps ${STEPS:-200} --warmup 20 --json-extra \
+    > gpurun_out/bench_$m.log 2>&1 || { echo "bench $m failed"; tail -40 gpurun_out/bench_$m.log; exit 1; }
+  grep '^{"metric' gpurun_out/bench_$m.log
+done
+if [ "${REF:-0}" = "1" ]; then
+  timeout -k 10 300 python -u bench.py --reference-workload > gpurun_out/bench_ref.log 2>&1 \
+    || { echo "reference workload failed"; tail -30 gpurun_out/bench_ref.log; exit 1; }
+  grep -E '^Average|^\{' gpurun_out/bench_ref.log
+fi
+if [ "${PROFILE:-0}" = "1" ]; then
+  rm -rf gpurun_out/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof -o run --output-format rocpd \
+    -- python3 bench.py --model ${PROF_MODEL:-deepfm} --steps 100 --warmup 10 --qps 0 > gpurun_out/prof.log 2>&1 \
+    || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
+  db=$(find gpurun_out/prof -name '*.db' | head -1)
+  python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} \
+    --title "${PROF_TITLE:-bench.py live path (${PROF_MODEL:-deepfm}, 32 x 512-candidate requests per step), 1 MI355X}" \
+    > gpurun_out/prof_summary.md && cat gpurun_out/prof_summary.md
+fi

@@ -601,3 +601,22 @@ def test_embed_pipelined_rows_per_wave(cuda, waves):
         _close(got[1], want[1], 0, 1e-6, "arena fm")
     finally:
         h.set_embed_wave_cap(4096)
+
+
+@pytest.mark.parametrize("D,F,L", [(64, 43, 3), (16, 43, 1), (64, 10, 7), (32, 64, 2)])
+def test_embed_cross_matches_layerwise_reference(cuda, D, F, L):
+    """K3 in K1: the gather computes DCN v1's whole cross network from its L + 1
+    dot products (alpha / c recurrence) - vs the layer-by-layer fp32 reference."""
+    g = torch.Generator().manual_seed(D + F + L)
+    V, B = 3000, 300
+    d = F * D
+    table = (torch.rand(V, D, generator=g) - 0.5).to(torch.bfloat16)
+    ids = torch.randint(0, 1 << 40, (B, F), generator=g)
+    wts = torch.rand(B, F, generator=g) * 2
+    w = (torch.rand(L, d, generator=g) - 0.5) / d ** 0.5
+    b = (torch.rand(L, d, generator=g) - 0.5) * 0.1
+    hw = (torch.rand(d, generator=g) - 0.5) / d ** 0.5
+    x, logit = ops.embed_cross(table.to(cuda), ids.to(cuda), wts.to(cuda), V, w.to(cuda), b.to(cuda), hw.to(cuda))
+    xr, lr = ops.embed_cross(table, ids, wts, V, w, b, hw)
+    _close(x, xr, 0, 0, "x")
+    _close(logit, lr, 1e-4, 1e-4, "cross logit")
