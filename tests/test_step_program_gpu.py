@@ -112,25 +112,6 @@ def test_step_program_engine_and_live_server(cuda, policy):
         live.close()
 
 
-@pytest.mark.parametrize("family", ["deepfm", "wdl"])
-def test_local_overlap_program(cuda, family):
-    """A local step as a two-lane program (gather on the aux lane, step k+1's
-    gather behind step k's first GEMM): every slot's scores match the eager
-    forward, including after steps on other slots ran in between."""
-    cfg = ModelConfig(family=family, vocab_size=100_000)
-    m = build_model(cfg, cuda)
-    F, S = cfg.num_fields, 3
-    ex = ShardExecutor(m, PackedLayout(F), [512, 2048], cuda, slots=S)
-    eng = FanoutEngine(ex, DistContext(device=cuda), mode="local", ingest="arena",
-                       arena=ArenaLayout(F, max_rows=2048), overlap=True)
-    for B in (512, 2048):
-        eng.prepare(B)
-    assert eng.program_active
-    for k in range(7):
-        B = (512, 2048)[k % 2]
-        assert eng.self_check(B, seed=k, slot=k % S)
-
-
 def test_dlrm_multi_hot_gpu_matches_cpu(cuda):
     """K1b bag kernel inside the multi-hot DLRM forward: GPU vs the fp32 CPU
     model with the same weights."""
