@@ -24,12 +24,14 @@ if [ "${REF:-0}" = "1" ]; then
   grep -E '^Average|^\{' gpurun_out/bench_ref.log
 fi
 if [ "${PROFILE:-0}" = "1" ]; then
-  rm -rf gpurun_out/prof
-  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof -o run --output-format rocpd \
-    -- python3 bench.py --model ${PROF_MODEL:-deepfm} --steps 100 --warmup 10 --qps 0 > gpurun_out/prof.log 2>&1 \
-    || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
-  db=$(find gpurun_out/prof -name '*.db' | head -1)
-  python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} \
-    --title "${PROF_TITLE:-bench.py live path (${PROF_MODEL:-deepfm}, 32 x 512-candidate requests per step), 1 MI355X}" \
-    > gpurun_out/prof_summary.md && cat gpurun_out/prof_summary.md
+  for pm in ${PROF_MODELS:-deepfm}; do
+    rm -rf gpurun_out/prof_$pm
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_$pm -o run --output-format rocpd \
+      -- python3 bench.py --model $pm --steps 100 --warmup 10 --qps 0 > gpurun_out/prof_$pm.log 2>&1 \
+      || { echo "prof $pm failed"; tail -30 gpurun_out/prof_$pm.log; exit 1; }
+    db=$(find gpurun_out/prof_$pm -name '*.db' | head -1)
+    python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} \
+      --title "bench.py live path ($pm, default step shape), 1 MI355X" > gpurun_out/prof_summary_$pm.md \
+      && head -30 gpurun_out/prof_summary_$pm.md
+  done
 fi
