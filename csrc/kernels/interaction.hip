@@ -221,6 +221,9 @@ __global__ void __launch_bounds__(256) cross_combine_kernel(const bf16* __restri
   const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (m >= M) return;
   const int nch = N / 8;
+  // the first cross layer's residual is x0 itself: read it once (a fifth of
+  // that pass's HBM bytes)
+  const bool xl_is_x0 = xl == x0;
   float v[MAXC][8];
   float amax = 0.f, acc = 0.f;
 #pragma unroll
@@ -230,7 +233,7 @@ __global__ void __launch_bounds__(256) cross_combine_kernel(const bf16* __restri
       const int64_t o = int64_t(m) * ld + ch * 8;
       const bf16x8 ty = *reinterpret_cast<const bf16x8*>(y + o);
       const bf16x8 t0 = *reinterpret_cast<const bf16x8*>(x0 + o);
-      const bf16x8 tl = *reinterpret_cast<const bf16x8*>(xl + o);
+      const bf16x8 tl = xl_is_x0 ? t0 : *reinterpret_cast<const bf16x8*>(xl + o);
       bf16x8 tz;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
