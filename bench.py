@@ -126,6 +126,10 @@ def parse_args():
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a step not finished by then fails the run instead of hanging it")
+    ap.add_argument("--h2d-wait", default=None, choices=["host", "device"],
+                    help="local steps: the launcher waits for each step's H2D copy on the host before it enqueues "
+                         "the kernels (copies never overlap) or the compute stream waits on the device (the next "
+                         "step's copy starts at once); default: the runtime's")
     ap.add_argument("--no-narrow", action="store_true",
                     help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed int32 rows / bf16")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
@@ -201,6 +205,8 @@ def build(a, ctx):
                        group=step_group)
     for b in buckets:
         eng.prepare(b)
+    if a.h2d_wait and dev.type == "cuda":
+        eng.runner().host_wait_h2d = a.h2d_wait == "host"
     if eng.program_active or eng.mode != "local":
         # one synthetic step of every bucket checked against a local / eager
         # forward on every rank (collective): a fan-out that scores wrong is

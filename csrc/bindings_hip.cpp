@@ -1015,6 +1015,9 @@ PYBIND11_MODULE(_hip, m) {
           "Bounded wait for the slot's step: (ok, error). Also polls the communicators' async errors.")
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
+      .def_property("host_wait_h2d", &dtfs::runtime::StepRunner::host_wait_h2d,
+                    &dtfs::runtime::StepRunner::set_host_wait_h2d,
+                    "local steps: wait for each step's H2D on the host (True) or on the device (False)")
       .def_property_readonly("compute_stream",
                              [](const dtfs::runtime::StepRunner& r) { return reinterpret_cast<uintptr_t>(r.compute_stream()); });
 
@@ -1112,6 +1115,8 @@ PYBIND11_MODULE(_hip, m) {
           },
           py::arg("handles"), py::arg("timeout_s") = 5.0,
           "Map every rank's mailbox (handles in rank order); messages <= cap then bypass RCCL")
+      .def("can_access_device", &dtfs::comm::RcclComm::can_access_device, py::arg("device"),
+           "hipDeviceCanAccessPeer from this communicator's device")
       .def_property_readonly("peer_enabled", &dtfs::comm::RcclComm::peer_enabled)
       .def_property_readonly("peer_cap", &dtfs::comm::RcclComm::peer_cap)
       .def_property_readonly("peer_exchanges", &dtfs::comm::RcclComm::peer_exchanges)

@@ -228,6 +228,16 @@ void RcclComm::abort() {
 
 // ---- one-shot peer exchange --------------------------------------------------
 
+bool RcclComm::can_access_device(int peer_device) const {
+  if (peer_device == device_) return true;
+  int ok = 0;
+  if (hipDeviceCanAccessPeer(&ok, device_, peer_device) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return ok != 0;
+}
+
 std::string RcclComm::peer_prepare(uint64_t cap) {
   if (peer_) throw std::runtime_error("peer exchange already prepared");
   if (nranks_ > kPeerMaxRanks) throw std::invalid_argument("peer exchange: too many ranks");

@@ -62,6 +62,8 @@ class RcclComm {
   // the same order on every rank and stream-ordered (one stream per
   // communicator): the sequence number advances kernel by kernel.
   std::string peer_prepare(uint64_t cap);
+  // hipDeviceCanAccessPeer from this communicator's device (1 for itself)
+  bool can_access_device(int peer_device) const;
   void peer_enable(const std::vector<std::string>& handles, double timeout_s);
   bool peer_enabled() const { return peer_ && peer_->enabled; }
   uint64_t peer_cap() const { return peer_ ? peer_->cap : 0; }

@@ -108,12 +108,14 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
   if (nbytes > 0) copy_checked(dst, src, nbytes, hipMemcpyHostToDevice, st, slot, "H2D");
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
-  if (consumer == compute_ && nbytes > 0) {
+  if (host_wait_h2d_ && consumer == compute_ && nbytes > 0) {
     // The launcher thread waits for the copy instead of the compute queue:
     // a cross-queue barrier packet in front of every step costs ~5-7 us of
-    // idle GPU at the step boundary (bench/step_timeline.py, MI355X), while
-    // the launcher runs ~3 steps (~500 us) ahead of the GPU, so waiting the
-    // ~100 us copy on the host costs nothing (+3.6 % served DeepFM, round 2).
+    // idle GPU at the step boundary when the copy has not landed yet
+    // (tools/studies/step_timeline.py, MI355X). The price: the launcher
+    // cannot issue the next step's copy while it waits, so copies never
+    // overlap and a step whose copy takes longer than its kernels is
+    // H2D-paced (set_host_wait_h2d(false) then lets the copy streams overlap).
     // Kernels are enqueued after the copy completed, so stream order alone is
     // enough.
     for (;;) {

@@ -147,6 +147,11 @@ class StepRunner {
   int slots() const { return int(done_.size()); }
   hipStream_t compute_stream() const { return compute_; }
   hipStream_t copy_stream() const { return copy_; }
+  // Local steps: the launcher waits on the host for each step's H2D before it
+  // enqueues the step's kernels (true), or the compute stream waits for the
+  // copy's event on the device (false) - see h2d().
+  void set_host_wait_h2d(bool v) { host_wait_h2d_ = v; }
+  bool host_wait_h2d() const { return host_wait_h2d_; }
 
  private:
   int device_;
@@ -154,6 +159,7 @@ class StepRunner {
                     const char* what);
   void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
   hipStream_t copy2_ = nullptr;  // second H2D stream, alternated with copy_ by local steps
+  bool host_wait_h2d_ = true;
   uint64_t n_h2d_ = 0;
   // host saw the slot's last step complete (set by wait/query, possibly from
   // another thread than the launcher)

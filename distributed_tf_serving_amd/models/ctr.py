@@ -290,8 +290,10 @@ class DLRM(CTRModel):
         assert D == 64, "DLRM dot-interaction kernel is built for D = 64"
         assert cfg.bottom_mlp[-1] == D, "bottom MLP must end at the embedding dim"
         self.T = T
-        self.dense_k = pad8(cfg.num_dense)
-        self.bottom = MLP(cfg.num_dense, cfg.bottom_mlp, self.dtype, self.device_, self.gen)
+        # dense features zero padded to one 128-byte K tile: the bottom MLP's
+        # first GEMM takes the LDS-DMA kernel, not the register-staged fallback
+        self.dense_k = -(-cfg.num_dense // 64) * 64
+        self.bottom = MLP(cfg.num_dense, cfg.bottom_mlp, self.dtype, self.device_, self.gen, in_pad=self.dense_k)
         self.inter_cols = ops.interaction_cols(T, D)
         self.top = MLP(self.inter_cols, cfg.mlp_dims, self.dtype, self.device_, self.gen)
         self.head_w = nn.Parameter(init_uniform_(torch.empty(self.top.out_dim, device=self.device_), 0.05, self.gen),

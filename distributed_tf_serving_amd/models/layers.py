@@ -119,13 +119,14 @@ class Dense(nn.Module):
 
 class MLP(nn.Module):
     def __init__(self, in_dim: int, dims: Sequence[int], dtype, device, gen, fp8: bool = False,
-                 last_act: str = "relu"):
+                 last_act: str = "relu", in_pad: Optional[int] = None):
+        """``in_pad``: the first layer's K (>= in_dim, zero weight columns)."""
         super().__init__()
         layers: List[Dense] = []
         d = in_dim
         for i, h in enumerate(dims):
             act = "relu" if i < len(dims) - 1 else last_act
-            layers.append(Dense(d, h, act, dtype, device, gen, fp8=fp8))
+            layers.append(Dense(d, h, act, dtype, device, gen, fp8=fp8, in_pad=in_pad if i == 0 else None))
             d = h
         self.layers = nn.ModuleList(layers)
         self.out_dim = d

@@ -373,8 +373,11 @@ def embed_cross(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: i
 
 # ------------------------------------------------------------------ K5
 def interaction_cols(num_sparse: int, dim: int = 64) -> int:
+    """Width of the interaction output (and the top MLP's K), zero padded to a
+    multiple of 64: the top MLP's first GEMM then reads whole 128-byte K tiles
+    (LDS-DMA / 8-phase kernels) instead of the register-staged fallback."""
     used = dim + (num_sparse + 1) * num_sparse // 2
-    return (used + 7) // 8 * 8
+    return (used + 63) // 64 * 64
 
 
 def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0,

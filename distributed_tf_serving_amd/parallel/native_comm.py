@@ -23,7 +23,8 @@ def peer_cap_from_env() -> int:
     return 0 if v <= 0 else (64 << 10 if v == 1 else v)
 
 
-def create_comm(ctx: DistContext, group=None, peer_cap: Optional[int] = None, peer_timeout_s: float = 5.0):
+def create_comm(ctx: DistContext, group=None, peer_cap: Optional[int] = None, peer_timeout_s: float = 5.0,
+                can_access=None):
     """A new RcclComm over the ranks of ``group`` (default: the world).
 
     ``peer_cap`` > 0 (default: ``peer_cap_from_env()``) also sets up the
@@ -47,20 +48,44 @@ def create_comm(ctx: DistContext, group=None, peer_cap: Optional[int] = None, pe
     dist.broadcast_object_list(obj, src=src, group=group)
     c = h.RcclComm(obj[0], world, rank, dev)
     if cap > 0:
-        enable_peer(c, cap, group, peer_timeout_s)
+        enable_peer(c, cap, group, peer_timeout_s, can_access=can_access)
     return c
 
 
-def enable_peer(comm, cap: int, group=None, timeout_s: float = 5.0) -> None:
+def enable_peer(comm, cap: int, group=None, timeout_s: float = 5.0, can_access=None) -> bool:
     """Collective: export every rank's mailbox, exchange the IPC handles over
     torch.distributed, map them. After it, every rank's exchanges of at most
-    ``cap`` bytes per peer run as one peer.hip kernel."""
+    ``cap`` bytes per peer run as one peer.hip kernel.
+
+    The kernel stores into every peer's memory directly, so it needs peer
+    access between EVERY pair of devices: each rank checks
+    ``hipDeviceCanAccessPeer`` to every other rank's device (``can_access``:
+    a test hook with the same signature) and the ranks agree; if any pair
+    cannot, no rank enables it and every exchange stays on RCCL (returns
+    False)."""
+    import sys
+
+    world = dist.get_world_size(group)
+    dev = torch.cuda.current_device()
+    devs = [None] * world
+    dist.all_gather_object(devs, dev, group=group)
+    check = can_access or comm.can_access_device
+    ok = all(bool(check(int(d))) for d in devs)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    if dist.get_backend(group) != "gloo":
+        flag = flag.cuda()
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if not int(flag.item()):
+        print(f"[native_comm] rank {dist.get_rank(group)}: a device pair has no peer access "
+              f"({'here' if not ok else 'on another rank'}); exchanges stay on RCCL", file=sys.stderr, flush=True)
+        return False
     mine = comm.peer_prepare(int(cap))
     handles = [None] * comm.nranks
     dist.all_gather_object(handles, mine, group=group)
     comm.peer_enable(handles, timeout_s)
     # every rank has mapped every mailbox before anyone pushes into one
     dist.barrier(group=group)
+    return True
 
 
 def check_comms(*comms) -> Optional[str]:

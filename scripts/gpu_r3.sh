@@ -23,6 +23,35 @@ if [ "${REF:-0}" = "1" ]; then
     || { echo "reference workload failed"; tail -30 gpurun_out/bench_ref.log; exit 1; }
   grep -E '^Average|^\{' gpurun_out/bench_ref.log
 fi
+if [ "${FRONTENDS:-}" != "" ]; then
+  # the reference workload (DCN, 1500 identical candidates, 6 closed-loop clients) over the gRPC front door,
+  # with K server processes sharing the port (serving/server.py --frontends K)
+  mkdir -p gpurun_out/frontends
+  for k in $FRONTENDS; do
+    port=$((9950 + k))
+    python -u -m distributed_tf_serving_amd.serving.server --preset reference_dcn --port $port --frontends $k \
+      > gpurun_out/frontends/server_$k.log 2>&1 &
+    spid=$!
+    python - "$port" <<'PYEOF' || { echo "server $k did not start"; kill $spid; tail -20 gpurun_out/frontends/server_$k.log; exit 1; }
+import socket, sys, time
+port = int(sys.argv[1]); t0 = time.time()
+while time.time() - t0 < 200:
+    try:
+        socket.create_connection(("127.0.0.1", port), timeout=1).close(); sys.exit(0)
+    except OSError:
+        time.sleep(1)
+sys.exit(1)
+PYEOF
+    sleep $((3 * k))
+    timeout -k 10 200 python -u -m distributed_tf_serving_amd.client.loadgen --hosts 127.0.0.1:$port --backends 1 \
+      --candidates 1500 --id-mode reference --concurrency 6 --requests ${REF_REQS:-1000} --warmup 30 --quiet \
+      --json-out gpurun_out/frontends/ref_grpc_$k.json > gpurun_out/frontends/loadgen_$k.log 2>&1
+    rc=$?
+    kill $spid; wait $spid 2>/dev/null
+    [ $rc = 0 ] || { echo "loadgen $k failed"; tail -20 gpurun_out/frontends/loadgen_$k.log; exit 1; }
+    echo "frontends=$k $(grep Average gpurun_out/frontends/loadgen_$k.log) $(cat gpurun_out/frontends/ref_grpc_$k.json)"
+  done
+fi
 if [ "${PROFILE:-0}" = "1" ]; then
   for pm in ${PROF_MODELS:-deepfm}; do
     rm -rf gpurun_out/prof_$pm

@@ -77,3 +77,13 @@ def test_peer_exchange_dead_rank_times_out():
         pytest.skip("no GPU")
     out = _run(2, "--fault", "--timeout-s", "1.5")
     assert out["fault_detected"] and 1.0 <= out["waited_s"] < 20
+
+
+def test_peer_exchange_falls_back_to_rccl_without_peer_access():
+    """One rank reports no hipDeviceCanAccessPeer to the others: the ranks agree
+    to keep every exchange on RCCL (no mailbox is mapped), and the exchanges
+    stay exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = _run(2, "--deny-access", "--sizes", "1,4096")
+    assert out["fallback"] == "rccl" and out["checked_sizes"] == [1, 4096]

@@ -86,6 +86,8 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--timeout-s", type=float, default=5.0)
     ap.add_argument("--fault", action="store_true", help="last rank skips an exchange; the others must time out")
+    ap.add_argument("--deny-access", action="store_true",
+                    help="the last rank reports no peer access to the others: every rank must fall back to RCCL")
     a = ap.parse_args(argv)
     ctx = init_from_env()
     dev, rank, world = ctx.device, ctx.rank, ctx.world
@@ -93,9 +95,21 @@ def main(argv=None) -> int:
         raise SystemExit("run with torch.distributed.run and >= 2 ranks")
     sizes = [int(s) for s in a.sizes.split(",")]
     cap = max(sizes)
-    peer = create_comm(ctx, peer_cap=cap, peer_timeout_s=a.timeout_s)
+    deny = (lambda d: int(d) == torch.cuda.current_device()) if (a.deny_access and rank == world - 1) else None
+    peer = create_comm(ctx, peer_cap=cap, peer_timeout_s=a.timeout_s, can_access=deny)
+    out = {"world": world}
+    if a.deny_access:
+        assert not peer.peer_enabled, "one rank had no peer access: the peer path must stay off everywhere"
+        for i, n in enumerate(sizes):
+            check(peer, world, rank, n, 300 + i, dev)
+        assert peer.peer_exchanges == 0 and peer.async_error() == ""
+        out.update(fallback="rccl", checked_sizes=sizes)
+        dist.barrier()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return 0
     assert peer.peer_enabled and peer.peer_cap >= cap
-    out = {"world": world, "cap": peer.peer_cap}
+    out["cap"] = peer.peer_cap
     if a.fault:
         x = torch.zeros(world * 64, dtype=torch.uint8, device=dev)
         y = torch.empty_like(x)
