@@ -95,7 +95,9 @@ def main(argv=None) -> int:
         raise SystemExit("run with torch.distributed.run and >= 2 ranks")
     sizes = [int(s) for s in a.sizes.split(",")]
     cap = max(sizes)
-    deny = (lambda d: int(d) == torch.cuda.current_device()) if (a.deny_access and rank == world - 1) else None
+    # (ranks sharing one GPU in the rehearsal all report the same device: the
+    # hook denies every pair, its own device included)
+    deny = (lambda d: False) if (a.deny_access and rank == world - 1) else None
     peer = create_comm(ctx, peer_cap=cap, peer_timeout_s=a.timeout_s, can_access=deny)
     out = {"world": world}
     if a.deny_access:
