@@ -130,6 +130,9 @@ def parse_args():
                     help="local steps: the launcher waits for each step's H2D copy on the host before it enqueues "
                          "the kernels (copies never overlap) or the compute stream waits on the device (the next "
                          "step's copy starts at once); default: the runtime's")
+    ap.add_argument("--embed-geometry", default=None, metavar="WAVES,ROWS",
+                    help="pipelined gather geometry for a study: resident-wave cap and rows in flight per wave "
+                         "(default: the kernel's 4096,1)")
     ap.add_argument("--no-narrow", action="store_true",
                     help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed int32 rows / bf16")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
@@ -176,6 +179,11 @@ def build(a, ctx):
     # thread, so they get a group of their own (the main thread syncs phases
     # on the default group)
     step_group = dist.new_group(backend="gloo") if (world > 1 and dev.type != "cuda") else None
+    if a.embed_geometry and dev.type == "cuda":  # before any capture: the graphs bake the grid in
+        from distributed_tf_serving_amd.ops import hip
+
+        w, r = (int(x) for x in a.embed_geometry.split(","))
+        hip().set_embed_wave_cap(w, r)
     model = build_parallel_model(cfg, dev, ctx, shard_tables="on" if a.shard_tables else "auto", group=step_group)
     F = cfg.num_fields
     B = a.requests_per_gpu * a.request_rows  # rows each GPU computes per step
