@@ -115,7 +115,7 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
     // (tools/studies/step_timeline.py, MI355X). The price: the launcher
     // cannot issue the next step's copy while it waits, so copies never
     // overlap and a step whose copy takes longer than its kernels is
-    // H2D-paced (set_host_wait_h2d(false) then lets the copy streams overlap).
+    // H2D-paced: the default is the device-side wait (step_runner.h).
     // Kernels are enqueued after the copy completed, so stream order alone is
     // enough.
     for (;;) {

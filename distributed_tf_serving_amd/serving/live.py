@@ -33,7 +33,7 @@ from .errors import Code, ServingError
 log = logging.getLogger(__name__)
 
 
-from .packing import NARROW_FAMILIES  # noqa: E402  (single-modulo families)
+from .packing import host_narrow_modulo  # noqa: E402
 
 
 def _code(c: int) -> Code:
@@ -71,15 +71,14 @@ class LiveScheduler:
         self.output_key, self.ids_key, self.wts_key = sc.output_key, sc.ids_key, sc.wts_key
         self.signature_name = sc.signature_name
         depth = int(depth or self.ex.slots)
-        # host-side K0 (csrc/runtime/narrow.h): single-table families hash ids
-        # with one modulo (the table size), so the host can narrow them to
-        # int32 rows + bf16 weights while it copies each request
+        # host-side K0 (csrc/runtime/narrow.h): families whose ids all hash with
+        # one modulo let the host narrow them to int32 rows while it copies
+        # each request (weights stay fp32): 8 instead of 12 bytes per feature
         model = self.ex.model
-        can_narrow = (getattr(model, "family", "") in NARROW_FAMILIES
-                      and 0 < int(getattr(model.cfg, "vocab_size", 0)) < (1 << 31))
+        m = host_narrow_modulo(model.cfg)
         if narrow is None:  # default: GPU servables (a CPU backend gains nothing from fewer bytes)
             narrow = bool(getattr(sc, "narrow_ingest", True)) and engine.cuda
-        self.narrow_modulo = int(model.cfg.vocab_size) if (narrow and can_narrow) else 0
+        self.narrow_modulo = m if narrow else 0
         self.arenas = [self.layout.alloc(pin=engine.cuda) for _ in range(int(n_arenas or depth + 3))]
         self.config = dict(
             fields=self.fields, ids_key=sc.ids_key, wts_key=sc.wts_key, model_name=self.model_name,

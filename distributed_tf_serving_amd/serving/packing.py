@@ -75,6 +75,22 @@ class PackedLayout:
 NARROW_FAMILIES = ("wdl", "deepfm", "dcn", "dcn_v2")
 
 
+def host_narrow_modulo(cfg) -> int:
+    """The modulo the host may apply to every id of a request before the GPU
+    sees it (int32 rows on the wire), 0 if none: the single table of the
+    shared-table families; for DLRM the per-table row count, which every
+    table shares (its per-table offset is added on the GPU, so a 100M-row x
+    30 table model still fits int32 rows; re-hashing a reduced row with the
+    same modulo is the identity)."""
+    if cfg.family in NARROW_FAMILIES:
+        m = int(getattr(cfg, "vocab_size", 0))
+    elif cfg.family == "dlrm":
+        m = int(getattr(cfg, "table_rows", 0))
+    else:
+        m = 0
+    return m if 0 < m < (1 << 31) else 0
+
+
 def layout_for(cfg, fanout: bool) -> PackedLayout:
     """Packed rows a shard backend uses: narrow when the rows are exchanged
     between GPUs (candidate fan-out) and the model allows it."""
