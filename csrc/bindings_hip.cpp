@@ -251,6 +251,92 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
   return {x, fm, q, qs};
 }
 
+// ---------------------------------------------------------------- K1 fused into K4
+// DeepFM / WDL first MLP layer straight from the table: the resolve kernel
+// (ids / weights -> field-major rows / weights + first-order term) then the
+// gather-GEMM (csrc/kernels/gemm.hip gemm_gather_kernel). Rows come from a
+// device request arena (arena, B, F) or from ids [B, F] (+ wts). Returns
+//   h     bf16 [B, N] = act(x . W^T + b), x = w * T[row] never materialised
+//   parts fp32 [1 + 4 fm2, Mp]: row 0 = bias + first-order FM term, rows 1..4
+//         the second-order FM term over 4 partitions (the head sums them).
+std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::Tensor> lin,
+                                      c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
+                                      c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
+                                      double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2) {
+  check_dev(table, "table");
+  check_dev(W, "W");
+  check_dev(b, "b");
+  check_same_dev(table, W, "W");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2 && table.size(1) == 64 &&
+                  table.is_contiguous(),
+              "gather-GEMM: table must be contiguous bf16 [V, 64]");
+  const int64_t V = table.size(0);
+  TORCH_CHECK(F >= 1 && F <= 64, "gather-GEMM handles 1..64 fields");
+  TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]");
+  TORCH_CHECK(W.scalar_type() == torch::kBFloat16 && W.dim() == 2 && W.size(1) == F * 64 && W.is_contiguous(),
+              "W must be contiguous bf16 [N, 64 F]");
+  const int64_t N = W.size(0);
+  TORCH_CHECK(N % 256 == 0 && (!fm2 || N >= 1024), "gather-GEMM needs N % 256 == 0 (and N >= 1024 with FM)");
+  TORCH_CHECK(b.scalar_type() == torch::kFloat32 && b.numel() == N, "b must be fp32 [N]");
+  TORCH_CHECK(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
+  }
+  dtfs::EmbedArgs a;
+  if (arena) {
+    check_dev(*arena, "arena");
+    check_same_dev(table, *arena, "arena");
+    TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous() &&
+                    arena->numel() > dtfs::kArenaPayloadOff,
+                "arena must be a contiguous uint8 device buffer");
+    TORCH_CHECK(!ids && !wts, "arena rows carry their own ids / weights");
+    a.arena = arena->data_ptr();
+  } else {
+    TORCH_CHECK(ids.has_value(), "gather-GEMM needs an arena or ids");
+    check_dev(*ids, "ids");
+    check_same_dev(table, *ids, "ids");
+    TORCH_CHECK((ids->scalar_type() == torch::kInt64 || ids->scalar_type() == torch::kInt32) && ids->dim() == 2 &&
+                    ids->size(0) == B && ids->size(1) == F && ids->stride(1) == 1 && ids->stride(0) >= F,
+                "ids must be int32/int64 [B, F] with contiguous rows");
+    a.ids = ids->data_ptr();
+    a.ids64 = ids->scalar_type() == torch::kInt64;
+    a.ids_ld = ids->stride(0);
+    if (wts) {
+      check_dev(*wts, "wts");
+      TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->size(0) == B && wts->size(1) == F &&
+                      wts->stride(1) == 1 && wts->stride(0) >= F,
+                  "wts must be fp32 [B, F] with contiguous rows");
+      a.wts = wts->data_ptr();
+      a.wts_ld = wts->stride(0);
+    }
+  }
+  c10::DeviceGuard g(table.device());
+  const int64_t Mp = (B + 255) / 256 * 256;
+  auto h = torch::empty({B, N}, table.options());
+  auto parts = torch::empty({fm2 ? 5 : 1, Mp}, table.options().dtype(torch::kFloat32));
+  auto rows_t = torch::empty({F, Mp}, table.options().dtype(torch::kInt32));
+  auto wts_t = torch::empty({F, Mp}, table.options().dtype(torch::kFloat32));
+  if (B == 0) return {h, parts};
+  a.table = table.data_ptr();
+  a.lin = lin ? lin->data_ptr<float>() : nullptr;
+  a.B = int(B);
+  a.F = int(F);
+  a.D = 64;
+  a.V = V;
+  a.modulo = modulo;
+  a.bias = float(bias);
+  auto st = cur_stream(table);
+  check_hip(dtfs::launch_embed_resolve(a, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), parts.data_ptr<float>(),
+                                       Mp, st),
+            "embed_resolve");
+  check_hip(dtfs::launch_gemm_gather(table.data_ptr(), V, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), Mp,
+                                     int(F), W.data_ptr(), b.data_ptr<float>(), h.data_ptr(), N,
+                                     fm2 ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st),
+            "gemm_gather");
+  return {h, parts};
+}
+
 // ---------------------------------------------------------------- K1b
 torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
                             c10::optional<torch::Tensor> psw, int64_t modulo, bool mean, bool out_bf16) {
@@ -471,6 +557,20 @@ torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tenso
 }
 
 // ---------------------------------------------------------------- K6
+// A head's extra logit: fp32 [M], or fp32 [P, >= M] partials summed in order
+// (row stride >= M, unit inner stride: the gather-GEMM path's [1 + 4, Mp]).
+static void check_extra(const torch::Tensor& e, int64_t M) {
+  TORCH_CHECK(e.scalar_type() == torch::kFloat32, "extra must be fp32");
+  if (e.dim() == 2) {
+    TORCH_CHECK(e.size(0) >= 1 && e.size(1) >= M && e.stride(1) == 1 && e.stride(0) >= M,
+                "extra partials must be fp32 [P, >= M] with contiguous rows");
+  } else {
+    TORCH_CHECK(e.numel() == M && e.is_contiguous(), "extra must be fp32 [M]");
+  }
+}
+static int extra_rows(const torch::Tensor& e) { return e.dim() == 2 ? int(e.size(0)) : 1; }
+static int64_t extra_stride(const torch::Tensor& e) { return e.dim() == 2 ? e.stride(0) : 0; }
+
 torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<torch::Tensor> extra, bool sigmoid) {
   check_dev(x, "x");
   check_dev(w, "w");
@@ -480,13 +580,14 @@ torch::Tensor head(torch::Tensor x, torch::Tensor w, double bias, c10::optional<
   TORCH_CHECK(w.scalar_type() == torch::kFloat32 && w.numel() == K, "w must be fp32 [K]");
   if (extra) {
     check_dev(*extra, "extra");
-    TORCH_CHECK(extra->scalar_type() == torch::kFloat32 && extra->numel() == M, "extra must be fp32 [M]");
+    check_extra(*extra, M);
   }
   c10::DeviceGuard g(x.device());
   auto out = torch::empty({M}, x.options().dtype(torch::kFloat32));
   check_hip(dtfs::launch_head(x.data_ptr(), K, w.data_ptr<float>(), float(bias),
                               extra ? extra->data_ptr<float>() : nullptr, int(M), int(K), sigmoid ? 2 : 0,
-                              out.data_ptr<float>(), cur_stream(x)),
+                              out.data_ptr<float>(), cur_stream(x), extra ? extra_rows(*extra) : 1,
+                              extra ? extra_stride(*extra) : 0),
             "head");
   return out;
 }
@@ -535,14 +636,15 @@ torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, in
   TORCH_CHECK(hw.scalar_type() == torch::kFloat32 && hw.numel() == N, "hw must be fp32 [N]");
   if (extra) {
     check_dev(*extra, "extra");
-    TORCH_CHECK(extra->scalar_type() == torch::kFloat32 && extra->numel() == M, "extra must be fp32 [M]");
+    check_extra(*extra, M);
   }
   c10::DeviceGuard g(A.device());
   torch::Tensor y;
   float* yp = score_out(A, M, out, y);
   check_hip(dtfs::launch_gemm_head(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr<float>(), int(act),
                                    hw.data_ptr<float>(), float(hbias), extra ? extra->data_ptr<float>() : nullptr,
-                                   sigmoid ? 2 : 0, yp, int(M), int(N), int(K), cur_stream(A)),
+                                   sigmoid ? 2 : 0, yp, int(M), int(N), int(K), cur_stream(A),
+                                   extra ? extra_rows(*extra) : 1, extra ? extra_stride(*extra) : 0),
             "gemm_head");
   return y;
 }
@@ -916,6 +1018,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
         py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none(),
         py::arg("k_pad") = 0, py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none());
+  m.def("embed_gemm", &embed_gemm, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"), py::arg("wts"),
+        py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W"), py::arg("b"), py::arg("act"),
+        py::arg("fm2"));
   m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
         py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
         py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0, py::arg("cross_w") = py::none(),

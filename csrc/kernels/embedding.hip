@@ -428,6 +428,94 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
   }
 }
 
+// ---------------------------------------------------------------- K1 front half (gather-GEMM path)
+// For the fused gather-GEMM (gemm.hip gemm_gather_kernel): row b's ids and
+// weights (request arena or id / weight rows) -> clamped table rows and
+// weights, written FIELD-MAJOR - rows_t[f][b], wts_t[f][b], b < Mp (B rounded
+// up to 256) - so the GEMM stages one K tile's 256 candidates with a single
+// 4-byte LDS-DMA per lane; plus the first-order FM term
+//   part0[b] = bias + sum_f lin[row(b, f)] * w(b, f).
+// Rows b in [B, Mp): row 0, weight 0 (they contribute nothing).
+// Block = 256 threads over 64 candidates. Item i = t + 256k is (row i / F,
+// field i % F): consecutive lanes read consecutive fields of one row, and a
+// thread issues all its items' loads before using any (a row is three
+// dependent round trips: descriptor, id / weight, lin). An LDS transpose
+// then writes each field's 64 rows as one 256-byte store.
+template <typename IdT, bool ARENA>
+__global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_t magic, int32_t* __restrict__ rows_t,
+                                                           float* __restrict__ wts_t, float* __restrict__ part0,
+                                                           int64_t Mp) {
+  constexpr int RB = 64, KMAX = (kWave * RB) / 256;  // items per thread for F <= 64
+  __shared__ int32_t s_row[kWave * RB];
+  __shared__ float s_w[kWave * RB];
+  __shared__ float s_lin[kWave * RB];
+  __shared__ int2 s_desc[RB];
+  const int F = a.F, t = threadIdx.x, n = F * RB;
+  const int b0 = blockIdx.x * RB;
+  const uint8_t* payload = nullptr;
+  int64_t a_rows = 0;
+  if constexpr (ARENA) {
+    const uint8_t* arena = static_cast<const uint8_t*>(a.arena);
+    a_rows = *reinterpret_cast<const int64_t*>(arena + 8);
+    payload = arena + kArenaPayloadOff;
+    if (t < RB) {
+      const int b = b0 + t;
+      const int2* desc = reinterpret_cast<const int2*>(payload + *reinterpret_cast<const int64_t*>(arena + 16));
+      s_desc[t] = (b < a.B && b < a_rows) ? desc[b] : int2{0, 0};
+    }
+    __syncthreads();
+  }
+  int64_t id[KMAX];
+  float w[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int i = t + 256 * k;
+    id[k] = 0;
+    w[k] = 0.f;
+    if (i >= n) continue;
+    const int r = i / F, f = i - r * F, b = b0 + r;
+    if constexpr (ARENA) {
+      if (b < a.B && b < a_rows) {
+        const int2 d = s_desc[r];
+        const ArenaRow ar{payload + (d.x & 0x7fffffff), payload + d.y, d.x < 0};
+        arena_feature(ar, f, id[k], w[k]);
+      }
+    } else if (b < a.B) {
+      id[k] = int64_t(static_cast<const IdT*>(a.ids)[int64_t(b) * a.ids_ld + f]);
+      w[k] = load_weight(a, int64_t(b) * a.wts_ld + f);
+    }
+  }
+  int32_t row[KMAX];
+  float lin[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    int64_t g = magic ? hash_row_magic(id[k], a.modulo, magic) : hash_row(id[k], a.modulo);
+    g = g < 0 ? 0 : (g >= a.V ? a.V - 1 : g);  // memory safety whatever the ids say
+    row[k] = int32_t(g);
+    lin[k] = (a.lin && t + 256 * k < n) ? a.lin[g] * w[k] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int i = t + 256 * k;
+    if (i >= n) continue;
+    const int r = i / F, f = i - r * F;
+    s_row[f * RB + r] = row[k];
+    s_w[f * RB + r] = w[k];
+    s_lin[f * RB + r] = lin[k];
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const int f = i / RB, r = i % RB;
+    rows_t[int64_t(f) * Mp + b0 + r] = s_row[i];
+    wts_t[int64_t(f) * Mp + b0 + r] = s_w[i];
+  }
+  if (t < RB) {
+    float s = a.bias;
+    for (int f = 0; f < F; ++f) s += s_lin[f * RB + t];
+    part0[b0 + t] = s;
+  }
+}
+
 // ---------------------------------------------------------------- K1b
 // Sum-pooled embedding bag: out[b, :] = sum_{i in [off[b], off[b+1])} w_i * T[idx_i, :]
 // One wave per bag; each lane owns 8 dims of up to D=512 (LPR<=64 lanes).
@@ -501,6 +589,23 @@ __global__ void __launch_bounds__(256) shard_route_kernel(const IdT* __restrict_
 
 // ---------------------------------------------------------------- launchers
 using namespace kern;
+
+hipError_t launch_embed_resolve(const EmbedArgs& a, int32_t* rows_t, float* wts_t, float* part0, int64_t Mp,
+                                hipStream_t st) {
+  if (a.F < 1 || a.F > kWave || a.modulo <= 0 || a.modulo_f || a.shard_lo_f || Mp % 256 != 0 || Mp < a.B ||
+      a.V < 1 || a.V > (int64_t(1) << 31) || !rows_t || !wts_t || !part0)
+    return hipErrorInvalidValue;
+  if (Mp == 0) return hipSuccess;
+  const uint64_t magic = a.modulo < (int64_t(1) << 32) ? ~uint64_t(0) / uint64_t(a.modulo) : 0;
+  dim3 grid(unsigned(Mp / 64)), block(256);
+  if (a.arena)
+    hipLaunchKernelGGL((embed_resolve_kernel<int64_t, true>), grid, block, 0, st, a, magic, rows_t, wts_t, part0, Mp);
+  else if (a.ids64)
+    hipLaunchKernelGGL((embed_resolve_kernel<int64_t, false>), grid, block, 0, st, a, magic, rows_t, wts_t, part0, Mp);
+  else
+    hipLaunchKernelGGL((embed_resolve_kernel<int32_t, false>), grid, block, 0, st, a, magic, rows_t, wts_t, part0, Mp);
+  return hipGetLastError();
+}
 
 hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n, int F, const int64_t* modulo_f,
                            const int64_t* offset_f, int64_t modulo, hipStream_t st) {

@@ -599,8 +599,9 @@ __global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restric
                                                         const uint8_t* __restrict__ W, int64_t ldw,
                                                         const float* __restrict__ bias, int act,
                                                         const float* __restrict__ hw, float hbias,
-                                                        const float* __restrict__ extra, int out_act,
-                                                        float* __restrict__ y, int M, int N, int K) {
+                                                        const float* __restrict__ extra, int extra_n,
+                                                        int64_t extra_ld, int out_act, float* __restrict__ y, int M,
+                                                        int N, int K) {
   constexpr int WN_ = 4, NW = 4;
   constexpr int BN = 16 * TN * WN_;
   constexpr int TM = BM / 16;
@@ -707,7 +708,8 @@ __global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restric
   for (int row = threadIdx.x; row < BM; row += blockDim.x) {
     const int m = m0 + row;
     if (m >= M) continue;
-    float s = hbias + (extra ? extra[m] : 0.f);
+    float s = hbias;
+    for (int e = 0; extra && e < extra_n; ++e) s += extra[e * extra_ld + m];
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[w * BM + row];
     y[m] = out_act == EPI_SIGMOID ? sigmoidf(s) : s;
@@ -973,6 +975,276 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
 }
 
 // ---------------------------------------------------------------------------
+// K1 fused into K4: the first MLP layer of DeepFM / WDL straight from the
+// embedding table (the north star's "LDS-staged sparse gather"):
+//   C[m, n] = act( sum_f bf16(w[m,f] * T[row(m,f)]) . W[n, 64f .. 64f+63] + b[n] )
+// on the 8-phase schedule of gemm_8ph_kernel (plain form). K tile f is field f:
+// its A tile is the 128-byte table row of each of the block's 256 candidates,
+// staged by the same LDS-DMA instructions as the dense kernel but from
+// table + row * 128 per lane. The rows and weights of a K tile come from
+// embed_resolve_kernel's field-major rows_t / wts_t [F][Mp] through an 8-slot
+// LDS ring: ONE 4-byte LDS-DMA per lane per K tile (waves 0-3 rows, 4-7
+// weights), issued in phase 0 three tiles ahead. That makes phase 0 issue 3
+// DMA instructions and the others 2, so every 4 consecutive phases issue 9:
+// the counted wait becomes vmcnt(9) and keeps the dense kernel's RAW / WAR
+// spacing (a DMA issued in phase s is retired by the wait of phase s + 4) for
+// the quarters and the ring alike. A stage's rows are read from the ring one
+// phase before it (into registers; mma()'s lgkmcnt(0) covers the read): ids of
+// tile u are retired by phase 0 of tile u - 2 and first read in phase 1 of
+// that tile (Aq0(u) is staged in its phase 2).
+// x = w * T[row] never exists in HBM: each wave scales its A fragments by the
+// candidate's weight right before their first MFMA (fp32 multiply, bf16 round:
+// the unfused path's x, bit for bit). The FM second-order term rides along,
+// split over the 4 column tiles of a row block: tile tn < 4 owns partition
+// p = tn = (qm << 1) | kk - rows 64 qm .. of each 128-row group, dims 32 kk ..
+// 32 kk + 31 - and wave wc its fragment i = wc, accumulating sum_f v and
+// sum_f v^2 (v = e * w in fp32, from the fragment before rounding) per lane;
+//   fm_part[(1 + p) * Mp + m] = 0.5 * (sum_d (sum_f v_fd)^2 - sum_{f,d} v_fd^2)
+// over the partition's dims, so the head adds 4 partials (+ part0 of the
+// resolve kernel) instead of a separate gather re-reading the table.
+template <typename OutT>
+__global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restrict__ table, int Vm1,
+                                                          const int32_t* __restrict__ rows_t,
+                                                          const float* __restrict__ wts_t, int64_t Mp,
+                                                          const uint8_t* __restrict__ W, const float* __restrict__ bias,
+                                                          OutT* __restrict__ C, int64_t ldc, float* __restrict__ fm_part,
+                                                          int M, int N, int F, int epi) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int BUF = (BM + BN) * 128;  // 64 KiB
+  constexpr int RING = 8;
+  // one LDS object (A/B double buffer | ring rows | ring weights): separate
+  // __shared__ arrays made the compiler put vmcnt(0) in front of the A-tile
+  // reads (LDS-DMA alias tracking), draining the DMA pipeline twice a K tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF + 2 * RING * BM * 4];
+  int32_t(*s_rows)[BM] = reinterpret_cast<int32_t(*)[BM]>(smem + 2 * BUF);
+  float(*s_wts)[BM] = reinterpret_cast<float(*)[BM]>(smem + 2 * BUF + RING * BM * 4);
+
+  const int tiles_n = N / BN, tiles_m = int(Mp / BM);
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane >> 3, ls = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = F;
+  const int64_t ldw = int64_t(F) * 64;
+
+  auto a_row = [&](int qm, int g) { return (g < 8 ? 0 : 128) + 64 * qm + 8 * (g & 7); };
+  auto b_row = [&](int qn, int g) { return 64 * (g >> 2) + 32 * qn + 8 * (g & 3); };
+  // Every staged row r = (multiple of 8) + lr has swizzle (r >> 1) & 7 =
+  // 4 (wid & 1) | (lr >> 1) (a_row / b_row of group wid + 8j), so one per-lane
+  // chunk offset serves every A and B stage; the row parts are wave-uniform
+  // (kept in SGPRs: the kernel sits at the 256-VGPR limit of 2 waves / SIMD).
+  const int coff = (ls ^ ((4 * (wid & 1)) | (lr >> 1))) << 4;
+  const int b_lane = lr * int(ldw) * 2 + coff;  // N * K * 2 < 2^31 (launcher)
+  // ring: this wave's 4-byte DMA of tile u's 64 rows (waves 0-3) or weights (4-7)
+  auto stage_ring = [&](int u) {
+    const int64_t src = int64_t(min(u, nk - 1)) * Mp + m0 + 64 * (wid & 3) + lane;
+    const void* g = wid < 4 ? static_cast<const void*>(rows_t + src) : static_cast<const void*>(wts_t + src);
+    void* l = wid < 4 ? static_cast<void*>(&s_rows[u & (RING - 1)][64 * (wid & 3)])
+                      : static_cast<void*>(&s_wts[u & (RING - 1)][64 * (wid & 3)]);
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
+                                     (__attribute__((address_space(3))) void*)(l), 4, 0, 0);
+  };
+  int ida[2];  // table rows of the next A stage
+  auto read_rows = [&](int q, int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) ida[j] = s_rows[kt & (RING - 1)][a_row(q, wid + 8 * j) + lr];
+  };
+  auto stage_a = [&](int q, int kt) {
+    uint8_t* base = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = min(max(ida[j], 0), Vm1);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(table + int64_t(r) * 128 + coff),
+                                       (__attribute__((address_space(3))) void*)(base + a_row(q, wid + 8 * j) * 128),
+                                       16, 0, 0);
+    }
+  };
+  auto stage_b = [&](int q, int kt) {
+    uint8_t* base = smem + (kt & 1) * BUF;
+    const int64_t kb = int64_t(min(kt, nk - 1)) * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rb = b_row(q, wid + 8 * j);  // n0 + rb + lr < N: N % 256 == 0
+      const uint8_t* src = W + (int64_t(n0 + rb) * ldw * 2 + kb) + uint32_t(b_lane);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + rb * 128), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the ring for tiles 0-2 (landed before any A stage reads it), then
+  // the dense kernel's prologue (tile 0 whole + tile 1's Aq0, Bq0)
+  stage_ring(0);
+  stage_ring(1);
+  stage_ring(2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  read_rows(0, 0);
+  stage_a(0, 0);
+  stage_b(0, 0);
+  stage_b(1, 0);
+  read_rows(1, 0);
+  stage_a(1, 0);
+  read_rows(0, 1);
+  stage_a(0, 1);
+  stage_b(0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+  asm volatile("" ::: "memory");
+
+  // one A fragment set (the dense kernel's PRE form keeps two: 32 more VGPRs
+  // than this kernel has, at 2 waves / SIMD, once the weights and the FM
+  // accumulators are live)
+  bf16x8 fa[2][4], fb[2][2][2];
+  float wa[4];  // candidate weights of the A fragments
+  auto read_a = [&](const uint8_t* buf, int qm, int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 128 * wr + 64 * qm + 16 * i + fr;
+      wa[i] = s_wts[kt & (RING - 1)][row];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
+    }
+  };
+  auto read_b = [&](const uint8_t* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 64 * wc + 32 * qn + 16 * j + fr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        fb[qn][kk][j] = *reinterpret_cast<const bf16x8*>(buf + BM * 128 + swz(row, kk * 4 + fq));
+    }
+  };
+  // FM partition of this tile (tiles_n >= 4 and fm_part given; else none)
+  const bool fm_on = fm_part != nullptr && tn < 4;
+  const int fm_qm = tn >> 1, fm_kk = tn & 1;
+  float fs[8], fsq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fs[j] = 0.f;
+  auto unpack = [](const bf16x8& v, float (&e)[8]) {
+    const i32x4 u = __builtin_bit_cast(i32x4, v);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      e[2 * p] = __uint_as_float(uint32_t(u[p]) << 16);
+      e[2 * p + 1] = __uint_as_float(uint32_t(u[p]) & 0xffff0000u);
+    }
+  };
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (qm == qn) {  // first use of this A set in the K tile: FM terms, then the weight scaling
+      if (fm_on && qm == fm_qm) {
+        bf16x8 v = fa[0][0];
+        float w = wa[0];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (kk == fm_kk && i == wc) {
+              v = fa[kk][i];
+              w = wa[i];
+            }
+        float e[8];
+        unpack(v, e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = e[j] * w;
+          fs[j] += x;
+          fsq += x * x;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (qm == qn) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          float e[8];
+          unpack(fa[kk][i], e);
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(e[j] * wa[i]);
+          fa[kk][i] = o;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4& c = acc[4 * qm + i][2 * qn + j];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[kk][i], c, 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // every 4 consecutive phases issue 9 DMA instructions (see above)
+  auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); };
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* buf = smem + (t & 1) * BUF;
+    // p0: A[qm0] B[qn0]; stage Bq1(t+1) and the ring for tile t+3; rows for p1's stage
+    read_a(buf, 0, t);
+    read_b(buf, 0);
+    stage_b(1, t + 1);
+    stage_ring(t + 3);
+    read_rows(1, t + 1);
+    wait_dma();
+    barrier();
+    mma(0, 0);
+    barrier();
+    // p1: B[qn1]; stage Aq1(t+1); rows for p2's stage
+    read_b(buf, 1);
+    stage_a(1, t + 1);
+    read_rows(0, t + 2);
+    wait_dma();
+    barrier();
+    mma(0, 1);
+    barrier();
+    // p2: A[qm1]; stage Aq0(t+2)
+    read_a(buf, 1, t);
+    stage_a(0, t + 2);
+    wait_dma();
+    barrier();
+    mma(1, 1);
+    barrier();
+    // p3: stage Bq0(t+2)
+    stage_b(0, t + 2);
+    wait_dma();
+    barrier();
+    mma(1, 0);
+    barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
+
+  store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
+                            nullptr, 0, epi);
+  if (fm_on) {
+    float part = -fsq;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part += fs[j] * fs[j];
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    if (fq == 0) fm_part[int64_t(1 + tn) * Mp + m0 + 128 * wr + 64 * fm_qm + 16 * wc + fr] = 0.5f * part;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Deep-pipelined LDS-DMA variant: a STAGES-deep ring of K tiles with PREFETCH =
 // STAGES - 1 tiles in flight across barriers (cdna_hip_programming.md §5
 // "Pipelining across barriers"): every iteration issues the DMA for tile
@@ -1224,9 +1496,10 @@ using namespace kern;
 
 hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
                             const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
-                            int K, hipStream_t st) {
+                            int K, hipStream_t st, int extra_n, int64_t extra_ld) {
   if (M == 0) return hipSuccess;
-  if ((K * 2) % 128 != 0 || N > 256 || N <= 0) return hipErrorInvalidValue;
+  if ((K * 2) % 128 != 0 || N > 256 || N <= 0 || extra_n < 1 || (extra_n > 1 && extra_ld < M))
+    return hipErrorInvalidValue;
   const uint8_t* a = static_cast<const uint8_t*>(A);
   const uint8_t* w = static_cast<const uint8_t*>(W);
   // 32-row tiles give >= 256 workgroups at the bench batch (8192 rows)
@@ -1234,17 +1507,32 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
   if (N > 128) {
     if (small)
       hipLaunchKernelGGL((gemm_head_kernel<32, 4>), dim3((M + 31) / 32), dim3(256), 0, st, a, lda, w, ldw, bias, act,
-                         hw, hbias, extra, out_act, y, M, N, K);
+                         hw, hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
     else
       hipLaunchKernelGGL((gemm_head_kernel<64, 4>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act,
-                         hw, hbias, extra, out_act, y, M, N, K);
+                         hw, hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
   } else if (N > 64) {
     hipLaunchKernelGGL((gemm_head_kernel<64, 2>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act, hw,
-                       hbias, extra, out_act, y, M, N, K);
+                       hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
   } else {
     hipLaunchKernelGGL((gemm_head_kernel<64, 1>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias, act, hw,
-                       hbias, extra, out_act, y, M, N, K);
+                       hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
+                              int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
+                              int N, int epi, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (F < 1 || N <= 0 || N % 256 != 0 || Mp % 256 != 0 || Mp < M || V < 1 || V > (int64_t(1) << 31) ||
+      ldc < N || ldc % 4 != 0 || (fm_part && N < 1024) || int64_t(N) * F * 128 >= (int64_t(1) << 31) || !table ||
+      !rows_t || !wts_t || !W || !C)
+    return hipErrorInvalidValue;
+  const int grid = int(Mp / 256) * (N / 256);
+  hipLaunchKernelGGL((gemm_gather_kernel<bf16>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(table),
+                     int(V - 1), rows_t, wts_t, Mp, static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc,
+                     fm_part, M, N, F, epi);
   return hipGetLastError();
 }
 

@@ -136,8 +136,8 @@ __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restric
 // ---------------------------------------------------------------- K6
 // y[m] = act(x[m,:] . w + bias + extra[m]); one wave per row; act: 0 none, 2 sigmoid.
 __global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, int64_t ldx, const float* __restrict__ w,
-                                                   float bias, const float* __restrict__ extra, int M, int K, int act,
-                                                   float* __restrict__ out) {
+                                                   float bias, const float* __restrict__ extra, int extra_n,
+                                                   int64_t extra_ld, int M, int K, int act, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (m >= M) return;
@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, i
   }
   p = wave_sum(p);
   if (lane == 0) {
-    float v = p + bias + (extra ? extra[m] : 0.f);
+    float v = p + bias;
+    for (int e = 0; extra && e < extra_n; ++e) v += extra[e * extra_ld + m];
     out[m] = act == 2 ? sigmoidf(v) : v;
   }
 }
@@ -337,11 +338,11 @@ hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* em
 }
 
 hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,
-                       int act, float* out, hipStream_t st) {
+                       int act, float* out, hipStream_t st, int extra_n, int64_t extra_ld) {
   if (M == 0) return hipSuccess;
-  if (K % 8) return hipErrorInvalidValue;
+  if (K % 8 || extra_n < 1 || (extra_n > 1 && extra_ld < M)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_kernel, dim3((M + 3) / 4), dim3(256), 0, st, static_cast<const bf16*>(x), ldx, w, bias,
-                     extra, M, K, act, out);
+                     extra, extra_n, extra_ld, M, K, act, out);
   return hipGetLastError();
 }
 

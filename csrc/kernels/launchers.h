@@ -67,6 +67,14 @@ hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 // rows in flight per wave (1 or 2).
 void set_embed_wave_cap(int waves, int rows_in_flight = 1);
 
+// Front half of K1 for the gather-GEMM (gemm_gather): shared-table rows /
+// weights of B candidates, field-major rows_t / wts_t [F][Mp] (Mp = B rounded
+// up to 256; padding rows: row 0, weight 0), and part0[b] = bias + the
+// first-order FM term. ids / wts / arena / lin / modulo / V / B / F / bias of
+// `a` are read; the outputs above replace out_x / out_fm.
+hipError_t launch_embed_resolve(const EmbedArgs& a, int32_t* rows_t, float* wts_t, float* part0, int64_t Mp,
+                                hipStream_t st);
+
 // K0 ingest: request arena (header + descriptors + raw request bytes) -> packed
 // rows [B, W] int64 (serving/arena.py, csrc/runtime/arena.h share the layout).
 constexpr int kArenaPayloadOff = 64 + 32 * 1024;  // descriptors: up to 1024 requests
@@ -104,6 +112,15 @@ struct MxIO {
   int nq = 0;
 };
 
+// K1 fused into K4 (gemm.hip gemm_gather_kernel): C bf16 [M, N] =
+// epi(sum_f bf16(w * T[row]) . W[:, 64f:64f+64]^T + bias) for a bf16 table
+// with 64-wide rows (128 B), rows_t / wts_t from launch_embed_resolve, W bf16
+// [N, 64F]; N % 256 == 0. fm_part (N >= 1024): rows 1..4 of the [5][Mp] FM
+// partials receive the second-order FM term split over 4 dim / row partitions.
+hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
+                              int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
+                              int N, int epi, hipStream_t st);
+
 // K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,
@@ -111,9 +128,11 @@ hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, c
                        int variant = 0, const MxIO* mx = nullptr);
 
 // K4+K6 fused: y[m] = out_act(act(A W^T + b)[m,:] . hw + hbias + extra[m]); N <= 256, bf16.
+// extra_n > 1: extra holds extra_n partial logits, extra[e * extra_ld + m]
+// (the gather-GEMM path's first-order + FM partitions), summed in order.
 hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
                             const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
-                            int K, hipStream_t st);
+                            int K, hipStream_t st, int extra_n = 1, int64_t extra_ld = 0);
 
 // K3: DCN-v1 cross network, all L layers fused.
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,
@@ -127,9 +146,9 @@ hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* em
                                   int64_t ldo, int out_cols, hipStream_t st, const int64_t* emb_off = nullptr,
                                   const int64_t* emb_stride = nullptr, int64_t emb_rows = 0);
 
-// K6: y = act(x . w + bias + extra), act 0 none / 2 sigmoid.
+// K6: y = act(x . w + bias + extra), act 0 none / 2 sigmoid (extra_n / extra_ld: launch_gemm_head).
 hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,
-                       int act, float* out, hipStream_t st);
+                       int act, float* out, hipStream_t st, int extra_n = 1, int64_t extra_ld = 0);
 
 // fp8 (OCP e4m3) per-row quantisation.
 // Kq >= K: output row width; columns [K, Kq) are zeroed (K padding for the

@@ -40,6 +40,9 @@ class CTRModel(nn.Module):
     """Base: holds config, exposes ``forward(ids, wts) -> CTR [B] fp32``."""
 
     family = "base"
+    # DeepFM / WDL: run the first MLP layer as the gather-GEMM where it applies
+    # (_gather_gemm); tests switch it off per instance to compare the two paths
+    use_gather_gemm = True
 
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__()
@@ -85,6 +88,17 @@ class CTRModel(nn.Module):
     # can read them straight from a request arena (ops.ArenaRows)
     supports_arena = False
 
+    def _gather_gemm(self, ids, wts, fm2: bool) -> bool:
+        """The first MLP layer runs as the gather-GEMM (ops.embed_gemm): GPU,
+        bf16 towers of >= 2 layers, a shape the kernel covers."""
+        layers = self.mlp.layers
+        first = layers[0]
+        on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
+        return (on_gpu and self.use_gather_gemm and len(layers) >= 2 and not first.fp8
+                and (wts is None or wts.dtype == torch.float32)
+                and first.act in ("relu", "none") and first.k == first.in_dim
+                and ops.embed_gemm_ok(self.emb, first.weight, int(ids.shape[0]), fm2))
+
     @torch.no_grad()
     def forward_arena(self, arena: torch.Tensor, B: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """CTR [B] for the first B candidate rows of a (device) request arena."""
@@ -113,6 +127,11 @@ class WideDeep(CTRModel):
                          want_x=True, want_fm=True, fm2=False)
 
     def _forward(self, ids, wts, out=None):
+        if self._gather_gemm(ids, wts, fm2=False):
+            first = self.mlp.layers[0]
+            h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
+                                     first.bias, first.act, fm2=False)
+            return self.mlp.forward_head(h, self.head_w, self.head_b, extra=wide, out=out, start=1)
         x, wide = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide, out=out)
 
@@ -137,6 +156,12 @@ class DeepFM(CTRModel):
                          want_x=True, want_fm=True, fm2=True)
 
     def _forward(self, ids, wts, out=None):
+        if self._gather_gemm(ids, wts, fm2=True):
+            # K1 + K2 inside the first layer's GEMM: x never reaches HBM
+            first = self.mlp.layers[0]
+            h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
+                                   first.bias, first.act, fm2=True)
+            return self.mlp.forward_head(h, self.head_w, self.head_b, extra=fm, out=out, start=1)
         x, fm = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm, out=out)
 

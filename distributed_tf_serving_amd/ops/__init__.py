@@ -371,6 +371,44 @@ def embed_cross(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: i
     return x, logit
 
 
+# ------------------------------------------------------------------ K1 fused into K4
+# Below this many candidate rows the gather-GEMM's 256x256 tiles leave most
+# CUs idle and the separate gather + smaller-tile GEMM wins (tools/studies/
+# microbench.py --gather-gemm, profiles/r03_gather_gemm.md).
+GATHER_GEMM_MIN_ROWS = 8192
+
+
+def embed_gemm_ok(table: torch.Tensor, W: torch.Tensor, B: int, fm2: bool) -> bool:
+    """Shapes the gather-GEMM covers: a bf16 [V, 64] table, a bf16 first layer
+    with N % 256 == 0 (N >= 1024 with the FM term), enough rows to fill the GPU."""
+    N, K = W.shape
+    return (table.is_cuda and table.dtype == torch.bfloat16 and table.dim() == 2 and table.shape[1] == 64
+            and W.dtype == torch.bfloat16 and N % 256 == 0 and (not fm2 or N >= 1024)
+            and table.shape[0] <= 2 ** 31 and N * K * 2 < 2 ** 31 and B >= GATHER_GEMM_MIN_ROWS)
+
+
+def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
+               bias: float, W: torch.Tensor, b: torch.Tensor, act: str = "relu",
+               fm2: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """K1 fused into the first MLP layer (K4): returns
+      h     = act(x W^T + b) bf16 [B, N], x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)),
+      parts = fp32 [1 + 4 fm2, >= B]: row 0 = bias + sum_f lin[row] w, rows 1.. the
+              second-order FM term in partitions (heads sum the rows, _extra_logit).
+    On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
+    table rows straight into the GEMM's LDS tiles); on the CPU the unfused math."""
+    m = int(modulo) if modulo > 0 else table.shape[0]
+    on_gpu = ids.arena.is_cuda if isinstance(ids, ArenaRows) else ids.is_cuda
+    if on_gpu:
+        a = _ACTS[act]
+        if isinstance(ids, ArenaRows):
+            return tuple(hip().embed_gemm(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias),
+                                          W, b, a, fm2))
+        return tuple(hip().embed_gemm(table, lin, None, _rows(ids), None if wts is None else _rows(wts),
+                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2))
+    x, fm = embed(table, ids, wts, lin=lin, modulo=m, bias=bias, want_x=True, want_fm=True, fm2=fm2)
+    return linear(x, W, b, act), fm.view(1, -1)
+
+
 # ------------------------------------------------------------------ K5
 def interaction_cols(num_sparse: int, dim: int = 64) -> int:
     """Width of the interaction output (and the top MLP's K), zero padded to a
@@ -428,14 +466,22 @@ def shard_route(ids: torch.Tensor, W: int, tm: int, col: torch.Tensor, mod: torc
 
 
 # ------------------------------------------------------------------ K6
+def _extra_logit(extra: torch.Tensor, M: int) -> torch.Tensor:
+    """A head's extra logit: fp32 [M], or [P, >= M] partial logits summed in
+    row order (embed_gemm's first-order + FM partitions)."""
+    if extra.dim() == 2:
+        return extra[:, :M].float().sum(0)
+    return extra.float()
+
+
 def head(x: torch.Tensor, w: torch.Tensor, bias: float = 0.0, extra: Optional[torch.Tensor] = None,
          sigmoid: bool = True) -> torch.Tensor:
-    """CTR head: act(x . w + bias + extra) -> fp32 [M]."""
+    """CTR head: act(x . w + bias + extra) -> fp32 [M] (``extra``: see _extra_logit)."""
     if x.is_cuda:
         return hip().head(x.contiguous(), w, float(bias), extra, sigmoid)
     y = x.float() @ w.float() + float(bias)
     if extra is not None:
-        y = y + extra.float()
+        y = y + _extra_logit(extra, y.shape[0])
     return torch.sigmoid(y) if sigmoid else y
 
 
@@ -459,7 +505,7 @@ def linear_head(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: str, hw:
         h = torch.relu(h)
     y = h @ hw.float() + float(hbias)  # the fused kernel keeps h in fp32 (no bf16 round trip)
     if extra is not None:
-        y = y + extra.float()
+        y = y + _extra_logit(extra, y.shape[0])
     y = torch.sigmoid(y) if sigmoid else y
     if out is not None:
         out.copy_(y)

@@ -29,7 +29,7 @@ if [ "${FRONTENDS:-}" != "" ]; then
   mkdir -p gpurun_out/frontends
   for k in $FRONTENDS; do
     port=$((9950 + k))
-    python -u -m distributed_tf_serving_amd.serving.server --preset reference_dcn --port $port --frontends $k \
+    timeout -k 10 400 python -u -m distributed_tf_serving_amd.serving.server --preset reference_dcn --port $port --frontends $k \
       > gpurun_out/frontends/server_$k.log 2>&1 &
     spid=$!
     python - "$port" <<'PYEOF' || { echo "server $k did not start"; kill $spid; tail -20 gpurun_out/frontends/server_$k.log; exit 1; }

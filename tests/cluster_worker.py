@@ -150,4 +150,14 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        # torchrun's failure summary hides a rank's own traceback: leave it where the test looks
+        import traceback
+
+        out = next((sys.argv[i + 1] for i, x in enumerate(sys.argv[:-1]) if x == "--out"), None)
+        if out:
+            with open(os.path.join(out, f"rank{os.environ.get('RANK', '?')}.err"), "w") as f:
+                f.write(traceback.format_exc())
+        raise

@@ -611,3 +611,92 @@ def test_embed_cross_matches_layerwise_reference(cuda, D, F, L):
     xr, lr = ops.embed_cross(table, ids, wts, V, w, b, hw)
     _close(x, xr, 0, 0, "x")
     _close(logit, lr, 1e-4, 1e-4, "cross logit")
+
+
+def _gather_gemm_case(B, F=43, V=50_000, N=1024, seed=5, ids32=False):
+    g = torch.Generator().manual_seed(seed)
+    table = ((torch.rand(V, 64, generator=g) - 0.5) * 0.2).to(torch.bfloat16)
+    lin = (torch.rand(V, generator=g) - 0.5) * 0.1
+    W = ((torch.rand(N, F * 64, generator=g) - 0.5) * 0.05).to(torch.bfloat16)
+    b = (torch.rand(N, generator=g) - 0.5) * 0.1
+    ids = torch.randint(-(1 << 40), 1 << 40, (B, F), generator=g)
+    if ids32:
+        ids = ids.remainder(1 << 31).to(torch.int32)
+    wts = torch.rand(B, F, generator=g)
+    return table, lin, W, b, ids, wts
+
+
+def _gather_gemm_ref(table, lin, W, b, ids, wts, V, bias, fm2):
+    rows = torch.remainder(ids.long(), V)
+    e = table[rows].float() * wts[..., None]  # [B, F, 64]
+    h = torch.relu(e.reshape(ids.shape[0], -1) @ W.float().t() + b)
+    fm = bias + (lin[rows] * wts).sum(1)
+    if fm2:
+        fm = fm + 0.5 * (e.sum(1).pow(2) - e.pow(2).sum(1)).sum(1)
+    return h, fm
+
+
+@pytest.mark.parametrize("B,ids32", [(1, False), (300, True), (4099, False), (16384, False)])
+@pytest.mark.parametrize("fm2", [True, False])
+def test_embed_gemm_matches_fp32_reference(cuda, B, ids32, fm2):
+    """K1 fused into K4 (gather-GEMM + resolve kernel): the first layer's
+    output and the FM partial logits vs the fp32 torch math, and vs the unfused
+    GPU path (gather kernel writing x, then the GEMM), which rounds x the same
+    way and runs the same MFMA sequence per output."""
+    V, bias = 50_000, 0.25
+    table, lin, W, b, ids, wts = _gather_gemm_case(B, V=V, ids32=ids32)
+    d = [t.to(cuda) for t in (table, lin, W, b, ids, wts)]
+    h, parts = ops.embed_gemm(d[0], d[4], d[5], d[1], V, bias, d[2], d[3], "relu", fm2=fm2)
+    assert h.shape == (B, 1024) and parts.shape[0] == (5 if fm2 else 1) and parts.shape[1] >= B
+    h_ref, fm_ref = _gather_gemm_ref(table, lin, W, b, ids, wts, V, bias, fm2)
+    _close(h, h_ref, 2e-2, 2e-3, "gather-GEMM h vs fp32")
+    _close(parts[:, :B].sum(0), fm_ref, 1e-4, 1e-4, "FM partials vs fp32")
+    xg, fmg = ops.embed(d[0], d[4], d[5], lin=d[1], modulo=V, bias=bias, want_x=True, want_fm=True, fm2=fm2)
+    _close(h, ops.linear(xg, d[2], d[3], "relu"), 1e-2, 1e-4, "gather-GEMM vs gather + GEMM")
+    _close(parts[:, :B].sum(0), fmg, 1e-5, 1e-5, "FM partials vs the gather kernel's FM")
+
+
+def test_embed_gemm_arena_rows(cuda):
+    """The gather-GEMM reading raw and packed-varint request bytes from a
+    device arena scores like the same rows unpacked (padding rows: zeros)."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    V = 30_000
+    table, lin, W, b, _, _ = _gather_gemm_case(1, V=V)
+    d = [t.to(cuda) for t in (table, lin, W, b)]
+    A, L = ArenaLayout(43, 4096), PackedLayout(43)
+    ar = A.alloc()
+    s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=12)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((3, True), (1500, False), (700, True), (90, False))]
+    ab = A.build(ar, A.place(ar, reqs))
+    assert not any(ab.errors)
+    dev = ar.to(cuda)
+    A.decode_varints(dev)
+    B = 2600  # > total_rows (2293): padding rows
+    packed = A.unpack_cpu(ar, L.alloc(B))
+    ids, wts = L.ids(packed), L.wts(packed)
+    h, parts = ops.embed_gemm(d[0], ops.ArenaRows(dev, B, 43), None, d[1], V, 0.0, d[2], d[3], "relu")
+    h_ref, fm_ref = _gather_gemm_ref(table, lin, W, b, ids, wts, V, 0.0, True)
+    _close(h, h_ref, 2e-2, 2e-3, "arena gather-GEMM h vs fp32")
+    _close(parts[:, :B].sum(0), fm_ref, 1e-4, 1e-4, "arena FM partials vs fp32")
+    hp, pp = ops.embed_gemm(d[0], ids.to(cuda), wts.to(cuda), d[1], V, 0.0, d[2], d[3], "relu")
+    _close(h, hp, 0, 0, "arena vs unpacked rows")
+    _close(parts[:, :B], pp[:, :B], 0, 0, "arena vs unpacked FM partials")
+
+
+@pytest.mark.parametrize("family", ["deepfm", "wdl"])
+def test_gather_gemm_model_path_matches_unfused(cuda, family):
+    """DeepFM / WDL at a served bucket size take the gather-GEMM path; scores
+    match the unfused path (gather kernel + GEMM) of the same weights."""
+    cfg = ModelConfig(family=family, vocab_size=100_000)
+    m = build_model(cfg, cuda)
+    B = max(8192, ops.GATHER_GEMM_MIN_ROWS)
+    ids = torch.randint(0, 1 << 40, (B, 43), device=cuda)
+    wts = torch.rand(B, 43, device=cuda)
+    assert m._gather_gemm(ids, wts, fm2=family == "deepfm")
+    got = m(ids, wts)
+    m.use_gather_gemm = False
+    want = m(ids, wts)
+    _close(got, want, 0, 5e-5, f"{family} gather-GEMM vs unfused")

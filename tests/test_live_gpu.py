@@ -114,3 +114,39 @@ def test_ranked_outputs_use_gpu_sort(server):
     perm = T.to_ndarray(resp.outputs["sorted_index"])
     assert got.shape == (1500,) and sorted(perm.tolist()) == list(range(1500))
     assert np.all(np.diff(srt) >= 0) and np.array_equal(srt, got[perm])
+
+
+def test_gather_gemm_served_steps_match_eager_forward():
+    """Served steps at a bucket that takes the gather-GEMM path (K1 inside the
+    first layer's GEMM, reading host-narrowed and raw arena rows): every
+    request's scores match the model's eager forward."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distributed_tf_serving_amd import ops
+
+    cfg = load_preset("deepfm_1gpu")
+    cfg.model.vocab_size = 200_000
+    cfg.serving.max_batch_rows = max(8192, ops.GATHER_GEMM_MIN_ROWS)
+    cfg.serving.allowed_batch_sizes = (cfg.serving.max_batch_rows,)
+    srv = ModelServer(cfg, device="cuda:0")
+    try:
+        model = srv.registry.resolve("DCN").model
+        assert model._gather_gemm(torch.zeros(cfg.serving.max_batch_rows, F, dtype=torch.int64, device="cuda"),
+                                  None, fm2=True)
+        synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=33)
+        reqs = []
+        for i in range(24):
+            ids, wts = synth.arrays([512, 3, 700, 129][i % 4])
+            data = native().encode_predict_request("DCN", "serving_default", None,
+                                                   [("feat_ids", torch.from_numpy(ids)),
+                                                    ("feat_wts", torch.from_numpy(wts))], i % 3 != 2)
+            reqs.append((data, ids, wts))
+        with cf.ThreadPoolExecutor(16) as pool:
+            outs = list(pool.map(lambda r: srv.service.predict_bytes(r[0], 30.0), reqs))
+        for (data, ids, wts), resp in zip(reqs, outs):
+            want = model(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+            np.testing.assert_allclose(_scores(resp), want, atol=5e-5)
+        st = srv.registry.resolve("DCN").scheduler.stats()
+        assert st["narrowed"] > 0 and not st["broken"]
+    finally:
+        srv.stop()

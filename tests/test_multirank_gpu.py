@@ -89,7 +89,8 @@ def test_native_cluster_server_ranks_sharing_one_gpu(tmp_path, n, mode):
            "--mode", mode, "--out", str(tmp_path), "--grpc-port", str(_port())]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    errs = {f.name: f.read_text()[-3000:] for f in sorted(tmp_path.glob("rank*.err"))}
+    assert p.returncode == 0, (errs, p.stdout[-2000:], p.stderr[-2000:])
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
     fronts = [r for r in res if r["serves"]]
     assert len(fronts) == (n if mode == "alltoall" else 1)

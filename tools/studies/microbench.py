@@ -131,6 +131,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
+    ap.add_argument("--gather-gemm", action="store_true", help="K1 fused into K4 vs gather + GEMM")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
     ap.add_argument("--serving", action="store_true",
                     help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
@@ -146,6 +147,10 @@ def main():
         shape, vs = a.variants.split(":")
         M, N, K = (int(x) for x in shape.split(","))
         print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
+        return
+    if a.gather_gemm:
+        for r in gather_gemm_study():
+            print(json.dumps(r), flush=True)
         return
     if a.embed_study:
         for r in embed_study():
@@ -170,6 +175,44 @@ def main():
         for B in ([512] if a.quick else [512, 4096]):
             print(json.dumps(bench_model(fam, B)), flush=True)
 
+
+
+def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024, dev="cuda"):
+    """K1 fused into K4 vs the separate gather + GEMM at the DeepFM serving
+    shape (Zipf ids, 1M x 64 table): resolve + gather-GEMM vs embed(x, FM) +
+    8-phase GEMM, interleaved rounds; also each half alone."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+
+    table = (torch.randn(V, 64, device=dev) * 0.05).to(torch.bfloat16)
+    lin = torch.randn(V, device=dev) * 0.01
+    W = (torch.randn(N, F * 64, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev) * 0.01
+    out = []
+    for B in rows:
+        ids_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
+        ids, wts = torch.from_numpy(ids_np).to(dev), torch.from_numpy(wts_np).to(dev)
+
+        def unfused():
+            x, fm = ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True)
+            return ops.linear(x, W, b, "relu")
+
+        def fused():
+            return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=True)
+
+        x, _ = ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True)
+        t = {k: [] for k in ("unfused", "fused", "embed", "gemm")}
+        for _ in range(5):  # interleaved
+            t["unfused"].append(_time(unfused, 20, 1))
+            t["fused"].append(_time(fused, 20, 1))
+            t["embed"].append(_time(lambda: ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True,
+                                                      want_fm=True, fm2=True), 20, 1))
+            t["gemm"].append(_time(lambda: ops.linear(x, W, b, "relu"), 20, 1))
+        r = {"op": "gather_gemm", "B": B, "N": N, "K": F * 64}
+        for k, v in t.items():
+            r[f"{k}_us"] = round(statistics.median(v), 2)
+        r["fused_tflops"] = round(2.0 * B * N * F * 64 / r["fused_us"] / 1e6, 1)
+        out.append(r)
+    return out
 
 
 def embed_study(B=16384, F=43, D=64, V=1_000_000, dev="cuda"):
