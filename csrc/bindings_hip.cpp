@@ -257,8 +257,8 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
 // gather-GEMM (csrc/kernels/gemm.hip gemm_gather_kernel). Rows come from a
 // device request arena (arena, B, F) or from ids [B, F] (+ wts). Returns
 //   h     bf16 [B, N] = act(x . W^T + b), x = w * T[row] never materialised
-//   parts fp32 [1 + 4 fm2, Mp]: row 0 = bias + first-order FM term, rows 1..4
-//         the second-order FM term over 4 partitions (the head sums them).
+//   parts fp32 [1 + fm2, Mp]: row 0 = bias + first-order FM term, row 1 the
+//         second-order FM term (the head sums the rows).
 std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::Tensor> lin,
                                       c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
                                       c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
@@ -314,7 +314,7 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
   c10::DeviceGuard g(table.device());
   const int64_t Mp = (B + 255) / 256 * 256;
   auto h = torch::empty({B, N}, table.options());
-  auto parts = torch::empty({fm2 ? 5 : 1, Mp}, table.options().dtype(torch::kFloat32));
+  auto parts = torch::empty({fm2 ? 2 : 1, Mp}, table.options().dtype(torch::kFloat32));
   auto rows_t = torch::empty({F, Mp}, table.options().dtype(torch::kInt32));
   auto wts_t = torch::empty({F, Mp}, table.options().dtype(torch::kFloat32));
   if (B == 0) return {h, parts};
@@ -558,7 +558,7 @@ torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tenso
 
 // ---------------------------------------------------------------- K6
 // A head's extra logit: fp32 [M], or fp32 [P, >= M] partials summed in order
-// (row stride >= M, unit inner stride: the gather-GEMM path's [1 + 4, Mp]).
+// (row stride >= M, unit inner stride: the gather-GEMM path's [2, Mp]).
 static void check_extra(const torch::Tensor& e, int64_t M) {
   TORCH_CHECK(e.scalar_type() == torch::kFloat32, "extra must be fp32");
   if (e.dim() == 2) {

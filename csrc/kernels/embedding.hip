@@ -436,16 +436,18 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
 // 4-byte LDS-DMA per lane; plus the first-order FM term
 //   part0[b] = bias + sum_f lin[row(b, f)] * w(b, f).
 // Rows b in [B, Mp): row 0, weight 0 (they contribute nothing).
-// Block = 256 threads over 64 candidates. Item i = t + 256k is (row i / F,
-// field i % F): consecutive lanes read consecutive fields of one row, and a
-// thread issues all its items' loads before using any (a row is three
-// dependent round trips: descriptor, id / weight, lin). An LDS transpose
-// then writes each field's 64 rows as one 256-byte store.
+// Block = 256 threads over 16 candidates (1024 blocks at 16384 rows: the
+// kernel is three dependent round trips - descriptor, id / weight, lin - so
+// it wants many waves in flight; 64-row blocks ran 21 us in the served step).
+// Item i = t + 256k is (row i / F, field i % F): consecutive lanes read
+// consecutive fields of one row, and a thread issues all its items' loads
+// before using any. An LDS transpose then writes each field's 16 rows as one
+// 64-byte store.
 template <typename IdT, bool ARENA>
 __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_t magic, int32_t* __restrict__ rows_t,
                                                            float* __restrict__ wts_t, float* __restrict__ part0,
                                                            int64_t Mp) {
-  constexpr int RB = 64, KMAX = (kWave * RB) / 256;  // items per thread for F <= 64
+  constexpr int RB = 16, KMAX = (kWave * RB) / 256;  // items per thread for F <= 64
   __shared__ int32_t s_row[kWave * RB];
   __shared__ float s_w[kWave * RB];
   __shared__ float s_lin[kWave * RB];
@@ -597,7 +599,7 @@ hipError_t launch_embed_resolve(const EmbedArgs& a, int32_t* rows_t, float* wts_
     return hipErrorInvalidValue;
   if (Mp == 0) return hipSuccess;
   const uint64_t magic = a.modulo < (int64_t(1) << 32) ? ~uint64_t(0) / uint64_t(a.modulo) : 0;
-  dim3 grid(unsigned(Mp / 64)), block(256);
+  dim3 grid(unsigned(Mp / 16)), block(256);
   if (a.arena)
     hipLaunchKernelGGL((embed_resolve_kernel<int64_t, true>), grid, block, 0, st, a, magic, rows_t, wts_t, part0, Mp);
   else if (a.ids64)

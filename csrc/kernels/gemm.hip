@@ -22,6 +22,7 @@
 // Epilogues: bias, ReLU, sigmoid, DCN-v2 cross (x0 * (acc + b) + xl), written
 // as bf16 or fp32.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "launchers.h"
@@ -984,24 +985,35 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
 // table + row * 128 per lane. The rows and weights of a K tile come from
 // embed_resolve_kernel's field-major rows_t / wts_t [F][Mp] through an 8-slot
 // LDS ring: ONE 4-byte LDS-DMA per lane per K tile (waves 0-3 rows, 4-7
-// weights), issued in phase 0 three tiles ahead. That makes phase 0 issue 3
-// DMA instructions and the others 2, so every 4 consecutive phases issue 9:
-// the counted wait becomes vmcnt(9) and keeps the dense kernel's RAW / WAR
-// spacing (a DMA issued in phase s is retired by the wait of phase s + 4) for
-// the quarters and the ring alike. A stage's rows are read from the ring one
-// phase before it (into registers; mma()'s lgkmcnt(0) covers the read): ids of
-// tile u are retired by phase 0 of tile u - 2 and first read in phase 1 of
-// that tile (Aq0(u) is staged in its phase 2).
-// x = w * T[row] never exists in HBM: each wave scales its A fragments by the
-// candidate's weight right before their first MFMA (fp32 multiply, bf16 round:
-// the unfused path's x, bit for bit). The FM second-order term rides along,
-// split over the 4 column tiles of a row block: tile tn < 4 owns partition
-// p = tn = (qm << 1) | kk - rows 64 qm .. of each 128-row group, dims 32 kk ..
-// 32 kk + 31 - and wave wc its fragment i = wc, accumulating sum_f v and
-// sum_f v^2 (v = e * w in fp32, from the fragment before rounding) per lane;
-//   fm_part[(1 + p) * Mp + m] = 0.5 * (sum_d (sum_f v_fd)^2 - sum_{f,d} v_fd^2)
-// over the partition's dims, so the head adds 4 partials (+ part0 of the
-// resolve kernel) instead of a separate gather re-reading the table.
+// weights), issued in phase 0 three tiles ahead. A stage's rows are read from
+// the ring a phase before it (mma()'s lgkmcnt(0) covers the read).
+//
+// The weights are applied ONCE per element, in LDS: x = bf16(w * e) (the
+// unfused gather's rounding, bit for bit) by a scale pass over each landed A
+// quarter - every thread rescales two 16-byte chunks in place - in a phase
+// that has no other use for that quarter. Scaling the MFMA fragments instead
+// costs each of the 4 column waves the same work again (measured: +48 us of
+// VALU on the 146 us kernel at 16384 rows); the pass adds 2 x 16 KB of LDS
+// traffic per K tile and ~40 VALU per wave, issued between the MFMAs. For the
+// spare phase Aq1 is staged one phase earlier than in the dense kernel:
+//   p0: stage Bq1(t+1) Aq1(t+1) ring(t+3)   p1: scale Aq1(t)
+//   p2: stage Aq0(t+2)                       p3: scale Aq0(t+1), stage Bq0(t+2)
+// 5 + 0 + 2 + 2 = 9 DMA instructions per 4 phases, so the counted wait
+// vmcnt(9) retires every DMA issued 4 phases earlier (quarters, ring alike).
+// Each quarter is loaded for scaling one phase after the wait that retires it
+// (the read segment, so the other group has passed that wait too) and read by
+// the MFMA phase after that: a group scales only the rows it reads, so its
+// own lgkmcnt(0) + barrier at the end of the scaling phase order the writes. WAR:
+// Aq1(t+1) overwrites buffer (t+1)&1 two phases after Aq1(t-1)'s last read
+// (p2 of tile t-1); the other quarters as in the dense kernel.
+//
+// FM (DeepFM) rides on the scale pass, which holds e and w in fp32: column
+// tile tn < 4 accumulates, for quarter tn >> 1 and row half tn & 1 of each
+// group, each thread's 8 dims of one candidate (sum_f v, sum_f v^2, v = e * w);
+// 8 lanes finish the row, so every candidate's second-order term
+//   fm_part[Mp + m] = 0.5 * (sum_d (sum_f v_fd)^2 - sum_{f,d} v_fd^2)
+// comes from exactly one tile, and the head adds it to part0 (bias + first
+// order, from the resolve kernel): no second pass over the table.
 template <typename OutT>
 __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restrict__ table, int Vm1,
                                                           const int32_t* __restrict__ rows_t,
@@ -1036,7 +1048,7 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   // Every staged row r = (multiple of 8) + lr has swizzle (r >> 1) & 7 =
   // 4 (wid & 1) | (lr >> 1) (a_row / b_row of group wid + 8j), so one per-lane
   // chunk offset serves every A and B stage; the row parts are wave-uniform
-  // (kept in SGPRs: the kernel sits at the 256-VGPR limit of 2 waves / SIMD).
+  // (kept in SGPRs: the kernel sits near the 256-VGPR limit of 2 waves / SIMD).
   const int coff = (ls ^ ((4 * (wid & 1)) | (lr >> 1))) << 4;
   const int b_lane = lr * int(ldw) * 2 + coff;  // N * K * 2 < 2^31 (launcher)
   // ring: this wave's 4-byte DMA of tile u's 64 rows (waves 0-3) or weights (4-7)
@@ -1075,14 +1087,69 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     }
   };
 
+  // scale pass, group-local: wave group wr only ever reads A rows 128 wr ..
+  // 128 wr + 127, so it scales exactly those rows of a quarter (64 q + rr and
+  // 64 q + rr + 32 within the group, chunk ch; a wave covers 8 whole rows,
+  // 1 KiB, conflict-free) and only its own barriers order the writes before its
+  // reads. The chunks are loaded in a phase's read segment (retired by then) and
+  // rescaled + written back in its MFMA segment, between the MFMAs.
+  const int sp_rr = (threadIdx.x & 255) >> 3, sp_ch = threadIdx.x & 7;
+  const bool fm_on = fm_part != nullptr && tn < 4;
+  const int fm_q = tn >> 1, fm_h = tn & 1;
+  float fs[8], fsq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fs[j] = 0.f;
+  i32x4 su[2];
+  float sw[2];
+  auto scale_row = [&](int q, int h) { return 128 * wr + 64 * q + sp_rr + 32 * h; };
+  auto scale_load = [&](const uint8_t* buf, int q, int u) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = scale_row(q, h);
+      su[h] = *reinterpret_cast<const i32x4*>(buf + r * 128 + sp_ch * 16);
+      sw[h] = s_wts[u & (RING - 1)][r];
+    }
+  };
+  auto scale_store = [&](uint8_t* buf, int q, int u) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      i32x4 o;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        int r;
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2"
+            : "=v"(r)
+            : "v"(__uint_as_float(uint32_t(su[h][p]) << 16) * sw[h]),
+              "v"(__uint_as_float(uint32_t(su[h][p]) & 0xffff0000u) * sw[h]));
+        o[p] = r;
+      }
+      *reinterpret_cast<i32x4*>(buf + scale_row(q, h) * 128 + sp_ch * 16) = o;
+    }
+    // FM: tile tn (< 4) takes quarter tn >> 1, row half tn & 1 of every group,
+    // so each candidate's term comes from one tile (one wave-uniform branch per
+    // pass; u == nk is the loop's trailing re-staged, dead tile)
+    if (fm_on && q == fm_q && u < nk) {
+      const i32x4 uf = fm_h ? su[1] : su[0];
+      const float wf = fm_h ? sw[1] : sw[0];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float x = __uint_as_float(uint32_t(uf[p]) << 16) * wf;
+        const float y = __uint_as_float(uint32_t(uf[p]) & 0xffff0000u) * wf;
+        fs[2 * p] += x;
+        fs[2 * p + 1] += y;
+        fsq += x * x + y * y;
+      }
+    }
+  };
+
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: the ring for tiles 0-2 (landed before any A stage reads it), then
-  // the dense kernel's prologue (tile 0 whole + tile 1's Aq0, Bq0)
+  // prologue: the ring for tiles 0-2, tile 0 whole + tile 1's Aq0 / Bq0, tile
+  // 0's Aq0 scaled by everyone, then the stagger
   stage_ring(0);
   stage_ring(1);
   stage_ring(2);
@@ -1098,20 +1165,20 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   stage_a(0, 1);
   stage_b(0, 1);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  __syncthreads();
+  scale_load(smem, 0, 0);  // tile 0's Aq0 (Aq1(0) is scaled by the loop's first phase 1)
+  scale_store(smem, 0, 0);
+  read_rows(1, 1);  // p0(0) stages Aq1(1)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
   asm volatile("" ::: "memory");
 
-  // one A fragment set (the dense kernel's PRE form keeps two: 32 more VGPRs
-  // than this kernel has, at 2 waves / SIMD, once the weights and the FM
-  // accumulators are live)
   bf16x8 fa[2][4], fb[2][2][2];
-  float wa[4];  // candidate weights of the A fragments
-  auto read_a = [&](const uint8_t* buf, int qm, int kt) {
+  auto read_a = [&](const uint8_t* buf, int qm) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 128 * wr + 64 * qm + 16 * i + fr;
-      wa[i] = s_wts[kt & (RING - 1)][row];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
     }
@@ -1125,59 +1192,14 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
         fb[qn][kk][j] = *reinterpret_cast<const bf16x8*>(buf + BM * 128 + swz(row, kk * 4 + fq));
     }
   };
-  // FM partition of this tile (tiles_n >= 4 and fm_part given; else none)
-  const bool fm_on = fm_part != nullptr && tn < 4;
-  const int fm_qm = tn >> 1, fm_kk = tn & 1;
-  float fs[8], fsq = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) fs[j] = 0.f;
-  auto unpack = [](const bf16x8& v, float (&e)[8]) {
-    const i32x4 u = __builtin_bit_cast(i32x4, v);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      e[2 * p] = __uint_as_float(uint32_t(u[p]) << 16);
-      e[2 * p + 1] = __uint_as_float(uint32_t(u[p]) & 0xffff0000u);
-    }
-  };
-  auto mma = [&](int qm, int qn) {
+  // one quadrant's 16 MFMAs; sbuf: also the scale pass of (sq, su) loaded in
+  // this phase's read segment, its VALU and stores issued between the MFMAs
+  auto mma = [&](int qm, int qn, bool scale = false, uint8_t* sbuf = nullptr, int sq = 0, int su_ = 0) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
     __builtin_amdgcn_sched_barrier(0);
-    if (qm == qn) {  // first use of this A set in the K tile: FM terms, then the weight scaling
-      if (fm_on && qm == fm_qm) {
-        bf16x8 v = fa[0][0];
-        float w = wa[0];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (kk == fm_kk && i == wc) {
-              v = fa[kk][i];
-              w = wa[i];
-            }
-        float e[8];
-        unpack(v, e);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = e[j] * w;
-          fs[j] += x;
-          fsq += x * x;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (qm == qn) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          float e[8];
-          unpack(fa[kk][i], e);
-          bf16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(e[j] * wa[i]);
-          fa[kk][i] = o;
-        }
-      }
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4& c = acc[4 * qm + i][2 * qn + j];
@@ -1185,6 +1207,15 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
         for (int kk = 0; kk < 2; ++kk)
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][kk][j], fa[kk][i], c, 0, 0, 0);
       }
+    if (scale) {  // a literal at every call: folded, one basic block with the MFMAs
+      scale_store(sbuf, sq, su_);
+      // interleave: the scale VALU issues while the MFMAs occupy the matrix pipe
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+      }
+      __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);    // the 2 LDS stores
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
@@ -1193,40 +1224,45 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // every 4 consecutive phases issue 9 DMA instructions (see above)
   auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); };
+  auto wait_lds = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   for (int t = 0; t < nk; ++t) {
-    const uint8_t* buf = smem + (t & 1) * BUF;
-    // p0: A[qm0] B[qn0]; stage Bq1(t+1) and the ring for tile t+3; rows for p1's stage
-    read_a(buf, 0, t);
+    uint8_t* buf = smem + (t & 1) * BUF;
+    uint8_t* nbuf = smem + ((t + 1) & 1) * BUF;
+    // p0: A[qm0] B[qn0]; stage Bq1(t+1), Aq1(t+1) (rows read in p3), the ring for tile t+3
+    read_a(buf, 0);
     read_b(buf, 0);
     stage_b(1, t + 1);
+    stage_a(1, t + 1);
     stage_ring(t + 3);
-    read_rows(1, t + 1);
     wait_dma();
     barrier();
     mma(0, 0);
     barrier();
-    // p1: B[qn1]; stage Aq1(t+1); rows for p2's stage
+    // p1: B[qn1]; scale Aq1(t) (load here, rescale + store between the MFMAs); rows for p2's stage
     read_b(buf, 1);
-    stage_a(1, t + 1);
+    scale_load(buf, 1, t);
     read_rows(0, t + 2);
     wait_dma();
     barrier();
-    mma(0, 1);
+    mma(0, 1, true, buf, 1, t);
+    wait_lds();
     barrier();
     // p2: A[qm1]; stage Aq0(t+2)
-    read_a(buf, 1, t);
+    read_a(buf, 1);
     stage_a(0, t + 2);
     wait_dma();
     barrier();
     mma(1, 1);
     barrier();
-    // p3: stage Bq0(t+2)
+    // p3: scale Aq0(t+1) (as in p1); rows for p0's stage; stage Bq0(t+2)
+    scale_load(nbuf, 0, t + 1);
+    read_rows(1, t + 2);
     stage_b(0, t + 2);
     wait_dma();
     barrier();
-    mma(1, 0);
+    mma(1, 0, true, nbuf, 0, t + 1);
+    wait_lds();
     barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1238,9 +1274,10 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     float part = -fsq;
 #pragma unroll
     for (int j = 0; j < 8; ++j) part += fs[j] * fs[j];
-    part += __shfl_xor(part, 16, 64);
-    part += __shfl_xor(part, 32, 64);
-    if (fq == 0) fm_part[int64_t(1 + tn) * Mp + m0 + 128 * wr + 64 * fm_qm + 16 * wc + fr] = 0.5f * part;
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    if (sp_ch == 0) fm_part[Mp + m0 + scale_row(fm_q, fm_h)] = 0.5f * part;
   }
 }
 

@@ -115,8 +115,8 @@ struct MxIO {
 // K1 fused into K4 (gemm.hip gemm_gather_kernel): C bf16 [M, N] =
 // epi(sum_f bf16(w * T[row]) . W[:, 64f:64f+64]^T + bias) for a bf16 table
 // with 64-wide rows (128 B), rows_t / wts_t from launch_embed_resolve, W bf16
-// [N, 64F]; N % 256 == 0. fm_part (N >= 1024): rows 1..4 of the [5][Mp] FM
-// partials receive the second-order FM term split over 4 dim / row partitions.
+// [N, 64F]; N % 256 == 0. fm_part (N >= 1024): row 1 of the [2][Mp] FM
+// partials receives the second-order FM term.
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                               int N, int epi, hipStream_t st);

@@ -375,7 +375,7 @@ def embed_cross(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: i
 # Below this many candidate rows the gather-GEMM's 256x256 tiles leave most
 # CUs idle and the separate gather + smaller-tile GEMM wins (tools/studies/
 # microbench.py --gather-gemm, profiles/r03_gather_gemm.md).
-GATHER_GEMM_MIN_ROWS = 8192
+GATHER_GEMM_MIN_ROWS = 16384
 
 
 def embed_gemm_ok(table: torch.Tensor, W: torch.Tensor, B: int, fm2: bool) -> bool:
@@ -392,8 +392,8 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
                fm2: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
     """K1 fused into the first MLP layer (K4): returns
       h     = act(x W^T + b) bf16 [B, N], x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)),
-      parts = fp32 [1 + 4 fm2, >= B]: row 0 = bias + sum_f lin[row] w, rows 1.. the
-              second-order FM term in partitions (heads sum the rows, _extra_logit).
+      parts = fp32 [1 + fm2, >= B]: row 0 = bias + sum_f lin[row] w, row 1 the
+              second-order FM term (heads sum the rows, _extra_logit).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
     table rows straight into the GEMM's LDS tiles); on the CPU the unfused math."""
     m = int(modulo) if modulo > 0 else table.shape[0]

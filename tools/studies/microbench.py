@@ -199,11 +199,15 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
         def fused():
             return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=True)
 
+        def fused_nofm():
+            return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=False)
+
         x, _ = ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True)
-        t = {k: [] for k in ("unfused", "fused", "embed", "gemm")}
+        t = {k: [] for k in ("unfused", "fused", "embed", "gemm", "fused_nofm")}
         for _ in range(5):  # interleaved
             t["unfused"].append(_time(unfused, 20, 1))
             t["fused"].append(_time(fused, 20, 1))
+            t["fused_nofm"].append(_time(fused_nofm, 20, 1))
             t["embed"].append(_time(lambda: ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True,
                                                       want_fm=True, fm2=True), 20, 1))
             t["gemm"].append(_time(lambda: ops.linear(x, W, b, "relu"), 20, 1))
