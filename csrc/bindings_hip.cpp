@@ -257,12 +257,14 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
 // gather-GEMM (csrc/kernels/gemm.hip gemm_gather_kernel). Rows come from a
 // device request arena (arena, B, F) or from ids [B, F] (+ wts). Returns
 //   h     bf16 [B, N] = act(x . W^T + b), x = w * T[row] never materialised
-//   parts fp32 [1 + fm2, Mp]: row 0 = bias + first-order FM term, row 1 the
-//         second-order FM term (the head sums the rows).
+//   parts fp32 [1 + (fm2 or cross), Mp]: row 0 = bias + first-order FM term,
+//         row 1 the second-order FM term or (cross_w / cross_c: DCN v1's folded
+//         cross weights) the cross logit; the head sums the rows.
 std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::Tensor> lin,
                                       c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
                                       c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
-                                      double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2) {
+                                      double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2,
+                                      c10::optional<torch::Tensor> cross_w, c10::optional<torch::Tensor> cross_c) {
   check_dev(table, "table");
   check_dev(W, "W");
   check_dev(b, "b");
@@ -311,10 +313,23 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
       a.wts_ld = wts->stride(0);
     }
   }
+  const bool cross = cross_w.has_value();
+  if (cross) {
+    check_dev(*cross_w, "cross_w");
+    TORCH_CHECK(cross_c.has_value(), "cross_w and cross_c go together");
+    check_dev(*cross_c, "cross_c");
+    TORCH_CHECK(!fm2, "a model has either the FM term or the cross network");
+    TORCH_CHECK(cross_w->scalar_type() == torch::kFloat32 && cross_w->dim() == 2 && cross_w->size(1) == F * 64 &&
+                    cross_w->size(0) >= 1 && cross_w->size(0) <= 4 && cross_w->is_contiguous(),
+                "cross_w must be contiguous fp32 [L + 1 <= 4, 64 F]");
+    TORCH_CHECK(cross_c->scalar_type() == torch::kFloat32 && cross_c->numel() == cross_w->size(0),
+                "cross_c must be fp32 [L + 1]");
+    TORCH_CHECK(N >= 1024, "the cross network rides on N >= 1024 (4 column tiles)");
+  }
   c10::DeviceGuard g(table.device());
   const int64_t Mp = (B + 255) / 256 * 256;
   auto h = torch::empty({B, N}, table.options());
-  auto parts = torch::empty({fm2 ? 2 : 1, Mp}, table.options().dtype(torch::kFloat32));
+  auto parts = torch::empty({(fm2 || cross) ? 2 : 1, Mp}, table.options().dtype(torch::kFloat32));
   auto rows_t = torch::empty({F, Mp}, table.options().dtype(torch::kInt32));
   auto wts_t = torch::empty({F, Mp}, table.options().dtype(torch::kFloat32));
   if (B == 0) return {h, parts};
@@ -332,7 +347,9 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
             "embed_resolve");
   check_hip(dtfs::launch_gemm_gather(table.data_ptr(), V, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), Mp,
                                      int(F), W.data_ptr(), b.data_ptr<float>(), h.data_ptr(), N,
-                                     fm2 ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st),
+                                     (fm2 || cross) ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st,
+                                     cross ? cross_w->data_ptr<float>() : nullptr,
+                                     cross ? cross_c->data_ptr<float>() : nullptr, cross ? int(cross_w->size(0)) : 0),
             "gemm_gather");
   return {h, parts};
 }
@@ -683,6 +700,20 @@ void pull_host(torch::Tensor dst, torch::Tensor src, int64_t nbytes, int64_t blo
 }
 
 // ---------------------------------------------------------------- fp8
+torch::Tensor dense_pad(torch::Tensor x, int64_t n, int64_t K) {
+  TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");  // a row view of packed request rows
+  TORCH_CHECK(x.scalar_type() == torch::kFloat32 && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) >= n &&
+                  x.size(1) >= n,
+              "x must be fp32 [M, >= n] with contiguous rows");
+  TORCH_CHECK(K % 8 == 0 && n >= 0 && n <= K, "K % 8 == 0, 0 <= n <= K");
+  c10::DeviceGuard g(x.device());
+  auto y = torch::empty({x.size(0), K}, x.options().dtype(torch::kBFloat16));
+  check_hip(dtfs::launch_dense_pad(x.data_ptr<float>(), x.stride(0), int(x.size(0)), int(n), y.data_ptr(), int(K),
+                                   cur_stream(x)),
+            "dense_pad");
+  return y;
+}
+
 std::vector<torch::Tensor> quant_rows_fp8(torch::Tensor x, int64_t k_pad) {
   check_dev(x, "x");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.dim() == 2, "x must be bf16 [M, K]");
@@ -1018,9 +1049,10 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("want_x") = true, py::arg("want_fm") = false, py::arg("fm2") = false, py::arg("out_x") = py::none(),
         py::arg("validate_tables") = false, py::arg("shard_lo_f") = py::none(), py::arg("shard_n_f") = py::none(),
         py::arg("k_pad") = 0, py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none());
+  m.def("dense_pad", &dense_pad, py::arg("x"), py::arg("n"), py::arg("K"));
   m.def("embed_gemm", &embed_gemm, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"), py::arg("wts"),
         py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W"), py::arg("b"), py::arg("act"),
-        py::arg("fm2"));
+        py::arg("fm2"), py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none());
   m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
         py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
         py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0, py::arg("cross_w") = py::none(),

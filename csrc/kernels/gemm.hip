@@ -1013,23 +1013,34 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
 // 8 lanes finish the row, so every candidate's second-order term
 //   fm_part[Mp + m] = 0.5 * (sum_d (sum_f v_fd)^2 - sum_{f,d} v_fd^2)
 // comes from exactly one tile, and the head adds it to part0 (bias + first
-// order, from the resolve kernel): no second pass over the table.
-template <typename OutT>
+// order, from the resolve kernel): no second pass over the table. DCN (EXTRA
+// 2) takes the same rows' L + 1 cross dot products instead and writes the
+// cross logit there.
+// EXTRA: what rides on the scale pass - 0 nothing (WDL), 1 the FM
+// second-order term (DeepFM), 2 the DCN v1 cross network (K3): the L + 1 dot
+// products of x0 with the folded cross weights (embedding.hip "K3 in the
+// gather"), whose K-tile slices travel through a third ring.
+template <typename OutT, int EXTRA>
 __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restrict__ table, int Vm1,
                                                           const int32_t* __restrict__ rows_t,
                                                           const float* __restrict__ wts_t, int64_t Mp,
                                                           const uint8_t* __restrict__ W, const float* __restrict__ bias,
                                                           OutT* __restrict__ C, int64_t ldc, float* __restrict__ fm_part,
-                                                          int M, int N, int F, int epi) {
+                                                          const float* __restrict__ cross_w,
+                                                          const float* __restrict__ cross_c, int cross_n, int M, int N,
+                                                          int F, int epi) {
   constexpr int BM = 256, BN = 256;
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
   constexpr int RING = 8;
-  // one LDS object (A/B double buffer | ring rows | ring weights): separate
-  // __shared__ arrays made the compiler put vmcnt(0) in front of the A-tile
-  // reads (LDS-DMA alias tracking), draining the DMA pipeline twice a K tile
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF + 2 * RING * BM * 4];
+  constexpr int XMAX = 4;  // cross weight rows per K tile (L + 1 <= 4)
+  // one LDS object (A/B double buffer | ring rows | ring weights | ring cross
+  // weights): separate __shared__ arrays made the compiler put vmcnt(0) in
+  // front of the A-tile reads (LDS-DMA alias tracking), draining the DMA
+  // pipeline twice a K tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF + 3 * RING * BM * 4];
   int32_t(*s_rows)[BM] = reinterpret_cast<int32_t(*)[BM]>(smem + 2 * BUF);
   float(*s_wts)[BM] = reinterpret_cast<float(*)[BM]>(smem + 2 * BUF + RING * BM * 4);
+  float(*s_xw)[XMAX][64] = reinterpret_cast<float(*)[XMAX][64]>(smem + 2 * BUF + 2 * RING * BM * 4);
 
   const int tiles_n = N / BN, tiles_m = int(Mp / BM);
   const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -1051,14 +1062,29 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   // (kept in SGPRs: the kernel sits near the 256-VGPR limit of 2 waves / SIMD).
   const int coff = (ls ^ ((4 * (wid & 1)) | (lr >> 1))) << 4;
   const int b_lane = lr * int(ldw) * 2 + coff;  // N * K * 2 < 2^31 (launcher)
-  // ring: this wave's 4-byte DMA of tile u's 64 rows (waves 0-3) or weights (4-7)
+  // ring: ONE 16-byte-per-lane LDS-DMA per wave per K tile (so every wave's
+  // counted waits stay identical): wave w fetches kind w % 3 - tile u's 256
+  // rows (1 KiB), their weights, or the cross weights' 64-column slices (lane
+  // l: row l >> 4, columns 4 (l & 15) ..; a dummy re-fetch of the rows
+  // without a cross network) - kinds fetched by two or three waves write the
+  // same bytes twice
+  const int rk = wid % 3;
   auto stage_ring = [&](int u) {
-    const int64_t src = int64_t(min(u, nk - 1)) * Mp + m0 + 64 * (wid & 3) + lane;
-    const void* g = wid < 4 ? static_cast<const void*>(rows_t + src) : static_cast<const void*>(wts_t + src);
-    void* l = wid < 4 ? static_cast<void*>(&s_rows[u & (RING - 1)][64 * (wid & 3)])
-                      : static_cast<void*>(&s_wts[u & (RING - 1)][64 * (wid & 3)]);
+    const int uc = min(u, nk - 1), slot = u & (RING - 1);
+    const void* g;
+    void* l;
+    if (rk == 2 && EXTRA == 2) {
+      const int xr = min(lane >> 4, cross_n - 1);
+      g = cross_w + int64_t(xr) * F * 64 + uc * 64 + (lane & 15) * 4;
+      l = &s_xw[slot][0][0];
+    } else {
+      const int64_t src = int64_t(uc) * Mp + m0 + lane * 4;
+      g = rk == 1 ? static_cast<const void*>(wts_t + src) : static_cast<const void*>(rows_t + src);
+      l = rk == 1 ? static_cast<void*>(&s_wts[slot][0])
+                  : (rk == 0 ? static_cast<void*>(&s_rows[slot][0]) : static_cast<void*>(&s_xw[slot][0][0]));
+    }
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
-                                     (__attribute__((address_space(3))) void*)(l), 4, 0, 0);
+                                     (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
   };
   int ida[2];  // table rows of the next A stage
   auto read_rows = [&](int q, int kt) {
@@ -1094,11 +1120,15 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   // reads. The chunks are loaded in a phase's read segment (retired by then) and
   // rescaled + written back in its MFMA segment, between the MFMAs.
   const int sp_rr = (threadIdx.x & 255) >> 3, sp_ch = threadIdx.x & 7;
-  const bool fm_on = fm_part != nullptr && tn < 4;
+  // the logical 8-dim chunk this thread always holds (rows 64 q + rr + 32 h all
+  // share the swizzle (rr >> 1) & 7)
+  const int sp_dim = 8 * (sp_ch ^ ((sp_rr >> 1) & 7));
+  const bool fm_on = EXTRA != 0 && fm_part != nullptr && tn < 4;
   const int fm_q = tn >> 1, fm_h = tn & 1;
-  float fs[8], fsq = 0.f;
+  constexpr int NFS = EXTRA == 1 ? 8 : (EXTRA == 2 ? XMAX : 1);
+  float fs[NFS], fsq = 0.f;  // FM: per-dim sums + sum of squares; cross: the dot products
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fs[j] = 0.f;
+  for (int j = 0; j < NFS; ++j) fs[j] = 0.f;
   i32x4 su[2];
   float sw[2];
   auto scale_row = [&](int q, int h) { return 128 * wr + 64 * q + sp_rr + 32 * h; };
@@ -1131,13 +1161,26 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     if (fm_on && q == fm_q && u < nk) {
       const i32x4 uf = fm_h ? su[1] : su[0];
       const float wf = fm_h ? sw[1] : sw[0];
+      float v[8];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const float x = __uint_as_float(uint32_t(uf[p]) << 16) * wf;
-        const float y = __uint_as_float(uint32_t(uf[p]) & 0xffff0000u) * wf;
-        fs[2 * p] += x;
-        fs[2 * p + 1] += y;
-        fsq += x * x + y * y;
+        v[2 * p] = __uint_as_float(uint32_t(uf[p]) << 16) * wf;
+        v[2 * p + 1] = __uint_as_float(uint32_t(uf[p]) & 0xffff0000u) * wf;
+      }
+      if constexpr (EXTRA == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          fs[j] += v[j];
+          fsq += v[j] * v[j];
+        }
+      } else if constexpr (EXTRA == 2) {
+#pragma unroll
+        for (int l = 0; l < XMAX; ++l) {
+          const f32x4 c0 = *reinterpret_cast<const f32x4*>(&s_xw[u & (RING - 1)][l][sp_dim]);
+          const f32x4 c1 = *reinterpret_cast<const f32x4*>(&s_xw[u & (RING - 1)][l][sp_dim + 4]);
+          fs[l] += v[0] * c0[0] + v[1] * c0[1] + v[2] * c0[2] + v[3] * c0[3] + v[4] * c1[0] + v[5] * c1[1] +
+                   v[6] * c1[2] + v[7] * c1[3];
+        }
       }
     }
   };
@@ -1270,14 +1313,33 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
 
   store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
                             nullptr, 0, epi);
-  if (fm_on) {
-    float part = -fsq;
+  if constexpr (EXTRA == 1) {
+    if (fm_on) {
+      float part = -fsq;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part += fs[j] * fs[j];
-    part += __shfl_xor(part, 1, 64);
-    part += __shfl_xor(part, 2, 64);
-    part += __shfl_xor(part, 4, 64);
-    if (sp_ch == 0) fm_part[Mp + m0 + scale_row(fm_q, fm_h)] = 0.5f * part;
+      for (int j = 0; j < 8; ++j) part += fs[j] * fs[j];
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      if (sp_ch == 0) fm_part[Mp + m0 + scale_row(fm_q, fm_h)] = 0.5f * part;
+    }
+  } else if constexpr (EXTRA == 2) {
+    if (fm_on) {  // x_l = alpha_l x0 + beta_l: alpha_{l+1} = alpha_l + alpha_l s_l + c_l
+#pragma unroll
+      for (int l = 0; l < XMAX; ++l) {
+        fs[l] += __shfl_xor(fs[l], 1, 64);
+        fs[l] += __shfl_xor(fs[l], 2, 64);
+        fs[l] += __shfl_xor(fs[l], 4, 64);
+      }
+      const int L = cross_n - 1;
+      float alpha = 1.f, dL = fs[0];
+#pragma unroll
+      for (int l = 0; l < XMAX; ++l) {
+        if (l < L) alpha += alpha * fs[l] + cross_c[l];
+        if (l == L) dL = fs[l];
+      }
+      if (sp_ch == 0) fm_part[Mp + m0 + scale_row(fm_q, fm_h)] = alpha * dL + cross_c[L];
+    }
   }
 }
 
@@ -1560,16 +1622,23 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
 
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
-                              int N, int epi, hipStream_t st) {
+                              int N, int epi, hipStream_t st, const float* cross_w, const float* cross_c,
+                              int cross_n) {
   if (M == 0) return hipSuccess;
   if (F < 1 || N <= 0 || N % 256 != 0 || Mp % 256 != 0 || Mp < M || V < 1 || V > (int64_t(1) << 31) ||
       ldc < N || ldc % 4 != 0 || (fm_part && N < 1024) || int64_t(N) * F * 128 >= (int64_t(1) << 31) || !table ||
       !rows_t || !wts_t || !W || !C)
     return hipErrorInvalidValue;
+  if (cross_w && (!fm_part || !cross_c || cross_n < 1 || cross_n > 4)) return hipErrorInvalidValue;
   const int grid = int(Mp / 256) * (N / 256);
-  hipLaunchKernelGGL((gemm_gather_kernel<bf16>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(table),
-                     int(V - 1), rows_t, wts_t, Mp, static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc,
-                     fm_part, M, N, F, epi);
+#define DTFS_GG(X)                                                                                                 \
+  hipLaunchKernelGGL((gemm_gather_kernel<bf16, X>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(table), \
+                     int(V - 1), rows_t, wts_t, Mp, static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc,  \
+                     fm_part, cross_w, cross_c, cross_n, M, N, F, epi)
+  if (cross_w) DTFS_GG(2);
+  else if (fm_part) DTFS_GG(1);
+  else DTFS_GG(0);
+#undef DTFS_GG
   return hipGetLastError();
 }
 

@@ -117,9 +117,13 @@ struct MxIO {
 // with 64-wide rows (128 B), rows_t / wts_t from launch_embed_resolve, W bf16
 // [N, 64F]; N % 256 == 0. fm_part (N >= 1024): row 1 of the [2][Mp] FM
 // partials receives the second-order FM term.
+// cross_w / cross_c / cross_n (DCN v1, with fm_part): the folded cross
+// weights fp32 [cross_n][64F] + constants (EmbedArgs.cross_*, cross_n <= 4);
+// fm_part's row 1 then receives the cross logit instead of the FM term.
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
-                              int N, int epi, hipStream_t st);
+                              int N, int epi, hipStream_t st, const float* cross_w = nullptr,
+                              const float* cross_c = nullptr, int cross_n = 0);
 
 // K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
@@ -145,6 +149,9 @@ hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, con
 hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* emb, int T, int B, void* out,
                                   int64_t ldo, int out_cols, hipStream_t st, const int64_t* emb_off = nullptr,
                                   const int64_t* emb_stride = nullptr, int64_t emb_rows = 0);
+
+// DLRM dense input: y bf16 [M, K] = x[:, :n] (fp32, row stride ldx) zero padded; K % 8 == 0.
+hipError_t launch_dense_pad(const float* x, int64_t ldx, int M, int n, void* y, int K, hipStream_t st);
 
 // K6: y = act(x . w + bias + extra), act 0 none / 2 sigmoid (extra_n / extra_ld: launch_gemm_head).
 hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,

@@ -189,6 +189,13 @@ class DCN(CTRModel):
         self.head_b = 0.0
 
     def _forward(self, ids, wts, out=None):
+        if self.cfg.num_cross_layers + 1 <= 4 and self._gather_gemm(ids, wts, fm2=True):
+            # gather + cross network + first MLP layer in one kernel (x0 never in HBM)
+            first = self.mlp.layers[0]
+            h, parts = ops.embed_gemm(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, first.weight, first.bias,
+                                      first.act, fm2=False,
+                                      cross=(self.cross_w, self.cross_b, self.head_wc, self._cross_consts()))
+            return self.mlp.forward_head(h, self.head_wd, self.head_b, extra=parts, out=out, start=1)
         # the whole cross network rides on the gather (ops.embed_cross): the
         # wave holding x0 computes its L + 1 weight dot products
         on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
@@ -347,13 +354,19 @@ class DLRM(CTRModel):
         return 1.0 / math.sqrt(self.cfg.embed_dim)
 
     def dense_input(self, wts: torch.Tensor) -> torch.Tensor:
+        """Dense features (the first num_dense weight columns) as the bottom
+        MLP's zero-padded bf16 input [B, dense_k]: one kernel on the GPU."""
         nd = self.cfg.num_dense
+        if wts.is_cuda and wts.dtype == torch.float32 and self.dtype == torch.bfloat16 and wts.stride(1) == 1:
+            return ops.hip().dense_pad(wts, nd, self.dense_k)
         x = torch.zeros(wts.shape[0], self.dense_k, dtype=self.dtype, device=wts.device)
         x[:, :nd] = wts[:, :nd]
         return x
 
     def sparse_ids(self, ids: torch.Tensor) -> torch.Tensor:
-        return ids[:, self.cfg.num_dense:].contiguous()
+        """The sparse id columns as a row view (the gather kernels take a row
+        stride; a .contiguous() copy here was a 9 us kernel per served step)."""
+        return ids[:, self.cfg.num_dense:]
 
     def lookup(self, ids: torch.Tensor, wts: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Local (single-process) lookup of every sparse table -> [B, T, D].

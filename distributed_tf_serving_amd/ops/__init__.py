@@ -380,7 +380,8 @@ GATHER_GEMM_MIN_ROWS = 16384
 
 def embed_gemm_ok(table: torch.Tensor, W: torch.Tensor, B: int, fm2: bool) -> bool:
     """Shapes the gather-GEMM covers: a bf16 [V, 64] table, a bf16 first layer
-    with N % 256 == 0 (N >= 1024 with the FM term), enough rows to fill the GPU."""
+    with N % 256 == 0 (N >= 1024 with the FM term or the cross network), enough
+    rows to fill the GPU."""
     N, K = W.shape
     return (table.is_cuda and table.dtype == torch.bfloat16 and table.dim() == 2 and table.shape[1] == 64
             and W.dtype == torch.bfloat16 and N % 256 == 0 and (not fm2 or N >= 1024)
@@ -389,22 +390,35 @@ def embed_gemm_ok(table: torch.Tensor, W: torch.Tensor, B: int, fm2: bool) -> bo
 
 def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
                bias: float, W: torch.Tensor, b: torch.Tensor, act: str = "relu",
-               fm2: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+               fm2: bool = True, cross=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """K1 fused into the first MLP layer (K4): returns
       h     = act(x W^T + b) bf16 [B, N], x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)),
       parts = fp32 [1 + fm2, >= B]: row 0 = bias + sum_f lin[row] w, row 1 the
               second-order FM term (heads sum the rows, _extra_logit).
+    ``cross = (w, b, head_w)`` (DCN v1, fm2 False): row 1 of parts is the cross
+    network's logit x_L . head_w instead (the GPU takes the folded weights,
+    ``cross_consts = cross_v1_consts(w, b, head_w)``, as ``cross[3]`` when given).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
     table rows straight into the GEMM's LDS tiles); on the CPU the unfused math."""
     m = int(modulo) if modulo > 0 else table.shape[0]
     on_gpu = ids.arena.is_cuda if isinstance(ids, ArenaRows) else ids.is_cuda
     if on_gpu:
         a = _ACTS[act]
+        xw = xc = None
+        if cross is not None:
+            xw, xc = cross[3] if len(cross) > 3 and cross[3] is not None else cross_v1_consts(*cross[:3])
         if isinstance(ids, ArenaRows):
             return tuple(hip().embed_gemm(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias),
-                                          W, b, a, fm2))
+                                          W, b, a, fm2, xw, xc))
         return tuple(hip().embed_gemm(table, lin, None, _rows(ids), None if wts is None else _rows(wts),
-                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2))
+                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2, xw, xc))
+    if cross is not None:
+        x, logit = embed_cross(table, ids, wts, m, cross[0], cross[1], cross[2])
+        first = torch.full((1, x.shape[0]), float(bias), dtype=torch.float32)
+        if lin is not None:
+            _, fm = embed(table, ids, wts, lin=lin, modulo=m, bias=bias, want_x=False, want_fm=True, fm2=False)
+            first = fm.view(1, -1)
+        return linear(x, W, b, act), torch.cat([first, logit.float().view(1, -1)])
     x, fm = embed(table, ids, wts, lin=lin, modulo=m, bias=bias, want_x=True, want_fm=True, fm2=fm2)
     return linear(x, W, b, act), fm.view(1, -1)
 

@@ -122,7 +122,9 @@ def main():
         if a.grpc_port:
             from distributed_tf_serving_amd.client.backends import GrpcBackend
 
-            port = srv.start_grpc(a.grpc_port + (rank if a.mode == "alltoall" else 0), host="127.0.0.1")
+            # alltoall: every rank is a front door; an ephemeral port each (port + rank
+            # could collide with the rendezvous / RCCL sockets)
+            port = srv.start_grpc(0 if a.mode == "alltoall" else a.grpc_port, host="127.0.0.1")
             be = GrpcBackend(f"127.0.0.1:{port}")
             gd = []
             for data, ids, wts in reqs[:4]:

@@ -686,7 +686,34 @@ def test_embed_gemm_arena_rows(cuda):
     _close(parts[:, :B], pp[:, :B], 0, 0, "arena vs unpacked FM partials")
 
 
-@pytest.mark.parametrize("family", ["deepfm", "wdl"])
+@pytest.mark.parametrize("B,L", [(1, 3), (4099, 3), (16384, 3), (300, 2), (300, 1)])
+def test_embed_gemm_cross_matches_layerwise_reference(cuda, B, L):
+    """The gather-GEMM with the DCN v1 cross network on the scale pass: the
+    cross logit vs the fp32 layer-by-layer math; h as without it."""
+    V, F, d = 50_000, 43, 43 * 64
+    table, lin, W, b, ids, wts = _gather_gemm_case(B, V=V)
+    g = torch.Generator().manual_seed(9)
+    cw = (torch.rand(max(L, 1), d, generator=g) - 0.5) * 0.02
+    cb = (torch.rand(max(L, 1), d, generator=g) - 0.5) * 0.02
+    hw = (torch.rand(d, generator=g) - 0.5) * 0.05
+    cw, cb = cw[:L], cb[:L]
+    dv = [t.to(cuda) for t in (table, W, b, ids, wts, cw, cb, hw)]
+    h, parts = ops.embed_gemm(dv[0], dv[3], dv[4], None, V, 0.0, dv[1], dv[2], "relu", fm2=False,
+                              cross=(dv[5], dv[6], dv[7]))
+    assert parts.shape[0] == 2
+    rows = torch.remainder(ids, V)
+    x0 = (table[rows].float() * wts[..., None]).reshape(B, -1)
+    xl = x0
+    for i in range(L):
+        xl = x0 * (xl @ cw[i])[:, None] + cb[i] + xl
+    want = xl @ hw
+    h_ref = torch.relu(x0 @ W.float().t() + b)
+    _close(h, h_ref, 2e-2, 2e-3, "cross gather-GEMM h vs fp32")
+    _close(parts[0, :B], torch.zeros(B), 0, 0, "part0 (no first-order term)")
+    _close(parts[1, :B], want, 1e-3, 1e-4, "cross logit vs layer-by-layer fp32")
+
+
+@pytest.mark.parametrize("family", ["deepfm", "wdl", "dcn"])
 def test_gather_gemm_model_path_matches_unfused(cuda, family):
     """DeepFM / WDL at a served bucket size take the gather-GEMM path; scores
     match the unfused path (gather kernel + GEMM) of the same weights."""
@@ -695,8 +722,17 @@ def test_gather_gemm_model_path_matches_unfused(cuda, family):
     B = max(8192, ops.GATHER_GEMM_MIN_ROWS)
     ids = torch.randint(0, 1 << 40, (B, 43), device=cuda)
     wts = torch.rand(B, 43, device=cuda)
-    assert m._gather_gemm(ids, wts, fm2=family == "deepfm")
+    assert m._gather_gemm(ids, wts, fm2=family != "wdl")
     got = m(ids, wts)
     m.use_gather_gemm = False
     want = m(ids, wts)
     _close(got, want, 0, 5e-5, f"{family} gather-GEMM vs unfused")
+
+
+@pytest.mark.parametrize("M,n,K,ld", [(1, 13, 64, 13), (300, 13, 64, 43), (4099, 64, 64, 70)])
+def test_dense_pad(cuda, M, n, K, ld):
+    x = torch.randn(M, ld + 5, device=cuda)[:, :ld]  # a row view, like packed request rows
+    y = ops.hip().dense_pad(x, n, K)
+    want = torch.zeros(M, K, dtype=torch.bfloat16)
+    want[:, :n] = x[:, :n].cpu().to(torch.bfloat16)
+    assert torch.equal(y.cpu(), want)

@@ -24,10 +24,15 @@ def _short(name: str) -> str:
     return name[:90]
 
 
-def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "") -> str:
+def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "", from_kernel: str = "") -> str:
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end, duration from kernels order by start"))
     copies = list(c.execute("select name, start, end, duration, size from memory_copies order by start"))
+    if from_kernel:  # drop start-up work (weight init, graph capture) before the first step kernel
+        t0 = next((s for name, s, e, d in rows if from_kernel in name), None)
+        if t0 is not None:
+            rows = [r for r in rows if r[1] >= t0]
+            copies = [r for r in copies if r[1] >= t0]
     agg = defaultdict(list)
     for name, s, e, d in rows:
         agg[_short(name)].append(d / 1e3)
@@ -69,8 +74,9 @@ def main():
     ap.add_argument("--steps", type=int, default=0)
     ap.add_argument("--title", default="")
     ap.add_argument("--last-kernel", default="", help="substring of the step's final kernel, for the step period")
+    ap.add_argument("--from-kernel", default="", help="ignore everything before the first kernel matching this")
     a = ap.parse_args()
-    print(summarize(a.db, a.steps, a.title, a.last_kernel), end="")
+    print(summarize(a.db, a.steps, a.title, a.last_kernel, a.from_kernel), end="")
 
 
 if __name__ == "__main__":
