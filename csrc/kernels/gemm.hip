@@ -984,8 +984,9 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
 // staged by the same LDS-DMA instructions as the dense kernel but from
 // table + row * 128 per lane. The rows and weights of a K tile come from
 // embed_resolve_kernel's field-major rows_t / wts_t [F][Mp] through an 8-slot
-// LDS ring: ONE 4-byte LDS-DMA per lane per K tile (waves 0-3 rows, 4-7
-// weights), issued in phase 0 three tiles ahead. A stage's rows are read from
+// LDS ring: ONE LDS-DMA per wave per K tile, issued in phase 1 four tiles
+// ahead (in phase 0, three ahead, it crowded the phase that already issues 4
+// quarter DMAs: 104.4 vs 107.9 us at 16384 rows). A stage's rows are read from
 // the ring a phase before it (mma()'s lgkmcnt(0) covers the read).
 //
 // The weights are applied ONCE per element, in LDS: x = bf16(w * e) (the
@@ -996,10 +997,12 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
 // VALU on the 146 us kernel at 16384 rows); the pass adds 2 x 16 KB of LDS
 // traffic per K tile and ~40 VALU per wave, issued between the MFMAs. For the
 // spare phase Aq1 is staged one phase earlier than in the dense kernel:
-//   p0: stage Bq1(t+1) Aq1(t+1) ring(t+3)   p1: scale Aq1(t)
-//   p2: stage Aq0(t+2)                       p3: scale Aq0(t+1), stage Bq0(t+2)
-// 5 + 0 + 2 + 2 = 9 DMA instructions per 4 phases, so the counted wait
-// vmcnt(9) retires every DMA issued 4 phases earlier (quarters, ring alike).
+//   p0: stage Bq1(t+1) Aq1(t+1)   p1: scale Aq1(t), ring(t+4)
+//   p2: stage Aq0(t+2)             p3: scale Aq0(t+1), stage Bq0(t+2)
+// 4 + 1 + 2 + 2 = 9 DMA instructions per 4 phases, so the counted wait
+// vmcnt(9) retires every DMA issued 4 phases earlier (quarters, ring alike):
+// ring(u) lands by phase 1 of tile u-3, one phase before its first read
+// (phase 1 of tile u-2 reads the rows for Aq0(u)).
 // Each quarter is loaded for scaling one phase after the wait that retires it
 // (the read segment, so the other group has passed that wait too) and read by
 // the MFMA phase after that: a group scales only the rows it reads, so its
@@ -1196,6 +1199,7 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   stage_ring(0);
   stage_ring(1);
   stage_ring(2);
+  stage_ring(3);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   read_rows(0, 0);
@@ -1272,20 +1276,21 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   for (int t = 0; t < nk; ++t) {
     uint8_t* buf = smem + (t & 1) * BUF;
     uint8_t* nbuf = smem + ((t + 1) & 1) * BUF;
-    // p0: A[qm0] B[qn0]; stage Bq1(t+1), Aq1(t+1) (rows read in p3), the ring for tile t+3
+    // p0: A[qm0] B[qn0]; stage Bq1(t+1), Aq1(t+1) (rows read in p3)
     read_a(buf, 0);
     read_b(buf, 0);
     stage_b(1, t + 1);
     stage_a(1, t + 1);
-    stage_ring(t + 3);
     wait_dma();
     barrier();
     mma(0, 0);
     barrier();
-    // p1: B[qn1]; scale Aq1(t) (load here, rescale + store between the MFMAs); rows for p2's stage
+    // p1: B[qn1]; scale Aq1(t) (load here, rescale + store between the MFMAs); rows for p2's stage;
+    // the ring for tile t+4
     read_b(buf, 1);
     scale_load(buf, 1, t);
     read_rows(0, t + 2);
+    stage_ring(t + 4);
     wait_dma();
     barrier();
     mma(0, 1, true, buf, 1, t);
