@@ -67,6 +67,15 @@ BASELINE_VALUE = None  # the reference publishes no numbers
 PRESETS = {"deepfm": "deepfm_1gpu", "dlrm": "dlrm_sharded8", "dcn_v2": "dcn_v2_fp8"}
 
 
+def dtype_label(cfg: ModelConfig) -> str:
+    """Compute dtype of the step. fp8 models keep the small MLP tail in bf16
+    (models/ctr.py DCNv2: the cross layers + the first MLP layer, 97 % of the
+    FLOPs, run MX-fp8; fp32 accumulation everywhere)."""
+    if cfg.gemm_dtype == "fp8":
+        return "fp8 (e4m3 cross layers + first MLP layer, 97 % of FLOPs) + bf16 MLP tail"
+    return cfg.gemm_dtype
+
+
 def describe_model(cfg: ModelConfig) -> str:
     mlp = "-".join(str(d) for d in cfg.mlp_dims)
     if cfg.family == "dlrm":
@@ -488,7 +497,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
-            "dtype": cfg.gemm_dtype,
+            "dtype": dtype_label(cfg),
             "data": "synthetic (zipf feature ids over 2^40, uniform weights; random-init weights)",
             "config": {
                 "model": describe_model(cfg),

@@ -770,6 +770,58 @@ std::vector<torch::Tensor> cross_combine(torch::Tensor y, torch::Tensor x0, torc
   return {z, q, s, dot};
 }
 
+// One DCN-v2 cross layer, fp8 GEMM + LDS-staged cross epilogue in one launch:
+// z = bf16(x0 * bf16(q W^T * sx * sw + b) + xl) (want_z) and / or the cross
+// logit as partials dot[tn, m] = z[m, 256 tn .. +256] . head_w (the head sums
+// them). Same rounding as linear_fp8 (plain) + cross_combine.
+std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, torch::Tensor Wq, torch::Tensor sw,
+                                          c10::optional<torch::Tensor> bias, torch::Tensor x0, torch::Tensor xl,
+                                          bool want_z, c10::optional<torch::Tensor> head_w) {
+  check_dev(q, "q");
+  check_same_dev(q, Wq, "Wq");
+  TORCH_CHECK(q.scalar_type() == torch::kFloat8_e4m3fn && Wq.scalar_type() == torch::kFloat8_e4m3fn && q.dim() == 2 &&
+                  Wq.dim() == 2 && q.is_contiguous() && Wq.is_contiguous(),
+              "q [M, K] and Wq [N, K] must be contiguous e4m3");
+  const int64_t M = q.size(0), K = q.size(1), N = Wq.size(0);
+  TORCH_CHECK(Wq.size(1) == K && K % 128 == 0, "K mismatch or K % 128 != 0: q ", q.sizes(), " Wq ", Wq.sizes());
+  TORCH_CHECK(N % 8 == 0 && M < (int64_t(1) << 31), "N must be a multiple of 8");
+  for (auto* t : {&sx, &sw}) {
+    check_same_dev(q, *t, "scales");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->is_contiguous(), "scales must be contiguous fp32");
+  }
+  TORCH_CHECK(sx.numel() == M && sw.numel() == N, "sx [M], sw [N]");
+  if (bias) {
+    check_same_dev(q, *bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == N && bias->is_contiguous(),
+                "bias must be fp32 [N]");
+  }
+  for (auto* t : {&x0, &xl}) {
+    check_same_dev(q, *t, "x0/xl");
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->dim() == 2 && t->size(0) == M && t->size(1) == N &&
+                    t->is_contiguous(),
+                "x0/xl must be contiguous bf16 [M, N]");
+  }
+  const float* hw = nullptr;
+  if (head_w && head_w->defined()) {
+    check_same_dev(q, *head_w, "head_w");
+    TORCH_CHECK(head_w->scalar_type() == torch::kFloat32 && head_w->numel() == N && head_w->is_contiguous(),
+                "head_w must be fp32 [N]");
+    hw = head_w->data_ptr<float>();
+  }
+  TORCH_CHECK(want_z || hw, "nothing to produce");
+  c10::DeviceGuard g(q.device());
+  torch::Tensor z, dot;
+  if (want_z) z = torch::empty({M, N}, x0.options());
+  const int64_t tiles_n = (N + 255) / 256;
+  if (hw) dot = torch::empty({tiles_n, M}, x0.options().dtype(torch::kFloat32));
+  check_hip(dtfs::launch_cross_gemm_fp8(q.data_ptr(), K, Wq.data_ptr(), K, bias ? bias->data_ptr<float>() : nullptr,
+                                        sx.data_ptr<float>(), sw.data_ptr<float>(), want_z ? z.data_ptr() : nullptr,
+                                        N, x0.data_ptr(), xl.data_ptr(), N, hw, hw ? dot.data_ptr<float>() : nullptr,
+                                        M, int(M), int(N), int(K), cur_stream(q)),
+            "cross_gemm_fp8");
+  return {z, dot};
+}
+
 // ---------------------------------------------------------------- K7
 std::vector<torch::Tensor> sort_scores(torch::Tensor s, bool descending, int64_t k) {
   check_dev(s, "scores");
@@ -1079,6 +1131,8 @@ PYBIND11_MODULE(_hip, m) {
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
+  m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
+        py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,
         py::arg("k_pad") = 0, py::arg("head_w") = py::none(),
         "split DCN-v2 cross layer: z = x0*y + xl, optionally quantised (e4m3 + row scale) and/or dotted with head_w");

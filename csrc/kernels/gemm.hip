@@ -760,15 +760,119 @@ __device__ unsigned long long g_8ph_stamps[4096][8][4];
   } while (0)
 #endif
 
-template <bool FP8, typename OutT, bool PRE = false>
+// DCN-v2 cross layer epilogue of the 256x256 8-phase tile, staged through LDS
+// (XSTAGE): the fused cross epilogue in registers (store_acc_t, EPI_CROSS)
+// loads x0 / xl as 8-byte pieces of 16 rows per fragment, one latency-bound
+// round trip per column tile with no MFMA work left to hide it (215.6 vs
+// 124.7 us plain at 16384 x 2752 x 2816), which is why the split form (plain
+// GEMM + an HBM-bound combine pass over y, x0, xl) won in round 2. Here the
+// tile's y = bf16(acc * sa * sw + b) - the split form's y, bit for bit - goes
+// to LDS (the K loop's buffers are dead; 520-byte rows: the 16 rows of a
+// lane group's 8-byte writes land on 32 distinct banks), then every wave
+// streams whole rows: 32 lanes x 16 bytes = one 256-column row segment, x0 / xl
+// read fully coalesced with 4 rows in flight per lane, z = bf16(x0 * y + xl)
+// written back as 16-byte vectors and / or dotted with head_w into one
+// partial logit per (column tile, row): dot[tn * ldd + m]. No y round trip
+// through HBM and no separate combine pass.
+constexpr int kXsLdy = 520;  // staged row pitch (bytes): 256 bf16 + 8
+constexpr int kXsBytes = 256 * kXsLdy;
+
+template <bool FP8>
+__device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], uint8_t* __restrict__ ys, int m0,
+                                                      int n0, int tn, int wr, int wc, int wid, int lane, int M, int N,
+                                                      const float* __restrict__ bias, const float* __restrict__ sa,
+                                                      const float* __restrict__ sw, bf16* __restrict__ Z,
+                                                      int64_t ldz, const bf16* __restrict__ X0,
+                                                      const bf16* __restrict__ XL, int64_t ldx,
+                                                      const float* __restrict__ hw, float* __restrict__ dot,
+                                                      int64_t ldd) {
+  const int fr = lane & 15, fq = lane >> 4;
+  __syncthreads();  // both wave groups are past their last K-loop LDS read
+  float sam[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sam[i] = (FP8 && sa) ? sa[min(m0 + 128 * wr + 16 * i + fr, M - 1)] : 1.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 64 * wc + 16 * j + 4 * fq;  // tile column of this lane's 4 values
+    const int nc = min(n0 + c, N - 4);
+    const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
+    if (FP8 && sw) s4 = *reinterpret_cast<const f32x4*>(sw + nc);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = acc[i][j][r];
+        if constexpr (FP8) x *= s4[r] * sam[i];
+        o[r] = f2bf(x + b4[r]);
+      }
+      *reinterpret_cast<bf16x4*>(ys + (128 * wr + 16 * i + fr) * kXsLdy + c * 2) = o;
+    }
+  }
+  __syncthreads();
+  // rows: wave wid owns tile rows 32 wid .. +32, two per pass (lanes 0-31 / 32-63)
+  const int col = (lane & 31) * 8;
+  const int n = n0 + col;
+  const bool col_ok = n < N;  // N % 8 == 0: a lane's 8 columns exist together
+  const int nr = min(n, N - 8);
+  const bool same = XL == X0;
+  float w8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) w8[e] = 0.f;
+  if (hw && col_ok) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(hw + n);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(hw + n + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w8[e] = a[e], w8[e + 4] = b[e];
+  }
+  constexpr int P = 4;  // rows in flight per lane
+#pragma unroll 1
+  for (int p0 = 0; p0 < 16; p0 += P) {
+    bf16x8 x0v[P], xlv[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int64_t m = min(m0 + 32 * wid + 2 * (p0 + u) + (lane >> 5), M - 1);
+      x0v[u] = *reinterpret_cast<const bf16x8*>(X0 + m * ldx + nr);
+      if (!same) xlv[u] = *reinterpret_cast<const bf16x8*>(XL + m * ldx + nr);
+    }
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int row = 32 * wid + 2 * (p0 + u) + (lane >> 5);
+      const int m = m0 + row;
+      const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(ys + row * kXsLdy + col * 2);
+      const bf16x8 l8 = same ? x0v[u] : xlv[u];
+      bf16x8 z8;
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        z8[e] = f2bf(bf2f(x0v[u][e]) * bf2f(y8[e]) + bf2f(l8[e]));
+        d += bf2f(z8[e]) * w8[e];
+      }
+      if (Z && col_ok && m < M) *reinterpret_cast<bf16x8*>(Z + int64_t(m) * ldz + n) = z8;
+      if (dot) {
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        d += __shfl_xor(d, 8, 64);
+        d += __shfl_xor(d, 16, 64);
+        if ((lane & 31) == 0 && m < M) dot[int64_t(tn) * ldd + m] = d;
+      }
+    }
+  }
+}
+
+template <bool FP8, typename OutT, bool PRE = false, bool XSTAGE = false>
 __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
-    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi) {
+    int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi,
+    const float* __restrict__ hw = nullptr, float* __restrict__ dot = nullptr, int64_t ldd = 0) {
   constexpr int BM = 256, BN = 256;
   constexpr int EB = FP8 ? 1 : 2;
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+  constexpr int SMEM = (XSTAGE && kXsBytes > 2 * BUF) ? kXsBytes : 2 * BUF;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   DTFS_STAMP(0);
 
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
@@ -962,7 +1066,13 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
   DTFS_STAMP(2);
 
-  store_acc_t<FP8, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  if constexpr (XSTAGE) {
+    static_assert(sizeof(OutT) == 2, "the staged cross epilogue writes bf16 z");
+    cross_staged_epilogue<FP8>(acc, smem, m0, n0, tn, wr, wc, wid, lane, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, hw,
+                               dot, ldd);
+  } else {
+    store_acc_t<FP8, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
+  }
   DTFS_STAMP(3);
 }
 
@@ -972,7 +1082,8 @@ static void launch_8ph(const void* A, int64_t lda, const void* W, int64_t ldw, c
                        int N, int K, int epi, hipStream_t st) {
   const int grid = ((M + 255) / 256) * ((N + 255) / 256);
   hipLaunchKernelGGL((gemm_8ph_kernel<FP8, OutT, PRE>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(A), lda,
-                     static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi);
+                     static_cast<const uint8_t*>(W), ldw, bias, sa, sw, C, ldc, X0, XL, ldx, M, N, K, epi,
+                     static_cast<const float*>(nullptr), static_cast<float*>(nullptr), int64_t(0));
 }
 
 // ---------------------------------------------------------------------------
@@ -1644,6 +1755,22 @@ hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_
   else if (fm_part) DTFS_GG(1);
   else DTFS_GG(0);
 #undef DTFS_GG
+  return hipGetLastError();
+}
+
+hipError_t launch_cross_gemm_fp8(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                                 const float* sa, const float* sw, void* Z, int64_t ldz, const void* X0,
+                                 const void* XL, int64_t ldx, const float* hw, float* dot, int64_t ldd, int M, int N,
+                                 int K, hipStream_t st) {
+  if (M == 0 || N == 0) return hipSuccess;
+  if (K % 128 != 0 || N % 8 != 0 || N < 8 || lda < K || ldw < K || !X0 || !XL || ldx < N || (!Z && !dot) ||
+      (Z && (ldz < N || ldz % 8 != 0)) || ldx % 8 != 0 || (dot && (!hw || ldd < M)))
+    return hipErrorInvalidValue;
+  const int grid = ((M + 255) / 256) * ((N + 255) / 256);
+  hipLaunchKernelGGL((gemm_8ph_kernel<true, bf16, true, true>), dim3(grid), dim3(512), 0, st,
+                     static_cast<const uint8_t*>(A), lda, static_cast<const uint8_t*>(W), ldw, bias, sa, sw,
+                     static_cast<bf16*>(Z), ldz, static_cast<const bf16*>(X0), static_cast<const bf16*>(XL), ldx, M, N,
+                     K, int(EPI_CROSS), hw, dot, ldd);
   return hipGetLastError();
 }
 

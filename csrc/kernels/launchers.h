@@ -170,6 +170,16 @@ hipError_t launch_cross_combine(const void* y, const void* x0, const void* xl, i
                                 int64_t ldz, void* q, int64_t ldq, float* scale, int Kq, const float* head_w,
                                 float* dot, hipStream_t st);
 
+// DCN-v2 cross layer in one launch (fp8 8-phase GEMM + LDS-staged cross
+// epilogue): y = (A W^T) * sa * sw + b, z = bf16(x0 * bf16(y) + xl) written to
+// Z (optional) and / or dotted with hw into one partial logit per 256-column
+// tile: dot[tn * ldd + m], tn < ceil(N / 256). A: e4m3 [M][K] (K % 128 == 0),
+// N % 8 == 0.
+hipError_t launch_cross_gemm_fp8(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                                 const float* sa, const float* sw, void* Z, int64_t ldz, const void* X0,
+                                 const void* XL, int64_t ldx, const float* hw, float* dot, int64_t ldd, int M, int N,
+                                 int K, hipStream_t st);
+
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();
 hipError_t launch_sort_scores(const float* in, int n, bool descending, float* out, int64_t* perm, int k_out,

@@ -291,14 +291,25 @@ class DCNv2(CTRModel):
             # 8-phase tile runs it) + one combine pass that writes z = x0*y + xl,
             # quantises it for the next layer and, for the last layer, reduces
             # the cross logit instead of writing z (profiles/dcn_v2_split_kernels.md)
+            # Full-chip steps: the combine rides on the GEMM as an LDS-staged
+            # epilogue (ops.cross_gemm_fp8; no y round trip), the last layer
+            # writing only per-column-tile partial cross logits; z is quantised
+            # for the next layer by one quant_rows pass
             xl, (q, sx) = x0, q0
+            fused = ops.cross_gemm_fits(x0.shape[0], self.d) and q.shape[1] % 128 == 0
             for i in range(L):
                 layer = self.cross[i]
-                y = ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias)  # plain bf16 epilogue
                 last = i == L - 1
-                z, q, sx, cross_logit = ops.cross_combine(y, x0, xl, want_z=not last,
-                                                          k_pad=0 if last else ops.FP8_K_PAD,
-                                                          head_w=self.head_wc if last else None)
+                if fused:
+                    z, cross_logit = ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, xl,
+                                                        want_z=not last, head_w=self.head_wc if last else None)
+                    if not last:
+                        q, sx = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
+                else:
+                    y = ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias)  # plain bf16 epilogue
+                    z, q, sx, cross_logit = ops.cross_combine(y, x0, xl, want_z=not last,
+                                                              k_pad=0 if last else ops.FP8_K_PAD,
+                                                              head_w=self.head_wc if last else None)
                 xl = z
         else:
             xl, xq = x0, q0

@@ -278,6 +278,36 @@ def cross_combine(y: torch.Tensor, x0: torch.Tensor, xl: torch.Tensor, want_z: b
     return (zb if want_z else None, q, s, d)
 
 
+CROSS_TILE = 256  # column tile of the fused cross GEMM: one partial logit per tile
+
+
+def cross_gemm_fits(M: int, N: int) -> bool:
+    """The fused cross GEMM runs 256x256 tiles: worth it once they fill the chip
+    (smaller steps take linear_fp8 + cross_combine on smaller tiles)."""
+    return -(-M // 256) * -(-N // 256) >= 256 and N % 8 == 0
+
+
+def cross_gemm_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
+                   b: Optional[torch.Tensor], x0: torch.Tensor, xl: torch.Tensor, want_z: bool = True,
+                   head_w: Optional[torch.Tensor] = None):
+    """One DCN-v2 cross layer in one launch (csrc/kernels/gemm.hip
+    cross_staged_epilogue): y = bf16(xq Wq^T * sx * sw + b), z = bf16(x0 * y + xl).
+    Returns (z or None, dot or None) with dot = fp32 [ceil(N / 256), M] partial
+    cross logits z[:, 256 t:256 t + 256] . head_w[256 t:256 t + 256] (a head
+    ``extra``). The same rounding as linear_fp8 + cross_combine."""
+    if xq.is_cuda:
+        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w)
+        return (z if want_z else None), (d if head_w is not None else None)
+    y = linear_fp8(xq, sx, Wq, sw, b)
+    zb = (x0.float() * y.float() + xl.float()).to(torch.bfloat16)
+    d = None
+    if head_w is not None:
+        N = zb.shape[1]
+        d = torch.stack([zb[:, t:t + CROSS_TILE].float() @ head_w[t:t + CROSS_TILE].float()
+                         for t in range(0, N, CROSS_TILE)])
+    return (zb if want_z else None), d
+
+
 def linear_fp8(xq: torch.Tensor, sx: Optional[torch.Tensor], Wq: torch.Tensor, sw: torch.Tensor,
                b: Optional[torch.Tensor] = None, act: str = "none", out_f32: bool = False,
                x0: Optional[torch.Tensor] = None, xl: Optional[torch.Tensor] = None,

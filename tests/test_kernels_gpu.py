@@ -320,6 +320,59 @@ def test_dcn_v2_split_cross_matches_fused(cuda, monkeypatch):
     assert (a - b).abs().max().item() < 0.02
 
 
+@pytest.mark.parametrize("M,N,same", [(700, 2752, False), (256, 264, True), (1030, 512, False)])
+def test_cross_gemm_fp8_staged_epilogue(cuda, M, N, same):
+    """One-launch DCN-v2 cross layer (8-phase fp8 GEMM + LDS-staged cross
+    epilogue) == plain fp8 GEMM + cross_combine (z bit for bit, per-tile partial
+    logits summing to the combine's dot), and close to the fp32 CPU reference;
+    ragged M / N tiles, x_l = x0 (first layer)."""
+    g = torch.Generator().manual_seed(M + N)
+    K = -(-N // 128) * 128
+    x0 = (torch.randn(M, N, generator=g) * 0.5).to(torch.bfloat16)
+    xl = x0 if same else (torch.randn(M, N, generator=g) * 0.5).to(torch.bfloat16)
+    W = torch.randn(N, N, generator=g) / N ** 0.5
+    Wq, sw = ops.quant_rows_fp8(W.to(torch.bfloat16), 128)
+    b = torch.randn(N, generator=g) * 0.1
+    q, sx = ops.quant_rows_fp8(xl, 128)
+    hw = torch.randn(N, generator=g) * 0.05
+    dq, dsx, dW, dsw, db, dx0, dhw = (t.to(cuda) for t in (q, sx, Wq, sw, b, x0, hw))
+    dxl = dx0 if same else xl.to(cuda)
+    assert q.shape[1] == K and Wq.shape == (N, K)
+    z, d = ops.cross_gemm_fp8(dq, dsx, dW, dsw, db, dx0, dxl, want_z=True, head_w=dhw)
+    y = ops.linear_fp8(dq, dsx, dW, dsw, db)
+    zr, _, _, dr = ops.cross_combine(y, dx0, dxl, True, 0, dhw)
+    z2, d2 = ops.cross_gemm_fp8(dq, dsx, dW, dsw, db, dx0, dxl, want_z=False, head_w=dhw)
+    z3, d3 = ops.cross_gemm_fp8(dq, dsx, dW, dsw, db, dx0, dxl, want_z=True)
+    torch.cuda.synchronize()
+    assert d.shape == (-(-N // 256), M) and z2 is None and d3 is None
+    assert torch.equal(z.cpu(), zr.cpu()) and torch.equal(z3.cpu(), zr.cpu())
+    _close(d.sum(0), dr, 1e-4, 1e-4, "partial logits")
+    assert torch.equal(d2.cpu(), d.cpu())
+    zc, dc = ops.cross_gemm_fp8(q, sx, Wq, sw, b, x0, xl, want_z=True, head_w=hw)
+    _close(z, zc, 2e-2, 2e-2, "z vs CPU")
+    _close(d, dc, 2e-2, 2e-2, "dot vs CPU")
+
+
+def test_dcn_v2_fused_cross_matches_split(cuda, monkeypatch):
+    """A full-chip DCN-v2 fp8 step (6144 rows: 264 cross tiles) through the
+    one-launch cross layers vs the split GEMM + combine path, same weights."""
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
+
+    cfg = ModelConfig(family="dcn_v2", vocab_size=20000, embed_dim=64, num_fields=43, mlp_dims=(1024, 512, 256),
+                      num_cross_layers=3, gemm_dtype="fp8")
+    m = build_model(cfg, cuda)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 1 << 30, (6144, 43), generator=g).to(cuda)
+    wts = torch.rand(6144, 43, generator=g).to(cuda)
+    assert ops.cross_gemm_fits(6144, 2752)
+    a = m(ids, wts)
+    monkeypatch.setattr(ops, "cross_gemm_fits", lambda M, N: False)
+    b = m(ids, wts)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() < 1e-3
+
+
 def test_cross_v2_epilogue(cuda):
     M, d = 130, 256
     x0 = torch.randn(M, d).to(torch.bfloat16)

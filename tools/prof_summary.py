@@ -24,7 +24,8 @@ def _short(name: str) -> str:
     return name[:90]
 
 
-def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "", from_kernel: str = "") -> str:
+def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "", from_kernel: str = "",
+              step_kernel: str = "", min_us: float = 0.0) -> str:
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end, duration from kernels order by start"))
     copies = list(c.execute("select name, start, end, duration, size from memory_copies order by start"))
@@ -65,7 +66,46 @@ def summarize(db: str, steps: int = 0, title: str = "", last_kernel: str = "", f
         if len(ends) > 4:
             period = statistics.median((b[1] - a[1]) / 1e3 for a, b in zip(ends, ends[1:]))
             out += ["", f"steady-state period between `{last_kernel}` launches: {period:.1f} us (median)"]
+    if step_kernel:
+        out += step_timeline(rows, copies, step_kernel, min_us)
     return "\n".join(out) + "\n"
+
+
+def step_timeline(rows, copies, step_kernel: str, min_us: float) -> list:
+    """Back-to-back steps: segment the kernel stream at every launch of
+    ``step_kernel`` (the step's first kernel) and, for the pairs of consecutive
+    segments whose ``step_kernel`` ran at least ``min_us`` (full-size steps),
+    report the start-to-start period, the kernel time inside it and the idle
+    rest - GPU-bound when idle ~ 0, host / copy-bound otherwise."""
+    starts = [i for i, r in enumerate(rows) if step_kernel in r[0]]
+    per, busy, idle, h2d = [], [], [], []
+    for a, b in zip(starts, starts[1:]):
+        if rows[a][3] / 1e3 < min_us or rows[b][3] / 1e3 < min_us:
+            continue
+        t0, t1 = rows[a][1], rows[b][1]
+        # union of kernel intervals in [t0, t1)
+        ivs = sorted((max(s, t0), min(e, t1)) for _, s, e, _ in rows[a:b + 1] if s < t1)
+        tot, cur_s, cur_e = 0, None, None
+        for s, e in ivs:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    tot += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            tot += cur_e - cur_s
+        per.append((t1 - t0) / 1e3)
+        busy.append(tot / 1e3)
+        idle.append((t1 - t0 - tot) / 1e3)
+        h2d.append(sum((min(e, t1) - max(s, t0)) for _, s, e, _, _ in copies if s < t1 and e > t0) / 1e3)
+    if not per:
+        return ["", f"no back-to-back full steps of `{step_kernel}` (>= {min_us} us)"]
+    med = statistics.median
+    return ["", f"back-to-back full steps ({len(per)} pairs, step starts at `{step_kernel}` >= {min_us} us): "
+            f"period {med(per):.1f} us, kernels busy {med(busy):.1f} us, GPU idle {med(idle):.1f} us, "
+            f"copy time inside the period {med(h2d):.1f} us (medians; p10/p90 period "
+            f"{sorted(per)[len(per) // 10]:.1f} / {sorted(per)[9 * len(per) // 10]:.1f} us)"]
 
 
 def main():
@@ -75,8 +115,10 @@ def main():
     ap.add_argument("--title", default="")
     ap.add_argument("--last-kernel", default="", help="substring of the step's final kernel, for the step period")
     ap.add_argument("--from-kernel", default="", help="ignore everything before the first kernel matching this")
+    ap.add_argument("--step-kernel", default="", help="substring of the step's FIRST kernel: step timeline")
+    ap.add_argument("--min-us", type=float, default=0.0, help="full-size steps: --step-kernel at least this long")
     a = ap.parse_args()
-    print(summarize(a.db, a.steps, a.title, a.last_kernel, a.from_kernel), end="")
+    print(summarize(a.db, a.steps, a.title, a.last_kernel, a.from_kernel, a.step_kernel, a.min_us), end="")
 
 
 if __name__ == "__main__":
