@@ -117,13 +117,13 @@ def parse_args():
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--shard-tables", action="store_true",
                     help="dlrm: shard the tables even on one GPU (exercises the embedding-exchange step program)")
-    ap.add_argument("--small-buckets", default="2048",
+    ap.add_argument("--small-buckets", default=None,
                     help="extra padding buckets (rows per GPU) below the full step, so a lightly loaded server "
                          "runs a step sized to what is queued (TF-Serving allowed_batch_sizes; at N > 1 every "
                          "rank agrees on the largest bucket any rank needs); '' = only the full step. 2048: "
                          "bench/bucket_cost.py on MI355X - a 512- or 1024-row step costs 64-66 us pipelined "
                          "(launch-chain bound), a 2048-row one 79 us, so smaller buckets only saturate at 20k QPS "
-                         "of 512-row requests")
+                         "of 512-row requests. Default 2048; dcn_v2 (a 0.6 ms full step) 2048,4096,8192")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--slots", type=int, default=4, help="step slots per rank (steps in flight)")
     ap.add_argument("--batch-timeout-us", type=int, default=200)
@@ -209,6 +209,10 @@ def build(a, ctx):
     if sharded and a.mode != "local":
         raise SystemExit("dlrm with sharded tables runs --mode local (the embedding exchange is the fan-out)")
     mode = a.mode if world > 1 else ("alltoall" if a.force_fanout else "local")
+    if a.small_buckets is None:
+        # a full DCN-v2 step is 0.6 ms: intermediate buckets keep a lightly
+        # loaded server from padding every step to the full one
+        a.small_buckets = "2048,4096,8192" if cfg.family == "dcn_v2" else "2048"
     small = [int(x) for x in a.small_buckets.split(",") if x.strip()] if a.small_buckets else []
     # an all-to-all splits every rank's rows evenly over the GPUs
     small = [b for b in small if mode != "alltoall" or b % world == 0]

@@ -771,14 +771,12 @@ std::vector<torch::Tensor> cross_combine(torch::Tensor y, torch::Tensor x0, torc
 }
 
 // One DCN-v2 cross layer, fp8 GEMM + LDS-staged cross epilogue in one launch:
-// z = bf16(x0 * bf16(q W^T * scale_q * sw + b) + xl) (want_z), the cross logit
-// as partials dot[tn, m] = z[m, 256 tn .. +256] . head_w (the head sums them)
-// and / or (emit_q) z as the next layer's MX-256 operand (e4m3 [M, Kq] + E8M0
-// [M, ceil(N / 256)]). scale_q: fp32 [M] row scales, or uint8 [M, nblk] MX-256
-// scales (a previous layer's emitted operand). Returns (z, dot, q, sq).
+// z = bf16(x0 * bf16(q W^T * sx * sw + b) + xl) (want_z) and / or the cross
+// logit as partials dot[tn, m] = z[m, 256 tn .. +256] . head_w (the head sums
+// them). Same rounding as linear_fp8 (plain) + cross_combine.
 std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, torch::Tensor Wq, torch::Tensor sw,
                                           c10::optional<torch::Tensor> bias, torch::Tensor x0, torch::Tensor xl,
-                                          bool want_z, c10::optional<torch::Tensor> head_w, bool emit_q) {
+                                          bool want_z, c10::optional<torch::Tensor> head_w) {
   check_dev(q, "q");
   check_same_dev(q, Wq, "Wq");
   TORCH_CHECK(q.scalar_type() == torch::kFloat8_e4m3fn && Wq.scalar_type() == torch::kFloat8_e4m3fn && q.dim() == 2 &&
@@ -787,18 +785,11 @@ std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, tor
   const int64_t M = q.size(0), K = q.size(1), N = Wq.size(0);
   TORCH_CHECK(Wq.size(1) == K && K % 128 == 0, "K mismatch or K % 128 != 0: q ", q.sizes(), " Wq ", Wq.sizes());
   TORCH_CHECK(N % 8 == 0 && M < (int64_t(1) << 31), "N must be a multiple of 8");
-  check_same_dev(q, sx, "scale_q");
-  check_same_dev(q, sw, "sw");
-  TORCH_CHECK(sw.scalar_type() == torch::kFloat32 && sw.is_contiguous() && sw.numel() == N, "sw must be fp32 [N]");
-  const bool mx_in = sx.scalar_type() == torch::kUInt8;
-  if (mx_in) {
-    TORCH_CHECK(sx.dim() == 2 && sx.size(0) == M && sx.size(1) >= (K + 255) / 256 && sx.stride(1) == 1 &&
-                    K <= 4096,
-                "MX-256 scales must be uint8 [M, >= ceil(K / 256)] (K <= 4096)");
-  } else {
-    TORCH_CHECK(sx.scalar_type() == torch::kFloat32 && sx.is_contiguous() && sx.numel() == M,
-                "row scales must be fp32 [M]");
+  for (auto* t : {&sx, &sw}) {
+    check_same_dev(q, *t, "scales");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->is_contiguous(), "scales must be contiguous fp32");
   }
+  TORCH_CHECK(sx.numel() == M && sw.numel() == N, "sx [M], sw [N]");
   if (bias) {
     check_same_dev(q, *bias, "bias");
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == N && bias->is_contiguous(),
@@ -817,29 +808,19 @@ std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, tor
                 "head_w must be fp32 [N]");
     hw = head_w->data_ptr<float>();
   }
-  TORCH_CHECK(want_z || hw || emit_q, "nothing to produce");
+  TORCH_CHECK(want_z || hw, "nothing to produce");
   c10::DeviceGuard g(q.device());
   const int64_t tiles_n = (N + 255) / 256;
-  torch::Tensor z, dot, qo, sqo;
+  torch::Tensor z, dot;
   if (want_z) z = torch::empty({M, N}, x0.options());
   if (hw) dot = torch::empty({tiles_n, M}, x0.options().dtype(torch::kFloat32));
-  const int64_t kq = (N + 127) / 128 * 128;
-  if (emit_q) {
-    qo = torch::empty({M, kq}, q.options());
-    sqo = torch::empty({M, tiles_n}, q.options().dtype(torch::kUInt8));
-  }
   dtfs::CrossGemmArgs a;
   a.A = q.data_ptr();
   a.lda = K;
   a.W = Wq.data_ptr();
   a.ldw = K;
   a.bias = bias ? bias->data_ptr<float>() : nullptr;
-  if (mx_in) {
-    a.sa_blk = sx.data_ptr<uint8_t>();
-    a.ld_sa_blk = sx.stride(0);
-  } else {
-    a.sa = sx.data_ptr<float>();
-  }
+  a.sa = sx.data_ptr<float>();
   a.sw = sw.data_ptr<float>();
   a.Z = want_z ? z.data_ptr() : nullptr;
   a.ldz = N;
@@ -849,18 +830,11 @@ std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, tor
   a.hw = hw;
   a.dot = hw ? dot.data_ptr<float>() : nullptr;
   a.ldd = M;
-  if (emit_q) {
-    a.q = qo.data_ptr();
-    a.ldq = kq;
-    a.kq = int(kq);
-    a.sq = sqo.data_ptr<uint8_t>();
-    a.ldsq = tiles_n;
-  }
   a.M = int(M);
   a.N = int(N);
   a.K = int(K);
   check_hip(dtfs::launch_cross_gemm_fp8(a, cur_stream(q)), "cross_gemm_fp8");
-  return {z, dot, qo, sqo};
+  return {z, dot};
 }
 
 // ---------------------------------------------------------------- K7
@@ -1173,8 +1147,7 @@ PYBIND11_MODULE(_hip, m) {
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
-        py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none(),
-        py::arg("emit_q") = false);
+        py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,
         py::arg("k_pad") = 0, py::arg("head_w") = py::none(),
         "split DCN-v2 cross layer: z = x0*y + xl, optionally quantised (e4m3 + row scale) and/or dotted with head_w");

@@ -66,21 +66,6 @@ __device__ __forceinline__ f32x4 mx_mfma_sb(const i32x8& a, const i32x8& b, cons
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, scale_b);
 }
 
-// Same, the b scale taken from byte `sel` (0..3, folded to a constant in
-// unrolled loops) of a VGPR holding four rows' scale bytes
-template <int SEL>
-__device__ __forceinline__ f32x4 mx_mfma_sb_sel(const i32x8& a, const i32x8& b, const f32x4& c, int scales) {
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, SEL, scales);
-}
-__device__ __forceinline__ f32x4 mx_mfma_sb_byte(const i32x8& a, const i32x8& b, const f32x4& c, int scales, int sel) {
-  switch (sel) {
-    case 0: return mx_mfma_sb_sel<0>(a, b, c, scales);
-    case 1: return mx_mfma_sb_sel<1>(a, b, c, scales);
-    case 2: return mx_mfma_sb_sel<2>(a, b, c, scales);
-    default: return mx_mfma_sb_sel<3>(a, b, c, scales);
-  }
-}
-
 // Every kernel below issues its MFMAs as D = W_frag x A_frag^T, i.e. it
 // computes the TRANSPOSED 16x16 output tile: with the C/D layout (col =
 // lane & 15, row = 4 * (lane >> 4) + r) a lane then holds C[m = fr][n = 4 fq
@@ -791,29 +776,12 @@ __device__ unsigned long long g_8ph_stamps[4096][8][4];
 // through HBM and no separate combine pass.
 constexpr int kXsLdy = 520;  // staged row pitch (bytes): 256 bf16 + 8
 constexpr int kXsBytes = 256 * kXsLdy;
-// "MX-256" activations between cross layers: e4m3 values + one E8M0 scale per
-// (row, 256-column block) - the producer tile's whole row segment, so its
-// epilogue finds the block maximum with 5 lane shuffles, and two 128-deep K
-// tiles of the consumer, which applies it through the block-scaled MFMA's own
-// scale operand (no per-row scale, no quant_rows pass over z). The consumer
-// stages its row panel of scale bytes in LDS once: [blk][wr][fr][qm * 4 + i]
-// = the 8 A rows a lane's fragments hold, one 8-byte read per block.
-constexpr int kMx256MaxBlk = 16;  // K <= 4096
-constexpr int kMx256Panel = kMx256MaxBlk * 256;
-
-// 32-lane (half-wave) reductions with the result in every lane: DPP within
-// each 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror), one
+// 32-lane (half-wave) sum with the result in every lane: DPP within each
+// 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror), one
 // ds_bpermute across the two rows
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float max32(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x141>(v));
-  v = fmaxf(v, dppf<0x140>(v));
-  return fmaxf(v, __shfl_xor(v, 16, 64));
 }
 __device__ __forceinline__ float sum32(float v) {
   v += dppf<0xB1>(v);
@@ -822,29 +790,12 @@ __device__ __forceinline__ float sum32(float v) {
   v += dppf<0x140>(v);
   return v + __shfl_xor(v, 16, 64);
 }
-// E8M0 exponent of a block: the smallest e with amax / 2^e <= 448 (e4m3 max),
-// from the float's bits (amax = 1.m x 2^(E - 127): e = E - 135, + 1 when
-// 1.m > 1.75), 0 for an all-zero block; clamped to [-126, 126]
-__device__ __forceinline__ int e8m0_exp(float amax) {
-  const uint32_t b = __float_as_uint(amax);
-  if (amax <= 0.f) return 0;
-  const int e = int(b >> 23) - 135 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
-  return max(-126, min(126, e));
-}
-
 // The cross GEMM's extra operands (one struct: the 8-phase kernel's argument
 // list stays the dense GEMM's otherwise).
 struct XsArgs {
   const float* hw = nullptr;  // head weights [N]: per-tile partial logits ...
   float* dot = nullptr;       // ... dot[tn * ldd + m]
   int64_t ldd = 0;
-  uint8_t* q = nullptr;  // MX-256 out: e4m3 [M][ldq], columns [N, kq) zero ...
-  int64_t ldq = 0;
-  int kq = 0;
-  uint8_t* sq = nullptr;  // ... + E8M0 [M][ldsq] per 256-column block
-  int64_t ldsq = 0;
-  const uint8_t* sa_blk = nullptr;  // MX-256 A operand scales [M][ld_sa_blk]
-  int64_t ld_sa_blk = 0;
 };
 
 template <bool FP8>
@@ -883,7 +834,6 @@ __device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], 
   const int col = (lane & 31) * 8;
   const int n = n0 + col;
   const bool col_ok = n < N;  // N % 8 == 0: a lane's 8 columns exist together
-  const bool q_ok = xs.q && n < xs.kq;  // K padding [N, kq) of the next layer's operand: zeros
   const int nr = min(n, N - 8);
   const bool same = XL == X0;
   float w8[8];
@@ -912,69 +862,31 @@ __device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], 
       const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(ys + row * kXsLdy + col * 2);
       const bf16x8 l8 = same ? x0v[u] : xlv[u];
       bf16x8 z8;
-      float d = 0.f, amax = 0.f;
+      float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        z8[e] = col_ok ? f2bf(bf2f(x0v[u][e]) * bf2f(y8[e]) + bf2f(l8[e])) : f2bf(0.f);
+        z8[e] = f2bf(bf2f(x0v[u][e]) * bf2f(y8[e]) + bf2f(l8[e]));
         d += bf2f(z8[e]) * w8[e];
-        amax = fmaxf(amax, fabsf(bf2f(z8[e])));
       }
       if (Z && col_ok && m < M) *reinterpret_cast<bf16x8*>(Z + int64_t(m) * ldz + n) = z8;
       if (xs.dot) {
         d = sum32(d);
         if ((lane & 31) == 0 && m < M) xs.dot[int64_t(tn) * xs.ldd + m] = d;
       }
-      if (xs.q) {
-        // block maximum over the row segment's 32 lanes -> E8M0 exponent
-        const int ex = e8m0_exp(max32(amax));
-        const float inv = __uint_as_float(uint32_t(127 - ex) << 23);  // 2^-ex
-        if (q_ok && m < M) {
-          int lo = 0, hi = 0;
-          lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(z8[0]) * inv, bf2f(z8[1]) * inv, lo, false);
-          lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(z8[2]) * inv, bf2f(z8[3]) * inv, lo, true);
-          hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(z8[4]) * inv, bf2f(z8[5]) * inv, hi, false);
-          hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(z8[6]) * inv, bf2f(z8[7]) * inv, hi, true);
-          *reinterpret_cast<int2*>(xs.q + int64_t(m) * xs.ldq + n) = make_int2(lo, hi);
-          if ((lane & 31) == 0) xs.sq[int64_t(m) * xs.ldsq + tn] = uint8_t(ex + 127);
-        }
-      }
     }
   }
 }
 
-// MX-256 A operand (gemm_8ph_kernel MXA): the M tile's scale bytes into the
-// LDS panel (layout above). Issued before the prologue's DMAs; the ds_writes
-// wait only for these loads (in-order vmcnt), and the prologue's barrier
-// (after an lgkmcnt(0)) publishes them.
-__device__ __forceinline__ void mx256_panel_load(uint8_t* __restrict__ panel, const uint8_t* __restrict__ sab,
-                                                 int64_t ld, int m0, int M, int nblk) {
-  uint8_t v[kMx256Panel / 512];
-#pragma unroll
-  for (int u = 0; u < kMx256Panel / 512; ++u) {
-    const int idx = threadIdx.x + u * 512;
-    const int row = idx & 255, blk = idx >> 8;
-    v[u] = blk < nblk ? sab[int64_t(min(m0 + row, M - 1)) * ld + blk] : uint8_t(127);
-  }
-#pragma unroll
-  for (int u = 0; u < kMx256Panel / 512; ++u) {
-    const int idx = threadIdx.x + u * 512;
-    const int row = idx & 255, blk = idx >> 8;
-    const int wr = row >> 7, qm = (row >> 6) & 1, i = (row >> 4) & 3, fr = row & 15;
-    panel[((blk * 2 + wr) * 16 + fr) * 8 + qm * 4 + i] = v[u];
-  }
-}
-
-template <bool FP8, typename OutT, bool PRE = false, bool XSTAGE = false, bool MXA = false>
+template <bool FP8, typename OutT, bool PRE = false, bool XSTAGE = false>
 __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
     const float* __restrict__ bias, const float* __restrict__ sa, const float* __restrict__ sw, OutT* __restrict__ C,
     int64_t ldc, const bf16* __restrict__ X0, const bf16* __restrict__ XL, int64_t ldx, int M, int N, int K, int epi,
     const XsArgs xs) {
-  static_assert(!MXA || FP8, "MX-256 scales are an fp8 operand feature");
   constexpr int BM = 256, BN = 256;
   constexpr int EB = FP8 ? 1 : 2;
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
-  constexpr int KLOOP = 2 * BUF + (MXA ? kMx256Panel : 0);
+  constexpr int KLOOP = 2 * BUF;
   constexpr int SMEM = (XSTAGE && kXsBytes > KLOOP) ? kXsBytes : KLOOP;
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   DTFS_STAMP(0);
@@ -1035,16 +947,6 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
 
   // prologue: tile 0 whole + tile 1's Aq0, Bq0 (staged at phases -2, -1 of the
   // steady-state schedule below)
-  uint8_t* const panel = smem + 2 * BUF;  // MXA: the M tile's MX-256 scale bytes
-  uint8_t pv[MXA ? kMx256Panel / 512 : 1];
-  if constexpr (MXA) {  // fetched ahead of the DMAs, written to LDS behind them
-    const int nblk = (nk + 1) / 2;
-#pragma unroll
-    for (int u = 0; u < kMx256Panel / 512; ++u) {
-      const int idx = threadIdx.x + u * 512, row = idx & 255, blk = idx >> 8;
-      pv[u] = blk < nblk ? xs.sa_blk[int64_t(min(m0 + row, M - 1)) * xs.ld_sa_blk + blk] : uint8_t(127);
-    }
-  }
   stage_a(0, 0);
   stage_b(0, 0);
   stage_b(1, 0);
@@ -1052,17 +954,6 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   if (nk > 1) {
     stage_a(0, 1);
     stage_b(0, 1);
-  }
-  if constexpr (MXA) {
-#pragma unroll
-    for (int u = 0; u < kMx256Panel / 512; ++u) {
-      const int idx = threadIdx.x + u * 512, row = idx & 255, blk = idx >> 8;
-      const int pr = row >> 7, pq = (row >> 6) & 1, pi = (row >> 4) & 3, pf = row & 15;
-      panel[((blk * 2 + pr) * 16 + pf) * 8 + pq * 4 + pi] = pv[u];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  if (nk > 1) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1114,16 +1005,6 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   // the scheduler sinks every (register-only) scaled fp8 MFMA of the K tile
   // past the phase barriers to the end of the iteration (seen in the gfx950
   // ISA), which serialises the two wave groups instead of overlapping them
-  // MXA: this K tile's scale bytes, [qm] = rows of A[qm] fragments 0..3 (one
-  // byte each), read with the tile's first fragments (p0)
-  uint32_t scw[2] = {0u, 0u};
-  auto read_scales = [&](int t) {
-    if constexpr (MXA) {
-      const uint2 v = *reinterpret_cast<const uint2*>(panel + (((t >> 1) * 2 + wr) * 16 + fr) * 8);
-      scw[0] = v.x;
-      scw[1] = v.y;
-    }
-  };
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
@@ -1134,10 +1015,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4& c = acc[4 * qm + i][2 * qn + j];
-        if constexpr (FP8 && MXA) {
-          // opsel_b = i picks byte i of the scale VGPR (row 16 i + fr's block scale)
-          c = mx_mfma_sb_byte(xb[qn][j], xa[set][i], c, int(scw[qm]), i);
-        } else if constexpr (FP8) {
+        if constexpr (FP8) {
           c = mx_mfma(xb[qn][j], xa[set][i], c);
         } else {
 #pragma unroll
@@ -1173,7 +1051,6 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     // p0
     if constexpr (!PRE) read_a(buf, 0);
     read_b(buf, 0);
-    read_scales(t);
     stage_b(1, t + 1);
     wait_dma();
     barrier();
@@ -1899,34 +1776,18 @@ hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& g, hipStream_t st) {
   if (g.M == 0 || g.N == 0) return hipSuccess;
   const int M = g.M, N = g.N, K = g.K;
   if (K % 128 != 0 || N % 8 != 0 || N < 8 || g.lda < K || g.ldw < K || !g.X0 || !g.XL || g.ldx < N ||
-      g.ldx % 8 != 0 || (!g.Z && !g.dot && !g.q) || (g.Z && (g.ldz < N || g.ldz % 8 != 0)) ||
-      (g.dot && (!g.hw || g.ldd < M)) || (!g.sa == !g.sa_blk))
+      g.ldx % 8 != 0 || !g.sa || (!g.Z && !g.dot) || (g.Z && (g.ldz < N || g.ldz % 8 != 0)) ||
+      (g.dot && (!g.hw || g.ldd < M)))
     return hipErrorInvalidValue;
-  const int tiles_n = (N + 255) / 256;
-  if (g.q && (!g.sq || g.kq < N || g.kq % 128 != 0 || g.kq > tiles_n * 256 || g.ldq < g.kq || g.ldq % 8 != 0 ||
-              g.ldsq < tiles_n))
-    return hipErrorInvalidValue;
-  if (g.sa_blk && (K > kMx256MaxBlk * 256 || g.ld_sa_blk < (K + 255) / 256)) return hipErrorInvalidValue;
   XsArgs xs;
   xs.hw = g.hw;
   xs.dot = g.dot;
   xs.ldd = g.ldd;
-  xs.q = static_cast<uint8_t*>(g.q);
-  xs.ldq = g.ldq;
-  xs.kq = g.kq;
-  xs.sq = g.sq;
-  xs.ldsq = g.ldsq;
-  xs.sa_blk = g.sa_blk;
-  xs.ld_sa_blk = g.ld_sa_blk;
-  const int grid = ((M + 255) / 256) * tiles_n;
-#define DTFS_XG(MXA)                                                                                               \
-  hipLaunchKernelGGL((gemm_8ph_kernel<true, bf16, true, true, MXA>), dim3(grid), dim3(512), 0, st,                  \
-                     static_cast<const uint8_t*>(g.A), g.lda, static_cast<const uint8_t*>(g.W), g.ldw, g.bias, g.sa, \
-                     g.sw, static_cast<bf16*>(g.Z), g.ldz, static_cast<const bf16*>(g.X0),                          \
-                     static_cast<const bf16*>(g.XL), g.ldx, M, N, K, int(EPI_CROSS), xs)
-  if (g.sa_blk) DTFS_XG(true);
-  else DTFS_XG(false);
-#undef DTFS_XG
+  const int grid = ((M + 255) / 256) * ((N + 255) / 256);
+  hipLaunchKernelGGL((gemm_8ph_kernel<true, bf16, true, true>), dim3(grid), dim3(512), 0, st,
+                     static_cast<const uint8_t*>(g.A), g.lda, static_cast<const uint8_t*>(g.W), g.ldw, g.bias, g.sa,
+                     g.sw, static_cast<bf16*>(g.Z), g.ldz, static_cast<const bf16*>(g.X0),
+                     static_cast<const bf16*>(g.XL), g.ldx, M, N, K, int(EPI_CROSS), xs);
   return hipGetLastError();
 }
 

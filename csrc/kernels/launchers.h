@@ -171,14 +171,10 @@ hipError_t launch_cross_combine(const void* y, const void* x0, const void* xl, i
                                 float* dot, hipStream_t st);
 
 // DCN-v2 cross layer in one launch (fp8 8-phase GEMM + LDS-staged cross
-// epilogue): y = (A W^T) * scale_A * sw + b, z = bf16(x0 * bf16(y) + xl),
-// written to Z and / or
-//   * dotted with hw into one partial logit per 256-column tile:
-//     dot[tn * ldd + m], tn < ceil(N / 256);
-//   * quantised as the next layer's "MX-256" operand: e4m3 q [M][ldq]
-//     (columns [N, kq) zero) + one E8M0 scale per (row, 256 columns) in sq.
-// scale_A: per-row fp32 sa [M], or MX-256 E8M0 bytes sa_blk [M][ld_sa_blk]
-// (a previous layer's q / sq). A: e4m3 [M][K], K % 128 == 0; N % 8 == 0.
+// epilogue): y = (A W^T) * sa * sw + b, z = bf16(x0 * bf16(y) + xl), written
+// to Z and / or dotted with hw into one partial logit per 256-column tile:
+// dot[tn * ldd + m], tn < ceil(N / 256). A: e4m3 [M][K] with per-row scales
+// sa, K % 128 == 0; N % 8 == 0.
 struct CrossGemmArgs {
   const void* A = nullptr;
   int64_t lda = 0;
@@ -186,8 +182,6 @@ struct CrossGemmArgs {
   int64_t ldw = 0;
   const float* bias = nullptr;
   const float* sa = nullptr;
-  const uint8_t* sa_blk = nullptr;
-  int64_t ld_sa_blk = 0;
   const float* sw = nullptr;
   void* Z = nullptr;
   int64_t ldz = 0;
@@ -197,11 +191,6 @@ struct CrossGemmArgs {
   const float* hw = nullptr;
   float* dot = nullptr;
   int64_t ldd = 0;
-  void* q = nullptr;
-  int64_t ldq = 0;
-  int kq = 0;
-  uint8_t* sq = nullptr;
-  int64_t ldsq = 0;
   int M = 0, N = 0, K = 0;
 };
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);

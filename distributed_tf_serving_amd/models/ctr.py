@@ -292,21 +292,21 @@ class DCNv2(CTRModel):
             # quantises it for the next layer and, for the last layer, reduces
             # the cross logit instead of writing z (profiles/dcn_v2_split_kernels.md)
             # Full-chip steps: the combine rides on the GEMM as an LDS-staged
-            # epilogue (ops.cross_gemm_fp8; no y round trip) that also writes z
-            # as the next layer's MX-256 operand (e4m3 + one E8M0 scale per
-            # 256-column block, applied by the MFMA); the last layer writes
-            # only per-column-tile partial cross logits
+            # epilogue (ops.cross_gemm_fp8; no y round trip), the last layer
+            # writing only per-column-tile partial cross logits; z is quantised
+            # for the next layer by one quant_rows pass (it reads z back from
+            # the Infinity Cache: cheaper than an e4m3 copy from the epilogue,
+            # profiles/r03_cross_fused.md)
             xl, (q, sx) = x0, q0
             fused = ops.cross_gemm_fits(x0.shape[0], self.d) and q.shape[1] % 128 == 0
             for i in range(L):
                 layer = self.cross[i]
                 last = i == L - 1
                 if fused:
-                    z, cross_logit, *qn = ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, xl,
-                                                             want_z=not last, head_w=self.head_wc if last else None,
-                                                             emit_q=not last)
+                    z, cross_logit = ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, xl,
+                                                        want_z=not last, head_w=self.head_wc if last else None)
                     if not last:
-                        q, sx = qn
+                        q, sx = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
                 else:
                     y = ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias)  # plain bf16 epilogue
                     z, q, sx, cross_logit = ops.cross_combine(y, x0, xl, want_z=not last,

@@ -287,54 +287,25 @@ def cross_gemm_fits(M: int, N: int) -> bool:
     return -(-M // 256) * -(-N // 256) >= 256 and N % 8 == 0
 
 
-def quant_mx256(x: torch.Tensor, kq: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """CPU reference of the cross GEMM's "MX-256" output: e4m3 q [M, kq] (K
-    padding zero) + E8M0 scale bytes [M, ceil(kq / 256)], one per (row, 256
-    columns): x ~= q * 2^(scale - 127)."""
-    M, K = x.shape
-    nb = -(-kq // CROSS_TILE)
-    xf = torch.zeros(M, nb * CROSS_TILE, dtype=torch.float32, device=x.device)
-    xf[:, :K] = x.float()
-    blk = xf.view(M, nb, CROSS_TILE)
-    e = _mx_exponent(blk.abs().amax(dim=2))
-    q = (blk * torch.exp2(-e.float())[:, :, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
-    return q.view(M, -1)[:, :kq].contiguous(), (e + 127).to(torch.uint8)
-
-
-def dequant_mx256(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    return q.float() * torch.exp2(s.float() - 127).repeat_interleave(CROSS_TILE, dim=1)[:, :q.shape[1]]
-
-
 def cross_gemm_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
                    b: Optional[torch.Tensor], x0: torch.Tensor, xl: torch.Tensor, want_z: bool = True,
-                   head_w: Optional[torch.Tensor] = None, emit_q: bool = False):
+                   head_w: Optional[torch.Tensor] = None):
     """One DCN-v2 cross layer in one launch (csrc/kernels/gemm.hip
     cross_staged_epilogue): y = bf16(xq Wq^T * sx * sw + b), z = bf16(x0 * y + xl).
-    ``sx``: fp32 [M] row scales, or uint8 [M, nblk] MX-256 scales (a previous
-    layer's ``emit_q`` output). Returns (z or None, dot or None) - plus
-    (q, sq), the next layer's MX-256 operand, with ``emit_q`` - where dot =
-    fp32 [ceil(N / 256), M] partial cross logits z[:, 256 t:256 t + 256] .
-    head_w[256 t:256 t + 256] (a head ``extra``). Same rounding as linear_fp8 +
-    cross_combine."""
+    Returns (z or None, dot or None) with dot = fp32 [ceil(N / 256), M] partial
+    cross logits z[:, 256 t:256 t + 256] . head_w[256 t:256 t + 256] (a head
+    ``extra``). The same rounding as linear_fp8 + cross_combine."""
     if xq.is_cuda:
-        z, d, q, sq = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w, emit_q)
-        out = ((z if want_z else None), (d if head_w is not None else None))
-        return out + ((q, sq) if emit_q else ())
-    if sx.dtype == torch.uint8:
-        y = dequant_mx256(xq, sx) @ (Wq.float() * sw[:, None]).t()
-        y = (y + b.float() if b is not None else y).to(torch.bfloat16)
-    else:
-        y = linear_fp8(xq, sx, Wq, sw, b)
+        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w)
+        return (z if want_z else None), (d if head_w is not None else None)
+    y = linear_fp8(xq, sx, Wq, sw, b)
     zb = (x0.float() * y.float() + xl.float()).to(torch.bfloat16)
     d = None
     if head_w is not None:
         N = zb.shape[1]
         d = torch.stack([zb[:, t:t + CROSS_TILE].float() @ head_w[t:t + CROSS_TILE].float()
                          for t in range(0, N, CROSS_TILE)])
-    out = ((zb if want_z else None), d)
-    if emit_q:
-        out += quant_mx256(zb, -(-zb.shape[1] // FP8_K_PAD) * FP8_K_PAD)
-    return out
+    return (zb if want_z else None), d
 
 
 def linear_fp8(xq: torch.Tensor, sx: Optional[torch.Tensor], Wq: torch.Tensor, sw: torch.Tensor,

@@ -49,33 +49,22 @@ def main():
         "split_last": lambda: ops.cross_combine(ops.linear_fp8(q, sx, wq, sw, b), x0, xl, False, 0, hw),
         "fused_last": lambda: ops.cross_gemm_fp8(q, sx, wq, sw, b, x0, xl, False, hw),
     }
-    _, _, q1, s1 = ops.cross_gemm_fp8(q, sx, wq, sw, b, x0, xl, True, None, True)
-    forms.update({
-        "mx_mid_rowscale_in": lambda: ops.cross_gemm_fp8(q, sx, wq, sw, b, x0, xl, True, None, True),
-        "mx_mid_mx_in": lambda: ops.cross_gemm_fp8(q1, s1, wq, sw, b, x0, xl, True, None, True),
-        "mx_last_mx_in": lambda: ops.cross_gemm_fp8(q1, s1, wq, sw, b, x0, xl, False, hw),
-    })
     w2 = [ops.quant_rows_fp8((torch.randn(N, N, device=dev, generator=g) / N ** 0.5).to(torch.bfloat16),
                              ops.FP8_K_PAD) for _ in range(3)]
 
-    def chain(mx: bool):
+    def chain():
         """3 cross layers from x0 (row-scaled e4m3 x0, as the gather writes it)"""
         qq, ss = ops.quant_rows_fp8(x0, ops.FP8_K_PAD)
         xl_ = x0
         for i, (wq_, sw_) in enumerate(w2):
             last = i == 2
-            if mx:
-                z, d, *qn = ops.cross_gemm_fp8(qq, ss, wq_, sw_, b, x0, xl_, not last, hw if last else None, not last)
-                if not last:
-                    qq, ss = qn
-            else:
-                z, d = ops.cross_gemm_fp8(qq, ss, wq_, sw_, b, x0, xl_, not last, hw if last else None)
-                if not last:
-                    qq, ss = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
+            z, d = ops.cross_gemm_fp8(qq, ss, wq_, sw_, b, x0, xl_, not last, hw if last else None)
+            if not last:
+                qq, ss = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
             xl_ = z
         return d
 
-    forms.update({"chain_quant_rows": lambda: chain(False), "chain_mx256": lambda: chain(True)})
+    forms["chain_quant_rows"] = chain
     res = {k: [] for k in forms}
     for _ in range(5):
         for k, fn in forms.items():
