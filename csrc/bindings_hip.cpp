@@ -540,6 +540,38 @@ torch::Tensor dot_interaction(torch::Tensor dense, torch::Tensor emb, int64_t ou
   return out;
 }
 
+// K1 + K5: dot interaction straight from the (local, one-hot) tables
+torch::Tensor dot_interaction_gather(torch::Tensor dense, torch::Tensor table, torch::Tensor ids,
+                                     torch::Tensor modulo_f, torch::Tensor offset_f, int64_t out_cols) {
+  check_dev(dense, "dense");
+  check_same_dev(dense, table, "table");
+  check_same_dev(dense, ids, "ids");
+  TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && table.scalar_type() == torch::kBFloat16, "bf16 inputs");
+  TORCH_CHECK(dense.dim() == 2 && dense.size(1) == 64 && dense.stride(1) == 1 && dense.stride(0) % 8 == 0,
+              "dense must be [B, 64] with unit inner stride");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == 64 && table.is_contiguous(), "table must be contiguous [V, 64]");
+  TORCH_CHECK((ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32) && ids.dim() == 2 &&
+                  ids.stride(1) == 1 && ids.size(0) == dense.size(0),
+              "ids must be int32/int64 [B, T] rows with unit inner stride");
+  const int64_t B = dense.size(0), T = ids.size(1);
+  for (auto* t : {&modulo_f, &offset_f}) {
+    check_same_dev(dense, *t, "table map");
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == T && t->is_contiguous(), "modulo_f / offset_f: int64 [T]");
+  }
+  TORCH_CHECK(T + 1 <= 32, "dot interaction kernel handles T + 1 <= 32 vectors");
+  const int64_t used = 64 + (T + 1) * T / 2;
+  if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
+  TORCH_CHECK(out_cols >= used && out_cols % 8 == 0 && out_cols <= 1024, "out_cols: >= used, a multiple of 8, <= 1024");
+  c10::DeviceGuard g(dense.device());
+  auto out = torch::empty({B, out_cols}, dense.options());
+  check_hip(dtfs::launch_dot_interaction_gather(dense.data_ptr(), dense.stride(0), table.data_ptr(), table.size(0),
+                                                ids.data_ptr(), ids.scalar_type() == torch::kInt64, ids.stride(0),
+                                                modulo_f.data_ptr<int64_t>(), offset_f.data_ptr<int64_t>(), int(T),
+                                                int(B), out.data_ptr(), out_cols, int(out_cols), cur_stream(dense)),
+            "dot_interaction_gather");
+  return out;
+}
+
 // ---------------------------------------------------------------- K1b routing
 torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tensor col, torch::Tensor mod,
                           torch::Tensor off, c10::optional<torch::Tensor> out_opt) {
@@ -1146,6 +1178,8 @@ PYBIND11_MODULE(_hip, m) {
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
+  m.def("dot_interaction_gather", &dot_interaction_gather, py::arg("dense"), py::arg("table"), py::arg("ids"),
+        py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);
   m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
         py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,

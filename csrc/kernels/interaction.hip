@@ -133,6 +133,67 @@ __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restric
   for (int c = used + lane; c < out_cols; c += 64) o[c] = f2bf(0.f);
 }
 
+// K1 fused into K5: the DLRM dot interaction straight from the embedding
+// tables (one-hot, local tables). The gather kernel wrote emb [B, T, 64] to
+// HBM and dot_interact_kernel read it back (63 MB each way per 16384-row
+// step at T = 30); here the wave of row b looks its T rows up itself:
+// lane (r, h), r = 1..T, reads table row off[r-1] + id(b, r-1) mod m[r-1],
+// all four 16-byte chunks issued before the first MFMA (4 KB of independent
+// random reads in flight per wave). The output row (dense | lower triangle |
+// zero pad) is assembled in LDS and written as 16-byte vectors instead of
+// 2-byte scattered stores.
+template <typename IdT>
+__global__ void __launch_bounds__(256) dot_interact_gather_kernel(
+    const bf16* __restrict__ dense, int64_t ldd, const bf16* __restrict__ table, int64_t table_rows,
+    const IdT* __restrict__ ids, int64_t ldi, const int64_t* __restrict__ modulo_f,
+    const int64_t* __restrict__ offset_f, int T, int B, bf16* __restrict__ out, int64_t ldo, int out_cols) {
+  constexpr int D = 64;
+  constexpr int ROWB = 4 * 2048;  // LDS bytes per block: 4 waves x one output row (<= 1024 columns)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[ROWB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * (blockDim.x / 64) + w;
+  if (b >= B) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int nv = T + 1;
+  int64_t row = -1;
+  if (r >= 1 && r < nv) {
+    const int t = r - 1;
+    const int64_t m = modulo_f[t];
+    int64_t v = int64_t(ids[int64_t(b) * ldi + t]) % m;
+    if (v < 0) v += m;
+    row = min(offset_f[t] + v, table_rows - 1);
+  }
+  bf16x8 x[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 16 * s + 8 * h;
+    x[s] = bf16x8{};
+    if (r == 0) x[s] = *reinterpret_cast<const bf16x8*>(dense + int64_t(b) * ldd + k);
+    else if (row >= 0) x[s] = *reinterpret_cast<const bf16x8*>(table + row * D + k);
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[s], x[s], acc, 0, 0, 0);
+  // assemble the row in this wave's LDS slice: [dense | lower triangle | zeros]
+  bf16* o = reinterpret_cast<bf16*>(lds + w * (ROWB / 4));
+  const int n8 = out_cols / 8;
+  for (int c = lane; c < n8; c += 64) *reinterpret_cast<bf16x8*>(o + c * 8) = bf16x8{};
+  __builtin_amdgcn_wave_barrier();
+  if (lane < D / 8) *reinterpret_cast<bf16x8*>(o + lane * 8) = *reinterpret_cast<const bf16x8*>(dense + int64_t(b) * ldd + lane * 8);
+  const int col = lane & 31;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int rowi = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    if (rowi < nv && col < rowi) o[D + rowi * (rowi - 1) / 2 + col] = f2bf(acc[reg]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bf16* dst = out + int64_t(b) * ldo;
+  for (int c = lane; c < n8; c += 64) *reinterpret_cast<bf16x8*>(dst + c * 8) = *reinterpret_cast<const bf16x8*>(o + c * 8);
+}
+
 // ---------------------------------------------------------------- K6
 // y[m] = act(x[m,:] . w + bias + extra[m]); one wave per row; act: 0 none, 2 sigmoid.
 __global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, int64_t ldx, const float* __restrict__ w,
@@ -351,6 +412,26 @@ hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* em
   if ((emb_off == nullptr) != (emb_stride == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dot_interact_kernel, dim3((B + 3) / 4), dim3(256), 0, st, static_cast<const bf16*>(dense), ldd,
                      static_cast<const bf16*>(emb), T, B, static_cast<bf16*>(out), ldo, out_cols, emb_off, emb_stride, emb_rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
+                                         const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
+                                         const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
+                                         hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  if (T < 1 || T + 1 > 32 || out_cols % 8 || out_cols > 1024 || out_cols < 64 + (T + 1) * T / 2 || ldo % 8 ||
+      ldo < out_cols || ldd % 8 || ldi < T || table_rows < 1 || !modulo_f || !offset_f)
+    return hipErrorInvalidValue;
+  dim3 grid((B + 3) / 4), block(256);
+  if (ids64)
+    hipLaunchKernelGGL(dot_interact_gather_kernel<int64_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
+                       static_cast<const bf16*>(table), table_rows, static_cast<const int64_t*>(ids), ldi, modulo_f,
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols);
+  else
+    hipLaunchKernelGGL(dot_interact_gather_kernel<int32_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
+                       static_cast<const bf16*>(table), table_rows, static_cast<const int32_t*>(ids), ldi, modulo_f,
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols);
   return hipGetLastError();
 }
 

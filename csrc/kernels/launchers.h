@@ -195,6 +195,14 @@ struct CrossGemmArgs {
 };
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 
+// K1 + K5: DLRM dot interaction with the one-hot gather fused in: vector t+1
+// of row b is table[offset_f[t] + ids[b * ldi + t] mod modulo_f[t]] (rows
+// clamped to the table); out [B][ldo] = [dense | lower triangle | zeros].
+hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
+                                         const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
+                                         const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
+                                         hipStream_t st);
+
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();
 hipError_t launch_sort_scores(const float* in, int n, bool descending, float* out, int64_t* perm, int k_out,

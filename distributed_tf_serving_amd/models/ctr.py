@@ -405,6 +405,12 @@ class DLRM(CTRModel):
 
     def _forward(self, ids, wts, out=None):
         dense_out = self.bottom(self.dense_input(wts))
+        if self.hot == 1 and self.emb is not None and ids.is_cuda:
+            # one-hot, local tables: the interaction kernel looks the rows up
+            # itself (no [B, T, 64] embedding round trip through HBM)
+            z = ops.dot_interaction_gather(dense_out, self.emb, self.sparse_ids(ids), self.modulo_f, self.offset_f,
+                                           self.inter_cols)
+            return self.top.forward_head(z, self.head_w, self.head_b, out=out)
         emb = self.lookup(ids, wts)
         return self.interact_and_top(dense_out, emb, out=out)
 

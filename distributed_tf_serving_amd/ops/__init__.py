@@ -490,6 +490,20 @@ def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0,
     return out.to(dense.dtype)
 
 
+def dot_interaction_gather(dense: torch.Tensor, table: torch.Tensor, ids: torch.Tensor, modulo_f: torch.Tensor,
+                           offset_f: torch.Tensor, out_cols: int = 0) -> torch.Tensor:
+    """K1 fused into K5 (one-hot DLRM, local tables): dot_interaction(dense,
+    table[offset_f + ids mod modulo_f]) without the [B, T, 64] embedding
+    intermediate. ``ids``: int32/int64 [B, T] rows (a row view is fine)."""
+    T = ids.shape[1]
+    if out_cols <= 0:
+        out_cols = interaction_cols(T, dense.shape[1])
+    if dense.is_cuda:
+        return hip().dot_interaction_gather(dense, table, _rows(ids), modulo_f, offset_f, int(out_cols))
+    rows = _hash_rows(ids, 0, modulo_f, offset_f).clamp(0, table.shape[0] - 1)
+    return dot_interaction(dense, table[rows], out_cols)
+
+
 # ------------------------------------------------------------------ K1b routing
 def shard_route(ids: torch.Tensor, W: int, tm: int, col: torch.Tensor, mod: torch.Tensor, off: torch.Tensor,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -408,6 +408,30 @@ def test_dot_interaction(cuda, T):
     _close(z, zr, 1e-2, 5e-2, "dot")
 
 
+@pytest.mark.parametrize("T,ids64", [(1, True), (26, False), (30, True), (31, False)])
+def test_dot_interaction_gather(cuda, T, ids64):
+    """K1 fused into K5: the interaction reads its rows from the tables (row
+    view of the ids, per-table modulo + offset, negative ids) == gather +
+    dot_interaction on the GPU (bit for bit) and the fp32 CPU reference."""
+    g = torch.Generator().manual_seed(T)
+    B, rows = 517, 1000
+    dense = torch.randn(B, 64, generator=g).to(torch.bfloat16)
+    table = torch.randn(T * rows, 64, generator=g).to(torch.bfloat16)
+    full = torch.randint(-(1 << 40), 1 << 40, (B, T + 13), generator=g)
+    ids = (full if ids64 else full.to(torch.int32))[:, 13:]  # a row view, like DLRM.sparse_ids
+    mod = torch.full((T,), rows, dtype=torch.int64)
+    off = torch.arange(T, dtype=torch.int64) * rows
+    dc, tc, ic, mc, oc = (t.to(cuda) for t in (dense, table, full if ids64 else full.to(torch.int32), mod, off))
+    z = ops.dot_interaction_gather(dc, tc, ic[:, 13:], mc, oc)
+    emb, _ = ops.embed(tc, ic[:, 13:], None, modulo_f=mc, offset_f=oc, want_x=True)
+    z2 = ops.dot_interaction(dc, emb.view(B, T, 64))
+    zr = ops.dot_interaction_gather(dense, table, ids, mod, off)
+    torch.cuda.synchronize()
+    assert z.shape == zr.shape == (B, ops.interaction_cols(T, 64))
+    assert torch.equal(z.cpu(), z2.cpu())
+    _close(z, zr, 1e-2, 5e-2, "dot gather")
+
+
 def test_head(cuda):
     x = torch.randn(101, 256).to(torch.bfloat16)
     w = torch.randn(256) * 0.05
