@@ -572,6 +572,36 @@ torch::Tensor dot_interaction_gather(torch::Tensor dense, torch::Tensor table, t
   return out;
 }
 
+// DLRM bottom MLP (512-256-64, relu) from the fp32 dense feature columns, one kernel
+torch::Tensor bottom_mlp3(torch::Tensor wts, int64_t nd, torch::Tensor W1, torch::Tensor b1, torch::Tensor W2,
+                          torch::Tensor b2, torch::Tensor W3, torch::Tensor b3) {
+  TORCH_CHECK(wts.is_cuda(), "wts must be a GPU tensor");
+  TORCH_CHECK(wts.scalar_type() == torch::kFloat32 && wts.dim() == 2 && wts.stride(1) == 1 && wts.size(1) >= nd,
+              "wts must be fp32 [M, >= nd] rows with unit inner stride");
+  const torch::Tensor* Ws[3] = {&W1, &W2, &W3};
+  const torch::Tensor* bs[3] = {&b1, &b2, &b3};
+  int64_t k = 64;
+  for (int i = 0; i < 3; ++i) {
+    check_same_dev(wts, *Ws[i], "weight");
+    check_same_dev(wts, *bs[i], "bias");
+    TORCH_CHECK(Ws[i]->scalar_type() == torch::kBFloat16 && Ws[i]->dim() == 2 && Ws[i]->is_contiguous() &&
+                    Ws[i]->size(1) == k,
+                "bottom MLP weight ", i, " must be contiguous bf16 [N, ", k, "]");
+    TORCH_CHECK(bs[i]->scalar_type() == torch::kFloat32 && bs[i]->numel() == Ws[i]->size(0) && bs[i]->is_contiguous(),
+                "bottom MLP bias must be fp32 [N]");
+    k = Ws[i]->size(0);
+  }
+  const int64_t M = wts.size(0), N3 = W3.size(0);
+  c10::DeviceGuard g(wts.device());
+  auto out = torch::empty({M, N3}, wts.options().dtype(torch::kBFloat16));
+  check_hip(dtfs::launch_bottom_mlp3(wts.data_ptr<float>(), wts.stride(0), int(nd), int(M), W1.data_ptr(),
+                                     b1.data_ptr<float>(), int(W1.size(0)), W2.data_ptr(), b2.data_ptr<float>(),
+                                     int(W2.size(0)), W3.data_ptr(), b3.data_ptr<float>(), int(N3), out.data_ptr(), N3,
+                                     cur_stream(wts)),
+            "bottom_mlp3");
+  return out;
+}
+
 // ---------------------------------------------------------------- K1b routing
 torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tensor col, torch::Tensor mod,
                           torch::Tensor off, c10::optional<torch::Tensor> out_opt) {
@@ -1180,6 +1210,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("dot_interaction_gather", &dot_interaction_gather, py::arg("dense"), py::arg("table"), py::arg("ids"),
         py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);
+  m.def("bottom_mlp3", &bottom_mlp3, py::arg("wts"), py::arg("nd"), py::arg("W1"), py::arg("b1"), py::arg("W2"),
+        py::arg("b2"), py::arg("W3"), py::arg("b3"));
   m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
         py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,

@@ -194,6 +194,92 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
   for (int c = lane; c < n8; c += 64) *reinterpret_cast<bf16x8*>(dst + c * 8) = *reinterpret_cast<const bf16x8*>(o + c * 8);
 }
 
+// ---------------------------------------------------------------- K4 (small)
+// DLRM bottom MLP in one kernel: the dense features (fp32 columns [0, nd) of
+// feat_wts) -> bf16, zero padded to K0 = 64 -> relu(. W1^T + b1) [N1] ->
+// relu(. W2^T + b2) [N2] -> relu(. W3^T + b3) [N3] (bf16 out). Per block 32
+// rows, every intermediate in LDS; the weights (~176 K bf16, L2-resident)
+// are read as MFMA B fragments straight from global memory. As separate
+// launches these are three small GEMMs + a pad kernel, each mostly launch /
+// prologue / epilogue (~31 us per 16384-row step for 5.8 GFLOP).
+// Layer layout: wave w owns output columns [w N / 4, (w + 1) N / 4); D = W_frag x
+// A_frag^T, so lane (fr, fq) holds rows 16 i + fr, columns 4 fq .. 4 fq + 3 of
+// each 16 x 16 tile. LDS row pitches are the row bytes + 16: the 16 rows of a
+// ds_read_b128 lane group land on 16 distinct 16-byte bank slots.
+template <int K, int NW, int PIN, int POUT>
+__device__ __forceinline__ void mlp_layer_lds(const uint8_t* __restrict__ ain, const bf16* __restrict__ W,
+                                              const float* __restrict__ b, uint8_t* __restrict__ hout,
+                                              bf16* __restrict__ gout, int64_t ldo, int m0, int M, int wid, int fr,
+                                              int fq) {
+  constexpr int TN = NW / 16;
+  f32x4 acc[2][TN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n0 = wid * NW;
+#pragma unroll 4
+  for (int s = 0; s < K / 32; ++s) {
+    bf16x8 a[2], w[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      w[j] = *reinterpret_cast<const bf16x8*>(W + int64_t(n0 + 16 * j + fr) * K + 32 * s + 8 * fq);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ain + (16 * i + fr) * PIN + (32 * s + 8 * fq) * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], a[i], acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + 16 * j + 4 * fq;
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(b + n);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(fmaxf(acc[i][j][r] + b4[r], 0.f));
+      const int row = 16 * i + fr;
+      if (gout) {
+        if (m0 + row < M) *reinterpret_cast<bf16x4*>(gout + int64_t(m0 + row) * ldo + n) = o;
+      } else {
+        *reinterpret_cast<bf16x4*>(hout + row * POUT + n * 2) = o;
+      }
+    }
+  }
+}
+
+template <int N1, int N2, int N3>
+__global__ void __launch_bounds__(256) bottom_mlp3_kernel(const float* __restrict__ wts, int64_t ldw, int nd, int M,
+                                                          const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                          const bf16* __restrict__ W2, const float* __restrict__ b2,
+                                                          const bf16* __restrict__ W3, const float* __restrict__ b3,
+                                                          bf16* __restrict__ out, int64_t ldo) {
+  constexpr int BM = 32, K0 = 64;
+  constexpr int PX = K0 * 2 + 16, P1 = N1 * 2 + 16, P2 = N2 * 2 + 16;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[BM * (PX + P1 + P2)];
+  uint8_t* X = lds;
+  uint8_t* H1 = X + BM * PX;
+  uint8_t* H2 = H1 + BM * P1;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const int m0 = blockIdx.x * BM;
+  {  // X: thread t -> row t / 8, columns 8 (t % 8) .. +8 (fp32 -> bf16, zero pad)
+    const int row = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
+    const int64_t m = min(m0 + row, M - 1);
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = f2bf(c0 + e < nd ? wts[m * ldw + c0 + e] : 0.f);
+    *reinterpret_cast<bf16x8*>(X + row * PX + c0 * 2) = v;
+  }
+  __syncthreads();
+  mlp_layer_lds<K0, N1 / 4, PX, P1>(X, W1, b1, H1, nullptr, 0, m0, M, wid, fr, fq);
+  __syncthreads();
+  mlp_layer_lds<N1, N2 / 4, P1, P2>(H1, W2, b2, H2, nullptr, 0, m0, M, wid, fr, fq);
+  __syncthreads();
+  mlp_layer_lds<N2, N3 / 4, P2, 0>(H2, W3, b3, nullptr, out, ldo, m0, M, wid, fr, fq);
+}
+
 // ---------------------------------------------------------------- K6
 // y[m] = act(x[m,:] . w + bias + extra[m]); one wave per row; act: 0 none, 2 sigmoid.
 __global__ void __launch_bounds__(256) head_kernel(const bf16* __restrict__ x, int64_t ldx, const float* __restrict__ w,
@@ -433,6 +519,21 @@ hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const v
                        static_cast<const bf16*>(table), table_rows, static_cast<const int32_t*>(ids), ldi, modulo_f,
                        offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols);
   return hipGetLastError();
+}
+
+hipError_t launch_bottom_mlp3(const float* wts, int64_t ldw, int nd, int M, const void* W1, const float* b1, int N1,
+                              const void* W2, const float* b2, int N2, const void* W3, const float* b3, int N3,
+                              void* out, int64_t ldo, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (nd < 1 || nd > 64 || ldw < nd || ldo < N3 || ldo % 4 || !W1 || !W2 || !W3 || !b1 || !b2 || !b3)
+    return hipErrorInvalidValue;
+  if (N1 == 512 && N2 == 256 && N3 == 64) {  // DLRM bottom_mlp [512, 256, 64]
+    hipLaunchKernelGGL((bottom_mlp3_kernel<512, 256, 64>), dim3((M + 31) / 32), dim3(256), 0, st, wts, ldw, nd, M,
+                       static_cast<const bf16*>(W1), b1, static_cast<const bf16*>(W2), b2,
+                       static_cast<const bf16*>(W3), b3, static_cast<bf16*>(out), ldo);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_head(const void* x, int64_t ldx, const float* w, float bias, const float* extra, int M, int K,

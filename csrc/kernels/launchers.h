@@ -203,6 +203,14 @@ hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const v
                                          const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
                                          hipStream_t st);
 
+// K4 (small) for the DLRM bottom MLP: relu(relu(relu(pad64(bf16(wts[:, :nd]))
+// W1^T + b1) W2^T + b2) W3^T + b3) in one kernel (W1 [N1][64], W2 [N2][N1], W3
+// [N3][N2] bf16; out bf16 [M][ldo]). Built for (N1, N2, N3) = (512, 256, 64);
+// hipErrorInvalidValue for other shapes.
+hipError_t launch_bottom_mlp3(const float* wts, int64_t ldw, int nd, int M, const void* W1, const float* b1, int N1,
+                              const void* W2, const float* b2, int N2, const void* W3, const float* b3, int N3,
+                              void* out, int64_t ldo, hipStream_t st);
+
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();
 hipError_t launch_sort_scores(const float* in, int n, bool descending, float* out, int64_t* perm, int k_out,

@@ -403,8 +403,19 @@ class DLRM(CTRModel):
         z = ops.dot_interaction(dense_out, emb, self.inter_cols)
         return self.top.forward_head(z, self.head_w, self.head_b, out=out)
 
+    def bottom_out(self, wts: torch.Tensor) -> torch.Tensor:
+        """Bottom MLP over the dense features: one fused kernel on the GPU for
+        the 512-256-64 tower (pad + 3 GEMMs were ~31 us of mostly launch /
+        prologue per 16384-row step), else layer by layer."""
+        L = self.bottom.layers
+        if (wts.is_cuda and wts.dtype == torch.float32 and self.dtype == torch.bfloat16 and self.dense_k == 64
+                and tuple(l.out_dim for l in L) == ops.BOTTOM_MLP3_DIMS and all(l.act == "relu" for l in L)
+                and not any(l.fp8 for l in L)):
+            return ops.bottom_mlp3(wts, self.cfg.num_dense, [(l.weight, l.bias) for l in L])
+        return self.bottom(self.dense_input(wts))
+
     def _forward(self, ids, wts, out=None):
-        dense_out = self.bottom(self.dense_input(wts))
+        dense_out = self.bottom_out(wts)
         if self.hot == 1 and self.emb is not None and ids.is_cuda:
             # one-hot, local tables: the interaction kernel looks the rows up
             # itself (no [B, T, 64] embedding round trip through HBM)

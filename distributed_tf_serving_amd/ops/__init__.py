@@ -504,6 +504,24 @@ def dot_interaction_gather(dense: torch.Tensor, table: torch.Tensor, ids: torch.
     return dot_interaction(dense, table[rows], out_cols)
 
 
+BOTTOM_MLP3_DIMS = (512, 256, 64)  # the fused DLRM bottom-MLP kernel's layer widths
+
+
+def bottom_mlp3(wts: torch.Tensor, nd: int, layers) -> torch.Tensor:
+    """DLRM bottom MLP in one kernel (csrc/kernels/interaction.hip
+    bottom_mlp3_kernel): relu layers 64 -> 512 -> 256 -> 64 over the fp32 dense
+    feature columns wts[:, :nd] (bf16, zero padded to 64). ``layers``: three
+    (weight bf16 [N, K], bias fp32 [N]) pairs. bf16 [M, 64]."""
+    (W1, b1), (W2, b2), (W3, b3) = layers
+    if wts.is_cuda:
+        return hip().bottom_mlp3(_rows(wts), int(nd), W1, b1, W2, b2, W3, b3)
+    x = torch.zeros(wts.shape[0], W1.shape[1], dtype=torch.bfloat16)
+    x[:, :nd] = wts[:, :nd].to(torch.bfloat16)
+    for W, b in layers:
+        x = linear(x, W, b, "relu")
+    return x
+
+
 # ------------------------------------------------------------------ K1b routing
 def shard_route(ids: torch.Tensor, W: int, tm: int, col: torch.Tensor, mod: torch.Tensor, off: torch.Tensor,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -397,7 +397,7 @@ class ShardedDLRM(nn.Module):
 
         def bottom():
             w = wts if wts.dtype == torch.float32 else wts.float()
-            st["dense"] = d.bottom(d.dense_input(w))
+            st["dense"] = d.bottom_out(w)
 
         def top():
             z = ops_k.dot_interaction(st["dense"], bufs["emb_all"], d.inter_cols, emb_off, emb_stride)

@@ -432,6 +432,30 @@ def test_dot_interaction_gather(cuda, T, ids64):
     _close(z, zr, 1e-2, 5e-2, "dot gather")
 
 
+@pytest.mark.parametrize("M,nd", [(1, 13), (517, 13), (4096, 64), (33, 1)])
+def test_bottom_mlp3(cuda, M, nd):
+    """Fused DLRM bottom MLP (pad + 3 relu layers in one kernel, a row view of
+    feat_wts) vs the same layers one GEMM at a time on the GPU and the fp32
+    CPU reference."""
+    g = torch.Generator().manual_seed(M + nd)
+    full = torch.rand(M, nd + 30, generator=g) * 2 - 1
+    dims, k, layers = ops.BOTTOM_MLP3_DIMS, 64, []
+    for n in dims:
+        layers.append(((torch.randn(n, k, generator=g) / k ** 0.5).to(torch.bfloat16), torch.randn(n, generator=g) * 0.1))
+        k = n
+    dl = [(w.to(cuda), b.to(cuda)) for w, b in layers]
+    y = ops.bottom_mlp3(full.to(cuda)[:, :nd + 5], nd, dl)
+    x = torch.zeros(M, 64, dtype=torch.bfloat16, device=cuda)
+    x[:, :nd] = full[:, :nd].to(torch.bfloat16).to(cuda)
+    for w, b in dl:
+        x = ops.linear(x, w, b, "relu")
+    yr = ops.bottom_mlp3(full[:, :nd + 5], nd, layers)
+    torch.cuda.synchronize()
+    assert y.shape == (M, 64) and y.dtype == torch.bfloat16
+    _close(y, x, 1e-2, 1e-2, "vs layer by layer")
+    _close(y, yr, 2e-2, 2e-2, "vs CPU")
+
+
 def test_head(cuda):
     x = torch.randn(101, 256).to(torch.bfloat16)
     w = torch.randn(256) * 0.05
