@@ -572,18 +572,26 @@ torch::Tensor dot_interaction_gather(torch::Tensor dense, torch::Tensor table, t
   return out;
 }
 
-// DLRM bottom MLP (512-256-64, relu) from the fp32 dense feature columns, one kernel
-torch::Tensor bottom_mlp3(torch::Tensor wts, int64_t nd, torch::Tensor W1, torch::Tensor b1, torch::Tensor W2,
-                          torch::Tensor b2, torch::Tensor W3, torch::Tensor b3) {
-  TORCH_CHECK(wts.is_cuda(), "wts must be a GPU tensor");
-  TORCH_CHECK(wts.scalar_type() == torch::kFloat32 && wts.dim() == 2 && wts.stride(1) == 1 && wts.size(1) >= nd,
-              "wts must be fp32 [M, >= nd] rows with unit inner stride");
+// DLRM bottom MLP (512-256-64, relu) from the fp32 dense feature columns, one
+// kernel. arena (uint8 device request arena, M = its first M rows) replaces wts.
+static torch::Tensor bottom_mlp3_impl(const torch::Tensor* wts, const torch::Tensor* arena, int64_t M, int64_t nd,
+                                      torch::Tensor W1, torch::Tensor b1, torch::Tensor W2, torch::Tensor b2,
+                                      torch::Tensor W3, torch::Tensor b3) {
+  const torch::Tensor& ref = wts ? *wts : *arena;
+  TORCH_CHECK(ref.is_cuda(), "bottom MLP input must be a GPU tensor");
+  if (wts) {
+    TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->stride(1) == 1 && wts->size(1) >= nd,
+                "wts must be fp32 [M, >= nd] rows with unit inner stride");
+  } else {
+    TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous(), "arena must be a contiguous uint8 buffer");
+  }
+  const torch::Tensor& wts_ = ref;
   const torch::Tensor* Ws[3] = {&W1, &W2, &W3};
   const torch::Tensor* bs[3] = {&b1, &b2, &b3};
   int64_t k = 64;
   for (int i = 0; i < 3; ++i) {
-    check_same_dev(wts, *Ws[i], "weight");
-    check_same_dev(wts, *bs[i], "bias");
+    check_same_dev(wts_, *Ws[i], "weight");
+    check_same_dev(wts_, *bs[i], "bias");
     TORCH_CHECK(Ws[i]->scalar_type() == torch::kBFloat16 && Ws[i]->dim() == 2 && Ws[i]->is_contiguous() &&
                     Ws[i]->size(1) == k,
                 "bottom MLP weight ", i, " must be contiguous bf16 [N, ", k, "]");
@@ -591,14 +599,56 @@ torch::Tensor bottom_mlp3(torch::Tensor wts, int64_t nd, torch::Tensor W1, torch
                 "bottom MLP bias must be fp32 [N]");
     k = Ws[i]->size(0);
   }
-  const int64_t M = wts.size(0), N3 = W3.size(0);
-  c10::DeviceGuard g(wts.device());
-  auto out = torch::empty({M, N3}, wts.options().dtype(torch::kBFloat16));
-  check_hip(dtfs::launch_bottom_mlp3(wts.data_ptr<float>(), wts.stride(0), int(nd), int(M), W1.data_ptr(),
-                                     b1.data_ptr<float>(), int(W1.size(0)), W2.data_ptr(), b2.data_ptr<float>(),
-                                     int(W2.size(0)), W3.data_ptr(), b3.data_ptr<float>(), int(N3), out.data_ptr(), N3,
-                                     cur_stream(wts)),
+  const int64_t N3 = W3.size(0);
+  c10::DeviceGuard g(wts_.device());
+  auto out = torch::empty({M, N3}, W1.options());
+  check_hip(dtfs::launch_bottom_mlp3(wts ? wts->data_ptr<float>() : nullptr, wts ? wts->stride(0) : 0, int(nd),
+                                     int(M), W1.data_ptr(), b1.data_ptr<float>(), int(W1.size(0)), W2.data_ptr(),
+                                     b2.data_ptr<float>(), int(W2.size(0)), W3.data_ptr(), b3.data_ptr<float>(),
+                                     int(N3), out.data_ptr(), N3, cur_stream(wts_),
+                                     arena ? arena->data_ptr() : nullptr),
             "bottom_mlp3");
+  return out;
+}
+
+torch::Tensor bottom_mlp3(torch::Tensor wts, int64_t nd, torch::Tensor W1, torch::Tensor b1, torch::Tensor W2,
+                          torch::Tensor b2, torch::Tensor W3, torch::Tensor b3) {
+  return bottom_mlp3_impl(&wts, nullptr, wts.size(0), nd, W1, b1, W2, b2, W3, b3);
+}
+
+torch::Tensor bottom_mlp3_arena(torch::Tensor arena, int64_t B, int64_t nd, torch::Tensor W1, torch::Tensor b1,
+                                torch::Tensor W2, torch::Tensor b2, torch::Tensor W3, torch::Tensor b3) {
+  return bottom_mlp3_impl(nullptr, &arena, B, nd, W1, b1, W2, b2, W3, b3);
+}
+
+// the dot interaction with its ids read from a device request arena (features
+// id_col0 .. id_col0 + T - 1 of each row)
+torch::Tensor dot_interaction_gather_arena(torch::Tensor dense, torch::Tensor table, torch::Tensor arena,
+                                           int64_t id_col0, torch::Tensor modulo_f, torch::Tensor offset_f,
+                                           int64_t out_cols) {
+  check_dev(dense, "dense");
+  check_same_dev(dense, table, "table");
+  check_same_dev(dense, arena, "arena");
+  TORCH_CHECK(arena.scalar_type() == torch::kUInt8 && arena.is_contiguous(), "arena must be a contiguous uint8 buffer");
+  TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && table.scalar_type() == torch::kBFloat16, "bf16 inputs");
+  TORCH_CHECK(dense.dim() == 2 && dense.size(1) == 64, "dense must be [B, 64]");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == 64 && table.is_contiguous(), "table must be contiguous [V, 64]");
+  const int64_t B = dense.size(0), T = modulo_f.numel();
+  for (auto* t : {&modulo_f, &offset_f}) {
+    check_same_dev(dense, *t, "table map");
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == T && t->is_contiguous(), "modulo_f / offset_f: int64 [T]");
+  }
+  TORCH_CHECK(T >= 1 && T + 1 <= 32 && id_col0 >= 0, "1 <= T <= 31 tables, id_col0 >= 0");
+  const int64_t used = 64 + (T + 1) * T / 2;
+  if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
+  TORCH_CHECK(out_cols >= used && out_cols % 8 == 0 && out_cols <= 1024, "out_cols: >= used, a multiple of 8, <= 1024");
+  c10::DeviceGuard g(dense.device());
+  auto out = torch::empty({B, out_cols}, dense.options());
+  check_hip(dtfs::launch_dot_interaction_gather(dense.data_ptr(), 64, table.data_ptr(), table.size(0), nullptr, true, 0,
+                                                modulo_f.data_ptr<int64_t>(), offset_f.data_ptr<int64_t>(), int(T),
+                                                int(B), out.data_ptr(), out_cols, int(out_cols), cur_stream(dense),
+                                                arena.data_ptr(), int(id_col0)),
+            "dot_interaction_gather_arena");
   return out;
 }
 
@@ -1212,6 +1262,10 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);
   m.def("bottom_mlp3", &bottom_mlp3, py::arg("wts"), py::arg("nd"), py::arg("W1"), py::arg("b1"), py::arg("W2"),
         py::arg("b2"), py::arg("W3"), py::arg("b3"));
+  m.def("bottom_mlp3_arena", &bottom_mlp3_arena, py::arg("arena"), py::arg("B"), py::arg("nd"), py::arg("W1"),
+        py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("W3"), py::arg("b3"));
+  m.def("dot_interaction_gather_arena", &dot_interaction_gather_arena, py::arg("dense"), py::arg("table"),
+        py::arg("arena"), py::arg("id_col0"), py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);
   m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
         py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,

@@ -79,15 +79,24 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* p) {
 // row_table_off @16 ({ids_off, wts_off} int32 per row, payload-relative).
 // A row whose ids_off has bit 31 set was narrowed by the host while it copied
 // the request (runtime/narrow.h): int32 table rows + fp32 weights, aligned.
+// Header @36 (int32 narrow_wcols): > 0 = a narrowed row carries only its
+// first narrow_wcols weights (the model reads no others); the rest read as 0.
+constexpr int kArenaAllWeights = 1 << 30;
+__device__ __forceinline__ int arena_narrow_wcols(const uint8_t* arena) {
+  const int w = *reinterpret_cast<const int32_t*>(arena + 36);
+  return w > 0 ? w : kArenaAllWeights;
+}
+
 struct ArenaRow {
   const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: 4 * F of int32 rows), or nullptr (padding row)
-  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 4-byte aligned)
+  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 4 * wcols, 4-byte aligned)
   bool narrow;
+  int wcols;  // narrow rows: weights present (arena_narrow_wcols)
 };
 
 __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payload_off, int64_t r) {
   const int64_t total = *reinterpret_cast<const int64_t*>(arena + 8);
-  ArenaRow out{nullptr, nullptr, false};
+  ArenaRow out{nullptr, nullptr, false, kArenaAllWeights};
   if (r < total) {
     const uint8_t* payload = arena + payload_off;
     const int64_t rt = *reinterpret_cast<const int64_t*>(arena + 16);
@@ -95,6 +104,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
     out.narrow = o.x < 0;
     out.ids = payload + (o.x & 0x7fffffff);
     out.wts = payload + o.y;
+    if (out.narrow) out.wcols = arena_narrow_wcols(arena);
   }
   return out;
 }
@@ -103,7 +113,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
 __device__ __forceinline__ void arena_feature(const ArenaRow& ar, int f, int64_t& id, float& w) {
   if (ar.narrow) {
     id = int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
-    w = reinterpret_cast<const float*>(ar.wts)[f];
+    w = f < ar.wcols ? reinterpret_cast<const float*>(ar.wts)[f] : 0.f;
   } else {
     id = int64_t(load_u64_unaligned(ar.ids + 8 * f));
     w = __uint_as_float(load_u32_unaligned(ar.wts + 4 * f));

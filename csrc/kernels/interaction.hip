@@ -146,7 +146,8 @@ template <typename IdT>
 __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
     const bf16* __restrict__ dense, int64_t ldd, const bf16* __restrict__ table, int64_t table_rows,
     const IdT* __restrict__ ids, int64_t ldi, const int64_t* __restrict__ modulo_f,
-    const int64_t* __restrict__ offset_f, int T, int B, bf16* __restrict__ out, int64_t ldo, int out_cols) {
+    const int64_t* __restrict__ offset_f, int T, int B, bf16* __restrict__ out, int64_t ldo, int out_cols,
+    const uint8_t* __restrict__ arena, int id_col0) {
   constexpr int D = 64;
   constexpr int ROWB = 4 * 2048;  // LDS bytes per block: 4 waves x one output row (<= 1024 columns)
   __shared__ __attribute__((aligned(16))) uint8_t lds[ROWB];
@@ -159,7 +160,15 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
   if (r >= 1 && r < nv) {
     const int t = r - 1;
     const int64_t m = modulo_f[t];
-    int64_t v = int64_t(ids[int64_t(b) * ldi + t]) % m;
+    int64_t id = 0;
+    if (arena) {  // the request arena's row b (K0 fused: no unpack pass); padding rows read id 0
+      const ArenaRow ar = arena_row(arena, kArenaPayloadOff, b);
+      float w;
+      if (ar.ids) arena_feature(ar, id_col0 + t, id, w);
+    } else {
+      id = int64_t(ids[int64_t(b) * ldi + t]);
+    }
+    int64_t v = id % m;
     if (v < 0) v += m;
     row = min(offset_f[t] + v, table_rows - 1);
   }
@@ -255,7 +264,8 @@ __global__ void __launch_bounds__(256) bottom_mlp3_kernel(const float* __restric
                                                           const bf16* __restrict__ W1, const float* __restrict__ b1,
                                                           const bf16* __restrict__ W2, const float* __restrict__ b2,
                                                           const bf16* __restrict__ W3, const float* __restrict__ b3,
-                                                          bf16* __restrict__ out, int64_t ldo) {
+                                                          bf16* __restrict__ out, int64_t ldo,
+                                                          const uint8_t* __restrict__ arena) {
   constexpr int BM = 32, K0 = 64;
   constexpr int PX = K0 * 2 + 16, P1 = N1 * 2 + 16, P2 = N2 * 2 + 16;
   __shared__ __attribute__((aligned(16))) uint8_t lds[BM * (PX + P1 + P2)];
@@ -268,8 +278,19 @@ __global__ void __launch_bounds__(256) bottom_mlp3_kernel(const float* __restric
     const int row = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
     const int64_t m = min(m0 + row, M - 1);
     bf16x8 v;
+    if (arena) {  // dense features = the first nd weights of the arena row (padding rows: 0)
+      const ArenaRow ar = arena_row(arena, kArenaPayloadOff, m);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = f2bf(c0 + e < nd ? wts[m * ldw + c0 + e] : 0.f);
+      for (int e = 0; e < 8; ++e) {
+        int64_t id;
+        float w = 0.f;
+        if (ar.ids && c0 + e < nd) arena_feature(ar, c0 + e, id, w);
+        v[e] = f2bf(w);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(c0 + e < nd ? wts[m * ldw + c0 + e] : 0.f);
+    }
     *reinterpret_cast<bf16x8*>(X + row * PX + c0 * 2) = v;
   }
   __syncthreads();
@@ -504,33 +525,37 @@ hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* em
 hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
                                          const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
                                          const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
-                                         hipStream_t st) {
+                                         hipStream_t st, const void* arena, int id_col0) {
   if (B == 0) return hipSuccess;
   if (T < 1 || T + 1 > 32 || out_cols % 8 || out_cols > 1024 || out_cols < 64 + (T + 1) * T / 2 || ldo % 8 ||
-      ldo < out_cols || ldd % 8 || ldi < T || table_rows < 1 || !modulo_f || !offset_f)
+      ldo < out_cols || ldd % 8 || (!arena && (!ids || ldi < T)) || (arena && id_col0 < 0) || table_rows < 1 ||
+      !modulo_f || !offset_f)
     return hipErrorInvalidValue;
+  const uint8_t* ar = static_cast<const uint8_t*>(arena);
   dim3 grid((B + 3) / 4), block(256);
   if (ids64)
     hipLaunchKernelGGL(dot_interact_gather_kernel<int64_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
                        static_cast<const bf16*>(table), table_rows, static_cast<const int64_t*>(ids), ldi, modulo_f,
-                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols);
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0);
   else
     hipLaunchKernelGGL(dot_interact_gather_kernel<int32_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
                        static_cast<const bf16*>(table), table_rows, static_cast<const int32_t*>(ids), ldi, modulo_f,
-                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols);
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0);
   return hipGetLastError();
 }
 
 hipError_t launch_bottom_mlp3(const float* wts, int64_t ldw, int nd, int M, const void* W1, const float* b1, int N1,
                               const void* W2, const float* b2, int N2, const void* W3, const float* b3, int N3,
-                              void* out, int64_t ldo, hipStream_t st) {
+                              void* out, int64_t ldo, hipStream_t st, const void* arena) {
   if (M == 0) return hipSuccess;
-  if (nd < 1 || nd > 64 || ldw < nd || ldo < N3 || ldo % 4 || !W1 || !W2 || !W3 || !b1 || !b2 || !b3)
+  if (nd < 1 || nd > 64 || (!arena && (!wts || ldw < nd)) || ldo < N3 || ldo % 4 || !W1 || !W2 || !W3 || !b1 ||
+      !b2 || !b3)
     return hipErrorInvalidValue;
   if (N1 == 512 && N2 == 256 && N3 == 64) {  // DLRM bottom_mlp [512, 256, 64]
     hipLaunchKernelGGL((bottom_mlp3_kernel<512, 256, 64>), dim3((M + 31) / 32), dim3(256), 0, st, wts, ldw, nd, M,
                        static_cast<const bf16*>(W1), b1, static_cast<const bf16*>(W2), b2,
-                       static_cast<const bf16*>(W3), b3, static_cast<bf16*>(out), ldo);
+                       static_cast<const bf16*>(W3), b3, static_cast<bf16*>(out), ldo,
+                       static_cast<const uint8_t*>(arena));
     return hipGetLastError();
   }
   return hipErrorInvalidValue;

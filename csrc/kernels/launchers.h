@@ -198,18 +198,21 @@ hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 // K1 + K5: DLRM dot interaction with the one-hot gather fused in: vector t+1
 // of row b is table[offset_f[t] + ids[b * ldi + t] mod modulo_f[t]] (rows
 // clamped to the table); out [B][ldo] = [dense | lower triangle | zeros].
+// arena (a device request arena): the ids are features id_col0 .. id_col0 +
+// T - 1 of arena row b instead (ids unused).
 hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
                                          const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
                                          const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
-                                         hipStream_t st);
+                                         hipStream_t st, const void* arena = nullptr, int id_col0 = 0);
 
 // K4 (small) for the DLRM bottom MLP: relu(relu(relu(pad64(bf16(wts[:, :nd]))
 // W1^T + b1) W2^T + b2) W3^T + b3) in one kernel (W1 [N1][64], W2 [N2][N1], W3
-// [N3][N2] bf16; out bf16 [M][ldo]). Built for (N1, N2, N3) = (512, 256, 64);
+// [N3][N2] bf16; out bf16 [M][ldo]; arena: the weights are the first nd
+// features of each request-arena row instead). Built for (N1, N2, N3) = (512, 256, 64);
 // hipErrorInvalidValue for other shapes.
 hipError_t launch_bottom_mlp3(const float* wts, int64_t ldw, int nd, int M, const void* W1, const float* b1, int N1,
                               const void* W2, const float* b2, int N2, const void* W3, const float* b3, int N3,
-                              void* out, int64_t ldo, hipStream_t st);
+                              void* out, int64_t ldo, hipStream_t st, const void* arena = nullptr);
 
 // K7: bitonic sort of n <= sort_max_elems() scores; first k_out of (sorted, perm).
 int sort_max_elems();

@@ -114,6 +114,7 @@ inline LiveConfig live_config_from(const py::dict& d) {
   if (get("step_timeout_us")) c.step_timeout_us = d["step_timeout_us"].cast<int64_t>();
   if (get("start_paused")) c.start_paused = d["start_paused"].cast<bool>();
   if (get("narrow_modulo")) c.narrow_modulo = d["narrow_modulo"].cast<int64_t>();
+  if (get("narrow_wts_cols")) c.narrow_wts_cols = d["narrow_wts_cols"].cast<int64_t>();
   return c;
 }
 

@@ -58,6 +58,8 @@ LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pa
   // narrow_ids' AVX2 path multiplies with the low 32 bits of the modulo
   if (cfg_.narrow_modulo < 0 || cfg_.narrow_modulo >= (int64_t(1) << 31))
     throw std::invalid_argument("narrow_modulo must be in [0, 2^31)");
+  if (cfg_.narrow_wts_cols < 0 || cfg_.narrow_wts_cols > cfg_.fields)
+    throw std::invalid_argument("narrow_wts_cols must be in [0, fields]");
   paused_ = cfg_.start_paused;
   launcher_ = std::thread([this] { launcher_loop(); });
   completer_ = std::thread([this] { completer_loop(); });
@@ -150,7 +152,8 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
       wts_src = tw->packed[0].p;
   }
   const bool narrow = ids_src && wts_src;
-  const int64_t need = narrow ? align64(4 * ne) + align64(4 * ne) + 8 * rows + 256 : need_of(int64_t(n), rows);
+  const int64_t wcols = cfg_.narrow_wts_cols > 0 ? cfg_.narrow_wts_cols : cfg_.fields;  // narrow weights kept per row
+  const int64_t need = narrow ? align64(4 * ne) + align64(4 * rows * wcols) + 8 * rows + 256 : need_of(int64_t(n), rows);
   if (need > arena_budget_) return reject(kOversize, "request does not fit one arena");
 
   const int64_t t0 = now_us();
@@ -215,7 +218,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
       p.narrow = true;
       p.ids_off = align64(o.used);
       p.wts_off = align64(p.ids_off + 4 * ne);
-      o.used = p.wts_off + 4 * ne;
+      o.used = p.wts_off + 4 * rows * wcols;
       ++st_.narrowed;
     } else {
       off = p.off = o.used;
@@ -243,7 +246,12 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   uint8_t* payload = arenas_[size_t(a)].base + kArenaPayloadOff;
   if (narrow) {  // ... narrowed on the way (K0 on the host)
     narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
-    std::memcpy(payload + pend_wts, wts_src, size_t(4 * ne));  // fp32 weights travel as they are
+    if (wcols == cfg_.fields) {
+      std::memcpy(payload + pend_wts, wts_src, size_t(4 * ne));  // fp32 weights travel as they are
+    } else {  // only the weight columns the model reads
+      for (int64_t r = 0; r < rows; ++r)
+        std::memcpy(payload + pend_wts + 4 * r * wcols, wts_src + 4 * r * cfg_.fields, size_t(4 * wcols));
+    }
   } else {
     std::memcpy(payload + off, data, n);
   }
@@ -506,7 +514,7 @@ void LiveServer::launcher_loop() {
     try {
       trace::Range tr("live_build");
       batch = arena_build_items(ar.base, ar.capacity, items, cfg_.ids_key, cfg_.wts_key, cfg_.fields, max_rows_,
-                                cfg_.varint_chunks);
+                                cfg_.varint_chunks, cfg_.narrow_wts_cols);
     } catch (const std::exception& e) {
       fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
       if (ctl_) {  // the other ranks launch step k: this rank cannot skip it

@@ -112,6 +112,11 @@ struct LiveConfig {
   // ids -> int32 rows (id mod narrow_modulo: the model's table size), weights
   // -> bf16. Halves the H2D bytes; other encodings travel raw.
   int64_t narrow_modulo = 0;
+  // > 0 (narrowed requests only): keep just the first narrow_wts_cols weights
+  // of each row - the model reads no others (one-hot DLRM: the dense
+  // features; its sparse fields' weights are unused). Fewer H2D bytes; the
+  // arena header tells the GPU readers, which see 0 for the dropped columns.
+  int64_t narrow_wts_cols = 0;
   // output keys the signature has besides output_key that only the caller's
   // general path produces: a request naming one in output_filter gets
   // kCallerPath instead of INVALID_ARGUMENT

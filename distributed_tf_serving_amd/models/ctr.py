@@ -403,24 +403,43 @@ class DLRM(CTRModel):
         z = ops.dot_interaction(dense_out, emb, self.inter_cols)
         return self.top.forward_head(z, self.head_w, self.head_b, out=out)
 
-    def bottom_out(self, wts: torch.Tensor) -> torch.Tensor:
+    def _bottom_fused(self) -> bool:
+        L = self.bottom.layers
+        return (self.dtype == torch.bfloat16 and self.dense_k == 64
+                and tuple(l.out_dim for l in L) == ops.BOTTOM_MLP3_DIMS and all(l.act == "relu" for l in L)
+                and not any(l.fp8 for l in L))
+
+    def bottom_out(self, wts) -> torch.Tensor:
         """Bottom MLP over the dense features: one fused kernel on the GPU for
         the 512-256-64 tower (pad + 3 GEMMs were ~31 us of mostly launch /
-        prologue per 16384-row step), else layer by layer."""
+        prologue per 16384-row step), else layer by layer. ``wts`` may be
+        :class:`ops.ArenaRows` (fused path only)."""
         L = self.bottom.layers
-        if (wts.is_cuda and wts.dtype == torch.float32 and self.dtype == torch.bfloat16 and self.dense_k == 64
-                and tuple(l.out_dim for l in L) == ops.BOTTOM_MLP3_DIMS and all(l.act == "relu" for l in L)
-                and not any(l.fp8 for l in L)):
+        if isinstance(wts, ops.ArenaRows) or (wts.is_cuda and wts.dtype == torch.float32 and self._bottom_fused()):
             return ops.bottom_mlp3(wts, self.cfg.num_dense, [(l.weight, l.bias) for l in L])
         return self.bottom(self.dense_input(wts))
 
+    def narrow_weight_cols(self) -> int:
+        """Leading feat_wts columns the forward reads: one-hot DLRM reads only
+        the dense features (its sparse lookups are unweighted), so host-narrowed
+        requests carry just those (serving/live.py); 0 = all."""
+        return self.cfg.num_dense if self.hot == 1 else 0
+
+    @property
+    def supports_arena(self) -> bool:
+        """One-hot, local tables, the fused bottom tower: the step reads the
+        request arena itself (no unpack pass: K0 fused into the bottom MLP
+        and the interaction's gather)."""
+        return self.hot == 1 and self.emb is not None and self._bottom_fused()
+
     def _forward(self, ids, wts, out=None):
-        dense_out = self.bottom_out(wts)
-        if self.hot == 1 and self.emb is not None and ids.is_cuda:
+        arena = isinstance(ids, ops.ArenaRows)
+        dense_out = self.bottom_out(ids if arena else wts)
+        if self.hot == 1 and self.emb is not None and (arena or ids.is_cuda):
             # one-hot, local tables: the interaction kernel looks the rows up
             # itself (no [B, T, 64] embedding round trip through HBM)
-            z = ops.dot_interaction_gather(dense_out, self.emb, self.sparse_ids(ids), self.modulo_f, self.offset_f,
-                                           self.inter_cols)
+            z = ops.dot_interaction_gather(dense_out, self.emb, ids if arena else self.sparse_ids(ids), self.modulo_f,
+                                           self.offset_f, self.inter_cols, id_col0=self.cfg.num_dense)
             return self.top.forward_head(z, self.head_w, self.head_b, out=out)
         emb = self.lookup(ids, wts)
         return self.interact_and_top(dense_out, emb, out=out)

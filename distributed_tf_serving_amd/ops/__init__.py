@@ -490,14 +490,20 @@ def dot_interaction(dense: torch.Tensor, emb: torch.Tensor, out_cols: int = 0,
     return out.to(dense.dtype)
 
 
-def dot_interaction_gather(dense: torch.Tensor, table: torch.Tensor, ids: torch.Tensor, modulo_f: torch.Tensor,
-                           offset_f: torch.Tensor, out_cols: int = 0) -> torch.Tensor:
+def dot_interaction_gather(dense: torch.Tensor, table: torch.Tensor, ids, modulo_f: torch.Tensor,
+                           offset_f: torch.Tensor, out_cols: int = 0, id_col0: int = 0) -> torch.Tensor:
     """K1 fused into K5 (one-hot DLRM, local tables): dot_interaction(dense,
     table[offset_f + ids mod modulo_f]) without the [B, T, 64] embedding
-    intermediate. ``ids``: int32/int64 [B, T] rows (a row view is fine)."""
-    T = ids.shape[1]
+    intermediate. ``ids``: int32/int64 [B, T] rows (a row view is fine), or
+    :class:`ArenaRows` whose features id_col0 .. id_col0 + T - 1 are the ids."""
+    T = int(modulo_f.numel())
     if out_cols <= 0:
         out_cols = interaction_cols(T, dense.shape[1])
+    if isinstance(ids, ArenaRows):
+        if ids.arena.is_cuda:
+            return hip().dot_interaction_gather_arena(dense, table, ids.arena, int(id_col0), modulo_f, offset_f,
+                                                      int(out_cols))
+        ids = _arena_unpack_host(ids)[0][:, id_col0:id_col0 + T]
     if dense.is_cuda:
         return hip().dot_interaction_gather(dense, table, _rows(ids), modulo_f, offset_f, int(out_cols))
     rows = _hash_rows(ids, 0, modulo_f, offset_f).clamp(0, table.shape[0] - 1)
@@ -513,6 +519,10 @@ def bottom_mlp3(wts: torch.Tensor, nd: int, layers) -> torch.Tensor:
     feature columns wts[:, :nd] (bf16, zero padded to 64). ``layers``: three
     (weight bf16 [N, K], bias fp32 [N]) pairs. bf16 [M, 64]."""
     (W1, b1), (W2, b2), (W3, b3) = layers
+    if isinstance(wts, ArenaRows):  # the dense features straight from the request arena
+        if wts.arena.is_cuda:
+            return hip().bottom_mlp3_arena(wts.arena, int(wts.B), int(nd), W1, b1, W2, b2, W3, b3)
+        wts = _arena_unpack_host(wts)[1]
     if wts.is_cuda:
         return hip().bottom_mlp3(_rows(wts), int(nd), W1, b1, W2, b2, W3, b3)
     x = torch.zeros(wts.shape[0], W1.shape[1], dtype=torch.bfloat16)

@@ -79,6 +79,10 @@ class LiveScheduler:
         if narrow is None:  # default: GPU servables (a CPU backend gains nothing from fewer bytes)
             narrow = bool(getattr(sc, "narrow_ingest", True)) and engine.cuda
         self.narrow_modulo = m if narrow else 0
+        # ... and models that read only the leading weight columns (one-hot
+        # DLRM: the dense features) get only those copied (fewer H2D bytes)
+        wc = int(getattr(model, "narrow_weight_cols", lambda: 0)()) if self.narrow_modulo else 0
+        self.narrow_wts_cols = wc if 0 < wc < self.fields else 0
         self.arenas = [self.layout.alloc(pin=engine.cuda) for _ in range(int(n_arenas or depth + 3))]
         self.config = dict(
             fields=self.fields, ids_key=sc.ids_key, wts_key=sc.wts_key, model_name=self.model_name,
@@ -88,7 +92,7 @@ class LiveScheduler:
             depth=depth, varint_chunks=self.layout.varint_chunks,
             max_pending=max(64, sc.max_queued_rows // max(1, min(self.buckets))),
             step_timeout_us=int(step_timeout_s * 1e6), peer_timeout_us=int(peer_timeout_s * 1e6),
-            start_paused=start_paused, narrow_modulo=self.narrow_modulo,
+            start_paused=start_paused, narrow_modulo=self.narrow_modulo, narrow_wts_cols=self.narrow_wts_cols,
             caller_outputs=["sorted_prediction", "sorted_index"])  # service.RANKED_OUTPUTS
         if engine.cuda:
             from ..ops import hip

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-case ${MODEL:-deepfm} in deepfm|wdl|dcn) sk="gemm_gather --min-us 80";; dlrm) sk="dense_pad --min-us 4";; *) sk="embed_pipe --min-us 30";; esac
+case ${MODEL:-deepfm} in deepfm|wdl|dcn) sk="gemm_gather --min-us 80";; dlrm) sk="bottom_mlp3 --min-us 14";; *) sk="embed_pipe --min-us 30";; esac
 for v in $AB_VALUES; do
   d=gpurun_out/profab_${MODEL}_$v
   rm -rf $d

@@ -59,7 +59,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
       -- python3 bench.py --model $pm --steps 100 --warmup 10 --qps 0 > gpurun_out/prof_$pm.log 2>&1 \
       || { echo "prof $pm failed"; tail -30 gpurun_out/prof_$pm.log; exit 1; }
     db=$(find gpurun_out/prof_$pm -name '*.db' | head -1)
-    case $pm in deepfm|wdl|dcn) sk="gemm_gather --min-us 80";; dlrm) sk="dense_pad --min-us 4";; *) sk="embed_pipe --min-us 30";; esac
+    case $pm in deepfm|wdl|dcn) sk="gemm_gather --min-us 80";; dlrm) sk="bottom_mlp3 --min-us 14";; *) sk="embed_pipe --min-us 30";; esac
     python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} --step-kernel $sk \
       --title "bench.py live path ($pm, default step shape), 1 MI355X" > gpurun_out/prof_summary_$pm.md \
       && head -30 gpurun_out/prof_summary_$pm.md

@@ -576,15 +576,20 @@ def test_unpack_arena_narrow_matches_cpu(cuda):
     assert torch.equal(got.cpu(), ref)
 
 
-@pytest.mark.parametrize("family", ["deepfm", "wdl", "dcn", "dcn_v2"])
+@pytest.mark.parametrize("family", ["deepfm", "wdl", "dcn", "dcn_v2", "dlrm"])
 def test_forward_arena_matches_packed(cuda, family):
     # K0 fused into K1: the gather reads ids / weights from the raw request bytes
+    # (DLRM: the fused bottom MLP reads the dense features, the fused
+    # interaction the sparse ids)
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.serving.arena import ArenaLayout
     from distributed_tf_serving_amd.serving.packing import PackedLayout
 
     cfg = ModelConfig(family=family, vocab_size=20_000)
+    if family == "dlrm":
+        cfg.table_rows = 5000
     m = build_model(cfg, cuda)
+    assert m.supports_arena
     A, L = ArenaLayout(43, 2048), PackedLayout(43)
     ar = A.alloc()
     s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=9)

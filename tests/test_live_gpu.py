@@ -150,3 +150,39 @@ def test_gather_gemm_served_steps_match_eager_forward():
         assert st["narrowed"] > 0 and not st["broken"]
     finally:
         srv.stop()
+
+
+def test_one_hot_dlrm_served_from_narrow_arena_matches_eager():
+    """One-hot DLRM on the GPU live server: host-narrowed requests carry only
+    the 13 dense weights, the fused bottom MLP and the fused gather +
+    interaction read the arena directly, and the scores equal the eager
+    forward of the full request (raw and packed encodings)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distributed_tf_serving_amd.config import ModelConfig
+
+    cfg = load_preset("deepfm_1gpu")
+    cfg.model = ModelConfig(family="dlrm", table_rows=20_000)
+    cfg.serving.max_batch_rows = 2048
+    cfg.serving.allowed_batch_sizes = (256, 2048)
+    srv = ModelServer(cfg, device="cuda:0")
+    try:
+        s = srv.registry.resolve("DCN")
+        live, model = s.scheduler, s.model
+        assert isinstance(live, LiveScheduler) and model.supports_arena
+        assert live.narrow_wts_cols == 13
+        synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=23)
+        reqs = []
+        for i in range(20):
+            ids, wts = synth.arrays([512, 1, 100, 37, 300][i % 5])
+            t = [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))]
+            reqs.append((native().encode_predict_request("DCN", "serving_default", None, t, i % 2 == 0), ids, wts))
+        with cf.ThreadPoolExecutor(8) as pool:
+            outs = list(pool.map(lambda r: srv.service.predict_bytes(r[0], 30.0), reqs))
+        for (data, ids, wts), resp in zip(reqs, outs):
+            want = model(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+            np.testing.assert_allclose(_scores(resp), want, atol=2e-5)
+        st = live.stats()
+        assert st["narrowed"] > 0 and not st["broken"]
+    finally:
+        srv.stop()

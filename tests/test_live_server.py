@@ -314,3 +314,33 @@ def test_live_server_narrowed_ingest_matches_fp32_forward_for_every_encoding():
         np.testing.assert_allclose(_scores(r_packed), want32, atol=1e-5)   # packed varint ids travel raw
     assert live.stats()["narrowed"] == len(reqs)
     live.close()
+
+
+def test_live_server_narrow_weight_columns_for_one_hot_dlrm():
+    """One-hot DLRM reads only its 13 dense weights: host-narrowed requests
+    carry just those (the arena header tells the readers), and the served
+    scores still equal the fp32 forward of the full request, raw and packed
+    encodings alike."""
+    from distributed_tf_serving_amd.config import ModelConfig
+
+    cfg = _cfg(max_rows=64, buckets=(8, 64))
+    cfg.model = ModelConfig(family="dlrm", table_rows=5000, param_dtype="fp32")
+    eng = _engine(cfg)
+    live = LiveScheduler(eng, cfg.serving, narrow=True)
+    assert live.narrow_modulo == 5000 and live.narrow_wts_cols == 13
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=13)
+    model = eng.ex.model
+    reqs = []
+    for rows in (1, 7, 33, 64):
+        ids, wts = synth.arrays(rows)
+        t = [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))]
+        reqs.append((native().encode_predict_request("DCN", "", None, t, True),
+                     native().encode_predict_request("DCN", "", None, t, False), ids, wts))
+    with cf.ThreadPoolExecutor(4) as pool:
+        outs = list(pool.map(lambda r: (live.predict_bytes(r[0], 10.0), live.predict_bytes(r[1], 10.0)), reqs))
+    for (raw, packed, ids, wts), (r_raw, r_packed) in zip(reqs, outs):
+        want = model(torch.from_numpy(ids), torch.from_numpy(wts)).numpy()
+        np.testing.assert_allclose(_scores(r_raw), want, atol=1e-5)
+        np.testing.assert_allclose(_scores(r_packed), want, atol=1e-5)
+    assert live.stats()["narrowed"] == len(reqs)
+    live.close()
