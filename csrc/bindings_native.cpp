@@ -664,6 +664,18 @@ PYBIND11_MODULE(_native, m) {
         return out;
       },
       py::arg("ids"), py::arg("modulo"), "Host K0: int64 ids -> int32 rows (python-style id mod modulo).");
+  m.def(
+      "narrow_ids24",
+      [](torch::Tensor ids, int64_t modulo) {
+        TORCH_CHECK(ids.device().is_cpu() && ids.scalar_type() == torch::kInt64, "ids must be CPU int64");
+        TORCH_CHECK(modulo >= 1 && modulo <= (int64_t(1) << 24), "modulo must be in [1, 2^24]");
+        auto src = ids.contiguous();
+        auto out = torch::empty({3 * src.numel() + runtime::kNarrow24Slack}, torch::kUInt8);
+        runtime::narrow_ids24(reinterpret_cast<const uint8_t*>(src.data_ptr()), out.data_ptr<uint8_t>(), src.numel(),
+                              modulo);
+        return out.narrow(0, 0, 3 * src.numel());
+      },
+      py::arg("ids"), py::arg("modulo"), "Host K0: int64 ids -> 3-byte little-endian rows (id mod modulo <= 2^24).");
   m.def("now_us", &runtime::now_us);
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));

@@ -87,16 +87,29 @@ __device__ __forceinline__ int arena_narrow_wcols(const uint8_t* arena) {
   return w > 0 ? w : kArenaAllWeights;
 }
 
+// Header @40 (int32): 3 = narrowed rows hold packed 3-byte table rows.
+__device__ __forceinline__ int arena_narrow_idb(const uint8_t* arena) {
+  return *reinterpret_cast<const int32_t*>(arena + 40) == 3 ? 3 : 4;
+}
+
 struct ArenaRow {
-  const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: 4 * F of int32 rows), or nullptr (padding row)
+  const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: idb * F bytes of rows), or nullptr (padding row)
   const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 4 * wcols, 4-byte aligned)
   bool narrow;
   int wcols;  // narrow rows: weights present (arena_narrow_wcols)
+  int idb;    // narrow rows: bytes per id (arena_narrow_idb)
 };
+
+// Table row of feature f of a narrowed row: int32, or 3 packed bytes (the
+// 4-byte load of the last one stays inside the arena's slack)
+__device__ __forceinline__ int64_t arena_narrow_id(const ArenaRow& ar, int f) {
+  if (ar.idb == 3) return int64_t(load_u32_unaligned(ar.ids + 3 * f) & 0xffffffu);
+  return int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
+}
 
 __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payload_off, int64_t r) {
   const int64_t total = *reinterpret_cast<const int64_t*>(arena + 8);
-  ArenaRow out{nullptr, nullptr, false, kArenaAllWeights};
+  ArenaRow out{nullptr, nullptr, false, kArenaAllWeights, 4};
   if (r < total) {
     const uint8_t* payload = arena + payload_off;
     const int64_t rt = *reinterpret_cast<const int64_t*>(arena + 16);
@@ -104,7 +117,10 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
     out.narrow = o.x < 0;
     out.ids = payload + (o.x & 0x7fffffff);
     out.wts = payload + o.y;
-    if (out.narrow) out.wcols = arena_narrow_wcols(arena);
+    if (out.narrow) {
+      out.wcols = arena_narrow_wcols(arena);
+      out.idb = arena_narrow_idb(arena);
+    }
   }
   return out;
 }
@@ -112,7 +128,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
 // Feature f of an arena row: raw int64 id (narrow: int32 row) and fp32 weight.
 __device__ __forceinline__ void arena_feature(const ArenaRow& ar, int f, int64_t& id, float& w) {
   if (ar.narrow) {
-    id = int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
+    id = arena_narrow_id(ar, f);
     w = f < ar.wcols ? reinterpret_cast<const float*>(ar.wts)[f] : 0.f;
   } else {
     id = int64_t(load_u64_unaligned(ar.ids + 8 * f));

@@ -261,11 +261,12 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
   const uint8_t* a_payload = nullptr;
   const int2* a_desc = nullptr;
   int64_t a_rows = 0;
-  int a_wcols = kArenaAllWeights;
+  int a_wcols = kArenaAllWeights, a_idb = 4;
   if constexpr (ARENA) {
     const uint8_t* arena = static_cast<const uint8_t*>(a.arena);
     a_rows = *reinterpret_cast<const int64_t*>(arena + 8);
     a_wcols = arena_narrow_wcols(arena);
+    a_idb = arena_narrow_idb(arena);
     a_payload = arena + kArenaPayloadOff;
     a_desc = reinterpret_cast<const int2*>(a_payload + *reinterpret_cast<const int64_t*>(arena + 16));
   }
@@ -277,7 +278,7 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
     id = 0;
     w = 0.f;
     if (!ok) return;
-    const ArenaRow ar{a_payload + (d.x & 0x7fffffff), a_payload + d.y, d.x < 0, a_wcols};
+    const ArenaRow ar{a_payload + (d.x & 0x7fffffff), a_payload + d.y, d.x < 0, a_wcols, a_idb};
     arena_feature(ar, lane, id, w);
   };
   // stage 2: hash -> table row (clamped), weight (0 for rows another shard owns)
@@ -458,11 +459,12 @@ __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_
   const int b0 = blockIdx.x * RB;
   const uint8_t* payload = nullptr;
   int64_t a_rows = 0;
-  int a_wcols = kArenaAllWeights;
+  int a_wcols = kArenaAllWeights, a_idb = 4;
   if constexpr (ARENA) {
     const uint8_t* arena = static_cast<const uint8_t*>(a.arena);
     a_rows = *reinterpret_cast<const int64_t*>(arena + 8);
     a_wcols = arena_narrow_wcols(arena);
+    a_idb = arena_narrow_idb(arena);
     payload = arena + kArenaPayloadOff;
     if (t < RB) {
       const int b = b0 + t;
@@ -483,7 +485,7 @@ __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_
     if constexpr (ARENA) {
       if (b < a.B && b < a_rows) {
         const int2 d = s_desc[r];
-        const ArenaRow ar{payload + (d.x & 0x7fffffff), payload + d.y, d.x < 0, a_wcols};
+        const ArenaRow ar{payload + (d.x & 0x7fffffff), payload + d.y, d.x < 0, a_wcols, a_idb};
         arena_feature(ar, f, id[k], w[k]);
       }
     } else if (b < a.B) {

@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
     for (int c = lane; c < W; c += 64) {
       uint64_t v = 0;
       if (c < F) {
-        v = uint64_t(int64_t(reinterpret_cast<const int32_t*>(src.ids)[c]));
+        v = uint64_t(arena_narrow_id(src, c));
       } else {
         const int f0 = 2 * (c - F);
         const uint32_t* wb = reinterpret_cast<const uint32_t*>(src.wts);

@@ -68,9 +68,11 @@ ArenaBatch arena_build(uint8_t* base, int64_t capacity, const std::vector<Span>&
 
 ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<ArenaItem>& items,
                              const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows,
-                             int64_t varint_chunks, int64_t narrow_wcols) {
+                             int64_t varint_chunks, int64_t narrow_wcols, int64_t narrow_id_bytes) {
   if (int64_t(items.size()) > kArenaMaxRequests) throw std::invalid_argument("too many requests for one arena");
   if (narrow_wcols < 0 || narrow_wcols > fields) throw std::invalid_argument("narrow_wcols must be in [0, fields]");
+  if (narrow_id_bytes != 3 && narrow_id_bytes != 4) throw std::invalid_argument("narrow_id_bytes must be 3 or 4");
+  const int64_t idb = narrow_id_bytes;
   const int64_t wcols = narrow_wcols > 0 ? narrow_wcols : fields;  // weights per narrowed row
   uint8_t* payload = base + kArenaPayloadOff;
   const int64_t cap = capacity - kArenaPayloadOff;
@@ -87,9 +89,9 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
       const int64_t ne = it.rows * fields;
       const int64_t nw = it.rows * wcols;
       if (it.rows < 0 || it.ids_off < 0 || it.wts_off < 0 || it.ids_off % 4 || it.wts_off % 4 ||
-          it.ids_off + 4 * ne > cap || it.wts_off + 4 * nw > cap)
+          it.ids_off + idb * ne + 4 > cap || it.wts_off + 4 * nw > cap)
         throw std::invalid_argument("narrow request outside arena");
-      end = std::max(end, std::max(it.ids_off + 4 * ne, it.wts_off + 4 * nw));
+      end = std::max(end, std::max(it.ids_off + idb * ne + 4, it.wts_off + 4 * nw));  // +4: a reader's 4-byte load of the last 3-byte id
       continue;
     }
     spans[i] = {it.off, it.len};
@@ -311,7 +313,7 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
     if (io & kNarrowFlag) {
       const int64_t ni = io & ~kNarrowFlag;
       for (int64_t r = 0; r < rows; ++r) {
-        tab[2 * (r0 + r) + 0] = int32_t(uint32_t(ni + r * 4 * fields) | 0x80000000u);
+        tab[2 * (r0 + r) + 0] = int32_t(uint32_t(ni + r * idb * fields) | 0x80000000u);
         tab[2 * (r0 + r) + 1] = int32_t(wo + r * 4 * wcols);
       }
       continue;
@@ -327,6 +329,7 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
   *reinterpret_cast<int64_t*>(base + 24) = vt;
   *reinterpret_cast<int32_t*>(base + 32) = int32_t(n_chunks);
   *reinterpret_cast<int32_t*>(base + 36) = int32_t(narrow_wcols);
+  *reinterpret_cast<int32_t*>(base + 40) = int32_t(idb);
   out.total_rows = row;
   out.n_valid = nd;
   out.n_gpu_varint = int64_t(gjobs.size());
@@ -342,6 +345,7 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
   const uint8_t* payload = base + kArenaPayloadOff;
   const int32_t nwc = *reinterpret_cast<const int32_t*>(base + 36);
   const int64_t wcols = nwc > 0 && nwc < fields ? nwc : fields;  // narrowed rows: weights kept per row
+  const int64_t idb = *reinterpret_cast<const int32_t*>(base + 40) == 3 ? 3 : 4;  // narrowed rows: bytes per id
   std::memset(dst, 0, size_t(B * W * 8));
   for (int32_t i = 0; i < n; ++i) {
     const bool narrow = (desc[4 * i + 0] & kNarrowFlag) != 0;
@@ -349,11 +353,15 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
       const int64_t row = desc[4 * i + 3] + r;
       if (row >= B) break;
       if (narrow) {  // int32 rows -> int64, fp32 weights as they are
-        const uint8_t* ip = payload + (desc[4 * i + 0] & ~kNarrowFlag) + r * 4 * fields;
+        const uint8_t* ip = payload + (desc[4 * i + 0] & ~kNarrowFlag) + r * idb * fields;
         const uint8_t* wp = payload + desc[4 * i + 1] + r * 4 * wcols;
         for (int64_t f = 0; f < fields; ++f) {
-          int32_t id;
-          std::memcpy(&id, ip + 4 * f, 4);
+          int32_t id = 0;
+          if (idb == 3) {
+            id = int32_t(uint32_t(ip[3 * f]) | uint32_t(ip[3 * f + 1]) << 8 | uint32_t(ip[3 * f + 2]) << 16);
+          } else {
+            std::memcpy(&id, ip + 4 * f, 4);
+          }
           const int64_t id64 = id;
           std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
         }

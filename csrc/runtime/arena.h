@@ -4,6 +4,7 @@
 //   [0]   int32 n_req      [8] int64 total_rows      [16] int64 row_table_off
 //   [24]  int64 varint_table_off   [32] int32 n_varint_chunks
 //   [36]  int32 narrow_wcols (0: narrowed rows carry all F weights)
+//   [40]  int32 narrow_id_bytes (3: narrowed rows are packed 3-byte rows; else 4)
 //   [64]  n_req x {ids_off, wts_off, rows, dst_row} int64 (offsets into payload)
 //   [kArenaPayloadOff] payload: serialized PredictRequests (+ scratch for
 //                      host-decoded typed fields), then at row_table_off a
@@ -81,12 +82,13 @@ std::vector<Span> arena_place(uint8_t* arena, int64_t capacity, const std::vecto
 ArenaBatch arena_build(uint8_t* arena, int64_t capacity, const std::vector<Span>& spans, const std::string& ids_key,
                        const std::string& wts_key, int64_t fields, int64_t max_rows, int64_t varint_chunks = 0);
 // Same over a mix of serialized and narrowed requests (results in item order).
+// narrow_id_bytes 3: narrowed ids are 3-byte rows (stride 3 F, header @40).
 // narrow_wcols > 0: narrowed requests carry only their rows' first
 // narrow_wcols weights (row stride 4 * narrow_wcols; header @36 records it, and
 // readers see weight 0 for the other columns).
 ArenaBatch arena_build_items(uint8_t* arena, int64_t capacity, const std::vector<ArenaItem>& items,
                              const std::string& ids_key, const std::string& wts_key, int64_t fields, int64_t max_rows,
-                             int64_t varint_chunks = 0, int64_t narrow_wcols = 0);
+                             int64_t varint_chunks = 0, int64_t narrow_wcols = 0, int64_t narrow_id_bytes = 4);
 
 // Host reference of the GPU varint kernel: fills the arena's device-only id
 // region from its chunk table (a no-op when the build decoded on the host).

@@ -153,7 +153,9 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   }
   const bool narrow = ids_src && wts_src;
   const int64_t wcols = cfg_.narrow_wts_cols > 0 ? cfg_.narrow_wts_cols : cfg_.fields;  // narrow weights kept per row
-  const int64_t need = narrow ? align64(4 * ne) + align64(4 * rows * wcols) + 8 * rows + 256 : need_of(int64_t(n), rows);
+  const int64_t idb = narrow_id_bytes();  // 3-byte rows for tables of <= 2^24 rows
+  const int64_t ids_bytes = idb == 3 ? 3 * ne + kNarrow24Slack : 4 * ne;
+  const int64_t need = narrow ? align64(ids_bytes) + align64(4 * rows * wcols) + 8 * rows + 256 : need_of(int64_t(n), rows);
   if (need > arena_budget_) return reject(kOversize, "request does not fit one arena");
 
   const int64_t t0 = now_us();
@@ -217,7 +219,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
     if (narrow) {
       p.narrow = true;
       p.ids_off = align64(o.used);
-      p.wts_off = align64(p.ids_off + 4 * ne);
+      p.wts_off = align64(p.ids_off + ids_bytes);
       o.used = p.wts_off + 4 * rows * wcols;
       ++st_.narrowed;
     } else {
@@ -245,7 +247,8 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
   // the one copy of the request: into pinned memory the DMA engine reads
   uint8_t* payload = arenas_[size_t(a)].base + kArenaPayloadOff;
   if (narrow) {  // ... narrowed on the way (K0 on the host)
-    narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
+    if (idb == 3) narrow_ids24(ids_src, payload + pend_ids, ne, cfg_.narrow_modulo);
+    else narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
     if (wcols == cfg_.fields) {
       std::memcpy(payload + pend_wts, wts_src, size_t(4 * ne));  // fp32 weights travel as they are
     } else {  // only the weight columns the model reads
@@ -514,7 +517,7 @@ void LiveServer::launcher_loop() {
     try {
       trace::Range tr("live_build");
       batch = arena_build_items(ar.base, ar.capacity, items, cfg_.ids_key, cfg_.wts_key, cfg_.fields, max_rows_,
-                                cfg_.varint_chunks, cfg_.narrow_wts_cols);
+                                cfg_.varint_chunks, cfg_.narrow_wts_cols, narrow_id_bytes());
     } catch (const std::exception& e) {
       fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
       if (ctl_) {  // the other ranks launch step k: this rank cannot skip it

@@ -137,6 +137,10 @@ struct LiveStats {
 
 class LiveServer {
  public:
+  // bytes per host-narrowed id: 3 when every row fits 24 bits, else 4
+  int64_t narrow_id_bytes() const {
+    return cfg_.narrow_modulo > 0 && cfg_.narrow_modulo <= (int64_t(1) << 24) ? 3 : 4;
+  }
   // arenas: pinned host buffers of ArenaLayout capacity (>= 2 + depth of them).
   // ctl: cluster mode (every step agreed with the other ranks), or null.
   LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas,

@@ -65,11 +65,51 @@ __attribute__((target("avx2,fma"))) void narrow_ids_avx2(const uint8_t* src, int
 
 const bool g_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
 
+// int32 rows (< 2^24) -> 3 bytes each: per 128-bit lane the low 3 bytes of its
+// 4 rows shuffled to the front (12 bytes), each lane stored as 16 bytes at a
+// 12-byte stride (the next store overwrites the 4 bytes of junk)
+__attribute__((target("avx2"))) void pack24_avx2(const int32_t* rows, uint8_t* dst, int64_t n) {
+  const __m256i shuf = _mm256_setr_epi8(0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -1, -1, -1, -1,
+                                        0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -1, -1, -1, -1);
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    const __m256i v = _mm256_shuffle_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(rows + i)), shuf);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + 3 * i), _mm256_castsi256_si128(v));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + 3 * i + 12), _mm256_extracti128_si256(v, 1));
+  }
+  for (; i < n; ++i) {
+    const uint32_t r = uint32_t(rows[i]);
+    dst[3 * i] = uint8_t(r);
+    dst[3 * i + 1] = uint8_t(r >> 8);
+    dst[3 * i + 2] = uint8_t(r >> 16);
+  }
+}
+
 }  // namespace
 
 void narrow_ids(const uint8_t* src, int32_t* dst, int64_t n, int64_t modulo) {
   if (g_avx2) narrow_ids_avx2(src, dst, n, modulo);
   else narrow_ids_scalar(src, dst, n, modulo);
+}
+
+void narrow_ids24(const uint8_t* src, uint8_t* dst, int64_t n, int64_t modulo) {
+  // in blocks that stay in L1: narrow to int32, then pack
+  constexpr int64_t kBlock = 2048;
+  alignas(32) int32_t tmp[kBlock];
+  for (int64_t i = 0; i < n; i += kBlock) {
+    const int64_t m = n - i < kBlock ? n - i : kBlock;
+    narrow_ids(src + 8 * i, tmp, m, modulo);
+    if (g_avx2) {
+      pack24_avx2(tmp, dst + 3 * i, m);
+    } else {
+      for (int64_t k = 0; k < m; ++k) {
+        const uint32_t r = uint32_t(tmp[k]);
+        dst[3 * (i + k)] = uint8_t(r);
+        dst[3 * (i + k) + 1] = uint8_t(r >> 8);
+        dst[3 * (i + k) + 2] = uint8_t(r >> 16);
+      }
+    }
+  }
 }
 
 }  // namespace runtime

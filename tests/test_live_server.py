@@ -287,6 +287,19 @@ def test_host_narrowing_matches_python():
         assert np.array_equal(got.astype(np.int64), want), m
 
 
+def test_host_narrowing_to_3_byte_rows_matches_python():
+    """runtime/narrow.cpp narrow_ids24 (AVX2 shuffle pack + scalar tail) vs
+    python's modulo, every length mod 8 and across the 2048-id blocks."""
+    rng = np.random.default_rng(5)
+    for n in (1, 7, 8, 9, 2047, 2048, 2049, 5003):
+        vals = rng.integers(-(1 << 62), 1 << 62, size=n, dtype=np.int64)
+        for m in (1, 1_000_000, 1 << 24):
+            got = native().narrow_ids24(torch.from_numpy(vals), m).numpy().reshape(n, 3).astype(np.int64)
+            rows = got[:, 0] | (got[:, 1] << 8) | (got[:, 2] << 16)
+            want = np.array([int(v) % m for v in vals.tolist()], dtype=np.int64)
+            assert np.array_equal(rows, want), (n, m)
+
+
 def test_live_server_narrowed_ingest_matches_fp32_forward_for_every_encoding():
     """Host-narrowed rows (int32 table rows + fp32 weights) and packed varint
     requests score exactly like the fp32 forward: the wire encoding does not
