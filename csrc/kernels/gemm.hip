@@ -97,18 +97,29 @@ __device__ __forceinline__ void store_acc_t(const f32x4 (&acc)[TM][TN], int mb, 
   if (!RAGGED || ((N | int(ldc) | int(ldx)) & 3) == 0) {  // N % 4 == 0: a lane's 4 columns exist together
     // column-tile outer: per j one bias / scale vector, then every row tile's
     // operand loads are issued before the first use (few live registers)
+    // every bias / scale vector of the tile is loaded before the first use:
+    // one memory round trip for the epilogue instead of one per column tile
+    // (tools/native/g8ph_stamps: the 8-phase epilogue took 6.3-8.8 us per
+    // 256x256 tile with the loads inside the column loop)
     float sam[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) sam[i] = (FP8 && sa) ? sa[min(mb + i * 16 + fr, M - 1)] : 1.f;
+    f32x4 b4v[TN], s4v[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nc = min(nb + j * 16 + fq * 4, N - 4);
+      b4v[j] = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
+      s4v[j] = f32x4{1.f, 1.f, 1.f, 1.f};
+      if constexpr (FP8) {
+        if (sw) s4v[j] = *reinterpret_cast<const f32x4*>(sw + nc);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = nb + j * 16 + fq * 4;
       const int nc = min(n, N - 4);
-      const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
-      if constexpr (FP8) {
-        if (sw) s4 = *reinterpret_cast<const f32x4*>(sw + nc);
-      }
+      const f32x4 b4 = b4v[j];
+      const f32x4 s4 = s4v[j];
       bf16x4 x0[TM], xl[TM];
       if (cross) {
 #pragma unroll
@@ -807,16 +818,24 @@ __device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], 
                                                       const bf16* __restrict__ XL, int64_t ldx, const XsArgs& xs) {
   const int fr = lane & 15, fq = lane >> 4;
   __syncthreads();  // both wave groups are past their last K-loop LDS read
+  // scale / bias vectors and, below, the x0 / xl rows are each loaded in one
+  // round trip (a latency-bound epilogue, one tile per CU and nothing else
+  // to run: tools/native/g8ph_stamps)
   float sam[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) sam[i] = (FP8 && sa) ? sa[min(m0 + 128 * wr + 16 * i + fr, M - 1)] : 1.f;
+  f32x4 b4v[4], s4v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nc = min(n0 + 64 * wc + 16 * j + 4 * fq, N - 4);
+    b4v[j] = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s4v[j] = (FP8 && sw) ? *reinterpret_cast<const f32x4*>(sw + nc) : f32x4{1.f, 1.f, 1.f, 1.f};
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = 64 * wc + 16 * j + 4 * fq;  // tile column of this lane's 4 values
-    const int nc = min(n0 + c, N - 4);
-    const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 s4 = f32x4{1.f, 1.f, 1.f, 1.f};
-    if (FP8 && sw) s4 = *reinterpret_cast<const f32x4*>(sw + nc);
+    const f32x4 b4 = b4v[j];
+    const f32x4 s4 = s4v[j];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       bf16x4 o;
@@ -845,7 +864,7 @@ __device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], 
 #pragma unroll
     for (int e = 0; e < 4; ++e) w8[e] = a[e], w8[e + 4] = b[e];
   }
-  constexpr int P = 4;  // rows in flight per lane
+  constexpr int P = 16;  // rows in flight per lane: all of them (the accumulators are dead by now)
 #pragma unroll 1
   for (int p0 = 0; p0 < 16; p0 += P) {
     bf16x8 x0v[P], xlv[P];
@@ -877,6 +896,70 @@ __device__ __forceinline__ void cross_staged_epilogue(const f32x4 (&acc)[8][4], 
   }
 }
 
+// Plain (bias / ReLU / sigmoid) epilogue of a 256x256 tile, staged through
+// LDS like the cross epilogue above. In registers each store instruction of
+// the transposed layout writes 32 bytes into each of 16 rows (16 partial
+// lines per instruction, 32 instructions per wave): tools/native/g8ph_stamps
+// measured 6.8 us for one tile's epilogue with nothing else running (the
+// staged cross epilogue, which also reads x0 / xl, took 5.6). Staged, a store
+// instruction writes two 512-byte row segments (8 whole lines), half as many
+// instructions. bf16 output, N % 8 == 0 and ldc % 8 == 0 (16-byte rows).
+template <bool FP8>
+__device__ __forceinline__ void plain_staged_epilogue(const f32x4 (&acc)[8][4], uint8_t* __restrict__ ys, int m0,
+                                                      int n0, int wr, int wc, int wid, int lane, int M, int N,
+                                                      const float* __restrict__ bias, const float* __restrict__ sa,
+                                                      const float* __restrict__ sw, bf16* __restrict__ C, int64_t ldc,
+                                                      int epi) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const int e = epi & 15;
+  const bool sig = e == EPI_SIGMOID;
+  const float lo = e == EPI_RELU ? 0.f : -__builtin_huge_valf();
+  __syncthreads();  // both wave groups are past their last K-loop LDS read
+  float sam[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sam[i] = (FP8 && sa) ? sa[min(m0 + 128 * wr + 16 * i + fr, M - 1)] : 1.f;
+  f32x4 b4v[4], s4v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nc = min(n0 + 64 * wc + 16 * j + 4 * fq, N - 4);
+    b4v[j] = bias ? *reinterpret_cast<const f32x4*>(bias + nc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s4v[j] = (FP8 && sw) ? *reinterpret_cast<const f32x4*>(sw + nc) : f32x4{1.f, 1.f, 1.f, 1.f};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 64 * wc + 16 * j + 4 * fq;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = acc[i][j][r];
+        if constexpr (FP8) x *= s4v[j][r] * sam[i];
+        v[r] = fmaxf(x + b4v[j][r], lo);
+      }
+      if (sig) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = sigmoidf(v[r]);
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+      *reinterpret_cast<bf16x4*>(ys + (128 * wr + 16 * i + fr) * kXsLdy + c * 2) = o;
+    }
+  }
+  __syncthreads();
+  const int col = (lane & 31) * 8;
+  const int n = n0 + col;
+  if (n >= N) return;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int row = 32 * wid + 2 * p + (lane >> 5);
+    const int m = m0 + row;
+    if (m < M)
+      *reinterpret_cast<bf16x8*>(C + int64_t(m) * ldc + n) = *reinterpret_cast<const bf16x8*>(ys + row * kXsLdy + col * 2);
+  }
+}
+
 template <bool FP8, typename OutT, bool PRE = false, bool XSTAGE = false>
 __global__ void __launch_bounds__(512) gemm_8ph_kernel(
     const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ W, int64_t ldw,
@@ -887,7 +970,7 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   constexpr int EB = FP8 ? 1 : 2;
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
   constexpr int KLOOP = 2 * BUF;
-  constexpr int SMEM = (XSTAGE && kXsBytes > KLOOP) ? kXsBytes : KLOOP;
+  constexpr int SMEM = kXsBytes > KLOOP ? kXsBytes : KLOOP;  // the staged epilogues reuse the K-loop buffers
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   DTFS_STAMP(0);
 
@@ -1085,6 +1168,9 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
   if constexpr (XSTAGE) {
     static_assert(sizeof(OutT) == 2, "the staged cross epilogue writes bf16 z");
     cross_staged_epilogue<FP8>(acc, smem, m0, n0, tn, wr, wc, wid, lane, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, xs);
+  } else if (sizeof(OutT) == 2 && (epi & 15) != EPI_CROSS && ((N | int(ldc)) & 7) == 0) {
+    plain_staged_epilogue<FP8>(acc, smem, m0, n0, wr, wc, wid, lane, M, N, bias, sa, sw,
+                               reinterpret_cast<bf16*>(C), ldc, epi);
   } else {
     store_acc_t<FP8, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, sa, sw, C, ldc, X0, XL, ldx, epi);
   }
@@ -1441,8 +1527,12 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
 
-  store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
-                            nullptr, 0, epi);
+  if (sizeof(OutT) == 2 && (epi & 15) != EPI_CROSS && ((N | int(ldc)) & 7) == 0)
+    plain_staged_epilogue<false>(acc, smem, m0, n0, wr, wc, wid, lane, M, N, bias, nullptr, nullptr,
+                                 reinterpret_cast<bf16*>(C), ldc, epi);
+  else
+    store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
+                              nullptr, 0, epi);
   if constexpr (EXTRA == 1) {
     if (fm_on) {
       float part = -fsq;

@@ -28,10 +28,10 @@ static double med(std::vector<double> v) {
 
 int main() {
   struct Cfg { int M, N, K; bool fp8; bool nobias; };
-  const Cfg cfgs[] = {{256, 256, 128, false, false}, {256, 256, 128, false, true}, {256, 256, 2816, false, false},
-                      {16384, 1024, 128, false, false}, {16384, 1024, 128, false, true},
-                      {16384, 1024, 2816, false, false}, {16384, 1024, 2816, true, false},
-                      {4096, 1024, 2816, true, false}};
+  const Cfg cfgs[] = {{256, 256, 128, false, false}, {256, 256, 2816, false, false},
+                      {16384, 1024, 128, false, false}, {16384, 1024, 576, false, false},
+                      {16384, 1024, 1024, false, false}, {16384, 1024, 2816, false, false},
+                      {16384, 1024, 2816, true, false}, {16384, 2752, 2816, true, false}};
   for (const Cfg& c : cfgs) {
     const int eb = c.fp8 ? 1 : 2;
     void *A, *W, *C;
