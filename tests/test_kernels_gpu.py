@@ -146,6 +146,23 @@ def test_gemm_variants_bf16(cuda, variant, M, N, K):
 
 
 @pytest.mark.parametrize("variant", [17, 18])
+@pytest.mark.parametrize("M,N,K", [(8192, 1024, 2752), (1000, 2752, 2752), (513, 1024, 192), (700, 1020, 256)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_8phase_bf16_out_epilogues(cuda, variant, M, N, K, epi):
+    """bf16 output of the 8-phase tile (the LDS-staged epilogue when N % 8 ==
+    0, the register epilogue otherwise: N = 1020) for none / ReLU / sigmoid,
+    ragged M and N, vs the fp32 CPU reference."""
+    g = torch.Generator().manual_seed(M + 3 * N + K + epi)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g) * 0.1
+    y = ops.hip().gemm(x.to(cuda), W.to(cuda), b.to(cuda), epi, None, None, False, None, None, None, variant)
+    ref = ops.linear(x, W, b, {0: "none", 1: "relu", 2: "sigmoid"}[epi], out_f32=True)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    _close(y, ref, 1e-2, 1e-2, f"8-phase bf16 out v{variant} {M}x{N}x{K} epi {epi}")
+
+
+@pytest.mark.parametrize("variant", [17, 18])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (8192, 2752, 2752), (700, 1024, 2816)])
 def test_gemm_8phase_fp8(cuda, M, N, K, variant):
     g = torch.Generator().manual_seed(M + N)
