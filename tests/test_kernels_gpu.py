@@ -482,7 +482,9 @@ def test_head(cuda):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 512), (37, 256, 512), (4096, 256, 512), (8192, 256, 512),
-                                   (5000, 256, 1024), (300, 128, 256), (77, 64, 128), (129, 40, 64)])
+                                   (5000, 256, 1024), (300, 128, 256), (77, 64, 128), (129, 40, 64),
+                                   # ragged rows / columns at the served batch sizes
+                                   (16421, 256, 512), (9000, 200, 256), (8200, 136, 128), (8192, 256, 1024)])
 @pytest.mark.parametrize("act", ["relu", "none"])
 def test_linear_head_fused(cuda, M, N, K, act):
     g = torch.Generator().manual_seed(M * 3 + N + K)
