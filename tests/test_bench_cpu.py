@@ -28,7 +28,10 @@ def _run_bench(n: int, extra=()):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
-               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240")
+               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240",
+               # an intermittent SIGSEGV of the world-1 run (2 of ~10 full-suite runs, never alone)
+               # left no output: the fault handler names the Python frame next time
+               PYTHONFAULTHANDLER="1")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -90,7 +93,10 @@ def test_bench_reference_workload(n):
         sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
-               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240")
+               DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="240",
+               # an intermittent SIGSEGV of the world-1 run (2 of ~10 full-suite runs, never alone)
+               # left no output: the fault handler names the Python frame next time
+               PYTHONFAULTHANDLER="1")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     assert "Average time cost with 1500 is " in p.stdout and " ms with 12 requests" in p.stdout, p.stdout
