@@ -197,6 +197,7 @@ void def_live_methods(py::class_<H>& c) {
             if (get("threads")) s.threads = spec["threads"].cast<int>();
             if (get("timeout_us")) s.timeout_us = spec["timeout_us"].cast<int64_t>();
             if (get("seed")) s.seed = spec["seed"].cast<uint64_t>();
+            if (get("debug_done_delay_us")) s.debug_done_delay_us = spec["debug_done_delay_us"].cast<int64_t>();
             dtfs::runtime::LoadResult r;
             {
               py::gil_scoped_release nogil;

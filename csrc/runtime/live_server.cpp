@@ -600,9 +600,14 @@ void LiveServer::watcher_loop() {
     const uint32_t seen = ctl_->bell();
     ctl_->heartbeat();
     if (!broken_) {
+      // any broken flag breaks this server, this rank's own included: the
+      // front door marks the cluster broken from Python on a communicator
+      // error (serving/cluster.py _watch) while this server may be idle, and
+      // only a broken server starts the rebuild
       const int by = ctl_->broken_by();
-      if (by >= 0 && by != ctl_->rank()) {
-        go_broken("rank " + std::to_string(by) + " gave up on the cluster");
+      if (by >= 0) {
+        go_broken(by == ctl_->rank() ? std::string("this rank gave up on the cluster")
+                                     : "rank " + std::to_string(by) + " gave up on the cluster");
       } else {
         const int silent = ctl_->silent_peer(cfg_.peer_timeout_us);
         if (silent >= 0) {

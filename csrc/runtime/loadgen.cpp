@@ -71,12 +71,22 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   WorkQ work;
   std::atomic<int64_t> next{0};
 
+  // Every completion callback runs on a LiveServer thread (the completer, or
+  // the submitter for a rejected request) and touches this frame's state
+  // (mu, next, work, res). The waiter below returns - destroying all of it -
+  // only once every callback has finished with it: `running` counts callbacks
+  // between their first and last critical section, and the waiter needs
+  // completed == total AND running == 0. (Round 3's version released mu and
+  // then did next.fetch_add / work.push: the waiter could wake in between and
+  // return, a use-after-return on the completer thread.)
+  int running = 0;
   auto on_done = [&](int64_t i, int64_t t_sched, Reply&& r) {
     const int64_t t = now_us();
-    bool push_token = false;
+    bool push_token = false, last = false;
     {
       std::lock_guard<std::mutex> lk(mu);
-      ++completed;
+      ++running;
+      last = ++completed == total;
       if (r.code == kOk) {
         ++res.ok;
       } else {
@@ -96,12 +106,17 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
         if (completed == spec.warmup + spec.count) t_close = double(t);
         push_token = true;
       }
-      if (completed == total) cv_all.notify_all();
     }
+    // test hook: hold the callback that counted the final completion here
+    // (tests/test_live_server.py)
+    if (spec.debug_done_delay_us > 0 && last)
+      std::this_thread::sleep_for(std::chrono::microseconds(spec.debug_done_delay_us));
     if (push_token) {
       const int64_t k = next.fetch_add(1);
       if (k < total) work.push(k, 0);
     }
+    std::lock_guard<std::mutex> lk(mu);
+    if (--running == 0 && completed >= total) cv_all.notify_all();
   };
 
   std::vector<std::thread> subs;
@@ -146,7 +161,7 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   }
   {
     std::unique_lock<std::mutex> lk(mu);
-    cv_all.wait(lk, [&] { return completed >= total; });
+    cv_all.wait(lk, [&] { return completed >= total && running == 0; });
   }
   work.close();
   for (auto& t : subs) t.join();

@@ -29,6 +29,8 @@ struct LoadSpec {
   int threads = 4;          // submitting threads (each copies its requests into the arena)
   int64_t timeout_us = 0;   // per-request deadline (0 = none)
   uint64_t seed = 1;
+  int64_t debug_done_delay_us = 0;  // test hook: the last request's completion callback sleeps this long
+                                    // after its completion is counted (run_load must still wait for it)
 };
 
 struct LoadResult {

@@ -31,10 +31,17 @@ thread, reference DCNClient.java:158-159, :185-188):
   immediately, and the communicators are aborted so no peer hangs;
 * every rank's watcher thread heartbeats into the segment; a rank silent for
   ``peer_timeout_s`` (a dead process) breaks the cluster the same way;
-* with ``recover=True`` rank 0 then rebuilds the cluster over the surviving
-  ranks (fresh step control and communicators, candidates re-split over the
-  survivors, same processes) and resumes serving: the requests in flight when
-  the rank died fail UNAVAILABLE once, later ones succeed.
+* with ``recover=True`` the survivors then rebuild the cluster among
+  themselves (fresh step control and communicators, candidates re-split over
+  the survivors, same processes) and resume serving: the requests in flight
+  when the rank died fail UNAVAILABLE once, later ones succeed (SURVEY.md
+  §5.3). No rank leads the rebuild: every survivor proposes the next epoch's
+  members through the job's key-value store and the first proposal wins
+  (``compare_set``), so any rank may die - rank 0 included - as long as the
+  store outlives it. ``serving/launch.py`` hosts the store in the launcher
+  process (torchrun's static rendezvous also keeps it in its agent, but the
+  agent tears every rank down once one fails). In ``scatter`` mode rank 0 is
+  the only front door: its death leaves nothing to serve, the followers exit.
 """
 from __future__ import annotations
 
@@ -92,6 +99,7 @@ class ClusterServer:
         self._stopping = threading.Event()
         self._lock = threading.RLock()
         self.recoveries = 0
+        self._injected_comm_error: Optional[str] = None
         self.engine = self.ctl = self.sched = None
         self._build(ctx, first=True, store=self._store)
         if self.serves and self.world > 1:
@@ -153,12 +161,10 @@ class ClusterServer:
             err = self.health()
             if err and self.ctl is not None and self.ctl.broken_by < 0:
                 log.error("communicator error on rank %d: %s", self.rank, err)
-                self.ctl.mark_broken(self.rank)
+                self.ctl.mark_broken(self.rank)  # the live server's watcher breaks it (even when idle)
             if self.broken and self.recover_on and not self._stopping.is_set():
                 try:
-                    if self.rank == 0:
-                        self._recover_leader()
-                    elif not self._rejoin():
+                    if not self._recover():
                         return
                 except Exception:  # noqa: BLE001
                     log.exception("cluster recovery failed; staying unavailable")
@@ -173,7 +179,14 @@ class ClusterServer:
 
     def health(self) -> Optional[str]:
         """First asynchronous communicator error of this rank (None = healthy)."""
+        if self._injected_comm_error:
+            return self._injected_comm_error
         return self.engine.comm_error() if self.engine is not None and self.engine.native_fanout_active else None
+
+    def inject_comm_error(self, msg: str = "injected communicator error") -> None:
+        """Fault injection (serving/faults.py family): report ``msg`` as this
+        rank's asynchronous communicator error until the next rebuild."""
+        self._injected_comm_error = msg
 
     # -- recovery (serving/cluster.py docstring; SURVEY.md §5.3) ----------------------
     def _survivors(self) -> List[int]:
@@ -182,31 +195,35 @@ class ClusterServer:
         ctl, lim = self.ctl, self.cfg.serving.peer_timeout_s
         return [r for r in range(ctl.world) if r == ctl.rank or ctl.heartbeat_age(r) < lim]
 
-    def _recover_leader(self) -> None:
-        """Rank 0 of a broken cluster: publish the survivors as the next
-        epoch's members (job store), wake the followers, rebuild."""
-        deadline = time.monotonic() + self.cfg.serving.peer_timeout_s
-        alive = self._survivors()
-        while len(alive) == self.ctl.world and time.monotonic() < deadline:
-            time.sleep(0.05)  # a stuck step before the heartbeat went stale
-            alive = self._survivors()
-        members = [self.members[r] for r in alive]
-        e = self.epoch + 1
-        log.warning("rebuilding the cluster over ranks %s (epoch %d)", members, e)
-        self._store.set(f"dtfs/recover/{e}", ",".join(str(m) for m in members))
-        self.ctl.bump_epoch()  # followers blocked on the old segment wake up
-        self._rebuild(e, members)
+    def _recover(self) -> bool:
+        """Any rank of a broken cluster: agree on the next epoch's members and
+        rebuild if this rank is one of them (False: it was left out, or the
+        scatter front door is gone).
 
-    def _rejoin(self) -> bool:
-        """A non-leader rank of a broken cluster: wait for the next epoch's
-        members; rebuild if this rank is one (False: it was left out)."""
+        Every survivor proposes the ranks whose heartbeat is fresh; the first
+        proposal to reach the store is the epoch's membership (``compare_set``
+        on a fresh key), so survivors with different views still agree and no
+        leader has to be alive. A rank that breaks before the dead peer's
+        heartbeat is stale (a stuck step) waits up to ``peer_timeout_s`` for
+        it, unless a proposal is already there."""
         e = self.epoch + 1
         key = f"dtfs/recover/{e}"
-        self._store.wait([key], datetime.timedelta(seconds=max(30.0, 4 * self.cfg.serving.step_timeout_s)))
+        if not self._store.check([key]):
+            deadline = time.monotonic() + self.cfg.serving.peer_timeout_s
+            alive = self._survivors()
+            while len(alive) == self.ctl.world and time.monotonic() < deadline and not self._store.check([key]):
+                time.sleep(0.05)
+                alive = self._survivors()
+            self._store.compare_set(key, "", ",".join(str(self.members[r]) for r in alive))
         members = [int(x) for x in self._store.get(key).decode().split(",")]
+        self.ctl.bump_epoch()  # ranks blocked on the old segment wake up and look for the proposal
         if self.orig_rank not in members:
             log.error("rank %d was left out of epoch %d", self.orig_rank, e)
             return False
+        if self.mode == "scatter" and self.members[0] not in members:
+            log.error("the scatter front door (rank %d) is gone: nothing left to serve", self.members[0])
+            return False
+        log.warning("rebuilding the cluster over ranks %s (epoch %d)", members, e)
         self._rebuild(e, members)
         return True
 
@@ -232,6 +249,7 @@ class ClusterServer:
         ctx = DistContext(rank=rank, world=world, local_rank=self.ctx.local_rank, device=self.ctx.device,
                           backend="gloo" if world > 1 else "none")
         self.epoch, self.members = epoch, list(members)
+        self._injected_comm_error = None
         self._build(ctx, first=False, store=self._store, model=old_eng.ex.model)
         self.recoveries += 1
         log.warning("rank %d serving again as rank %d of %d (epoch %d)", self.orig_rank, rank, world, epoch)
@@ -275,7 +293,7 @@ class ClusterServer:
                 sched.close()
                 return steps
             if ctl.broken_by >= 0 or sched.broken or ctl.epoch > 0:
-                if self.recover_on and self._rejoin():
+                if self.recover_on and self._recover():
                     continue
                 raise RuntimeError(f"cluster broken: {self.broken or f'rank {ctl.broken_by} gave up'}")
 

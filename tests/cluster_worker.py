@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--requests", type=int, default=24)
     ap.add_argument("--kill-rank", type=int, default=-1, help="this rank exits abruptly after --kill-after steps")
     ap.add_argument("--kill-after", type=int, default=3)
+    ap.add_argument("--inject-comm-error", type=int, default=-1,
+                    help="this front-door rank reports a communicator error while idle, after --kill-after requests")
     a = ap.parse_args()
 
     import numpy as np
@@ -54,21 +56,32 @@ def main():
     cfg.serving.allowed_batch_sizes = (96, 768)  # divisible by 1, 2, 3
     cfg.serving.batch_timeout_us = 300
     phase = dist.new_group(backend="gloo")
-    fault = {"after": a.kill_after} if rank == a.kill_rank else None
-    if a.kill_rank >= 0:
-        # recovery rehearsal: rank a.kill_rank dies after a few steps; rank 0
-        # keeps sending requests until the rebuilt cluster served 5 in a row
-        srv = ClusterServer(cfg, ctx, mode="scatter", control_timeout_s=3, step_timeout_s=5, follower_fault=fault,
+    fault = {"after": a.kill_after} if rank == a.kill_rank and a.mode == "scatter" else None
+    if a.kill_rank >= 0 or a.inject_comm_error >= 0:
+        # recovery rehearsal: rank a.kill_rank dies after a few steps (a scatter
+        # follower by its step count, an alltoall front door after kill_after of
+        # its own requests - rank 0 included), or rank a.inject_comm_error (an
+        # idle front door) reports a communicator error; every front door keeps
+        # sending requests until the rebuilt cluster served 5 in a row
+        srv = ClusterServer(cfg, ctx, mode=a.mode, control_timeout_s=3, step_timeout_s=5, follower_fault=fault,
                             recover=True)
         res = {"rank": rank}
-        if rank == 0:
+        if srv.serves:
             from distributed_tf_serving_amd.serving.errors import ServingError
 
             model = srv.registry.resolve("DCN").model
-            synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=7)
+            synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=7 + rank)
             outcomes, diffs = [], []
             t_end = time.monotonic() + 70
+            injected = False
             while time.monotonic() < t_end:
+                n_ok = outcomes.count("ok")
+                if a.mode == "alltoall" and rank == a.kill_rank and n_ok >= a.kill_after:
+                    os._exit(17)
+                if rank == a.inject_comm_error and n_ok >= a.kill_after and not injected:
+                    time.sleep(0.3)  # the front door is idle when the error arrives
+                    srv.inject_comm_error()
+                    injected = True
                 ids, wts = synth.arrays(300)
                 data = native().encode_predict_request("DCN", "serving_default", None,
                                                        [("feat_ids", torch.from_numpy(ids)),
@@ -86,13 +99,22 @@ def main():
                     break
             res.update(outcomes=outcomes, max_diff=max(diffs) if diffs else None, recoveries=srv.recoveries,
                        world_after=srv.world)
+            with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+                json.dump(res, f)  # before stop(): a survivor's peers may already be gone
+            # alltoall: every front door keeps its live server up (joining the
+            # others' steps) until all of this epoch's front doors are done
+            key = f"test/done/{srv.epoch}"
+            srv._store.add(key, 1)
+            t_wait = time.monotonic() + 60
+            while srv.mode == "alltoall" and srv._store.add(key, 0) < srv.world and time.monotonic() < t_wait:
+                time.sleep(0.05)
             srv.stop()
         else:
             res["followed"] = srv.serve_follower()
             res.update(recoveries=srv.recoveries, world_after=srv.world)
             srv.stop()
-        with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
-            json.dump(res, f)
+            with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+                json.dump(res, f)
         return
     srv = ClusterServer(cfg, ctx, mode=a.mode, control_timeout_s=20, step_timeout_s=20, follower_fault=fault)
     res = {"rank": rank, "serves": srv.serves}

@@ -357,3 +357,18 @@ def test_live_server_narrow_weight_columns_for_one_hot_dlrm():
         np.testing.assert_allclose(_scores(r_packed), want, atol=1e-5)
     assert live.stats()["narrowed"] == len(reqs)
     live.close()
+
+
+def test_load_generator_waits_for_the_last_completion_callback(server):
+    """Regression (round 3): run_load returned as soon as the last completion
+    was counted, while that callback still went on to touch run_load's stack
+    (next / work) on the completer thread - a use-after-return that surfaced as
+    an intermittent SIGSEGV. The hook holds the final callback 150 ms after it
+    counts; run_load must not return before the callback is done."""
+    live = server.registry.resolve("DCN").scheduler
+    synth = SyntheticRequests(fields=F, seed=6)
+    reqs = [synth.serialized(16) for _ in range(4)]
+    for kw in (dict(concurrency=4, threads=2), dict(qps=3000.0, threads=2)):
+        r = live.run_load(reqs, warmup=2, count=12, debug_done_delay_us=150_000, **kw)
+        assert r["errors"] == 0 and r["ok"] == r["submitted"]
+        assert r["wall_us"] >= 150_000, r["wall_us"]

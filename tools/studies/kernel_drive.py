@@ -19,7 +19,8 @@ from distributed_tf_serving_amd.client.synth import SyntheticRequests
 from distributed_tf_serving_amd.config import load_preset
 from distributed_tf_serving_amd.models import build_model
 
-PRESETS = {"deepfm": "deepfm_1gpu", "dcn_v2": "dcn_v2_fp8", "dcn": "reference_dcn", "wdl": "wdl_tiny_cpu"}
+PRESETS = {"deepfm": "deepfm_1gpu", "dcn_v2": "dcn_v2_fp8", "dcn": "reference_dcn", "wdl": "wdl_tiny_cpu",
+           "dlrm": "dlrm_sharded8"}
 
 
 def main(argv=None):
@@ -27,8 +28,13 @@ def main(argv=None):
     ap.add_argument("--model", default="deepfm", choices=sorted(PRESETS))
     ap.add_argument("--rows", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--table-rows", type=int, default=4_000_000,
+                    help="dlrm: rows per table (30 tables; 4M = 15 GB, far past the 256 MiB Infinity Cache like "
+                         "the served 60M-100M tables, but quick to initialise once per counter pass)")
     a = ap.parse_args(argv)
     cfg = load_preset(PRESETS[a.model]).model
+    if a.model == "dlrm":
+        cfg.table_rows = a.table_rows
     dev = torch.device("cuda:0")
     model = build_model(cfg, dev)
     ids, wts = SyntheticRequests(fields=cfg.num_fields, id_space=1 << 40, dist="zipf", seed=3).arrays(a.rows)
