@@ -22,11 +22,11 @@ ThreadPool::~ThreadPool() {
   for (auto& t : workers_) t.join();
 }
 
-void ThreadPool::drain() {
+void ThreadPool::drain(const std::function<void(int64_t)>& fn, int64_t n) {
   for (;;) {
     const int64_t i = next_.fetch_add(1, std::memory_order_relaxed);
-    if (i >= n_) break;
-    (*fn_)(i);
+    if (i >= n) break;
+    fn(i);
     done_.fetch_add(1, std::memory_order_acq_rel);
   }
 }
@@ -34,19 +34,24 @@ void ThreadPool::drain() {
 void ThreadPool::worker_loop() {
   uint64_t seen = 0;
   for (;;) {
-    // spin a little, then sleep until a new epoch
+    // spin a little on the epoch, then sleep until a new one
     int spins = 0;
     while (epoch_.load(std::memory_order_acquire) == seen && !stop_.load()) {
-      if (++spins > 20000) {
-        std::unique_lock<std::mutex> lk(wake_mu_);
-        wake_cv_.wait(lk, [&] { return epoch_.load() != seen || stop_.load(); });
-        break;
-      }
+      if (++spins > 20000) break;
     }
-    if (stop_.load()) return;
-    seen = epoch_.load(std::memory_order_acquire);
-    active_.fetch_add(1, std::memory_order_acq_rel);
-    if (fn_) drain();
+    const std::function<void(int64_t)>* fn = nullptr;
+    int64_t n = 0;
+    {
+      std::unique_lock<std::mutex> lk(wake_mu_);
+      wake_cv_.wait(lk, [&] { return epoch_.load() != seen || stop_.load(); });
+      if (stop_.load()) return;
+      seen = epoch_.load();
+      if (!open_) continue;  // woke after the round closed: nothing left to join
+      fn = fn_;
+      n = n_;
+      active_.fetch_add(1, std::memory_order_acq_rel);
+    }
+    drain(*fn, n);
     active_.fetch_sub(1, std::memory_order_acq_rel);
   }
 }
@@ -58,22 +63,25 @@ void ThreadPool::parallel_for(int64_t n, const std::function<void(int64_t)>& fn)
     return;
   }
   std::lock_guard<std::mutex> guard(mu_);
-  // wait for stragglers of the previous round to leave drain()
-  while (active_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-  fn_ = &fn;
-  n_ = n;
-  done_.store(0, std::memory_order_relaxed);
-  next_.store(0, std::memory_order_release);
   {
     std::lock_guard<std::mutex> lk(wake_mu_);
+    fn_ = &fn;
+    n_ = n;
+    done_.store(0, std::memory_order_relaxed);
+    next_.store(0, std::memory_order_relaxed);
+    open_ = true;
     epoch_.fetch_add(1, std::memory_order_acq_rel);
   }
   wake_cv_.notify_all();
-  drain();
+  drain(fn, n);
   while (done_.load(std::memory_order_acquire) < n) std::this_thread::yield();
-  // keep fn_ valid until every worker has left drain()
+  {
+    std::lock_guard<std::mutex> lk(wake_mu_);
+    open_ = false;  // no worker joins any more; the ones inside finish their claims
+    fn_ = nullptr;
+  }
+  // fn must outlive every worker still between its last claim and leaving drain()
   while (active_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-  fn_ = nullptr;
 }
 
 ThreadPool& ThreadPool::global() {

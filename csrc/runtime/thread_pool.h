@@ -32,7 +32,7 @@ class ThreadPool {
 
  private:
   void worker_loop();
-  void drain();
+  void drain(const std::function<void(int64_t)>& fn, int64_t n);
 
   std::vector<std::thread> workers_;
   std::mutex mu_;        // serialises parallel_for callers
@@ -40,9 +40,13 @@ class ThreadPool {
   std::condition_variable wake_cv_;
   std::atomic<uint64_t> epoch_{0};
   std::atomic<bool> stop_{false};
+  // the current round (guarded by wake_mu_): a worker joins only an open round,
+  // copying fn_ / n_ and counting itself in active_ under the lock, so the
+  // caller can close a round (and set up the next) once active_ is back to 0
   const std::function<void(int64_t)>* fn_ = nullptr;
-  std::atomic<int64_t> next_{0};
   int64_t n_ = 0;
+  bool open_ = false;
+  std::atomic<int64_t> next_{0};
   std::atomic<int64_t> done_{0};
   std::atomic<int> active_{0};
 };

@@ -104,23 +104,28 @@ def _py_includes():
 
 
 SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+TSAN_FLAGS = ["-fsanitize=thread", "-fno-omit-frame-pointer"]
 
 
 def build_native(verbose=False, force=False, sanitize=False) -> str:
-    """``sanitize``: ASan + UBSan host build of the native runtime (SURVEY.md
-    §5.2), into its own object dir. Run it with the sanitizer runtime
-    preloaded, e.g. ``scripts/sanitize_native.sh``; rebuild without the flag
-    afterwards (the instrumented .so replaces the normal one in-tree)."""
+    """``sanitize``: ASan + UBSan (True / "address") or ThreadSanitizer
+    ("thread") host build of the native runtime, into its
+    own object dir. Run it with the sanitizer runtime
+    preloaded and ``DTFS_NATIVE_SO`` pointing at it, e.g.
+    ``scripts/sanitize_native.sh`` (the in-tree .so is left alone)."""
     tdir, tinc, tlib, abi = _torch_paths()
-    out = os.path.join(PKG_DIR, "_native" + EXT_SUFFIX)
-    odir = os.path.join(BUILD, "native_asan" if sanitize else "native")
+    san = [] if not sanitize else (TSAN_FLAGS if sanitize == "thread" else SANITIZE_FLAGS)
+    odir = os.path.join(BUILD, {"thread": "native_tsan"}.get(sanitize, "native_asan") if sanitize else "native")
+    # a sanitizer build lands in its own directory, never over the in-tree .so
+    # (GPU runs ship the package directory); load it with DTFS_NATIVE_SO=<path>
+    out = os.path.join(odir if sanitize else PKG_DIR, "_native" + EXT_SUFFIX)
     os.makedirs(odir, exist_ok=True)
     hdr = _headers_mtime()
     flags = ["-O1" if sanitize else "-O3", "-g" if sanitize else "-g0", "-std=c++17", "-fPIC", "-Wall",
              "-Wno-unused-function", "-fvisibility=hidden",
              f"-I{CSRC}"] + [f"-I{p}" for p in tinc + _py_includes()] + _common_defs("_native", abi)
     if sanitize:
-        flags += SANITIZE_FLAGS
+        flags += san
         force = True  # the output name is shared with the normal build
     objs, jobs = [], []
     for s in NATIVE_SOURCES:
@@ -131,7 +136,7 @@ def build_native(verbose=False, force=False, sanitize=False) -> str:
             jobs.append([CXX, *flags, "-c", src, "-o", obj])
     _compile_all(jobs, verbose)
     if force or jobs or not os.path.exists(out):
-        _run([CXX, "-shared", "-o", out, *objs, *(SANITIZE_FLAGS if sanitize else []), f"-L{tlib}", "-lc10",
+        _run([CXX, "-shared", "-o", out, *objs, *san, f"-L{tlib}", "-lc10",
               "-ltorch", "-ltorch_cpu", "-ltorch_python", "-ldl", f"-Wl,-rpath,{tlib}"], verbose)
     return out
 
@@ -184,13 +189,14 @@ if __name__ == "__main__":
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--native-only", action="store_true")
-    ap.add_argument("--sanitize", action="store_true", help="ASan+UBSan host build of _native (implies --native-only)")
+    ap.add_argument("--sanitize", nargs="?", const="address", default=None, choices=["address", "thread"],
+                    help="ASan+UBSan (default) or TSan host build of _native (implies --native-only)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     if a.clean:
         clean()
         sys.exit(0)
-    print(build_native(a.verbose, a.force or a.sanitize, sanitize=a.sanitize))
+    print(build_native(a.verbose, a.force or bool(a.sanitize), sanitize=a.sanitize or False))
     if a.sanitize:
         sys.exit(0)
     if not a.native_only:

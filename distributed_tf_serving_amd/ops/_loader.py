@@ -55,12 +55,28 @@ def _torch_rccl_path() -> str:
     return p if os.path.exists(p) else "librccl.so.1"
 
 
+def _load_native_from(path: str):
+    """A sanitizer build of `_native` kept out of the package directory
+    (scripts/sanitize_native.sh sets DTFS_NATIVE_SO): the in-tree .so, which
+    GPU runs ship, is never replaced by an instrumented one."""
+    import importlib.util
+    import sys
+
+    spec = importlib.util.spec_from_file_location("distributed_tf_serving_amd._native", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["distributed_tf_serving_amd._native"] = mod
+    return mod
+
+
 def native():
     """The `_native` host runtime (wire codec, batcher)."""
     global _native_mod
     if _native_mod is not None:
         return _native_mod
     with _lock:
+        if _native_mod is None and os.environ.get("DTFS_NATIVE_SO"):
+            _native_mod = _load_native_from(os.environ["DTFS_NATIVE_SO"])
         if _native_mod is None:
             try:
                 _native_mod = importlib.import_module("distributed_tf_serving_amd._native")
