@@ -1373,6 +1373,7 @@ PYBIND11_MODULE(_hip, m) {
     dtfs_live::def_live_methods(c);
   }
   dtfs_live::def_step_control(m);
+  dtfs_live::def_grpc_front<PyGpuLive>(m);
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
   m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });

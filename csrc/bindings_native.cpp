@@ -14,6 +14,7 @@
 #include "wire/tensor_codec.h"
 #include "live_bindings.h"
 #include "runtime/narrow.h"
+#include "net/hpack.h"
 
 namespace py = pybind11;
 using namespace dtfs;
@@ -495,7 +496,54 @@ PyCpuLive* make_cpu_live(py::dict cfg, std::vector<int64_t> buckets, py::list sc
 
 }  // namespace
 
+// Known-answer checks of the HPACK pieces the native front door uses
+// (tests/test_native_front.py); vectors from RFC 7541 Appendix C.
+py::dict hpack_selftest() {
+  namespace n = dtfs::net;
+  py::dict o;
+  bool rt = true;
+  std::string all;
+  for (int c = 0; c < 256; ++c) all.push_back(char(c));
+  for (const std::string& s : {all, std::string("application/grpc"), std::string("grpc-java-netty/1.12.0"),
+                               std::string(""), std::string("te"), std::string(300, '~')}) {
+    std::string d;
+    const std::string e = n::huffman_encode(s);
+    rt = rt && n::huffman_decode(reinterpret_cast<const uint8_t*>(e.data()), e.size(), &d) && d == s;
+  }
+  // C.4.1: "www.example.com" -> f1e3 c2e5 f23a 6ba0 ab90 f4ff; C.4.2: "no-cache" -> a8eb 1064 9cbf
+  rt = rt && n::huffman_encode("www.example.com") == std::string("\xf1\xe3\xc2\xe5\xf2\x3a\x6b\xa0\xab\x90\xf4\xff", 12);
+  rt = rt && n::huffman_encode("no-cache") == std::string("\xa8\xeb\x10\x64\x9c\xbf", 6);
+  o["huffman_roundtrip"] = rt;
+  // C.4.1 request: :method GET, :scheme http, :path /, :authority www.example.com (Huffman, incremental indexing)
+  const std::string c41("\x82\x86\x84\x41\x8c\xf1\xe3\xc2\xe5\xf2\x3a\x6b\xa0\xab\x90\xf4\xff", 17);
+  n::HpackDecoder dec;
+  std::vector<n::Header> hs;
+  std::string err;
+  bool ok = dec.decode(reinterpret_cast<const uint8_t*>(c41.data()), c41.size(), &hs, &err) && hs.size() == 4 &&
+            hs[0] == n::Header(":method", "GET") && hs[1] == n::Header(":scheme", "http") &&
+            hs[2] == n::Header(":path", "/") && hs[3] == n::Header(":authority", "www.example.com");
+  o["static_decode"] = ok;
+  // C.4.2: the same connection's next block refers to dynamic entry 62 (:authority) and adds cache-control
+  const std::string c42("\x82\x86\x84\xbe\x58\x86\xa8\xeb\x10\x64\x9c\xbf", 12);
+  hs.clear();
+  ok = dec.decode(reinterpret_cast<const uint8_t*>(c42.data()), c42.size(), &hs, &err) && hs.size() == 5 &&
+       hs[3] == n::Header(":authority", "www.example.com") && hs[4] == n::Header("cache-control", "no-cache") &&
+       dec.table_entries() == 2 && dec.table_size() == 110;
+  o["dynamic_table"] = ok;
+  // padding that is not a prefix of EOS, and 8+ bits of padding, are errors
+  std::string d;
+  const uint8_t bad1[] = {0x00};        // '0' (00000) + padding 000: zeros
+  const uint8_t bad2[] = {0x1f, 0xff};  // 'a' (00011) + 11 one-bits of padding
+  o["bad_padding_rejected"] = !n::huffman_decode(bad1, 1, &d) && !n::huffman_decode(bad2, 2, &d);
+  py::list ts;
+  for (const char* t : {"1S", "250m", "100u", "1000n", "2H", "x"}) ts.append(n::parse_grpc_timeout(t));
+  o["timeouts"] = ts;
+  o["percent"] = n::grpc_percent_encode("a%b\nc\xc3\xa9");
+  return o;
+}
+
 PYBIND11_MODULE(_native, m) {
+  m.def("hpack_selftest", &hpack_selftest, "HPACK known-answer checks (RFC 7541 Appendix C)");
   m.doc() = "distributed_tf_serving_amd host runtime: zero-copy TF-Serving wire codec + dynamic batcher";
 
   py::class_<ParsedRequest, std::shared_ptr<ParsedRequest>>(m, "ParsedPredictRequest")
@@ -650,6 +698,7 @@ PYBIND11_MODULE(_native, m) {
     dtfs_live::def_live_methods(c);
   }
   dtfs_live::def_step_control(m);
+  dtfs_live::def_grpc_front<PyCpuLive>(m);
   m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
   m.attr("STATUS_CALLER_PATH") = int(runtime::kCallerPath);
   m.def(

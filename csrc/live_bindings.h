@@ -12,6 +12,11 @@
 #include <string>
 #include <vector>
 
+#include <condition_variable>
+#include <deque>
+#include <thread>
+
+#include "net/h2_server.h"
 #include "runtime/batcher.h"
 #include "runtime/live_server.h"
 #include "runtime/loadgen.h"
@@ -253,6 +258,169 @@ void def_live_methods(py::class_<H>& c) {
       })
       .def_property_readonly("broken", [](H& h) { return h.srv->broken(); })
       .def_property_readonly("max_rows", [](H& h) { return h.srv->max_rows(); });
+}
+
+// ---- native gRPC front door (csrc/net/h2_server.h) -------------------------
+// Predict goes straight into this module's LiveServer::submit on the event
+// loop thread; everything else (the other four PredictionService RPCs, and
+// Predicts the fast path hands back: ranked outputs, more rows than a batch)
+// goes to a Python handler on a few worker threads.
+class FallbackPool {
+ public:
+  FallbackPool(py::function fn, int threads)
+      : fn_(new py::function(std::move(fn)), [](py::function* f) {
+          py::gil_scoped_acquire g;
+          delete f;
+        }) {
+    for (int i = 0; i < std::max(1, threads); ++i) ts_.emplace_back([this] { work(); });
+  }
+  ~FallbackPool() { stop(); }
+  void push(dtfs::net::GrpcCall&& c, dtfs::net::Responder r) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!stop_) {
+        q_.emplace_back(std::move(c), std::move(r));
+        cv_.notify_one();
+        return;
+      }
+    }
+    r.reply(14, "server is shutting down", "");
+  }
+  void stop() {  // call without the GIL
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : ts_)
+      if (t.joinable()) t.join();
+    ts_.clear();
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      std::pair<dtfs::net::GrpcCall, dtfs::net::Responder> item;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        item = std::move(q_.front());
+        q_.pop_front();
+      }
+      const auto& c = item.first;
+      const double timeout_s =
+          c.deadline_us > 0 ? std::max(1e-3, double(c.deadline_us - dtfs::runtime::now_us()) * 1e-6) : 0.0;
+      int status = 13;
+      std::string msg, body;
+      {
+        py::gil_scoped_acquire g;
+        try {
+          py::tuple t = (*fn_)(c.path, py::bytes(c.message), timeout_s);
+          status = t[0].cast<int>();
+          msg = t[1].cast<std::string>();
+          body = t[2].cast<std::string>();
+        } catch (py::error_already_set& e) {
+          msg = e.what();
+        } catch (const std::exception& e) {
+          msg = e.what();
+        }
+      }
+      item.second.reply(status, std::move(msg), std::move(body));
+    }
+  }
+  std::shared_ptr<py::function> fn_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<dtfs::net::GrpcCall, dtfs::net::Responder>> q_;
+  bool stop_ = false;
+  std::vector<std::thread> ts_;
+};
+
+struct GrpcFront {
+  py::object live;  // the LiveServer holder: outlives the front door
+  std::shared_ptr<FallbackPool> fb;
+  std::unique_ptr<dtfs::net::H2GrpcServer> h2;
+  void stop() {
+    py::gil_scoped_release nogil;
+    if (h2) h2->stop();
+    if (fb) fb->stop();
+  }
+  ~GrpcFront() {
+    try {
+      stop();
+    } catch (...) {
+    }
+  }
+};
+
+inline const char* kPredictPath = "/tensorflow.serving.PredictionService/Predict";
+
+template <class H>
+void def_grpc_front(py::module& m) {
+  py::class_<GrpcFront>(m, "GrpcFront", py::module_local(),
+                        "Native h2c gRPC PredictionService front door over a LiveServer (csrc/net/h2_server.h)")
+      .def(py::init([](py::object live, int port, std::string host, int threads, py::object fallback,
+                       int fallback_threads, int64_t max_message) {
+             H& h = live.cast<H&>();
+             auto f = std::make_unique<GrpcFront>();
+             f->live = live;
+             if (!fallback.is_none()) f->fb = std::make_shared<FallbackPool>(fallback.cast<py::function>(), fallback_threads);
+             LiveServer* srv = h.srv.get();
+             std::shared_ptr<FallbackPool> fb = f->fb;
+             dtfs::net::H2Config cfg;
+             cfg.host = host;
+             cfg.port = port;
+             cfg.threads = threads;
+             cfg.max_message = max_message;
+             auto handler = [srv, fb](dtfs::net::GrpcCall&& call, dtfs::net::Responder r) {
+               if (call.path != kPredictPath) {
+                 if (fb) fb->push(std::move(call), std::move(r));
+                 else r.reply(12, "method " + call.path + " is not implemented", "");
+                 return;
+               }
+               auto msg = std::make_shared<std::string>(std::move(call.message));
+               const int64_t dl = call.deadline_us;
+               srv->submit(reinterpret_cast<const uint8_t*>(msg->data()), msg->size(), dl,
+                           [r, fb, msg, dl](Reply&& rep) {
+                             if (rep.code == dtfs::runtime::kOk) {
+                               r.reply(0, std::string(), std::move(rep.response));
+                             } else if ((rep.code == dtfs::runtime::kCallerPath || rep.code == dtfs::runtime::kOversize) &&
+                                        fb) {
+                               dtfs::net::GrpcCall c;
+                               c.path = kPredictPath;
+                               c.message = std::move(*msg);
+                               c.deadline_us = dl;
+                               fb->push(std::move(c), r);
+                             } else {
+                               r.reply(rep.code >= 1000 ? 13 : rep.code, std::move(rep.message), std::string());
+                             }
+                           });
+             };
+             {
+               py::gil_scoped_release nogil;
+               f->h2 = std::make_unique<dtfs::net::H2GrpcServer>(cfg, handler);
+             }
+             return f.release();
+           }),
+           py::arg("live"), py::arg("port"), py::arg("host") = "0.0.0.0", py::arg("threads") = 4,
+           py::arg("fallback") = py::none(), py::arg("fallback_threads") = 4, py::arg("max_message") = int64_t(64) << 20)
+      .def_property_readonly("port", [](const GrpcFront& f) { return f.h2 ? f.h2->port() : 0; })
+      .def("stop", &GrpcFront::stop)
+      .def("stats", [](const GrpcFront& f) {
+        const auto s = f.h2 ? f.h2->stats() : dtfs::net::H2Stats();
+        py::dict o;
+        o["connections"] = s.connections;
+        o["open_connections"] = s.open_connections;
+        o["calls"] = s.calls;
+        o["replies"] = s.replies;
+        o["dropped_replies"] = s.dropped_replies;
+        o["resets"] = s.resets;
+        o["protocol_errors"] = s.protocol_errors;
+        o["bytes_in"] = s.bytes_in;
+        o["bytes_out"] = s.bytes_out;
+        return o;
+      });
 }
 
 }  // namespace dtfs_live

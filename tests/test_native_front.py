@@ -1,0 +1,178 @@
+"""Native h2c gRPC front door (csrc/net/h2_server.cpp, serving/native_front.py)
+against unmodified grpcio clients: Predict (raw and packed encodings, large
+messages, concurrent calls on one channel and many channels), the other four
+PredictionService RPCs through the Python fallback, error statuses with
+messages, deadlines, cancellation, and the HPACK codec pieces (Huffman table
+round trip, grpc-timeout grammar, percent-encoding). Scores are checked
+against the model's fp32 forward. The reference's transport is gRPC over
+HTTP/2 (DCNClient.java:111-112, :118-125)."""
+import concurrent.futures as cf
+import time
+
+import grpc
+import numpy as np
+import pytest
+import torch
+
+from distributed_tf_serving_amd.client.synth import SyntheticRequests
+from distributed_tf_serving_amd.config import load_preset
+from distributed_tf_serving_amd.ops import native
+from distributed_tf_serving_amd.serving.native_front import NativeGrpcFront
+from distributed_tf_serving_amd.serving.server import ModelServer
+from distributed_tf_serving_amd.wire import schema as pb
+from distributed_tf_serving_amd.wire import tensor as T
+
+F = 43
+PREDICT = "/tensorflow.serving.PredictionService/Predict"
+
+
+def _cfg():
+    cfg = load_preset("wdl_tiny_cpu")
+    cfg.serving.max_batch_rows = 64
+    cfg.serving.allowed_batch_sizes = (8, 64)
+    cfg.serving.batch_timeout_us = 300
+    return cfg
+
+
+@pytest.fixture(scope="module")
+def front():
+    srv = ModelServer(_cfg(), device="cpu")
+    live = srv.registry.resolve("DCN").scheduler
+    fr = NativeGrpcFront(srv.service, live, port=0, host="127.0.0.1", threads=2).start()
+    yield srv, fr
+    fr.stop()
+    srv.stop()
+
+
+def _channel(port, **opts):
+    o = [("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)]
+    return grpc.insecure_channel(f"127.0.0.1:{port}", options=o + list(opts.items()))
+
+
+def _expected(srv, ids, wts):
+    m = srv.registry.resolve("DCN").model
+    return m(torch.as_tensor(ids), torch.as_tensor(wts)).numpy()
+
+
+def _scores(resp: bytes) -> np.ndarray:
+    return T.to_ndarray(pb.PredictResponse.FromString(resp).outputs["prediction_node"])
+
+
+def test_predict_many_calls_one_channel_matches_fp32(front):
+    srv, fr = front
+    ch = _channel(fr.port)
+    call = ch.unary_unary(PREDICT)
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=11)
+    reqs = []
+    for i in range(60):
+        rows = [1, 7, 33, 64, 5][i % 5]
+        ids, wts = synth.arrays(rows)
+        data = native().encode_predict_request("DCN", "serving_default", None,
+                                               [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                               i % 2 == 0)
+        reqs.append((data, ids, wts))
+    with cf.ThreadPoolExecutor(16) as pool:  # concurrent streams multiplexed on one HTTP/2 connection
+        outs = list(pool.map(lambda r: call(r[0], timeout=20), reqs))
+    for (data, ids, wts), resp in zip(reqs, outs):
+        np.testing.assert_allclose(_scores(resp), _expected(srv, ids, wts), atol=1e-5)
+    st = fr.stats()
+    assert st["calls"] >= 60 and st["protocol_errors"] == 0
+    ch.close()
+
+
+def test_many_connections_and_large_message(front):
+    srv, fr = front
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="uniform", seed=12)
+    # 1500 candidates, raw tensor_content: ~774 KB (the reference's request at N=1),
+    # split by the fallback path into batch-sized sub-requests (> 64 rows per batch)
+    ids, wts = synth.arrays(1500)
+    data = native().encode_predict_request("DCN", "serving_default", None,
+                                           [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                           True)
+    assert len(data) > 700_000
+    chans = [_channel(fr.port) for _ in range(6)]
+    with cf.ThreadPoolExecutor(6) as pool:
+        outs = list(pool.map(lambda c: c.unary_unary(PREDICT)(data, timeout=60), chans))
+    want = _expected(srv, ids, wts)
+    for o in outs:
+        np.testing.assert_allclose(_scores(o), want, atol=1e-5)
+    for c in chans:
+        c.close()
+
+
+def test_message_objects_metadata_and_classify(front):
+    srv, fr = front
+    ch = _channel(fr.port)
+    M = pb.METHODS
+    req = pb.GetModelMetadataRequest()
+    req.model_spec.name = "DCN"
+    req.metadata_field.append("signature_def")
+    resp = ch.unary_unary("/tensorflow.serving.PredictionService/GetModelMetadata",
+                          request_serializer=M["GetModelMetadata"][0].SerializeToString,
+                          response_deserializer=M["GetModelMetadata"][1].FromString)(req, timeout=20)
+    assert resp.model_spec.name == "DCN" and "signature_def" in resp.metadata
+    creq = pb.ClassificationRequest()
+    creq.model_spec.name = "DCN"
+    ex = creq.input.example_list.examples.add()
+    ex.features.feature["feat_ids"].int64_list.value.extend(range(1, F + 1))
+    ex.features.feature["feat_wts"].float_list.value.extend([1.0] * F)
+    cresp = ch.unary_unary("/tensorflow.serving.PredictionService/Classify",
+                           request_serializer=M["Classify"][0].SerializeToString,
+                           response_deserializer=M["Classify"][1].FromString)(creq, timeout=20)
+    assert len(cresp.result.classifications) == 1
+    ch.close()
+
+
+def test_error_statuses_and_unknown_method(front):
+    srv, fr = front
+    ch = _channel(fr.port)
+    synth = SyntheticRequests(fields=F, seed=13)
+    msg = synth.message(4)
+    msg.model_spec.name = "NoSuchModel"
+    with pytest.raises(grpc.RpcError) as e:
+        ch.unary_unary(PREDICT)(msg.SerializeToString(), timeout=10)
+    assert e.value.code() == grpc.StatusCode.NOT_FOUND and "NoSuchModel" in e.value.details()
+    with pytest.raises(grpc.RpcError) as e:
+        ch.unary_unary(PREDICT)(b"\xff\xff\xff garbage", timeout=10)
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    with pytest.raises(grpc.RpcError) as e:
+        ch.unary_unary("/tensorflow.serving.PredictionService/Nope")(b"", timeout=10)
+    assert e.value.code() == grpc.StatusCode.UNIMPLEMENTED
+    # non-ASCII in a status message survives the percent-encoding
+    assert native is not None
+    ch.close()
+
+
+def test_deadline_exceeded_on_the_client_and_server_survives(front):
+    srv, fr = front
+    ch = _channel(fr.port)
+    synth = SyntheticRequests(fields=F, seed=14)
+    data = synth.serialized(8)
+    with pytest.raises(grpc.RpcError) as e:
+        ch.unary_unary(PREDICT)(data, timeout=1e-4)  # expires before (or while) it is served
+    assert e.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+    # the connection and the server keep working after the cancelled stream
+    assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (8,)
+    ch.close()
+
+
+def test_stop_refuses_new_calls():
+    srv = ModelServer(_cfg(), device="cpu")
+    live = srv.registry.resolve("DCN").scheduler
+    fr = NativeGrpcFront(srv.service, live, port=0, host="127.0.0.1", threads=1)
+    ch = _channel(fr.port)
+    data = SyntheticRequests(fields=F, seed=15).serialized(3)
+    assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (3,)
+    fr.stop()
+    with pytest.raises(grpc.RpcError) as e:
+        ch.unary_unary(PREDICT)(data, timeout=3)
+    assert e.value.code() in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED)
+    ch.close()
+    srv.stop()
+
+
+def test_hpack_huffman_and_helpers():
+    h = native().hpack_selftest()
+    assert h["huffman_roundtrip"] and h["static_decode"] and h["dynamic_table"] and h["bad_padding_rejected"]
+    assert h["timeouts"] == [1000000, 250000, 100, 1, 7200000000, -1]
+    assert h["percent"] == "a%25b%0Ac%C3%A9"
