@@ -45,6 +45,7 @@ if [ -n "${COUNTERS:-}" ]; then
     python -m tools.counters_summary $OUT --only ${model}_ \
       --title "$model serving-shape forward ($rows rows), 1 MI355X (rocprofv3 --pmc, 4 passes)" > $OUT/summary_$model.md
     cat $OUT/summary_$model.md
+    rm -rf $OUT/${model}_p*  # raw CSVs: tens of MB each (gpurun copies back <= 64 MiB)
   done
 fi
 if [ -n "${PROF_MODELS:-}" ]; then
