@@ -153,6 +153,11 @@ def parse_args():
                          "every request is scattered over the GPUs (the reference's 3-host fan-out, inside a node)")
     ap.add_argument("--ref-requests", type=int, default=1000, help="requests per client thread (reference: 1000)")
     ap.add_argument("--ref-clients", type=int, default=6, help="closed-loop client threads (reference: 6)")
+    ap.add_argument("--over-grpc", action="store_true",
+                    help="--reference-workload on 1 GPU: the clients are a separate process of native h2c gRPC "
+                         "clients (client/native_load.py) talking to the native gRPC front door "
+                         "(serving/native_front.py) over TCP, instead of in-process submits")
+    ap.add_argument("--grpc-threads", type=int, default=4, help="--over-grpc: front-door event-loop threads")
     ap.add_argument("--print-requests", action="store_true",
                     help="--reference-workload: also print one 'Time cost' line per request, like the reference")
     a = ap.parse_args()
@@ -382,6 +387,41 @@ def run_live(a, ctx, cfg, model, eng, B):
     return window_s, extra
 
 
+def run_reference_over_grpc(a, live, cfg) -> dict:
+    """The reference workload over the network: this process serves the native
+    gRPC front door (csrc/net/h2_server.cpp) on the live server; a child
+    process of native h2c clients (client/native_load.py, no GPU) runs the
+    reference's closed loop against it over TCP (reference DCNClient.java:
+    111-112, 205-241)."""
+    import subprocess
+
+    from distributed_tf_serving_amd.serving.native_front import NativeGrpcFront
+
+    front = NativeGrpcFront(None, live, port=0, host="127.0.0.1", threads=a.grpc_threads)
+    cmd = [sys.executable, "-m", "distributed_tf_serving_amd.client.native_load", "--port", str(front.port),
+           "--candidates", str(a.request_rows), "--concurrency", str(a.ref_clients), "--requests",
+           str(a.ref_requests), "--warmup", "10", "--id-mode", "reference", "--timeout-s", str(a.step_timeout_s)]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    try:
+        p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    finally:
+        st = front.stats()
+        front.stop()
+    line = next((ln for ln in p.stdout.splitlines() if ln.startswith("{")), None)
+    if p.returncode != 0 or line is None:
+        raise SystemExit(f"native gRPC clients failed ({p.returncode}): {p.stdout[-2000:]} {p.stderr[-2000:]}")
+    res = json.loads(line)
+    print(next(ln for ln in p.stdout.splitlines() if ln.startswith("Average")), flush=True)
+    return {"metric": "reference workload (DCNClient.java) over gRPC: average request latency",
+            "value": round(res["avg_ms"], 4), "unit": "ms", "higher_is_better": False, "n_gpus": 1,
+            "requests": res["requests"], "errors": res["errors"], "clients": a.ref_clients,
+            "candidates": a.request_rows, "p50_ms": round(res["p50_ms"], 4), "p99_ms": round(res["p99_ms"], 4),
+            "requests_per_s": res["requests_per_s"], "scores_per_s": res["scores_per_s"],
+            "front_door": {k: st[k] for k in ("connections", "calls", "replies", "protocol_errors", "bytes_in")},
+            "path": "native h2c clients (separate process) -> TCP -> native gRPC front door -> live server (1 GPU)",
+            "model": describe_model(cfg), "encoding": "int64_val / float_val (like the reference client)"}
+
+
 def run_reference(a, ctx, cfg, model, eng, B):
     """--reference-workload: the reference client's closed loop against this
     server (reference DCNClient.java:205-241): ``--ref-clients`` threads x
@@ -408,6 +448,11 @@ def run_reference(a, ctx, cfg, model, eng, B):
     if control is not None:
         live.resume()
     out = None
+    if pool and a.over_grpc:
+        if world > 1:
+            raise SystemExit("--over-grpc runs on one GPU (the front door of a cluster is serving/cluster.py)")
+        out = run_reference_over_grpc(a, live, cfg)
+        pool = None
     if pool:
         n = a.ref_clients * a.ref_requests
         r = live.run_load(pool, warmup=10 * a.ref_clients, count=n, concurrency=a.ref_clients,

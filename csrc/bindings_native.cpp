@@ -15,6 +15,7 @@
 #include "live_bindings.h"
 #include "runtime/narrow.h"
 #include "net/hpack.h"
+#include "net/h2_client.h"
 
 namespace py = pybind11;
 using namespace dtfs;
@@ -544,6 +545,49 @@ py::dict hpack_selftest() {
 
 PYBIND11_MODULE(_native, m) {
   m.def("hpack_selftest", &hpack_selftest, "HPACK known-answer checks (RFC 7541 Appendix C)");
+  m.def(
+      "grpc_call",
+      [](const std::string& host, int port, const std::string& path, py::bytes data, double timeout_s) {
+        const std::string req = data;
+        int st = -1;
+        std::string msg, body;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          dtfs::net::H2Client c(host, port);
+          ok = c.call(path, req, timeout_s > 0 ? int64_t(timeout_s * 1e6) : 0, &st, &msg, &body);
+        }
+        if (!ok) throw std::runtime_error("gRPC transport failure: " + msg);
+        return py::make_tuple(st, msg, py::bytes(body));
+      },
+      py::arg("host"), py::arg("port"), py::arg("path"), py::arg("request"), py::arg("timeout_s") = 0.0,
+      "One unary gRPC call over the native h2c client: (status, message, response bytes).");
+  m.def(
+      "run_grpc_load",
+      [](const std::string& host, int port, const std::string& path, const std::vector<std::string>& requests,
+         int concurrency, int64_t warmup, int64_t count, double timeout_s) {
+        dtfs::net::GrpcLoadSpec sp;
+        sp.concurrency = concurrency;
+        sp.warmup = warmup;
+        sp.count = count;
+        sp.timeout_us = timeout_s > 0 ? int64_t(timeout_s * 1e6) : 0;
+        dtfs::net::GrpcLoadResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = dtfs::net::run_grpc_load(host, port, path, requests, sp);
+        }
+        py::dict o;
+        o["latency_us"] = r.latency_us;
+        o["ok"] = r.ok;
+        o["errors"] = r.errors;
+        o["window_us"] = r.window_us;
+        o["wall_us"] = r.wall_us;
+        o["first_error"] = r.first_error;
+        return o;
+      },
+      py::arg("host"), py::arg("port"), py::arg("path"), py::arg("requests"), py::arg("concurrency") = 6,
+      py::arg("warmup") = 0, py::arg("count") = 1000, py::arg("timeout_s") = 0.0,
+      "Closed-loop gRPC load over native h2c clients (one connection per client thread).");
   m.doc() = "distributed_tf_serving_amd host runtime: zero-copy TF-Serving wire codec + dynamic batcher";
 
   py::class_<ParsedRequest, std::shared_ptr<ParsedRequest>>(m, "ParsedPredictRequest")

@@ -45,6 +45,7 @@ NATIVE_SOURCES = [
     "runtime/step_control.cpp",
     "net/hpack.cpp",
     "net/h2_server.cpp",
+    "net/h2_client.cpp",
 ]
 HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp",
                     "runtime/kernel_seq.cpp",

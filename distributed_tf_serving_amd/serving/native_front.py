@@ -72,15 +72,18 @@ class NativeGrpcFront:
 
     def __init__(self, service, live, port: int = 9999, host: str = "0.0.0.0", threads: int = 4,
                  fallback_threads: int = 4, max_message_mb: int = 64):
-        """``live``: the servable's :class:`serving.live.LiveScheduler`."""
+        """``live``: the servable's :class:`serving.live.LiveScheduler`;
+        ``service`` None serves Predict's fast path only (UNIMPLEMENTED for
+        the rest, INTERNAL for what the fast path hands back)."""
         self.service = service
         self.live = live
         mod = type(live.srv).__module__
         from ..ops import hip, native
 
         m = hip() if mod.endswith("_hip") else native()
-        self._front = m.GrpcFront(live.srv, int(port), host, int(threads), make_fallback(service),
-                                  int(fallback_threads), int(max_message_mb) << 20)
+        fb = make_fallback(service) if service is not None else None  # None: Predict fast path only
+        self._front = m.GrpcFront(live.srv, int(port), host, int(threads), fb, int(fallback_threads),
+                                  int(max_message_mb) << 20)
         self.port = int(self._front.port)
         self._done = threading.Event()
 

@@ -176,3 +176,41 @@ def test_hpack_huffman_and_helpers():
     assert h["huffman_roundtrip"] and h["static_decode"] and h["dynamic_table"] and h["bad_padding_rejected"]
     assert h["timeouts"] == [1000000, 250000, 100, 1, 7200000000, -1]
     assert h["percent"] == "a%25b%0Ac%C3%A9"
+
+
+def test_native_client_and_load_generator(front):
+    """The native h2c client (csrc/net/h2_client.cpp) against the native front
+    door: one call, a status error, and the closed-loop generator the
+    over-the-network reference workload uses."""
+    srv, fr = front
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=16)
+    ids, wts = synth.arrays(20)
+    data = native().encode_predict_request("DCN", "serving_default", None,
+                                           [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                           True)
+    st, msg, body = native().grpc_call("127.0.0.1", fr.port, PREDICT, data, 10.0)
+    assert st == 0, msg
+    np.testing.assert_allclose(_scores(body), _expected(srv, ids, wts), atol=1e-5)
+    st, msg, _ = native().grpc_call("127.0.0.1", fr.port, PREDICT, b"\xff\xff", 10.0)
+    assert st == 3 and msg
+    reqs = [synth.serialized(32) for _ in range(4)]
+    r = native().run_grpc_load("127.0.0.1", fr.port, PREDICT, reqs, concurrency=4, warmup=8, count=80,
+                               timeout_s=20.0)
+    assert r["errors"] == 0 and r["ok"] == 88 and len(r["latency_us"]) == 80 and r["window_us"] > 0, r["first_error"]
+
+
+def test_native_client_talks_to_grpcio_server():
+    """Interop the other way: the native client against the grpcio front door."""
+    from distributed_tf_serving_amd.serving.grpc_server import GrpcFrontDoor
+
+    srv = ModelServer(_cfg(), device="cpu")
+    gd = GrpcFrontDoor(srv.service, port=0, host="127.0.0.1", max_workers=4).start()
+    try:
+        data = SyntheticRequests(fields=F, seed=17).serialized(9)
+        st, msg, body = native().grpc_call("127.0.0.1", gd.port, PREDICT, data, 20.0)
+        assert st == 0 and _scores(body).shape == (9,), msg
+        st, msg, _ = native().grpc_call("127.0.0.1", gd.port, PREDICT, b"\xff\xff", 20.0)
+        assert st == 3
+    finally:
+        gd.stop()
+        srv.stop()

@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
     ap.add_argument("--gather-gemm", action="store_true", help="K1 fused into K4 vs gather + GEMM")
+    ap.add_argument("--gather-locality", action="store_true",
+                    help="gather-GEMM time by where the table rows come from (L2 / MALL / HBM)")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
     ap.add_argument("--serving", action="store_true",
                     help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
@@ -148,6 +150,9 @@ def main():
         M, N, K = (int(x) for x in shape.split(","))
         print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
         return
+    if a.gather_locality:
+        for r in gather_locality_study():
+            print(json.dumps(r), flush=True)
     if a.gather_gemm:
         for r in gather_gemm_study():
             print(json.dumps(r), flush=True)
@@ -215,6 +220,43 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
         for k, v in t.items():
             r[f"{k}_us"] = round(statistics.median(v), 2)
         r["fused_tflops"] = round(2.0 * B * N * F * 64 / r["fused_us"] / 1e6, 1)
+        out.append(r)
+    return out
+
+
+def gather_locality_study(rows=(2048, 16384), F=43, V=1_000_000, N=1024, dev="cuda"):
+    """Is the gather-GEMM bound by where its A rows come from? The same fused
+    kernel on ids whose table rows are: all within 256 rows (L2-resident),
+    sequential (row = 43 m + f), Zipf over 2^40 (the bench), uniform over the
+    1M-row table; plus the dense 8-phase GEMM on the materialised x. ids map
+    to rows by id mod V (K0), so the row pattern is chosen exactly."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+
+    table = (torch.randn(V, 64, device=dev) * 0.05).to(torch.bfloat16)
+    lin = torch.randn(V, device=dev) * 0.01
+    W = (torch.randn(N, F * 64, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev) * 0.01
+    out = []
+    for B in rows:
+        g = torch.Generator(device="cpu").manual_seed(B)
+        zipf_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
+        wts = torch.from_numpy(wts_np).to(dev)
+        pats = {
+            "l2_hot256": torch.randint(0, 256, (B, F), generator=g),
+            "sequential": (torch.arange(B * F).view(B, F) % V),
+            "zipf": torch.from_numpy(zipf_np),
+            "uniform": torch.randint(0, V, (B, F), generator=g),
+        }
+        pats = {k: v.to(torch.int64).to(dev) for k, v in pats.items()}
+        x, _ = ops.embed(table, pats["zipf"], wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True)
+        t = {k: [] for k in list(pats) + ["dense_gemm"]}
+        for _ in range(5):
+            for k, ids in pats.items():
+                t[k].append(_time(lambda: ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=True), 20, 1))
+            t["dense_gemm"].append(_time(lambda: ops.linear(x, W, b, "relu"), 20, 1))
+        r = {"op": "gather_locality", "B": B, "N": N, "K": F * 64}
+        for k, v in t.items():
+            r[f"{k}_us"] = round(statistics.median(v), 2)
         out.append(r)
     return out
 
