@@ -13,6 +13,7 @@
 #include "kernels/launchers.h"
 #include "comm/rccl_comm.h"
 #include "live_bindings.h"
+#include "runtime/numa.h"
 #include "runtime/step_runner.h"
 
 namespace {
@@ -1376,6 +1377,33 @@ PYBIND11_MODULE(_hip, m) {
   dtfs_live::def_grpc_front<PyGpuLive>(m);
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
+  // NUMA-local pinned host memory (runtime/numa.h): pages placed on `node`
+  // first, then registered with the GPU; freed by unregister + munmap
+  m.def(
+      "alloc_pinned_on_node",
+      [](int64_t bytes, int node) {
+        void* p = dtfs::runtime::alloc_on_node(size_t(bytes), node);
+        if (hipHostRegister(p, size_t(bytes), hipHostRegisterDefault) != hipSuccess) {
+          dtfs::runtime::free_on_node(p, size_t(bytes));
+          throw std::runtime_error("hipHostRegister failed");
+        }
+        const size_t n = size_t(bytes);
+        return torch::from_blob(p, {bytes},
+                                [n](void* q) {
+                                  (void)hipHostUnregister(q);
+                                  dtfs::runtime::free_on_node(q, n);
+                                },
+                                torch::TensorOptions().dtype(torch::kUInt8));
+      },
+      py::arg("bytes"), py::arg("node"));
+  m.def(
+      "pci_bus_id",
+      [](int device) {
+        char buf[64] = {0};
+        if (hipDeviceGetPCIBusId(buf, sizeof(buf), device) != hipSuccess) return std::string();
+        return std::string(buf);
+      },
+      py::arg("device"), "PCI bus id of a GPU (\"0000:65:00.0\"), for its NUMA node");
   m.def("rccl_unique_id", []() { return py::bytes(dtfs::comm::unique_id()); });
   py::class_<dtfs::comm::RcclComm>(m, "RcclComm", "Native RCCL communicator (fan-out collectives over xGMI)")
       .def(py::init([](py::bytes uid, int nranks, int rank, int device) {

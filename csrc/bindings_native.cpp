@@ -15,6 +15,7 @@
 #include "live_bindings.h"
 #include "runtime/narrow.h"
 #include "net/hpack.h"
+#include "runtime/numa.h"
 #include "net/h2_client.h"
 
 namespace py = pybind11;
@@ -544,6 +545,27 @@ py::dict hpack_selftest() {
 }
 
 PYBIND11_MODULE(_native, m) {
+  // NUMA placement (runtime/numa.h; utils/affinity.py)
+  m.def("numa_node_count", &dtfs::runtime::numa_node_count);
+  m.def("numa_node_cpus", &dtfs::runtime::numa_node_cpus, py::arg("node"));
+  m.def("pci_numa_node", &dtfs::runtime::pci_numa_node, py::arg("bus_id"));
+  m.def("bind_process_cpus", &dtfs::runtime::bind_process_cpus, py::arg("cpus"),
+        "bind every thread of this process to these CPUs; returns the threads re-bound");
+  m.def("prefer_numa_node", &dtfs::runtime::prefer_numa_node, py::arg("node"));
+  m.def(
+      "alloc_on_node",
+      [](int64_t bytes, int node) {
+        void* p = dtfs::runtime::alloc_on_node(size_t(bytes), node);
+        const size_t n = size_t(bytes);
+        return torch::from_blob(p, {bytes}, [n](void* q) { dtfs::runtime::free_on_node(q, n); },
+                                torch::TensorOptions().dtype(torch::kUInt8));
+      },
+      py::arg("bytes"), py::arg("node"), "uint8 CPU tensor whose pages live on `node` (mmap + mbind + touch)");
+  m.def(
+      "page_numa_node", [](const torch::Tensor& t, int64_t offset) {
+        return dtfs::runtime::page_numa_node(static_cast<const uint8_t*>(t.data_ptr()) + offset);
+      },
+      py::arg("tensor"), py::arg("offset") = 0);
   m.def("hpack_selftest", &hpack_selftest, "HPACK known-answer checks (RFC 7541 Appendix C)");
   m.def(
       "grpc_call",

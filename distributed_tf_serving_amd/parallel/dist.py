@@ -51,6 +51,11 @@ def init_from_env(device: str = "auto", backend: Optional[str] = None, timeout_s
     if use_cuda:
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
+        # threads + pinned arenas on the GPU's socket (utils/affinity.py),
+        # before the process group / live server create their threads
+        from ..utils.affinity import place_rank
+
+        place_rank(dev)
     else:
         dev = torch.device("cpu")
     be = backend or ("nccl" if use_cuda else "gloo")

@@ -83,7 +83,12 @@ class LiveScheduler:
         # DLRM: the dense features) get only those copied (fewer H2D bytes)
         wc = int(getattr(model, "narrow_weight_cols", lambda: 0)()) if self.narrow_modulo else 0
         self.narrow_wts_cols = wc if 0 < wc < self.fields else 0
-        self.arenas = [self.layout.alloc(pin=engine.cuda) for _ in range(int(n_arenas or depth + 3))]
+        if engine.cuda:  # pinned, on this rank's NUMA node when it has one (utils/affinity.py)
+            from ..utils.affinity import alloc_pinned_arena
+
+            self.arenas = [alloc_pinned_arena(self.layout.capacity) for _ in range(int(n_arenas or depth + 3))]
+        else:
+            self.arenas = [self.layout.alloc() for _ in range(int(n_arenas or depth + 3))]
         self.config = dict(
             fields=self.fields, ids_key=sc.ids_key, wts_key=sc.wts_key, model_name=self.model_name,
             signature_name=sc.signature_name, output_key=sc.output_key, version=self.version,

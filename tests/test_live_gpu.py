@@ -186,3 +186,52 @@ def test_one_hot_dlrm_served_from_narrow_arena_matches_eager():
         assert st["narrowed"] > 0 and not st["broken"]
     finally:
         srv.stop()
+
+
+def test_numa_placement_and_node_local_pinned_arena():
+    """utils/affinity.py on the GPU box: the GPU's PCI bus id resolves, and a
+    node-local arena is pinned (hipHostRegister) with its pages on the node;
+    an H2D copy from it is exact."""
+    from distributed_tf_serving_amd.ops import hip
+    from distributed_tf_serving_amd.utils import affinity
+
+    bus = hip().pci_bus_id(0)
+    assert bus.count(":") == 2, bus
+    node = native().pci_numa_node(bus)
+    t = hip().alloc_pinned_on_node(4 << 20, max(node, 0))
+    assert t.is_pinned()
+    t[:] = torch.arange(4 << 20, dtype=torch.int64).remainder(251).to(torch.uint8)
+    d = t.to("cuda:0", non_blocking=True)
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), t)
+    pg = native().page_numa_node(t, 0)
+    if pg >= 0:
+        assert pg == max(node, 0)
+    a = affinity.alloc_pinned_arena(1 << 20)
+    assert a.is_pinned() and a.numel() == 1 << 20
+
+
+def test_native_grpc_front_door_on_gpu(server):
+    """The native h2c front door over the GPU live server (csrc/net/h2_server.cpp
+    calling the _hip module's LiveServer::submit), driven by the native client."""
+    from distributed_tf_serving_amd.serving.native_front import NativeGrpcFront
+
+    live = server.registry.resolve("DCN").scheduler
+    fr = NativeGrpcFront(server.service, live, port=0, host="127.0.0.1", threads=2)
+    try:
+        synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=21)
+        ids, wts = synth.arrays(300)
+        data = native().encode_predict_request("DCN", "serving_default", None,
+                                               [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(wts))],
+                                               True)
+        st, msg, body = native().grpc_call("127.0.0.1", fr.port, "/tensorflow.serving.PredictionService/Predict",
+                                           data, 30.0)
+        assert st == 0, msg
+        m = server.registry.resolve("DCN").model
+        want = m(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+        np.testing.assert_allclose(_scores(body), want, atol=2e-3)
+        r = native().run_grpc_load("127.0.0.1", fr.port, "/tensorflow.serving.PredictionService/Predict",
+                                   [data], concurrency=6, warmup=12, count=120, timeout_s=30.0)
+        assert r["errors"] == 0 and r["ok"] == 132, r["first_error"]
+    finally:
+        fr.stop()
