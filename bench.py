@@ -263,6 +263,8 @@ def fp32_check(cfg, model, live, request: bytes) -> dict:
     from distributed_tf_serving_amd.wire import schema as pb
     from distributed_tf_serving_amd.wire import tensor as T
 
+    if cfg.family == "dlrm" and model.param_bytes() > (4 << 30):
+        return fp32_check_dlrm_sparse(cfg, model, live, request)
     if model.param_bytes() > (4 << 30):
         return {"status": "skipped (model too large for a CPU copy)"}
     ref = build_model(cfg, "cpu")
@@ -281,6 +283,45 @@ def fp32_check(cfg, model, live, request: bytes) -> dict:
     tol = 5e-2 if cfg.gemm_dtype == "fp8" else 2e-2
     return {"status": "ok" if diff <= tol else "MISMATCH", "max_abs_diff": round(diff, 6), "tol": tol,
             "rows": int(got.numel())}
+
+
+def fp32_check_dlrm_sparse(cfg, model, live, request: bytes) -> dict:
+    """DLRM tables too large for a CPU copy (30 x 60M-100M rows): the fp32
+    reference rebuilds ONLY the table rows the request references, from the
+    tables' hashed init (models/layers.py hashed_rows_at: a value depends only
+    on (seed, table, row), so it is the GPU table's content, rounded to its
+    bf16), copies the dense towers, and runs the CPU reference math."""
+    from distributed_tf_serving_amd.models.ctr import DLRM
+    from distributed_tf_serving_amd.models.layers import hashed_rows_at
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
+
+    dense = getattr(model, "dense", model)  # ShardedDLRM keeps its towers in .dense
+    ref = DLRM(cfg, "cpu", materialize_tables=False).eval()
+    sd = {k: v.detach().cpu() for k, v in dense.state_dict().items() if not k.startswith("emb")}
+    ref.load_state_dict(sd, strict=False)
+    req = pb.PredictRequest.FromString(request)
+    ids = torch.from_numpy(T.to_ndarray(req.inputs["feat_ids"])).long()
+    wts = torch.from_numpy(T.to_ndarray(req.inputs["feat_wts"])).float()
+    nd, Tn, hot, D = cfg.num_dense, cfg.num_sparse, max(1, int(cfg.multi_hot)), cfg.embed_dim
+    B = ids.shape[0]
+    rows = torch.remainder(ids[:, nd:], cfg.table_rows).view(B, Tn, hot)
+    emb = torch.empty(B, Tn, hot, D)
+    for t in range(Tn):
+        v = hashed_rows_at(rows[:, t].reshape(-1), D, t, cfg.seed, ref.table_bound)
+        emb[:, t] = v.to(torch.bfloat16).float().view(B, hot, D)  # the table stores bf16
+    if hot == 1:
+        e = emb[:, :, 0].to(torch.bfloat16)
+    else:  # weighted bags, pooled in fp32 and stored bf16 (the K1b kernel's output)
+        e = (emb * wts[:, nd:].view(B, Tn, hot, 1)).sum(2).to(torch.bfloat16)
+    with torch.no_grad():
+        want = ref.interact_and_top(ref.bottom_out(wts), e).float()
+    resp = pb.PredictResponse.FromString(live.predict_bytes(request, 30.0))
+    got = torch.from_numpy(T.to_ndarray(resp.outputs["prediction_node"]))
+    diff = float((got - want).abs().max())
+    tol = 2e-2
+    return {"status": "ok" if diff <= tol else "MISMATCH", "max_abs_diff": round(diff, 6), "tol": tol,
+            "rows": int(got.numel()), "reference": f"sparse: {B * Tn * hot} referenced table rows rebuilt on the CPU"}
 
 
 def pct(lat_us, q):
@@ -378,6 +419,20 @@ def run_live(a, ctx, cfg, model, eng, B):
         extra["server"]["idle_steps_per_s"] = round((live.stats()["steps"] - t0) / 0.05, 1)
     extra["ingest"] = ("host-narrowed int32 rows + fp32 weights (K0 on the submitting thread)" if live.narrow_modulo
                        else "raw request bytes, unpacked on the GPU")
+    if hasattr(model, "exchange_bytes"):  # sharded tables: the embedding exchange of one step, per rank
+        extra["embedding_exchange"] = {
+            "bytes_per_step_per_rank": int(model.exchange_bytes(B)),
+            "plan": {"world": model.plan.world, "row_wise_tables": len(model.plan.row_wise()),
+                     "tables_per_rank": [len(model.plan.table_wise(r)) for r in range(model.plan.world)]},
+            "multi_hot": int(getattr(model, "hot", 1)),
+            "hot_row_cache": None,  # every remote row crosses xGMI (no replica cache yet)
+        }
+    try:
+        from distributed_tf_serving_amd.utils.affinity import placement
+
+        extra["numa"] = placement()
+    except Exception:  # noqa: BLE001 - informational only
+        pass
     if a.json_extra and rank == 0:
         per = {k: round(st[k] / max(1, st["steps"]), 1) for k in ("copy_us", "build_us", "launch_us", "wait_us",
                                                                   "encode_us")}

@@ -357,7 +357,8 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
 
 // ---------------------------------------------------------------- K1b
 torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tensor offsets,
-                            c10::optional<torch::Tensor> psw, int64_t modulo, bool mean, bool out_bf16) {
+                            c10::optional<torch::Tensor> psw, int64_t modulo, bool mean, bool out_bf16,
+                            c10::optional<torch::Tensor> out_opt) {
   check_dev(table, "table");
   check_dev(idx, "indices");
   check_dev(offsets, "offsets");
@@ -375,7 +376,16 @@ torch::Tensor embedding_bag(torch::Tensor table, torch::Tensor idx, torch::Tenso
     TORCH_CHECK(psw->scalar_type() == torch::kFloat32 && psw->numel() == idx.numel(), "per_sample_weights: fp32 [nnz]");
   }
   c10::DeviceGuard g(table.device());
-  auto out = torch::empty({nbags, D}, table.options().dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
+  torch::Tensor out;
+  if (out_opt) {  // a static buffer (captured steps: the exchange's send buffer)
+    check_dev(*out_opt, "out");
+    TORCH_CHECK(out_opt->scalar_type() == (out_bf16 ? torch::kBFloat16 : torch::kFloat32) && out_opt->is_contiguous() &&
+                    out_opt->numel() == nbags * D,
+                "out must be contiguous [nbags, D] of the output dtype");
+    out = *out_opt;
+  } else {
+    out = torch::empty({nbags, D}, table.options().dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
+  }
   check_hip(dtfs::launch_embedding_bag(table.data_ptr(), idx.data_ptr(), idx.scalar_type() == torch::kInt64,
                                        offsets.data_ptr<int64_t>(), psw ? psw->data_ptr<float>() : nullptr, int(nbags),
                                        idx.numel(), int(D), modulo, mean, out_bf16 ? nullptr : out.data_ptr<float>(),
@@ -654,35 +664,75 @@ torch::Tensor dot_interaction_gather_arena(torch::Tensor dense, torch::Tensor ta
 }
 
 // ---------------------------------------------------------------- K1b routing
-torch::Tensor shard_route(torch::Tensor ids, int64_t W, int64_t tm, torch::Tensor col, torch::Tensor mod,
-                          torch::Tensor off, c10::optional<torch::Tensor> out_opt) {
-  TORCH_CHECK(ids.is_cuda() && ids.dim() == 2 && ids.stride(1) == 1 && ids.stride(0) >= ids.size(1),
-              "ids must be a GPU [B, F] row view with contiguous rows");
-  TORCH_CHECK(ids.scalar_type() == torch::kInt64 || ids.scalar_type() == torch::kInt32, "ids must be int32/int64");
-  TORCH_CHECK(W >= 1 && tm >= 1, "W, tm >= 1");
+torch::Tensor shard_route(c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> arena, int64_t B, int64_t F,
+                          int64_t W, int64_t tm, torch::Tensor col, torch::Tensor mod, torch::Tensor off,
+                          c10::optional<torch::Tensor> out_opt, int64_t hot, c10::optional<torch::Tensor> wts,
+                          c10::optional<torch::Tensor> out_w) {
+  TORCH_CHECK(ids.has_value() != arena.has_value(), "shard_route: ids or a device arena");
+  TORCH_CHECK(W >= 1 && tm >= 1 && hot >= 1 && B >= 0 && F >= 1, "W, tm, hot, F >= 1");
+  dtfs::RouteArgs a;
+  torch::Tensor ref;
+  if (ids) {
+    TORCH_CHECK(ids->is_cuda() && ids->dim() == 2 && ids->stride(1) == 1 && ids->stride(0) >= ids->size(1),
+                "ids must be a GPU [B, F] row view with contiguous rows");
+    TORCH_CHECK(ids->scalar_type() == torch::kInt64 || ids->scalar_type() == torch::kInt32, "ids must be int32/int64");
+    TORCH_CHECK(ids->size(0) == B && ids->size(1) == F, "ids must be [B, F]");
+    a.ids = ids->data_ptr();
+    a.ids64 = ids->scalar_type() == torch::kInt64;
+    a.ld = ids->stride(0);
+    ref = *ids;
+    if (wts) {
+      check_dev(*wts, "wts");
+      TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->size(0) == B &&
+                      wts->size(1) == F && wts->stride(1) == 1,
+                  "wts must be fp32 [B, F] with contiguous rows");
+      a.wts = wts->data_ptr<float>();
+      a.wts_ld = wts->stride(0);
+    }
+  } else {
+    check_dev(*arena, "arena");
+    TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous() && arena->numel() > dtfs::kArenaPayloadOff,
+                "arena must be a contiguous uint8 device buffer");
+    TORCH_CHECK(!wts, "arena rows carry their own weights");
+    a.arena = arena->data_ptr<uint8_t>();
+    ref = *arena;
+  }
   check_dev(col, "col");
   check_dev(mod, "mod");
   check_dev(off, "off");
   TORCH_CHECK(col.scalar_type() == torch::kInt32 && col.numel() == W * tm, "col must be int32 [W * tm]");
   TORCH_CHECK(mod.scalar_type() == torch::kInt64 && mod.numel() == W * tm, "mod must be int64 [W * tm]");
   TORCH_CHECK(off.scalar_type() == torch::kInt64 && off.numel() == W * tm, "off must be int64 [W * tm]");
-  check_same_dev(ids, col, "col");
+  check_same_dev(ref, col, "col");
   // route columns are clamped into [0, F) by the kernel (capturable: no sync)
-  const int64_t B = ids.size(0), F = ids.size(1);
-  c10::DeviceGuard g(ids.device());
+  c10::DeviceGuard g(ref.device());
   torch::Tensor out;
+  const int64_t n = W * B * tm * hot;
   if (out_opt) {
     check_dev(*out_opt, "out");
-    TORCH_CHECK(out_opt->scalar_type() == torch::kInt32 && out_opt->numel() == W * B * tm, "out must be int32 [W, B, tm]");
-    check_same_dev(ids, *out_opt, "out");
+    TORCH_CHECK(out_opt->scalar_type() == torch::kInt32 && out_opt->numel() == n && out_opt->is_contiguous(),
+                "out must be contiguous int32 [W, B, tm * hot]");
+    check_same_dev(ref, *out_opt, "out");
     out = *out_opt;
   } else {
-    out = torch::empty({W, B, tm}, ids.options().dtype(torch::kInt32));
+    out = torch::empty({W, B, tm * hot}, ref.options().dtype(torch::kInt32));
   }
-  check_hip(dtfs::launch_shard_route(ids.data_ptr(), ids.scalar_type() == torch::kInt64, ids.stride(0), int(B),
-                                     int(F), int(W), int(tm), col.data_ptr<int32_t>(), mod.data_ptr<int64_t>(),
-                                     off.data_ptr<int64_t>(), out.data_ptr<int32_t>(), cur_stream(ids)),
-            "shard_route");
+  if (out_w) {
+    check_dev(*out_w, "out_w");
+    TORCH_CHECK(out_w->scalar_type() == torch::kFloat32 && out_w->numel() == n && out_w->is_contiguous(),
+                "out_w must be contiguous fp32 [W, B, tm * hot]");
+    a.out_w = out_w->data_ptr<float>();
+  }
+  a.B = int(B);
+  a.F = int(F);
+  a.W = int(W);
+  a.tm = int(tm);
+  a.hot = int(hot);
+  a.col = col.data_ptr<int32_t>();
+  a.mod = mod.data_ptr<int64_t>();
+  a.off = off.data_ptr<int64_t>();
+  a.out = out.data_ptr<int32_t>();
+  check_hip(dtfs::launch_shard_route(a, cur_stream(ref)), "shard_route");
   return out;
 }
 
@@ -1239,7 +1289,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("cross_c") = py::none());
   m.def("embedding_bag", &embedding_bag, py::arg("table"), py::arg("indices"), py::arg("offsets"),
         py::arg("per_sample_weights") = py::none(), py::arg("modulo") = 0, py::arg("mean") = false,
-        py::arg("out_bf16") = false);
+        py::arg("out_bf16") = false, py::arg("out") = py::none());
   m.def("gemm", &gemm, py::arg("A"), py::arg("W"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("x0") = py::none(), py::arg("xl") = py::none(), py::arg("out_f32") = false,
         py::arg("sa") = py::none(), py::arg("sw") = py::none(), py::arg("out") = py::none(),
@@ -1249,12 +1299,17 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("head_w") = py::none());
   m.def("dot_interaction", &dot_interaction, py::arg("dense"), py::arg("emb"), py::arg("out_cols") = 0,
         py::arg("emb_off") = py::none(), py::arg("emb_stride") = py::none());
-  m.def("shard_route", &shard_route, py::arg("ids"), py::arg("W"), py::arg("tm"), py::arg("col"), py::arg("mod"),
-        py::arg("off"), py::arg("out") = py::none());
+  m.def("shard_route", &shard_route, py::arg("ids"), py::arg("arena"), py::arg("B"), py::arg("F"), py::arg("W"),
+        py::arg("tm"), py::arg("col"), py::arg("mod"), py::arg("off"), py::arg("out") = py::none(),
+        py::arg("hot") = 1, py::arg("wts") = py::none(), py::arg("out_w") = py::none(),
+        "K1b routing: rows (+ weights) of every candidate's owned-table ids grouped by owner rank");
   m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
+  m.def("set_gather_variant", &dtfs::set_gather_variant, py::arg("variant"),
+        "gather-GEMM kernel: 1 = output-side weights (default), 0 = LDS scale pass (A/B studies)");
+  m.def("gather_variant", &dtfs::gather_variant);
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");

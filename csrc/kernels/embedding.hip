@@ -574,22 +574,33 @@ __global__ void __launch_bounds__(256) bag_kernel(const bf16* __restrict__ table
 // Embedding model parallelism (parallel/embedding_sharding.py): the int32 row
 // every (candidate b, owned-table slot) pair looks up on the table's owner,
 // grouped by owner so ONE all-to-all hands each rank exactly its rows:
-//   out[(s*B + b)*tm + j] = off[s*tm + j] + (ids[b*ld + col[s*tm + j]] mod mod[s*tm + j])
+//   out[((s*B + b)*tm + j)*hot + h] = off[s*tm + j] + (id(b, col[s*tm + j] + h) mod mod[s*tm + j])
 // s = owner rank, j = its j-th owned table (pad slots point at row off + 0).
-template <typename IdT>
-__global__ void __launch_bounds__(256) shard_route_kernel(const IdT* __restrict__ ids, int64_t ld, int B, int F,
-                                                          int W, int tm,
-                                                          const int32_t* __restrict__ col,
-                                                          const int64_t* __restrict__ mod,
-                                                          const int64_t* __restrict__ off, int32_t* __restrict__ out) {
-  const int64_t n = int64_t(W) * B * tm;
+__global__ void __launch_bounds__(256) shard_route_kernel(RouteArgs a) {
+  // element i = ((s * B + b) * tm + j) * hot + h: owner s, candidate b, owned
+  // table slot j, id h of the slot's bag; the slot's ids are columns
+  // col[s tm + j] .. + hot - 1 of the row (one-hot: hot = 1)
+  const int64_t n = int64_t(a.W) * a.B * a.tm * a.hot;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    const int j = int(i % tm);
-    const int64_t sb = i / tm;
-    const int b = int(sb % B), s = int(sb / B);
-    const int slot = s * tm + j;
-    const int c = min(max(col[slot], 0), F - 1);
-    out[i] = int32_t(off[slot] + hash_row(int64_t(ids[int64_t(b) * ld + c]), mod[slot]));
+    const int h = int(i % a.hot);
+    const int64_t q = i / a.hot;
+    const int j = int(q % a.tm);
+    const int64_t sb = q / a.tm;
+    const int b = int(sb % a.B), s = int(sb / a.B);
+    const int slot = s * a.tm + j;
+    const int c = min(max(a.col[slot] + h, 0), a.F - 1);
+    int64_t id = 0;
+    float w = 0.f;
+    if (a.arena) {  // K0 fused: the id (and weight) straight from the request bytes
+      const ArenaRow ar = arena_row(a.arena, kArenaPayloadOff, b);
+      if (ar.ids) arena_feature(ar, c, id, w);
+    } else {
+      id = a.ids64 ? static_cast<const int64_t*>(a.ids)[int64_t(b) * a.ld + c]
+                   : int64_t(static_cast<const int32_t*>(a.ids)[int64_t(b) * a.ld + c]);
+      w = a.wts ? a.wts[int64_t(b) * a.wts_ld + c] : 1.f;
+    }
+    a.out[i] = int32_t(a.off[slot] + hash_row(id, a.mod[slot]));
+    if (a.out_w) a.out_w[i] = w;
   }
 }
 
@@ -628,18 +639,12 @@ hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n,
   return hipGetLastError();
 }
 
-hipError_t launch_shard_route(const void* ids, bool ids64, int64_t ld, int B, int F, int W, int tm, const int32_t* col,
-                              const int64_t* mod, const int64_t* off, int32_t* out, hipStream_t st) {
-  const int64_t n = int64_t(W) * B * tm;
+hipError_t launch_shard_route(const RouteArgs& a, hipStream_t st) {
+  const int64_t n = int64_t(a.W) * a.B * a.tm * a.hot;
   if (n == 0) return hipSuccess;
-  if (F < 1) return hipErrorInvalidValue;
+  if (a.F < 1 || a.hot < 1 || !a.out || (!a.ids && !a.arena)) return hipErrorInvalidValue;
   const int blocks = int(std::min<int64_t>((n + 255) / 256, 4096));
-  if (ids64)
-    hipLaunchKernelGGL(shard_route_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, static_cast<const int64_t*>(ids),
-                       ld, B, F, W, tm, col, mod, off, out);
-  else
-    hipLaunchKernelGGL(shard_route_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, static_cast<const int32_t*>(ids),
-                       ld, B, F, W, tm, col, mod, off, out);
+  hipLaunchKernelGGL(shard_route_kernel, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

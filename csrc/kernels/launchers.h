@@ -15,8 +15,25 @@ hipError_t launch_pack_ids(const void* ids, bool ids64, int32_t* out, int64_t n,
 // K1b routing: out[(s*B + b)*tm + j] = off[s*tm+j] + (ids[b*ld + col[s*tm+j]] mod mod[s*tm+j])
 // (int32 rows grouped by owner rank for the embedding all-to-all); col is
 // clamped into [0, F).
-hipError_t launch_shard_route(const void* ids, bool ids64, int64_t ld, int B, int F, int W, int tm, const int32_t* col,
-                              const int64_t* mod, const int64_t* off, int32_t* out, hipStream_t st);
+// K1b routing (embedding model parallelism): table rows (and weights) of
+// every candidate grouped by owner rank, out[s][b][j][h] = off[s tm + j] +
+// (id(b, col[s tm + j] + h) mod mod[s tm + j]); ids from an [B, F] row view or
+// straight from a device request arena.
+struct RouteArgs {
+  const void* ids = nullptr;
+  bool ids64 = true;
+  int64_t ld = 0;
+  const uint8_t* arena = nullptr;  // instead of ids (+ wts)
+  const float* wts = nullptr;      // optional per-id weights (multi-hot bags)
+  int64_t wts_ld = 0;
+  int B = 0, F = 0, W = 1, tm = 1, hot = 1;
+  const int32_t* col = nullptr;
+  const int64_t* mod = nullptr;
+  const int64_t* off = nullptr;
+  int32_t* out = nullptr;   // [W, B, tm, hot]
+  float* out_w = nullptr;   // optional, same shape
+};
+hipError_t launch_shard_route(const RouteArgs& a, hipStream_t st);
 
 // K1: weighted gather (+ first/second-order FM). out_x bf16 [B, F*D] and/or out_fm fp32 [B].
 struct EmbedArgs {
@@ -120,6 +137,9 @@ struct MxIO {
 // cross_w / cross_c / cross_n (DCN v1, with fm_part): the folded cross
 // weights fp32 [cross_n][64F] + constants (EmbedArgs.cross_*, cross_n <= 4);
 // fm_part's row 1 then receives the cross logit instead of the FM term.
+// Gather-GEMM variant (A/B studies): 1 = output-side weights (default), 0 = LDS scale pass.
+void set_gather_variant(int v);
+int gather_variant();
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                               int N, int epi, hipStream_t st, const float* cross_w = nullptr,

@@ -55,6 +55,22 @@ def _lsr(z: torch.Tensor, s: int) -> torch.Tensor:
     return torch.bitwise_and(torch.bitwise_right_shift(z, s), (1 << (64 - s)) - 1)
 
 
+def hashed_rows_at(rows: torch.Tensor, D: int, table_id: int, seed: int, bound: float) -> torch.Tensor:
+    """The values hashed_uniform_rows_ gives table ``table_id``'s rows ``rows``
+    (int64, any order / repeats) -> fp32 [len(rows), D]: an fp32 reference can
+    rebuild just the rows a request touches (bench.py's sparse check)."""
+    dev = rows.device
+    cols = torch.arange(D, device=dev, dtype=torch.int64)
+    salt = _s64((seed * 0x9E3779B97F4A7C15 + table_id * 0xD1B54A32D192ED03) & _M64)
+    z = rows.to(torch.int64).view(-1)[:, None] * D + cols[None, :] + salt
+    z = z + _s64(0x9E3779B97F4A7C15)
+    z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    z = torch.bitwise_xor(z, _lsr(z, 31))
+    u = _lsr(z, 40).to(torch.float32) * (1.0 / (1 << 24))  # top 24 bits -> [0, 1)
+    return (u * 2.0 - 1.0) * bound
+
+
 def hashed_uniform_rows_(out: torch.Tensor, table_id: int, row_lo: int, seed: int, bound: float,
                          chunk_rows: int = 1 << 19) -> torch.Tensor:
     """Fill ``out`` [n, D] with U(-bound, bound) values that depend only on
@@ -63,19 +79,11 @@ def hashed_uniform_rows_(out: torch.Tensor, table_id: int, row_lo: int, seed: in
     bit for bit (splitmix64 of the element index; identical on CPU and GPU)."""
     n, D = out.shape
     dev = out.device
-    cols = torch.arange(D, device=dev, dtype=torch.int64)
-    salt = _s64((seed * 0x9E3779B97F4A7C15 + table_id * 0xD1B54A32D192ED03) & _M64)
     with torch.no_grad():
         for r0 in range(0, n, chunk_rows):
             r1 = min(n, r0 + chunk_rows)
             rows = torch.arange(row_lo + r0, row_lo + r1, device=dev, dtype=torch.int64)
-            z = rows[:, None] * D + cols[None, :] + salt
-            z = z + _s64(0x9E3779B97F4A7C15)
-            z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
-            z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
-            z = torch.bitwise_xor(z, _lsr(z, 31))
-            u = _lsr(z, 40).to(torch.float32) * (1.0 / (1 << 24))  # top 24 bits -> [0, 1)
-            out[r0:r1].copy_((u * 2.0 - 1.0) * bound)
+            out[r0:r1].copy_(hashed_rows_at(rows, D, table_id, seed, bound))
     return out
 
 

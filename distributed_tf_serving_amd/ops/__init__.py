@@ -161,19 +161,24 @@ def embed_fp8(table: torch.Tensor, ids, wts: Optional[torch.Tensor], modulo: int
 
 def embedding_bag(table: torch.Tensor, indices: torch.Tensor, offsets: torch.Tensor,
                   per_sample_weights: Optional[torch.Tensor] = None, modulo: int = 0, mean: bool = False,
-                  out_bf16: bool = False) -> torch.Tensor:
-    """Sum (or mean) pooled multi-hot lookup; offsets are CSR [nbags + 1]."""
+                  out_bf16: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum (or mean) pooled multi-hot lookup; offsets are CSR [nbags + 1].
+    ``out``: a static [nbags, D] buffer to write (captured steps)."""
     if table.is_cuda:
         m = int(modulo) if modulo > 0 else table.shape[0]
         return hip().embedding_bag(table, indices.contiguous(), offsets.contiguous(), per_sample_weights, m, mean,
-                                   out_bf16)
+                                   out_bf16, out)
     rows = _hash_rows(indices, modulo if modulo > 0 else table.shape[0])
-    out = torch.nn.functional.embedding_bag(rows, table.float(), offsets[:-1], mode="mean" if mean else "sum",
+    res = torch.nn.functional.embedding_bag(rows, table.float(), offsets[:-1], mode="mean" if mean else "sum",
                                             per_sample_weights=None if mean else per_sample_weights,
                                             include_last_offset=False)
     if mean and per_sample_weights is not None:
         raise ValueError("per_sample_weights with mean pooling is not supported")
-    return out.to(torch.bfloat16) if out_bf16 else out
+    res = res.to(torch.bfloat16) if out_bf16 else res
+    if out is not None:
+        out.copy_(res.view(out.shape))
+        return out
+    return res
 
 
 # ------------------------------------------------------------------ K4 / K3b
@@ -533,18 +538,33 @@ def bottom_mlp3(wts: torch.Tensor, nd: int, layers) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ K1b routing
-def shard_route(ids: torch.Tensor, W: int, tm: int, col: torch.Tensor, mod: torch.Tensor, off: torch.Tensor,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Embedding-parallel routing: int32 [W, B, tm] with
-    out[s, b, j] = off[s*tm + j] + (ids[b, col[s*tm + j]] mod mod[s*tm + j]),
-    i.e. the local row on owner rank s of its j-th table for candidate b."""
-    B = ids.shape[0]
+def shard_route(ids, W: int, tm: int, col: torch.Tensor, mod: torch.Tensor, off: torch.Tensor,
+                out: Optional[torch.Tensor] = None, hot: int = 1, wts: Optional[torch.Tensor] = None,
+                out_w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Embedding-parallel routing: int32 [W, B, tm * hot] with
+    out[s, b, j * hot + h] = off[s*tm + j] + (ids[b, col[s*tm + j] + h] mod mod[s*tm + j]),
+    i.e. the local row on owner rank s of its j-th table for candidate b (a
+    multi-hot table's ``hot`` ids are consecutive columns); ``out_w`` gets the
+    matching weights (multi-hot bags). ``ids`` may be :class:`ArenaRows`: the
+    GPU kernel then reads ids and weights from the request bytes."""
+    if isinstance(ids, ArenaRows):
+        if ids.arena.is_cuda:
+            return hip().shard_route(None, ids.arena, int(ids.B), int(ids.F), int(W), int(tm), col, mod, off, out,
+                                     int(hot), None, out_w)
+        ids, wts = _arena_unpack_host(ids)
+    B, F = ids.shape
     if ids.is_cuda:
-        return hip().shard_route(_rows(ids), int(W), int(tm), col, mod, off, out)
-    else:
-        c = col.long().clamp(0, ids.shape[1] - 1)
-        r = (off.view(1, -1) + torch.remainder(ids.long()[:, c], mod.view(1, -1))).to(torch.int32)  # [B, W*tm]
-        r = r.view(B, W, tm).transpose(0, 1).contiguous()
+        return hip().shard_route(_rows(ids), None, int(B), int(F), int(W), int(tm), col, mod, off, out, int(hot),
+                                 None if wts is None else _rows(wts), out_w)
+    h = torch.arange(hot, dtype=torch.int64)
+    c = (col.long().view(-1, 1) + h.view(1, -1)).clamp(0, F - 1).view(-1)  # [W*tm*hot]
+    md = mod.view(-1, 1).expand(-1, hot).reshape(-1)
+    of = off.view(-1, 1).expand(-1, hot).reshape(-1)
+    r = (of.view(1, -1) + torch.remainder(ids.long()[:, c], md.view(1, -1))).to(torch.int32)  # [B, W*tm*hot]
+    r = r.view(B, W, tm * hot).transpose(0, 1).contiguous()
+    if out_w is not None:
+        w = (wts.float()[:, c] if wts is not None else torch.ones(B, c.numel())).view(B, W, tm * hot)
+        out_w.copy_(w.transpose(0, 1).reshape(out_w.shape))
     if out is not None:
         out.copy_(r.view(out.shape))
         return out

@@ -181,11 +181,16 @@ class ShardedEmbedding(nn.Module):
     step is capturable and replayed by the native StepRunner."""
 
     def __init__(self, plan: ShardingPlan, ctx: DistContext, seed: int, bound: float, dtype=torch.bfloat16,
-                 device="cpu", group=None, col_base: int = 0):
+                 device="cpu", group=None, col_base: int = 0, hot: int = 1):
         super().__init__()
         self.plan, self.ctx, self.group = plan, ctx, group
         self.world, self.rank = plan.world, ctx.rank if plan.world > 1 else 0
         self.col_base = int(col_base)
+        # multi-hot: table t's ids are columns col_base + t * hot .. + hot - 1,
+        # pooled (weighted sum) on the owner by the K1b bag kernel
+        self.hot = int(hot)
+        if self.hot > 1 and plan.row_wise():
+            raise NotImplementedError("multi-hot tables shard table-wise (plan them with policy='table')")
         dev = torch.device(device)
         T = len(plan.tables)
         self.T = T
@@ -225,7 +230,7 @@ class ShardedEmbedding(nn.Module):
             for j in range(self.tmax):
                 if j < len(self.tw_by_rank[s]):
                     t = self.tw_by_rank[s][j]
-                    cols.append(self.col_base + t)
+                    cols.append(self.col_base + t * self.hot)
                     mods.append(plan.tables[t].rows)
                     offs.append(lay[s][1][t])
                 else:
@@ -258,20 +263,43 @@ class ShardedEmbedding(nn.Module):
         return self.world * B * self.tmax if self.tw_tables else 0
 
     def alloc(self, B: int) -> Dict[str, torch.Tensor]:
-        """Static exchange buffers of one (bucket, slot)."""
-        dev, W, tm, D, Tr = self.store.device, self.world, self.tmax, self.D, len(self.rw)
+        """Static exchange buffers of one (bucket, slot). One rank: the
+        exchange is the identity, so receive buffers alias the send buffers
+        and the lookup writes straight into ``emb_all`` (no collectives)."""
+        dev, W, tm, D, Tr, hot = self.store.device, self.world, self.tmax, self.D, len(self.rw), self.hot
         i32 = dict(dtype=torch.int32, device=dev)
         bf = dict(dtype=self.store.dtype, device=dev)
-        bufs = {"emb_all": torch.zeros(max(1, self.n_tw_rows(B) + B * Tr), D, **bf)}
+        nt = self.n_tw_rows(B)
+        bufs = {"emb_all": torch.zeros(max(1, nt + B * Tr), D, **bf)}
         if self.tw_tables:
-            bufs["send_ids"] = torch.zeros(W, B, tm, **i32)
-            bufs["recv_ids"] = torch.zeros(W, B, tm, **i32)
-            bufs["emb_send"] = torch.zeros(W * B, tm * D, **bf)
+            bufs["send_ids"] = torch.zeros(W, B, tm * hot, **i32)
+            bufs["recv_ids"] = bufs["send_ids"] if W == 1 else torch.zeros(W, B, tm * hot, **i32)
+            bufs["emb_send"] = bufs["emb_all"][:nt].view(W * B, tm * D) if W == 1 else torch.zeros(W * B, tm * D, **bf)
+            if hot > 1:
+                bufs["send_w"] = torch.zeros(W, B, tm * hot, dtype=torch.float32, device=dev)
+                bufs["recv_w"] = bufs["send_w"] if W == 1 else torch.zeros(W, B, tm * hot, dtype=torch.float32,
+                                                                               device=dev)
+                bufs["bag_off"] = torch.arange(0, W * B * tm * hot + 1, hot, dtype=torch.int64, device=dev)
         if Tr:
             bufs["rw_ids"] = torch.zeros(1, B, Tr, **i32)
             bufs["rw_all"] = torch.zeros(W, B, Tr, **i32)
             bufs["rw_part"] = torch.zeros(W * B, Tr * D, **bf)
         return bufs
+
+    def exchange_bytes(self, B: int) -> int:
+        """Bytes this rank sends to OTHER ranks per step (ids + weights out,
+        embeddings back): what crosses xGMI."""
+        W, tm, D, Tr, hot = self.world, self.tmax, self.D, len(self.rw), self.hot
+        if W == 1:
+            return 0
+        eb = self.store.element_size()
+        n = 0
+        if self.tw_tables:
+            n += (W - 1) * B * tm * hot * (4 + (4 if hot > 1 else 0))  # ids (+ weights) to the owners
+            n += (W - 1) * B * tm * D * eb                             # pooled rows back to the requesters
+        if Tr:
+            n += (W - 1) * B * Tr * 4 + (W - 1) * B * Tr * D * eb      # all-gather ids, reduce-scatter rows
+        return n
 
     def table_map(self, B: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """(emb_off, emb_stride) int64 [T]: table t of candidate b is row
@@ -292,20 +320,29 @@ class ShardedEmbedding(nn.Module):
         return m
 
     # -- one step's aux-lane ops -----------------------------------------------
-    def program(self, ids: torch.Tensor, B: int, bufs: Dict[str, torch.Tensor]) -> List[sp.Op]:
-        W, tm, D, Tr = self.world, self.tmax, self.D, len(self.rw)
+    def program(self, ids, B: int, bufs: Dict[str, torch.Tensor], wts: Optional[torch.Tensor] = None) -> List[sp.Op]:
+        """``ids``: [B, F] row view (+ ``wts`` for multi-hot bags), or
+        :class:`ops.ArenaRows` - the route kernel then reads ids and weights
+        straight from the request bytes (K0 fused into the routing)."""
+        W, tm, D, Tr, hot = self.world, self.tmax, self.D, len(self.rw), self.hot
         ops: List[sp.Op] = []
 
         def route():
             if self.tw_tables:
-                ops_k.shard_route(ids, W, tm, self.tw_col, self.tw_mod, self.tw_off, out=bufs["send_ids"])
+                ops_k.shard_route(ids, W, tm, self.tw_col, self.tw_mod, self.tw_off, out=bufs["send_ids"], hot=hot,
+                                  wts=wts, out_w=bufs.get("send_w"))
             if Tr:
                 ops_k.shard_route(ids, 1, Tr, self.rw_col, self.rw_mod, self.rw_zero[:Tr], out=bufs["rw_ids"])
 
         def lookup():
             if self.tw_tables:  # rows arrive hashed and offset: the gather needs no modulo
-                ops_k.embed(self.store, bufs["recv_ids"].view(W * B, tm), None, modulo=self.store.shape[0],
-                            want_x=True, out_x=bufs["emb_send"])
+                if hot == 1:
+                    ops_k.embed(self.store, bufs["recv_ids"].view(W * B, tm), None, modulo=self.store.shape[0],
+                                want_x=True, out_x=bufs["emb_send"])
+                else:  # K1b: weighted bags of `hot` rows, pooled on the owner
+                    ops_k.embedding_bag(self.store, bufs["recv_ids"].view(-1), bufs["bag_off"],
+                                        per_sample_weights=bufs["recv_w"].view(-1), modulo=self.store.shape[0],
+                                        out_bf16=True, out=bufs["emb_send"].view(W * B * tm, D))
             if Tr:
                 ops_k.embed(self.store, bufs["rw_all"].view(W * B, Tr), None, modulo_f=self.rw_mod,
                             offset_f=self.rw_off, want_x=True, out_x=bufs["rw_part"], shard_lo_f=self.rw_lo,
@@ -313,24 +350,27 @@ class ShardedEmbedding(nn.Module):
 
         ops.append(sp.Kernels(sp.AUX, route, "route"))
         ops.append(sp.Sync("record", sp.AUX, 0))  # ids routed: the dense tower may read the batch
-        if self.tw_tables:
+        if self.tw_tables and W > 1:
             ops.append(sp.Coll("alltoall", sp.AUX, bufs["send_ids"], bufs["recv_ids"]))
+            if hot > 1:
+                ops.append(sp.Coll("alltoall", sp.AUX, bufs["send_w"], bufs["recv_w"]))
         if Tr:
             ops.append(sp.Coll("allgather", sp.AUX, bufs["rw_ids"], bufs["rw_all"]))
         ops.append(sp.Kernels(sp.AUX, lookup, "lookup"))
         nt = self.n_tw_rows(B)
-        if self.tw_tables:
+        if self.tw_tables and W > 1:
             ops.append(sp.Coll("alltoall", sp.AUX, bufs["emb_send"], bufs["emb_all"][:nt]))
         if Tr:
             ops.append(sp.Coll("reduce_scatter", sp.AUX, bufs["rw_part"], bufs["emb_all"][nt:nt + B * Tr]))
         return ops
 
-    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+    def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Eager exchange (collective): ids [B, F] (tables at columns
         col_base..) -> [B, T, D]."""
         B = ids.shape[0]
         bufs = self.alloc(B)
-        sp.run_eager(self.program(ids.contiguous(), B, bufs), self.group)
+        w = None if wts is None else wts.float().contiguous()
+        sp.run_eager(self.program(ids.contiguous(), B, bufs, w), self.group)
         off, stride = self.table_map(B)
         rows = off.view(1, -1) + torch.arange(B, device=off.device).view(-1, 1) * stride.view(1, -1)
         return bufs["emb_all"][rows]
@@ -366,14 +406,15 @@ class ShardedDLRM(nn.Module):
                  policy: str = "auto", budget_bytes: int = int(0.8 * MI355X_HBM_BYTES), group=None):
         super().__init__()
         self.cfg, self.ctx, self.group = cfg, ctx, group
-        if int(getattr(cfg, "multi_hot", 1)) != 1:
-            raise NotImplementedError("sharded DLRM tables are one-hot (multi-hot bags run unsharded)")
+        self.hot = max(1, int(getattr(cfg, "multi_hot", 1)))
         world = ctx.world if ctx.is_distributed else 1
+        if self.hot > 1 and policy == "auto":
+            policy = "table"  # multi-hot bags pool on their table's owner
         self.plan = plan or plan_sharding(dlrm_tables(cfg), world, budget_bytes, policy)
         self.dense = DLRM(cfg, device=device, materialize_tables=False)
         self.dense.gen = None
         self.emb = ShardedEmbedding(self.plan, ctx, cfg.seed, self.dense.table_bound, DTYPES[cfg.param_dtype],
-                                    device, group, col_base=cfg.num_dense)
+                                    device, group, col_base=cfg.num_dense, hot=self.hot)
         self.device_ = torch.device(device)
 
     def signature(self):
@@ -385,19 +426,42 @@ class ShardedDLRM(nn.Module):
     def alloc(self, B: int) -> Dict[str, torch.Tensor]:
         return self.emb.alloc(B)
 
-    def build_program(self, ids: torch.Tensor, wts: torch.Tensor, B: int, bufs: Dict[str, torch.Tensor],
+    def narrow_weight_cols(self) -> int:
+        """One-hot: only the dense features' weights are read (the request
+        arena carries just those, serving/live.py); multi-hot bags read all."""
+        return self.cfg.num_dense if self.hot == 1 else 0
+
+    @property
+    def supports_arena(self) -> bool:
+        """The step reads the request arena itself: the route kernel takes the
+        sparse ids (and bag weights) from the request bytes, the fused bottom
+        MLP the dense features - no unpack pass (parallel/fanout.py)."""
+        return self.dense._bottom_fused() and self.dense.dtype == torch.bfloat16
+
+    def exchange_bytes(self, B: int) -> int:
+        return self.emb.exchange_bytes(B)
+
+    def build_program(self, ids, wts: Optional[torch.Tensor], B: int, bufs: Dict[str, torch.Tensor],
                       out: Optional[torch.Tensor] = None, state: Optional[dict] = None) -> List[sp.Op]:
-        """One step over static inputs: ids [B, F] / wts [B, F] row views,
-        scores -> ``out`` (or ``state["scores"]``)."""
+        """One step over static inputs: ids [B, F] / wts [B, F] row views, or
+        ``ids`` = :class:`ops.ArenaRows` (wts None: both come from the request
+        bytes); scores -> ``out`` (or ``state["scores"]``)."""
         d = self.dense
         st = {} if state is None else state
         emb_off, emb_stride = self.emb.table_map(B)
-        ops = self.emb.program(ids, B, bufs)
+        arena = isinstance(ids, ops_k.ArenaRows)
+        bag_w = None
+        if self.hot > 1 and not arena:
+            bag_w = wts if wts.dtype == torch.float32 else wts.float()
+        ops = self.emb.program(ids, B, bufs, bag_w)
         k = next(i for i, o in enumerate(ops) if isinstance(o, sp.Sync))  # after the route: the batch is read
 
         def bottom():
-            w = wts if wts.dtype == torch.float32 else wts.float()
-            st["dense"] = d.bottom_out(w)
+            if arena:  # the fused bottom tower reads the dense features from the arena
+                st["dense"] = d.bottom_out(ids)
+            else:
+                w = wts if wts.dtype == torch.float32 else wts.float()
+                st["dense"] = d.bottom_out(w)
 
         def top():
             z = ops_k.dot_interaction(st["dense"], bufs["emb_all"], d.inter_cols, emb_off, emb_stride)

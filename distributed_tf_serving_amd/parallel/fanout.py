@@ -272,8 +272,18 @@ class FanoutEngine:
         h_out = self.host_out(B, slot)
         bufs = self._prog_bufs[key] = model.alloc(B) if hasattr(model, "alloc") else {}
         state: dict = {}
-        ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
-        ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B], state=state)
+        if getattr(model, "supports_arena", False):
+            # K0 fused: the program's kernels read ids / weights straight from
+            # the request bytes (no unpack pass, no packed-row buffer)
+            from ..ops import ArenaRows
+
+            ops = [sp.Kernels(sp.AUX, lambda: self.arena.decode_varints(arena_dev), "varints")]
+            ops += model.build_program(ArenaRows(arena_dev, B, self.layout.fields), None, B, bufs, out=h_out[:B],
+                                       state=state)
+        else:
+            ops = [sp.Kernels(sp.AUX, lambda: self._unpack(arena_dev, buf), "unpack")]
+            ops += model.build_program(self.layout.ids(buf), self.layout.wts(buf), B, bufs, out=h_out[:B],
+                                       state=state)
         # warm-up: one eager run (collective on every rank, like the capture below)
         sp.run_eager(ops, self.group)
         torch.cuda.synchronize(self.dev)

@@ -15,7 +15,10 @@ from distributed_tf_serving_amd.parallel.embedding_sharding import (GiB, MI355X_
 from distributed_tf_serving_amd.parallel.dist import split_rows
 
 
-def _small_cfg():
+def _small_cfg(hot: int = 1):
+    if hot > 1:  # 5 tables x `hot` ids each (multi-hot bags, weighted by feat_wts)
+        return ModelConfig(family="dlrm", num_fields=5 + 5 * hot, num_dense=5, table_rows=997, embed_dim=64,
+                           bottom_mlp=(32, 64), mlp_dims=(64, 32), multi_hot=hot)
     return ModelConfig(family="dlrm", num_fields=20, num_dense=5, table_rows=997, embed_dim=64,
                        bottom_mlp=(32, 64), mlp_dims=(64, 32))
 
@@ -90,7 +93,7 @@ def _mixed_plan(cfg, world):
     return ShardingPlan(plan.tables, world, pl, plan.budget_bytes)
 
 
-def _worker(rank, world, port, policy, B, q):
+def _worker(rank, world, port, policy, B, q, hot=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -100,7 +103,7 @@ def _worker(rank, world, port, policy, B, q):
 
     try:
         ctx = init_from_env(device="cpu")
-        cfg = _small_cfg()
+        cfg = _small_cfg(hot)
         plan = _mixed_plan(cfg, world) if policy == "mixed" else None
         m = ShardedDLRM(cfg, ctx, plan=plan, policy=policy if policy != "mixed" else "auto")
         ref = build_model(cfg)
@@ -119,20 +122,24 @@ def _worker(rank, world, port, policy, B, q):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world,policy", [(2, "table"), (3, "table"), (2, "row"), (3, "mixed")])
-def test_sharded_dlrm_matches_unsharded(world, policy):
+@pytest.mark.parametrize("world,policy,hot", [(2, "table", 1), (3, "table", 1), (2, "row", 1), (3, "mixed", 1),
+                                              (2, "table", 3), (3, "auto", 2)])
+def test_sharded_dlrm_matches_unsharded(world, policy, hot):
+    """Sharded tables (table-wise, row-wise, mixed; one-hot and multi-hot
+    bags pooled on the owner) score exactly like the unsharded
+    DLRM of the same seed."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     B = 6
-    procs = [ctx.Process(target=_worker, args=(r, world, port, policy, B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, policy, B, q, hot)) for r in range(world)]
     [p.start() for p in procs]
     res = {}
     for _ in range(world):
         r, err, nbytes, nrw = q.get(timeout=240)
         res[r] = (err, nbytes, nrw)
     [p.join(timeout=60) for p in procs]
-    cfg = _small_cfg()
+    cfg = _small_cfg(hot)
     full_bytes = cfg.num_sparse * cfg.table_rows * 64 * 2
     for r in range(world):
         err, nbytes, nrw = res[r]
@@ -144,3 +151,43 @@ def test_sharded_dlrm_matches_unsharded(world, policy):
         if policy == "mixed":
             assert 0 < nrw < cfg.num_sparse
     assert sum(res[r][1] for r in range(world)) == pytest.approx(full_bytes, rel=0.01)
+
+
+@pytest.mark.parametrize("hot", [1, 3])
+def test_sharded_dlrm_one_rank_arena_program(hot):
+    """One rank: the sharded step program reading the request arena (the
+    route kernel's and the fused bottom tower's K0) scores like the unsharded
+    model; the exchange degenerates to the identity (no collectives, receive
+    buffers alias the send buffers)."""
+    from distributed_tf_serving_amd import ops
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.parallel import step_program as sp
+    from distributed_tf_serving_amd.parallel.dist import DistContext
+    from distributed_tf_serving_amd.parallel.embedding_sharding import ShardedDLRM
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    cfg = _small_cfg(hot)
+    cfg.bottom_mlp = (512, 256, 64)  # the fused bottom tower's shape (reads the arena)
+    m = ShardedDLRM(cfg, DistContext())
+    assert m.supports_arena and m.narrow_weight_cols() == (cfg.num_dense if hot == 1 else 0)
+    ref = build_model(cfg)
+    F = cfg.num_fields
+    A, L = ArenaLayout(F, 64), PackedLayout(F)
+    ar = A.alloc()
+    s = SyntheticRequests(fields=F, dist="zipf", id_space=1 << 40, seed=4)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((5, True), (9, False))]
+    ab = A.build(ar, A.place(ar, reqs))
+    assert not any(ab.errors)
+    B = 16
+    bufs = m.alloc(B)
+    assert "recv_ids" not in bufs or bufs["recv_ids"] is bufs["send_ids"]
+    out = torch.zeros(B)
+    ops_ = m.build_program(ops.ArenaRows(ar, B, F), None, B, bufs, out=out)
+    assert not any(isinstance(o, sp.Coll) for o in ops_)
+    sp.run_eager(ops_, None)
+    packed = A.unpack_cpu(ar, L.alloc(B))
+    want = ref(L.ids(packed)[:14], L.wts(packed)[:14])
+    assert (out[:14] - want).abs().max().item() < 1e-5
+    assert m.exchange_bytes(B) == 0

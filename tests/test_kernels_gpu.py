@@ -861,3 +861,44 @@ def test_dense_pad(cuda, M, n, K, ld):
     want = torch.zeros(M, K, dtype=torch.bfloat16)
     want[:, :n] = x[:, :n].cpu().to(torch.bfloat16)
     assert torch.equal(y.cpu(), want)
+
+
+@pytest.mark.parametrize("hot", [1, 3])
+def test_shard_route_arena_and_multi_hot(cuda, hot):
+    """K1b routing on the GPU: from ids + weights and straight from a device
+    request arena (raw and packed-varint requests), one-hot and multi-hot,
+    vs the CPU reference; the bag kernel writes into a static out buffer."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    F, W, tm = 4 + 6 * hot, 3, 2
+    A, L = ArenaLayout(F, 256), PackedLayout(F)
+    ar = A.alloc()
+    s = SyntheticRequests(fields=F, dist="zipf", id_space=1 << 40, seed=8)
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in ((30, True), (70, False), (1, True))]
+    assert not any(A.build(ar, A.place(ar, reqs)).errors)
+    B = 120  # > 101 rows: padding rows route id 0
+    packed = A.unpack_cpu(ar, L.alloc(B))
+    ids, wts = L.ids(packed), L.wts(packed)
+    col = torch.tensor([4 + hot * t for t in range(W * tm)], dtype=torch.int32)
+    mod = torch.tensor([997, 1000, 13, 50_000, 7, 101], dtype=torch.int64)
+    off = torch.tensor([0, 997, 0, 13, 0, 7], dtype=torch.int64)
+    want_w = torch.empty(W, B, tm * hot)
+    want = ops.shard_route(ids, W, tm, col, mod, off, hot=hot, wts=wts, out_w=want_w)
+    dev = ar.to(cuda)
+    A.decode_varints(dev)
+    d = [t.to(cuda) for t in (col, mod, off)]
+    got_w = torch.empty(W, B, tm * hot, device=cuda)
+    got = ops.shard_route(ops.ArenaRows(dev, B, F), W, tm, *d, hot=hot, out_w=got_w)
+    assert torch.equal(got.cpu(), want) and torch.equal(got_w.cpu(), want_w)
+    got2 = ops.shard_route(ids.to(cuda), W, tm, *d, hot=hot, wts=wts.to(cuda))
+    assert torch.equal(got2.cpu(), want)
+    if hot > 1:  # the owner's pooled bags into a static buffer
+        table = torch.randn(50_000, 64, device=cuda).to(torch.bfloat16)
+        offs = torch.arange(0, W * B * tm * hot + 1, hot, dtype=torch.int64, device=cuda)
+        out = torch.empty(W * B * tm, 64, dtype=torch.bfloat16, device=cuda)
+        r = ops.embedding_bag(table, got.view(-1), offs, per_sample_weights=got_w.view(-1), out_bf16=True, out=out)
+        assert r.data_ptr() == out.data_ptr()
+        ref = ops.embedding_bag(table.cpu(), got.cpu().view(-1), offs.cpu(), per_sample_weights=got_w.cpu().view(-1))
+        _close(out.float(), ref, 2e-2, 1e-2, "bag into a static buffer")
