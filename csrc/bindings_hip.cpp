@@ -1308,7 +1308,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
   m.def("set_gather_variant", &dtfs::set_gather_variant, py::arg("variant"),
-        "gather-GEMM kernel: 1 = output-side weights (default), 0 = LDS scale pass (A/B studies)");
+        "gather-GEMM kernel: 0 = LDS scale pass (default), 1 = output-side weights (A/B studies)");
   m.def("gather_variant", &dtfs::gather_variant);
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "

@@ -2155,7 +2155,7 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
   return hipGetLastError();
 }
 
-static int g_gather_variant = 1;
+static int g_gather_variant = 0;
 void set_gather_variant(int v) { g_gather_variant = v; }
 int gather_variant() { return g_gather_variant; }
 

@@ -7,7 +7,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest $TESTS -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -x -v --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_r4.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_r4.log; exit 1; }
   tail -3 gpurun_out/pytest_r4.log
 fi
@@ -26,6 +26,15 @@ for m in ${MODELS:-}; do
     > gpurun_out/bench_$m.log 2>&1 || { echo "bench $m failed"; tail -40 gpurun_out/bench_$m.log; exit 1; }
   grep '^{"metric' gpurun_out/bench_$m.log | cut -c1-1500
 done
+if [ "${REF:-0}" = "1" ]; then
+  # the reference workload in process, then over TCP from a separate process of native h2c clients
+  timeout -k 10 300 python -u bench.py --reference-workload > gpurun_out/bench_ref.log 2>&1 \
+    || { echo "reference workload failed"; tail -30 gpurun_out/bench_ref.log; exit 1; }
+  grep -E '^Average|^\{' gpurun_out/bench_ref.log | cut -c1-1200
+  timeout -k 10 400 python -u bench.py --reference-workload --over-grpc --grpc-threads ${GRPC_THREADS:-4} \
+    > gpurun_out/bench_ref_grpc.log 2>&1 || { echo "reference workload over gRPC failed"; tail -30 gpurun_out/bench_ref_grpc.log; exit 1; }
+  grep -E '^Average|^\{' gpurun_out/bench_ref_grpc.log | cut -c1-1500
+fi
 if [ -n "${COUNTERS:-}" ]; then
   OUT=gpurun_out/ctr4
   rm -rf $OUT && mkdir -p $OUT

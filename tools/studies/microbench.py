@@ -260,7 +260,7 @@ def gather_variant_study(rows=(2048, 16384), F=43, V=1_000_000, N=1024, dev="cud
                 r[f"v{v}_h_maxdiff"] = float((res[v][0].float() - res[variants[0]][0].float()).abs().max())
                 r[f"v{v}_parts_maxdiff"] = float((res[v][1][:, :B] - res[variants[0]][1][:, :B]).abs().max())
             out.append(r)
-    h.set_gather_variant(1)
+    h.set_gather_variant(0)
     return out
 
 
