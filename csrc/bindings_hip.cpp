@@ -1307,9 +1307,6 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
-  m.def("set_gather_variant", &dtfs::set_gather_variant, py::arg("variant"),
-        "gather-GEMM kernel: 0 = LDS scale pass (default), 1 = output-side weights (A/B studies)");
-  m.def("gather_variant", &dtfs::gather_variant);
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");

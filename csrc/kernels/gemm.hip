@@ -1564,321 +1564,6 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------------------
-// The gather-GEMM with the feature weights applied on the OUTPUT side (OSW).
-// Every K tile is one field f, and within it a row's weight w(m, f) is a
-// constant, so
-//   C[m, n] = sum_f w(m, f) * (sum_d T[row(m, f), d] W[n, 64 f + d])
-// - each 16x16 output tile takes its K tile as two MFMAs into a zeroed
-// temporary (raw table rows: no scaling of A at all) and adds w(m, f) x tmp to
-// the accumulator: 4 v_fma per tile, issued in the MFMA gaps (an MFMA of the
-// 16x16x32 form leaves 8 of its 16 cycles of vector issue free). The scale
-// pass of gemm_gather_kernel (2 x 16 KB LDS read-modify-write per K tile, ~40
-// VALU per wave, and the phase it needed) is gone; the A quarters keep the
-// dense 8-phase kernel's schedule:
-//   p0: stage Bq1(t+1)            p1: stage Aq1(t+1), ring(t+4)
-//   p2: stage Aq0(t+2)            p3: stage Bq0(t+2)
-// 9 DMA instructions per 4 phases -> vmcnt(9) retires what was issued 4
-// phases earlier. The rows for a stage are read from the ring one segment
-// ahead of it (p0 for Aq1, p1 - after Aq1's addresses are formed - for Aq0).
-// The MFMA sums are no longer bf16(w * e) . W but w * (e . W) in fp32: closer
-// to the exact product, not bit-identical to the unfused gather's rounding.
-// FM / the DCN cross dots still need w * e in fp32 for one quarter-half of the
-// rows per block: a READ-only pass (one 16-byte chunk and its weight per
-// thread per K tile, loaded with the MFMA fragments of that quarter).
-// Measured against gemm_gather_kernel in profiles/r04_gather_osw.md.
-template <typename OutT, int EXTRA>
-__global__ void __launch_bounds__(512) gemm_gather_osw_kernel(const uint8_t* __restrict__ table, int Vm1,
-                                                              const int32_t* __restrict__ rows_t,
-                                                              const float* __restrict__ wts_t, int64_t Mp,
-                                                              const uint8_t* __restrict__ W,
-                                                              const float* __restrict__ bias, OutT* __restrict__ C,
-                                                              int64_t ldc, float* __restrict__ fm_part,
-                                                              const float* __restrict__ cross_w,
-                                                              const float* __restrict__ cross_c, int cross_n, int M,
-                                                              int N, int F, int epi) {
-  constexpr int BM = 256, BN = 256;
-  constexpr int BUF = (BM + BN) * 128;  // 64 KiB
-  constexpr int RING = 8;
-  constexpr int XMAX = 4;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF + 3 * RING * BM * 4];
-  int32_t(*s_rows)[BM] = reinterpret_cast<int32_t(*)[BM]>(smem + 2 * BUF);
-  float(*s_wts)[BM] = reinterpret_cast<float(*)[BM]>(smem + 2 * BUF + RING * BM * 4);
-  float(*s_xw)[XMAX][64] = reinterpret_cast<float(*)[XMAX][64]>(smem + 2 * BUF + 2 * RING * BM * 4);
-
-  const int tiles_n = N / BN, tiles_m = int(Mp / BM);
-  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int lr = lane >> 3, ls = lane & 7;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int nk = F;
-  const int64_t ldw = int64_t(F) * 64;
-
-  auto a_row = [&](int qm, int g) { return (g < 8 ? 0 : 128) + 64 * qm + 8 * (g & 7); };
-  auto b_row = [&](int qn, int g) { return 64 * (g >> 2) + 32 * qn + 8 * (g & 3); };
-  const int coff = (ls ^ ((4 * (wid & 1)) | (lr >> 1))) << 4;  // see gemm_gather_kernel
-  const int b_lane = lr * int(ldw) * 2 + coff;
-  const int rk = wid % 3;
-  auto stage_ring = [&](int u) {
-    const int uc = min(u, nk - 1), slot = u & (RING - 1);
-    const void* g;
-    void* l;
-    if (rk == 2 && EXTRA == 2) {
-      const int xr = min(lane >> 4, cross_n - 1);
-      g = cross_w + int64_t(xr) * F * 64 + uc * 64 + (lane & 15) * 4;
-      l = &s_xw[slot][0][0];
-    } else {
-      const int64_t src = int64_t(uc) * Mp + m0 + lane * 4;
-      g = rk == 1 ? static_cast<const void*>(wts_t + src) : static_cast<const void*>(rows_t + src);
-      l = rk == 1 ? static_cast<void*>(&s_wts[slot][0])
-                  : (rk == 0 ? static_cast<void*>(&s_rows[slot][0]) : static_cast<void*>(&s_xw[slot][0][0]));
-    }
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
-                                     (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
-  };
-  int ida[2];
-  auto read_rows = [&](int q, int kt) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) ida[j] = s_rows[kt & (RING - 1)][a_row(q, wid + 8 * j) + lr];
-  };
-  auto stage_a = [&](int q, int kt) {
-    uint8_t* base = smem + (kt & 1) * BUF;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = min(max(ida[j], 0), Vm1);
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(table + int64_t(r) * 128 + coff),
-                                       (__attribute__((address_space(3))) void*)(base + a_row(q, wid + 8 * j) * 128),
-                                       16, 0, 0);
-    }
-  };
-  auto stage_b = [&](int q, int kt) {
-    uint8_t* base = smem + (kt & 1) * BUF;
-    const int64_t kb = int64_t(min(kt, nk - 1)) * 128;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rb = b_row(q, wid + 8 * j);
-      const uint8_t* src = W + (int64_t(n0 + rb) * ldw * 2 + kb) + uint32_t(b_lane);
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
-                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + rb * 128), 16, 0, 0);
-    }
-  };
-
-  // FM / cross: the block's quarter-half of rows, one chunk per thread (read only)
-  const int sp_rr = (threadIdx.x & 255) >> 3, sp_ch = threadIdx.x & 7;
-  const int sp_dim = 8 * (sp_ch ^ ((sp_rr >> 1) & 7));
-  const bool fm_on = EXTRA != 0 && fm_part != nullptr && tn < 4;
-  const int fm_q = tn >> 1, fm_h = tn & 1;
-  const int fm_row = 128 * wr + 64 * fm_q + sp_rr + 32 * fm_h;
-  constexpr int NFS = EXTRA == 1 ? 8 : (EXTRA == 2 ? XMAX : 1);
-  float fs[NFS], fsq = 0.f;
-#pragma unroll
-  for (int j = 0; j < NFS; ++j) fs[j] = 0.f;
-  i32x4 fu = {0, 0, 0, 0};
-  float fw = 0.f;
-  auto fm_load = [&](const uint8_t* buf, int u) {
-    fu = *reinterpret_cast<const i32x4*>(buf + fm_row * 128 + sp_ch * 16);
-    fw = s_wts[u & (RING - 1)][fm_row];
-  };
-  auto fm_acc = [&](int u) {
-    float v[8];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      v[2 * p] = __uint_as_float(uint32_t(fu[p]) << 16) * fw;
-      v[2 * p + 1] = __uint_as_float(uint32_t(fu[p]) & 0xffff0000u) * fw;
-    }
-    if constexpr (EXTRA == 1) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        fs[j] += v[j];
-        fsq += v[j] * v[j];
-      }
-    } else if constexpr (EXTRA == 2) {
-#pragma unroll
-      for (int l = 0; l < XMAX; ++l) {
-        const f32x4 c0 = *reinterpret_cast<const f32x4*>(&s_xw[u & (RING - 1)][l][sp_dim]);
-        const f32x4 c1 = *reinterpret_cast<const f32x4*>(&s_xw[u & (RING - 1)][l][sp_dim + 4]);
-        fs[l] += v[0] * c0[0] + v[1] * c0[1] + v[2] * c0[2] + v[3] * c0[3] + v[4] * c1[0] + v[5] * c1[1] +
-                 v[6] * c1[2] + v[7] * c1[3];
-      }
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: the ring for tiles 0-3, then the dense kernel's: tile 0 whole +
-  // tile 1's Aq0 / Bq0 (phases -2, -1 of the schedule), and the stagger
-  stage_ring(0);
-  stage_ring(1);
-  stage_ring(2);
-  stage_ring(3);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  read_rows(0, 0);
-  stage_a(0, 0);
-  stage_b(0, 0);
-  stage_b(1, 0);
-  read_rows(1, 0);
-  stage_a(1, 0);
-  read_rows(0, 1);
-  stage_a(0, 1);
-  stage_b(0, 1);
-  read_rows(1, 1);  // p0(0) reads nothing more: p1(0) stages Aq1(1)
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __syncthreads();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
-  asm volatile("" ::: "memory");
-
-  bf16x8 fa[2][4], fb[2][2][2];
-  float wv[4];
-  auto read_a = [&](const uint8_t* buf, int qm, int t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 128 * wr + 64 * qm + 16 * i + fr;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(buf + swz(row, kk * 4 + fq));
-      wv[i] = s_wts[t & (RING - 1)][row];
-    }
-  };
-  auto read_b = [&](const uint8_t* buf, int qn) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = 64 * wc + 32 * qn + 16 * j + fr;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        fb[qn][kk][j] = *reinterpret_cast<const bf16x8*>(buf + BM * 128 + swz(row, kk * 4 + fq));
-    }
-  };
-  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  // one quadrant: 8 output tiles, each = 2 MFMAs into a zeroed temporary + 4
-  // v_fma with the row weight; fm: the FM / cross VALU of this K tile too
-  auto mma = [&](int qm, int qn) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-    __builtin_amdgcn_sched_barrier(0);
-    // software-pipelined: tile k's MFMAs, then tile k-1's FMAs (its MFMA
-    // result is ready by then), so at most two temporaries are live
-    f32x4 prev = zero4;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = k >> 1, j = k & 1;
-      f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][0][j], fa[0][i], zero4, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][1][j], fa[1][i], t, 0, 0, 0);
-      if (k > 0) {
-        const int ip = (k - 1) >> 1, jp = (k - 1) & 1;
-        f32x4& c = acc[4 * qm + ip][2 * qn + jp];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = fmaf(wv[ip], prev[r], c[r]);
-      }
-      prev = t;
-      // pin the pairing: left free, the scheduler issues all 16 MFMAs first and
-      // keeps 8 temporaries live (spills at 256 VGPRs)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    {
-      f32x4& c = acc[4 * qm + 3][2 * qn + 1];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c[r] = fmaf(wv[3], prev[r], c[r]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto barrier = [] {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); };
-  for (int t = 0; t < nk; ++t) {
-    const uint8_t* buf = smem + (t & 1) * BUF;
-    // p0: A[qm0] (+ weights) B[qn0]; stage Bq1(t+1); the FM / cross terms of
-    // this K tile when the block's quarter is 0 (VALU in the read segment: it
-    // overlaps the other wave group's MFMAs; inside the MFMA cluster it made
-    // the compiler spill ~120 VGPRs)
-    read_a(buf, 0, t);
-    read_b(buf, 0);
-    if (EXTRA != 0 && fm_on && fm_q == 0) {
-      fm_load(buf, t);
-      fm_acc(t);
-    }
-    stage_b(1, t + 1);
-    wait_dma();
-    barrier();
-    mma(0, 0);
-    barrier();
-    // p1: B[qn1]; stage Aq1(t+1) (rows read in p0), then the rows for p2's stage; ring(t+4)
-    read_b(buf, 1);
-    stage_a(1, t + 1);
-    read_rows(0, t + 2);
-    stage_ring(t + 4);
-    wait_dma();
-    barrier();
-    mma(0, 1);
-    barrier();
-    // p2: A[qm1] (+ weights); stage Aq0(t+2); FM when its quarter is 1; rows for p1(t+1)'s stage
-    read_a(buf, 1, t);
-    if (EXTRA != 0 && fm_on && fm_q == 1) {
-      fm_load(buf, t);
-      fm_acc(t);
-    }
-    stage_a(0, t + 2);
-    read_rows(1, t + 2);
-    wait_dma();
-    barrier();
-    mma(1, 1);
-    barrier();
-    // p3: stage Bq0(t+2)
-    stage_b(0, t + 2);
-    wait_dma();
-    barrier();
-    mma(1, 0);
-    barrier();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
-
-  if (sizeof(OutT) == 2 && (epi & 15) != EPI_CROSS && ((N | int(ldc)) & 7) == 0)
-    plain_staged_epilogue<false>(acc, smem, m0, n0, wr, wc, wid, lane, M, N, bias, nullptr, nullptr,
-                                 reinterpret_cast<bf16*>(C), ldc, epi);
-  else
-    store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
-                              nullptr, 0, epi);
-  if constexpr (EXTRA == 1) {
-    if (fm_on) {
-      float part = -fsq;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += fs[j] * fs[j];
-      part += __shfl_xor(part, 1, 64);
-      part += __shfl_xor(part, 2, 64);
-      part += __shfl_xor(part, 4, 64);
-      if (sp_ch == 0) fm_part[Mp + m0 + fm_row] = 0.5f * part;
-    }
-  } else if constexpr (EXTRA == 2) {
-    if (fm_on) {
-#pragma unroll
-      for (int l = 0; l < XMAX; ++l) {
-        fs[l] += __shfl_xor(fs[l], 1, 64);
-        fs[l] += __shfl_xor(fs[l], 2, 64);
-        fs[l] += __shfl_xor(fs[l], 4, 64);
-      }
-      const int L = cross_n - 1;
-      float alpha = 1.f, dL = fs[0];
-#pragma unroll
-      for (int l = 0; l < XMAX; ++l) {
-        if (l < L) alpha += alpha * fs[l] + cross_c[l];
-        if (l == L) dL = fs[l];
-      }
-      if (sp_ch == 0) fm_part[Mp + m0 + fm_row] = alpha * dL + cross_c[L];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Deep-pipelined LDS-DMA variant: a STAGES-deep ring of K tiles with PREFETCH =
 // STAGES - 1 tiles in flight across barriers (cdna_hip_programming.md §5
 // "Pipelining across barriers"): every iteration issues the DMA for tile
@@ -2155,10 +1840,6 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
   return hipGetLastError();
 }
 
-static int g_gather_variant = 0;
-void set_gather_variant(int v) { g_gather_variant = v; }
-int gather_variant() { return g_gather_variant; }
-
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                               int N, int epi, hipStream_t st, const float* cross_w, const float* cross_c,
@@ -2170,17 +1851,10 @@ hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_
     return hipErrorInvalidValue;
   if (cross_w && (!fm_part || !cross_c || cross_n < 1 || cross_n > 4)) return hipErrorInvalidValue;
   const int grid = int(Mp / 256) * (N / 256);
-  // g_gather_variant: 1 = output-side weights (gemm_gather_osw_kernel), 0 = the LDS scale pass
 #define DTFS_GG(X)                                                                                                 \
-  if (g_gather_variant == 1)                                                                                       \
-    hipLaunchKernelGGL((gemm_gather_osw_kernel<bf16, X>), dim3(grid), dim3(512), 0, st,                           \
-                       static_cast<const uint8_t*>(table), int(V - 1), rows_t, wts_t, Mp,                          \
-                       static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc, fm_part, cross_w, cross_c, \
-                       cross_n, M, N, F, epi);                                                                     \
-  else                                                                                                             \
-    hipLaunchKernelGGL((gemm_gather_kernel<bf16, X>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(table), \
-                       int(V - 1), rows_t, wts_t, Mp, static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc,  \
-                       fm_part, cross_w, cross_c, cross_n, M, N, F, epi)
+  hipLaunchKernelGGL((gemm_gather_kernel<bf16, X>), dim3(grid), dim3(512), 0, st, static_cast<const uint8_t*>(table), \
+                     int(V - 1), rows_t, wts_t, Mp, static_cast<const uint8_t*>(W), bias, static_cast<bf16*>(C), ldc,  \
+                     fm_part, cross_w, cross_c, cross_n, M, N, F, epi)
   if (cross_w) DTFS_GG(2);
   else if (fm_part) DTFS_GG(1);
   else DTFS_GG(0);

@@ -137,9 +137,6 @@ struct MxIO {
 // cross_w / cross_c / cross_n (DCN v1, with fm_part): the folded cross
 // weights fp32 [cross_n][64F] + constants (EmbedArgs.cross_*, cross_n <= 4);
 // fm_part's row 1 then receives the cross logit instead of the FM term.
-// Gather-GEMM variant (A/B studies): 0 = LDS scale pass (default), 1 = output-side weights.
-void set_gather_variant(int v);
-int gather_variant();
 hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                               int F, const void* W, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                               int N, int epi, hipStream_t st, const float* cross_w = nullptr,

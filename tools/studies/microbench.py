@@ -132,8 +132,6 @@ def main():
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
     ap.add_argument("--gather-gemm", action="store_true", help="K1 fused into K4 vs gather + GEMM")
-    ap.add_argument("--gather-variants", action="store_true",
-                    help="gather-GEMM kernel variants (LDS scale pass vs output-side weights), interleaved")
     ap.add_argument("--gather-locality", action="store_true",
                     help="gather-GEMM time by where the table rows come from (L2 / MALL / HBM)")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
@@ -152,9 +150,6 @@ def main():
         M, N, K = (int(x) for x in shape.split(","))
         print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
         return
-    if a.gather_variants:
-        for r in gather_variant_study():
-            print(json.dumps(r), flush=True)
     if a.gather_locality:
         for r in gather_locality_study():
             print(json.dumps(r), flush=True)
@@ -226,41 +221,6 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
             r[f"{k}_us"] = round(statistics.median(v), 2)
         r["fused_tflops"] = round(2.0 * B * N * F * 64 / r["fused_us"] / 1e6, 1)
         out.append(r)
-    return out
-
-
-def gather_variant_study(rows=(2048, 16384), F=43, V=1_000_000, N=1024, dev="cuda", variants=(0, 1)):
-    """The gather-GEMM's kernel variants (ops.hip().set_gather_variant: 0 = LDS
-    scale pass, 1 = output-side weights) at the DeepFM shape, with and without
-    the FM term, interleaved rounds; max |diff| of each variant vs variant 0."""
-    from distributed_tf_serving_amd.client.synth import SyntheticRequests
-
-    h = ops.hip()
-    table = (torch.randn(V, 64, device=dev) * 0.05).to(torch.bfloat16)
-    lin = torch.randn(V, device=dev) * 0.01
-    W = (torch.randn(N, F * 64, device=dev) * 0.02).to(torch.bfloat16)
-    b = torch.randn(N, device=dev) * 0.01
-    out = []
-    for B in rows:
-        ids_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
-        ids, wts = torch.from_numpy(ids_np).to(dev), torch.from_numpy(wts_np).to(dev)
-        for fm2 in (False, True):
-            t = {v: [] for v in variants}
-            res = {}
-            for _ in range(5):
-                for v in variants:
-                    h.set_gather_variant(v)
-                    t[v].append(_time(lambda: ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=fm2), 20, 1))
-            for v in variants:
-                h.set_gather_variant(v)
-                res[v] = ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=fm2)
-            r = {"op": "gather_variants", "B": B, "fm2": fm2}
-            for v in variants:
-                r[f"v{v}_us"] = round(statistics.median(t[v]), 2)
-                r[f"v{v}_h_maxdiff"] = float((res[v][0].float() - res[variants[0]][0].float()).abs().max())
-                r[f"v{v}_parts_maxdiff"] = float((res[v][1][:, :B] - res[variants[0]][1][:, :B]).abs().max())
-            out.append(r)
-    h.set_gather_variant(0)
     return out
 
 
