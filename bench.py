@@ -102,6 +102,9 @@ def parse_args():
     ap.add_argument("--peer-comm", type=int, default=None,
                     help="one-shot peer exchange (csrc/kernels/peer.hip) for fan-out / step-program messages of at "
                          "most this many bytes per peer (1 = 64 KiB, 0 = RCCL only; default: $DTFS_PEER_COMM or 0)")
+    ap.add_argument("--scatter-path", default="shared", choices=["shared", "rccl"],
+                    help="scatter mode: shared = each GPU DMAs its share of rank 0's shared request arenas; "
+                         "rccl = RCCL scatter / gather of packed rows")
     ap.add_argument("--mode", default=None, choices=["alltoall", "scatter", "local"],
                     help="N > 1: alltoall = every request fanned out over all GPUs (config 3, default); local = "
                          "one independent replica per GPU (default for dlrm: its tables are sharded instead and "
@@ -222,13 +225,21 @@ def build(a, ctx):
     # an all-to-all splits every rank's rows evenly over the GPUs
     small = [b for b in small if mode != "alltoall" or b % world == 0]
     buckets = sorted({b for b in small if 0 < b < B} | {B})
+    # scatter on one node: every rank DMAs its share of rank 0's shared arenas
+    # (csrc/runtime/shared_scatter.h); --scatter-path rccl: the RCCL scatter
+    shared = mode == "scatter" and world > 1 and a.scatter_path == "shared"
     # fan-out rows travel narrow (int32 table rows + bf16 weights: half the xGMI bytes)
-    layout = layout_for(cfg, mode != "local" and not a.no_narrow) if mode != "local" else PackedLayout(F)
+    layout = (layout_for(cfg, not a.no_narrow) if mode != "local" and not shared else PackedLayout(F))
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=not a.no_graphs, slots=a.slots)
     rows_in_max = B * (world if mode == "scatter" else 1)
-    arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max))
+    arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max), gpu_varint=not shared)
+    seg = None
+    if shared:
+        from distributed_tf_serving_amd.parallel.shared_scatter import scatter_for_engine
+
+        seg = scatter_for_engine(ctx, F, arena_layout.capacity, a.slots, B, tag="bench")
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
-                       group=step_group)
+                       group=step_group, shared_scatter=seg)
     for b in buckets:
         eng.prepare(b)
     if a.h2d_wait and dev.type == "cuda":
@@ -240,7 +251,7 @@ def build(a, ctx):
         for b in buckets:
             if not eng.self_check(b, seed=rank):
                 raise SystemExit(f"rank {rank}: the fan-out step's scores differ from a local forward (bucket {b})")
-        if dev.type == "cuda" and eng.mode != "local" and not eng.native_fanout_active:
+        if dev.type == "cuda" and eng.mode != "local" and eng.scatter is None and not eng.native_fanout_active:
             raise SystemExit(f"rank {rank}: the native fan-out step is not active")
     return cfg, model, eng, B
 
@@ -427,6 +438,14 @@ def run_live(a, ctx, cfg, model, eng, B):
             "multi_hot": int(getattr(model, "hot", 1)),
             "hot_row_cache": None,  # every remote row crosses xGMI (no replica cache yet)
         }
+    if eng.scatter is not None:
+        # shared-arena scatter: host->device bytes this rank copied per step (its
+        # share of rank 0's batch), gathered from every rank
+        per = torch.tensor([float(eng.scatter.h2d_bytes) / max(1, eng.scatter.h2d_steps)], dtype=torch.float64)
+        allp = [torch.zeros_like(per) for _ in range(world)]
+        dist.all_gather(allp, per, group=phase)
+        extra["scatter"] = {"path": "shared arena (each GPU DMAs its own share over its own link)",
+                            "h2d_bytes_per_step_by_rank": [int(x.item()) for x in allp]}
     try:
         from distributed_tf_serving_amd.utils.affinity import placement
 
@@ -577,6 +596,10 @@ def main():
         if eng.mode == "local":
             par = f"candidate-dp{world} (" + ("one GPU, no fan-out" if world == 1 else
                                               "one independent replica per GPU, no collectives") + ")"
+        elif eng.scatter is not None:
+            par = (f"candidate-dp{world} (scatter fan-out through rank 0's shared request arenas: every GPU DMAs "
+                   f"its own share, scores written into rank 0's shared output; "
+                   + ("native C++ step" if dev.type == "cuda" else "host reference (CPU)") + ")")
         else:
             par = (f"candidate-dp{world} ({eng.mode} fan-out over RCCL"
                    + (", native C++ step" if eng.native_fanout_active else ", gloo (CPU)")

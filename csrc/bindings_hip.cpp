@@ -261,32 +261,10 @@ std::vector<torch::Tensor> embed_arena(torch::Tensor table, c10::optional<torch:
 //   parts fp32 [1 + (fm2 or cross), Mp]: row 0 = bias + first-order FM term,
 //         row 1 the second-order FM term or (cross_w / cross_c: DCN v1's folded
 //         cross weights) the cross logit; the head sums the rows.
-std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::Tensor> lin,
-                                      c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
-                                      c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
-                                      double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2,
-                                      c10::optional<torch::Tensor> cross_w, c10::optional<torch::Tensor> cross_c) {
-  check_dev(table, "table");
-  check_dev(W, "W");
-  check_dev(b, "b");
-  check_same_dev(table, W, "W");
-  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2 && table.size(1) == 64 &&
-                  table.is_contiguous(),
-              "gather-GEMM: table must be contiguous bf16 [V, 64]");
-  const int64_t V = table.size(0);
-  TORCH_CHECK(F >= 1 && F <= 64, "gather-GEMM handles 1..64 fields");
-  TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]");
-  TORCH_CHECK(W.scalar_type() == torch::kBFloat16 && W.dim() == 2 && W.size(1) == F * 64 && W.is_contiguous(),
-              "W must be contiguous bf16 [N, 64 F]");
-  const int64_t N = W.size(0);
-  TORCH_CHECK(N % 256 == 0 && (!fm2 || N >= 1024), "gather-GEMM needs N % 256 == 0 (and N >= 1024 with FM)");
-  TORCH_CHECK(b.scalar_type() == torch::kFloat32 && b.numel() == N, "b must be fp32 [N]");
-  TORCH_CHECK(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
-  if (lin) {
-    check_dev(*lin, "lin");
-    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
-  }
-  dtfs::EmbedArgs a;
+// Request rows of a gather-GEMM: a device request arena, or ids (+ weights).
+void embed_gemm_inputs(const torch::Tensor& table, const c10::optional<torch::Tensor>& arena,
+                       const c10::optional<torch::Tensor>& ids, const c10::optional<torch::Tensor>& wts, int64_t B,
+                       int64_t F, dtfs::EmbedArgs& a) {
   if (arena) {
     check_dev(*arena, "arena");
     check_same_dev(table, *arena, "arena");
@@ -314,6 +292,59 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
       a.wts_ld = wts->stride(0);
     }
   }
+}
+
+// K1 resolve into fresh field-major buffers (B rounded up to 256 rows).
+std::vector<torch::Tensor> embed_gemm_resolve_into(const torch::Tensor& table, const c10::optional<torch::Tensor>& lin,
+                                                   dtfs::EmbedArgs a, int64_t B, int64_t F, int64_t modulo,
+                                                   double bias, int64_t n_parts) {
+  const int64_t Mp = (B + 255) / 256 * 256;
+  auto parts = torch::empty({n_parts, Mp}, table.options().dtype(torch::kFloat32));
+  auto rows_t = torch::empty({F, Mp}, table.options().dtype(torch::kInt32));
+  auto wts_t = torch::empty({F, Mp}, table.options().dtype(torch::kFloat32));
+  if (B == 0) return {rows_t, wts_t, parts};
+  a.table = table.data_ptr();
+  a.lin = lin ? lin->data_ptr<float>() : nullptr;
+  a.B = int(B);
+  a.F = int(F);
+  a.D = 64;
+  a.V = table.size(0);
+  a.modulo = modulo;
+  a.bias = float(bias);
+  check_hip(dtfs::launch_embed_resolve(a, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), parts.data_ptr<float>(),
+                                       Mp, cur_stream(table)),
+            "embed_resolve");
+  return {rows_t, wts_t, parts};
+}
+
+std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::Tensor> lin,
+                                      c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
+                                      c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
+                                      double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2,
+                                      c10::optional<torch::Tensor> cross_w, c10::optional<torch::Tensor> cross_c,
+                                      c10::optional<std::vector<torch::Tensor>> resolved) {
+  check_dev(table, "table");
+  check_dev(W, "W");
+  check_dev(b, "b");
+  check_same_dev(table, W, "W");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2 && table.size(1) == 64 &&
+                  table.is_contiguous(),
+              "gather-GEMM: table must be contiguous bf16 [V, 64]");
+  const int64_t V = table.size(0);
+  TORCH_CHECK(F >= 1 && F <= 64, "gather-GEMM handles 1..64 fields");
+  TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]");
+  TORCH_CHECK(W.scalar_type() == torch::kBFloat16 && W.dim() == 2 && W.size(1) == F * 64 && W.is_contiguous(),
+              "W must be contiguous bf16 [N, 64 F]");
+  const int64_t N = W.size(0);
+  TORCH_CHECK(N % 256 == 0 && (!fm2 || N >= 1024), "gather-GEMM needs N % 256 == 0 (and N >= 1024 with FM)");
+  TORCH_CHECK(b.scalar_type() == torch::kFloat32 && b.numel() == N, "b must be fp32 [N]");
+  TORCH_CHECK(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
+  }
+  dtfs::EmbedArgs a;
+  embed_gemm_inputs(table, arena, ids, wts, B, F, a);
   const bool cross = cross_w.has_value();
   if (cross) {
     check_dev(*cross_w, "cross_w");
@@ -330,22 +361,23 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
   c10::DeviceGuard g(table.device());
   const int64_t Mp = (B + 255) / 256 * 256;
   auto h = torch::empty({B, N}, table.options());
-  auto parts = torch::empty({(fm2 || cross) ? 2 : 1, Mp}, table.options().dtype(torch::kFloat32));
-  auto rows_t = torch::empty({F, Mp}, table.options().dtype(torch::kInt32));
-  auto wts_t = torch::empty({F, Mp}, table.options().dtype(torch::kFloat32));
+  std::vector<torch::Tensor> r;
+  if (resolved) {
+    // the resolve pass ran earlier (embed_gemm_resolve, e.g. on another lane)
+    r = *resolved;
+    TORCH_CHECK(r.size() == 3, "resolved = (rows_t, wts_t, parts)");
+    TORCH_CHECK(r[0].scalar_type() == torch::kInt32 && r[0].dim() == 2 && r[0].size(0) == F && r[0].size(1) == Mp &&
+                    r[0].is_contiguous() && r[1].scalar_type() == torch::kFloat32 && r[1].sizes() == r[0].sizes() &&
+                    r[1].is_contiguous() && r[2].scalar_type() == torch::kFloat32 && r[2].dim() == 2 &&
+                    r[2].size(0) == ((fm2 || cross) ? 2 : 1) && r[2].size(1) == Mp && r[2].is_contiguous(),
+                "resolved tensors do not match this gather-GEMM's shape");
+    for (const auto& t : r) check_same_dev(table, t, "resolved");
+  } else {
+    r = embed_gemm_resolve_into(table, lin, a, B, F, modulo, bias, (fm2 || cross) ? 2 : 1);
+  }
+  const torch::Tensor &rows_t = r[0], &wts_t = r[1], &parts = r[2];
   if (B == 0) return {h, parts};
-  a.table = table.data_ptr();
-  a.lin = lin ? lin->data_ptr<float>() : nullptr;
-  a.B = int(B);
-  a.F = int(F);
-  a.D = 64;
-  a.V = V;
-  a.modulo = modulo;
-  a.bias = float(bias);
   auto st = cur_stream(table);
-  check_hip(dtfs::launch_embed_resolve(a, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), parts.data_ptr<float>(),
-                                       Mp, st),
-            "embed_resolve");
   check_hip(dtfs::launch_gemm_gather(table.data_ptr(), V, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), Mp,
                                      int(F), W.data_ptr(), b.data_ptr<float>(), h.data_ptr(), N,
                                      (fm2 || cross) ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st,
@@ -353,6 +385,31 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
                                      cross ? cross_c->data_ptr<float>() : nullptr, cross ? int(cross_w->size(0)) : 0),
             "gemm_gather");
   return {h, parts};
+}
+
+// The gather-GEMM's front half alone (K1 resolve): field-major table rows /
+// weights + the first-order partial, for a gather-GEMM launched later (or on
+// another stream: the step program's aux lane resolves step k+1 while the
+// compute lane finishes step k).
+std::vector<torch::Tensor> embed_gemm_resolve(torch::Tensor table, c10::optional<torch::Tensor> lin,
+                                              c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> ids,
+                                              c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
+                                              double bias, int64_t n_parts) {
+  check_dev(table, "table");
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2 && table.size(1) == 64 &&
+                  table.is_contiguous(),
+              "gather-GEMM: table must be contiguous bf16 [V, 64]");
+  TORCH_CHECK(F >= 1 && F <= 64, "gather-GEMM handles 1..64 fields");
+  TORCH_CHECK(modulo > 0 && modulo <= table.size(0), "modulo must be in (0, table rows]");
+  TORCH_CHECK(n_parts == 1 || n_parts == 2, "n_parts must be 1 or 2");
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == table.size(0), "lin must be fp32 [V]");
+  }
+  dtfs::EmbedArgs a;
+  embed_gemm_inputs(table, arena, ids, wts, B, F, a);
+  c10::DeviceGuard g(table.device());
+  return embed_gemm_resolve_into(table, lin, a, B, F, modulo, bias, n_parts);
 }
 
 // ---------------------------------------------------------------- K1b
@@ -1176,6 +1233,46 @@ dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object
 // The device side of a GPU live server: the StepRunner plus, per bucket and
 // slot, the step to launch (direct kernel launches of the captured step, its
 // graph, or the fan-out step with its RCCL communicators).
+// One shared-scatter step of this rank (runtime/shared_scatter.h): rank 0
+// publishes the plan over its built shared arena, every rank copies only its
+// share (copy stream, its own PCIe link) into `dst` and launches the local step
+// on it; the step's head writes the rank's scores into rank 0's shared output.
+// Returns the step index.
+uint64_t scatter_step(dtfs::runtime::StepRunner& r, dtfs::runtime::SharedScatter& sc, int slot, int64_t rows_per_rank,
+                      const uint8_t* arena, void* dst, int64_t dst_cap, const dtfs::runtime::KernelSequence* seq,
+                      hipGraphExec_t graph, int64_t timeout_us) {
+  const uint64_t k = sc.begin_step();
+  if (sc.rank() == 0) {
+    const int ai = arena ? sc.arena_index(arena) : -1;
+    if (ai < 0) throw std::runtime_error("shared scatter: rank 0's batch is not in a shared arena");
+    sc.publish_plan(k, ai, rows_per_rank);
+  }
+  dtfs::runtime::RankShare mine;
+  int ai = -1;
+  if (!sc.wait_plan(k, timeout_us, &mine, &ai))
+    throw std::runtime_error("shared scatter: no plan for step " + std::to_string(k) + " from rank 0");
+  const auto copies = dtfs::runtime::share_copies(sc.arena(ai), mine, sc.stage(slot));
+  int64_t n = 0;
+  for (const auto& c : copies) {
+    if (c.dst_off < 0 || c.dst_off + c.n > dst_cap) throw std::runtime_error("shared scatter: share outside the device arena");
+    n += c.n;
+  }
+  sc.add_h2d(n);
+  r.launch_copies(slot, dst, copies, seq, graph, true);
+  return k;
+}
+
+// Wait for step k on `slot`: this rank's step, then (rank 0) every rank's share.
+bool scatter_wait(dtfs::runtime::StepRunner& r, dtfs::runtime::SharedScatter& sc, int slot, uint64_t k,
+                  int64_t timeout_us, const std::vector<dtfs::comm::RcclComm*>& comms, std::string* err) {
+  if (!r.wait_for(slot, timeout_us, comms, err)) return false;
+  sc.mark_done(k);
+  if (sc.rank() != 0) return true;
+  if (!sc.wait_done(k, timeout_us, err)) return false;
+  sc.compact_scores(k, slot);
+  return true;
+}
+
 class GpuBackend : public dtfs::runtime::StepBackend {
  public:
   GpuBackend(dtfs::runtime::StepRunner* runner, std::vector<int64_t> buckets,
@@ -1198,8 +1295,23 @@ class GpuBackend : public dtfs::runtime::StepBackend {
   }
   int slots() const override { return int(slots_[0].size()); }
   const std::vector<int64_t>& buckets() const override { return buckets_; }
+  // shared-scatter mode: every local-kind slot's step runs on this rank's
+  // share of rank 0's batch; share_rows[b] = rows per rank of bucket b
+  void set_scatter(dtfs::runtime::SharedScatter* sc, std::vector<int64_t> share_rows, int64_t timeout_us) {
+    TORCH_CHECK(share_rows.size() == buckets_.size(), "shared scatter: one share row count per bucket");
+    TORCH_CHECK(slots() <= dtfs::runtime::kScatterMaxSlots && slots() <= sc->slots(), "shared scatter: too many slots");
+    sc_ = sc;
+    share_rows_ = std::move(share_rows);
+    slot_step_.assign(size_t(slots()), 0);
+    timeout_us_ = timeout_us;
+  }
   void launch(int slot, int b, const uint8_t* arena, const dtfs::runtime::ArenaBatch& batch) override {
     const auto& s = slots_[size_t(b)][size_t(slot)];
+    if (sc_ && !s.program && !s.fanout) {
+      slot_step_[size_t(slot)] = scatter_step(*runner_, *sc_, slot, share_rows_[size_t(b)], arena, s.h2d_dst,
+                                              s.h2d_cap, s.seq, s.graph, timeout_us_);
+      return;
+    }
     // the header + descriptors always travel, so an empty (lockstep) step
     // sees zero rows instead of the slot's previous batch
     const int64_t nbytes = batch.used_bytes;
@@ -1218,6 +1330,7 @@ class GpuBackend : public dtfs::runtime::StepBackend {
     }
   }
   bool wait(int slot, int64_t timeout_us, std::string* err) override {
+    if (sc_) return scatter_wait(*runner_, *sc_, slot, slot_step_[size_t(slot)], timeout_us, comms_, err);
     return runner_->wait_for(slot, timeout_us, comms_, err);
   }
   const float* scores(int slot, int b) const override { return slots_[size_t(b)][size_t(slot)].h_out; }
@@ -1232,6 +1345,10 @@ class GpuBackend : public dtfs::runtime::StepBackend {
   std::vector<int64_t> buckets_;
   std::vector<std::vector<dtfs::runtime::LoopSlot>> slots_;  // [bucket][slot]
   std::vector<dtfs::comm::RcclComm*> comms_;
+  dtfs::runtime::SharedScatter* sc_ = nullptr;
+  std::vector<int64_t> share_rows_;
+  std::vector<uint64_t> slot_step_;  // step index of each slot's last launch (launcher writes, completer reads)
+  int64_t timeout_us_ = 10'000'000;
 };
 
 struct PyGpuLive {
@@ -1246,7 +1363,7 @@ struct PyGpuLive {
 
 // buckets: [(rows, [slot dict per slot]), ...] ascending.
 PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, py::list arenas,
-                         py::object control) {
+                         py::object control, py::object scatter, py::object share_rows) {
   auto* p = new PyGpuLive();
   dtfs::runtime::StepControl* ctl = dtfs_live::control_from(control, &p->keep);
   p->keep.push_back(runner_obj);
@@ -1263,6 +1380,10 @@ PyGpuLive* make_gpu_live(py::object runner_obj, py::dict cfg, py::list buckets, 
   }
   auto ar = dtfs_live::arenas_from(arenas, true, &p->keep);
   p->backend = std::make_unique<GpuBackend>(&runner, std::move(rows), std::move(slots));
+  if (auto* sc = dtfs_live::scatter_from(scatter, &p->keep)) {
+    const auto lc = dtfs_live::live_config_from(cfg);
+    p->backend->set_scatter(sc, share_rows.cast<std::vector<int64_t>>(), lc.step_timeout_us);
+  }
   p->srv = std::make_unique<dtfs::runtime::LiveServer>(p->backend.get(), dtfs_live::live_config_from(cfg),
                                                        std::move(ar), ctl);
   return p;
@@ -1282,7 +1403,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dense_pad", &dense_pad, py::arg("x"), py::arg("n"), py::arg("K"));
   m.def("embed_gemm", &embed_gemm, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"), py::arg("wts"),
         py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W"), py::arg("b"), py::arg("act"),
-        py::arg("fm2"), py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none());
+        py::arg("fm2"), py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none(),
+        py::arg("resolved") = py::none());
+  m.def("embed_gemm_resolve", &embed_gemm_resolve, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"),
+        py::arg("wts"), py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("n_parts"),
+        "gather-GEMM front half (K1 resolve) -> (rows_t, wts_t, parts) for embed_gemm(resolved=...)");
   m.def("embed_arena", &embed_arena, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("B"), py::arg("F"),
         py::arg("modulo"), py::arg("bias") = 0.0, py::arg("want_x") = true, py::arg("want_fm") = false,
         py::arg("fm2") = false, py::arg("out_x") = py::none(), py::arg("k_pad") = 0, py::arg("cross_w") = py::none(),
@@ -1422,11 +1547,51 @@ PYBIND11_MODULE(_hip, m) {
                             "Live serving core (csrc/runtime/live_server.h) on this GPU: requests are batched into "
                             "pinned arenas and run as captured step kernels (or the fan-out step)");
     c.def(py::init(&make_gpu_live), py::arg("runner"), py::arg("config"), py::arg("buckets"), py::arg("arenas"),
-          py::arg("control") = py::none());
+          py::arg("control") = py::none(), py::arg("scatter") = py::none(), py::arg("share_rows") = py::none());
     dtfs_live::def_live_methods(c);
   }
   dtfs_live::def_step_control(m);
   dtfs_live::def_grpc_front<PyGpuLive>(m);
+  {
+    auto sc = dtfs_live::def_shared_scatter(m);
+    sc.def(
+          "register_with_gpu",
+          [](dtfs::runtime::SharedScatter& s) {
+            // every rank pins the whole mapping for its own GPU: its DMA reads
+            // rank 0's arenas, its head kernel writes the shared scores
+            check_hip(hipHostRegister(s.base(), s.bytes(), hipHostRegisterMapped), "hipHostRegister(shared scatter)");
+            s.set_on_unmap([](void* p, size_t) { (void)hipHostUnregister(p); });
+          })
+        .def(
+            "launch",
+            [](dtfs::runtime::SharedScatter& s, dtfs::runtime::StepRunner& r, int slot, int64_t rows_per_rank,
+               c10::optional<torch::Tensor> arena, torch::Tensor dst, py::object seq, uintptr_t graph_exec,
+               double timeout_s) {
+              TORCH_CHECK(dst.is_cuda() && dst.is_contiguous() && dst.numel() >= s.arena_cap(),
+                          "dst must be a device arena of the segment's capacity");
+              const dtfs::runtime::KernelSequence* ks =
+                  seq.is_none() ? nullptr : &seq.cast<dtfs::runtime::KernelSequence&>();
+              TORCH_CHECK(ks || graph_exec, "need a kernel sequence or a graph");
+              const uint8_t* a = arena ? static_cast<const uint8_t*>(arena->data_ptr()) : nullptr;
+              return scatter_step(r, s, slot, rows_per_rank, a, dst.data_ptr(), int64_t(dst.nbytes()), ks,
+                                  reinterpret_cast<hipGraphExec_t>(graph_exec), int64_t(timeout_s * 1e6));
+            },
+            py::arg("runner"), py::arg("slot"), py::arg("rows_per_rank"), py::arg("arena"), py::arg("dst"),
+            py::arg("seq"), py::arg("graph_exec"), py::arg("timeout_s") = 10.0,
+            "engine-level shared-scatter step (self-check); returns the step index")
+        .def(
+            "wait",
+            [](dtfs::runtime::SharedScatter& s, dtfs::runtime::StepRunner& r, int slot, uint64_t k, double timeout_s) {
+              std::string err;
+              bool ok;
+              {
+                py::gil_scoped_release nogil;
+                ok = scatter_wait(r, s, slot, k, int64_t(timeout_s * 1e6), {}, &err);
+              }
+              return py::make_tuple(ok, err);
+            },
+            py::arg("runner"), py::arg("slot"), py::arg("step"), py::arg("timeout_s") = 10.0);
+  }
 
   m.def("rccl_set_library", &dtfs::comm::set_library, py::arg("path"));
   // NUMA-local pinned host memory (runtime/numa.h): pages placed on `node`

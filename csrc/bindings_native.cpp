@@ -764,6 +764,7 @@ PYBIND11_MODULE(_native, m) {
     dtfs_live::def_live_methods(c);
   }
   dtfs_live::def_step_control(m);
+  dtfs_live::def_shared_scatter(m);
   dtfs_live::def_grpc_front<PyCpuLive>(m);
   m.attr("STATUS_OVERSIZE") = int(runtime::kOversize);
   m.attr("STATUS_CALLER_PATH") = int(runtime::kCallerPath);

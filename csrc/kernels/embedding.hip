@@ -451,9 +451,12 @@ __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_
                                                            float* __restrict__ wts_t, float* __restrict__ part0,
                                                            int64_t Mp) {
   constexpr int RB = 16, KMAX = (kWave * RB) / 256;  // items per thread for F <= 64
-  __shared__ int32_t s_row[kWave * RB];
-  __shared__ float s_w[kWave * RB];
-  __shared__ float s_lin[kWave * RB];
+  // field stride RB + 1: the transposing stores (consecutive lanes =
+  // consecutive fields) hit 64 distinct banks instead of 4
+  constexpr int RS = RB + 1;
+  __shared__ int32_t s_row[kWave * RS];
+  __shared__ float s_w[kWave * RS];
+  __shared__ float s_lin[kWave * RS];
   __shared__ int2 s_desc[RB];
   const int F = a.F, t = threadIdx.x, n = F * RB;
   const int b0 = blockIdx.x * RB;
@@ -507,19 +510,19 @@ __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_
     const int i = t + 256 * k;
     if (i >= n) continue;
     const int r = i / F, f = i - r * F;
-    s_row[f * RB + r] = row[k];
-    s_w[f * RB + r] = w[k];
-    s_lin[f * RB + r] = lin[k];
+    s_row[f * RS + r] = row[k];
+    s_w[f * RS + r] = w[k];
+    s_lin[f * RS + r] = lin[k];
   }
   __syncthreads();
   for (int i = t; i < n; i += 256) {
     const int f = i / RB, r = i % RB;
-    rows_t[int64_t(f) * Mp + b0 + r] = s_row[i];
-    wts_t[int64_t(f) * Mp + b0 + r] = s_w[i];
+    rows_t[int64_t(f) * Mp + b0 + r] = s_row[f * RS + r];
+    wts_t[int64_t(f) * Mp + b0 + r] = s_w[f * RS + r];
   }
   if (t < RB) {
     float s = a.bias;
-    for (int f = 0; f < F; ++f) s += s_lin[f * RB + t];
+    for (int f = 0; f < F; ++f) s += s_lin[f * RS + t];
     part0[b0 + t] = s;
   }
 }

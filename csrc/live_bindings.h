@@ -20,6 +20,7 @@
 #include "runtime/batcher.h"
 #include "runtime/live_server.h"
 #include "runtime/loadgen.h"
+#include "runtime/shared_scatter.h"
 #include "runtime/step_control.h"
 
 namespace dtfs_live {
@@ -89,6 +90,116 @@ inline void def_step_control(py::module& m) {
           },
           py::arg("timeout_s"))
       .def("unlink", &StepControl::unlink);
+}
+
+// SharedScatter (runtime/shared_scatter.h) of this module (module-local like
+// StepControl). Host-side operations only; the GPU module adds registration
+// and the device launch (bindings_hip.cpp).
+using dtfs::runtime::SharedScatter;
+using ScatterClass = py::class_<SharedScatter, std::shared_ptr<SharedScatter>>;
+
+inline ScatterClass def_shared_scatter(py::module& m) {
+  ScatterClass c(m, "SharedScatter", py::module_local(),
+                 "Scatter fan-out through rank 0's shared request arenas (one node; runtime/shared_scatter.h)");
+  c.def(py::init<std::string, int, int, bool, int64_t, int, int64_t, int, int64_t, int>(), py::arg("name"),
+        py::arg("world"), py::arg("rank"), py::arg("create"), py::arg("fields") = 0, py::arg("n_arenas") = 0,
+        py::arg("arena_cap") = 0, py::arg("slots") = 0, py::arg("out_floats") = 0, py::arg("node") = -1)
+      .def_property_readonly("world", &SharedScatter::world)
+      .def_property_readonly("rank", &SharedScatter::rank)
+      .def_property_readonly("n_arenas", &SharedScatter::n_arenas)
+      .def_property_readonly("slots", &SharedScatter::slots)
+      .def_property_readonly("arena_cap", &SharedScatter::arena_cap)
+      .def_property_readonly("out_floats", &SharedScatter::out_floats)
+      .def_property_readonly("h2d_bytes", &SharedScatter::h2d_bytes)
+      .def_property_readonly("h2d_steps", &SharedScatter::h2d_steps)
+      .def_property_readonly("all_attached", &SharedScatter::all_attached)
+      .def("unlink", &SharedScatter::unlink)
+      // views into the mapping: valid while this object lives (the engine keeps it)
+      .def(
+          "arena",
+          [](SharedScatter& s, int i) {
+            return torch::from_blob(s.arena(i), {s.arena_cap()}, torch::TensorOptions().dtype(torch::kUInt8));
+          },
+          py::arg("index"))
+      .def(
+          "out",
+          [](SharedScatter& s, int slot) {
+            return torch::from_blob(s.out(slot), {s.out_floats()}, torch::TensorOptions().dtype(torch::kFloat32));
+          },
+          py::arg("slot"))
+      .def(
+          "arena_index",
+          [](SharedScatter& s, torch::Tensor t) { return s.arena_index(static_cast<const uint8_t*>(t.data_ptr())); },
+          py::arg("arena"))
+      .def("begin_step", &SharedScatter::begin_step)
+      .def("publish_plan", &SharedScatter::publish_plan, py::arg("step"), py::arg("arena_index"),
+           py::arg("rows_per_rank"))
+      .def(
+          "take_share",
+          [](SharedScatter& s, uint64_t k, torch::Tensor dst, double timeout_s) {
+            // host path (CPU backend): wait for step k's plan and copy this
+            // rank's share into dst (an arena of the same layout) with memcpy
+            TORCH_CHECK(dst.device().is_cpu() && dst.is_contiguous() && dst.scalar_type() == torch::kUInt8 &&
+                            dst.numel() >= s.arena_cap(),
+                        "dst must be a contiguous CPU uint8 arena of the segment's capacity");
+            dtfs::runtime::RankShare mine;
+            int ai = -1;
+            bool ok;
+            {
+              py::gil_scoped_release nogil;
+              ok = s.wait_plan(k, int64_t(timeout_s * 1e6), &mine, &ai);
+            }
+            TORCH_CHECK(ok, "shared scatter: no plan for step ", k, " from rank 0");
+            uint8_t hdr[64];
+            const auto copies = dtfs::runtime::share_copies(s.arena(ai), mine, hdr);
+            uint8_t* d = dst.data_ptr<uint8_t>();
+            int64_t n = 0;
+            for (const auto& cp : copies) {
+              std::memcpy(d + cp.dst_off, cp.src, size_t(cp.n));
+              n += cp.n;
+            }
+            s.add_h2d(n);
+            return py::make_tuple(mine.row0, mine.rows, n);
+          },
+          py::arg("step"), py::arg("dst"), py::arg("timeout_s") = 10.0)
+      .def("mark_done", &SharedScatter::mark_done, py::arg("step"))
+      .def("compact_scores", &SharedScatter::compact_scores, py::arg("step"), py::arg("slot"))
+      .def(
+          "wait_done",
+          [](const SharedScatter& s, uint64_t k, double timeout_s) {
+            std::string err;
+            bool ok;
+            {
+              py::gil_scoped_release nogil;
+              ok = s.wait_done(k, int64_t(timeout_s * 1e6), &err);
+            }
+            return py::make_tuple(ok, err);
+          },
+          py::arg("step"), py::arg("timeout_s"))
+      .def_static(
+          "shares",
+          [](torch::Tensor arena, int64_t fields, int world, int64_t rows_per_rank) {
+            // plan of a built arena, for tests: [(row0, rows, [(lo, hi), ...]), ...]
+            TORCH_CHECK(arena.device().is_cpu() && arena.is_contiguous(), "arena must be a contiguous CPU tensor");
+            std::vector<dtfs::runtime::RankShare> sh(static_cast<size_t>(world));
+            dtfs::runtime::compute_shares(arena.data_ptr<uint8_t>(), arena.numel(), fields, world, rows_per_rank,
+                                          sh.data());
+            py::list out;
+            for (const auto& r : sh) {
+              py::list rg;
+              for (int i = 0; i < r.n_ranges; ++i) rg.append(py::make_tuple(r.r[i].lo, r.r[i].hi));
+              out.append(py::make_tuple(r.row0, r.rows, rg));
+            }
+            return out;
+          },
+          py::arg("arena"), py::arg("fields"), py::arg("world"), py::arg("rows_per_rank"));
+  return c;
+}
+
+inline SharedScatter* scatter_from(const py::object& o, std::vector<py::object>* keep) {
+  if (o.is_none()) return nullptr;
+  keep->push_back(o);
+  return &o.cast<SharedScatter&>();
 }
 
 inline StepControl* control_from(const py::object& o, std::vector<py::object>* keep) {

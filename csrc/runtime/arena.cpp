@@ -340,37 +340,40 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
 void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, int64_t fields) {
   // the GPU decodes varint ids in its own copy of the arena; do the same here
   arena_varint_cpu(const_cast<uint8_t*>(base));
-  const int32_t n = std::min<int32_t>(*reinterpret_cast<const int32_t*>(base), int32_t(kArenaMaxRequests));
-  const int64_t* desc = reinterpret_cast<const int64_t*>(base + 64);
+  // rows through the row table, exactly as the GPU readers find them
+  // (csrc/kernels/common.h arena_row): a shared-scatter share carries only its
+  // rows' table entries and bytes, not the request descriptors
+  int64_t total, rt;
+  std::memcpy(&total, base + 8, 8);
+  std::memcpy(&rt, base + 16, 8);
   const uint8_t* payload = base + kArenaPayloadOff;
   const int32_t nwc = *reinterpret_cast<const int32_t*>(base + 36);
   const int64_t wcols = nwc > 0 && nwc < fields ? nwc : fields;  // narrowed rows: weights kept per row
   const int64_t idb = *reinterpret_cast<const int32_t*>(base + 40) == 3 ? 3 : 4;  // narrowed rows: bytes per id
   std::memset(dst, 0, size_t(B * W * 8));
-  for (int32_t i = 0; i < n; ++i) {
-    const bool narrow = (desc[4 * i + 0] & kNarrowFlag) != 0;
-    for (int64_t r = 0; r < desc[4 * i + 2]; ++r) {
-      const int64_t row = desc[4 * i + 3] + r;
-      if (row >= B) break;
-      if (narrow) {  // int32 rows -> int64, fp32 weights as they are
-        const uint8_t* ip = payload + (desc[4 * i + 0] & ~kNarrowFlag) + r * idb * fields;
-        const uint8_t* wp = payload + desc[4 * i + 1] + r * 4 * wcols;
-        for (int64_t f = 0; f < fields; ++f) {
-          int32_t id = 0;
-          if (idb == 3) {
-            id = int32_t(uint32_t(ip[3 * f]) | uint32_t(ip[3 * f + 1]) << 8 | uint32_t(ip[3 * f + 2]) << 16);
-          } else {
-            std::memcpy(&id, ip + 4 * f, 4);
-          }
-          const int64_t id64 = id;
-          std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
+  const int64_t n = std::min(total, B);
+  for (int64_t row = 0; row < n; ++row) {
+    int32_t e[2];
+    std::memcpy(e, payload + rt + 8 * row, 8);
+    const bool narrow = e[0] < 0;
+    const uint8_t* ip = payload + int64_t(uint32_t(e[0]) & 0x7fffffffu);
+    const uint8_t* wp = payload + e[1];
+    if (narrow) {  // int32 / 3-byte rows -> int64, fp32 weights as they are
+      for (int64_t f = 0; f < fields; ++f) {
+        int32_t id = 0;
+        if (idb == 3) {
+          id = int32_t(uint32_t(ip[3 * f]) | uint32_t(ip[3 * f + 1]) << 8 | uint32_t(ip[3 * f + 2]) << 16);
+        } else {
+          std::memcpy(&id, ip + 4 * f, 4);
         }
-        std::memcpy(dst + row * W * 8 + 8 * fields, wp, size_t(4 * wcols));  // dropped columns stay 0
-        continue;
+        const int64_t id64 = id;
+        std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
       }
-      std::memcpy(dst + row * W * 8, payload + desc[4 * i + 0] + r * 8 * fields, size_t(8 * fields));
-      std::memcpy(dst + row * W * 8 + 8 * fields, payload + desc[4 * i + 1] + r * 4 * fields, size_t(4 * fields));
+      std::memcpy(dst + row * W * 8 + 8 * fields, wp, size_t(4 * wcols));  // dropped columns stay 0
+      continue;
     }
+    std::memcpy(dst + row * W * 8, ip, size_t(8 * fields));
+    std::memcpy(dst + row * W * 8 + 8 * fields, wp, size_t(4 * fields));
   }
 }
 

@@ -115,6 +115,12 @@ void* alloc_on_node(size_t bytes, int node) {
   return p;
 }
 
+bool bind_range_to_node(void* p, size_t bytes, int node) {
+  if (!p || node < 0 || node >= kMaxNodes) return false;
+  NodeMask m(node);
+  return syscall(SYS_mbind, p, bytes, kMpolBind, m.bits, (unsigned long)kMaxNodes, 0u) == 0;
+}
+
 void free_on_node(void* p, size_t bytes) {
   if (!p) return;
   const size_t pg = size_t(sysconf(_SC_PAGESIZE));

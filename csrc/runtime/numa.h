@@ -31,6 +31,9 @@ bool prefer_numa_node(int node);
 // Page-aligned; free with free_on_node(p, bytes).
 void* alloc_on_node(size_t bytes, int node);
 void free_on_node(void* p, size_t bytes);
+// Place the (not yet touched) pages of [p, p + bytes) on `node` (mbind
+// MPOL_BIND; p page-aligned). false: no NUMA support / bad node.
+bool bind_range_to_node(void* p, size_t bytes, int node);
 // The NUMA node of the page holding `p` (move_pages query), -1 on error.
 int page_numa_node(const void* p);
 

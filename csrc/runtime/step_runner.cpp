@@ -54,9 +54,13 @@ StepRunner::~StepRunner() {
     if (s) hipStreamDestroy(s);
 }
 
+void StepRunner::ensure_aux_stream() {
+  if (!ingress_) ck(hipStreamCreateWithFlags(&ingress_, hipStreamNonBlocking), "hipStreamCreate(ingress)");
+}
+
 void StepRunner::ensure_fanout_streams() {
-  if (ingress_) return;
-  ck(hipStreamCreateWithFlags(&ingress_, hipStreamNonBlocking), "hipStreamCreate(ingress)");
+  if (egress_) return;
+  ensure_aux_stream();
   ck(hipStreamCreateWithFlags(&egress_, hipStreamNonBlocking), "hipStreamCreate(egress)");
   in_done_.resize(done_.size());
   fwd_done_.resize(done_.size());
@@ -96,6 +100,13 @@ void StepRunner::copy_checked(void* dst, const void* src, int64_t nbytes, hipMem
 }
 
 void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate) {
+  std::vector<ShareCopy> one;
+  if (nbytes > 0) one.push_back(ShareCopy{0, static_cast<const uint8_t*>(src), nbytes});
+  h2d_copies(slot, dst, one, consumer, alternate);
+}
+
+void StepRunner::h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer,
+                            bool alternate) {
   hipStream_t st = copy_;
   if (alternate) {
     if (!copy2_) ck(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking), "hipStreamCreate(copy2)");
@@ -106,7 +117,12 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
   // server waits for step k - depth before it launches k).
   if (used_[slot] && !observed_[slot].load(std::memory_order_acquire))
     ck(hipStreamWaitEvent(st, done_[slot], 0), "hipStreamWaitEvent(copy)");
-  if (nbytes > 0) copy_checked(dst, src, nbytes, hipMemcpyHostToDevice, st, slot, "H2D");
+  int64_t nbytes = 0;
+  for (const ShareCopy& c : copies) {
+    if (c.n <= 0) continue;
+    copy_checked(static_cast<uint8_t*>(dst) + c.dst_off, c.src, c.n, hipMemcpyHostToDevice, st, slot, "H2D");
+    nbytes += c.n;
+  }
   ck(hipEventRecord(h2d_done_[slot], st), "hipEventRecord(h2d)");
   if (host_wait_h2d_ && consumer == compute_ && nbytes > 0) {
     // The launcher thread waits for the copy instead of the compute queue:
@@ -208,7 +224,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
-  ensure_fanout_streams();  // the aux lane is the ingress stream
+  ensure_aux_stream();  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
     // lane-to-lane dependencies stay on the device: no system-scope release
@@ -218,9 +234,11 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
       ck(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate(program)");
   }
   hipStream_t lanes[2] = {compute_, ingress_};
-  // WAR on the slot's buffers + the H2D of the request bytes (one copy stream:
-  // a third hardware queue for copies would alias the aux lane's)
-  h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], false);
+  // WAR on the slot's buffers + the H2D of the request bytes. Copies
+  // alternate over two copy streams unless the fan-out streams exist too
+  // (copy, copy2, compute, aux = GPU_MAX_HW_QUEUES 4; a fifth stream would
+  // alias a queue and serialise the step)
+  h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
   for (const ProgOp& o : p.ops) {
     hipStream_t st = lanes[o.lane];
@@ -274,6 +292,21 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d(slot, dst, src, nbytes, compute_, true);
   seq->launch(compute_, done_[slot], false, skip_varint);
+  used_[slot] = 1;
+}
+
+void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, const KernelSequence* seq,
+                               hipGraphExec_t graph, bool skip_varint) {
+  if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
+  if (!seq && !graph) throw std::invalid_argument("launch_copies: no kernel sequence or graph");
+  ck(hipSetDevice(device_), "hipSetDevice");
+  h2d_copies(slot, dst, copies, compute_, true);
+  if (seq) {
+    seq->launch(compute_, done_[slot], false, skip_varint);
+  } else {
+    ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
+    ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
+  }
   used_[slot] = 1;
 }
 

@@ -20,6 +20,7 @@
 
 #include "../comm/rccl_comm.h"
 #include "kernel_seq.h"
+#include "shared_scatter.h"  // ShareCopy
 
 namespace dtfs {
 namespace runtime {
@@ -129,6 +130,10 @@ class StepRunner {
   // Same, replaying the step as direct kernel launches (no graph-launch gap).
   void launch_seq(int slot, void* dst, const void* src, int64_t nbytes, const KernelSequence* seq,
                   bool skip_varint = false);
+  // Same, with the H2D as several copies into dst (a rank's share of a
+  // shared-scatter batch, runtime/shared_scatter.h); seq or graph.
+  void launch_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, const KernelSequence* seq,
+                     hipGraphExec_t graph, bool skip_varint = false);
   // Enqueue one fan-out step (see FanoutStep).
   void launch_fanout(int slot, const FanoutStep& s);
   // Enqueue one programmed step (see StepProgram).
@@ -158,6 +163,7 @@ class StepRunner {
   void copy_checked(void* dst, const void* src, int64_t nbytes, hipMemcpyKind kind, hipStream_t st, int slot,
                     const char* what);
   void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
+  void h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer, bool alternate);
   hipStream_t copy2_ = nullptr;  // second H2D stream, alternated with copy_ by local steps
   // default: the device waits (round 3, one box, 3 interleaved reps of the
   // served DeepFM step with fp32-weight 5.8 MB copies: 92.5 / 94.7 / 94.7 M
@@ -168,6 +174,7 @@ class StepRunner {
   // another thread than the launcher)
   std::unique_ptr<std::atomic<bool>[]> observed_;
   void ensure_fanout_streams();
+  void ensure_aux_stream();
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
   std::vector<hipEvent_t> prog_ev_;  // [slot * kProgEvents + k], created on first program launch

@@ -47,13 +47,15 @@ NATIVE_SOURCES = [
     "net/h2_server.cpp",
     "net/h2_client.cpp",
     "runtime/numa.cpp",
+    "runtime/shared_scatter.cpp",
 ]
 HIP_HOST_SOURCES = ["bindings_hip.cpp", "runtime/step_runner.cpp", "comm/rccl_comm.cpp",
                     "runtime/kernel_seq.cpp",
                     # shared with _native (the loop parses arenas / encodes responses itself)
                     "runtime/arena.cpp", "runtime/thread_pool.cpp", "wire/tensor_codec.cpp", "runtime/trace.cpp",
                     "runtime/batcher.cpp", "runtime/live_server.cpp", "runtime/loadgen.cpp", "runtime/narrow.cpp",
-                    "runtime/step_control.cpp", "net/hpack.cpp", "net/h2_server.cpp", "runtime/numa.cpp"]
+                    "runtime/step_control.cpp", "net/hpack.cpp", "net/h2_server.cpp", "runtime/numa.cpp",
+                    "runtime/shared_scatter.cpp"]
 
 
 def _torch_paths():

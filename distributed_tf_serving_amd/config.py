@@ -82,6 +82,9 @@ class ServingConfig:
     live: bool = True                 # native live server (csrc/runtime/live_server.h); False: Python scheduler
     step_timeout_s: float = 10.0      # a GPU step that takes longer marks the server broken (UNAVAILABLE)
     peer_timeout_s: float = 5.0       # multi-rank: a rank silent this long (no heartbeat) breaks the cluster
+    # scatter mode on one node: "shared" = every rank DMAs its share of rank 0's
+    # shared request arenas (csrc/runtime/shared_scatter.h); "rccl" = RCCL scatter
+    scatter_path: str = "shared"
     narrow_ingest: bool = True        # GPU live server: int64 ids -> int32 rows, fp32 weights -> bf16 on the host
 
 

@@ -81,7 +81,7 @@ class CTRModel(nn.Module):
             wts = wts.float()
         return self._forward(ids, wts, out)
 
-    def _forward(self, ids, wts, out=None):  # pragma: no cover - abstract
+    def _forward(self, ids, wts, out=None, resolved=None):  # pragma: no cover - abstract
         raise NotImplementedError
 
     # families whose only use of ids / weights is the first embedding gather
@@ -98,6 +98,40 @@ class CTRModel(nn.Module):
                 and (wts is None or wts.dtype == torch.float32)
                 and first.act in ("relu", "none") and first.k == first.in_dim
                 and ops.embed_gemm_ok(self.emb, first.weight, int(ids.shape[0]), fm2))
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        """The step runs the gather-GEMM (so its resolve pass can move to the aux lane)."""
+        return False
+
+    def _resolve(self, ids, wts):
+        """The gather-GEMM's front half of this family (ops.embed_gemm_resolve)."""
+        raise NotImplementedError
+
+    # A local GPU step as a two-lane program (parallel/step_program.py): the
+    # gather-GEMM's resolve pass of step k+1 runs on the aux lane right after
+    # its H2D, while the compute lane finishes step k (DTFS_RESOLVE_LANE=1,
+    # parallel/fanout.py _program_enabled).
+    resolve_lane = False
+
+    def build_program(self, ids, wts, B: int, bufs: dict, out: Optional[torch.Tensor] = None,
+                      state: Optional[dict] = None) -> list:
+        from ..parallel import step_program as sp
+
+        st = {} if state is None else state
+        if self.resolve_lane and self._resolve_applies(ids, wts):
+            def resolve():
+                st["resolved"] = self._resolve(ids, wts)
+
+            def main():
+                st["scores"] = self._forward(ids, wts, out, resolved=st["resolved"])
+
+            return [sp.Kernels(sp.AUX, resolve, "resolve"), sp.Sync("record", sp.AUX, 0),
+                    sp.Sync("wait", sp.COMPUTE, 0), sp.Kernels(sp.COMPUTE, main, "forward")]
+
+        def fwd():
+            st["scores"] = self._forward(ids, wts, out)
+
+        return [sp.Sync("record", sp.AUX, 0), sp.Sync("wait", sp.COMPUTE, 0), sp.Kernels(sp.COMPUTE, fwd, "forward")]
 
     @torch.no_grad()
     def forward_arena(self, arena: torch.Tensor, B: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -126,11 +160,19 @@ class WideDeep(CTRModel):
         return ops.embed(self.emb, ids, wts, lin=self.wide, modulo=self.cfg.vocab_size, bias=self.wide_bias,
                          want_x=True, want_fm=True, fm2=False)
 
-    def _forward(self, ids, wts, out=None):
+    resolve_lane = True
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        return self._gather_gemm(ids, wts, fm2=False)
+
+    def _resolve(self, ids, wts):
+        return ops.embed_gemm_resolve(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, False)
+
+    def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_gemm(ids, wts, fm2=False):
             first = self.mlp.layers[0]
             h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
-                                     first.bias, first.act, fm2=False)
+                                     first.bias, first.act, fm2=False, resolved=resolved)
             return self.mlp.forward_head(h, self.head_w, self.head_b, extra=wide, out=out, start=1)
         x, wide = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide, out=out)
@@ -155,12 +197,20 @@ class DeepFM(CTRModel):
         return ops.embed(self.emb, ids, wts, lin=self.lin, modulo=self.cfg.vocab_size, bias=self.fm_bias,
                          want_x=True, want_fm=True, fm2=True)
 
-    def _forward(self, ids, wts, out=None):
+    resolve_lane = True
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        return self._gather_gemm(ids, wts, fm2=True)
+
+    def _resolve(self, ids, wts):
+        return ops.embed_gemm_resolve(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, True)
+
+    def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_gemm(ids, wts, fm2=True):
             # K1 + K2 inside the first layer's GEMM: x never reaches HBM
             first = self.mlp.layers[0]
             h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
-                                   first.bias, first.act, fm2=True)
+                                   first.bias, first.act, fm2=True, resolved=resolved)
             return self.mlp.forward_head(h, self.head_w, self.head_b, extra=fm, out=out, start=1)
         x, fm = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm, out=out)
@@ -188,13 +238,22 @@ class DCN(CTRModel):
                                     requires_grad=False)
         self.head_b = 0.0
 
-    def _forward(self, ids, wts, out=None):
+    resolve_lane = True
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        return self.cfg.num_cross_layers + 1 <= 4 and self._gather_gemm(ids, wts, fm2=True)
+
+    def _resolve(self, ids, wts):
+        return ops.embed_gemm_resolve(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, True)
+
+    def _forward(self, ids, wts, out=None, resolved=None):
         if self.cfg.num_cross_layers + 1 <= 4 and self._gather_gemm(ids, wts, fm2=True):
             # gather + cross network + first MLP layer in one kernel (x0 never in HBM)
             first = self.mlp.layers[0]
             h, parts = ops.embed_gemm(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, first.weight, first.bias,
                                       first.act, fm2=False,
-                                      cross=(self.cross_w, self.cross_b, self.head_wc, self._cross_consts()))
+                                      cross=(self.cross_w, self.cross_b, self.head_wc, self._cross_consts()),
+                                      resolved=resolved)
             return self.mlp.forward_head(h, self.head_wd, self.head_b, extra=parts, out=out, start=1)
         # the whole cross network rides on the gather (ops.embed_cross): the
         # wave holding x0 computes its L + 1 weight dot products

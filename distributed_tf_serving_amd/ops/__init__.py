@@ -423,9 +423,24 @@ def embed_gemm_ok(table: torch.Tensor, W: torch.Tensor, B: int, fm2: bool) -> bo
             and table.shape[0] <= 2 ** 31 and N * K * 2 < 2 ** 31 and B >= GATHER_GEMM_MIN_ROWS)
 
 
+def embed_gemm_resolve(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor],
+                       modulo: int, bias: float, two_parts: bool) -> Tuple[torch.Tensor, ...]:
+    """The gather-GEMM's front half alone (GPU): (rows_t, wts_t, parts) for
+    ``embed_gemm(..., resolved=...)``, so a step program can resolve step k+1
+    on its aux lane while the compute lane finishes step k. ``two_parts``: the
+    consumer computes the FM term or the cross network (fm2 or cross)."""
+    m = int(modulo) if modulo > 0 else table.shape[0]
+    n_parts = 2 if two_parts else 1
+    if isinstance(ids, ArenaRows):
+        return tuple(hip().embed_gemm_resolve(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m,
+                                              float(bias), n_parts))
+    return tuple(hip().embed_gemm_resolve(table, lin, None, _rows(ids), None if wts is None else _rows(wts),
+                                          int(ids.shape[0]), int(ids.shape[1]), m, float(bias), n_parts))
+
+
 def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
                bias: float, W: torch.Tensor, b: torch.Tensor, act: str = "relu",
-               fm2: bool = True, cross=None) -> Tuple[torch.Tensor, torch.Tensor]:
+               fm2: bool = True, cross=None, resolved=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """K1 fused into the first MLP layer (K4): returns
       h     = act(x W^T + b) bf16 [B, N], x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)),
       parts = fp32 [1 + fm2, >= B]: row 0 = bias + sum_f lin[row] w, row 1 the
@@ -433,6 +448,7 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
     ``cross = (w, b, head_w)`` (DCN v1, fm2 False): row 1 of parts is the cross
     network's logit x_L . head_w instead (the GPU takes the folded weights,
     ``cross_consts = cross_v1_consts(w, b, head_w)``, as ``cross[3]`` when given).
+    ``resolved``: the front half from :func:`embed_gemm_resolve` (GPU only).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
     table rows straight into the GEMM's LDS tiles); on the CPU the unfused math."""
     m = int(modulo) if modulo > 0 else table.shape[0]
@@ -442,11 +458,12 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
         xw = xc = None
         if cross is not None:
             xw, xc = cross[3] if len(cross) > 3 and cross[3] is not None else cross_v1_consts(*cross[:3])
+        r = list(resolved) if resolved is not None else None
         if isinstance(ids, ArenaRows):
             return tuple(hip().embed_gemm(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias),
-                                          W, b, a, fm2, xw, xc))
+                                          W, b, a, fm2, xw, xc, r))
         return tuple(hip().embed_gemm(table, lin, None, _rows(ids), None if wts is None else _rows(wts),
-                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2, xw, xc))
+                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2, xw, xc, r))
     if cross is not None:
         x, logit = embed_cross(table, ids, wts, m, cross[0], cross[1], cross[2])
         first = torch.full((1, x.shape[0]), float(bias), dtype=torch.float32)

@@ -16,6 +16,13 @@ network hop becomes collectives on device buffers of packed rows
               scales with N instead of saturating rank 0's link.
 ``local``     no fan-out (each rank serves its own rows): the baseline.
 
+``scatter`` on one node runs through rank 0's shared request arenas when the
+engine gets a ``shared_scatter`` segment (parallel/shared_scatter.py,
+csrc/runtime/shared_scatter.h): every rank DMAs only its share of rank 0's
+batch over its own PCIe link, runs the LOCAL step on it and writes its scores
+into rank 0's shared output - no collective in the step. The RCCL scatter is
+the fallback.
+
 Per step every rank runs, on its own HIP streams::
 
     H2D (copy stream) -> collective -> graph(forward) -> collective -> D2H
@@ -66,10 +73,28 @@ class _RunnerEvent:
         return self.runner.query(self.slot)
 
 
+class _ScatterEvent:
+    """A shared-scatter step: this rank's step, then (rank 0) every rank's share."""
+
+    __slots__ = ("eng", "slot", "k")
+
+    def __init__(self, eng, slot, k):
+        self.eng, self.slot, self.k = eng, slot, k
+
+    def synchronize(self, timeout_s: Optional[float] = None):
+        ok, err = self.eng.scatter.wait(self.eng.runner(), self.slot, self.k, float(timeout_s or 1e6))
+        if not ok:
+            raise StepTimeout(f"shared scatter step failed: {err}")
+
+    def query(self) -> bool:  # polled by _wait_event: wait in full instead
+        self.synchronize(self.eng.step_timeout_s)
+        return True
+
+
 def _wait_event(ev, timeout_s: Optional[float]) -> None:
     """Bounded wait on a torch event or a _RunnerEvent."""
-    if isinstance(ev, _RunnerEvent) or timeout_s is None:
-        ev.synchronize(timeout_s) if isinstance(ev, _RunnerEvent) else ev.synchronize()
+    if isinstance(ev, (_RunnerEvent, _ScatterEvent)) or timeout_s is None:
+        ev.synchronize(timeout_s) if isinstance(ev, (_RunnerEvent, _ScatterEvent)) else ev.synchronize()
         return
     deadline = time.monotonic() + timeout_s
     spins = 0
@@ -101,7 +126,7 @@ class StepHandle:
 class FanoutEngine:
     def __init__(self, executor: ShardExecutor, ctx: DistContext, mode: str = "alltoall", group=None,
                  step_graphs: bool = True, native_launch: bool = True, ingest: str = "packed", arena=None,
-                 native_fanout: bool = True, force_fanout: bool = False):
+                 native_fanout: bool = True, force_fanout: bool = False, shared_scatter=None):
         """``ingest="packed"``: the host decodes into packed rows (host_in) and
         the H2D moves rows. ``ingest="arena"``: the host only parses request
         framing into a request arena (serving/arena.py); the H2D moves the raw
@@ -130,6 +155,9 @@ class FanoutEngine:
         self.group = group
         self.native_fanout = native_fanout
         self.force_fanout = force_fanout
+        # shared-arena scatter (scatter mode, one node): the step is local
+        self.scatter = shared_scatter if (self.mode == "scatter" and ingest == "arena") else None
+        self._local_arena: Dict[int, torch.Tensor] = {}
         self._cin = self._cout = None
         self._cprog = None  # step-program communicator (embedding-parallel models)
         self._programs: Dict[Tuple[int, int], object] = {}
@@ -180,6 +208,8 @@ class FanoutEngine:
         return t
 
     def host_out(self, B: int, slot: int = 0) -> torch.Tensor:
+        if self.scatter is not None:  # rank 0's shared output; rank r's share at r * B
+            return self.scatter.out(slot)[: self.world * B]
         key = (B, slot)
         t = self._host_out.get(key)
         if t is None:
@@ -187,8 +217,16 @@ class FanoutEngine:
             self._host_out[key] = t
         return t
 
+    def step_out(self, B: int, slot: int = 0) -> torch.Tensor:
+        """Where this rank's step writes its B scores."""
+        if self.scatter is not None:
+            return self.scatter.out(slot)[self.rank * B: (self.rank + 1) * B]
+        return self.host_out(B, slot)[:B]
+
     def host_arena(self, slot: int = 0) -> torch.Tensor:
         """Pinned request arena of a slot (arena ingest)."""
+        if self.scatter is not None:  # rank 0's batches live in the shared segment
+            return self.scatter.arena(slot % self.scatter.n_arenas)
         t = self._host_arena.get(slot)
         if t is None:
             t = self._host_arena[slot] = self.arena.alloc(pin=self.cuda)
@@ -222,7 +260,7 @@ class FanoutEngine:
     def prepare(self, B: int) -> None:
         self.check_bucket(B)
         if self._program_enabled():
-            if self._cprog is None:
+            if self._cprog is None and getattr(self.ex.model, "supports_program", False):
                 from .native_comm import create_comm
 
                 self._cprog = create_comm(self.ctx, self.group)
@@ -237,7 +275,8 @@ class FanoutEngine:
         if native:
             self._ensure_comms()
         for s in range(self.ex.slots):
-            self.host_in(B, s)
+            if self.scatter is None:  # shared scatter: the batch stays in rank 0's shared arenas
+                self.host_in(B, s)
             self.host_out(B, s)
             if self._step_graphs_enabled():
                 self._capture_step(B, s)
@@ -252,10 +291,16 @@ class FanoutEngine:
     def _program_enabled(self) -> bool:
         if not (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"):
             return False
-        # embedding-parallel models: the exchange is the program. (Local
-        # steps stay serial: a cross-step overlapped gather slowed the fused
-        # head 12.6 -> 61 us, 176-182 vs 174-175 us per step, profiles/step_overlap.md)
-        return bool(getattr(self.ex.model, "supports_program", False))
+        # embedding-parallel models: the exchange is the program. Local
+        # gather-GEMM steps may run as one too (DTFS_RESOLVE_LANE=1): the
+        # resolve pass of step k+1 on the aux lane right after its H2D, the
+        # compute lane waiting only for that (a cross-step overlapped GATHER
+        # slowed the fused head 12.6 -> 61 us, profiles/step_overlap.md; the
+        # resolve pass is a tenth of its bytes)
+        m = self.ex.model
+        if getattr(m, "supports_program", False):
+            return True
+        return os.environ.get("DTFS_RESOLVE_LANE", "0") == "1" and bool(getattr(m, "resolve_lane", False))
 
     def _capture_program(self, B: int, slot: int) -> None:
         """Build and capture the step program of one (bucket, slot): GPU unpack
@@ -303,6 +348,8 @@ class FanoutEngine:
 
     # -- native fan-out (world > 1) -----------------------------------------------
     def _native_fanout_enabled(self) -> bool:
+        if self.scatter is not None:
+            return False
         return (self.cuda and self.mode in ("alltoall", "scatter") and self.native_fanout and self.native_launch
                 and self.ex.use_graphs and not getattr(self.ex.model, "has_collectives", False))
 
@@ -408,6 +455,10 @@ class FanoutEngine:
                 err = f"max |diff| {diff:.3g}"
         except Exception as e:  # surfaced through the agreement below
             ok, err = False, repr(e)
+        if not ok:
+            import sys
+
+            print(f"[fanout] rank {self.rank}: self-check of bucket {B} failed: {err}", file=sys.stderr, flush=True)
         if self.ctx.is_distributed:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
                                 device=self.dev if self.ctx.backend == "nccl" else "cpu")
@@ -500,7 +551,8 @@ class FanoutEngine:
 
     # -- whole-step graphs (no fan-out) ------------------------------------------
     def _step_graphs_enabled(self) -> bool:
-        return self.cuda and self.mode == "local" and self.ex.use_graphs and self.step_graphs
+        return (self.cuda and (self.mode == "local" or self.scatter is not None) and self.ex.use_graphs
+                and self.step_graphs)
 
     def _capture_step(self, B: int, slot: int) -> None:
         """Capture forward -> D2H of one (bucket, slot) as ONE HIP graph.
@@ -515,7 +567,7 @@ class FanoutEngine:
         if key in self._step_graph:
             return
         cur = torch.cuda.current_stream(self.dev)
-        h_out = self.host_out(B, slot)
+        out = self.step_out(B, slot)
         buf = self.ex.input_buffer(B, slot)
         arena_dev = self.dev_arena(slot) if self.ingest == "arena" else None
 
@@ -526,11 +578,11 @@ class FanoutEngine:
             # (no D2H copy node, which a graph would run as a blit kernel)
             if fused_ingest:  # K0 fused into K1: the gather reads the request bytes
                 self.arena.decode_varints(arena_dev)
-                self.ex.model.forward_arena(arena_dev, B, out=h_out[:B])
+                self.ex.model.forward_arena(arena_dev, B, out=out)
                 return
             if arena_dev is not None:  # K0 on the GPU: request bytes -> packed rows
                 self._unpack(arena_dev, buf)
-            self.ex._forward(buf, out=h_out[:B])
+            self.ex._forward(buf, out=out)
 
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(cur)
@@ -596,6 +648,8 @@ class FanoutEngine:
         rows = self.contrib_rows(B)
         t0 = time.perf_counter()
         exec_in = self.ex.input_buffer(B, slot)
+        if not self.cuda and self.scatter is not None:
+            return self._launch_shared_scatter_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
         if not self.cuda:
             if arena_mode:  # host reference of the GPU unpack
                 packed = self.host_in(B, slot)
@@ -612,6 +666,8 @@ class FanoutEngine:
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
         if self.program_active:
             return self._launch_program(B, slot, h_in, h_out, rows, t0, nbytes)
+        if self.scatter is not None:
+            return self._launch_shared_scatter(B, slot, h_in, h_out, rows, t0)
         if self._step_graphs_enabled():
             return self._launch_step_graph(B, slot, h_in, h_out, rows, t0, nbytes)
         if self.native_fanout_active:
@@ -674,6 +730,48 @@ class FanoutEngine:
             done.record(self.d2h_stream)
         self._ev_out_free[slot] = done
         return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=done, t_submit=t0, timeout_s=self.step_timeout_s)
+
+    # -- shared-arena scatter ----------------------------------------------------
+    def _launch_shared_scatter(self, B: int, slot: int, h_in, h_out, rows: int, t0: float) -> StepHandle:
+        """One step on this rank's share of rank 0's shared batch (GPU): the
+        native StepRunner copies the share and launches the captured local
+        step (csrc/bindings_hip.cpp scatter_step)."""
+        self._capture_step(B, slot)
+        g = self._step_graph[(B, slot)]
+        k = self.scatter.launch(self.runner(), slot, B, h_in if self.rank == 0 else None, self.dev_arena(slot), None,
+                                g.raw_cuda_graph_exec(), self.step_timeout_s or 30.0)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_ScatterEvent(self, slot, k), t_submit=t0,
+                          timeout_s=self.step_timeout_s)
+
+    def _launch_shared_scatter_cpu(self, B, slot, h_in, h_out, rows, exec_in, t0) -> StepHandle:
+        """Host reference of the shared-arena scatter step (CPU ranks, gloo
+        tests): the same plan and share copies (memcpy instead of DMA) into a
+        private arena, the local forward, scores into rank 0's shared output."""
+        seg = self.scatter
+        timeout = self.step_timeout_s or 30.0
+        k = seg.begin_step()
+        if self.rank == 0:
+            ai = seg.arena_index(h_in)
+            if ai < 0:
+                raise RuntimeError("shared scatter: rank 0's batch is not in a shared arena")
+            seg.publish_plan(k, ai, B)
+        local = self._local_arena.get(slot)
+        if local is None:
+            local = self._local_arena[slot] = self.arena.alloc()
+        row0, n, _ = seg.take_share(k, local, timeout)
+        packed = self.layout.alloc(B)
+        self.arena.unpack_cpu(local, packed)
+        exec_in[:B].copy_(packed[:B])
+        scores = self.ex.run(B, slot).contiguous()
+        if n:  # the rank's fixed slice, as the GPU step's captured head writes it
+            self.step_out(B, slot)[:n].copy_(scores[:n])
+        seg.mark_done(k)
+        if self.rank == 0:
+            ok, err = seg.wait_done(k, timeout)
+            if not ok:
+                raise StepTimeout(f"shared scatter step failed: {err}")
+            seg.compact_scores(k, slot)
+        return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=None, t_submit=t0)
 
     def _launch_cpu(self, B, slot, h_in, h_out, rows, exec_in, t0) -> StepHandle:
         if self.mode == "alltoall":

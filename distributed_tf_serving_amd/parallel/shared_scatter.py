@@ -1,0 +1,69 @@
+"""Bootstrap of the shared-arena scatter (csrc/runtime/shared_scatter.h).
+
+Scatter mode is the reference topology: rank 0 is the only front door and
+every request's candidates are split over the shards (reference
+DCNClient.java:46-74 split, :146-164 dispatch + join). Over RCCL that means
+rank 0's single PCIe link carries every rank's request bytes, then xGMI carries
+them again. With the shared arena, rank 0's request arenas and score outputs
+are one POSIX shared-memory segment that every rank of the node maps and
+registers with its own GPU: per step each rank DMAs only its share of the
+batch over its own link and writes its scores straight into rank 0's output
+(no collective in the step). Same bootstrap as the step control
+(parallel/control.py): rank 0 creates the segment under a random name,
+publishes the name in the job's store, waits for every rank to attach and
+unlinks the name.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import secrets
+import time
+
+from .control import default_store
+
+
+def create_shared_scatter(module, world: int, rank: int, fields: int, n_arenas: int, arena_cap: int, slots: int,
+                          out_floats: int, store=None, prefix: str = "dtfs/scatter/0", node: int = -1,
+                          register: bool = False, timeout_s: float = 60.0):
+    """A SharedScatter of ``module`` (``_hip`` for GPU ranks, which also
+    register the mapping with their device, ``_native`` for CPU ranks).
+    Not a collective: every rank calls it with the same ``prefix``."""
+    store = store if store is not None else default_store()
+    name_key, att_key = f"{prefix}/name", f"{prefix}/attached"
+    if rank == 0:
+        name = f"/dtfs-sct-{os.getpid()}-{secrets.token_hex(6)}"
+        seg = module.SharedScatter(name, world, 0, True, fields, n_arenas, arena_cap, slots, out_floats, node)
+        store.set(name_key, name)
+    else:
+        store.wait([name_key], datetime.timedelta(seconds=timeout_s))
+        name = store.get(name_key).decode()
+        seg = module.SharedScatter(name, world, rank, False)
+    if register:
+        seg.register_with_gpu()
+    store.add(att_key, 1)
+    if rank == 0:
+        deadline = time.monotonic() + timeout_s
+        try:
+            while store.add(att_key, 0) < world:
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"shared scatter {name}: only {store.add(att_key, 0)} of {world} ranks attached")
+                time.sleep(0.002)
+        finally:
+            seg.unlink()
+    return seg
+
+
+def scatter_for_engine(ctx, fields: int, arena_cap: int, slots: int, max_rows_per_rank: int, tag: str = "serve",
+                       store=None, n_arenas: int = 0):
+    """The segment of a scatter-mode job on one node (None for one rank).
+    ``n_arenas`` defaults to what the live server allocates (slots + 3)."""
+    if ctx.world <= 1:
+        return None
+    from ..ops import hip, native
+    from ..utils.affinity import current_node
+
+    cuda = ctx.device.type == "cuda"
+    return create_shared_scatter(hip() if cuda else native(), ctx.world, ctx.rank, fields, n_arenas or slots + 3,
+                                 arena_cap, slots, ctx.world * max_rows_per_rank, store=store,
+                                 prefix=f"dtfs/scatter/{tag}", node=current_node() if cuda else -1, register=cuda)

@@ -127,7 +127,8 @@ class ClusterServer:
             # the step's gloo collectives run on the live server's launcher
             # thread: their own group, never interleaved with other traffic
             group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=self.cfg.serving.step_timeout_s))
-        eng = build_engine(self.cfg, ctx.device, self.slots, ctx=ctx, mode=mode, group=group, model=model)
+        eng = build_engine(self.cfg, ctx.device, self.slots, ctx=ctx, mode=mode, group=group, model=model,
+                           scatter_tag=f"cluster/{self.epoch}", store=store)
         eng.step_timeout_s = self.cfg.serving.step_timeout_s
         if self.self_check_on and mode != "local":
             B = eng.ex.buckets[-1]
@@ -251,6 +252,15 @@ class ClusterServer:
         self.epoch, self.members = epoch, list(members)
         self._injected_comm_error = None
         self._build(ctx, first=False, store=self._store, model=old_eng.ex.model)
+        args = getattr(self, "_native_front_args", None)
+        if args is not None and self.serves and self.front is not None:
+            # the native front door is bound to one live server: re-open it
+            # over the new one (clients see a short UNAVAILABLE window)
+            old_front = self.front
+            old_front.stop()
+            from .native_front import NativeGrpcFront
+
+            self.front = NativeGrpcFront(self.service, self.sched, port=args[0], host=args[1], threads=args[2]).start()
         self.recoveries += 1
         log.warning("rank %d serving again as rank %d of %d (epoch %d)", self.orig_rank, rank, world, epoch)
 
@@ -268,6 +278,17 @@ class ClusterServer:
         if monitoring_port is not None:
             self.metrics.serve_http(monitoring_port, host)
         return self.front.port
+
+    def start_native_grpc(self, port: int = 9999, host: str = "0.0.0.0", threads: int = 4) -> int:
+        """The C++ h2c front door (serving/native_front.py) over this rank's
+        live server; a rebuilt cluster re-opens it over the new one."""
+        from .native_front import NativeGrpcFront
+
+        assert self.serves, "this rank is not a front door"
+        with self._lock:
+            self._native_front_args = (port, host, threads)
+            self.front = NativeGrpcFront(self.service, self.sched, port=port, host=host, threads=threads).start()
+            return self.front.port
 
     # -- followers ----------------------------------------------------------------------
     def serve_follower(self) -> int:
@@ -321,6 +342,9 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=9999)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--grpc-workers", type=int, default=32)
+    ap.add_argument("--front", default="native", choices=["native", "grpcio"],
+                    help="native: C++ h2c front door, Predict straight into the live server; grpcio: Python gRPC")
+    ap.add_argument("--front-threads", type=int, default=4, help="native front door: event-loop threads")
     ap.add_argument("--monitoring-port", type=int, default=None,
                     help="serve Prometheus metrics over HTTP on this port (rank 0)")
     ap.add_argument("--control-timeout-s", type=float, default=5.0,
@@ -346,12 +370,32 @@ def main(argv=None):
         if not a.no_gc_freeze:  # every rank, after warm-up, before traffic
             tune_for_serving()
         if srv.serves:
-            port = srv.start_grpc(a.port + (srv.rank if a.mode == "alltoall" else 0), a.host, a.grpc_workers,
-                                  a.monitoring_port if srv.rank == 0 else None)
-            print(f"rank {srv.rank}: serving on port {port} over {ctx.world} GPU(s) ({a.mode})", flush=True)
-            signal.signal(signal.SIGTERM, lambda *_: srv.front.stop() if srv.front else None)
+            p = a.port + (srv.rank if a.mode == "alltoall" else 0)
+            if a.front == "native":
+                port = srv.start_native_grpc(p, a.host, a.front_threads)
+                if a.monitoring_port is not None and srv.rank == 0:
+                    from .monitoring import ServingMetrics
+
+                    srv.metrics = ServingMetrics(srv.registry)
+                    srv.metrics.serve_http(a.monitoring_port, a.host)
+            else:
+                port = srv.start_grpc(p, a.host, a.grpc_workers, a.monitoring_port if srv.rank == 0 else None)
+            print(f"rank {srv.rank}: serving on port {port} over {ctx.world} GPU(s) ({a.mode}, {a.front} front door)",
+                  flush=True)
+            stop = threading.Event()
+
+            def on_term(*_):
+                stop.set()
+                if srv.front:
+                    srv.front.stop()
+
+            signal.signal(signal.SIGTERM, on_term)
             try:
-                srv.front.wait()
+                while True:  # a rebuilt cluster swaps in a new native front door
+                    f = srv.front
+                    f.wait()
+                    if stop.is_set() or srv.front is f:
+                        break
             except KeyboardInterrupt:
                 pass
         else:

@@ -83,12 +83,20 @@ class LiveScheduler:
         # DLRM: the dense features) get only those copied (fewer H2D bytes)
         wc = int(getattr(model, "narrow_weight_cols", lambda: 0)()) if self.narrow_modulo else 0
         self.narrow_wts_cols = wc if 0 < wc < self.fields else 0
-        if engine.cuda:  # pinned, on this rank's NUMA node when it has one (utils/affinity.py)
+        seg = engine.scatter
+        n_ar = int(n_arenas or depth + 3)
+        if seg is not None and engine.rank == 0:
+            # shared-arena scatter: rank 0 batches straight into the segment
+            # every rank reads its share from (parallel/shared_scatter.py)
+            if seg.n_arenas < max(n_ar, depth + 2):
+                raise ValueError(f"shared scatter segment has {seg.n_arenas} arenas, the live server needs {n_ar}")
+            self.arenas = [seg.arena(i) for i in range(n_ar)]
+        elif engine.cuda:  # pinned, on this rank's NUMA node when it has one (utils/affinity.py)
             from ..utils.affinity import alloc_pinned_arena
 
-            self.arenas = [alloc_pinned_arena(self.layout.capacity) for _ in range(int(n_arenas or depth + 3))]
+            self.arenas = [alloc_pinned_arena(self.layout.capacity) for _ in range(n_ar)]
         else:
-            self.arenas = [self.layout.alloc() for _ in range(int(n_arenas or depth + 3))]
+            self.arenas = [self.layout.alloc() for _ in range(n_ar)]
         self.config = dict(
             fields=self.fields, ids_key=sc.ids_key, wts_key=sc.wts_key, model_name=self.model_name,
             signature_name=sc.signature_name, output_key=sc.output_key, version=self.version,
@@ -103,7 +111,8 @@ class LiveScheduler:
             from ..ops import hip
 
             spec = [(R, engine.loop_slots(B)) for B, R in zip(self.buckets, self.step_rows)]
-            self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas, control)
+            self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas, control, seg,
+                                        self.buckets if seg is not None else None)
         else:
             slots = self.ex.slots
             scores = [[engine.host_out(B, s) for B in self.buckets] for s in range(slots)]
@@ -191,6 +200,10 @@ class LiveScheduler:
 
     def stats(self) -> dict:
         st = dict(self.srv.stats())
+        seg = self.eng.scatter
+        if seg is not None:  # shared-arena scatter: what this rank copied for its shares
+            st["scatter_h2d_bytes"] = int(seg.h2d_bytes)
+            st["scatter_h2d_steps"] = int(seg.h2d_steps)
         # the names the monitoring endpoint reads (serving/monitoring.py)
         st.setdefault("batches", st["steps"])
         st.setdefault("batched_rows", st["rows"])

@@ -50,7 +50,8 @@ def live_enabled(cfg: Config, device: torch.device) -> bool:
 
 
 def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistContext] = None,
-                 mode: str = "local", group=None, model=None) -> FanoutEngine:
+                 mode: str = "local", group=None, model=None, scatter_tag: str = "serve",
+                 store=None) -> FanoutEngine:
     """Model + executor + fan-out engine of one rank, every bucket prepared
     (HIP graphs captured). With ``ctx`` of a multi-rank job, DLRM tables are
     sharded over the ranks (parallel/embedding_sharding.py) and ``mode``
@@ -58,7 +59,9 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
     live server ingests request arenas (the GPU unpacks raw request bytes).
     ``group``: process group of the step's collectives (CPU: a dedicated gloo
     group, since they run on the live server's launcher thread). ``model``:
-    reuse a built replica (a cluster rebuilt over fewer ranks keeps its weights)."""
+    reuse a built replica (a cluster rebuilt over fewer ranks keeps its weights).
+    ``scatter_tag``: store prefix of the shared-scatter segment (unique per
+    segment: a rebuilt cluster makes a new one)."""
     from ..parallel.embedding_sharding import build_parallel_model
 
     sc = cfg.serving
@@ -72,14 +75,23 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
         buckets = [b for b in buckets if b % world == 0] or [sc.max_batch_rows * world]
     use_graphs = sc.use_graphs
     live = live_enabled(cfg, dev)
+    # scatter on one node through rank 0's shared arenas: the step is local
+    shared = live and mode == "scatter" and world > 1 and getattr(sc, "scatter_path", "shared") == "shared"
     # rows exchanged between GPUs travel narrow (int32 rows + bf16 weights)
-    fanout = live and mode != "local" and world > 1
+    fanout = live and mode != "local" and world > 1 and not shared
     layout = layout_for(cfg.model, fanout) if fanout else PackedLayout(cfg.model.num_fields)
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=use_graphs, slots=slots)
     if live:
         rows_in = max(buckets) * (world if mode == "scatter" else 1)
-        eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", group=group,
-                           arena=ArenaLayout(cfg.model.num_fields, max_rows=rows_in))
+        # shared scatter: shares are cut from the row table, so ids are decoded on the host
+        arena = ArenaLayout(cfg.model.num_fields, max_rows=rows_in, gpu_varint=not shared)
+        seg = None
+        if shared:
+            from ..parallel.shared_scatter import scatter_for_engine
+
+            seg = scatter_for_engine(ctx, cfg.model.num_fields, arena.capacity, slots, max(buckets),
+                                     tag=scatter_tag, store=store)
+        eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", group=group, arena=arena, shared_scatter=seg)
     else:
         eng = FanoutEngine(ex, ctx, mode=mode, group=group)
     for B in buckets:
@@ -128,6 +140,18 @@ class ModelServer:
                                    metrics=self.metrics).start()
         return self.front.port
 
+    def start_native_grpc(self, port: int = 9999, host: str = "0.0.0.0", threads: int = 4) -> int:
+        """The C++ h2c front door (serving/native_front.py): Predict goes from
+        the event loop straight into the servable's native live server."""
+        from .live import LiveScheduler
+        from .native_front import NativeGrpcFront
+
+        sched = self.registry.resolve(self.cfg.serving.model_name).scheduler
+        if not isinstance(sched, LiveScheduler):
+            raise ValueError("the native front door needs a live-server servable (serving.live)")
+        self.front = NativeGrpcFront(self.service, sched, port=port, host=host, threads=threads).start()
+        return self.front.port
+
     def start_monitoring(self, port: int, host: str = "0.0.0.0") -> int:
         """Prometheus text format over HTTP (TF-Serving's monitoring endpoint)."""
         return self.metrics.serve_http(port, host)
@@ -165,6 +189,11 @@ def main(argv=None):
                          "live server on the same GPU: scales the grpcio front door past one GIL "
                          "(profiles/grpc_ceiling.md)")
     ap.add_argument("--frontend-index", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--front", default="auto", choices=["auto", "native", "grpcio"],
+                    help="native: C++ h2c front door, Predict straight into the live server (csrc/net); grpcio: "
+                         "the Python gRPC server; auto: native when the servable runs on the live server and no "
+                         "fault is injected")
+    ap.add_argument("--front-threads", type=int, default=4, help="native front door: event-loop threads")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     children = []
@@ -192,11 +221,18 @@ def main(argv=None):
         srv.service = FaultyService(srv.service, FaultInjector(FaultSpec.parse(a.inject_fault)))
     if not a.no_gc_freeze:  # after warm-up (graphs captured), before the port takes traffic
         logging.getLogger(__name__).info("gc: %s", tune_for_serving())
-    port = srv.start_grpc(a.port, a.host, a.grpc_workers)
+    from .live import LiveScheduler
+
+    live = isinstance(srv.registry.resolve(cfg.serving.model_name).scheduler, LiveScheduler)
+    front = a.front if a.front != "auto" else ("native" if live and not a.inject_fault else "grpcio")
+    if front == "native":
+        port = srv.start_native_grpc(a.port, a.host, a.front_threads)
+    else:
+        port = srv.start_grpc(a.port, a.host, a.grpc_workers)
     if a.monitoring_port is not None:
         srv.start_monitoring(a.monitoring_port, a.host)
     if a.frontend_index == 0:
-        print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port}"
+        print(f"serving model {cfg.serving.model_name!r} ({cfg.model.family}) on port {port} ({front} front door)"
               + (f" ({a.frontends} frontend processes)" if a.frontends > 1 else ""), flush=True)
     signal.signal(signal.SIGTERM, lambda *_: srv.stop())
     try:

@@ -26,6 +26,22 @@ for m in ${MODELS:-}; do
     > gpurun_out/bench_$m.log 2>&1 || { echo "bench $m failed"; tail -40 gpurun_out/bench_$m.log; exit 1; }
   grep '^{"metric' gpurun_out/bench_$m.log | cut -c1-1500
 done
+if [ -n "${BENCHES:-}" ]; then
+  # ';'-separated bench.py argument sets, e.g. BENCHES="--model dlrm;--model dlrm --shard-tables"
+  IFS=';' read -ra SETS <<< "$BENCHES"
+  i=0
+  for args in "${SETS[@]}"; do
+    i=$((i+1))
+    # leading VAR=value words are environment settings for this set (e.g. "DTFS_RESOLVE_LANE=1 --model deepfm")
+    envs=(); rest=()
+    for w in $args; do
+      if [ ${#rest[@]} -eq 0 ] && [[ $w =~ ^[A-Z_][A-Z0-9_]*= ]]; then envs+=("$w"); else rest+=("$w"); fi
+    done
+    timeout -k 10 500 env "${envs[@]}" python -u bench.py "${rest[@]}" --steps ${STEPS:-200} --warmup 20 > gpurun_out/bench_set$i.log 2>&1 \
+      || { echo "bench [$args] failed"; tail -40 gpurun_out/bench_set$i.log; exit 1; }
+    echo "[$args]"; grep '^{"metric' gpurun_out/bench_set$i.log | cut -c1-2500
+  done
+fi
 if [ "${REF:-0}" = "1" ]; then
   # the reference workload in process, then over TCP from a separate process of native h2c clients
   timeout -k 10 300 python -u bench.py --reference-workload > gpurun_out/bench_ref.log 2>&1 \

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall"])
     ap.add_argument("--out", required=True)
     ap.add_argument("--grpc-port", type=int, default=0, help="> 0: also serve gRPC on port + rank and query it")
+    ap.add_argument("--front", default="native", choices=["native", "grpcio"],
+                    help="front door of the gRPC check: the C++ h2c server or grpcio")
     ap.add_argument("--requests", type=int, default=24)
     ap.add_argument("--kill-rank", type=int, default=-1, help="this rank exits abruptly after --kill-after steps")
     ap.add_argument("--kill-after", type=int, default=3)
@@ -146,7 +148,9 @@ def main():
 
             # alltoall: every rank is a front door; an ephemeral port each (port + rank
             # could collide with the rendezvous / RCCL sockets)
-            port = srv.start_grpc(0 if a.mode == "alltoall" else a.grpc_port, host="127.0.0.1")
+            p = 0 if a.mode == "alltoall" else a.grpc_port
+            port = (srv.start_native_grpc(p, host="127.0.0.1") if a.front == "native"
+                    else srv.start_grpc(p, host="127.0.0.1"))
             be = GrpcBackend(f"127.0.0.1:{port}")
             gd = []
             for data, ids, wts in reqs[:4]:

@@ -62,6 +62,14 @@ def test_bench_json_contract(n):
 def test_bench_scatter_mode_world2():
     out = _run_bench(2, ("--mode", "scatter"))
     assert "scatter" in out["config"]["parallelism"] and out["config"]["global_batch"] == 128
+    # shared-arena scatter: each rank copied its own share of rank 0's batches
+    per = out["scatter"]["h2d_bytes_per_step_by_rank"]
+    assert len(per) == 2 and all(b > 64 for b in per), per
+
+
+def test_bench_scatter_mode_rccl_path_world2():
+    out = _run_bench(2, ("--mode", "scatter", "--scatter-path", "rccl"))
+    assert "scatter" in out["config"]["parallelism"] and "scatter" not in out
 
 
 @pytest.mark.slow

@@ -33,7 +33,7 @@ def _cfg():
     return cfg
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, scatter_path="shared"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -46,7 +46,10 @@ def _worker(rank, world, port, q):
     try:
         ctx = init_from_env(device="cpu")
         cfg = _cfg()
+        cfg.serving.scatter_path = scatter_path
         srv = ClusterServer(cfg, ctx)
+        seg = srv.engine.scatter
+        assert (seg is not None) == (scatter_path == "shared")
         if rank == 0:
             ref = build_model(cfg.model)
             rng = np.random.default_rng(3)
@@ -65,11 +68,11 @@ def _worker(rank, world, port, q):
                 errs.append(float(np.abs(got - want).max()))
             stats = srv.registry.resolve(cfg.serving.model_name).scheduler.stats()
             srv.stop()
-            q.put((rank, errs, stats["steps"]))
+            q.put((rank, errs, (stats["steps"], stats.get("scatter_h2d_bytes", 0))))
         else:
             n = srv.serve_follower()
             srv.stop()
-            q.put((rank, None, n))
+            q.put((rank, None, (n, seg.h2d_bytes if seg is not None else 0)))
         shutdown()
     except Exception:  # pragma: no cover - surfaced by the assertion below
         import traceback
@@ -77,23 +80,34 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc(), -1))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_cluster_server_scatter_gather(world):
+@pytest.mark.parametrize("world,path", [(2, "shared"), (3, "shared"), (2, "rccl")])
+def test_cluster_server_scatter_gather(world, path):
+    """Scores = a local forward at every request size; every rank runs every
+    step. Shared-arena scatter (csrc/runtime/shared_scatter.h): each rank
+    copies only its own share of rank 0's batches (no rank copies the whole
+    batch); "rccl": the collective scatter fallback (gloo here)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, path)) for r in range(world)]
     [p.start() for p in procs]
     res = {}
     for _ in range(world):
         r, payload, steps = q.get(timeout=300)
         res[r] = (payload, steps)
     [p.join(timeout=60) for p in procs]
-    errs, steps0 = res[0]
+    errs, (steps0, _) = res[0]
     assert isinstance(errs, list), f"rank 0 failed: {errs}"
     assert max(errs) < 1e-5, errs
     for r in range(1, world):
-        assert res[r][1] == steps0, f"rank {r} followed {res[r][1]} steps, rank 0 ran {steps0}: {res[r][0]}"
+        assert res[r][1][0] == steps0, f"rank {r} followed {res[r][1]} steps, rank 0 ran {steps0}: {res[r][0]}"
+    if path == "shared":
+        h2d = [res[r][1][1] for r in range(world)]
+        total = sum(h2d)
+        assert all(b > 0 for b in h2d), h2d
+        # rank 0 copied its own share only: about 1/world of the request bytes
+        # (plus 64-byte headers of steps where its share is empty)
+        assert h2d[0] < total * (1.0 / world + 0.25), h2d
 
 
 def _fault_worker(rank, world, port, q, die_rank, die_after):
@@ -189,16 +203,18 @@ def _run_worker(n, mode, out, extra=(), env_extra=None, timeout=240):
     return subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("world,mode", [(2, "alltoall"), (3, "scatter"), (3, "alltoall")])
-def test_native_cluster_serves_exact_scores_and_idles(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,front", [(2, "alltoall", "native"), (3, "scatter", "native"),
+                                              (3, "alltoall", "grpcio")])
+def test_native_cluster_serves_exact_scores_and_idles(tmp_path, world, mode, front):
     """The ClusterServer on the native live server in both fan-out modes: every
     front door's concurrent requests (raw and packed encodings, sizes that do
     not divide by the world) score exactly like a local forward, over the
-    in-process service and the gRPC front door; an idle cluster launches no
+    in-process service and the gRPC front door (the C++ h2c server or
+    grpcio); an idle cluster launches no
     step (the step control proposes steps only for queued work)."""
     import json
 
-    p = _run_worker(world, mode, tmp_path, ("--grpc-port", str(_free_port())))
+    p = _run_worker(world, mode, tmp_path, ("--grpc-port", str(_free_port()), "--front", front))
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     fronts = [r for r in res if r["serves"]]

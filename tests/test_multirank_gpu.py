@@ -22,18 +22,22 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,mode,peer", [(2, "alltoall", 0), (3, "alltoall", 0), (2, "scatter", 0), (2, "local", 0),
-                                         (3, "alltoall", 262144), (2, "scatter", 262144)])
-def test_bench_ranks_sharing_one_gpu(n, mode, peer):
+@pytest.mark.parametrize("n,mode,peer,scatter_path", [
+    (2, "alltoall", 0, "shared"), (3, "alltoall", 0, "shared"), (2, "scatter", 0, "shared"),
+    (3, "scatter", 0, "shared"), (2, "scatter", 0, "rccl"), (2, "local", 0, "shared"),
+    (3, "alltoall", 262144, "shared"), (2, "scatter", 262144, "rccl")])
+def test_bench_ranks_sharing_one_gpu(n, mode, peer, scatter_path):
     """peer > 0: the fan-out's exchanges of at most that many bytes per peer go
-    through the one-shot peer kernel (csrc/kernels/peer.hip) instead of RCCL."""
+    through the one-shot peer kernel (csrc/kernels/peer.hip) instead of RCCL.
+    Scatter runs both paths: rank 0's shared request arenas (each rank DMAs
+    its share, runtime/shared_scatter.h) and the RCCL scatter fallback."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
            "--steps", "20", "--warmup", "4", "--prime-steps", "10", "--requests-per-gpu", "4", "--request-rows", "96", "--mode", mode,
            "--pool", "8", "--client-threads", "2", "--qps", "500", "--qps-seconds", "0.4", "--small-buckets", "96",
-           "--step-timeout-s", "20"]
+           "--step-timeout-s", "20", "--scatter-path", scatter_path]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
                DTFS_PEER_COMM=str(peer))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
@@ -48,7 +52,13 @@ def test_bench_ranks_sharing_one_gpu(n, mode, peer):
     if mode != "local":
         assert out["server"]["idle_steps_per_s"] == 0, out["server"]
         assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
+    if mode == "alltoall" or (mode == "scatter" and scatter_path == "rccl"):
         assert ("one-shot peer exchange" in out["config"]["parallelism"]) == (peer > 0), out["config"]["parallelism"]
+    if mode == "scatter" and scatter_path == "shared":
+        # every rank DMA'd only its share of rank 0's batch: 96-row requests, 4
+        # per GPU -> each rank copies about the same bytes per step
+        per = out["scatter"]["h2d_bytes_per_step_by_rank"]
+        assert len(per) == n and min(per) > 0.5 * max(per), per
 
 
 @pytest.mark.parametrize("n,peer", [(2, 0), (3, 0), (3, 1 << 20)])

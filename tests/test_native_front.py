@@ -37,10 +37,10 @@ def _cfg():
 @pytest.fixture(scope="module")
 def front():
     srv = ModelServer(_cfg(), device="cpu")
-    live = srv.registry.resolve("DCN").scheduler
-    fr = NativeGrpcFront(srv.service, live, port=0, host="127.0.0.1", threads=2).start()
+    srv.start_native_grpc(0, "127.0.0.1", threads=2)  # the server CLI's default front door
+    fr = srv.front
+    assert isinstance(fr, NativeGrpcFront)
     yield srv, fr
-    fr.stop()
     srv.stop()
 
 

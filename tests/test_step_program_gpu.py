@@ -125,3 +125,69 @@ def test_dlrm_multi_hot_gpu_matches_cpu(cuda):
     got = gm(ids.to(cuda), wts.to(cuda)).float().cpu()
     want = cm(ids, wts).float()
     assert (got - want).abs().max().item() < 2e-2
+
+
+def test_gather_gemm_resolved_on_another_stream_is_identical(cuda):
+    """embed_gemm_resolve + embed_gemm(resolved=...) (the resolve pass moved to
+    the step program's aux lane) gives bit-identical results to the one-call
+    gather-GEMM."""
+    g = torch.Generator().manual_seed(5)
+    B, F, V, N = 16384, 43, 100_003, 1024
+    table = ((torch.rand(V, 64, generator=g) - 0.5) * 0.2).to(torch.bfloat16).to(cuda)
+    lin = ((torch.rand(V, generator=g) - 0.5) * 0.02).to(cuda)
+    W = ((torch.rand(N, F * 64, generator=g) - 0.5) * 0.05).to(torch.bfloat16).to(cuda)
+    b = ((torch.rand(N, generator=g) - 0.5) * 0.1).to(cuda)
+    ids = torch.randint(0, 1 << 40, (B, F), generator=g).to(cuda)
+    wts = torch.rand(B, F, generator=g).to(cuda)
+    h0, p0 = ops.embed_gemm(table, ids, wts, lin, V, 0.25, W, b, "relu", fm2=True)
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        r = ops.embed_gemm_resolve(table, ids, wts, lin, V, 0.25, True)
+    torch.cuda.current_stream(cuda).wait_stream(side)
+    h1, p1 = ops.embed_gemm(table, ids, wts, lin, V, 0.25, W, b, "relu", fm2=True, resolved=r)
+    torch.cuda.synchronize()
+    assert torch.equal(h0, h1) and torch.equal(p0[:, :B], p1[:, :B])
+
+
+def test_resolve_lane_program_engine_and_live_server(cuda, monkeypatch):
+    """DTFS_RESOLVE_LANE=1: a local DeepFM step at the gather-GEMM bucket runs
+    as a two-lane program (resolve on the aux lane after the H2D, the compute
+    lane waits only for it); self-check and served requests match the model."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.live import LiveScheduler
+    from distributed_tf_serving_amd.wire import schema as pb
+    from distributed_tf_serving_amd.wire import tensor as T
+
+    monkeypatch.setenv("DTFS_RESOLVE_LANE", "1")
+    cfg = ModelConfig(family="deepfm", vocab_size=100_003, embed_dim=64, mlp_dims=(1024, 512, 256))
+    m = build_model(cfg, cuda)
+    F, S = cfg.num_fields, 3
+    buckets = [2048, 16384]
+    ex = ShardExecutor(m, PackedLayout(F), buckets, cuda, slots=S)
+    eng = FanoutEngine(ex, DistContext(device=cuda), mode="local", ingest="arena", arena=ArenaLayout(F, max_rows=16384))
+    for B in buckets:
+        eng.prepare(B)
+    assert eng.program_active and eng._cprog is None
+    kinds = [o["kind"] for o in eng._programs[(16384, 0)].spec["ops"]]
+    assert kinds == ["kernels", "kernels", "record", "wait", "kernels"], kinds  # varints, resolve | forward
+    for B in buckets:
+        assert eng.self_check(B, seed=3)
+    sc = ServingConfig(max_batch_rows=16384, allowed_batch_sizes=tuple(buckets), batch_timeout_us=100)
+    live = LiveScheduler(eng, sc, buckets=buckets, depth=S)
+    try:
+        synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=19)
+        reqs = [synth.serialized(512, raw=True) for _ in range(40)]  # > 16384 rows: full gather-GEMM steps
+        import concurrent.futures as cf
+
+        with cf.ThreadPoolExecutor(8) as pool:
+            outs = list(pool.map(lambda q: live.predict_bytes(q, 30.0), reqs))
+        for req, out in zip(reqs, outs):
+            r = pb.PredictRequest.FromString(req)
+            ids = torch.from_numpy(T.to_ndarray(r.inputs["feat_ids"])).to(cuda)
+            wts = torch.from_numpy(T.to_ndarray(r.inputs["feat_wts"])).to(cuda)
+            want = m(ids, wts).float().cpu()
+            got = torch.from_numpy(T.to_ndarray(pb.PredictResponse.FromString(out).outputs["prediction_node"]))
+            assert (got - want).abs().max().item() < 5e-3  # 512-row forward vs rows inside a 16384-row step
+    finally:
+        live.close()
