@@ -448,8 +448,23 @@ class ShardedDLRM(nn.Module):
         bytes); scores -> ``out`` (or ``state["scores"]``)."""
         d = self.dense
         st = {} if state is None else state
-        emb_off, emb_stride = self.emb.table_map(B)
         arena = isinstance(ids, ops_k.ArenaRows)
+        fused = self._local_fused(ids)
+        if fused is not None:
+            # one rank, one-hot, table-wise: the exchange is the identity, so
+            # the interaction kernel gathers the rows from this rank's store
+            # itself, exactly like the unsharded DLRM (no route, no [B, T, 64]
+            # round trip through HBM)
+            mod, off = fused
+
+            def step():
+                dense_out = d.bottom_out(ids if arena else (wts if wts.dtype == torch.float32 else wts.float()))
+                z = ops_k.dot_interaction_gather(dense_out, self.emb.store, ids if arena else d.sparse_ids(ids), mod,
+                                                 off, d.inter_cols, id_col0=self.cfg.num_dense)
+                st["scores"] = d.top.forward_head(z, d.head_w, d.head_b, out=out)
+
+            return [sp.Sync("record", sp.AUX, 0), sp.Sync("wait", sp.COMPUTE, 0), sp.Kernels(sp.COMPUTE, step, "step")]
+        emb_off, emb_stride = self.emb.table_map(B)
         bag_w = None
         if self.hot > 1 and not arena:
             bag_w = wts if wts.dtype == torch.float32 else wts.float()
@@ -470,6 +485,21 @@ class ShardedDLRM(nn.Module):
         ops[k + 1:k + 1] = [sp.Sync("wait", sp.COMPUTE, 0), sp.Kernels(sp.COMPUTE, bottom, "bottom")]
         ops += [sp.Sync("record", sp.AUX, 1), sp.Sync("wait", sp.COMPUTE, 1), sp.Kernels(sp.COMPUTE, top, "top")]
         return ops
+
+    def _local_fused(self, ids):
+        """(modulo_f, offset_f) of every table in this rank's store when the
+        whole lookup is local and fusable into the interaction (one rank,
+        one-hot, table-wise, GPU), else None."""
+        e = self.emb
+        on_gpu = ids.arena.is_cuda if isinstance(ids, ops_k.ArenaRows) else ids.is_cuda
+        if not (on_gpu and e.world == 1 and self.hot == 1 and not e.rw and e.T):
+            return None
+        if getattr(self, "_lf", None) is None:
+            dev = e.store.device
+            offs = dict((t, o) for t, _, _, o in e.segments)
+            self._lf = (torch.tensor([t.rows for t in self.plan.tables], dtype=torch.int64, device=dev),
+                        torch.tensor([offs[t] for t in range(e.T)], dtype=torch.int64, device=dev))
+        return self._lf
 
     @torch.no_grad()
     def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor], out: Optional[torch.Tensor] = None):

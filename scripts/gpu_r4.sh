@@ -75,15 +75,17 @@ if [ -n "${COUNTERS:-}" ]; then
 fi
 if [ -n "${PROF_MODELS:-}" ]; then
   for pm in $PROF_MODELS; do
-    rm -rf gpurun_out/prof_$pm
-    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_$pm -o run --output-format rocpd \
-      -- python3 bench.py --model $pm --steps 100 --warmup 10 --qps 0 ${BENCH_ARGS:-} > gpurun_out/prof_$pm.log 2>&1 \
-      || { echo "prof $pm failed"; tail -30 gpurun_out/prof_$pm.log; exit 1; }
-    db=$(find gpurun_out/prof_$pm -name '*.db' | head -1)
+    tag=$pm${PROF_TAG:+_$PROF_TAG}
+    rm -rf gpurun_out/prof_$tag
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_$tag -o run --output-format rocpd \
+      -- python3 bench.py --model $pm --steps 100 --warmup 10 --qps 0 ${BENCH_ARGS:-} > gpurun_out/prof_$tag.log 2>&1 \
+      || { echo "prof $pm failed"; tail -30 gpurun_out/prof_$tag.log; exit 1; }
+    db=$(find gpurun_out/prof_$tag -name '*.db' | head -1)
     case $pm in deepfm|wdl|dcn) sk="gemm_gather --min-us 60";; dlrm) sk="bottom_mlp3 --min-us 14";; *) sk="embed_pipe --min-us 30";; esac
     python -m tools.prof_summary "$db" --steps ${PROF_STEPS:-110} --step-kernel $sk \
-      --title "bench.py live path ($pm ${BENCH_ARGS:-}), 1 MI355X" > gpurun_out/prof_summary_$pm.md \
-      && head -30 gpurun_out/prof_summary_$pm.md
+      --title "bench.py live path ($pm ${BENCH_ARGS:-} ${PROF_TAG:-}), 1 MI355X" > gpurun_out/prof_summary_$tag.md \
+      && head -30 gpurun_out/prof_summary_$tag.md
+    rm -f "$db"  # the summary is what travels back (the rocpd database is tens of MB)
   done
 fi
 echo "gpu_r4 done"
