@@ -637,6 +637,7 @@ def main():
                 "encoding": a.encoding,
                 "path": ("served: native live server (batching, arena copy, parse, step, encode) driven by "
                          "in-process native client threads"),
+                "two_lane_buckets": sorted(eng._program_buckets),  # steps run as a two-lane program
             },
         }
         out.update(extra)

@@ -163,6 +163,7 @@ class FanoutEngine:
         self._programs: Dict[Tuple[int, int], object] = {}
         self._prog_bufs: Dict[Tuple[int, int], dict] = {}
         self.program_active = False
+        self._program_buckets: set = set()  # buckets whose step is a two-lane program
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
@@ -259,7 +260,7 @@ class FanoutEngine:
 
     def prepare(self, B: int) -> None:
         self.check_bucket(B)
-        if self._program_enabled():
+        if self._program_enabled(B):
             if self._cprog is None and getattr(self.ex.model, "supports_program", False):
                 from .native_comm import create_comm
 
@@ -268,6 +269,7 @@ class FanoutEngine:
                 self.host_out(B, s)
                 self._capture_program(B, s)
             self.program_active = True
+            self._program_buckets.add(B)
             return
         native = self._native_fanout_enabled()
         if self.force_fanout and self.world == 1 and self.mode != "local" and not native:
@@ -288,19 +290,26 @@ class FanoutEngine:
         self.native_fanout_active = native and not self._native_disabled
 
     # -- programmed steps (embedding-parallel models) ------------------------------
-    def _program_enabled(self) -> bool:
+    def _program_enabled(self, B: int) -> bool:
         if not (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"):
             return False
         # embedding-parallel models: the exchange is the program. Local
-        # gather-GEMM steps may run as one too (DTFS_RESOLVE_LANE=1): the
-        # resolve pass of step k+1 on the aux lane right after its H2D, the
-        # compute lane waiting only for that (a cross-step overlapped GATHER
-        # slowed the fused head 12.6 -> 61 us, profiles/step_overlap.md; the
-        # resolve pass is a tenth of its bytes)
+        # gather-GEMM steps run as one too (DTFS_RESOLVE_LANE=0 turns it
+        # off): the resolve pass of step k+1 on the aux lane right after its
+        # H2D, the compute lane waiting only for that - 108.4 vs 104.5 M
+        # scores/s interleaved on one box (profiles/r04_session2.md). (A
+        # cross-step overlapped GATHER slowed the fused head 12.6 -> 61 us,
+        # profiles/step_overlap.md; the resolve pass is a tenth of its bytes.)
         m = self.ex.model
         if getattr(m, "supports_program", False):
             return True
-        return os.environ.get("DTFS_RESOLVE_LANE", "0") == "1" and bool(getattr(m, "resolve_lane", False))
+        if os.environ.get("DTFS_RESOLVE_LANE", "1") != "1" or not getattr(m, "resolve_lane", False):
+            return False
+        # only the buckets whose step runs the gather-GEMM (smaller steps keep
+        # the one-stream step: no cross-lane hop on the light-load path)
+        from ..ops import ArenaRows
+
+        return bool(m._resolve_applies(ArenaRows(self.dev_arena(0), B, self.layout.fields), None))
 
     def _capture_program(self, B: int, slot: int) -> None:
         """Build and capture the step program of one (bucket, slot): GPU unpack
@@ -512,7 +521,7 @@ class FanoutEngine:
         rows = self.contrib_rows(B)
         for s in range(self.ex.slots):
             h_out = self.host_out(B, s)
-            if self.program_active:
+            if B in self._program_buckets:
                 self._capture_program(B, s)
                 out.append(dict(program=self._programs[(B, s)].spec, h2d_dst=self.dev_arena(s), h_out=h_out))
             elif self._step_graphs_enabled():
@@ -664,7 +673,7 @@ class FanoutEngine:
                         self.arena.unpack_cpu(h_in, packed[:rows])
                 h_in = packed
             return self._launch_cpu(B, slot, h_in, h_out, rows, exec_in, t0)
-        if self.program_active:
+        if B in self._program_buckets:
             return self._launch_program(B, slot, h_in, h_out, rows, t0, nbytes)
         if self.scatter is not None:
             return self._launch_shared_scatter(B, slot, h_in, h_out, rows, t0)

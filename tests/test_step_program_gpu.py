@@ -151,9 +151,10 @@ def test_gather_gemm_resolved_on_another_stream_is_identical(cuda):
 
 
 def test_resolve_lane_program_engine_and_live_server(cuda, monkeypatch):
-    """DTFS_RESOLVE_LANE=1: a local DeepFM step at the gather-GEMM bucket runs
-    as a two-lane program (resolve on the aux lane after the H2D, the compute
-    lane waits only for it); self-check and served requests match the model."""
+    """A local DeepFM step at the gather-GEMM bucket runs as a two-lane program
+    (resolve on the aux lane after the H2D, the compute lane waits only for
+    it; the default), the small bucket as the one-stream step; self-check and
+    served requests match the model."""
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.serving.live import LiveScheduler
     from distributed_tf_serving_amd.wire import schema as pb
@@ -168,7 +169,7 @@ def test_resolve_lane_program_engine_and_live_server(cuda, monkeypatch):
     eng = FanoutEngine(ex, DistContext(device=cuda), mode="local", ingest="arena", arena=ArenaLayout(F, max_rows=16384))
     for B in buckets:
         eng.prepare(B)
-    assert eng.program_active and eng._cprog is None
+    assert eng.program_active and eng._cprog is None and eng._program_buckets == {16384}
     kinds = [o["kind"] for o in eng._programs[(16384, 0)].spec["ops"]]
     assert kinds == ["kernels", "kernels", "record", "wait", "kernels"], kinds  # varints, resolve | forward
     for B in buckets:
