@@ -771,6 +771,30 @@ __device__ unsigned long long g_8ph_stamps[4096][8][4];
   } while (0)
 #endif
 
+// Diagnostic build only (tools/native/gg_stamps.hip defines it): per-phase
+// s_memtime stamps of gemm_gather_kernel for ONE K tile in the middle of the
+// loop, kept in registers and written by lane 0 after the epilogue (a store
+// inside the loop would shift the counted vmcnt waits), plus entry / prologue /
+// loop / epilogue. Never defined in the extension build.
+#ifdef DTFS_GG_STAMPS
+__device__ unsigned long long g_gg_stamps[4096][8][16];
+#define GG_T(k)                                             \
+  do {                                                      \
+    if (t == gg_t) gg_s[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define GG_AT(k)                                   \
+  do {                                             \
+    gg_s[k] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+#else
+#define GG_T(k) \
+  do {          \
+  } while (0)
+#define GG_AT(k) \
+  do {           \
+  } while (0)
+#endif
+
 // DCN-v2 cross layer epilogue of the 256x256 8-phase tile, staged through LDS
 // (XSTAGE): the fused cross epilogue in registers (store_acc_t, EPI_CROSS)
 // loads x0 / xl as 8-byte pieces of 16 rows per fragment, one latency-bound
@@ -1247,6 +1271,12 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   constexpr int BUF = (BM + BN) * 128;  // 64 KiB
   constexpr int RING = 8;
   constexpr int XMAX = 4;  // cross weight rows per K tile (L + 1 <= 4)
+#ifdef DTFS_GG_STAMPS
+  unsigned long long gg_s[16] = {};
+  const int gg_t = F / 2;
+  gg_s[13] = __builtin_amdgcn_s_memrealtime();
+#endif
+  GG_AT(0);
   // one LDS object (A/B double buffer | ring rows | ring weights | ring cross
   // weights): separate __shared__ arrays made the compiler put vmcnt(0) in
   // front of the A-tile reads (LDS-DMA alias tracking), draining the DMA
@@ -1431,6 +1461,7 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   __syncthreads();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
   asm volatile("" ::: "memory");
+  GG_AT(1);
 
   bf16x8 fa[2][4], fb[2][2][2];
   auto read_a = [&](const uint8_t* buf, int qm) {
@@ -1488,44 +1519,54 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     uint8_t* buf = smem + (t & 1) * BUF;
     uint8_t* nbuf = smem + ((t + 1) & 1) * BUF;
     // p0: A[qm0] B[qn0]; stage Bq1(t+1), Aq1(t+1) (rows read in p3)
+    GG_T(2);
     read_a(buf, 0);
     read_b(buf, 0);
     stage_b(1, t + 1);
     stage_a(1, t + 1);
     wait_dma();
     barrier();
+    GG_T(3);
     mma(0, 0);
     barrier();
     // p1: B[qn1]; scale Aq1(t) (load here, rescale + store between the MFMAs); rows for p2's stage;
     // the ring for tile t+4
+    GG_T(4);
     read_b(buf, 1);
     scale_load(buf, 1, t);
     read_rows(0, t + 2);
     stage_ring(t + 4);
     wait_dma();
     barrier();
+    GG_T(5);
     mma(0, 1, true, buf, 1, t);
     wait_lds();
     barrier();
     // p2: A[qm1]; stage Aq0(t+2)
+    GG_T(6);
     read_a(buf, 1);
     stage_a(0, t + 2);
     wait_dma();
     barrier();
+    GG_T(7);
     mma(1, 1);
     barrier();
     // p3: scale Aq0(t+1) (as in p1); rows for p0's stage; stage Bq0(t+2)
+    GG_T(8);
     scale_load(nbuf, 0, t + 1);
     read_rows(1, t + 2);
     stage_b(0, t + 2);
     wait_dma();
     barrier();
+    GG_T(9);
     mma(1, 0, true, nbuf, 0, t + 1);
     wait_lds();
     barrier();
+    GG_T(10);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) __builtin_amdgcn_s_barrier();  // match the staggered group's barrier count
+  GG_AT(11);
 
   if (sizeof(OutT) == 2 && (epi & 15) != EPI_CROSS && ((N | int(ldc)) & 7) == 0)
     plain_staged_epilogue<false>(acc, smem, m0, n0, wr, wc, wid, lane, M, N, bias, nullptr, nullptr,
@@ -1533,6 +1574,11 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   else
     store_acc_t<false, false>(acc, m0 + 128 * wr, n0 + 64 * wc, fr, fq, M, N, bias, nullptr, nullptr, C, ldc, nullptr,
                               nullptr, 0, epi);
+#ifdef DTFS_GG_STAMPS
+  GG_AT(12);
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)
+    for (int k = 0; k < 16; ++k) g_gg_stamps[blockIdx.x][threadIdx.x >> 6][k] = gg_s[k];
+#endif
   if constexpr (EXTRA == 1) {
     if (fm_on) {
       float part = -fsq;

@@ -120,6 +120,9 @@ class CTRModel(nn.Module):
 
         st = {} if state is None else state
         if self.resolve_lane and self._resolve_applies(ids, wts):
+            # (gating step k+1's resolve on step k's tower - so it runs beside the
+            # head instead of GEMM2 - measured no better: 105.4 vs 106.1 / 104.0 M
+            # serial on one box, profiles/r04_session2.md)
             def resolve():
                 st["resolved"] = self._resolve(ids, wts)
 
@@ -169,12 +172,16 @@ class WideDeep(CTRModel):
     def _resolve(self, ids, wts):
         return ops.embed_gemm_resolve(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, False)
 
+    def _gg_front(self, ids, wts, resolved=None):
+        first = self.mlp.layers[0]
+        h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
+                                 first.bias, first.act, fm2=False, resolved=resolved)
+        return h, wide, self.head_w, self.head_b
+
     def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_gemm(ids, wts, fm2=False):
-            first = self.mlp.layers[0]
-            h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
-                                     first.bias, first.act, fm2=False, resolved=resolved)
-            return self.mlp.forward_head(h, self.head_w, self.head_b, extra=wide, out=out, start=1)
+            h, wide, hw, hb = self._gg_front(ids, wts, resolved)
+            return self.mlp.forward_head(h, hw, hb, extra=wide, out=out, start=1)
         x, wide = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=wide, out=out)
 
@@ -206,13 +213,17 @@ class DeepFM(CTRModel):
     def _resolve(self, ids, wts):
         return ops.embed_gemm_resolve(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, True)
 
+    def _gg_front(self, ids, wts, resolved=None):
+        # K1 + K2 inside the first layer's GEMM: x never reaches HBM
+        first = self.mlp.layers[0]
+        h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
+                               first.bias, first.act, fm2=True, resolved=resolved)
+        return h, fm, self.head_w, self.head_b
+
     def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_gemm(ids, wts, fm2=True):
-            # K1 + K2 inside the first layer's GEMM: x never reaches HBM
-            first = self.mlp.layers[0]
-            h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
-                                   first.bias, first.act, fm2=True, resolved=resolved)
-            return self.mlp.forward_head(h, self.head_w, self.head_b, extra=fm, out=out, start=1)
+            h, fm, hw, hb = self._gg_front(ids, wts, resolved)
+            return self.mlp.forward_head(h, hw, hb, extra=fm, out=out, start=1)
         x, fm = self._front(ids, wts)
         return self.mlp.forward_head(x, self.head_w, self.head_b, extra=fm, out=out)
 
@@ -247,15 +258,19 @@ class DCN(CTRModel):
     def _resolve(self, ids, wts):
         return ops.embed_gemm_resolve(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, True)
 
+    def _gg_front(self, ids, wts, resolved=None):
+        # gather + cross network + first MLP layer in one kernel (x0 never in HBM)
+        first = self.mlp.layers[0]
+        h, parts = ops.embed_gemm(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, first.weight, first.bias,
+                                  first.act, fm2=False,
+                                  cross=(self.cross_w, self.cross_b, self.head_wc, self._cross_consts()),
+                                  resolved=resolved)
+        return h, parts, self.head_wd, self.head_b
+
     def _forward(self, ids, wts, out=None, resolved=None):
         if self.cfg.num_cross_layers + 1 <= 4 and self._gather_gemm(ids, wts, fm2=True):
-            # gather + cross network + first MLP layer in one kernel (x0 never in HBM)
-            first = self.mlp.layers[0]
-            h, parts = ops.embed_gemm(self.emb, ids, wts, None, self.cfg.vocab_size, 0.0, first.weight, first.bias,
-                                      first.act, fm2=False,
-                                      cross=(self.cross_w, self.cross_b, self.head_wc, self._cross_consts()),
-                                      resolved=resolved)
-            return self.mlp.forward_head(h, self.head_wd, self.head_b, extra=parts, out=out, start=1)
+            h, parts, hw, hb = self._gg_front(ids, wts, resolved)
+            return self.mlp.forward_head(h, hw, hb, extra=parts, out=out, start=1)
         # the whole cross network rides on the gather (ops.embed_cross): the
         # wave holding x0 computes its L + 1 weight dot products
         on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
