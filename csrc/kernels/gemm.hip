@@ -1377,6 +1377,9 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
   float sw[2];
   auto scale_row = [&](int q, int h) { return 128 * wr + 64 * q + sp_rr + 32 * h; };
   auto scale_load = [&](const uint8_t* buf, int q, int u) {
+#ifdef DTFS_GG_NO_SCALE  // diagnostic build only: timing without the scale pass (wrong results)
+    return;
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int r = scale_row(q, h);
@@ -1385,6 +1388,9 @@ __global__ void __launch_bounds__(512) gemm_gather_kernel(const uint8_t* __restr
     }
   };
   auto scale_store = [&](uint8_t* buf, int q, int u) {
+#ifdef DTFS_GG_NO_SCALE
+    return;
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       i32x4 o;

@@ -8,12 +8,15 @@
 // from a 1M-row table (the gather's time does not depend on row locality,
 // profiles/r04_gather_locality.md).
 // Build: hipcc --offload-arch=gfx950 -O3 -I../../csrc -o gg_stamps gg_stamps.hip
+// Ablations (timing only, the results are wrong): -DDTFS_GG_NO_SCALE drops the
+// scale pass; argument "wdl" runs without the FM term (EXTRA 0).
 #define DTFS_GG_STAMPS 1
 #define DTFS_8PH_STAMPS 1
 #include "../../csrc/kernels/gemm.hip"
 
 #include <algorithm>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 static void fill_bf16(void* p, size_t n, uint32_t seed) {
@@ -31,7 +34,8 @@ static double med(std::vector<double> v) {
   return v.empty() ? 0.0 : v[v.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool wdl = argc > 1 && std::string(argv[1]) == "wdl";
   const int F = 43, N = 1024, V = 1 << 20, K = F * 64;
   void *table, *W, *C;
   float *bias, *fm, *wts;
@@ -62,8 +66,8 @@ int main() {
   for (int M : {2048, 16384}) {
     // rows_t / wts_t are field-major [F][Mp] with Mp = M here (a multiple of 256)
     auto gather = [&] {
-      return dtfs::launch_gemm_gather(table, V, rows, wts, M, F, W, bias, C, N, fm, M, N, 1, nullptr, nullptr,
-                                      nullptr, 0);
+      return dtfs::launch_gemm_gather(table, V, rows, wts, M, F, W, bias, C, N, wdl ? nullptr : fm, M, N, 1, nullptr,
+                                      nullptr, nullptr, 0);
     };
     auto dense = [&] {  // the same GEMM with x already in HBM (C's rows stand in for x; timing only)
       return dtfs::launch_gemm(table, K, W, K, bias, nullptr, nullptr, C, N, false, nullptr, nullptr, 0, M, N, K, 1,
@@ -100,9 +104,15 @@ int main() {
             tile.push_back(double(t[10] - t[2]));
             for (int k = 0; k < 8; ++k) seg[k].push_back(double(t[3 + k] - t[2 + k]));
           }
-        printf("{\"kernel\": \"gemm_gather (FM)\", \"M\": %d, \"N\": %d, \"F\": %d, \"blocks\": %d, \"event_us\": %.2f, "
+        printf("{\"kernel\": \"gemm_gather (%s%s)\", \"M\": %d, \"N\": %d, \"F\": %d, \"blocks\": %d, \"event_us\": %.2f, "
                "\"median_cycles\": {\"prologue\": %.0f, \"loop\": %.0f, \"loop_per_k_tile\": %.0f, \"epilogue\": %.0f, "
                "\"sampled_tile\": %.0f, \"phases\": [",
+               wdl ? "no FM" : "FM",
+#ifdef DTFS_GG_NO_SCALE
+               ", no scale pass",
+#else
+               "",
+#endif
                M, N, F, nb, ms * 1e3 / 20, med(pro), med(loop), med(loop) / F, med(epi), med(tile));
         for (int p = 0; p < 4; ++p)
           printf("%s{\"wait\": %.0f, \"mma\": %.0f}", p ? ", " : "", med(seg[2 * p]), med(seg[2 * p + 1]));
