@@ -146,7 +146,8 @@ def parse_args():
                     help="pipelined gather geometry for a study: resident-wave cap and rows in flight per wave "
                          "(default: the kernel's 4096,1)")
     ap.add_argument("--no-narrow", action="store_true",
-                    help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed int32 rows / bf16")
+                    help="ship raw int64 ids / fp32 weights to the GPU instead of host-narrowed 3-byte / int32 rows "
+                         "with fp32 weights")
     ap.add_argument("--json-extra", action="store_true", help="print extra diagnostics to stderr")
     ap.add_argument("--reference-workload", action="store_true",
                     help="the reference's own run instead (DCNClient.java:25-42, 57-74, 205-241): model DCN, requests "
@@ -228,7 +229,7 @@ def build(a, ctx):
     # scatter on one node: every rank DMAs its share of rank 0's shared arenas
     # (csrc/runtime/shared_scatter.h); --scatter-path rccl: the RCCL scatter
     shared = mode == "scatter" and world > 1 and a.scatter_path == "shared"
-    # fan-out rows travel narrow (int32 table rows + bf16 weights: half the xGMI bytes)
+    # fan-out rows travel narrow (int32 table rows + fp32 weights: 8 instead of 12 bytes per feature over xGMI)
     layout = (layout_for(cfg, not a.no_narrow) if mode != "local" and not shared else PackedLayout(F))
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=not a.no_graphs, slots=a.slots)
     rows_in_max = B * (world if mode == "scatter" else 1)

@@ -96,7 +96,7 @@ hipError_t launch_embed_resolve(const EmbedArgs& a, int32_t* rows_t, float* wts_
 // rows [B, W] int64 (serving/arena.py, csrc/runtime/arena.h share the layout).
 constexpr int kArenaPayloadOff = 64 + 32 * 1024;  // descriptors: up to 1024 requests
 constexpr int kArenaMaxRequests = 1024;
-// narrow_modulo > 0: narrow rows [int32 (id mod m) x F | bf16 weights x F | pad].
+// narrow_modulo > 0: narrow rows [int32 (id mod m) x F | fp32 weights x F | pad].
 hipError_t launch_unpack_arena(const void* arena, int64_t* packed, int B, int F, int W, int max_req,
                                hipStream_t st, int64_t narrow_modulo = 0);
 // Packed varint ids of a built arena -> its device-only int64 id region

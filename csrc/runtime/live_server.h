@@ -109,8 +109,9 @@ struct LiveConfig {
   bool start_paused = false;
   // > 0: requests with raw tensor_content int64 ids + fp32 weights are
   // narrowed by the submitting thread while it copies them (runtime/narrow.h):
-  // ids -> int32 rows (id mod narrow_modulo: the model's table size), weights
-  // -> bf16. Halves the H2D bytes; other encodings travel raw.
+  // ids -> table rows (id mod narrow_modulo: the model's table size) as 3-byte
+  // rows when the table has <= 2^24 rows, else int32; weights stay fp32 (7 or
+  // 8 bytes per feature instead of 12); other encodings travel raw.
   int64_t narrow_modulo = 0;
   // > 0 (narrowed requests only): keep just the first narrow_wts_cols weights
   // of each row - the model reads no others (one-hot DLRM: the dense
@@ -172,7 +173,7 @@ class LiveServer {
     int64_t off, len, rows, deadline_us, t_arrive;
     Completion done;
     bool narrow = false;
-    int64_t ids_off = 0, wts_off = 0;  // narrow: payload offsets of the int32 rows / bf16 weights
+    int64_t ids_off = 0, wts_off = 0;  // narrow: payload offsets of the 3-byte / int32 rows and fp32 weights
   };
   struct Arena {
     uint8_t* base = nullptr;

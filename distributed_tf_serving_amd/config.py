@@ -85,7 +85,7 @@ class ServingConfig:
     # scatter mode on one node: "shared" = every rank DMAs its share of rank 0's
     # shared request arenas (csrc/runtime/shared_scatter.h); "rccl" = RCCL scatter
     scatter_path: str = "shared"
-    narrow_ingest: bool = True        # GPU live server: int64 ids -> int32 rows, fp32 weights -> bf16 on the host
+    narrow_ingest: bool = True        # GPU live server: int64 ids -> 3-byte / int32 table rows on the host (fp32 weights)
 
 
 @dataclass

@@ -76,7 +76,7 @@ class CTRModel(nn.Module):
     def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """CTR [B] fp32. ``out`` (fp32 [B], device or pinned host) receives the
         scores straight from the head kernel (no separate D2H copy)."""
-        # bf16 weights (narrow fan-out rows) go to the gather as they are
+        # bf16 weights go to the gather as they are (narrow fan-out rows carry fp32)
         if wts is not None and wts.dtype not in (torch.float32, torch.bfloat16):
             wts = wts.float()
         return self._forward(ids, wts, out)

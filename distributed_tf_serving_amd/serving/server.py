@@ -77,7 +77,7 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
     live = live_enabled(cfg, dev)
     # scatter on one node through rank 0's shared arenas: the step is local
     shared = live and mode == "scatter" and world > 1 and getattr(sc, "scatter_path", "shared") == "shared"
-    # rows exchanged between GPUs travel narrow (int32 rows + bf16 weights)
+    # rows exchanged between GPUs travel narrow (int32 rows + fp32 weights)
     fanout = live and mode != "local" and world > 1 and not shared
     layout = layout_for(cfg.model, fanout) if fanout else PackedLayout(cfg.model.num_fields)
     ex = ShardExecutor(model, layout, buckets, dev, use_graphs=use_graphs, slots=slots)
