@@ -1435,6 +1435,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
+  m.def("set_head_variant", &dtfs::set_head_variant, py::arg("variant"),
+        "fused last layer + head kernel: 0 double-buffered, 1 / 2 pipelined (64 x 3 / 32 x 4 stages); A/B studies");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("dot_interaction_gather", &dot_interaction_gather, py::arg("dense"), py::arg("table"), py::arg("ids"),
         py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);

@@ -83,6 +83,9 @@ hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 // Pipelined K1 kernel geometry: resident-wave cap (0 = one row per wave) and
 // rows in flight per wave (1 or 2).
 void set_embed_wave_cap(int waves, int rows_in_flight = 1);
+// fused last layer + head kernel: 0 double-buffered (default), 1 / 2 pipelined
+// (64-row tiles x 3 stages / 32-row tiles x 4 stages); A/B studies
+void set_head_variant(int v);
 
 // Front half of K1 for the gather-GEMM (gemm_gather): shared-table rows /
 // weights of B candidates, field-major rows_t / wts_t [F][Mp] (Mp = B rounded

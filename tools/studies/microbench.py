@@ -135,6 +135,7 @@ def main():
     ap.add_argument("--gather-locality", action="store_true",
                     help="gather-GEMM time by where the table rows come from (L2 / MALL / HBM)")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
+    ap.add_argument("--head", action="store_true", help="fused last layer + head: double-buffered vs pipelined")
     ap.add_argument("--serving", action="store_true",
                     help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
     a = ap.parse_args()
@@ -149,6 +150,10 @@ def main():
         shape, vs = a.variants.split(":")
         M, N, K = (int(x) for x in shape.split(","))
         print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
+        return
+    if a.head:
+        for r in head_study():
+            print(json.dumps(r), flush=True)
         return
     if a.gather_locality:
         for r in gather_locality_study():
@@ -180,6 +185,39 @@ def main():
         for B in ([512] if a.quick else [512, 4096]):
             print(json.dumps(bench_model(fam, B)), flush=True)
 
+
+
+def head_study(rows=(2048, 16384), K=512, N=256, dev="cuda", rounds=4):
+    """Fused last layer + head (ops.linear_head) per kernel variant
+    (hip().set_head_variant: 0 double-buffered, 1 pipelined 64-row x 3 stages,
+    2 pipelined 32-row x 4 stages), interleaved; every variant checked against
+    variant 0 and an fp32 reference."""
+    from distributed_tf_serving_amd.ops import hip
+
+    out = []
+    for M in rows:
+        g = torch.Generator(device="cpu").manual_seed(M)
+        x = ((torch.rand(M, K, generator=g) - 0.5)).to(torch.bfloat16).to(dev)
+        W = ((torch.rand(N, K, generator=g) - 0.5) / K ** 0.5).to(torch.bfloat16).to(dev)
+        b = (torch.rand(N, generator=g) - 0.5).to(dev)
+        hw = ((torch.rand(N, generator=g) - 0.5) * 0.1).to(dev)
+        extra = (torch.rand(2, M, generator=g) - 0.5).to(dev)
+        ref = torch.sigmoid(torch.relu(x.float() @ W.float().t() + b) @ hw + extra.sum(0))
+        res = {"op": "linear_head", "M": M, "K": K, "N": N}
+        times = {v: [] for v in (0, 1, 2)}
+        for _ in range(rounds):
+            for v in (0, 1, 2):
+                hip().set_head_variant(v)
+                times[v].append(_time(lambda: ops.linear_head(x, W, b, "relu", hw, 0.0, extra=extra), rounds=1))
+        for v in (0, 1, 2):
+            hip().set_head_variant(v)
+            y = ops.linear_head(x, W, b, "relu", hw, 0.0, extra=extra)
+            torch.cuda.synchronize()
+            res[f"v{v}_us"] = round(statistics.median(times[v]), 2)
+            res[f"v{v}_maxdiff_fp32"] = float((y - ref).abs().max())
+        hip().set_head_variant(0)
+        out.append(res)
+    return out
 
 
 def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024, dev="cuda"):
