@@ -12,7 +12,7 @@ SAN=${SAN:-both}
 if [ $# -gt 0 ]; then SUITES="$*"; else
   SUITES="tests/test_wire.py tests/test_runtime_cpu.py tests/test_serving_e2e.py tests/test_faults.py \
 tests/test_live_server.py tests/test_arena_cpu.py tests/test_step_control.py tests/test_bench_cpu.py \
-tests/test_cluster_server.py"
+tests/test_cluster_server.py tests/test_shared_scatter.py tests/test_native_front.py"
 fi
 status=0
 if [ "$SAN" = address ] || [ "$SAN" = both ]; then
@@ -34,7 +34,7 @@ if [ "$SAN" = thread ] || [ "$SAN" = both ]; then
   CLANG=/opt/rocm/lib/llvm/bin/clang++
   SRCS="tools/native/live_stress.cpp csrc/runtime/live_server.cpp csrc/runtime/loadgen.cpp csrc/runtime/step_control.cpp \
 csrc/runtime/arena.cpp csrc/runtime/narrow.cpp csrc/runtime/batcher.cpp csrc/runtime/thread_pool.cpp csrc/runtime/trace.cpp \
-csrc/wire/tensor_codec.cpp"
+csrc/runtime/shared_scatter.cpp csrc/runtime/numa.cpp csrc/wire/tensor_codec.cpp"
   mkdir -p build/stress
   t=0
   $CLANG -O1 -g -std=c++17 -fsanitize=thread -fno-omit-frame-pointer -Icsrc $SRCS -o build/stress/live_stress_tsan \

@@ -11,7 +11,8 @@
 // launch() records the step and fills the bucket's scores after a short
 // "device time"; wait() honours the timeout. Scenarios: closed loop, open loop,
 // close() while requests are queued, a broken cluster (mark_broken) with
-// requests in flight, and two ranks serving concurrently.
+// requests in flight, two ranks serving concurrently, and three ranks of a
+// shared-arena scatter (runtime/shared_scatter.h) cycling the plan ring.
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -26,6 +27,7 @@
 
 #include "runtime/live_server.h"
 #include "runtime/loadgen.h"
+#include "runtime/shared_scatter.h"
 #include "runtime/step_control.h"
 #include "wire/tensor_codec.h"
 
@@ -213,6 +215,73 @@ void two_ranks(bool break_midway) {
   c.join();
 }
 
+// Three ranks on one shared-scatter segment, one thread each: rank 0 builds a
+// batch of a varying size in one of two shared arenas and publishes the plan;
+// every rank copies its share (memcpy standing in for the DMA), checks it
+// against the rows' own bytes, and marks the step done; rank 0 reuses an arena
+// only after every rank finished the step that read it.
+void shared_scatter_ring() {
+  const std::string name = "/dtfs-stress-sct-" + std::to_string(getpid());
+  const int W = 3, F = 43, B = 128, steps = 400;
+  const int64_t cap = 8 << 20;
+  SharedScatter s0(name, W, 0, true, F, 2, cap, 2, int64_t(W) * B);
+  SharedScatter s1(name, W, 1, false), s2(name, W, 2, false);
+  s0.unlink();
+  const auto reqs = make_requests(12, 29, F, true);
+  std::atomic<int> bad{0};
+  auto take = [&](SharedScatter& s, uint64_t k, std::vector<uint8_t>& dst) {
+    RankShare mine;
+    int ai = -1;
+    if (!s.wait_plan(k, 5'000'000, &mine, &ai)) {
+      ++bad;
+      return;
+    }
+    uint8_t hdr[64];
+    const uint8_t* src = s.arena(ai);
+    for (const auto& c : share_copies(src, mine, hdr)) std::memcpy(dst.data() + c.dst_off, c.src, size_t(c.n));
+    int64_t rows, rt;
+    std::memcpy(&rows, dst.data() + 8, 8);
+    std::memcpy(&rt, src + 16, 8);
+    if (rows != mine.rows) ++bad;
+    // every row's table entry arrived at the table's start, and its ids match the source batch
+    for (int64_t i = 0; i < mine.rows; ++i) {
+      int32_t e[2], f[2];
+      std::memcpy(e, dst.data() + kArenaPayloadOff + rt + 8 * i, 8);
+      std::memcpy(f, src + kArenaPayloadOff + rt + 8 * (mine.row0 + i), 8);
+      if (e[0] != f[0] || e[1] != f[1] ||
+          std::memcmp(dst.data() + kArenaPayloadOff + (e[0] & 0x7fffffff), src + kArenaPayloadOff + (e[0] & 0x7fffffff),
+                      8 * F) != 0)
+        ++bad;
+    }
+    s.mark_done(k);
+  };
+  auto follower = [&](SharedScatter* s) {
+    std::vector<uint8_t> dst(static_cast<size_t>(cap));
+    for (int k = 0; k < steps; ++k) take(*s, s->begin_step(), dst);
+  };
+  std::thread t1(follower, &s1), t2(follower, &s2);
+  std::vector<uint8_t> dst0(static_cast<size_t>(cap));
+  for (int k = 0; k < steps; ++k) {
+    const int ai = k % 2, n = 1 + k % 12;  // 29 .. 348 rows: some ranks get nothing
+    std::vector<std::pair<const char*, size_t>> rq;
+    for (int i = 0; i < n; ++i) rq.emplace_back(reqs[size_t(i)].data(), reqs[size_t(i)].size());
+    uint8_t* a = s0.arena(ai);
+    const auto spans = arena_place(a, cap, rq, 0);
+    arena_build(a, cap, spans, "feat_ids", "feat_wts", F, int64_t(W) * B, 0);
+    const uint64_t kk = s0.begin_step();
+    s0.publish_plan(kk, ai, B);
+    take(s0, kk, dst0);
+    std::string err;
+    if (!s0.wait_done(kk, 5'000'000, &err)) {
+      ++bad;
+      break;
+    }
+  }
+  t1.join();
+  t2.join();
+  check(bad.load() == 0, "shared scatter: 3 ranks, every share copied and checked, plan ring reused");
+}
+
 }  // namespace
 
 int main() {
@@ -220,6 +289,7 @@ int main() {
   close_under_load();
   two_ranks(false);
   two_ranks(true);
+  shared_scatter_ring();
   std::printf("%s\n", fails ? "live_stress: FAILED" : "live_stress: all ok");
   return fails ? 1 : 0;
 }
