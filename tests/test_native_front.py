@@ -214,3 +214,42 @@ def test_native_client_talks_to_grpcio_server():
     finally:
         gd.stop()
         srv.stop()
+
+
+def test_server_cli_serves_through_the_native_front_door():
+    """`python -m ...serving.server` picks the native front door for a live
+    servable (--front auto), answers a grpcio Predict, and exits on SIGTERM."""
+    import os
+    import signal
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-m", "distributed_tf_serving_amd.serving.server", "--preset", "wdl_tiny_cpu",
+                          "--device", "cpu", "--host", "127.0.0.1", "--port", str(port), "--no-gc-freeze"],
+                         cwd=repo, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
+    try:
+        line = ""
+        deadline = time.monotonic() + 120
+        while time.monotonic() < deadline:
+            line = p.stdout.readline()
+            if not line or line.startswith("serving model"):
+                break
+        assert "native front door" in line, line
+        ch = _channel(port)
+        data = SyntheticRequests(fields=F, seed=21).serialized(5)
+        assert _scores(ch.unary_unary(PREDICT)(data, timeout=30)).shape == (5,)
+        ch.close()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    assert p.returncode == 0, p.returncode
