@@ -23,6 +23,12 @@ def _short(name: str) -> str:
 def timeline(db: str, anchor: str = "gemm_8ph", last: int = 60, window_us: float = 400.0) -> str:
     c = sqlite3.connect(db)
     rows = [(_short(n), s / 1e3, e / 1e3) for n, s, e in c.execute("select name, start, end from kernels order by start")]
+    try:  # SDMA copies too (H2D of the request arena): where they sit against the kernels
+        rows += [("copy (H2D arena)" if size >= 1 << 20 else "copy (small)", s / 1e3, e / 1e3)
+                 for s, e, size in c.execute("select start, end, size from memory_copies")]
+        rows.sort(key=lambda r: r[1])
+    except sqlite3.Error:
+        pass
     anchors = [r for r in rows if anchor in r[0]]
     if len(anchors) < 3:
         return f"fewer than 3 '{anchor}' dispatches"
