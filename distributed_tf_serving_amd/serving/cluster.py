@@ -7,8 +7,12 @@ that fan-out moves inside one node, onto the native live server of every rank
 
 ``scatter``   rank 0 runs the PredictionService front door (gRPC and/or
               in-process); each batch of up to world x B candidate rows is
-              scattered over the GPUs (RCCL / the one-shot peer kernel), each
-              GPU scores its share, the scores are gathered back to rank 0.
+              split evenly over the GPUs. By default (``serving.scatter_path:
+              shared``) rank 0 batches into shared request arenas every rank
+              maps: each GPU DMAs only its share over its own PCIe link and
+              writes its scores into rank 0's shared output, no collective
+              (csrc/runtime/shared_scatter.h); ``rccl`` scatters packed rows
+              (RCCL / the one-shot peer kernel) and gathers the scores back.
 ``alltoall``  every rank is a front door (gRPC port + rank); each rank's rows
               are split over all GPUs and the scores return to it.
 
@@ -18,8 +22,11 @@ csrc/runtime/step_control.h): a step runs only when some rank has requests
 every rank's batch, so a lone request costs a small step, not a full one.
 No Python runs per step or per request on any rank.
 
-    torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m distributed_tf_serving_amd.serving.cluster \\
-        --preset deepfm_fanout4 --port 9999
+    python -m distributed_tf_serving_amd.serving.launch --nproc-per-node 4 -- \\
+        -m distributed_tf_serving_amd.serving.cluster --preset deepfm_fanout4 --port 9999
+
+Front doors are the C++ h2c gRPC server by default (``--front native``,
+serving/native_front.py: Predict straight into the live server) or grpcio.
 
 Failure handling (the reference has none: a failed shard kills the requester
 thread, reference DCNClient.java:158-159, :185-188):
