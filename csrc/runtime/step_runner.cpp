@@ -32,7 +32,18 @@ StepRunner::StepRunner(int device, int slots) : device_(device) {
   // fan-out runner keeps one (its ingress / egress streams take the other
   // hardware queues).
   ck(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking), "hipStreamCreate(copy)");
-  ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
+  // A/B knobs (env, read once): DTFS_COPY_STREAMS=1 keeps every H2D on one copy
+  // stream; DTFS_COMPUTE_PRIORITY=1 creates the compute stream at the highest
+  // priority (its hardware queue is served first when queues are shared)
+  if (const char* e = std::getenv("DTFS_COPY_STREAMS")) two_copy_streams_ = std::atoi(e) != 1;
+  const char* pe = std::getenv("DTFS_COMPUTE_PRIORITY");
+  if (pe && std::atoi(pe) == 1) {
+    int least = 0, greatest = 0;
+    ck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+    ck(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, greatest), "hipStreamCreate(compute, priority)");
+  } else {
+    ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
+  }
   h2d_done_.resize(slots);
   done_.resize(slots);
   used_.assign(size_t(slots), 0);
@@ -108,7 +119,7 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
 void StepRunner::h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer,
                             bool alternate) {
   hipStream_t st = copy_;
-  if (alternate) {
+  if (alternate && two_copy_streams_) {
     if (!copy2_) ck(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking), "hipStreamCreate(copy2)");
     if (n_h2d_++ & 1) st = copy2_;
   }
