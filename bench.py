@@ -120,6 +120,11 @@ def parse_args():
     ap.add_argument("--table-rows", type=int, default=0, help="dlrm: rows per table (default: preset, 100M)")
     ap.add_argument("--shard-tables", action="store_true",
                     help="dlrm: shard the tables even on one GPU (exercises the embedding-exchange step program)")
+    ap.add_argument("--exchange", default=None, choices=["alltoall", "peer"],
+                    help="dlrm sharded tables: ids + rows through RCCL all-to-alls, or rows loaded from the owner's "
+                         "HBM over xGMI behind a per-rank hot-row replica cache (default: the preset's)")
+    ap.add_argument("--hot-cache-rows", type=int, default=None,
+                    help="peer exchange: replica cache rows per rank (default: the config's; 0 = no cache)")
     ap.add_argument("--small-buckets", default=None,
                     help="extra padding buckets (rows per GPU) below the full step, so a lightly loaded server "
                          "runs a step sized to what is queued (TF-Serving allowed_batch_sizes; at N > 1 every "
@@ -193,6 +198,10 @@ def build(a, ctx):
                       file=sys.stderr)
             rows = fit
         cfg.table_rows = rows
+        if a.exchange:
+            cfg.embedding_exchange = a.exchange
+        if a.hot_cache_rows is not None:
+            cfg.hot_cache_rows = a.hot_cache_rows
     # CPU (gloo): the step's collectives run on the live server's launcher
     # thread, so they get a group of their own (the main thread syncs phases
     # on the default group)
@@ -266,6 +275,30 @@ def request_pool(a, ctx, eng, B, F):
     synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank)
     n = max(1, a.pool) if n_req else 0
     return [synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n)], n_req
+
+
+def fresh_hit_rate(cfg, model, ctx, rows: int = 32768) -> float:
+    """Fraction of remote lookups of a FRESH draw of the synthetic stream
+    (another seed than the served pool) that the installed hot set holds."""
+    import numpy as np
+
+    from distributed_tf_serving_amd.parallel.hot_cache import KEY_SHIFT
+
+    cache, peer = model.cache, model.emb.peer
+    ids, _ = SyntheticRequests(fields=cfg.num_fields, id_space=1 << 40, dist="zipf",
+                               seed=99991 + ctx.rank).arrays(rows)
+    hot, col0 = int(getattr(model, "hot", 1)), cfg.num_dense
+    keys = cache.keys.cpu().numpy()
+    hit = tot = 0
+    for t in range(peer.T):
+        if not bool(peer.tremote_cpu[t]):
+            continue
+        v = ids[:, col0 + t * hot:col0 + (t + 1) * hot].astype(np.int64) % np.int64(peer.rows[t])
+        k = (np.int64(t) << KEY_SHIFT) | v.reshape(-1)
+        pos = np.clip(np.searchsorted(keys, k), 0, max(0, keys.size - 1))
+        hit += int((keys[pos] == k).sum()) if keys.size else 0
+        tot += k.size
+    return round(hit / tot, 4) if tot else 0.0
 
 
 def fp32_check(cfg, model, live, request: bytes) -> dict:
@@ -378,12 +411,25 @@ def run_live(a, ctx, cfg, model, eng, B):
     if control is not None:
         live.resume()  # every rank is past its start-up collectives: steps may begin
     timeout_us = int(a.step_timeout_s * 1e6)
+    cache = getattr(model, "cache", None)
+    if cache is not None and pool:
+        # peer exchange: serve a few steps so the kernels sample the stream,
+        # then install the hot set (the refresher is off while the clock runs:
+        # a synthetic stream's hot set does not drift)
+        live.run_load(pool, warmup=0, count=max(8, a.warmup) * n_req, concurrency=conc, threads=a.client_threads,
+                      timeout_us=timeout_us)
+        for _ in range(2):
+            cache.refresh()
+        sync()
+        cache.reset_counts()
+    steps0 = live.stats()["steps"]
     if pool:
         r = live.run_load(pool, warmup=untimed * n_req, count=a.steps * n_req, concurrency=conc,
                           threads=a.client_threads, timeout_us=timeout_us)
     else:  # a rank without requests (scatter followers): its live server joins rank 0's steps
         r = {"window_us": 0.0, "latency_us": [], "errors": 0, "ok": 0}
     st_load = live.stats()
+    cache_counts = cache.counts() if cache is not None else None  # the throughput run's lookups
     window_s = r["window_us"] * 1e-6
     if r["errors"]:
         print(f"rank {rank}: {r['errors']} requests failed: {r.get('first_error')}", file=sys.stderr, flush=True)
@@ -437,8 +483,22 @@ def run_live(a, ctx, cfg, model, eng, B):
             "plan": {"world": model.plan.world, "row_wise_tables": len(model.plan.row_wise()),
                      "tables_per_rank": [len(model.plan.table_wise(r)) for r in range(model.plan.world)]},
             "multi_hot": int(getattr(model, "hot", 1)),
-            "hot_row_cache": None,  # every remote row crosses xGMI (no replica cache yet)
+            "mode": model.emb.exchange,
+            "hot_row_cache": None,
         }
+        if cache is not None:
+            hits, misses = cache_counts
+            steps = max(1, st_load["steps"] - steps0)
+            lookups_per_step = (hits + misses) / steps
+            extra["embedding_exchange"]["hot_row_cache"] = {
+                **cache.describe(),
+                "hits": hits, "misses": misses, "hit_rate": round(hits / max(1, hits + misses), 4),
+                # measured over the throughput run (warmup + timed steps)
+                "remote_lookups_per_step": round(lookups_per_step, 1),
+                "xgmi_bytes_per_step_per_rank": int(misses / steps * cfg.embed_dim * 2),
+                # the pool repeats: the same hot set on a fresh draw of the stream
+                "hit_rate_fresh_stream": fresh_hit_rate(cfg, model, ctx),
+            }
     if eng.scatter is not None:
         # shared-arena scatter: host->device bytes this rank copied per step (its
         # share of rank 0's batch), gathered from every rank
@@ -608,7 +668,11 @@ def main():
                       if getattr(eng, "_cin", None) is not None and eng._cin.peer_enabled else "")
                    + (f", {eng.layout.row_bytes} B rows: int32 table rows + fp32 weights" if eng.layout.narrow
                       else f", {eng.layout.row_bytes} B rows: raw int64 ids + fp32 weights") + ")")
-        if hasattr(model, "plan"):
+        if hasattr(model, "plan") and getattr(model.emb, "exchange", "") == "peer" and model.plan.world > 1:
+            par += (f" + embedding-mp{model.plan.world} (table-wise, rows loaded from the owner's HBM over xGMI, "
+                    + (f"{model.cache.cap}-row hot-row replica cache per rank" if model.cache is not None
+                       else "no replica cache") + ")")
+        elif hasattr(model, "plan"):
             par += (f" + embedding-mp{model.plan.world} ({len(model.plan.row_wise())} row-wise tables, all-to-all; "
                     + ("native two-lane step program" if eng.program_active else "eager torch.distributed")
                     + (f", one-shot peer exchange for messages <= {eng._cprog.peer_cap} B per peer"

@@ -6,6 +6,8 @@
 // current HIP stream, so they compose with torch streams and HIP-graph capture.
 #include <torch/extension.h>
 
+#include <cstring>
+
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -793,6 +795,204 @@ torch::Tensor shard_route(c10::optional<torch::Tensor> ids, c10::optional<torch:
   return out;
 }
 
+// ---------------------------------------------------------------- peer lookup
+// tbase int64 [T] (device addresses), trows int64 [T], tremote int32 [T],
+// cache int64 [5], stats int64 [128], ring int64 [cap], ring_ctr int64 [1]
+static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Tensor& tbase, const torch::Tensor& trows,
+                                      const torch::Tensor& tremote, const c10::optional<torch::Tensor>& cache,
+                                      const c10::optional<torch::Tensor>& stats,
+                                      const c10::optional<torch::Tensor>& ring,
+                                      const c10::optional<torch::Tensor>& ring_ctr, int64_t sample_every) {
+  const int64_t T = tbase.numel();
+  for (auto* t : {&tbase, &trows}) {
+    check_same_dev(ref, *t, "peer table map");
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == T && t->is_contiguous(), "tbase / trows: int64 [T]");
+  }
+  check_same_dev(ref, tremote, "tremote");
+  TORCH_CHECK(tremote.scalar_type() == torch::kInt32 && tremote.numel() == T && tremote.is_contiguous(),
+              "tremote: int32 [T]");
+  dtfs::PeerLookupArgs p;
+  p.tbase = tbase.data_ptr<int64_t>();
+  p.trows = trows.data_ptr<int64_t>();
+  p.tremote = tremote.data_ptr<int32_t>();
+  if (cache) {
+    check_same_dev(ref, *cache, "cache");
+    TORCH_CHECK(cache->scalar_type() == torch::kInt64 && cache->numel() == 5 && cache->is_contiguous(), "cache: int64 [5]");
+    p.cache = cache->data_ptr<int64_t>();
+  }
+  if (stats) {
+    check_same_dev(ref, *stats, "stats");
+    TORCH_CHECK(stats->scalar_type() == torch::kInt64 && stats->numel() == 128 && stats->is_contiguous(),
+                "stats: int64 [128]");
+    p.stats = reinterpret_cast<unsigned long long*>(stats->data_ptr<int64_t>());
+  }
+  if (ring) {
+    TORCH_CHECK(ring_ctr.has_value(), "ring needs ring_ctr");
+    check_same_dev(ref, *ring, "ring");
+    check_same_dev(ref, *ring_ctr, "ring_ctr");
+    TORCH_CHECK(ring->scalar_type() == torch::kInt64 && ring->numel() >= 1 && ring->is_contiguous(), "ring: int64 [cap]");
+    TORCH_CHECK(ring_ctr->scalar_type() == torch::kInt64 && ring_ctr->numel() == 1, "ring_ctr: int64 [1]");
+    p.ring = ring->data_ptr<int64_t>();
+    p.ring_ctr = reinterpret_cast<unsigned long long*>(ring_ctr->data_ptr<int64_t>());
+    p.ring_cap = ring->numel();
+    p.sample_every = int(std::max<int64_t>(sample_every, 0));
+  }
+  return p;
+}
+
+// K1 + K5 through the peer lookup: ids [B, >= id_col0 + T] int32/int64 rows,
+// or a device request arena (B rows)
+torch::Tensor dot_interaction_gather_peer(torch::Tensor dense, c10::optional<torch::Tensor> ids,
+                                          c10::optional<torch::Tensor> arena, int64_t id_col0, torch::Tensor tbase,
+                                          torch::Tensor trows, torch::Tensor tremote,
+                                          c10::optional<torch::Tensor> cache, c10::optional<torch::Tensor> stats,
+                                          c10::optional<torch::Tensor> ring, c10::optional<torch::Tensor> ring_ctr,
+                                          int64_t sample_every, int64_t out_cols) {
+  check_dev(dense, "dense");
+  TORCH_CHECK(ids.has_value() != arena.has_value(), "dot_interaction_gather_peer: ids or a device arena");
+  TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && dense.dim() == 2 && dense.size(1) == 64 &&
+                  dense.stride(1) == 1 && dense.stride(0) % 8 == 0,
+              "dense must be bf16 [B, 64] with unit inner stride");
+  const int64_t B = dense.size(0), T = tbase.numel();
+  TORCH_CHECK(T >= 1 && T + 1 <= 32 && id_col0 >= 0, "1 <= T <= 31 tables, id_col0 >= 0");
+  const void* idp = nullptr;
+  bool ids64 = true;
+  int64_t ldi = 0;
+  if (ids) {
+    check_same_dev(dense, *ids, "ids");
+    TORCH_CHECK((ids->scalar_type() == torch::kInt64 || ids->scalar_type() == torch::kInt32) && ids->dim() == 2 &&
+                    ids->stride(1) == 1 && ids->size(0) == B && ids->size(1) >= id_col0 + T,
+                "ids must be int32/int64 [B, >= id_col0 + T] rows with unit inner stride");
+    ids64 = ids->scalar_type() == torch::kInt64;
+    ldi = ids->stride(0);
+    idp = static_cast<const uint8_t*>(ids->data_ptr()) + id_col0 * ids->element_size();
+  } else {
+    check_same_dev(dense, *arena, "arena");
+    TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous(), "arena must be a contiguous uint8 buffer");
+  }
+  const auto p = peer_args(dense, tbase, trows, tremote, cache, stats, ring, ring_ctr, sample_every);
+  const int64_t used = 64 + (T + 1) * T / 2;
+  if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
+  TORCH_CHECK(out_cols >= used && out_cols % 8 == 0 && out_cols <= 1024, "out_cols: >= used, a multiple of 8, <= 1024");
+  c10::DeviceGuard g(dense.device());
+  auto out = torch::empty({B, out_cols}, dense.options());
+  check_hip(dtfs::launch_dot_interaction_gather(dense.data_ptr(), dense.stride(0), nullptr, 0, idp, ids64, ldi, nullptr,
+                                                nullptr, int(T), int(B), out.data_ptr(), out_cols, int(out_cols),
+                                                cur_stream(dense), arena ? arena->data_ptr() : nullptr,
+                                                arena ? int(id_col0) : 0, &p),
+            "dot_interaction_gather_peer");
+  return out;
+}
+
+// K1b through the peer lookup: pooled bags -> out bf16 [B, T, 64]
+void peer_bag(c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts, c10::optional<torch::Tensor> arena,
+              int64_t B, int64_t col0, int64_t hot, torch::Tensor tbase, torch::Tensor trows, torch::Tensor tremote,
+              c10::optional<torch::Tensor> cache, c10::optional<torch::Tensor> stats, c10::optional<torch::Tensor> ring,
+              c10::optional<torch::Tensor> ring_ctr, int64_t sample_every, torch::Tensor out) {
+  check_dev(out, "out");
+  TORCH_CHECK(ids.has_value() != arena.has_value(), "peer_bag: ids (+ wts) or a device arena");
+  const int64_t T = tbase.numel();
+  TORCH_CHECK(T >= 1 && hot >= 1 && col0 >= 0 && B >= 0, "T, hot >= 1, col0 >= 0");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.is_contiguous() && out.numel() == B * T * 64,
+              "out must be contiguous bf16 [B, T, 64]");
+  const void* idp = nullptr;
+  const float* wp = nullptr;
+  bool ids64 = true;
+  int64_t ldi = 0, ldw = 0;
+  const int64_t need = col0 + T * hot;
+  if (ids) {
+    TORCH_CHECK(wts.has_value(), "peer_bag: ids need wts");
+    check_same_dev(out, *ids, "ids");
+    check_same_dev(out, *wts, "wts");
+    TORCH_CHECK((ids->scalar_type() == torch::kInt64 || ids->scalar_type() == torch::kInt32) && ids->dim() == 2 &&
+                    ids->stride(1) == 1 && ids->size(0) == B && ids->size(1) >= need,
+                "ids must be int32/int64 [B, >= col0 + T * hot] rows with unit inner stride");
+    TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->stride(1) == 1 && wts->size(0) == B &&
+                    wts->size(1) >= need,
+                "wts must be fp32 [B, >= col0 + T * hot] rows with unit inner stride");
+    ids64 = ids->scalar_type() == torch::kInt64;
+    idp = ids->data_ptr();
+    ldi = ids->stride(0);
+    wp = wts->data_ptr<float>();
+    ldw = wts->stride(0);
+  } else {
+    check_same_dev(out, *arena, "arena");
+    TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous(), "arena must be a contiguous uint8 buffer");
+  }
+  const auto p = peer_args(out, tbase, trows, tremote, cache, stats, ring, ring_ctr, sample_every);
+  c10::DeviceGuard g(out.device());
+  check_hip(dtfs::launch_peer_bag(p, idp, ids64, ldi, wp, ldw, arena ? arena->data_ptr() : nullptr, int(col0), int(T),
+                                  int(hot), int(B), out.data_ptr(), cur_stream(out)),
+            "peer_bag");
+}
+
+// replica cache maintenance (parallel/hot_cache.py)
+void peer_cache_fill(torch::Tensor keys, torch::Tensor slots, torch::Tensor tbase, torch::Tensor trows,
+                     torch::Tensor rows) {
+  check_dev(rows, "rows");
+  for (auto* t : {&keys, &slots, &tbase, &trows}) check_same_dev(rows, *t, "cache fill input");
+  TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous() && slots.scalar_type() == torch::kInt32 &&
+                  slots.is_contiguous() && slots.numel() == keys.numel(),
+              "keys int64 [n], slots int32 [n]");
+  TORCH_CHECK(tbase.scalar_type() == torch::kInt64 && trows.scalar_type() == torch::kInt64 &&
+                  tbase.numel() == trows.numel() && tbase.is_contiguous() && trows.is_contiguous(),
+              "tbase / trows int64 [T]");
+  TORCH_CHECK(rows.scalar_type() == torch::kBFloat16 && rows.dim() == 2 && rows.size(1) == 64 && rows.is_contiguous(),
+              "rows must be contiguous bf16 [cap, 64]");
+  c10::DeviceGuard g(rows.device());
+  check_hip(dtfs::launch_peer_cache_fill(keys.data_ptr<int64_t>(), slots.data_ptr<int32_t>(), keys.numel(),
+                                         tbase.data_ptr<int64_t>(), trows.data_ptr<int64_t>(), int(tbase.numel()),
+                                         rows.data_ptr(), rows.size(0), cur_stream(rows)),
+            "peer_cache_fill");
+}
+
+void cache_index_build(torch::Tensor keys, torch::Tensor slots, torch::Tensor idx_keys, torch::Tensor idx_slots) {
+  check_dev(idx_keys, "idx_keys");
+  for (auto* t : {&keys, &slots, &idx_slots}) check_same_dev(idx_keys, *t, "cache index input");
+  TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous() && slots.scalar_type() == torch::kInt32 &&
+                  slots.is_contiguous() && slots.numel() == keys.numel(),
+              "keys int64 [n], slots int32 [n]");
+  TORCH_CHECK(idx_keys.scalar_type() == torch::kInt64 && idx_keys.is_contiguous() &&
+                  idx_slots.scalar_type() == torch::kInt32 && idx_slots.is_contiguous() &&
+                  idx_slots.numel() == idx_keys.numel(),
+              "idx_keys int64 [H], idx_slots int32 [H]");
+  const int64_t H = idx_keys.numel();
+  TORCH_CHECK(H >= 2 && (H & (H - 1)) == 0 && 2 * keys.numel() <= H, "index size: a power of two >= 2 n");
+  c10::DeviceGuard g(idx_keys.device());
+  check_hip(dtfs::launch_cache_index_build(keys.data_ptr<int64_t>(), slots.data_ptr<int32_t>(), keys.numel(),
+                                           idx_keys.data_ptr<int64_t>(), idx_slots.data_ptr<int32_t>(), H - 1,
+                                           cur_stream(idx_keys)),
+            "cache_index_build");
+}
+
+// IPC: export a device tensor's allocation (handle bytes + the tensor's byte
+// offset in it) / map a peer's export as a tensor (closed when it dies)
+py::tuple ipc_export(torch::Tensor t) {
+  check_dev(t, "t");
+  c10::DeviceGuard g(t.device());
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  check_hip(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(t.data_ptr())), "hipMemGetAddressRange");
+  hipIpcMemHandle_t h;
+  check_hip(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base)), "hipIpcGetMemHandle");
+  const int64_t off = static_cast<int64_t>(static_cast<const char*>(t.data_ptr()) - static_cast<const char*>(base));
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)), off);
+}
+
+torch::Tensor ipc_open(py::bytes handle, int64_t offset, std::vector<int64_t> shape, torch::Tensor like) {
+  check_dev(like, "like");
+  const std::string hb = handle;
+  TORCH_CHECK(hb.size() == sizeof(hipIpcMemHandle_t), "ipc_open: bad handle");
+  TORCH_CHECK(offset >= 0, "ipc_open: offset >= 0");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, hb.data(), sizeof(h));
+  c10::DeviceGuard g(like.device());
+  void* base = nullptr;
+  check_hip(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  void* p = static_cast<char*>(base) + offset;
+  return torch::from_blob(p, shape, [base](void*) { (void)hipIpcCloseMemHandle(base); }, like.options());
+}
+
 // ---------------------------------------------------------------- K6
 // A head's extra logit: fp32 [M], or fp32 [P, >= M] partials summed in order
 // (row stride >= M, unit inner stride: the gather-GEMM path's [2, Mp]).
@@ -1428,6 +1628,23 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("tm"), py::arg("col"), py::arg("mod"), py::arg("off"), py::arg("out") = py::none(),
         py::arg("hot") = 1, py::arg("wts") = py::none(), py::arg("out_w") = py::none(),
         "K1b routing: rows (+ weights) of every candidate's owned-table ids grouped by owner rank");
+  m.def("dot_interaction_gather_peer", &dot_interaction_gather_peer, py::arg("dense"), py::arg("ids"),
+        py::arg("arena"), py::arg("id_col0"), py::arg("tbase"), py::arg("trows"), py::arg("tremote"),
+        py::arg("cache") = py::none(), py::arg("stats") = py::none(), py::arg("ring") = py::none(),
+        py::arg("ring_ctr") = py::none(), py::arg("sample_every") = 0, py::arg("out_cols") = 0,
+        "K1 + K5 with the rows read where they live (peer stores over xGMI, replica cache first)");
+  m.def("peer_bag", &peer_bag, py::arg("ids"), py::arg("wts"), py::arg("arena"), py::arg("B"), py::arg("col0"),
+        py::arg("hot"), py::arg("tbase"), py::arg("trows"), py::arg("tremote"), py::arg("cache") = py::none(),
+        py::arg("stats") = py::none(), py::arg("ring") = py::none(), py::arg("ring_ctr") = py::none(),
+        py::arg("sample_every") = 0, py::arg("out"),
+        "K1b multi-hot bags with the rows read where they live -> bf16 [B, T, 64]");
+  m.def("peer_cache_fill", &peer_cache_fill, py::arg("keys"), py::arg("slots"), py::arg("tbase"), py::arg("trows"),
+        py::arg("rows"), "replica cache: copy the keys' table rows into their slots");
+  m.def("cache_index_build", &cache_index_build, py::arg("keys"), py::arg("slots"), py::arg("idx_keys"),
+        py::arg("idx_slots"), "replica cache: open-addressing index keys -> slots (idx_keys pre-filled with -1)");
+  m.def("ipc_export", &ipc_export, py::arg("t"), "(IPC handle bytes, byte offset) of a device tensor's allocation");
+  m.def("ipc_open", &ipc_open, py::arg("handle"), py::arg("offset"), py::arg("shape"), py::arg("like"),
+        "map a peer's ipc_export as a tensor (dtype / device of `like`)");
   m.def("head", &head, py::arg("x"), py::arg("w"), py::arg("bias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),

@@ -4,6 +4,7 @@
 // quantisation for the fp8 towers.
 #include "common.h"
 #include "launchers.h"
+#include "peer_lookup.h"
 
 namespace dtfs {
 namespace kern {
@@ -142,12 +143,15 @@ __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restric
 // random reads in flight per wave). The output row (dense | lower triangle |
 // zero pad) is assembled in LDS and written as 16-byte vectors instead of
 // 2-byte scattered stores.
+// With peer.tbase set, the rows come through the peer lookup (peer_lookup.h):
+// table-wise shards read where they live, hot remote rows from the replica
+// cache - the same one-kernel step at any number of ranks.
 template <typename IdT>
 __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
     const bf16* __restrict__ dense, int64_t ldd, const bf16* __restrict__ table, int64_t table_rows,
     const IdT* __restrict__ ids, int64_t ldi, const int64_t* __restrict__ modulo_f,
     const int64_t* __restrict__ offset_f, int T, int B, bf16* __restrict__ out, int64_t ldo, int out_cols,
-    const uint8_t* __restrict__ arena, int id_col0) {
+    const uint8_t* __restrict__ arena, int id_col0, PeerLookupArgs peer) {
   constexpr int D = 64;
   constexpr int ROWB = 4 * 2048;  // LDS bytes per block: 4 waves x one output row (<= 1024 columns)
   __shared__ __attribute__((aligned(16))) uint8_t lds[ROWB];
@@ -156,10 +160,12 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
   if (b >= B) return;
   const int r = lane & 31, h = lane >> 5;
   const int nv = T + 1;
-  int64_t row = -1;
+  const bf16* src = nullptr;
+  int hit = -1;
+  int64_t key = 0;
   if (r >= 1 && r < nv) {
     const int t = r - 1;
-    const int64_t m = modulo_f[t];
+    const int64_t m = peer.tbase ? peer.trows[t] : modulo_f[t];
     int64_t id = 0;
     if (arena) {  // the request arena's row b (K0 fused: no unpack pass); padding rows read id 0
       const ArenaRow ar = arena_row(arena, kArenaPayloadOff, b);
@@ -170,7 +176,16 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
     }
     int64_t v = id % m;
     if (v < 0) v += m;
-    row = min(offset_f[t] + v, table_rows - 1);
+    if (peer.tbase) {
+      src = peer_row(peer, cache_view(peer), t, v, hit);
+      key = (int64_t(t) << 40) | v;
+    } else {
+      src = table + min(offset_f[t] + v, table_rows - 1) * D;
+    }
+  }
+  if (peer.tbase) {  // converged: the ballots see every lane (lanes h = 1 repeat h = 0's rows)
+    peer_count(peer, hit, h == 0);
+    ring_push(peer, key, h == 0 && hit >= 0 && peer.sample_every > 0 && b % peer.sample_every == 0);
   }
   bf16x8 x[4];
 #pragma unroll
@@ -178,7 +193,7 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
     const int k = 16 * s + 8 * h;
     x[s] = bf16x8{};
     if (r == 0) x[s] = *reinterpret_cast<const bf16x8*>(dense + int64_t(b) * ldd + k);
-    else if (row >= 0) x[s] = *reinterpret_cast<const bf16x8*>(table + row * D + k);
+    else if (src) x[s] = *reinterpret_cast<const bf16x8*>(src + k);
   }
   f32x16 acc;
 #pragma unroll
@@ -525,22 +540,25 @@ hipError_t launch_dot_interaction(const void* dense, int64_t ldd, const void* em
 hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
                                          const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
                                          const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
-                                         hipStream_t st, const void* arena, int id_col0) {
+                                         hipStream_t st, const void* arena, int id_col0,
+                                         const PeerLookupArgs* peer) {
   if (B == 0) return hipSuccess;
+  const bool pl = peer && peer->tbase;
   if (T < 1 || T + 1 > 32 || out_cols % 8 || out_cols > 1024 || out_cols < 64 + (T + 1) * T / 2 || ldo % 8 ||
-      ldo < out_cols || ldd % 8 || (!arena && (!ids || ldi < T)) || (arena && id_col0 < 0) || table_rows < 1 ||
-      !modulo_f || !offset_f)
+      ldo < out_cols || ldd % 8 || (!arena && (!ids || ldi < T)) || (arena && id_col0 < 0) ||
+      (!pl && (table_rows < 1 || !modulo_f || !offset_f)) || (pl && (!peer->trows || !peer->tremote)))
     return hipErrorInvalidValue;
+  const PeerLookupArgs pa = pl ? *peer : PeerLookupArgs{};
   const uint8_t* ar = static_cast<const uint8_t*>(arena);
   dim3 grid((B + 3) / 4), block(256);
   if (ids64)
     hipLaunchKernelGGL(dot_interact_gather_kernel<int64_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
                        static_cast<const bf16*>(table), table_rows, static_cast<const int64_t*>(ids), ldi, modulo_f,
-                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0);
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0, pa);
   else
     hipLaunchKernelGGL(dot_interact_gather_kernel<int32_t>, grid, block, 0, st, static_cast<const bf16*>(dense), ldd,
                        static_cast<const bf16*>(table), table_rows, static_cast<const int32_t*>(ids), ldi, modulo_f,
-                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0);
+                       offset_f, T, B, static_cast<bf16*>(out), ldo, out_cols, ar, id_col0, pa);
   return hipGetLastError();
 }
 

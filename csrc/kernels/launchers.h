@@ -215,15 +215,55 @@ struct CrossGemmArgs {
 };
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 
+// Peer lookup (kernels/peer_lookup.h): table-wise sharded tables read
+// one-sidedly where they live. Row v of table t is at device address
+// tbase[t] + 128 v (this rank's store, or the owner's store mapped over xGMI
+// by IPC; v = id mod trows[t]); tremote[t] = 1 marks a table owned by another
+// rank, whose rows are looked up in the replica cache first. cache = device
+// int64 [5] {index (keys int64 [mask + 1] | slots int32 [mask + 1]; 0 =
+// empty), unused, mask, rows [cap][64] bf16, cap}, read by each wave at its
+// start (the host swaps indices by rewriting word 0). stats [128]:
+// hits at 2i, misses at 2i + 1 (i = block % 64). Candidates b with b %
+// sample_every == 0 push their remote keys (t << 40 | v) into ring (wrapping).
+struct PeerLookupArgs {
+  const int64_t* tbase = nullptr;
+  const int64_t* trows = nullptr;
+  const int32_t* tremote = nullptr;
+  const int64_t* cache = nullptr;
+  unsigned long long* stats = nullptr;
+  int64_t* ring = nullptr;
+  unsigned long long* ring_ctr = nullptr;
+  int64_t ring_cap = 0;
+  int sample_every = 0;
+};
+
 // K1 + K5: DLRM dot interaction with the one-hot gather fused in: vector t+1
 // of row b is table[offset_f[t] + ids[b * ldi + t] mod modulo_f[t]] (rows
 // clamped to the table); out [B][ldo] = [dense | lower triangle | zeros].
 // arena (a device request arena): the ids are features id_col0 .. id_col0 +
-// T - 1 of arena row b instead (ids unused).
+// T - 1 of arena row b instead (ids unused). peer: the rows come through the
+// peer lookup instead (table, table_rows, modulo_f, offset_f unused).
 hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const void* table, int64_t table_rows,
                                          const void* ids, bool ids64, int64_t ldi, const int64_t* modulo_f,
                                          const int64_t* offset_f, int T, int B, void* out, int64_t ldo, int out_cols,
-                                         hipStream_t st, const void* arena = nullptr, int id_col0 = 0);
+                                         hipStream_t st, const void* arena = nullptr, int id_col0 = 0,
+                                         const PeerLookupArgs* peer = nullptr);
+
+// K1b through the peer lookup: out[b][t] (bf16 [B][T][64]) = sum_j w(b, c) *
+// row(t, id(b, c)), c = col0 + t * hot + j (ids / wts [B][F] row views, or
+// the features of a device request arena row).
+hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64, int64_t ldi, const float* wts,
+                           int64_t ldw, const void* arena, int col0, int T, int hot, int B, void* out,
+                           hipStream_t st);
+
+// Replica cache maintenance: rows[slots[i]] = row (keys[i] & (2^40 - 1)) of
+// table keys[i] >> 40 (read through tbase: over xGMI for a peer's table);
+// and the open-addressing index (idx_keys pre-filled with -1, mask + 1 a
+// power of two >= 2 n) mapping keys[i] -> slots[i].
+hipError_t launch_peer_cache_fill(const int64_t* keys, const int32_t* slots, int64_t n, const int64_t* tbase,
+                                  const int64_t* trows, int T, void* rows, int64_t cap, hipStream_t st);
+hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* idx_keys,
+                                    int32_t* idx_slots, int64_t mask, hipStream_t st);
 
 // K4 (small) for the DLRM bottom MLP: relu(relu(relu(pad64(bf16(wts[:, :nd]))
 // W1^T + b1) W2^T + b2) W3^T + b3) in one kernel (W1 [N1][64], W2 [N2][N1], W3

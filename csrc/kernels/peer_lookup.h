@@ -1,0 +1,106 @@
+// Device side of the peer lookup (launchers.h PeerLookupArgs): a table-wise
+// sharded table's row is read where it lives - this rank's store, or the
+// owner's store mapped over xGMI by IPC - unless the row is in this rank's
+// replica cache of hot remote rows (an open-addressing index over keys
+// (t << 40) | row, built by cache_index_build_kernel, immutable while any
+// step reads it). Every remote lookup is counted (hit / miss) and rows whose
+// candidate index b is a multiple of sample_every push their remote keys into
+// a ring the host reads to find the hot rows (parallel/hot_cache.py).
+#pragma once
+#include "common.h"
+#include "launchers.h"
+
+namespace dtfs {
+namespace kern {
+
+constexpr int64_t kCacheEmpty = -1;
+constexpr int kCacheMaxProbe = 32;  // the index is built at <= 50 % load
+
+__device__ __forceinline__ uint64_t cache_hash(int64_t key, uint64_t mask) {
+  return ((uint64_t(key) * 0x9E3779B97F4A7C15ull) >> 24) & mask;
+}
+
+struct CacheView {
+  const int64_t* keys;
+  const int32_t* slots;
+  uint64_t mask;  // 0: the cache is empty
+  const bf16* rows;
+  int64_t cap;
+};
+
+__device__ __forceinline__ CacheView cache_view(const PeerLookupArgs& p) {
+  CacheView c{nullptr, nullptr, 0, nullptr, 0};
+  if (p.cache) {
+    // one index buffer = keys int64 [mask + 1] | slots int32 [mask + 1]: the
+    // host swaps indices by rewriting the single word cache[0]
+    c.keys = reinterpret_cast<const int64_t*>(p.cache[0]);
+    c.mask = uint64_t(p.cache[2]);
+    c.slots = c.keys ? reinterpret_cast<const int32_t*>(c.keys + (c.mask + 1)) : nullptr;
+    c.rows = reinterpret_cast<const bf16*>(p.cache[3]);
+    c.cap = p.cache[4];
+    if (!c.keys || !c.slots || !c.rows || c.cap < 1) c.mask = 0;
+  }
+  return c;
+}
+
+// Row v of table t (D = 64): its address, and hit = -1 (table held here),
+// 1 (remote, cached), 0 (remote, read over xGMI).
+__device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const CacheView& c, int t, int64_t v,
+                                                int& hit) {
+  const bf16* src = reinterpret_cast<const bf16*>(p.tbase[t]) + v * 64;
+  hit = -1;
+  if (p.tremote[t]) {
+    hit = 0;
+    if (c.mask) {
+      const int64_t key = (int64_t(t) << 40) | v;
+      uint64_t h = cache_hash(key, c.mask);
+      for (int probe = 0; probe < kCacheMaxProbe; ++probe) {
+        const int64_t k = c.keys[h];
+        if (k == key) {
+          const int64_t s = c.slots[h];
+          if (s >= 0 && s < c.cap) {
+            src = c.rows + s * 64;
+            hit = 1;
+          }
+          break;
+        }
+        if (k == kCacheEmpty) break;
+        h = (h + 1) & c.mask;
+      }
+    }
+  }
+  return src;
+}
+
+// Wave-aggregated counters: one atomic per wave and kind. Called by every
+// lane of the wave (ballots); lanes with counted = false contribute nothing.
+__device__ __forceinline__ void peer_count(const PeerLookupArgs& p, int hit, bool counted) {
+  if (!p.stats) return;
+  const uint64_t hits = __ballot(counted && hit == 1), miss = __ballot(counted && hit == 0);
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    unsigned long long* s = p.stats + 2 * (blockIdx.x & 63);
+    if (hits) atomicAdd(s, (unsigned long long)__popcll(hits));
+    if (miss) atomicAdd(s + 1, (unsigned long long)__popcll(miss));
+  }
+}
+
+// Push the keys of the active lanes into the sample ring (wrapping).
+__device__ __forceinline__ void ring_push(const PeerLookupArgs& p, int64_t key, bool active) {
+  if (!p.ring || p.ring_cap < 1) return;
+  const uint64_t m = __ballot(active);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(p.ring_ctr, (unsigned long long)__popcll(m));
+  const uint32_t lo = __shfl(uint32_t(base), leader), hi = __shfl(uint32_t(base >> 32), leader);
+  base = (uint64_t(hi) << 32) | lo;
+  if (active) {
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    p.ring[int64_t((base + below) % uint64_t(p.ring_cap))] = key;
+  }
+}
+
+}  // namespace kern
+}  // namespace dtfs

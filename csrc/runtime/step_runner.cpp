@@ -49,9 +49,15 @@ StepRunner::StepRunner(int device, int slots) : device_(device) {
   used_.assign(size_t(slots), 0);
   observed_.reset(new std::atomic<bool>[size_t(slots)]);
   for (int i = 0; i < slots; ++i) observed_[i].store(false);
+  // DTFS_DONE_DEVICE_SCOPE=1 (A/B only): step-done events without the
+  // system-scope release (the scores are written to fine-grained host memory,
+  // which the L2 does not cache)
+  const char* de = std::getenv("DTFS_DONE_DEVICE_SCOPE");
+  const unsigned done_flags =
+      hipEventDisableTiming | ((de && std::atoi(de) == 1) ? hipEventDisableSystemFence : 0u);
   for (int i = 0; i < slots; ++i) {
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
-    ck(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming), "hipEventCreate");
+    ck(hipEventCreateWithFlags(&done_[i], done_flags), "hipEventCreate");
   }
 }
 

@@ -532,6 +532,57 @@ def dot_interaction_gather(dense: torch.Tensor, table: torch.Tensor, ids, modulo
     return dot_interaction(dense, table[rows], out_cols)
 
 
+def dot_interaction_gather_peer(dense: torch.Tensor, ids, peer, cache=None, out_cols: int = 0,
+                                id_col0: int = 0) -> torch.Tensor:
+    """K1 + K5 through the peer lookup (parallel/hot_cache.py): table t's row
+    of candidate b is read where it lives - this rank's store, the owner's
+    store over xGMI, or this rank's replica cache of hot remote rows. ``ids``:
+    int32/int64 [B, >= id_col0 + T] rows or :class:`ArenaRows`."""
+    T = peer.T
+    if out_cols <= 0:
+        out_cols = interaction_cols(T, dense.shape[1])
+    kw = cache.kernel_args() if cache is not None else {}
+    if dense.is_cuda:
+        if isinstance(ids, ArenaRows):
+            return hip().dot_interaction_gather_peer(dense, None, ids.arena, int(id_col0), peer.tbase, peer.trows,
+                                                     peer.tremote, out_cols=int(out_cols), **kw)
+        return hip().dot_interaction_gather_peer(dense, _rows(ids), None, int(id_col0), peer.tbase, peer.trows,
+                                                 peer.tremote, out_cols=int(out_cols), **kw)
+    from ..parallel.hot_cache import peer_gather_cpu
+
+    if isinstance(ids, ArenaRows):
+        ids = _arena_unpack_host(ids)[0]
+    emb = peer_gather_cpu(peer, cache, ids[:, id_col0:id_col0 + T], None, 1)
+    return dot_interaction(dense, emb, out_cols)
+
+
+def peer_bag(ids, wts: Optional[torch.Tensor], B: int, col0: int, hot: int, peer, cache=None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K1b through the peer lookup: bf16 [B, T, 64] pooled bags (table t's bag =
+    columns col0 + t * hot .. + hot - 1 of ``ids`` / ``wts``, or of the
+    :class:`ArenaRows`)."""
+    T = peer.T
+    dev = peer.trows.device
+    if out is None:
+        out = torch.empty(B, T, 64, dtype=peer.stores[peer.rank].dtype, device=dev)
+    kw = cache.kernel_args() if cache is not None else {}
+    if dev.type == "cuda":
+        if isinstance(ids, ArenaRows):
+            hip().peer_bag(None, None, ids.arena, int(B), int(col0), int(hot), peer.tbase, peer.trows, peer.tremote,
+                           out=out, **kw)
+        else:
+            hip().peer_bag(_rows(ids), _rows(wts.float()), None, int(B), int(col0), int(hot), peer.tbase, peer.trows,
+                           peer.tremote, out=out, **kw)
+        return out
+    from ..parallel.hot_cache import peer_gather_cpu
+
+    if isinstance(ids, ArenaRows):
+        ids, wts = _arena_unpack_host(ids)
+    n = T * hot
+    out.copy_(peer_gather_cpu(peer, cache, ids[:, col0:col0 + n], wts[:, col0:col0 + n], hot).view_as(out))
+    return out
+
+
 BOTTOM_MLP3_DIMS = (512, 256, 64)  # the fused DLRM bottom-MLP kernel's layer widths
 
 

@@ -21,6 +21,11 @@ parallelism (collective C3):
     rank owns each row, so the bf16 sum is exact.
   Every message has a fixed shape for a given batch size (no count exchange),
   so the step stays HIP-graph capturable on RCCL.
+  - peer (``ModelConfig.embedding_exchange = "peer"``, table-wise): no
+    exchange at all - each rank maps its peers' stores (IPC) and the lookup
+    loads every row where it lives over xGMI, hot remote rows from a per-rank
+    replica cache refreshed from online counts (parallel/hot_cache.py); the
+    bytes crossing xGMI are the cache misses x 128.
 * **`ShardedDLRM`**: the DLRM forward with sharded tables; dense towers are
   replicated and run data-parallel over each rank's candidates.
 
@@ -32,6 +37,7 @@ per direction instead of one per table.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -43,6 +49,7 @@ from .. import ops as ops_k
 from ..config import ModelConfig
 from ..models.ctr import DLRM
 from ..models.layers import DTYPES, hashed_uniform_rows_
+from . import hot_cache
 from . import step_program as sp
 from .dist import DistContext, split_rows
 
@@ -181,10 +188,14 @@ class ShardedEmbedding(nn.Module):
     step is capturable and replayed by the native StepRunner."""
 
     def __init__(self, plan: ShardingPlan, ctx: DistContext, seed: int, bound: float, dtype=torch.bfloat16,
-                 device="cpu", group=None, col_base: int = 0, hot: int = 1):
+                 device="cpu", group=None, col_base: int = 0, hot: int = 1, exchange: str = "alltoall",
+                 cache_rows: int = 0, cache_sample_every: int = 8):
         super().__init__()
         self.plan, self.ctx, self.group = plan, ctx, group
         self.world, self.rank = plan.world, ctx.rank if plan.world > 1 else 0
+        if exchange not in ("alltoall", "peer"):
+            raise ValueError(f"unknown embedding exchange {exchange!r}")
+        self.exchange = exchange
         self.col_base = int(col_base)
         # multi-hot: table t's ids are columns col_base + t * hot .. + hot - 1,
         # pooled (weighted sum) on the owner by the K1b bag kernel
@@ -218,11 +229,36 @@ class ShardedEmbedding(nn.Module):
 
         lay = [layout(r) for r in range(self.world)]
         self.rows_local, my_off, self.segments = lay[self.rank]  # segments: (table, global lo, rows, local offset)
-        store = torch.empty(max(1, self.rows_local), self.D, dtype=dtype, device=dev)
+        peer = exchange == "peer" and self.world > 1
+        if peer and self.rw:
+            raise ValueError("the peer exchange shards table-wise (plan the tables with policy='table')")
+        shm_tag = None
+        if peer and dev.type == "cpu":  # peers map this rank's store from a shared-memory file
+            import uuid
+
+            tok: list = [None] * self.world
+            dist.all_gather_object(tok, uuid.uuid4().hex[:12], group=group)
+            shm_tag = f"/dev/shm/dtfs_peer_{tok[0]}_{self.rank}"
+            store = hot_cache.shm_store(self.rows_local, dtype, shm_tag)
+        else:
+            store = torch.empty(max(1, self.rows_local), self.D, dtype=dtype, device=dev)
         for t, s, n, o in self.segments:
             if n:
                 hashed_uniform_rows_(store[o:o + n], t, s, seed, bound)
         self.store = nn.Parameter(store, requires_grad=False)
+        # peer exchange: every rank's store mapped here, each table's rows read
+        # where they live, hot remote rows from this rank's replica cache
+        self.peer: Optional[hot_cache.PeerTables] = None
+        self.cache: Optional[hot_cache.HotRowCache] = None
+        if exchange == "peer":
+            stores = hot_cache.open_peer_stores(self.store.data, group, shm_tag) if peer else [self.store.data]
+            if shm_tag is not None:
+                os.unlink(shm_tag)  # every rank has it mapped (open_peer_stores ends in a barrier)
+            owner = [next(r for r in range(self.world) if t in self.tw_by_rank[r]) for t in range(T)]
+            self.peer = hot_cache.PeerTables(stores, owner, [lay[owner[t]][1][t] for t in range(T)],
+                                             [plan.tables[t].rows for t in range(T)], self.rank)
+            if peer and cache_rows > 0 and self.peer.remote_tables:
+                self.cache = hot_cache.HotRowCache(self.peer, cache_rows, sample_every=cache_sample_every)
         i64 = dict(dtype=torch.int64, device=dev)
         # table-wise route: slot (s, j) <- table tw_by_rank[s][j] (pad: column 0, row 0 of s)
         cols, mods, offs = [], [], []
@@ -288,11 +324,15 @@ class ShardedEmbedding(nn.Module):
 
     def exchange_bytes(self, B: int) -> int:
         """Bytes this rank sends to OTHER ranks per step (ids + weights out,
-        embeddings back): what crosses xGMI."""
+        embeddings back): what crosses xGMI. Peer exchange: the rows this
+        rank loads from peers with no replica cache (every remote lookup);
+        the cache's counters give the measured bytes (misses x 128)."""
         W, tm, D, Tr, hot = self.world, self.tmax, self.D, len(self.rw), self.hot
         if W == 1:
             return 0
         eb = self.store.element_size()
+        if self.peer is not None:
+            return B * self.peer.remote_tables * hot * D * eb
         n = 0
         if self.tw_tables:
             n += (W - 1) * B * tm * hot * (4 + (4 if hot > 1 else 0))  # ids (+ weights) to the owners
@@ -365,9 +405,12 @@ class ShardedEmbedding(nn.Module):
         return ops
 
     def forward(self, ids: torch.Tensor, wts: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Eager exchange (collective): ids [B, F] (tables at columns
-        col_base..) -> [B, T, D]."""
+        """Eager exchange (collective unless peer): ids [B, F] (tables at
+        columns col_base..) -> [B, T, D]."""
         B = ids.shape[0]
+        if self.peer is not None:
+            w = wts.float() if wts is not None else torch.ones(ids.shape, dtype=torch.float32, device=ids.device)
+            return ops_k.peer_bag(ids, w, B, self.col_base, self.hot, self.peer, self.cache)
         bufs = self.alloc(B)
         w = None if wts is None else wts.float().contiguous()
         sp.run_eager(self.program(ids.contiguous(), B, bufs, w), self.group)
@@ -408,13 +451,17 @@ class ShardedDLRM(nn.Module):
         self.cfg, self.ctx, self.group = cfg, ctx, group
         self.hot = max(1, int(getattr(cfg, "multi_hot", 1)))
         world = ctx.world if ctx.is_distributed else 1
-        if self.hot > 1 and policy == "auto":
-            policy = "table"  # multi-hot bags pool on their table's owner
+        exchange = getattr(cfg, "embedding_exchange", "alltoall")
+        if (self.hot > 1 or exchange == "peer") and policy == "auto":
+            # multi-hot bags pool on their table's owner; peers read whole
+            # tables where they live
+            policy = "table"
         self.plan = plan or plan_sharding(dlrm_tables(cfg), world, budget_bytes, policy)
         self.dense = DLRM(cfg, device=device, materialize_tables=False)
         self.dense.gen = None
         self.emb = ShardedEmbedding(self.plan, ctx, cfg.seed, self.dense.table_bound, DTYPES[cfg.param_dtype],
-                                    device, group, col_base=cfg.num_dense, hot=self.hot)
+                                    device, group, col_base=cfg.num_dense, hot=self.hot, exchange=exchange,
+                                    cache_rows=int(getattr(cfg, "hot_cache_rows", 0)))
         self.device_ = torch.device(device)
 
     def signature(self):
@@ -424,7 +471,29 @@ class ShardedDLRM(nn.Module):
         return self.dense.param_bytes() + self.emb.local_bytes()
 
     def alloc(self, B: int) -> Dict[str, torch.Tensor]:
+        if self._peer_step():
+            e = self.emb
+            return {"emb_all": torch.zeros(B * e.T, e.D, dtype=e.store.dtype, device=e.store.device)} if self.hot > 1 \
+                else {}
         return self.emb.alloc(B)
+
+    def _peer_step(self) -> bool:
+        """The step reads every table where it lives (peer exchange, > 1 rank)."""
+        return self.emb.peer is not None and self.emb.world > 1
+
+    # -- hot-row replica cache (peer exchange) ---------------------------------
+    @property
+    def cache(self) -> Optional[hot_cache.HotRowCache]:
+        return self.emb.cache
+
+    def start_cache(self, interval_s: float = 1.0) -> None:
+        """Refresh the replica cache from its online counts every interval_s."""
+        if self.emb.cache is not None:
+            self.emb.cache.start(interval_s)
+
+    def stop_cache(self) -> None:
+        if self.emb.cache is not None:
+            self.emb.cache.stop()
 
     def narrow_weight_cols(self) -> int:
         """One-hot: only the dense features' weights are read (the request
@@ -449,6 +518,25 @@ class ShardedDLRM(nn.Module):
         d = self.dense
         st = {} if state is None else state
         arena = isinstance(ids, ops_k.ArenaRows)
+        if self._peer_step():
+            # peer exchange: no collective - the lookup loads each row from its
+            # owner's HBM over xGMI (or this rank's replica cache), fused into
+            # the interaction for one-hot tables, a pooled bag pass for multi-hot
+            e, col0 = self.emb, self.cfg.num_dense
+            bag_w = None if (arena or self.hot == 1) else (wts if wts.dtype == torch.float32 else wts.float())
+
+            def peer_step():
+                dense_out = d.bottom_out(ids if arena else (wts if wts.dtype == torch.float32 else wts.float()))
+                if self.hot == 1:
+                    z = ops_k.dot_interaction_gather_peer(dense_out, ids, e.peer, e.cache, d.inter_cols, id_col0=col0)
+                else:
+                    emb = ops_k.peer_bag(ids, bag_w, B, col0, self.hot, e.peer, e.cache,
+                                         out=bufs["emb_all"].view(B, e.T, e.D))
+                    z = ops_k.dot_interaction(dense_out, emb, d.inter_cols)
+                st["scores"] = d.top.forward_head(z, d.head_w, d.head_b, out=out)
+
+            return [sp.Sync("record", sp.AUX, 0), sp.Sync("wait", sp.COMPUTE, 0),
+                    sp.Kernels(sp.COMPUTE, peer_step, "step")]
         fused = self._local_fused(ids)
         if fused is not None:
             # one rank, one-hot, table-wise: the exchange is the identity, so
@@ -511,7 +599,8 @@ class ShardedDLRM(nn.Module):
 
     @property
     def has_collectives(self) -> bool:
-        """The forward issues collectives (the engine runs it as a step program)."""
-        return self.plan.world > 1
+        """The forward issues collectives (every rank must run every step);
+        the peer exchange has none: each rank's steps are its own."""
+        return self.plan.world > 1 and not self._peer_step()
 
     supports_program = True

@@ -1,0 +1,352 @@
+"""Peer lookup and the hot-row replica cache for table-wise sharded embeddings.
+
+SURVEY §2.4 K1b / §2.5 C3 asks for embedding model parallelism over 8 GPUs;
+the reference has no sharded embeddings at all (its TF-Serving shards each run
+a full replica, reference ``README.md``). The exchange mode of
+:class:`~.embedding_sharding.ShardedEmbedding` built here is MI355X-first:
+
+* **Peer lookup** (``exchange="peer"``). The 8 GPUs of a node are fully
+  connected by xGMI and every GPU can load from a peer's HBM. Each rank
+  exports its table store once (IPC handle; on the CPU a shared-memory file),
+  maps every peer's store, and the step's lookup kernel reads each candidate's
+  row *where it lives*: no ids all-to-all, no lookup pass on the owner, no rows
+  all-to-all, and no collective coupling the ranks' steps. The one-hot step is
+  the same single fused kernel as one rank's (``dot_interact_gather_kernel``
+  with the peer lookup on, csrc/kernels/interaction.hip); multi-hot bags pool
+  through ``peer_bag_kernel`` (csrc/kernels/peer_lookup.hip).
+* **Hot-row replica cache** (:class:`HotRowCache`). Most lookups of a skewed
+  (Zipf) id stream hit a small set of rows. Each rank keeps copies of the hot
+  rows of tables owned by OTHER ranks in HBM left over after its shard
+  (288 GB per GPU), behind an open-addressing index; the lookup probes it
+  first and goes over xGMI only on a miss, so the bytes crossing xGMI per step
+  are ``misses x 128``. The hot set comes from online counts: the kernel pushes
+  the remote keys of every ``sample_every``-th candidate into a ring, and
+  :meth:`HotRowCache.refresh` (a background thread in serving, or called
+  between steps) folds the ring into exponentially decayed counts, picks the
+  top rows, copies the new ones from their owners into free slots and swaps
+  in a freshly built index - never touching a slot or an index that a step in
+  flight may read.
+
+Keys are ``(t << 40) | row``. Counters: ``stats`` int64 [128] (hits at even,
+misses at odd entries, summed by :meth:`HotRowCache.counts`).
+"""
+from __future__ import annotations
+
+import threading
+from contextlib import nullcontext
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+KEY_SHIFT = 40
+ROW_MASK = (1 << KEY_SHIFT) - 1
+D = 64
+
+
+def _next_pow2(n: int) -> int:
+    p = 2
+    while p < n:
+        p <<= 1
+    return p
+
+
+class PeerTables:
+    """Where each table's rows live, seen from this rank: table t is rows
+    ``off[t] .. off[t] + rows[t]`` of ``stores[owner[t]]`` - this rank's own
+    store, a peer's store mapped by IPC (GPU) or a peer's shared-memory file
+    (CPU). ``tbase`` (GPU): the device address of each table's row 0."""
+
+    def __init__(self, stores: Sequence[torch.Tensor], owner: Sequence[int], off: Sequence[int],
+                 rows: Sequence[int], rank: int):
+        self.stores = list(stores)
+        self.owner, self.off, self.rows, self.rank = list(owner), list(off), list(rows), int(rank)
+        self.T = len(self.owner)
+        dev = self.stores[self.rank].device
+        for t in range(self.T):
+            s = self.stores[self.owner[t]]
+            if s.dim() != 2 or s.shape[1] != D or not s.is_contiguous():
+                raise ValueError("peer stores must be contiguous [rows, 64]")
+            if self.off[t] < 0 or self.off[t] + self.rows[t] > s.shape[0]:
+                raise ValueError(f"table {t}: rows {self.off[t]}..{self.off[t] + self.rows[t]} outside its owner's "
+                                 f"store ({s.shape[0]} rows)")
+        self.trows = torch.tensor(self.rows, dtype=torch.int64, device=dev)
+        self.tremote = torch.tensor([int(o != self.rank) for o in self.owner], dtype=torch.int32, device=dev)
+        self.tbase = None
+        if dev.type == "cuda":
+            self.tbase = torch.tensor([self.stores[o].data_ptr() + self.off[t] * D * self.stores[o].element_size()
+                                       for t, o in enumerate(self.owner)], dtype=torch.int64, device=dev)
+        self._owner_cpu = torch.tensor(self.owner, dtype=torch.int64)
+        self._off_cpu = torch.tensor(self.off, dtype=torch.int64)
+        self.trows_cpu = torch.tensor(self.rows, dtype=torch.int64)
+        self.tremote_cpu = self.tremote.cpu().bool()
+
+    @property
+    def remote_tables(self) -> int:
+        return int(self.tremote_cpu.sum())
+
+    def row_cpu(self, t: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+        """Rows v of tables t (int64 [n] each) read from their owners' stores."""
+        out = torch.empty(t.numel(), D, dtype=self.stores[self.rank].dtype)
+        own = self._owner_cpu[t]
+        for r in torch.unique(own).tolist():
+            m = own == r
+            out[m] = self.stores[r][self._off_cpu[t[m]] + v[m]]
+        return out
+
+
+class HotRowCache:
+    """This rank's replica of hot rows of tables owned by other ranks.
+
+    ``capacity`` rows ([capacity, 64] bf16) behind two open-addressing index
+    buffers (keys int64 [H] | slots int32 [H], H = the power of two >= 2 x
+    capacity): one serves the steps while :meth:`refresh` rebuilds the other.
+    ``desc`` (int64 [5], read by the kernels at their start) = {active index,
+    0, H - 1, rows, capacity}: a refresh changes only its first word (one
+    8-byte store), so a kernel sees the old index or the new one, whole.
+
+    Slot safety: :meth:`refresh` first waits for the device (every step that
+    could still read the index replaced by the previous refresh is done); the
+    rows it adds go only into slots the CURRENT index does not reference, and
+    it keeps at most ``fill`` x capacity rows hot so there are free slots for
+    the next turnover."""
+
+    def __init__(self, peer: PeerTables, capacity: int, ring_cap: int = 1 << 20, sample_every: int = 8,
+                 decay: float = 0.5, fill: float = 0.75):
+        self.peer = peer
+        self.cap = max(1, int(capacity))
+        self.H = _next_pow2(2 * self.cap)
+        self.sample_every, self.decay, self.fill = int(sample_every), float(decay), float(fill)
+        dev = peer.trows.device
+        self.device = dev
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.rows = torch.zeros(self.cap, D, dtype=peer.stores[peer.rank].dtype, device=dev)
+        self.index = [torch.full((self.H + self.H // 2,), -1, **i64) for _ in range(2)]
+        self.desc = torch.tensor([0, 0, self.H - 1, self.rows.data_ptr() if dev.type == "cuda" else 0, self.cap], **i64)
+        self.stats = torch.zeros(128, **i64)
+        self.ring = torch.full((max(1, int(ring_cap)),), -1, **i64)
+        self.ring_ctr = torch.zeros(1, **i64)
+        self.keys = torch.empty(0, **i64)          # the active hot set, sorted
+        self.slots = torch.empty(0, dtype=torch.int32, device=dev)
+        self.cand_keys = torch.empty(0, **i64)     # candidates with decayed counts
+        self.cand_score = torch.empty(0, dtype=torch.float32, device=dev)
+        self.active = -1
+        self.refreshes = 0
+        self.last_filled = 0
+        self._stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._lock = threading.Lock()
+        self._thread: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+
+    # -- kernel arguments -------------------------------------------------------
+    def kernel_args(self) -> dict:
+        return dict(cache=self.desc, stats=self.stats, ring=self.ring, ring_ctr=self.ring_ctr,
+                    sample_every=self.sample_every)
+
+    def index_views(self, side: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        buf = self.index[side]
+        return buf[:self.H], buf[self.H:].view(torch.int32)
+
+    # -- counters ---------------------------------------------------------------
+    def counts(self) -> Tuple[int, int]:
+        """(hits, misses) of remote lookups since the last reset."""
+        s = self.stats.view(64, 2).sum(0).cpu()
+        return int(s[0]), int(s[1])
+
+    def hit_rate(self) -> float:
+        h, m = self.counts()
+        return h / (h + m) if h + m else 0.0
+
+    def reset_counts(self) -> None:
+        self.stats.zero_()
+
+    # -- CPU reference of the kernels' cache side ---------------------------------
+    def lookup_cpu(self, keys: torch.Tensor) -> torch.Tensor:
+        """Slot of each key in the active set, -1 if absent."""
+        k = self.keys.cpu()
+        if k.numel() == 0:
+            return torch.full_like(keys, -1, dtype=torch.int64)
+        pos = torch.searchsorted(k, keys).clamp(max=k.numel() - 1)
+        found = k[pos] == keys
+        return torch.where(found, self.slots.cpu().long()[pos], torch.full_like(pos, -1))
+
+    def count_cpu(self, hits: int, misses: int) -> None:
+        self.stats[0] += hits
+        self.stats[1] += misses
+
+    def push_cpu(self, keys: torch.Tensor) -> None:
+        n = keys.numel()
+        if n == 0:
+            return
+        cap = self.ring.numel()
+        base = int(self.ring_ctr[0])
+        pos = (torch.arange(n, dtype=torch.int64) + base) % cap
+        self.ring[pos] = keys
+        self.ring_ctr[0] = base + n
+
+    # -- refresh ----------------------------------------------------------------
+    @torch.no_grad()
+    def refresh(self) -> int:
+        """Fold the sampled keys into the counts and install the new hot set.
+        Returns the number of rows copied in. Safe while steps run."""
+        with self._lock:
+            return self._refresh()
+
+    def _refresh(self) -> int:
+        cuda = self.device.type == "cuda"
+        if cuda:  # every step that may read the previously replaced index is done
+            torch.cuda.synchronize(self.device)
+        with (torch.cuda.stream(self._stream) if cuda else nullcontext()):
+            n = int(self.ring_ctr.item())
+            samp = self.ring[:min(n, self.ring.numel())].clone()
+            self.ring_ctr.zero_()
+            samp = samp[samp >= 0]
+            if samp.numel():
+                k, c = torch.unique(samp, return_counts=True)
+                keys = torch.cat([self.cand_keys, k])
+                score = torch.cat([self.cand_score * self.decay, c.float()])
+                uk, inv = torch.unique(keys, return_inverse=True)
+                s = torch.zeros(uk.numel(), dtype=torch.float32, device=self.device).scatter_add_(0, inv, score)
+                top = torch.topk(s, min(uk.numel(), 4 * self.cap)).indices  # sorted by score
+                self.cand_keys, self.cand_score = uk[top], s[top]
+            target = min(self.cand_keys.numel(), max(1, int(self.fill * self.cap)))
+            hot = self.cand_keys[:target]
+            kept = torch.isin(self.keys, hot)
+            kept_keys, kept_slots = self.keys[kept], self.slots[kept]
+            new = hot[~torch.isin(hot, self.keys)]  # hottest first
+            used = torch.zeros(self.cap, dtype=torch.bool, device=self.device)
+            if self.slots.numel():
+                used[self.slots.long()] = True  # referenced by the active index: not writable now
+            free = (~used).nonzero().view(-1)
+            new = new[:free.numel()]
+            new_slots = free[:new.numel()].to(torch.int32)
+            if new.numel():
+                self._fill(new, new_slots)
+            keys = torch.cat([kept_keys, new])
+            slots = torch.cat([kept_slots, new_slots])
+            order = torch.argsort(keys)
+            keys, slots = keys[order].contiguous(), slots[order].contiguous()
+            side = 0 if self.active != 0 else 1
+            if cuda:
+                ik, isl = self.index_views(side)
+                ik.fill_(-1)
+                if keys.numel():
+                    from ..ops import hip
+
+                    hip().cache_index_build(keys, slots, ik, isl)
+                self.desc[0:1].fill_(self.index[side].data_ptr())  # one 8-byte store: the swap
+        if cuda:
+            self._stream.synchronize()
+        self.keys, self.slots = keys, slots
+        self.active = side
+        self.refreshes += 1
+        self.last_filled = int(new.numel())
+        return self.last_filled
+
+    def _fill(self, keys: torch.Tensor, slots: torch.Tensor) -> None:
+        p = self.peer
+        if self.device.type == "cuda":
+            from ..ops import hip
+
+            hip().peer_cache_fill(keys, slots, p.tbase, p.trows, self.rows)
+        else:
+            t, v = keys >> KEY_SHIFT, keys & ROW_MASK
+            self.rows[slots.long()] = p.row_cpu(t, v)
+
+    # -- background refresh (serving) ---------------------------------------------
+    def start(self, interval_s: float = 1.0) -> None:
+        """Refresh every ``interval_s`` seconds on a daemon thread."""
+        if self._thread is not None:
+            return
+        self._stop.clear()
+
+        def loop():
+            while not self._stop.wait(interval_s):
+                try:
+                    self.refresh()
+                except Exception as e:  # the cache is an optimisation: keep serving
+                    print(f"[hot_cache] refresh failed: {e!r}", flush=True)
+                    return
+
+        self._thread = threading.Thread(target=loop, name="dtfs-hot-cache", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    def describe(self) -> dict:
+        h, m = self.counts()
+        return {"capacity_rows": self.cap, "hot_rows": int(self.keys.numel()), "refreshes": self.refreshes,
+                "hits": h, "misses": m, "hit_rate": round(h / (h + m), 4) if h + m else None}
+
+
+def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.Tensor, wts: Optional[torch.Tensor],
+                    hot: int) -> torch.Tensor:
+    """CPU reference of the peer lookup (kernels/peer_lookup.h): ids [B, T *
+    hot] (table t's bag = columns t * hot .. + hot - 1), wts the same shape for
+    bags (None: one-hot) -> bf16 [B, T, 64]; counts and samples like the kernels."""
+    B, T = ids.shape[0], peer.T
+    t = torch.arange(T, dtype=torch.int64).repeat_interleave(hot).view(1, -1).expand(B, -1).reshape(-1)
+    v = torch.remainder(ids.long().reshape(-1), peer.trows_cpu[t])
+    rows = peer.row_cpu(t, v).float()
+    if cache is not None:
+        remote = peer.tremote_cpu[t]
+        keys = (t << KEY_SHIFT) | v
+        slot = cache.lookup_cpu(keys)
+        hit = remote & (slot >= 0)
+        if bool(hit.any()):
+            rows[hit] = cache.rows.cpu()[slot[hit]].float()
+        cache.count_cpu(int(hit.sum()), int((remote & ~hit).sum()))
+        if cache.sample_every > 0:
+            b = torch.arange(B, dtype=torch.int64).repeat_interleave(T * hot)
+            cache.push_cpu(keys[remote & (b % cache.sample_every == 0)])
+    if wts is None:
+        out = rows.view(B, T, D)
+    else:
+        out = (rows.view(B, T, hot, D) * wts.float().reshape(B, T, hot, 1)).sum(2)
+    return out.to(peer.stores[peer.rank].dtype)
+
+
+def open_peer_stores(store: torch.Tensor, group=None, shm_tag: Optional[str] = None) -> List[torch.Tensor]:
+    """Every rank's store as seen from this rank (collective). GPU: IPC
+    handles (+ the store's offset in its allocation) exchanged with
+    all_gather_object, each peer's store mapped for loads over xGMI. CPU:
+    ``store`` is a shared-memory file mapping made by :func:`shm_store` and
+    ``shm_tag`` its path."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if world == 1:
+        return [store]
+    if store.is_cuda:
+        from ..ops import hip
+
+        h, off = hip().ipc_export(store)
+        mine = (h, int(off), list(store.shape))
+    else:
+        if shm_tag is None:
+            raise ValueError("CPU peer stores need their shared-memory tag")
+        mine = (shm_tag, 0, list(store.shape))
+    allv: list = [None] * world
+    dist.all_gather_object(allv, mine, group=group)
+    out: List[torch.Tensor] = []
+    for r, (h, off, shape) in enumerate(allv):
+        if r == rank:
+            out.append(store)
+        elif store.is_cuda:
+            from ..ops import hip
+
+            out.append(hip().ipc_open(h, off, shape, store))
+        else:
+            n = int(shape[0]) * int(shape[1])
+            out.append(torch.from_file(h, shared=True, size=n, dtype=store.dtype).view(*shape))
+    dist.barrier(group=group)  # every rank has mapped every file: the names can go
+    return out
+
+
+def shm_store(rows: int, dtype, tag: str) -> torch.Tensor:
+    """A [rows, 64] CPU tensor in a shared-memory file other ranks can map."""
+    return torch.from_file(tag, shared=True, size=max(1, rows) * D, dtype=dtype).view(max(1, rows), D)

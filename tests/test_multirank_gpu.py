@@ -87,6 +87,55 @@ def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
     assert ("one-shot peer exchange" in par) == (peer > 0), par
 
 
+@pytest.mark.parametrize("n,hot", [(2, 1), (3, 1), (2, 3)])
+def test_peer_exchange_ranks_sharing_one_gpu(n, hot):
+    """Peer exchange (parallel/hot_cache.py) on N ranks: every rank maps the
+    others' table stores by IPC and its lookups load remote rows directly (the
+    8-GPU node does the same over xGMI); scores match the unsharded DLRM of the
+    same seed through the eager forward and the arena step program, before
+    and after the hot-row replica cache fills, and cached rows are hit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "tools.studies.peer_lookup_check",
+           "--hot", str(hot)]
+    env = dict(os.environ, DTFS_SHARE_GPU="1")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    ranks = json.loads(line[0])["ranks"]
+    assert len(ranks) == n
+    tol = 1e-6 if hot == 1 else 2e-3  # one-hot: the same fused kernel as the local model
+    for r in ranks:
+        assert r["remote_tables"] > 0
+        for rnd in r["rounds"]:
+            assert rnd["max_abs_diff"] <= tol and rnd["max_abs_diff_arena_program"] <= tol, r["rounds"]
+        assert r["rounds"][0]["hits"] == 0 and r["rounds"][-1]["hits"] > 0, r["rounds"]
+
+
+def test_bench_sharded_dlrm_peer_exchange_ranks_sharing_one_gpu():
+    """bench.py --exchange peer on 2 ranks: no collective in the step (the
+    ranks' live servers run independently), the replica cache installed
+    before the clock, hit rate and xGMI bytes in the JSON."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--model", "dlrm", "--table-rows", "1000000", "--steps", "20", "--warmup", "4", "--prime-steps", "10",
+           "--requests-per-gpu", "4", "--request-rows", "96", "--pool", "8", "--client-threads", "2",
+           "--qps", "0", "--step-timeout-s", "20", "--exchange", "peer", "--hot-cache-rows", "65536"]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    out = json.loads(line[-1])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    assert "xGMI" in out["config"]["parallelism"], out["config"]["parallelism"]
+    c = out["embedding_exchange"]["hot_row_cache"]
+    assert c["hit_rate"] > 0.2 and c["xgmi_bytes_per_step_per_rank"] < out["embedding_exchange"]["bytes_per_step_per_rank"]
+
+
 @pytest.mark.parametrize("n,mode", [(2, "scatter"), (3, "alltoall")])
 def test_native_cluster_server_ranks_sharing_one_gpu(tmp_path, n, mode):
     """serving/cluster.py on N ranks over RCCL: every front door's concurrent
