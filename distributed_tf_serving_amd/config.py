@@ -77,6 +77,7 @@ class ServingConfig:
     output_key: str = "prediction_node"
     max_batch_rows: int = 8192        # dynamic batcher: rows per GPU batch
     batch_timeout_us: int = 200       # oldest request waits at most this long
+    hot_cache_refresh_s: float = 1.0  # peer-exchange DLRM: replica cache refresh period
     max_queued_rows: int = 1 << 22    # backpressure bound (rows)
     max_request_rows: int = 1 << 18   # one request's candidates (checked before any allocation)
     allowed_batch_sizes: Tuple[int, ...] = (512, 1024, 2048, 4096, 8192)  # padding buckets (HIP graphs)

@@ -67,7 +67,11 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
     sc = cfg.serving
     dev = torch.device(device) if device is not None else (ctx.device if ctx is not None else pick_device(sc.device))
     ctx = ctx or DistContext(device=dev)
-    if model is None or getattr(model, "has_collectives", False):  # sharded tables re-shard over the new world
+    sharded = getattr(getattr(model, "plan", None), "world", 1) > 1
+    if model is None or sharded or getattr(model, "has_collectives", False):
+        # sharded tables re-shard over the new world
+        if model is not None and hasattr(model, "stop_cache"):
+            model.stop_cache()
         model = build_parallel_model(cfg.model, dev, ctx, group=group)
     world = ctx.world if ctx.is_distributed else 1
     buckets = sorted(set(sc.allowed_batch_sizes) | {sc.max_batch_rows})
@@ -96,6 +100,8 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
         eng = FanoutEngine(ex, ctx, mode=mode, group=group)
     for B in buckets:
         eng.prepare(B)
+    if hasattr(model, "start_cache"):  # peer exchange: keep the hot-row replica current
+        model.start_cache(getattr(sc, "hot_cache_refresh_s", 1.0))
     return eng
 
 
