@@ -796,25 +796,37 @@ torch::Tensor shard_route(c10::optional<torch::Tensor> ids, c10::optional<torch:
 }
 
 // ---------------------------------------------------------------- peer lookup
-// tbase int64 [T] (device addresses), trows int64 [T], tremote int32 [T],
-// cache int64 [5], stats int64 [128], ring int64 [cap], ring_ctr int64 [1]
-static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Tensor& tbase, const torch::Tensor& trows,
-                                      const torch::Tensor& tremote, const c10::optional<torch::Tensor>& cache,
+// PeerTables (parallel/hot_cache.py): cbase int64 [W * max_chunks] (device
+// addresses of every rank's store chunks), towner int32 [T], toff int64 [T],
+// trows int64 [T], tremote int32 [T]; the replica cache: cache int64 [5],
+// stats int64 [128], ring int64 [cap], ring_ctr int64 [1]
+static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Tensor& cbase,
+                                      const torch::Tensor& towner, const torch::Tensor& toff,
+                                      const torch::Tensor& trows, const torch::Tensor& tremote, int64_t chunk_shift,
+                                      const c10::optional<torch::Tensor>& cache,
                                       const c10::optional<torch::Tensor>& stats,
                                       const c10::optional<torch::Tensor>& ring,
                                       const c10::optional<torch::Tensor>& ring_ctr, int64_t sample_every) {
-  const int64_t T = tbase.numel();
-  for (auto* t : {&tbase, &trows}) {
+  const int64_t T = trows.numel();
+  for (auto* t : {&cbase, &toff, &trows}) {
     check_same_dev(ref, *t, "peer table map");
-    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == T && t->is_contiguous(), "tbase / trows: int64 [T]");
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->is_contiguous(), "cbase / toff / trows: contiguous int64");
   }
-  check_same_dev(ref, tremote, "tremote");
-  TORCH_CHECK(tremote.scalar_type() == torch::kInt32 && tremote.numel() == T && tremote.is_contiguous(),
-              "tremote: int32 [T]");
+  for (auto* t : {&towner, &tremote}) {
+    check_same_dev(ref, *t, "peer table map");
+    TORCH_CHECK(t->scalar_type() == torch::kInt32 && t->numel() == T && t->is_contiguous(), "towner / tremote: int32 [T]");
+  }
+  TORCH_CHECK(toff.numel() == T && cbase.numel() >= 1, "toff: int64 [T], cbase: int64 [W * max_chunks]");
+  TORCH_CHECK(chunk_shift >= 1 && chunk_shift <= 40, "chunk_shift in [1, 40]");
   dtfs::PeerLookupArgs p;
-  p.tbase = tbase.data_ptr<int64_t>();
+  p.cbase = cbase.data_ptr<int64_t>();
+  p.towner = towner.data_ptr<int32_t>();
+  p.toff = toff.data_ptr<int64_t>();
   p.trows = trows.data_ptr<int64_t>();
   p.tremote = tremote.data_ptr<int32_t>();
+  p.chunk_shift = int(chunk_shift);
+  p.max_chunks = int(cbase.size(-1));
+  TORCH_CHECK(cbase.dim() == 2, "cbase must be [W, max_chunks]");
   if (cache) {
     check_same_dev(ref, *cache, "cache");
     TORCH_CHECK(cache->scalar_type() == torch::kInt64 && cache->numel() == 5 && cache->is_contiguous(), "cache: int64 [5]");
@@ -843,8 +855,9 @@ static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Ten
 // K1 + K5 through the peer lookup: ids [B, >= id_col0 + T] int32/int64 rows,
 // or a device request arena (B rows)
 torch::Tensor dot_interaction_gather_peer(torch::Tensor dense, c10::optional<torch::Tensor> ids,
-                                          c10::optional<torch::Tensor> arena, int64_t id_col0, torch::Tensor tbase,
-                                          torch::Tensor trows, torch::Tensor tremote,
+                                          c10::optional<torch::Tensor> arena, int64_t id_col0, torch::Tensor cbase,
+                                          torch::Tensor towner, torch::Tensor toff, torch::Tensor trows,
+                                          torch::Tensor tremote, int64_t chunk_shift,
                                           c10::optional<torch::Tensor> cache, c10::optional<torch::Tensor> stats,
                                           c10::optional<torch::Tensor> ring, c10::optional<torch::Tensor> ring_ctr,
                                           int64_t sample_every, int64_t out_cols) {
@@ -853,7 +866,7 @@ torch::Tensor dot_interaction_gather_peer(torch::Tensor dense, c10::optional<tor
   TORCH_CHECK(dense.scalar_type() == torch::kBFloat16 && dense.dim() == 2 && dense.size(1) == 64 &&
                   dense.stride(1) == 1 && dense.stride(0) % 8 == 0,
               "dense must be bf16 [B, 64] with unit inner stride");
-  const int64_t B = dense.size(0), T = tbase.numel();
+  const int64_t B = dense.size(0), T = trows.numel();
   TORCH_CHECK(T >= 1 && T + 1 <= 32 && id_col0 >= 0, "1 <= T <= 31 tables, id_col0 >= 0");
   const void* idp = nullptr;
   bool ids64 = true;
@@ -870,7 +883,8 @@ torch::Tensor dot_interaction_gather_peer(torch::Tensor dense, c10::optional<tor
     check_same_dev(dense, *arena, "arena");
     TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous(), "arena must be a contiguous uint8 buffer");
   }
-  const auto p = peer_args(dense, tbase, trows, tremote, cache, stats, ring, ring_ctr, sample_every);
+  const auto p = peer_args(dense, cbase, towner, toff, trows, tremote, chunk_shift, cache, stats, ring, ring_ctr,
+                           sample_every);
   const int64_t used = 64 + (T + 1) * T / 2;
   if (out_cols <= 0) out_cols = (used + 7) / 8 * 8;
   TORCH_CHECK(out_cols >= used && out_cols % 8 == 0 && out_cols <= 1024, "out_cols: >= used, a multiple of 8, <= 1024");
@@ -886,12 +900,12 @@ torch::Tensor dot_interaction_gather_peer(torch::Tensor dense, c10::optional<tor
 
 // K1b through the peer lookup: pooled bags -> out bf16 [B, T, 64]
 void peer_bag(c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts, c10::optional<torch::Tensor> arena,
-              int64_t B, int64_t col0, int64_t hot, torch::Tensor tbase, torch::Tensor trows, torch::Tensor tremote,
-              c10::optional<torch::Tensor> cache, c10::optional<torch::Tensor> stats, c10::optional<torch::Tensor> ring,
+              int64_t B, int64_t col0, int64_t hot, torch::Tensor cbase, torch::Tensor towner, torch::Tensor toff,
+              torch::Tensor trows, torch::Tensor tremote, int64_t chunk_shift, c10::optional<torch::Tensor> cache, c10::optional<torch::Tensor> stats, c10::optional<torch::Tensor> ring,
               c10::optional<torch::Tensor> ring_ctr, int64_t sample_every, torch::Tensor out) {
   check_dev(out, "out");
   TORCH_CHECK(ids.has_value() != arena.has_value(), "peer_bag: ids (+ wts) or a device arena");
-  const int64_t T = tbase.numel();
+  const int64_t T = trows.numel();
   TORCH_CHECK(T >= 1 && hot >= 1 && col0 >= 0 && B >= 0, "T, hot >= 1, col0 >= 0");
   TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.is_contiguous() && out.numel() == B * T * 64,
               "out must be contiguous bf16 [B, T, 64]");
@@ -919,7 +933,8 @@ void peer_bag(c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts
     check_same_dev(out, *arena, "arena");
     TORCH_CHECK(arena->scalar_type() == torch::kUInt8 && arena->is_contiguous(), "arena must be a contiguous uint8 buffer");
   }
-  const auto p = peer_args(out, tbase, trows, tremote, cache, stats, ring, ring_ctr, sample_every);
+  const auto p = peer_args(out, cbase, towner, toff, trows, tremote, chunk_shift, cache, stats, ring, ring_ctr,
+                           sample_every);
   c10::DeviceGuard g(out.device());
   check_hip(dtfs::launch_peer_bag(p, idp, ids64, ldi, wp, ldw, arena ? arena->data_ptr() : nullptr, int(col0), int(T),
                                   int(hot), int(B), out.data_ptr(), cur_stream(out)),
@@ -927,22 +942,21 @@ void peer_bag(c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts
 }
 
 // replica cache maintenance (parallel/hot_cache.py)
-void peer_cache_fill(torch::Tensor keys, torch::Tensor slots, torch::Tensor tbase, torch::Tensor trows,
+void peer_cache_fill(torch::Tensor keys, torch::Tensor slots, torch::Tensor cbase, torch::Tensor towner,
+                     torch::Tensor toff, torch::Tensor trows, torch::Tensor tremote, int64_t chunk_shift,
                      torch::Tensor rows) {
   check_dev(rows, "rows");
-  for (auto* t : {&keys, &slots, &tbase, &trows}) check_same_dev(rows, *t, "cache fill input");
+  for (auto* t : {&keys, &slots}) check_same_dev(rows, *t, "cache fill input");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous() && slots.scalar_type() == torch::kInt32 &&
                   slots.is_contiguous() && slots.numel() == keys.numel(),
               "keys int64 [n], slots int32 [n]");
-  TORCH_CHECK(tbase.scalar_type() == torch::kInt64 && trows.scalar_type() == torch::kInt64 &&
-                  tbase.numel() == trows.numel() && tbase.is_contiguous() && trows.is_contiguous(),
-              "tbase / trows int64 [T]");
   TORCH_CHECK(rows.scalar_type() == torch::kBFloat16 && rows.dim() == 2 && rows.size(1) == 64 && rows.is_contiguous(),
               "rows must be contiguous bf16 [cap, 64]");
+  const auto p = peer_args(rows, cbase, towner, toff, trows, tremote, chunk_shift, c10::nullopt, c10::nullopt,
+                           c10::nullopt, c10::nullopt, 0);
   c10::DeviceGuard g(rows.device());
-  check_hip(dtfs::launch_peer_cache_fill(keys.data_ptr<int64_t>(), slots.data_ptr<int32_t>(), keys.numel(),
-                                         tbase.data_ptr<int64_t>(), trows.data_ptr<int64_t>(), int(tbase.numel()),
-                                         rows.data_ptr(), rows.size(0), cur_stream(rows)),
+  check_hip(dtfs::launch_peer_cache_fill(p, int(trows.numel()), keys.data_ptr<int64_t>(), slots.data_ptr<int32_t>(),
+                                         keys.numel(), rows.data_ptr(), rows.size(0), cur_stream(rows)),
             "peer_cache_fill");
 }
 
@@ -963,6 +977,18 @@ void cache_index_build(torch::Tensor keys, torch::Tensor slots, torch::Tensor id
                                            idx_keys.data_ptr<int64_t>(), idx_slots.data_ptr<int32_t>(), H - 1,
                                            cur_stream(idx_keys)),
             "cache_index_build");
+}
+
+// A device buffer of exactly nbytes from hipMalloc (not the caching
+// allocator): the peer exchange exports each store chunk as its own
+// allocation, so a peer maps exactly that chunk
+torch::Tensor device_alloc(int64_t nbytes, torch::Tensor like) {
+  check_dev(like, "like");
+  TORCH_CHECK(nbytes > 0, "device_alloc: nbytes > 0");
+  c10::DeviceGuard g(like.device());
+  void* p = nullptr;
+  check_hip(hipMalloc(&p, size_t(nbytes)), "hipMalloc");
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipFree(q); }, like.options().dtype(torch::kUInt8));
 }
 
 // IPC: export a device tensor's allocation (handle bytes + the tensor's byte
@@ -1629,17 +1655,21 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("hot") = 1, py::arg("wts") = py::none(), py::arg("out_w") = py::none(),
         "K1b routing: rows (+ weights) of every candidate's owned-table ids grouped by owner rank");
   m.def("dot_interaction_gather_peer", &dot_interaction_gather_peer, py::arg("dense"), py::arg("ids"),
-        py::arg("arena"), py::arg("id_col0"), py::arg("tbase"), py::arg("trows"), py::arg("tremote"),
-        py::arg("cache") = py::none(), py::arg("stats") = py::none(), py::arg("ring") = py::none(),
-        py::arg("ring_ctr") = py::none(), py::arg("sample_every") = 0, py::arg("out_cols") = 0,
+        py::arg("arena"), py::arg("id_col0"), py::arg("cbase"), py::arg("towner"), py::arg("toff"), py::arg("trows"),
+        py::arg("tremote"), py::arg("chunk_shift"), py::arg("cache") = py::none(), py::arg("stats") = py::none(),
+        py::arg("ring") = py::none(), py::arg("ring_ctr") = py::none(), py::arg("sample_every") = 0,
+        py::arg("out_cols") = 0,
         "K1 + K5 with the rows read where they live (peer stores over xGMI, replica cache first)");
   m.def("peer_bag", &peer_bag, py::arg("ids"), py::arg("wts"), py::arg("arena"), py::arg("B"), py::arg("col0"),
-        py::arg("hot"), py::arg("tbase"), py::arg("trows"), py::arg("tremote"), py::arg("cache") = py::none(),
-        py::arg("stats") = py::none(), py::arg("ring") = py::none(), py::arg("ring_ctr") = py::none(),
-        py::arg("sample_every") = 0, py::arg("out"),
+        py::arg("hot"), py::arg("cbase"), py::arg("towner"), py::arg("toff"), py::arg("trows"), py::arg("tremote"),
+        py::arg("chunk_shift"), py::arg("cache") = py::none(), py::arg("stats") = py::none(),
+        py::arg("ring") = py::none(), py::arg("ring_ctr") = py::none(), py::arg("sample_every") = 0, py::arg("out"),
         "K1b multi-hot bags with the rows read where they live -> bf16 [B, T, 64]");
-  m.def("peer_cache_fill", &peer_cache_fill, py::arg("keys"), py::arg("slots"), py::arg("tbase"), py::arg("trows"),
-        py::arg("rows"), "replica cache: copy the keys' table rows into their slots");
+  m.def("peer_cache_fill", &peer_cache_fill, py::arg("keys"), py::arg("slots"), py::arg("cbase"), py::arg("towner"),
+        py::arg("toff"), py::arg("trows"), py::arg("tremote"), py::arg("chunk_shift"), py::arg("rows"),
+        "replica cache: copy the keys' table rows into their slots");
+  m.def("device_alloc", &device_alloc, py::arg("nbytes"), py::arg("like"),
+        "uint8 device buffer of exactly nbytes (its own hipMalloc allocation)");
   m.def("cache_index_build", &cache_index_build, py::arg("keys"), py::arg("slots"), py::arg("idx_keys"),
         py::arg("idx_slots"), "replica cache: open-addressing index keys -> slots (idx_keys pre-filled with -1)");
   m.def("ipc_export", &ipc_export, py::arg("t"), "(IPC handle bytes, byte offset) of a device tensor's allocation");

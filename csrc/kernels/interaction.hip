@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) dot_interact_kernel(const bf16* __restric
 // random reads in flight per wave). The output row (dense | lower triangle |
 // zero pad) is assembled in LDS and written as 16-byte vectors instead of
 // 2-byte scattered stores.
-// With peer.tbase set, the rows come through the peer lookup (peer_lookup.h):
+// With peer.cbase set, the rows come through the peer lookup (peer_lookup.h):
 // table-wise shards read where they live, hot remote rows from the replica
 // cache - the same one-kernel step at any number of ranks.
 template <typename IdT>
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
   int64_t key = 0;
   if (r >= 1 && r < nv) {
     const int t = r - 1;
-    const int64_t m = peer.tbase ? peer.trows[t] : modulo_f[t];
+    const int64_t m = peer.cbase ? peer.trows[t] : modulo_f[t];
     int64_t id = 0;
     if (arena) {  // the request arena's row b (K0 fused: no unpack pass); padding rows read id 0
       const ArenaRow ar = arena_row(arena, kArenaPayloadOff, b);
@@ -176,14 +176,14 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
     }
     int64_t v = id % m;
     if (v < 0) v += m;
-    if (peer.tbase) {
+    if (peer.cbase) {
       src = peer_row(peer, cache_view(peer), t, v, hit);
       key = (int64_t(t) << 40) | v;
     } else {
       src = table + min(offset_f[t] + v, table_rows - 1) * D;
     }
   }
-  if (peer.tbase) {  // converged: the ballots see every lane (lanes h = 1 repeat h = 0's rows)
+  if (peer.cbase) {  // converged: the ballots see every lane (lanes h = 1 repeat h = 0's rows)
     peer_count(peer, hit, h == 0);
     ring_push(peer, key, h == 0 && hit >= 0 && peer.sample_every > 0 && b % peer.sample_every == 0);
   }
@@ -543,10 +543,11 @@ hipError_t launch_dot_interaction_gather(const void* dense, int64_t ldd, const v
                                          hipStream_t st, const void* arena, int id_col0,
                                          const PeerLookupArgs* peer) {
   if (B == 0) return hipSuccess;
-  const bool pl = peer && peer->tbase;
+  const bool pl = peer && peer->cbase;
   if (T < 1 || T + 1 > 32 || out_cols % 8 || out_cols > 1024 || out_cols < 64 + (T + 1) * T / 2 || ldo % 8 ||
       ldo < out_cols || ldd % 8 || (!arena && (!ids || ldi < T)) || (arena && id_col0 < 0) ||
-      (!pl && (table_rows < 1 || !modulo_f || !offset_f)) || (pl && (!peer->trows || !peer->tremote)))
+      (!pl && (table_rows < 1 || !modulo_f || !offset_f)) || (pl && (!peer->trows || !peer->tremote || !peer->towner || !peer->toff || peer->max_chunks < 1 ||
+              peer->chunk_shift < 1 || peer->chunk_shift > 40)))
     return hipErrorInvalidValue;
   const PeerLookupArgs pa = pl ? *peer : PeerLookupArgs{};
   const uint8_t* ar = static_cast<const uint8_t*>(arena);

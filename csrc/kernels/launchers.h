@@ -216,19 +216,25 @@ struct CrossGemmArgs {
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 
 // Peer lookup (kernels/peer_lookup.h): table-wise sharded tables read
-// one-sidedly where they live. Row v of table t is at device address
-// tbase[t] + 128 v (this rank's store, or the owner's store mapped over xGMI
-// by IPC; v = id mod trows[t]); tremote[t] = 1 marks a table owned by another
-// rank, whose rows are looked up in the replica cache first. cache = device
-// int64 [5] {index (keys int64 [mask + 1] | slots int32 [mask + 1]; 0 =
-// empty), unused, mask, rows [cap][64] bf16, cap}, read by each wave at its
-// start (the host swaps indices by rewriting word 0). stats [128]:
-// hits at 2i, misses at 2i + 1 (i = block % 64). Candidates b with b %
-// sample_every == 0 push their remote keys (t << 40 | v) into ring (wrapping).
+// one-sidedly where they live. A rank's store is a list of chunks of 2^shift
+// rows (separate allocations, each mapped by the peers through IPC); chunk c
+// of rank r is at device address cbase[r * max_chunks + c]. Row v of table t
+// (v = id mod trows[t]) is row g = toff[t] + v of rank towner[t]'s store.
+// tremote[t] = 1 marks a table owned by another rank, whose rows are looked
+// up in the replica cache first. cache = device int64 [5] {index (keys int64
+// [mask + 1] | slots int32 [mask + 1]; 0 = empty), unused, mask, rows
+// [cap][64] bf16, cap}, read by each wave at its start (the host swaps
+// indices by rewriting word 0). stats [128]: hits at 2i, misses at 2i + 1 (i
+// = block % 64). Candidates b with b % sample_every == 0 push their remote
+// keys (t << 40 | v) into ring (wrapping).
 struct PeerLookupArgs {
-  const int64_t* tbase = nullptr;
+  const int64_t* cbase = nullptr;
+  const int32_t* towner = nullptr;
+  const int64_t* toff = nullptr;
   const int64_t* trows = nullptr;
   const int32_t* tremote = nullptr;
+  int chunk_shift = 0;
+  int max_chunks = 0;
   const int64_t* cache = nullptr;
   unsigned long long* stats = nullptr;
   int64_t* ring = nullptr;
@@ -257,11 +263,11 @@ hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64,
                            hipStream_t st);
 
 // Replica cache maintenance: rows[slots[i]] = row (keys[i] & (2^40 - 1)) of
-// table keys[i] >> 40 (read through tbase: over xGMI for a peer's table);
+// table keys[i] >> 40 (read where it lives: over xGMI for a peer's table);
 // and the open-addressing index (idx_keys pre-filled with -1, mask + 1 a
 // power of two >= 2 n) mapping keys[i] -> slots[i].
-hipError_t launch_peer_cache_fill(const int64_t* keys, const int32_t* slots, int64_t n, const int64_t* tbase,
-                                  const int64_t* trows, int T, void* rows, int64_t cap, hipStream_t st);
+hipError_t launch_peer_cache_fill(const PeerLookupArgs& p, int T, const int64_t* keys, const int32_t* slots,
+                                  int64_t n, void* rows, int64_t cap, hipStream_t st);
 hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* idx_keys,
                                     int32_t* idx_slots, int64_t mask, hipStream_t st);
 

@@ -45,9 +45,16 @@ __device__ __forceinline__ CacheView cache_view(const PeerLookupArgs& p) {
 
 // Row v of table t (D = 64): its address, and hit = -1 (table held here),
 // 1 (remote, cached), 0 (remote, read over xGMI).
+// Row v of table t where it lives (its owner's store chunk)
+__device__ __forceinline__ const bf16* store_row(const PeerLookupArgs& p, int t, int64_t v) {
+  const int64_t g = p.toff[t] + v;
+  const int64_t c = int64_t(p.towner[t]) * p.max_chunks + (g >> p.chunk_shift);
+  return reinterpret_cast<const bf16*>(p.cbase[c]) + (g & ((int64_t(1) << p.chunk_shift) - 1)) * 64;
+}
+
 __device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const CacheView& c, int t, int64_t v,
                                                 int& hit) {
-  const bf16* src = reinterpret_cast<const bf16*>(p.tbase[t]) + v * 64;
+  const bf16* src = store_row(p, t, v);
   hit = -1;
   if (p.tremote[t]) {
     hit = 0;

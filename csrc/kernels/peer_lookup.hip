@@ -62,10 +62,8 @@ __global__ void __launch_bounds__(256) peer_bag_kernel(PeerLookupArgs p, const I
 }
 
 // 8 lanes per key: rows[slot] = table row of the key, read where it lives
-__global__ void __launch_bounds__(256) peer_cache_fill_kernel(const int64_t* __restrict__ keys,
+__global__ void __launch_bounds__(256) peer_cache_fill_kernel(PeerLookupArgs p, int T, const int64_t* __restrict__ keys,
                                                               const int32_t* __restrict__ slots, int64_t n,
-                                                              const int64_t* __restrict__ tbase,
-                                                              const int64_t* __restrict__ trows, int T,
                                                               bf16* __restrict__ rows, int64_t cap) {
   const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 3;
   const int c = threadIdx.x & 7;
@@ -74,8 +72,8 @@ __global__ void __launch_bounds__(256) peer_cache_fill_kernel(const int64_t* __r
   const int64_t t = key >> 40;
   const int64_t s = slots[i];
   if (key < 0 || t >= T || s < 0 || s >= cap) return;
-  const int64_t v = min(key & ((int64_t(1) << 40) - 1), trows[t] - 1);
-  const bf16* src = reinterpret_cast<const bf16*>(tbase[t]) + v * 64;
+  const int64_t v = min(key & ((int64_t(1) << 40) - 1), p.trows[t] - 1);
+  const bf16* src = store_row(p, int(t), v);
   *reinterpret_cast<bf16x8*>(rows + s * 64 + c * 8) = *reinterpret_cast<const bf16x8*>(src + c * 8);
 }
 
@@ -107,7 +105,8 @@ hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64,
                            int64_t ldw, const void* arena, int col0, int T, int hot, int B, void* out,
                            hipStream_t st) {
   if (B == 0) return hipSuccess;
-  if (!p.tbase || !p.trows || !p.tremote || T < 1 || hot < 1 || col0 < 0 || !out ||
+  if (!p.cbase || !p.towner || !p.toff || !p.trows || !p.tremote || p.max_chunks < 1 || p.chunk_shift < 1 ||
+      p.chunk_shift > 40 || T < 1 || hot < 1 || col0 < 0 || !out ||
       (!arena && (!ids || !wts || ldi < col0 + T * hot || ldw < col0 + T * hot)) ||
       (p.ring && (!p.ring_ctr || p.ring_cap < 1)))
     return hipErrorInvalidValue;
@@ -123,12 +122,14 @@ hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64,
   return hipGetLastError();
 }
 
-hipError_t launch_peer_cache_fill(const int64_t* keys, const int32_t* slots, int64_t n, const int64_t* tbase,
-                                  const int64_t* trows, int T, void* rows, int64_t cap, hipStream_t st) {
+hipError_t launch_peer_cache_fill(const PeerLookupArgs& p, int T, const int64_t* keys, const int32_t* slots,
+                                  int64_t n, void* rows, int64_t cap, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (!keys || !slots || !tbase || !trows || T < 1 || !rows || cap < 1 || n < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(peer_cache_fill_kernel, dim3(unsigned((n * 8 + 255) / 256)), dim3(256), 0, st, keys, slots, n,
-                     tbase, trows, T, static_cast<bf16*>(rows), cap);
+  if (!p.cbase || !p.towner || !p.toff || !p.trows || p.max_chunks < 1 || p.chunk_shift < 1 || p.chunk_shift > 40 ||
+      !keys || !slots || T < 1 || !rows || cap < 1 || n < 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_cache_fill_kernel, dim3(unsigned((n * 8 + 255) / 256)), dim3(256), 0, st, p, T, keys, slots,
+                     n, static_cast<bf16*>(rows), cap);
   return hipGetLastError();
 }
 

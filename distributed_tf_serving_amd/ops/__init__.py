@@ -544,10 +544,10 @@ def dot_interaction_gather_peer(dense: torch.Tensor, ids, peer, cache=None, out_
     kw = cache.kernel_args() if cache is not None else {}
     if dense.is_cuda:
         if isinstance(ids, ArenaRows):
-            return hip().dot_interaction_gather_peer(dense, None, ids.arena, int(id_col0), peer.tbase, peer.trows,
-                                                     peer.tremote, out_cols=int(out_cols), **kw)
-        return hip().dot_interaction_gather_peer(dense, _rows(ids), None, int(id_col0), peer.tbase, peer.trows,
-                                                 peer.tremote, out_cols=int(out_cols), **kw)
+            return hip().dot_interaction_gather_peer(dense, None, ids.arena, int(id_col0), out_cols=int(out_cols),
+                                                     **peer.kernel_args(), **kw)
+        return hip().dot_interaction_gather_peer(dense, _rows(ids), None, int(id_col0), out_cols=int(out_cols),
+                                                 **peer.kernel_args(), **kw)
     from ..parallel.hot_cache import peer_gather_cpu
 
     if isinstance(ids, ArenaRows):
@@ -564,15 +564,14 @@ def peer_bag(ids, wts: Optional[torch.Tensor], B: int, col0: int, hot: int, peer
     T = peer.T
     dev = peer.trows.device
     if out is None:
-        out = torch.empty(B, T, 64, dtype=peer.stores[peer.rank].dtype, device=dev)
+        out = torch.empty(B, T, 64, dtype=peer.dtype, device=dev)
     kw = cache.kernel_args() if cache is not None else {}
     if dev.type == "cuda":
         if isinstance(ids, ArenaRows):
-            hip().peer_bag(None, None, ids.arena, int(B), int(col0), int(hot), peer.tbase, peer.trows, peer.tremote,
-                           out=out, **kw)
+            hip().peer_bag(None, None, ids.arena, int(B), int(col0), int(hot), out=out, **peer.kernel_args(), **kw)
         else:
-            hip().peer_bag(_rows(ids), _rows(wts.float()), None, int(B), int(col0), int(hot), peer.tbase, peer.trows,
-                           peer.tremote, out=out, **kw)
+            hip().peer_bag(_rows(ids), _rows(wts.float()), None, int(B), int(col0), int(hot), out=out,
+                           **peer.kernel_args(), **kw)
         return out
     from ..parallel.hot_cache import peer_gather_cpu
 

@@ -239,24 +239,36 @@ class ShardedEmbedding(nn.Module):
             tok: list = [None] * self.world
             dist.all_gather_object(tok, uuid.uuid4().hex[:12], group=group)
             shm_tag = f"/dev/shm/dtfs_peer_{tok[0]}_{self.rank}"
-            store = hot_cache.shm_store(self.rows_local, dtype, shm_tag)
+        if peer:
+            # chunks of 8 M rows, each its own allocation (GPU: its own IPC
+            # object - a peer maps exactly that chunk)
+            chunks = hot_cache.alloc_store(self.rows_local, dtype, dev, shm_tag)
         else:
-            store = torch.empty(max(1, self.rows_local), self.D, dtype=dtype, device=dev)
-        for t, s, n, o in self.segments:
-            if n:
-                hashed_uniform_rows_(store[o:o + n], t, s, seed, bound)
-        self.store = nn.Parameter(store, requires_grad=False)
+            chunks = [torch.empty(max(1, self.rows_local), self.D, dtype=dtype, device=dev)]
+        per = chunks[0].shape[0]
+        for t, s, n, o in self.segments:  # each segment's rows, chunk by chunk
+            r = o
+            while r < o + n:
+                c, i = divmod(r, per)
+                k = min(o + n - r, chunks[c].shape[0] - i)
+                hashed_uniform_rows_(chunks[c][i:i + k], t, s + (r - o), seed, bound)
+                r += k
+        self.store = nn.Parameter(chunks[0], requires_grad=False)
+        # the other chunks (peer exchange with > 8 M local rows)
+        self.store_chunks = nn.ParameterList([nn.Parameter(c, requires_grad=False) for c in chunks[1:]])
         # peer exchange: every rank's store mapped here, each table's rows read
         # where they live, hot remote rows from this rank's replica cache
         self.peer: Optional[hot_cache.PeerTables] = None
         self.cache: Optional[hot_cache.HotRowCache] = None
         if exchange == "peer":
-            stores = hot_cache.open_peer_stores(self.store.data, group, shm_tag) if peer else [self.store.data]
+            mine = [c.data for c in [self.store, *self.store_chunks]]
+            stores = hot_cache.open_peer_stores(mine, group, shm_tag) if peer else [mine]
             if shm_tag is not None:
                 os.unlink(shm_tag)  # every rank has it mapped (open_peer_stores ends in a barrier)
             owner = [next(r for r in range(self.world) if t in self.tw_by_rank[r]) for t in range(T)]
             self.peer = hot_cache.PeerTables(stores, owner, [lay[owner[t]][1][t] for t in range(T)],
-                                             [plan.tables[t].rows for t in range(T)], self.rank)
+                                             [plan.tables[t].rows for t in range(T)], self.rank,
+                                             chunk_shift=hot_cache.CHUNK_SHIFT if peer else None)
             if peer and cache_rows > 0 and self.peer.remote_tables:
                 self.cache = hot_cache.HotRowCache(self.peer, cache_rows, sample_every=cache_sample_every)
         i64 = dict(dtype=torch.int64, device=dev)
@@ -292,7 +304,7 @@ class ShardedEmbedding(nn.Module):
         self._maps: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 
     def local_bytes(self) -> int:
-        return self.store.numel() * self.store.element_size()
+        return sum(c.numel() * c.element_size() for c in [self.store, *self.store_chunks])
 
     # -- exchange buffers / table map ----------------------------------------
     def n_tw_rows(self, B: int) -> int:

@@ -50,35 +50,61 @@ def _next_pow2(n: int) -> int:
     return p
 
 
-class PeerTables:
-    """Where each table's rows live, seen from this rank: table t is rows
-    ``off[t] .. off[t] + rows[t]`` of ``stores[owner[t]]`` - this rank's own
-    store, a peer's store mapped by IPC (GPU) or a peer's shared-memory file
-    (CPU). ``tbase`` (GPU): the device address of each table's row 0."""
+CHUNK_SHIFT = 23  # 8 M rows (1 GiB of bf16 rows) per store chunk
 
-    def __init__(self, stores: Sequence[torch.Tensor], owner: Sequence[int], off: Sequence[int],
-                 rows: Sequence[int], rank: int):
-        self.stores = list(stores)
+
+class PeerTables:
+    """Where each table's rows live, seen from this rank. ``stores[r]`` is rank
+    r's store as a list of chunks (chunk c = store rows ``c << chunk_shift``
+    onwards; every chunk but the last has exactly 2^chunk_shift rows): this
+    rank's own, a peer's mapped by IPC (GPU: each chunk is its own allocation
+    and its own IPC object), or views of a peer's shared-memory file (CPU). A
+    rank given as one tensor is one chunk. Table t is rows ``off[t] ..
+    off[t] + rows[t]`` of ``stores[owner[t]]``."""
+
+    def __init__(self, stores: Sequence, owner: Sequence[int], off: Sequence[int], rows: Sequence[int], rank: int,
+                 chunk_shift: Optional[int] = None):
+        self.stores = [[s] if isinstance(s, torch.Tensor) else list(s) for s in stores]
         self.owner, self.off, self.rows, self.rank = list(owner), list(off), list(rows), int(rank)
         self.T = len(self.owner)
-        dev = self.stores[self.rank].device
+        if chunk_shift is None:
+            if all(len(c) == 1 for c in self.stores):
+                chunk_shift = max(1, max(int(c[0].shape[0]) for c in self.stores) - 1).bit_length()
+            else:
+                chunk_shift = CHUNK_SHIFT
+        self.chunk_shift = int(chunk_shift)
+        per = 1 << self.chunk_shift
+        total = []
+        for r, chunks in enumerate(self.stores):
+            for i, c in enumerate(chunks):
+                if c.dim() != 2 or c.shape[1] != D or not c.is_contiguous():
+                    raise ValueError("peer store chunks must be contiguous [rows, 64]")
+                if c.shape[0] > per or (i < len(chunks) - 1 and c.shape[0] != per):
+                    raise ValueError(f"rank {r} chunk {i}: {c.shape[0]} rows, chunks hold 2^{self.chunk_shift}")
+            total.append(sum(int(c.shape[0]) for c in chunks))
         for t in range(self.T):
-            s = self.stores[self.owner[t]]
-            if s.dim() != 2 or s.shape[1] != D or not s.is_contiguous():
-                raise ValueError("peer stores must be contiguous [rows, 64]")
-            if self.off[t] < 0 or self.off[t] + self.rows[t] > s.shape[0]:
+            if self.off[t] < 0 or self.off[t] + self.rows[t] > total[self.owner[t]]:
                 raise ValueError(f"table {t}: rows {self.off[t]}..{self.off[t] + self.rows[t]} outside its owner's "
-                                 f"store ({s.shape[0]} rows)")
-        self.trows = torch.tensor(self.rows, dtype=torch.int64, device=dev)
+                                 f"store ({total[self.owner[t]]} rows)")
+        mine = self.stores[self.rank][0]
+        dev = mine.device
+        self.dtype = mine.dtype
+        maxc = max(len(c) for c in self.stores)
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.trows = torch.tensor(self.rows, **i64)
+        self.toff = torch.tensor(self.off, **i64)
+        self.towner = torch.tensor(self.owner, dtype=torch.int32, device=dev)
         self.tremote = torch.tensor([int(o != self.rank) for o in self.owner], dtype=torch.int32, device=dev)
-        self.tbase = None
-        if dev.type == "cuda":
-            self.tbase = torch.tensor([self.stores[o].data_ptr() + self.off[t] * D * self.stores[o].element_size()
-                                       for t, o in enumerate(self.owner)], dtype=torch.int64, device=dev)
+        self.cbase = torch.tensor([[c.data_ptr() for c in chunks] + [0] * (maxc - len(chunks))
+                                   for chunks in self.stores], **i64)
         self._owner_cpu = torch.tensor(self.owner, dtype=torch.int64)
         self._off_cpu = torch.tensor(self.off, dtype=torch.int64)
         self.trows_cpu = torch.tensor(self.rows, dtype=torch.int64)
         self.tremote_cpu = self.tremote.cpu().bool()
+
+    def kernel_args(self) -> dict:
+        return dict(cbase=self.cbase, towner=self.towner, toff=self.toff, trows=self.trows, tremote=self.tremote,
+                    chunk_shift=self.chunk_shift)
 
     @property
     def remote_tables(self) -> int:
@@ -86,11 +112,15 @@ class PeerTables:
 
     def row_cpu(self, t: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
         """Rows v of tables t (int64 [n] each) read from their owners' stores."""
-        out = torch.empty(t.numel(), D, dtype=self.stores[self.rank].dtype)
+        out = torch.empty(t.numel(), D, dtype=self.dtype)
         own = self._owner_cpu[t]
-        for r in torch.unique(own).tolist():
-            m = own == r
-            out[m] = self.stores[r][self._off_cpu[t[m]] + v[m]]
+        g = self._off_cpu[t] + v
+        chunk = g >> self.chunk_shift
+        local = g & ((1 << self.chunk_shift) - 1)
+        key = own * (1 << 20) + chunk
+        for k in torch.unique(key).tolist():
+            m = key == k
+            out[m] = self.stores[k >> 20][k & ((1 << 20) - 1)][local[m]].cpu()
         return out
 
 
@@ -119,7 +149,7 @@ class HotRowCache:
         dev = peer.trows.device
         self.device = dev
         i64 = dict(dtype=torch.int64, device=dev)
-        self.rows = torch.zeros(self.cap, D, dtype=peer.stores[peer.rank].dtype, device=dev)
+        self.rows = torch.zeros(self.cap, D, dtype=peer.dtype, device=dev)
         self.index = [torch.full((self.H + self.H // 2,), -1, **i64) for _ in range(2)]
         self.desc = torch.tensor([0, 0, self.H - 1, self.rows.data_ptr() if dev.type == "cuda" else 0, self.cap], **i64)
         self.stats = torch.zeros(128, **i64)
@@ -247,7 +277,7 @@ class HotRowCache:
         if self.device.type == "cuda":
             from ..ops import hip
 
-            hip().peer_cache_fill(keys, slots, p.tbase, p.trows, self.rows)
+            hip().peer_cache_fill(keys, slots, rows=self.rows, **p.kernel_args())
         else:
             t, v = keys >> KEY_SHIFT, keys & ROW_MASK
             self.rows[slots.long()] = p.row_cpu(t, v)
@@ -306,47 +336,68 @@ def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.T
         out = rows.view(B, T, D)
     else:
         out = (rows.view(B, T, hot, D) * wts.float().reshape(B, T, hot, 1)).sum(2)
-    return out.to(peer.stores[peer.rank].dtype)
+    return out.to(peer.dtype)
 
 
-def open_peer_stores(store: torch.Tensor, group=None, shm_tag: Optional[str] = None) -> List[torch.Tensor]:
-    """Every rank's store as seen from this rank (collective). GPU: IPC
-    handles (+ the store's offset in its allocation) exchanged with
-    all_gather_object, each peer's store mapped for loads over xGMI. CPU:
-    ``store`` is a shared-memory file mapping made by :func:`shm_store` and
-    ``shm_tag`` its path."""
+def open_peer_stores(chunks: List[torch.Tensor], group=None, shm_tag: Optional[str] = None,
+                     chunk_shift: Optional[int] = None) -> List[List[torch.Tensor]]:
+    """Every rank's store chunks as seen from this rank (collective). GPU:
+    one IPC handle per chunk (each chunk its own allocation, see
+    :func:`alloc_store`) exchanged with all_gather_object, each peer chunk
+    mapped for loads over xGMI. CPU: the chunks are views of one
+    shared-memory file made by :func:`alloc_store`, ``shm_tag`` its path."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
+    chunk_shift = CHUNK_SHIFT if chunk_shift is None else chunk_shift
     if world == 1:
-        return [store]
-    if store.is_cuda:
+        return [chunks]
+    cuda = chunks[0].is_cuda
+    if cuda:
         from ..ops import hip
 
-        h, off = hip().ipc_export(store)
-        mine = (h, int(off), list(store.shape))
+        mine = [(*hip().ipc_export(c), list(c.shape)) for c in chunks]
     else:
         if shm_tag is None:
             raise ValueError("CPU peer stores need their shared-memory tag")
-        mine = (shm_tag, 0, list(store.shape))
+        mine = [(shm_tag, 0, [sum(int(c.shape[0]) for c in chunks), D])]
     allv: list = [None] * world
     dist.all_gather_object(allv, mine, group=group)
-    out: List[torch.Tensor] = []
-    for r, (h, off, shape) in enumerate(allv):
+    out: List[List[torch.Tensor]] = []
+    for r, theirs in enumerate(allv):
         if r == rank:
-            out.append(store)
-        elif store.is_cuda:
+            out.append(list(chunks))
+        elif cuda:
             from ..ops import hip
 
-            out.append(hip().ipc_open(h, off, shape, store))
+            out.append([hip().ipc_open(h, off, shape, chunks[0]) for h, off, shape in theirs])
         else:
-            n = int(shape[0]) * int(shape[1])
-            out.append(torch.from_file(h, shared=True, size=n, dtype=store.dtype).view(*shape))
-    dist.barrier(group=group)  # every rank has mapped every file: the names can go
+            path, _, shape = theirs[0]
+            whole = torch.from_file(path, shared=True, size=int(shape[0]) * D, dtype=chunks[0].dtype).view(*shape)
+            out.append(list(torch.split(whole, 1 << chunk_shift)))
+    dist.barrier(group=group)  # every rank has mapped every chunk: the file names can go
     return out
 
 
-def shm_store(rows: int, dtype, tag: str) -> torch.Tensor:
-    """A [rows, 64] CPU tensor in a shared-memory file other ranks can map."""
-    return torch.from_file(tag, shared=True, size=max(1, rows) * D, dtype=dtype).view(max(1, rows), D)
+def alloc_store(rows: int, dtype, device, shm_tag: Optional[str] = None,
+                chunk_shift: Optional[int] = None) -> List[torch.Tensor]:
+    """A store of ``rows`` [64]-wide rows as chunks of 2^chunk_shift rows.
+    GPU: each chunk is its own hipMalloc allocation (a peer maps exactly that
+    chunk); CPU: views of one shared-memory file other ranks can map."""
+    rows = max(1, int(rows))
+    per = 1 << (CHUNK_SHIFT if chunk_shift is None else chunk_shift)
+    if torch.device(device).type == "cuda":
+        from ..ops import hip
+
+        like = torch.empty(0, device=device)
+        out = []
+        for c0 in range(0, rows, per):
+            n = min(per, rows - c0)
+            out.append(hip().device_alloc(n * D * torch.tensor([], dtype=dtype).element_size(), like)
+                       .view(dtype).view(n, D))
+        return out
+    if shm_tag is None:
+        return list(torch.split(torch.empty(rows, D, dtype=dtype), per))
+    whole = torch.from_file(shm_tag, shared=True, size=rows * D, dtype=dtype).view(rows, D)
+    return list(torch.split(whole, per))

@@ -39,7 +39,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, hot, q):
+def _worker(rank, world, port, hot, q, chunk_shift=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -48,9 +48,15 @@ def _worker(rank, world, port, hot, q):
     from distributed_tf_serving_amd.parallel.embedding_sharding import ShardedDLRM
 
     try:
+        if chunk_shift is not None:  # stores split into many small chunks
+            from distributed_tf_serving_amd.parallel import hot_cache
+
+            hot_cache.CHUNK_SHIFT = chunk_shift
         ctx = init_from_env(device="cpu")
         cfg = _cfg(hot)
         m = ShardedDLRM(cfg, ctx)
+        if chunk_shift is not None:
+            assert m.emb.peer.chunk_shift == chunk_shift and len(m.emb.peer.stores[1 - rank]) > 10
         ref = build_model(cfg)
         assert not m.has_collectives and m.emb.exchange == "peer" and m.cache is not None
         m.cache.sample_every = 1  # small batches: sample every candidate
@@ -74,12 +80,12 @@ def _worker(rank, world, port, hot, q):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world,hot", [(2, 1), (3, 1), (2, 3)])
-def test_peer_exchange_matches_unsharded(world, hot):
+@pytest.mark.parametrize("world,hot,chunk_shift", [(2, 1, None), (3, 1, None), (2, 3, None), (2, 1, 6)])
+def test_peer_exchange_matches_unsharded(world, hot, chunk_shift):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, hot, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, hot, q, chunk_shift)) for r in range(world)]
     [p.start() for p in procs]
     res = {}
     for _ in range(world):
@@ -96,13 +102,27 @@ def test_peer_exchange_matches_unsharded(world, hot):
         assert xb > 0
 
 
-def _local_peer(T=4, rows=50, remote=(1, 3)):
-    """Two 'ranks' in one process: tables in `remote` live in store 1."""
+def _local_peer(T=4, rows=50, remote=(1, 3), chunk_shift=None):
+    """Two 'ranks' in one process: tables in `remote` live in store 1
+    (chunk_shift: each store split into chunks of 2^chunk_shift rows)."""
     torch.manual_seed(0)
     stores = [torch.randn(T * rows, 64).to(torch.bfloat16), torch.randn(T * rows, 64).to(torch.bfloat16)]
+    if chunk_shift is not None:
+        stores = [list(torch.split(s, 1 << chunk_shift)) for s in stores]
     owner = [1 if t in remote else 0 for t in range(T)]
     off = [t * rows for t in range(T)]
-    return PeerTables(stores, owner, off, [rows] * T, rank=0)
+    return PeerTables(stores, owner, off, [rows] * T, rank=0, chunk_shift=chunk_shift)
+
+
+def test_chunked_store_rows():
+    """Rows read through 16-row chunks equal the rows of the whole store."""
+    whole, chunked = _local_peer(), _local_peer(chunk_shift=4)
+    assert chunked.chunk_shift == 4 and len(chunked.stores[1]) == 13
+    t = torch.arange(4).repeat_interleave(50)
+    v = torch.arange(50).repeat(4)
+    assert torch.equal(whole.row_cpu(t, v), chunked.row_cpu(t, v))
+    with pytest.raises(ValueError):  # a middle chunk must hold exactly 2^shift rows
+        PeerTables([[torch.zeros(8, 64), torch.zeros(16, 64)]], [0], [0], [20], rank=0, chunk_shift=4)
 
 
 def test_cache_refresh_slot_safety_and_turnover():
@@ -146,22 +166,25 @@ def test_local_tables_never_cached_or_counted():
 
 
 # ---------------------------------------------------------------------- GPU
-def _gpu_peer(dev, T=6, rows=4096, remote=(1, 2, 4)):
+def _gpu_peer(dev, T=6, rows=4096, remote=(1, 2, 4), chunk_shift=None):
     g = torch.Generator(device="cpu").manual_seed(3)
     stores = [torch.randn(T * rows, 64, generator=g).to(torch.bfloat16).to(dev) for _ in range(2)]
+    if chunk_shift is not None:  # chunks = views of the store; the kernels only see chunk addresses
+        stores = [list(torch.split(s, 1 << chunk_shift)) for s in stores]
     owner = [1 if t in remote else 0 for t in range(T)]
-    return PeerTables(stores, owner, [t * rows for t in range(T)], [rows] * T, rank=0)
+    return PeerTables(stores, owner, [t * rows for t in range(T)], [rows] * T, rank=0, chunk_shift=chunk_shift)
 
 
 def _cpu_twin(p):
-    return PeerTables([s.cpu() for s in p.stores], p.owner, p.off, p.rows, p.rank)
+    return PeerTables([[c.cpu() for c in s] for s in p.stores], p.owner, p.off, p.rows, p.rank, p.chunk_shift)
 
 
 @pytest.mark.gpu
-def test_peer_kernels_match_reference(cuda):
+@pytest.mark.parametrize("chunk_shift", [None, 9])
+def test_peer_kernels_match_reference(cuda, chunk_shift):
     from distributed_tf_serving_amd import ops
 
-    p = _gpu_peer(cuda)
+    p = _gpu_peer(cuda, chunk_shift=chunk_shift)
     pc = _cpu_twin(p)
     T, B, col0 = p.T, 1000, 3
     g = torch.Generator().manual_seed(5)
