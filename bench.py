@@ -416,9 +416,9 @@ def run_live(a, ctx, cfg, model, eng, B):
         # peer exchange: serve a few steps so the kernels sample the stream,
         # then install the hot set (the refresher is off while the clock runs:
         # a synthetic stream's hot set does not drift)
-        live.run_load(pool, warmup=0, count=max(8, a.warmup) * n_req, concurrency=conc, threads=a.client_threads,
-                      timeout_us=timeout_us)
-        for _ in range(2):
+        for _ in range(3):
+            live.run_load(pool, warmup=0, count=max(8, a.warmup) * n_req, concurrency=conc,
+                          threads=a.client_threads, timeout_us=timeout_us)
             cache.refresh()
         sync()
         cache.reset_counts()

@@ -960,22 +960,19 @@ void peer_cache_fill(torch::Tensor keys, torch::Tensor slots, torch::Tensor cbas
             "peer_cache_fill");
 }
 
-void cache_index_build(torch::Tensor keys, torch::Tensor slots, torch::Tensor idx_keys, torch::Tensor idx_slots) {
-  check_dev(idx_keys, "idx_keys");
-  for (auto* t : {&keys, &slots, &idx_slots}) check_same_dev(idx_keys, *t, "cache index input");
+void cache_index_build(torch::Tensor keys, torch::Tensor slots, torch::Tensor entries) {
+  check_dev(entries, "entries");
+  for (auto* t : {&keys, &slots}) check_same_dev(entries, *t, "cache index input");
   TORCH_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous() && slots.scalar_type() == torch::kInt32 &&
                   slots.is_contiguous() && slots.numel() == keys.numel(),
               "keys int64 [n], slots int32 [n]");
-  TORCH_CHECK(idx_keys.scalar_type() == torch::kInt64 && idx_keys.is_contiguous() &&
-                  idx_slots.scalar_type() == torch::kInt32 && idx_slots.is_contiguous() &&
-                  idx_slots.numel() == idx_keys.numel(),
-              "idx_keys int64 [H], idx_slots int32 [H]");
-  const int64_t H = idx_keys.numel();
+  TORCH_CHECK(entries.scalar_type() == torch::kInt64 && entries.is_contiguous() && entries.numel() % 2 == 0,
+              "entries: int64 [H, 2]");
+  const int64_t H = entries.numel() / 2;
   TORCH_CHECK(H >= 2 && (H & (H - 1)) == 0 && 2 * keys.numel() <= H, "index size: a power of two >= 2 n");
-  c10::DeviceGuard g(idx_keys.device());
+  c10::DeviceGuard g(entries.device());
   check_hip(dtfs::launch_cache_index_build(keys.data_ptr<int64_t>(), slots.data_ptr<int32_t>(), keys.numel(),
-                                           idx_keys.data_ptr<int64_t>(), idx_slots.data_ptr<int32_t>(), H - 1,
-                                           cur_stream(idx_keys)),
+                                           entries.data_ptr<int64_t>(), H - 1, cur_stream(entries)),
             "cache_index_build");
 }
 
@@ -1670,8 +1667,8 @@ PYBIND11_MODULE(_hip, m) {
         "replica cache: copy the keys' table rows into their slots");
   m.def("device_alloc", &device_alloc, py::arg("nbytes"), py::arg("like"),
         "uint8 device buffer of exactly nbytes (its own hipMalloc allocation)");
-  m.def("cache_index_build", &cache_index_build, py::arg("keys"), py::arg("slots"), py::arg("idx_keys"),
-        py::arg("idx_slots"), "replica cache: open-addressing index keys -> slots (idx_keys pre-filled with -1)");
+  m.def("cache_index_build", &cache_index_build, py::arg("keys"), py::arg("slots"), py::arg("entries"),
+        "replica cache: open-addressing index keys -> slots ({key, slot} entries pre-filled with -1)");
   m.def("ipc_export", &ipc_export, py::arg("t"), "(IPC handle bytes, byte offset) of a device tensor's allocation");
   m.def("ipc_open", &ipc_open, py::arg("handle"), py::arg("offset"), py::arg("shape"), py::arg("like"),
         "map a peer's ipc_export as a tensor (dtype / device of `like`)");

@@ -221,10 +221,10 @@ hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 // of rank r is at device address cbase[r * max_chunks + c]. Row v of table t
 // (v = id mod trows[t]) is row g = toff[t] + v of rank towner[t]'s store.
 // tremote[t] = 1 marks a table owned by another rank, whose rows are looked
-// up in the replica cache first. cache = device int64 [5] {index (keys int64
-// [mask + 1] | slots int32 [mask + 1]; 0 = empty), unused, mask, rows
-// [cap][64] bf16, cap}, read by each wave at its start (the host swaps
-// indices by rewriting word 0). stats [128]: hits at 2i, misses at 2i + 1 (i
+// up in the replica cache first. cache = device int64 [5] {index (entries
+// int64 [mask + 1][2] = {key, slot}, key -1 = empty; 0 = no index), unused,
+// mask, rows [cap][64] bf16, cap}, read by each wave at its start (the host
+// swaps indices by rewriting word 0). stats [128]: hits at 2i, misses at 2i + 1 (i
 // = block % 64). Candidates b with b % sample_every == 0 push their remote
 // keys (t << 40 | v) into ring (wrapping).
 struct PeerLookupArgs {
@@ -264,12 +264,12 @@ hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64,
 
 // Replica cache maintenance: rows[slots[i]] = row (keys[i] & (2^40 - 1)) of
 // table keys[i] >> 40 (read where it lives: over xGMI for a peer's table);
-// and the open-addressing index (idx_keys pre-filled with -1, mask + 1 a
-// power of two >= 2 n) mapping keys[i] -> slots[i].
+// and the open-addressing index (entries [mask + 1][2] pre-filled with -1,
+// mask + 1 a power of two >= 2 n) mapping keys[i] -> slots[i].
 hipError_t launch_peer_cache_fill(const PeerLookupArgs& p, int T, const int64_t* keys, const int32_t* slots,
                                   int64_t n, void* rows, int64_t cap, hipStream_t st);
-hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* idx_keys,
-                                    int32_t* idx_slots, int64_t mask, hipStream_t st);
+hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* entries,
+                                    int64_t mask, hipStream_t st);
 
 // K4 (small) for the DLRM bottom MLP: relu(relu(relu(pad64(bf16(wts[:, :nd]))
 // W1^T + b1) W2^T + b2) W3^T + b3) in one kernel (W1 [N1][64], W2 [N2][N1], W3

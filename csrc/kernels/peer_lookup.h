@@ -15,36 +15,32 @@ namespace kern {
 
 constexpr int64_t kCacheEmpty = -1;
 constexpr int kCacheMaxProbe = 32;  // the index is built at <= 50 % load
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint64_t cache_hash(int64_t key, uint64_t mask) {
   return ((uint64_t(key) * 0x9E3779B97F4A7C15ull) >> 24) & mask;
 }
 
 struct CacheView {
-  const int64_t* keys;
-  const int32_t* slots;
-  uint64_t mask;  // 0: the cache is empty
+  const int64_t* entries;  // [mask + 1] x {key, slot}: one 16-byte load per probe
+  uint64_t mask;           // 0: the cache is empty
   const bf16* rows;
   int64_t cap;
 };
 
 __device__ __forceinline__ CacheView cache_view(const PeerLookupArgs& p) {
-  CacheView c{nullptr, nullptr, 0, nullptr, 0};
+  CacheView c{nullptr, 0, nullptr, 0};
   if (p.cache) {
-    // one index buffer = keys int64 [mask + 1] | slots int32 [mask + 1]: the
-    // host swaps indices by rewriting the single word cache[0]
-    c.keys = reinterpret_cast<const int64_t*>(p.cache[0]);
+    // the host swaps indices by rewriting the single word cache[0]
+    c.entries = reinterpret_cast<const int64_t*>(p.cache[0]);
     c.mask = uint64_t(p.cache[2]);
-    c.slots = c.keys ? reinterpret_cast<const int32_t*>(c.keys + (c.mask + 1)) : nullptr;
     c.rows = reinterpret_cast<const bf16*>(p.cache[3]);
     c.cap = p.cache[4];
-    if (!c.keys || !c.slots || !c.rows || c.cap < 1) c.mask = 0;
+    if (!c.entries || !c.rows || c.cap < 1) c.mask = 0;
   }
   return c;
 }
 
-// Row v of table t (D = 64): its address, and hit = -1 (table held here),
-// 1 (remote, cached), 0 (remote, read over xGMI).
 // Row v of table t where it lives (its owner's store chunk)
 __device__ __forceinline__ const bf16* store_row(const PeerLookupArgs& p, int t, int64_t v) {
   const int64_t g = p.toff[t] + v;
@@ -62,9 +58,10 @@ __device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const C
       const int64_t key = (int64_t(t) << 40) | v;
       uint64_t h = cache_hash(key, c.mask);
       for (int probe = 0; probe < kCacheMaxProbe; ++probe) {
-        const int64_t k = c.keys[h];
+        const i64x2 e = *reinterpret_cast<const i64x2*>(c.entries + 2 * h);
+        const int64_t k = e[0];
         if (k == key) {
-          const int64_t s = c.slots[h];
+          const int64_t s = e[1];
           if (s >= 0 && s < c.cap) {
             src = c.rows + s * 64;
             hit = 1;

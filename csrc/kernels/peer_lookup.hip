@@ -79,18 +79,17 @@ __global__ void __launch_bounds__(256) peer_cache_fill_kernel(PeerLookupArgs p, 
 
 __global__ void __launch_bounds__(256) cache_index_build_kernel(const int64_t* __restrict__ keys,
                                                                 const int32_t* __restrict__ slots, int64_t n,
-                                                                int64_t* __restrict__ idx_keys,
-                                                                int32_t* __restrict__ idx_slots, uint64_t mask) {
+                                                                int64_t* __restrict__ entries, uint64_t mask) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t key = keys[i];
   if (key < 0) return;
   uint64_t h = cache_hash(key, mask);
   for (uint64_t probe = 0; probe <= mask; ++probe) {
-    const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(idx_keys + h),
+    const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(entries + 2 * h),
                                              (unsigned long long)kCacheEmpty, (unsigned long long)key);
     if (old == (unsigned long long)kCacheEmpty || old == (unsigned long long)key) {
-      idx_slots[h] = slots[i];
+      entries[2 * h + 1] = slots[i];
       return;
     }
     h = (h + 1) & mask;
@@ -133,13 +132,13 @@ hipError_t launch_peer_cache_fill(const PeerLookupArgs& p, int T, const int64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* idx_keys,
-                                    int32_t* idx_slots, int64_t mask, hipStream_t st) {
+hipError_t launch_cache_index_build(const int64_t* keys, const int32_t* slots, int64_t n, int64_t* entries,
+                                    int64_t mask, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (!keys || !slots || !idx_keys || !idx_slots || mask < 1 || ((mask + 1) & mask) || n < 0 || 2 * n > mask + 1)
+  if (!keys || !slots || !entries || mask < 1 || ((mask + 1) & mask) || n < 0 || 2 * n > mask + 1)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(cache_index_build_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, keys, slots, n,
-                     idx_keys, idx_slots, uint64_t(mask));
+                     entries, uint64_t(mask));
   return hipGetLastError();
 }
 

@@ -128,8 +128,9 @@ class HotRowCache:
     """This rank's replica of hot rows of tables owned by other ranks.
 
     ``capacity`` rows ([capacity, 64] bf16) behind two open-addressing index
-    buffers (keys int64 [H] | slots int32 [H], H = the power of two >= 2 x
-    capacity): one serves the steps while :meth:`refresh` rebuilds the other.
+    buffers ({key, slot} int64 entries [H, 2], H = the power of two >= 2 x
+    capacity; one 16-byte load per probe): one serves the steps while
+    :meth:`refresh` rebuilds the other.
     ``desc`` (int64 [5], read by the kernels at their start) = {active index,
     0, H - 1, rows, capacity}: a refresh changes only its first word (one
     8-byte store), so a kernel sees the old index or the new one, whole.
@@ -150,7 +151,7 @@ class HotRowCache:
         self.device = dev
         i64 = dict(dtype=torch.int64, device=dev)
         self.rows = torch.zeros(self.cap, D, dtype=peer.dtype, device=dev)
-        self.index = [torch.full((self.H + self.H // 2,), -1, **i64) for _ in range(2)]
+        self.index = [torch.full((self.H, 2), -1, **i64) for _ in range(2)]  # {key, slot} entries
         self.desc = torch.tensor([0, 0, self.H - 1, self.rows.data_ptr() if dev.type == "cuda" else 0, self.cap], **i64)
         self.stats = torch.zeros(128, **i64)
         self.ring = torch.full((max(1, int(ring_cap)),), -1, **i64)
@@ -171,10 +172,6 @@ class HotRowCache:
     def kernel_args(self) -> dict:
         return dict(cache=self.desc, stats=self.stats, ring=self.ring, ring_ctr=self.ring_ctr,
                     sample_every=self.sample_every)
-
-    def index_views(self, side: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        buf = self.index[side]
-        return buf[:self.H], buf[self.H:].view(torch.int32)
 
     # -- counters ---------------------------------------------------------------
     def counts(self) -> Tuple[int, int]:
@@ -257,12 +254,12 @@ class HotRowCache:
             keys, slots = keys[order].contiguous(), slots[order].contiguous()
             side = 0 if self.active != 0 else 1
             if cuda:
-                ik, isl = self.index_views(side)
-                ik.fill_(-1)
+                idx = self.index[side]
+                idx.fill_(-1)
                 if keys.numel():
                     from ..ops import hip
 
-                    hip().cache_index_build(keys, slots, ik, isl)
+                    hip().cache_index_build(keys, slots, idx)
                 self.desc[0:1].fill_(self.index[side].data_ptr())  # one 8-byte store: the swap
         if cuda:
             self._stream.synchronize()
