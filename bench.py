@@ -487,15 +487,16 @@ def run_live(a, ctx, cfg, model, eng, B):
             "hot_row_cache": None,
         }
         if cache is not None:
-            hits, misses = cache_counts
+            hits, misses = cache_counts  # counted on every sample_every-th candidate
             steps = max(1, st_load["steps"] - steps0)
-            lookups_per_step = (hits + misses) / steps
+            lookups_per_step = (hits + misses) * cache.count_scale / steps
             extra["embedding_exchange"]["hot_row_cache"] = {
                 **cache.describe(),
                 "hits": hits, "misses": misses, "hit_rate": round(hits / max(1, hits + misses), 4),
                 # measured over the throughput run (warmup + timed steps)
                 "remote_lookups_per_step": round(lookups_per_step, 1),
-                "xgmi_bytes_per_step_per_rank": int(misses / steps * cfg.embed_dim * 2),
+                "xgmi_bytes_per_step_per_rank": int(misses * cache.count_scale / steps * cfg.embed_dim * 2),
+                "counted_every": cache.count_scale,
                 # the pool repeats: the same hot set on a fresh draw of the stream
                 "hit_rate_fresh_stream": fresh_hit_rate(cfg, model, ctx),
             }

@@ -799,7 +799,7 @@ torch::Tensor shard_route(c10::optional<torch::Tensor> ids, c10::optional<torch:
 // PeerTables (parallel/hot_cache.py): cbase int64 [W * max_chunks] (device
 // addresses of every rank's store chunks), towner int32 [T], toff int64 [T],
 // trows int64 [T], tremote int32 [T]; the replica cache: cache int64 [5],
-// stats int64 [128], ring int64 [cap], ring_ctr int64 [1]
+// stats int64 [128], ring int64 [cap] (64 segments), ring_ctr int64 [64]
 static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Tensor& cbase,
                                       const torch::Tensor& towner, const torch::Tensor& toff,
                                       const torch::Tensor& trows, const torch::Tensor& tremote, int64_t chunk_shift,
@@ -842,8 +842,11 @@ static dtfs::PeerLookupArgs peer_args(const torch::Tensor& ref, const torch::Ten
     TORCH_CHECK(ring_ctr.has_value(), "ring needs ring_ctr");
     check_same_dev(ref, *ring, "ring");
     check_same_dev(ref, *ring_ctr, "ring_ctr");
-    TORCH_CHECK(ring->scalar_type() == torch::kInt64 && ring->numel() >= 1 && ring->is_contiguous(), "ring: int64 [cap]");
-    TORCH_CHECK(ring_ctr->scalar_type() == torch::kInt64 && ring_ctr->numel() == 1, "ring_ctr: int64 [1]");
+    TORCH_CHECK(ring->scalar_type() == torch::kInt64 && ring->numel() >= 64 && ring->numel() % 64 == 0 &&
+                    ring->is_contiguous(),
+                "ring: int64 [cap], cap a multiple of 64");
+    TORCH_CHECK(ring_ctr->scalar_type() == torch::kInt64 && ring_ctr->numel() == 64 && ring_ctr->is_contiguous(),
+                "ring_ctr: int64 [64]");
     p.ring = ring->data_ptr<int64_t>();
     p.ring_ctr = reinterpret_cast<unsigned long long*>(ring_ctr->data_ptr<int64_t>());
     p.ring_cap = ring->numel();

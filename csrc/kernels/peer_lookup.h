@@ -76,6 +76,14 @@ __device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const C
   return src;
 }
 
+// Candidates whose lookups are counted and sampled: every sample_every-th
+// (all of them when sample_every <= 1). Counting a sample keeps the counters'
+// atomics (one per wave and kind, on 128 addresses) off most waves - counting
+// every lookup cost ~3 us per 16384-candidate step (tools/studies/peer_lookup_bench.py).
+__device__ __forceinline__ bool peer_sampled(const PeerLookupArgs& p, int64_t b) {
+  return p.sample_every <= 1 || b % p.sample_every == 0;
+}
+
 // Wave-aggregated counters: one atomic per wave and kind. Called by every
 // lane of the wave (ballots); lanes with counted = false contribute nothing.
 __device__ __forceinline__ void peer_count(const PeerLookupArgs& p, int hit, bool counted) {
@@ -89,20 +97,24 @@ __device__ __forceinline__ void peer_count(const PeerLookupArgs& p, int hit, boo
   }
 }
 
-// Push the keys of the active lanes into the sample ring (wrapping).
+// Push the keys of the active lanes into the sample ring: 64 segments of
+// ring_cap / 64 keys, each with its own write counter ring_ctr[block % 64]
+// (wrapping), so the pushes of concurrent waves spread over 64 addresses.
 __device__ __forceinline__ void ring_push(const PeerLookupArgs& p, int64_t key, bool active) {
-  if (!p.ring || p.ring_cap < 1) return;
+  if (!p.ring || p.ring_cap < 64) return;
   const uint64_t m = __ballot(active);
   if (!m) return;
   const int lane = threadIdx.x & 63;
   const int leader = __ffsll((unsigned long long)m) - 1;
+  const int seg = blockIdx.x & 63;
+  const uint64_t seg_cap = uint64_t(p.ring_cap) / 64;
   unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(p.ring_ctr, (unsigned long long)__popcll(m));
+  if (lane == leader) base = atomicAdd(p.ring_ctr + seg, (unsigned long long)__popcll(m));
   const uint32_t lo = __shfl(uint32_t(base), leader), hi = __shfl(uint32_t(base >> 32), leader);
   base = (uint64_t(hi) << 32) | lo;
   if (active) {
     const int below = __popcll(m & ((1ull << lane) - 1ull));
-    p.ring[int64_t((base + below) % uint64_t(p.ring_cap))] = key;
+    p.ring[int64_t(seg * seg_cap + (base + below) % seg_cap)] = key;
   }
 }
 

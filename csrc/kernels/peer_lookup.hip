@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(256) peer_bag_kernel(PeerLookupArgs p, const I
   ArenaRow ar{nullptr, nullptr, false, kArenaAllWeights, 4};
   if (arena && valid) ar = arena_row(arena, kArenaPayloadOff, b);
   const int64_t m = p.trows[t];
-  const bool sample = valid && c == 0 && p.sample_every > 0 && b % p.sample_every == 0;
+  const bool sample = valid && c == 0 && peer_sampled(p, b);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < hot; ++j) {  // uniform trip count: the ballots below see every lane
     const int col = col0 + t * hot + j;
@@ -50,8 +50,8 @@ __global__ void __launch_bounds__(256) peer_bag_kernel(PeerLookupArgs p, const I
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += w * bf2f(x[e]);
     }
-    peer_count(p, hit, valid && c == 0);
-    ring_push(p, (int64_t(t) << 40) | v, sample && hit >= 0);
+    peer_count(p, hit, sample);
+    ring_push(p, (int64_t(t) << 40) | v, sample && hit >= 0 && p.sample_every > 0);
   }
   if (valid) {
     bf16x8 o;
@@ -107,7 +107,7 @@ hipError_t launch_peer_bag(const PeerLookupArgs& p, const void* ids, bool ids64,
   if (!p.cbase || !p.towner || !p.toff || !p.trows || !p.tremote || p.max_chunks < 1 || p.chunk_shift < 1 ||
       p.chunk_shift > 40 || T < 1 || hot < 1 || col0 < 0 || !out ||
       (!arena && (!ids || !wts || ldi < col0 + T * hot || ldw < col0 + T * hot)) ||
-      (p.ring && (!p.ring_ctr || p.ring_cap < 1)))
+      (p.ring && (!p.ring_ctr || p.ring_cap < 64)))
     return hipErrorInvalidValue;
   const int64_t threads = int64_t(B) * T * 8;
   const dim3 grid(unsigned((threads + 255) / 256)), block(256);

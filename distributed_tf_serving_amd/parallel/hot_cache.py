@@ -154,8 +154,8 @@ class HotRowCache:
         self.index = [torch.full((self.H, 2), -1, **i64) for _ in range(2)]  # {key, slot} entries
         self.desc = torch.tensor([0, 0, self.H - 1, self.rows.data_ptr() if dev.type == "cuda" else 0, self.cap], **i64)
         self.stats = torch.zeros(128, **i64)
-        self.ring = torch.full((max(1, int(ring_cap)),), -1, **i64)
-        self.ring_ctr = torch.zeros(1, **i64)
+        self.ring = torch.full((max(64, -(-int(ring_cap) // 64) * 64),), -1, **i64)  # 64 segments
+        self.ring_ctr = torch.zeros(64, **i64)
         self.keys = torch.empty(0, **i64)          # the active hot set, sorted
         self.slots = torch.empty(0, dtype=torch.int32, device=dev)
         self.cand_keys = torch.empty(0, **i64)     # candidates with decayed counts
@@ -175,9 +175,15 @@ class HotRowCache:
 
     # -- counters ---------------------------------------------------------------
     def counts(self) -> Tuple[int, int]:
-        """(hits, misses) of remote lookups since the last reset."""
+        """(hits, misses) of the counted remote lookups since the last reset:
+        those of every ``sample_every``-th candidate (all when it is <= 1);
+        :attr:`count_scale` x these estimates the totals."""
         s = self.stats.view(64, 2).sum(0).cpu()
         return int(s[0]), int(s[1])
+
+    @property
+    def count_scale(self) -> int:
+        return max(1, self.sample_every)
 
     def hit_rate(self) -> float:
         h, m = self.counts()
@@ -201,6 +207,7 @@ class HotRowCache:
         self.stats[1] += misses
 
     def push_cpu(self, keys: torch.Tensor) -> None:
+        """The kernels' ring push (one segment: the whole ring, counter 0)."""
         n = keys.numel()
         if n == 0:
             return
@@ -223,8 +230,8 @@ class HotRowCache:
         if cuda:  # every step that may read the previously replaced index is done
             torch.cuda.synchronize(self.device)
         with (torch.cuda.stream(self._stream) if cuda else nullcontext()):
-            n = int(self.ring_ctr.item())
-            samp = self.ring[:min(n, self.ring.numel())].clone()
+            samp = self.ring.clone()
+            self.ring.fill_(-1)  # each refresh counts only the keys pushed since the last one
             self.ring_ctr.zero_()
             samp = samp[samp >= 0]
             if samp.numel():
@@ -325,10 +332,11 @@ def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.T
         hit = remote & (slot >= 0)
         if bool(hit.any()):
             rows[hit] = cache.rows.cpu()[slot[hit]].float()
-        cache.count_cpu(int(hit.sum()), int((remote & ~hit).sum()))
+        b = torch.arange(B, dtype=torch.int64).repeat_interleave(T * hot)
+        sampled = (b % cache.sample_every == 0) if cache.sample_every > 1 else torch.ones_like(b, dtype=torch.bool)
+        cache.count_cpu(int((hit & sampled).sum()), int((remote & ~hit & sampled).sum()))
         if cache.sample_every > 0:
-            b = torch.arange(B, dtype=torch.int64).repeat_interleave(T * hot)
-            cache.push_cpu(keys[remote & (b % cache.sample_every == 0)])
+            cache.push_cpu(keys[remote & sampled])
     if wts is None:
         out = rows.view(B, T, D)
     else:

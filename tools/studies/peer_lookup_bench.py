@@ -73,6 +73,16 @@ def main() -> None:
     cache.reset_counts()
     out["peer_cache_us"] = round(timed(lambda ids: ops.dot_interaction_gather_peer(dense, ids, peer, cache)), 2)
     h, m = cache.counts()
+    from distributed_tf_serving_amd.ops import hip
+
+    # the same lookups without the counters / sampling, and the counters alone
+    out["peer_cache_no_counters_us"] = round(timed(lambda ids: hip().dot_interaction_gather_peer(
+        dense, ids, None, 0, cache=cache.desc, **peer.kernel_args())), 2)
+    out["peer_counters_only_us"] = round(timed(lambda ids: hip().dot_interaction_gather_peer(
+        dense, ids, None, 0, stats=cache.stats, ring=cache.ring, ring_ctr=cache.ring_ctr, sample_every=8,
+        **peer.kernel_args())), 2)
+    out["peer_stats_only_us"] = round(timed(lambda ids: hip().dot_interaction_gather_peer(
+        dense, ids, None, 0, stats=cache.stats, **peer.kernel_args())), 2)
     out["hit_rate"] = round(h / max(1, h + m), 4)
     out["hot_rows"] = int(cache.keys.numel())
     # the same hot set on a fresh draw of the stream
