@@ -183,9 +183,9 @@ __global__ void __launch_bounds__(256) dot_interact_gather_kernel(
       src = table + min(offset_f[t] + v, table_rows - 1) * D;
     }
   }
-  if (peer.cbase && peer_sampled(peer, b)) {  // wave-uniform; converged: the ballots see every lane
-    peer_count(peer, hit, h == 0);  // lanes h = 1 repeat h = 0's rows
-    ring_push(peer, key, h == 0 && hit >= 0 && peer.sample_every > 0);
+  if (peer.cbase) {  // wave-uniform branches; converged: the ballots see every lane
+    if (peer_counted(peer, b)) peer_count(peer, hit, h == 0);  // lanes h = 1 repeat h = 0's rows
+    if (peer.sample_every > 0 && peer_sampled(peer, b)) ring_push(peer, key, h == 0 && hit >= 0);
   }
   bf16x8 x[4];
 #pragma unroll

@@ -225,10 +225,11 @@ hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
 // int64 [mask + 1][2] = {key, slot}, key -1 = empty; 0 = no index), unused,
 // mask, rows [cap][64] bf16, cap}, read by each wave at its start (the host
 // swaps indices by rewriting word 0). Candidates b with b % sample_every ==
-// 0 (all when sample_every <= 1) are counted - stats [128]: hits at 2i,
-// misses at 2i + 1 (i = block % 64) - and, when sample_every > 0, push their
-// remote keys (t << 40 | v) into ring: 64 segments of ring_cap / 64 keys,
-// segment block % 64 written at ring_ctr[block % 64] (int64 [64], wrapping).
+// sample_every / 2 (all when sample_every <= 1) are counted - stats [128]:
+// hits at 2i, misses at 2i + 1 (i = block % 64); when sample_every > 0,
+// candidates with b % sample_every == 0 push their remote keys (t << 40 | v)
+// into ring: 64 segments of ring_cap / 64 keys, segment block % 64 written at
+// ring_ctr[block % 64] (int64 [64], wrapping).
 struct PeerLookupArgs {
   const int64_t* cbase = nullptr;
   const int32_t* towner = nullptr;

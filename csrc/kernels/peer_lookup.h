@@ -76,12 +76,18 @@ __device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const C
   return src;
 }
 
-// Candidates whose lookups are counted and sampled: every sample_every-th
-// (all of them when sample_every <= 1). Counting a sample keeps the counters'
-// atomics (one per wave and kind, on 128 addresses) off most waves - counting
-// every lookup cost ~3 us per 16384-candidate step (tools/studies/peer_lookup_bench.py).
+// Candidates whose remote keys are sampled for the hot set (b % sample_every
+// == 0) and, disjoint from them, candidates whose lookups are counted (b %
+// sample_every == sample_every / 2): a repeating request stream then cannot
+// report its own samples back as hits. sample_every <= 1: every candidate is
+// both. Counting a subset keeps the counters' atomics (one per wave and kind,
+// on 128 addresses) off most waves - counting every lookup cost ~3 us per
+// 16384-candidate step (tools/studies/peer_lookup_bench.py).
 __device__ __forceinline__ bool peer_sampled(const PeerLookupArgs& p, int64_t b) {
   return p.sample_every <= 1 || b % p.sample_every == 0;
+}
+__device__ __forceinline__ bool peer_counted(const PeerLookupArgs& p, int64_t b) {
+  return p.sample_every <= 1 || b % p.sample_every == p.sample_every / 2;
 }
 
 // Wave-aggregated counters: one atomic per wave and kind. Called by every

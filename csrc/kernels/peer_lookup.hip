@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(256) peer_bag_kernel(PeerLookupArgs p, const I
   ArenaRow ar{nullptr, nullptr, false, kArenaAllWeights, 4};
   if (arena && valid) ar = arena_row(arena, kArenaPayloadOff, b);
   const int64_t m = p.trows[t];
-  const bool sample = valid && c == 0 && peer_sampled(p, b);
+  const bool sample = valid && c == 0 && p.sample_every > 0 && peer_sampled(p, b);
+  const bool counted = valid && c == 0 && peer_counted(p, b);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < hot; ++j) {  // uniform trip count: the ballots below see every lane
     const int col = col0 + t * hot + j;
@@ -50,8 +51,8 @@ __global__ void __launch_bounds__(256) peer_bag_kernel(PeerLookupArgs p, const I
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += w * bf2f(x[e]);
     }
-    peer_count(p, hit, sample);
-    ring_push(p, (int64_t(t) << 40) | v, sample && hit >= 0 && p.sample_every > 0);
+    peer_count(p, hit, counted);
+    ring_push(p, (int64_t(t) << 40) | v, sample && hit >= 0);
   }
   if (valid) {
     bf16x8 o;

@@ -176,8 +176,9 @@ class HotRowCache:
     # -- counters ---------------------------------------------------------------
     def counts(self) -> Tuple[int, int]:
         """(hits, misses) of the counted remote lookups since the last reset:
-        those of every ``sample_every``-th candidate (all when it is <= 1);
-        :attr:`count_scale` x these estimates the totals."""
+        those of every ``sample_every``-th candidate, offset by half a period
+        from the candidates whose keys are sampled for the hot set (all when
+        ``sample_every`` <= 1); :attr:`count_scale` x these estimates the totals."""
         s = self.stats.view(64, 2).sum(0).cpu()
         return int(s[0]), int(s[1])
 
@@ -333,9 +334,11 @@ def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.T
         if bool(hit.any()):
             rows[hit] = cache.rows.cpu()[slot[hit]].float()
         b = torch.arange(B, dtype=torch.int64).repeat_interleave(T * hot)
-        sampled = (b % cache.sample_every == 0) if cache.sample_every > 1 else torch.ones_like(b, dtype=torch.bool)
-        cache.count_cpu(int((hit & sampled).sum()), int((remote & ~hit & sampled).sum()))
-        if cache.sample_every > 0:
+        n = cache.sample_every
+        sampled = (b % n == 0) if n > 1 else torch.ones_like(b, dtype=torch.bool)
+        counted = (b % n == n // 2) if n > 1 else torch.ones_like(b, dtype=torch.bool)
+        cache.count_cpu(int((hit & counted).sum()), int((remote & ~hit & counted).sum()))
+        if n > 0:
             cache.push_cpu(keys[remote & sampled])
     if wts is None:
         out = rows.view(B, T, D)
