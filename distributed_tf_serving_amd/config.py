@@ -48,10 +48,11 @@ class ModelConfig:
     bottom_mlp: Tuple[int, ...] = (512, 256, 64)   # dlrm bottom MLP (last = embed_dim)
     table_rows: int = 1_000_000       # dlrm: rows per sparse table
     multi_hot: int = 1                # dlrm: ids per sparse table (> 1: weighted sum-pooled bag, K1b)
-    # dlrm tables sharded over ranks: "alltoall" (ids + rows through RCCL) or
+    # dlrm tables sharded over ranks: "alltoall" (ids + rows through RCCL),
     # "peer" (rows loaded from the owner's HBM over xGMI, hot remote rows from a
-    # per-rank replica cache of hot_cache_rows rows; parallel/hot_cache.py)
-    embedding_exchange: str = "alltoall"
+    # per-rank replica cache of hot_cache_rows rows; parallel/hot_cache.py) or
+    # "auto" (peer on GPUs that can all load from each other, else alltoall)
+    embedding_exchange: str = "auto"
     hot_cache_rows: int = 1 << 20
     param_dtype: str = "bf16"         # storage dtype of embeddings + dense weights
     gemm_dtype: str = "bf16"          # bf16 | fp8 (dcn_v2 towers on CDNA4 fp8 MFMA)

@@ -431,6 +431,22 @@ class ShardedEmbedding(nn.Module):
         return bufs["emb_all"][rows]
 
 
+def peer_access_everywhere(ctx: DistContext, device: torch.device, group=None) -> bool:
+    """True when this job's ranks are on GPUs that can all load from each
+    other's memory (collective at world > 1): the peer exchange's condition.
+    One rank, or the CPU: False (nothing to exchange / no peer mapping)."""
+    world = ctx.world if ctx.is_distributed else 1
+    if device.type != "cuda" or world == 1:
+        return False
+    mine = torch.cuda.current_device() if device.index is None else device.index
+    devs: list = [None] * world
+    dist.all_gather_object(devs, mine, group=group)
+    ok = all(d == mine or torch.cuda.can_device_access_peer(mine, d) for d in devs)
+    votes: list = [None] * world
+    dist.all_gather_object(votes, bool(ok), group=group)
+    return all(votes)
+
+
 def build_parallel_model(cfg: ModelConfig, device, ctx: Optional[DistContext] = None, shard_tables: str = "auto",
                          policy: str = "auto", budget_bytes: int = int(0.8 * MI355X_HBM_BYTES), group=None):
     """The model a rank serves: DLRM tables are sharded across the process
@@ -464,6 +480,8 @@ class ShardedDLRM(nn.Module):
         self.hot = max(1, int(getattr(cfg, "multi_hot", 1)))
         world = ctx.world if ctx.is_distributed else 1
         exchange = getattr(cfg, "embedding_exchange", "alltoall")
+        if exchange == "auto":
+            exchange = "peer" if peer_access_everywhere(ctx, torch.device(device), group) else "alltoall"
         if (self.hot > 1 or exchange == "peer") and policy == "auto":
             # multi-hot bags pool on their table's owner; peers read whole
             # tables where they live

@@ -73,7 +73,7 @@ def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
            "--model", "dlrm", "--table-rows", "1000000", "--steps", "20", "--warmup", "4", "--prime-steps", "10",
            "--requests-per-gpu", "4", "--request-rows", "96", "--pool", "8", "--client-threads", "2",
-           "--qps", "0", "--step-timeout-s", "20"]
+           "--qps", "0", "--step-timeout-s", "20", "--exchange", "alltoall"]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
                DTFS_PEER_COMM=str(peer))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
