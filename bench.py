@@ -125,6 +125,9 @@ def parse_args():
                          "HBM over xGMI behind a per-rank hot-row replica cache (default: the preset's)")
     ap.add_argument("--hot-cache-rows", type=int, default=None,
                     help="peer exchange: replica cache rows per rank (default: the config's; 0 = no cache)")
+    ap.add_argument("--cache-learn-rounds", type=int, default=6,
+                    help="peer exchange: untimed (max(8, warmup)-step run + cache refresh) rounds before the clock "
+                         "(a server refreshes every second)")
     ap.add_argument("--small-buckets", default=None,
                     help="extra padding buckets (rows per GPU) below the full step, so a lightly loaded server "
                          "runs a step sized to what is queued (TF-Serving allowed_batch_sizes; at N > 1 every "
@@ -416,7 +419,7 @@ def run_live(a, ctx, cfg, model, eng, B):
         # peer exchange: serve a few steps so the kernels sample the stream,
         # then install the hot set (the refresher is off while the clock runs:
         # a synthetic stream's hot set does not drift)
-        for _ in range(3):
+        for _ in range(a.cache_learn_rounds):
             live.run_load(pool, warmup=0, count=max(8, a.warmup) * n_req, concurrency=conc,
                           threads=a.client_threads, timeout_us=timeout_us)
             cache.refresh()
