@@ -204,6 +204,12 @@ class LiveScheduler:
         if seg is not None:  # shared-arena scatter: what this rank copied for its shares
             st["scatter_h2d_bytes"] = int(seg.h2d_bytes)
             st["scatter_h2d_steps"] = int(seg.h2d_steps)
+        cache = getattr(self.eng.ex.model, "cache", None)
+        if cache is not None:  # peer exchange: the hot-row replica cache (counted candidates)
+            h, m = cache.counts()
+            st["hot_cache_rows"] = int(cache.keys.numel())
+            st["hot_cache_refreshes"] = int(cache.refreshes)
+            st["hot_cache_hits"], st["hot_cache_misses"] = h, m
         # the names the monitoring endpoint reads (serving/monitoring.py)
         st.setdefault("batches", st["steps"])
         st.setdefault("batched_rows", st["rows"])

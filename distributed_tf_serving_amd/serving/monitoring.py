@@ -43,6 +43,11 @@ _SCHED = {
     "batched_rows": ("batching_rows", "candidate rows batched", True),
     "steps": ("gpu_steps", "serving steps completed on the device", True),
     "rows_served": ("rows_served", "candidate rows scored", True),
+    # peer-exchange DLRM: the hot-row replica cache (hits / misses of the counted candidates)
+    "hot_cache_rows": ("hot_cache_rows", "remote table rows held in this rank's replica cache", False),
+    "hot_cache_refreshes": ("hot_cache_refreshes", "replica cache refreshes", True),
+    "hot_cache_hits": ("hot_cache_hits", "counted remote lookups served by the replica cache", True),
+    "hot_cache_misses": ("hot_cache_misses", "counted remote lookups read from the owner's HBM", True),
 }
 
 

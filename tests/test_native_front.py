@@ -148,9 +148,16 @@ def test_deadline_exceeded_on_the_client_and_server_survives(front):
     ch = _channel(fr.port)
     synth = SyntheticRequests(fields=F, seed=14)
     data = synth.serialized(8)
-    with pytest.raises(grpc.RpcError) as e:
-        ch.unary_unary(PREDICT)(data, timeout=1e-4)  # expires before (or while) it is served
-    assert e.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+    # a 100 us deadline expires before (or while) the call is served - unless
+    # the in-process server answers inside it, so try a few times
+    codes = []
+    for _ in range(20):
+        try:
+            assert _scores(ch.unary_unary(PREDICT)(data, timeout=1e-4)).shape == (8,)
+        except grpc.RpcError as e:
+            codes.append(e.code())
+            break
+    assert codes == [grpc.StatusCode.DEADLINE_EXCEEDED], codes
     # the connection and the server keep working after the cancelled stream
     assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (8,)
     ch.close()
