@@ -1964,7 +1964,9 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
     //        81.8 us vs 87.2 for 8-wave 128x128); a ragged last column panel
     //        (N = 2752) or fewer tiles than CUs loses to 14
     //  * 14: >= 512 tiles of 128x128: 8 waves per block (2 per SIMD), 2 blocks/CU
-    //        (46.1 us vs 48.9 for 4 waves at 8192x1024x2752)
+    //        (46.1 us vs 48.9 for 4 waves at 8192x1024x2752; DeepFM's GEMM2
+    //        16384x512x1024: 22.6 us vs 24.1 for one 128x256 or 256x128 tile
+    //        per CU and 30.3 for the 8-phase 256x256, round 4)
     //  * 10: >= 512 tiles of 128x64 (8192 x 512: 15.5 us vs 16.9 for 64x64)
     //  *  4: otherwise (narrow N): 64x64 LDS-DMA
     // K not a multiple of one 128-byte K tile: the register-staged gemm_kernel.
