@@ -72,7 +72,19 @@ StepRunner::~StepRunner() {
 }
 
 void StepRunner::ensure_aux_stream() {
-  if (!ingress_) ck(hipStreamCreateWithFlags(&ingress_, hipStreamNonBlocking), "hipStreamCreate(ingress)");
+  if (ingress_) return;
+  // DTFS_AUX_CUS=n (A/B only): the aux lane's queue limited to n of the CUs
+  // (the first n bits of the CU mask), so step k+1's resolve pass takes fewer
+  // CU slots from step k's GEMMs
+  const char* e = std::getenv("DTFS_AUX_CUS");
+  const int n = e ? std::atoi(e) : 0;
+  if (n > 0 && n < 256) {
+    uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
+    ck(hipExtStreamCreateWithCUMask(&ingress_, 8, mask), "hipExtStreamCreateWithCUMask(ingress)");
+    return;
+  }
+  ck(hipStreamCreateWithFlags(&ingress_, hipStreamNonBlocking), "hipStreamCreate(ingress)");
 }
 
 void StepRunner::ensure_fanout_streams() {
