@@ -226,3 +226,52 @@ def test_ipc_export_open_same_process(cuda):
     y = x[8:]
     h, off = hip().ipc_export(y)
     assert off >= 8 * 64 * 4 and isinstance(h, bytes)
+
+
+@pytest.mark.gpu
+def test_refresh_while_lookups_run(cuda):
+    """Refreshes (new rows copied into free slots, the other index built and
+    swapped in by one 8-byte store) while another thread keeps launching
+    cached lookups on its own stream: every lookup returns exactly the rows of
+    the uncached lookup, through hot-set turnover."""
+    import threading
+    import time
+
+    from distributed_tf_serving_amd import ops
+
+    p = _gpu_peer(cuda, chunk_shift=9)
+    c = HotRowCache(p, capacity=1024, ring_cap=1 << 14, sample_every=2)
+    g = torch.Generator().manual_seed(9)
+    B, T = 2048, p.T
+    # three batches whose hot ids differ: the hot set turns over as the mix shifts
+    batches = [(_skewed(B, T, g, hot_ids=48) + 100 * k).to(cuda) for k in range(3)]
+    dense = torch.randn(B, 64, generator=g).to(torch.bfloat16).to(cuda)
+    want = [ops.dot_interaction_gather_peer(dense, ids, p, None) for ids in batches]
+    torch.cuda.synchronize()
+    stop, errs, done = threading.Event(), [], [0]
+
+    def worker():
+        s = torch.cuda.Stream(cuda)
+        k = 0
+        with torch.cuda.stream(s):
+            while not stop.is_set():
+                z = ops.dot_interaction_gather_peer(dense, batches[k % 3], p, c)
+                s.synchronize()
+                if not torch.equal(z, want[k % 3]):
+                    errs.append(k)
+                k += 1
+        done[0] = k
+
+    t = threading.Thread(target=worker)
+    t.start()
+    try:
+        for _ in range(12):
+            time.sleep(0.02)
+            c.refresh()
+    finally:
+        stop.set()
+        t.join(timeout=60)
+    assert not errs, errs[:5]
+    assert done[0] > 12 and c.refreshes == 12 and c.keys.numel() > 0
+    h, m = c.counts()
+    assert h > 0
