@@ -707,6 +707,8 @@ def main():
                 "path": ("served: native live server (batching, arena copy, parse, step, encode) driven by "
                          "in-process native client threads"),
                 "two_lane_buckets": sorted(eng._program_buckets),  # steps run as a two-lane program
+                # CUs of the program's aux lane (0: unmasked; step_runner.cpp ensure_aux_stream)
+                "aux_lane_cus": int(getattr(getattr(eng, "_runner", None), "aux_cus", 0) or 0),
             },
         }
         out.update(extra)

@@ -1708,6 +1708,7 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<dtfs::runtime::StepRunner>(m, "StepRunner",
                                         "Native per-GPU step launcher: SDMA H2D + graph launch per pipeline slot")
       .def(py::init<int, int>(), py::arg("device"), py::arg("slots"))
+      .def_property_readonly("aux_cus", &dtfs::runtime::StepRunner::aux_cus)
       .def(
           "launch",
           [](dtfs::runtime::StepRunner& r, int slot, torch::Tensor dst, torch::Tensor src, int64_t nbytes,

@@ -71,17 +71,28 @@ StepRunner::~StepRunner() {
     if (s) hipStreamDestroy(s);
 }
 
-void StepRunner::ensure_aux_stream() {
+void StepRunner::ensure_aux_stream(bool program) {
   if (ingress_) return;
-  // DTFS_AUX_CUS=n (A/B only): the aux lane's queue limited to n of the CUs
-  // (the first n bits of the CU mask), so step k+1's resolve pass takes fewer
-  // CU slots from step k's GEMMs
-  const char* e = std::getenv("DTFS_AUX_CUS");
-  const int n = e ? std::atoi(e) : 0;
+  // A step program's aux lane (only step programs create it first; the fan-out
+  // streams create it plain) runs on half of the CUs: step k+1's resolve pass
+  // then leaves the other half to step k's GEMMs and head instead of taking CU
+  // slots all over the chip - DeepFM 111.0 / 111.1 vs 108.9 / 108.6 M and
+  // 103.0 / 103.3 vs 102.0 / 102.2 M on two boxes; 64 CUs was unstable (76.7 /
+  // 106.8 M), 96 / 160 / 192 no better than none (profiles/r04_session2.md).
+  // DTFS_AUX_CUS=n overrides the CU count (0: no mask).
+  int n = 0;
+  if (program) {
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_);
+    n = cus >= 256 ? cus / 2 : 0;
+    if (const char* e = std::getenv("DTFS_AUX_CUS")) n = std::atoi(e);
+    if (n >= cus) n = 0;
+  }
   if (n > 0 && n < 256) {
-    uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the first n bits
     for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
     ck(hipExtStreamCreateWithCUMask(&ingress_, 8, mask), "hipExtStreamCreateWithCUMask(ingress)");
+    aux_cus_ = n;
     return;
   }
   ck(hipStreamCreateWithFlags(&ingress_, hipStreamNonBlocking), "hipStreamCreate(ingress)");
@@ -89,7 +100,7 @@ void StepRunner::ensure_aux_stream() {
 
 void StepRunner::ensure_fanout_streams() {
   if (egress_) return;
-  ensure_aux_stream();
+  ensure_aux_stream(false);
   ck(hipStreamCreateWithFlags(&egress_, hipStreamNonBlocking), "hipStreamCreate(egress)");
   in_done_.resize(done_.size());
   fwd_done_.resize(done_.size());
@@ -253,7 +264,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
-  ensure_aux_stream();  // the aux lane is the ingress stream
+  ensure_aux_stream(true);  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
     // lane-to-lane dependencies stay on the device: no system-scope release

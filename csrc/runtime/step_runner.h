@@ -150,6 +150,7 @@ class StepRunner {
   bool query(int slot);
   // Microseconds between the slot's last H2D start and compute end (diagnostic).
   int slots() const { return int(done_.size()); }
+  int aux_cus() const { return aux_cus_; }  // CUs of the step-program aux lane (0: unmasked / not created)
   hipStream_t compute_stream() const { return compute_; }
   hipStream_t copy_stream() const { return copy_; }
   // Local steps: the launcher waits on the host for each step's H2D before it
@@ -175,11 +176,12 @@ class StepRunner {
   // another thread than the launcher)
   std::unique_ptr<std::atomic<bool>[]> observed_;
   void ensure_fanout_streams();
-  void ensure_aux_stream();
+  void ensure_aux_stream(bool program);
   hipStream_t copy_ = nullptr, compute_ = nullptr, ingress_ = nullptr, egress_ = nullptr;
   std::vector<hipEvent_t> h2d_done_, done_, in_done_, fwd_done_;
   std::vector<hipEvent_t> prog_ev_;  // [slot * kProgEvents + k], created on first program launch
   int last_prog_slot_ = -1;
+  int aux_cus_ = 0;  // CUs of the program aux lane's queue (0: unmasked)
   std::vector<char> used_;  // not vector<bool>: written by the launcher, read by the waiter
 };
 
