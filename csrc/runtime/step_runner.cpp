@@ -280,12 +280,25 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alias a queue and serialise the step)
   h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
+  // DTFS_BIND_DONE=1 (A/B only): the step-done event rides on the last
+  // kernel's dispatch (hipExtLaunchKernel stop event) when the program ends in
+  // a compute-lane kernel sequence, instead of a separate marker packet
+  static const bool bind_done = [] {
+    const char* e = std::getenv("DTFS_BIND_DONE");
+    return e && std::atoi(e) == 1;
+  }();
+  const ProgOp* last = p.ops.empty() ? nullptr : &p.ops.back();
+  const bool bound = bind_done && last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
   for (const ProgOp& o : p.ops) {
     hipStream_t st = lanes[o.lane];
     switch (o.kind) {
       case ProgOp::kKernels:
-        if (o.seq) o.seq->launch(st, nullptr, false, skip_varint);
-        else ck(hipGraphLaunch(o.graph, st), "hipGraphLaunch(program)");
+        if (o.seq) {
+          if (bound && &o == last) o.seq->launch(st, done_[slot], true, skip_varint);
+          else o.seq->launch(st, nullptr, false, skip_varint);
+        } else {
+          ck(hipGraphLaunch(o.graph, st), "hipGraphLaunch(program)");
+        }
         break;
       case ProgOp::kAllToAll:
         o.comm->alltoall(o.send, o.recv, o.bytes, st);
@@ -311,7 +324,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
         break;
     }
   }
-  ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
+  if (!bound) ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
   used_[slot] = 1;
   last_prog_slot_ = slot;
 }
