@@ -280,12 +280,18 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alias a queue and serialise the step)
   h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
-  // DTFS_BIND_DONE=1 (A/B only): the step-done event rides on the last
-  // kernel's dispatch (hipExtLaunchKernel stop event) when the program ends in
-  // a compute-lane kernel sequence, instead of a separate marker packet
+  // The step-done event rides on the last kernel's dispatch (hipExtLaunchKernel
+  // stop event) when the program ends in a compute-lane kernel sequence,
+  // instead of a separate marker packet behind it: one packet less at the step
+  // boundary, DeepFM 112.2 / 112.7 / 111.3 vs 110.4 / 110.1 / 109.7 M
+  // interleaved (profiles/r04_session2.md). The event keeps its system-scope
+  // release (done_ events are created without hipEventDisableSystemFence, and a
+  // bound event sets the scope of the command it is bound to), so the scores
+  // the head kernel wrote to pinned host memory are visible when it signals.
+  // DTFS_BIND_DONE=0 restores the marker.
   static const bool bind_done = [] {
     const char* e = std::getenv("DTFS_BIND_DONE");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   const ProgOp* last = p.ops.empty() ? nullptr : &p.ops.back();
   const bool bound = bind_done && last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
