@@ -260,6 +260,22 @@ void StepProgram::validate() const {
   if (joined < aux_ops) throw std::invalid_argument("program: aux-lane work is not joined into the compute lane");
 }
 
+// The step-done event rides on the step's last kernel dispatch
+// (hipExtLaunchKernel stop event) instead of a separate marker packet behind
+// it: one packet less at the step boundary, DeepFM 112.2 / 112.7 / 111.3 vs
+// 110.4 / 110.1 / 109.7 M interleaved (profiles/r04_session2.md). The event
+// keeps its system-scope release (done_ events are created without
+// hipEventDisableSystemFence, and a bound event sets the scope of the command
+// it is bound to), so the scores the head kernel wrote to pinned host memory
+// are visible when it signals. DTFS_BIND_DONE=0 restores the marker.
+static bool bind_done_event() {
+  static const bool on = [] {
+    const char* e = std::getenv("DTFS_BIND_DONE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes,
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
@@ -280,19 +296,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alias a queue and serialise the step)
   h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
-  // The step-done event rides on the last kernel's dispatch (hipExtLaunchKernel
-  // stop event) when the program ends in a compute-lane kernel sequence,
-  // instead of a separate marker packet behind it: one packet less at the step
-  // boundary, DeepFM 112.2 / 112.7 / 111.3 vs 110.4 / 110.1 / 109.7 M
-  // interleaved (profiles/r04_session2.md). The event keeps its system-scope
-  // release (done_ events are created without hipEventDisableSystemFence, and a
-  // bound event sets the scope of the command it is bound to), so the scores
-  // the head kernel wrote to pinned host memory are visible when it signals.
-  // DTFS_BIND_DONE=0 restores the marker.
-  static const bool bind_done = [] {
-    const char* e = std::getenv("DTFS_BIND_DONE");
-    return !(e && std::atoi(e) == 0);
-  }();
+  const bool bind_done = bind_done_event();
   const ProgOp* last = p.ops.empty() ? nullptr : &p.ops.back();
   const bool bound = bind_done && last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
   for (const ProgOp& o : p.ops) {
@@ -350,7 +354,7 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d(slot, dst, src, nbytes, compute_, true);
-  seq->launch(compute_, done_[slot], false, skip_varint);
+  seq->launch(compute_, done_[slot], bind_done_event(), skip_varint);
   used_[slot] = 1;
 }
 
@@ -361,7 +365,7 @@ void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d_copies(slot, dst, copies, compute_, true);
   if (seq) {
-    seq->launch(compute_, done_[slot], false, skip_varint);
+    seq->launch(compute_, done_[slot], bind_done_event(), skip_varint);
   } else {
     ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
     ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
