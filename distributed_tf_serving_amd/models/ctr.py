@@ -349,12 +349,27 @@ class DCNv2(CTRModel):
             return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
-    def _forward(self, ids, wts, out=None):
+    # the fp8 gather of step k+1 on the aux lane while step k's cross GEMMs run
+    # (the two-lane step program of CTRModel.build_program)
+    resolve_lane = True
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
+        return (on_gpu and self.fp8 and not self.low_rank and self.cfg.num_fields <= 64
+                and ids.shape[0] >= 8192)
+
+    def _resolve(self, ids, wts):
+        x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
+        return x0, tuple(q0)
+
+    def _forward(self, ids, wts, out=None, resolved=None):
         # fp8 towers: x0 is quantised once, for the first cross layer AND the
         # first MLP layer (both read it) - by the gather itself, which holds each
         # row in one wave's registers (ops.embed_fp8; no separate quant pass)
         fp8_full = self.fp8 and not self.low_rank
-        if fp8_full and self.cfg.num_fields <= 64:
+        if resolved is not None:  # gathered on the aux lane (resolve_lane)
+            x0, q0 = resolved
+        elif fp8_full and self.cfg.num_fields <= 64:
             x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
             q0 = tuple(q0)
         else:
