@@ -349,9 +349,12 @@ class DCNv2(CTRModel):
             return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
-    # the fp8 gather of step k+1 on the aux lane while step k's cross GEMMs run
-    # (the two-lane step program of CTRModel.build_program)
-    resolve_lane = True
+    # The fp8 gather of step k+1 on the aux lane while step k's cross GEMMs run
+    # (the two-lane step program of CTRModel.build_program) measured no gain:
+    # 26.86 / 26.85 vs 27.13 / 26.99 M scores/s one-stream, interleaved
+    # (profiles/r04_session2.md) - the cross GEMMs hold every CU, so the gather
+    # only moves, it does not overlap. The hooks stay for A/B (set it True).
+    resolve_lane = False
 
     def _resolve_applies(self, ids, wts) -> bool:
         on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
