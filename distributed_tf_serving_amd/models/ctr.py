@@ -525,7 +525,26 @@ class DLRM(CTRModel):
         and the interaction's gather)."""
         return self.hot == 1 and self.emb is not None and self._bottom_fused()
 
-    def _forward(self, ids, wts, out=None):
+    # step k+1's bottom MLP + gathered interaction on the aux lane while step
+    # k's top MLP runs (the two-lane program of CTRModel.build_program)
+    resolve_lane = True
+
+    def _resolve_applies(self, ids, wts) -> bool:
+        arena = isinstance(ids, ops.ArenaRows)
+        on_gpu = ids.arena.is_cuda if arena else ids.is_cuda
+        return on_gpu and self.hot == 1 and self.emb is not None and ids.shape[0] >= 8192
+
+    def _resolve(self, ids, wts):
+        """Bottom MLP + the one-hot gather fused into the dot interaction: the
+        top MLP's input z."""
+        arena = isinstance(ids, ops.ArenaRows)
+        dense_out = self.bottom_out(ids if arena else wts)
+        return ops.dot_interaction_gather(dense_out, self.emb, ids if arena else self.sparse_ids(ids), self.modulo_f,
+                                          self.offset_f, self.inter_cols, id_col0=self.cfg.num_dense)
+
+    def _forward(self, ids, wts, out=None, resolved=None):
+        if resolved is not None:  # z from the aux lane (resolve_lane)
+            return self.top.forward_head(resolved, self.head_w, self.head_b, out=out)
         arena = isinstance(ids, ops.ArenaRows)
         dense_out = self.bottom_out(ids if arena else wts)
         if self.hot == 1 and self.emb is not None and (arena or ids.is_cuda):

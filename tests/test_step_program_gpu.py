@@ -216,3 +216,25 @@ def test_dcn_v2_fp8_gather_resolved_on_another_stream_is_identical(cuda):
         got = m._forward(ids, wts, resolved=r)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+def test_dlrm_interaction_resolved_on_another_stream_is_identical(cuda):
+    """DLRM's resolve lane: bottom MLP + gathered dot interaction run on a
+    second stream and handed to the top MLP give the one-stream scores, bit
+    for bit."""
+    cfg = _cfg()
+    m = build_model(cfg, cuda)
+    g = torch.Generator().manual_seed(23)
+    B = 8192
+    ids = torch.randint(0, 10**9, (B, cfg.num_fields), generator=g).to(cuda)
+    wts = torch.rand(B, cfg.num_fields, generator=g).to(cuda)
+    assert m.resolve_lane and m._resolve_applies(ids, wts) and not m._resolve_applies(ids[:2048], wts[:2048])
+    with torch.no_grad():
+        want = m._forward(ids, wts)
+        s = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(s):
+            z = m._resolve(ids, wts)
+        torch.cuda.current_stream(cuda).wait_stream(s)
+        got = m._forward(ids, wts, resolved=z)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
