@@ -525,9 +525,11 @@ class DLRM(CTRModel):
         and the interaction's gather)."""
         return self.hot == 1 and self.emb is not None and self._bottom_fused()
 
-    # step k+1's bottom MLP + gathered interaction on the aux lane while step
+    # Step k+1's bottom MLP + gathered interaction on the aux lane while step
     # k's top MLP runs (the two-lane program of CTRModel.build_program)
-    resolve_lane = True
+    # measured slower: 100.2 / 100.5 vs 106.1 / 107.0 M scores/s one-stream,
+    # interleaved (profiles/r04_session2.md). The hooks stay for A/B.
+    resolve_lane = False
 
     def _resolve_applies(self, ids, wts) -> bool:
         arena = isinstance(ids, ops.ArenaRows)

@@ -228,7 +228,8 @@ def test_dlrm_interaction_resolved_on_another_stream_is_identical(cuda):
     B = 8192
     ids = torch.randint(0, 10**9, (B, cfg.num_fields), generator=g).to(cuda)
     wts = torch.rand(B, cfg.num_fields, generator=g).to(cuda)
-    assert m.resolve_lane and m._resolve_applies(ids, wts) and not m._resolve_applies(ids[:2048], wts[:2048])
+    # the hooks (the lane itself is off for DLRM: slower)
+    assert m._resolve_applies(ids, wts) and not m._resolve_applies(ids[:2048], wts[:2048])
     with torch.no_grad():
         want = m._forward(ids, wts)
         s = torch.cuda.Stream(cuda)
