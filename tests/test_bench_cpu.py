@@ -101,7 +101,8 @@ def test_bench_sharded_dlrm_peer_exchange_world2():
     shared-memory file on the CPU), the hot-row replica cache fills from the
     kernels' samples before the clock starts, and the JSON reports its hit
     rate and the bytes that crossed to the peer per step."""
-    out = _run_bench(2, ("--model", "dlrm", "--table-rows", "5000", "--exchange", "peer", "--hot-cache-rows", "4096", "--cache-learn-rounds", "2"))
+    out = _run_bench(2, ("--model", "dlrm", "--table-rows", "5000", "--exchange", "peer", "--hot-cache-rows", "4096",
+                         "--cache-learn-rounds", "2"))
     par = out["config"]["parallelism"]
     assert "embedding-mp2" in par and "xGMI" in par and "replica cache" in par, par
     ex = out["embedding_exchange"]
