@@ -31,6 +31,9 @@ void check_dev(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+// device only: for row views whose strides the caller checks itself
+void check_gpu(const torch::Tensor& t, const char* name) { TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor"); }
+
 void check_same_dev(const torch::Tensor& a, const torch::Tensor& b, const char* name) {
   TORCH_CHECK(a.device() == b.device(), name, " must be on ", a.device());
 }
@@ -277,7 +280,7 @@ void embed_gemm_inputs(const torch::Tensor& table, const c10::optional<torch::Te
     a.arena = arena->data_ptr();
   } else {
     TORCH_CHECK(ids.has_value(), "gather-GEMM needs an arena or ids");
-    check_dev(*ids, "ids");
+    check_gpu(*ids, "ids");  // row views (e.g. the fan-out's narrow exchange rows) pass: strides checked below
     check_same_dev(table, *ids, "ids");
     TORCH_CHECK((ids->scalar_type() == torch::kInt64 || ids->scalar_type() == torch::kInt32) && ids->dim() == 2 &&
                     ids->size(0) == B && ids->size(1) == F && ids->stride(1) == 1 && ids->stride(0) >= F,
@@ -286,7 +289,7 @@ void embed_gemm_inputs(const torch::Tensor& table, const c10::optional<torch::Te
     a.ids64 = ids->scalar_type() == torch::kInt64;
     a.ids_ld = ids->stride(0);
     if (wts) {
-      check_dev(*wts, "wts");
+      check_gpu(*wts, "wts");
       TORCH_CHECK(wts->scalar_type() == torch::kFloat32 && wts->dim() == 2 && wts->size(0) == B && wts->size(1) == F &&
                       wts->stride(1) == 1 && wts->stride(0) >= F,
                   "wts must be fp32 [B, F] with contiguous rows");
@@ -1112,6 +1115,43 @@ torch::Tensor gemm_head(torch::Tensor A, torch::Tensor W, torch::Tensor bias, in
   return y;
 }
 
+// K4 + K4 + K6: the two-layer MLP tail + head in one launch (mlp_tail.hip).
+// W2p / W3p hold the weights in MFMA fragment order (ops.pack_bfrag).
+torch::Tensor mlp_tail(torch::Tensor X, torch::Tensor W2p, torch::Tensor b2, int64_t act2, torch::Tensor W3p,
+                       torch::Tensor b3, int64_t act3, torch::Tensor hw, double hbias,
+                       c10::optional<torch::Tensor> extra, bool sigmoid, c10::optional<torch::Tensor> out) {
+  for (auto* t : {&X, &W2p, &b2, &W3p, &b3, &hw}) check_dev(*t, "mlp_tail operand");
+  check_same_dev(X, W2p, "W2p");
+  check_same_dev(X, W3p, "W3p");
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && X.dim() == 2 && X.stride(1) == 1, "X must be bf16 [M, K1] rows");
+  TORCH_CHECK(W2p.scalar_type() == torch::kBFloat16 && W3p.scalar_type() == torch::kBFloat16 && W2p.is_contiguous() &&
+                  W3p.is_contiguous(),
+              "W2p, W3p must be contiguous bf16 (pack_bfrag)");
+  const int64_t M = X.size(0), K1 = X.size(1), N2 = b2.numel(), N3 = b3.numel();
+  TORCH_CHECK(N2 == 512 && N3 == 256, "mlp_tail covers N2 = 512, N3 = 256");
+  TORCH_CHECK(K1 == 1024, "mlp_tail covers K1 = 1024");
+  TORCH_CHECK(K1 % 128 == 0 && X.stride(0) % 8 == 0, "mlp_tail needs K1 % 128 == 0 and 16-byte rows");
+  TORCH_CHECK(W2p.numel() == N2 * K1 && W3p.numel() == N3 * N2, "packed weight sizes");
+  TORCH_CHECK(b2.scalar_type() == torch::kFloat32 && b3.scalar_type() == torch::kFloat32 &&
+                  hw.scalar_type() == torch::kFloat32 && hw.numel() == N3,
+              "b2, b3, hw must be fp32 [N2], [N3], [N3]");
+  TORCH_CHECK((act2 == 0 || act2 == 1) && (act3 == 0 || act3 == 1), "act must be 0 (none) or 1 (relu)");
+  if (extra) {
+    check_dev(*extra, "extra");
+    check_extra(*extra, M);
+  }
+  c10::DeviceGuard g(X.device());
+  torch::Tensor y;
+  float* yp = score_out(X, M, out, y);
+  check_hip(dtfs::launch_mlp_tail(X.data_ptr(), X.stride(0), int(M), int(K1), W2p.data_ptr(), b2.data_ptr<float>(),
+                                  int(act2), int(N2), W3p.data_ptr(), b3.data_ptr<float>(), int(act3), int(N3),
+                                  hw.data_ptr<float>(), float(hbias), extra ? extra->data_ptr<float>() : nullptr,
+                                  extra ? extra_rows(*extra) : 0, extra ? extra_stride(*extra) : 0, sigmoid ? 2 : 0,
+                                  yp, cur_stream(X)),
+            "mlp_tail");
+  return y;
+}
+
 // ---------------------------------------------------------------- K0 ingest
 void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields, int64_t narrow_modulo) {
   check_dev(arena, "arena");
@@ -1679,11 +1719,12 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sigmoid") = true);
   m.def("gemm_head", &gemm_head, py::arg("A"), py::arg("W"), py::arg("bias"), py::arg("act"), py::arg("hw"),
         py::arg("hbias") = 0.0, py::arg("extra") = py::none(), py::arg("sigmoid") = true, py::arg("out") = py::none());
+  m.def("mlp_tail", &mlp_tail, py::arg("X"), py::arg("W2p"), py::arg("b2"), py::arg("act2"), py::arg("W3p"),
+        py::arg("b3"), py::arg("act3"), py::arg("hw"), py::arg("hbias") = 0.0, py::arg("extra") = py::none(),
+        py::arg("sigmoid") = true, py::arg("out") = py::none());
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");
-  m.def("set_head_variant", &dtfs::set_head_variant, py::arg("variant"),
-        "fused last layer + head kernel: 0 double-buffered, 1 / 2 pipelined (64 x 3 / 32 x 4 stages); A/B studies");
   m.def("quant_rows_fp8", &quant_rows_fp8, py::arg("x"), py::arg("k_pad") = 1);
   m.def("dot_interaction_gather", &dot_interaction_gather, py::arg("dense"), py::arg("table"), py::arg("ids"),
         py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);

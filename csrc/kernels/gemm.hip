@@ -729,158 +729,6 @@ __global__ void __launch_bounds__(256) gemm_head_kernel(const uint8_t* __restric
   }
 }
 
-// The same fused last layer + head with a STAGES-deep LDS-DMA ring: PF =
-// STAGES - 1 K tiles in flight across barriers, a counted vmcnt per tile and a
-// raw s_barrier (gemm_pipe_kernel's schedule). The double-buffered kernel above
-// waits for each tile's DMA inside its own iteration (__syncthreads drains
-// vmcnt), so a dispatch takes ~11-13 us whatever the row count (2048 or 16384
-// rows): the weight tiles' L2 latency, not the 4.3 GFLOP, sets its length.
-template <int BM, int TN, int STAGES>
-__global__ void __launch_bounds__(256) gemm_head_pipe_kernel(const uint8_t* __restrict__ A, int64_t lda,
-                                                             const uint8_t* __restrict__ W, int64_t ldw,
-                                                             const float* __restrict__ bias, int act,
-                                                             const float* __restrict__ hw, float hbias,
-                                                             const float* __restrict__ extra, int extra_n,
-                                                             int64_t extra_ld, int out_act, float* __restrict__ y,
-                                                             int M, int N, int K) {
-  constexpr int WN_ = 4, NW = 4;
-  constexpr int BN = 16 * TN * WN_;
-  constexpr int TM = BM / 16;
-  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // LDS-DMA instructions per wave per tile
-  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "tile rows must split evenly over waves");
-  constexpr int STAGE_BYTES = (BM + BN) * 128;
-  constexpr int PF = STAGES - 1;
-  constexpr int LOADS = IA + IB;
-  static_assert(PF >= 1 && PF <= 3, "the wait ladder covers 1..3 tiles in flight");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE_BYTES + NW * BM * 4];
-  float* red = reinterpret_cast<float*>(smem + STAGES * STAGE_BYTES);
-
-  const int m0 = blockIdx.x * BM;
-  const int lane = threadIdx.x & 63;
-  const int wn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lr = lane >> 3, ls = lane & 7;
-  const uint8_t* a_src[IA];
-  const uint8_t* b_src[IB];
-#pragma unroll
-  for (int j = 0; j < IA; ++j) {
-    const int r = 8 * (wn + j * NW) + lr;
-    a_src[j] = A + int64_t(min(m0 + r, M - 1)) * lda * 2 + ((ls ^ ((r >> 1) & 7)) << 4);
-  }
-#pragma unroll
-  for (int j = 0; j < IB; ++j) {
-    const int r = 8 * (wn + j * NW) + lr;
-    b_src[j] = W + int64_t(min(r, N - 1)) * ldw * 2 + ((ls ^ ((r >> 1) & 7)) << 4);
-  }
-  auto stage = [&](int slot, int kt) {
-    uint8_t* base = smem + slot * STAGE_BYTES;
-    const int64_t kb0 = int64_t(kt) * 128;
-#pragma unroll
-    for (int j = 0; j < IA; ++j)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(a_src[j] + kb0),
-                                       (__attribute__((address_space(3))) void*)(base + (wn + j * NW) * 1024), 16,
-                                       0, 0);
-#pragma unroll
-    for (int j = 0; j < IB; ++j)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(b_src[j] + kb0),
-                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + (wn + j * NW) * 1024),
-                                       16, 0, 0);
-  };
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (K * 2) / 128;
-  const int fr = lane & 15, fq = lane >> 4;
-  // prologue: PF tiles in flight, tile 0 landed
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-    if (p < nk) stage(p, p);
-  if (nk >= PF) {
-    if constexpr (PF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-    else if constexpr (PF == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // short K: drain
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  for (int kt = 0; kt < nk; ++kt) {
-    const int slot = kt % STAGES;
-    if (kt + PF < nk) stage((kt + PF) % STAGES, kt + PF);
-    const uint8_t* as = smem + slot * STAGE_BYTES;
-    const uint8_t* bs = as + BM * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(as + swz(i * 16 + fr, kk * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * 16 * TN + j * 16 + fr, kk * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    // RAW for tile kt+1: at most the tiles issued after it are outstanding
-    // (this wave), every wave's after the barrier; WAR: the slot restaged next
-    // iteration was read in iteration kt + 1 + PF - STAGES = kt, before it
-    if (kt + 1 < nk) {
-      const int ahead = min(PF - 1, nk - 1 - (kt + 1));
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  }
-  // epilogue (as gemm_head_kernel): per-row partial dot over this wave's columns
-  float part[TM][4];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[i][r] = 0.f;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = wn * 16 * TN + j * 16 + fr;
-    const bool ok = n < N;
-    const float bn = ok ? bias[n] : 0.f;
-    const float wv = ok ? hw[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = acc[i][j][r] + bn;
-        if (act == EPI_RELU) v = fmaxf(v, 0.f);
-        part[i][r] += v * wv;
-      }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = part[i][r];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      if (fr == 0) red[wn * BM + i * 16 + fq * 4 + r] = v;
-    }
-  __syncthreads();
-  for (int row = threadIdx.x; row < BM; row += blockDim.x) {
-    const int m = m0 + row;
-    if (m >= M) continue;
-    float s = hbias;
-    for (int e = 0; extra && e < extra_n; ++e) s += extra[e * extra_ld + m];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w * BM + row];
-    y[m] = out_act == EPI_SIGMOID ? sigmoidf(s) : s;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // 256x256 "8-phase" GEMM (cdna_hip_programming.md §5, "The 256² 8-phase
 // template": staggered wave groups + counted vmcnt + raw barriers).
@@ -2020,10 +1868,6 @@ static void dispatch(const void* A, int64_t lda, const void* W, int64_t ldw, con
 
 using namespace kern;
 
-// head kernel choice (A/B): 0 double-buffered gemm_head_kernel, 1 / 2 the
-// pipelined gemm_head_pipe_kernel (64-row tiles x 3 stages / 32-row x 4)
-std::atomic<int> g_head_variant{0};
-void set_head_variant(int v) { g_head_variant.store(v < 0 || v > 2 ? 0 : v, std::memory_order_relaxed); }
 
 hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
                             const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
@@ -2035,17 +1879,6 @@ hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t l
   const uint8_t* w = static_cast<const uint8_t*>(W);
   // 32-row tiles give >= 256 workgroups at the bench batch (8192 rows)
   const bool small = M >= 4096;
-  const int hv = g_head_variant.load(std::memory_order_relaxed);
-  if (N > 128 && hv == 1) {  // pipelined: 64-row tiles, 3 K tiles in flight (120 KiB LDS)
-    hipLaunchKernelGGL((gemm_head_pipe_kernel<64, 4, 3>), dim3((M + 63) / 64), dim3(256), 0, st, a, lda, w, ldw, bias,
-                       act, hw, hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
-    return hipGetLastError();
-  }
-  if (N > 128 && hv == 2) {  // pipelined: 32-row tiles, 4 K tiles in flight (144 KiB LDS)
-    hipLaunchKernelGGL((gemm_head_pipe_kernel<32, 4, 4>), dim3((M + 31) / 32), dim3(256), 0, st, a, lda, w, ldw, bias,
-                       act, hw, hbias, extra, extra_n, extra_ld, out_act, y, M, N, K);
-    return hipGetLastError();
-  }
   if (N > 128) {
     if (small)
       hipLaunchKernelGGL((gemm_head_kernel<32, 4>), dim3((M + 31) / 32), dim3(256), 0, st, a, lda, w, ldw, bias, act,

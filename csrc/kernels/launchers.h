@@ -83,9 +83,6 @@ hipError_t launch_embed(const EmbedArgs& a, hipStream_t st);
 // Pipelined K1 kernel geometry: resident-wave cap (0 = one row per wave) and
 // rows in flight per wave (1 or 2).
 void set_embed_wave_cap(int waves, int rows_in_flight = 1);
-// fused last layer + head kernel: 0 double-buffered (default), 1 / 2 pipelined
-// (64-row tiles x 3 stages / 32-row tiles x 4 stages); A/B studies
-void set_head_variant(int v);
 
 // Front half of K1 for the gather-GEMM (gemm_gather): shared-table rows /
 // weights of B candidates, field-major rows_t / wts_t [F][Mp] (Mp = B rounded
@@ -157,6 +154,14 @@ hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, c
 hipError_t launch_gemm_head(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int act,
                             const float* hw, float hbias, const float* extra, int out_act, float* y, int M, int N,
                             int K, hipStream_t st, int extra_n = 1, int64_t extra_ld = 0);
+
+// K4 + K4 + K6 fused MLP tail (mlp_tail.hip): h2 = act2(X W2^T + b2) (bf16, in
+// LDS), y[m] = out_act(act3(h2 W3^T + b3)[m,:] . hw + hbias + sum_e extra[e][m]).
+// W2p / W3p: the weights in MFMA fragment order (ops.pack_bfrag). N2 = 512,
+// N3 = 256, K1 = 1024; out_act 0 none / 2 sigmoid; y device or mapped host.
+hipError_t launch_mlp_tail(const void* X, int64_t ldx, int M, int K1, const void* W2p, const float* b2, int act2,
+                           int N2, const void* W3p, const float* b3, int act3, int N3, const float* hw, float hbias,
+                           const float* extra, int extra_n, int64_t extra_ld, int out_act, float* y, hipStream_t st);
 
 // K3: DCN-v1 cross network, all L layers fused.
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,

@@ -117,6 +117,17 @@ class Dense(nn.Module):
         self.register_buffer("w_scale", sw.contiguous(), persistent=False)
         self.fp8 = True
 
+    def packed(self) -> torch.Tensor:
+        """The weight in MFMA fragment order (ops.pack_bfrag) for the fused MLP
+        tail, re-packed whenever the weight changed (load_state_dict bumps its
+        version). Built by the eager warm-up that precedes every graph capture."""
+        key = (self.weight.data_ptr(), self.weight._version)
+        cached = getattr(self, "_packed", None)
+        if cached is None or cached[0] != key:
+            cached = (key, ops.pack_bfrag(self.weight.detach()))
+            self._packed = cached
+        return cached[1]
+
     def forward(self, x: torch.Tensor, xq=None) -> torch.Tensor:
         """``xq``: (q, scale) of x already quantised by the caller (fp8 layers)."""
         if self.fp8:
@@ -149,11 +160,16 @@ class MLP(nn.Module):
                      out: Optional[torch.Tensor] = None, xq=None, start: int = 0) -> torch.Tensor:
         """MLP then CTR head. On the GPU the last layer and the head run as one
         kernel (ops.linear_head) whenever its shape allows; it writes ``out``
-        (device or pinned host memory) directly. (Fusing the last TWO layers
-        as well streams both weights through every 64-row block: measured
-        48.0 us vs 34.5 us for GEMM + fused head at 16384 rows on MI355X -
-        weight-load latency bound - so that fusion is not used.)
+        (device or pinned host memory) directly. When exactly two layers remain
+        (1024 -> 512 -> 256) on a batch that fills the GPU, both layers and the
+        head run as ONE kernel (ops.mlp_tail: 64-row workgroups, h2 kept in LDS,
+        weights loaded in MFMA fragment order straight into registers).
         ``start``: x is already the output of layers[:start]."""
+        rest = self.layers[start:]
+        if len(rest) == 2 and x.is_cuda and xq is None and ops.mlp_tail_ok(x, rest[0], rest[1]):
+            l2, l3 = rest
+            return ops.mlp_tail(x, l2.packed(), l2.bias, l2.act, l3.packed(), l3.bias, l3.act, head_w, head_b,
+                                extra=extra, sigmoid=sigmoid, out=out)
         for k, layer in enumerate(self.layers[start:-1], start):
             x = layer(x, xq if k == 0 else None)
         last = self.layers[-1]

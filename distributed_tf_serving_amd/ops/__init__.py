@@ -686,6 +686,48 @@ def linear_head(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: str, hw:
     return y
 
 
+def pack_bfrag(W: torch.Tensor) -> torch.Tensor:
+    """bf16 weights [N, K] -> MFMA B-fragment order (csrc/kernels/mlp_tail.hip):
+    block (n16, k64, kk) is 64 lanes x 8 values, lane (fr, fq) holding
+    W[16 n16 + fr, 64 k64 + 32 kk + 8 fq + e] - one wave-instruction per
+    fragment reads 1 KiB of contiguous bytes."""
+    N, K = W.shape
+    if N % 16 or K % 64:
+        raise ValueError(f"pack_bfrag needs N % 16 == 0 and K % 64 == 0, got {tuple(W.shape)}")
+    return W.reshape(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous()
+
+
+# The fused MLP tail replaces GEMM2 + the fused last-layer/head kernel at or
+# above this many rows (one 64-row workgroup per CU at 16384). A module flag,
+# not an environment knob: microbenchmarks and tests flip it in-process.
+MLP_TAIL = True
+MLP_TAIL_MIN_ROWS = 8192
+
+
+def mlp_tail_ok(x: torch.Tensor, l2, l3) -> bool:
+    """Shapes the fused two-layer tail + head kernel covers: bf16 [M, 1024] ->
+    512 -> 256 -> score, ReLU / linear layers, enough rows to fill the GPU."""
+    return (MLP_TAIL and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
+            and x.shape[1] == 1024 and x.shape[0] >= MLP_TAIL_MIN_ROWS
+            and not l2.fp8 and not l3.fp8 and tuple(l2.weight.shape) == (512, 1024)
+            and tuple(l3.weight.shape) == (256, 512) and l2.act in ("relu", "none") and l3.act in ("relu", "none"))
+
+
+def mlp_tail(x: torch.Tensor, W2p: torch.Tensor, b2: torch.Tensor, act2: str, W3p: torch.Tensor,
+             b3: torch.Tensor, act3: str, hw: torch.Tensor, hbias: float = 0.0,
+             extra: Optional[torch.Tensor] = None, sigmoid: bool = True,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K4 + K4 + K6 fused (GPU): out_act(act3(bf16(act2(x W2^T + b2)) W3^T + b3) . hw + hbias + extra).
+    ``W2p`` / ``W3p``: :func:`pack_bfrag` of the two weights. ``out`` may be
+    pinned host memory (the kernel writes the scores there)."""
+    return hip().mlp_tail(x, W2p, b2, _ACTS[act2], W3p, b3, _ACTS[act3], hw, float(hbias), extra, sigmoid, out)
+
+
+def unpack_bfrag(Wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """Inverse of :func:`pack_bfrag` (tests)."""
+    return Wp.reshape(N // 16, K // 64, 2, 4, 16, 8).permute(0, 4, 1, 2, 3, 5).reshape(N, K)
+
+
 # ------------------------------------------------------------------ K7
 def sort_scores(scores: torch.Tensor, descending: bool = False, k: int = -1):
     """Sorted scores + the candidate permutation (the reference drops the latter,

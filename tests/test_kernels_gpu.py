@@ -511,6 +511,62 @@ def test_linear_head_into_pinned_host(cuda):
     _close(out, ops.linear_head(x, W, b, "relu", hw, 0.0, None, True), 1e-4, 1e-3, "linear_head pinned")
 
 
+def _mlp_tail_ref(x, W2, b2, act2, W3, b3, act3, hw, hb, extra, sig):
+    """fp32 reference of the fused tail: h2 rounded to bf16 like the kernel (the unfused path's rounding)."""
+    h2 = x.float() @ W2.float().t() + b2
+    if act2 == "relu":
+        h2 = torch.relu(h2)
+    return ops.linear_head(h2.to(torch.bfloat16), W3, b3, act3, hw, hb, extra, sig)
+
+
+@pytest.mark.parametrize("M", [8192, 8200, 16384, 16421])
+@pytest.mark.parametrize("act3", ["relu", "none"])
+def test_mlp_tail_fused(cuda, M, act3):
+    g = torch.Generator().manual_seed(M + (act3 == "relu"))
+    x = torch.randn(M, 1024, generator=g).to(torch.bfloat16)
+    W2 = (torch.randn(512, 1024, generator=g) / 32).to(torch.bfloat16)
+    W3 = (torch.randn(256, 512, generator=g) / 512 ** 0.5).to(torch.bfloat16)
+    b2, b3 = torch.randn(512, generator=g) * 0.1, torch.randn(256, generator=g) * 0.1
+    hw = torch.randn(256, generator=g) * 0.05
+    parts = torch.randn(2, M + 100, generator=g)  # the gather-GEMM's [2, Mp] partial logits
+    W2p, W3p = ops.pack_bfrag(W2.to(cuda)), ops.pack_bfrag(W3.to(cuda))
+    for extra, sig in ((parts, True), (None, False)):
+        y = ops.mlp_tail(x.to(cuda), W2p, b2.to(cuda), "relu", W3p, b3.to(cuda), act3, hw.to(cuda), 0.2,
+                         None if extra is None else extra.to(cuda), sig)
+        ref = _mlp_tail_ref(x, W2, b2, "relu", W3, b3, act3, hw, 0.2, extra, sig)
+        # h2 is bf16: a ReLU/rounding boundary flip moves a logit by ~1e-3
+        _close(y, ref, 2e-3, 2e-3, f"mlp_tail {M} {act3}")
+
+
+def test_mlp_tail_into_pinned_host_and_model_path(cuda):
+    M = 16384
+    cfg = ModelConfig(family="deepfm", vocab_size=20000)
+    m = build_model(cfg, cuda)
+    l2, l3 = m.mlp.layers[1], m.mlp.layers[2]
+    x = (torch.randn(M, 1024) * 0.5).to(torch.bfloat16).to(cuda)
+    extra = torch.randn(2, M).to(cuda)
+    out = torch.zeros(M, dtype=torch.float32).pin_memory()
+    y = m.mlp.forward_head(x, m.head_w, 0.1, extra=extra, out=out, start=1)
+    torch.cuda.synchronize()
+    assert y.data_ptr() == out.data_ptr()
+    try:
+        ops.MLP_TAIL = False
+        want = m.mlp.forward_head(x, m.head_w, 0.1, extra=extra, start=1)
+    finally:
+        ops.MLP_TAIL = True
+    _close(out, want, 2e-3, 2e-3, "mlp_tail model path vs GEMM2 + fused head")
+    # a weight update re-packs (load_state_dict bumps the version)
+    with torch.no_grad():
+        l2.weight.mul_(0.5)
+    y2 = m.mlp.forward_head(x, m.head_w, 0.1, extra=extra, start=1)
+    try:
+        ops.MLP_TAIL = False
+        want2 = m.mlp.forward_head(x, m.head_w, 0.1, extra=extra, start=1)
+    finally:
+        ops.MLP_TAIL = True
+    _close(y2, want2, 2e-3, 2e-3, "mlp_tail after a weight update")
+
+
 @pytest.mark.parametrize("n", [1, 7, 1500, 4096, 8192])
 @pytest.mark.parametrize("desc", [False, True])
 def test_sort(cuda, n, desc):
@@ -779,6 +835,27 @@ def test_embed_gemm_matches_fp32_reference(cuda, B, ids32, fm2):
     xg, fmg = ops.embed(d[0], d[4], d[5], lin=d[1], modulo=V, bias=bias, want_x=True, want_fm=True, fm2=fm2)
     _close(h, ops.linear(xg, d[2], d[3], "relu"), 1e-2, 1e-4, "gather-GEMM vs gather + GEMM")
     _close(parts[:, :B].sum(0), fmg, 1e-5, 1e-5, "FM partials vs the gather kernel's FM")
+
+
+def test_embed_gemm_narrow_exchange_rows(cuda):
+    """The candidate fan-out hands the forward its exchanged rows as strided
+    views of [int32 row x F | fp32 weight x F] (serving/packing.py narrow
+    layout): the gather-GEMM reads them in place, same result as contiguous
+    copies. (Rejected as non-contiguous until round 5: the 16384-row fan-out
+    step could not be built.)"""
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    V, B = 40_000, 16384
+    table, lin, W, b, ids, wts = _gather_gemm_case(B, V=V)
+    L = PackedLayout(43, narrow_modulo=V)
+    buf = L.pack(ids, wts).to(cuda)
+    iv, wv = L.ids(buf), L.wts(buf)
+    assert not iv.is_contiguous() and iv.stride(1) == 1
+    d = [t.to(cuda) for t in (table, lin, W, b)]
+    h, parts = ops.embed_gemm(d[0], iv, wv, d[1], V, 0.1, d[2], d[3], "relu")
+    hc, pc = ops.embed_gemm(d[0], iv.contiguous(), wv.contiguous(), d[1], V, 0.1, d[2], d[3], "relu")
+    _close(h, hc, 0, 0, "strided vs contiguous rows")
+    _close(parts[:, :B], pc[:, :B], 0, 0, "strided vs contiguous FM partials")
 
 
 def test_embed_gemm_arena_rows(cuda):

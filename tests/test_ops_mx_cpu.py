@@ -1,6 +1,7 @@
 """OCP MX-fp8 reference path (CPU): block quantisation round trip, the GEMM's
 block-scaled input, and the DCN-v2 cross chain that hands MX-fp8 operands from
 one layer's epilogue to the next (GPU kernels: tests/test_kernels_gpu.py)."""
+import pytest
 import torch
 
 from distributed_tf_serving_amd import ops
@@ -34,3 +35,34 @@ def test_linear_fp8_block_scaled_input_equals_dequantised():
     y = ops.linear_fp8(q, None, wq, sw, None, out_f32=True, sx_blk=s)
     ref = ops.dequant_mx_fp8(q, s) @ (wq.float() * sw[:, None]).t()
     torch.testing.assert_close(y, ref)
+
+
+def test_pack_bfrag_layout_and_round_trip():
+    # fragment (n16, k64, kk), lane (fr, fq), value e = W[16 n16 + fr, 64 k64 + 32 kk + 8 fq + e]
+    N, K = 48, 192
+    W = torch.arange(N * K, dtype=torch.float32).view(N, K).to(torch.bfloat16)
+    P = ops.pack_bfrag(W).view(N // 16, K // 64, 2, 64, 8)
+    for n16, k64, kk, lane in ((0, 0, 0, 0), (2, 1, 1, 37), (1, 2, 0, 63), (2, 2, 1, 16)):
+        fr, fq = lane & 15, lane >> 4
+        want = W[16 * n16 + fr, 64 * k64 + 32 * kk + 8 * fq: 64 * k64 + 32 * kk + 8 * fq + 8]
+        assert torch.equal(P[n16, k64, kk, lane], want)
+    assert torch.equal(ops.unpack_bfrag(ops.pack_bfrag(W), N, K), W)
+    with pytest.raises(ValueError):
+        ops.pack_bfrag(W[:, :100])
+
+
+def test_mlp_tail_only_on_gpu_shapes():
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
+
+    m = build_model(ModelConfig(family="deepfm", vocab_size=1000), "cpu")
+    l2, l3 = m.mlp.layers[1], m.mlp.layers[2]
+    x = torch.zeros(16384, 1024, dtype=torch.bfloat16)
+    assert not ops.mlp_tail_ok(x, l2, l3)  # CPU tensors take the reference path
+    # the packed copy follows the weight (re-packed after an in-place update)
+    p1 = l2.packed()
+    assert l2.packed() is p1
+    with torch.no_grad():
+        l2.weight.add_(1.0)
+    p2 = l2.packed()
+    assert p2 is not p1 and torch.equal(ops.unpack_bfrag(p2, 512, 1024), l2.weight)

@@ -135,7 +135,8 @@ def main():
     ap.add_argument("--gather-locality", action="store_true",
                     help="gather-GEMM time by where the table rows come from (L2 / MALL / HBM)")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
-    ap.add_argument("--head", action="store_true", help="fused last layer + head: double-buffered vs pipelined")
+    ap.add_argument("--tail", action="store_true",
+                    help="MLP tail 1024 -> 512 -> 256 -> score: GEMM2 + fused head vs the one-kernel tail")
     ap.add_argument("--serving", action="store_true",
                     help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
     a = ap.parse_args()
@@ -151,8 +152,8 @@ def main():
         M, N, K = (int(x) for x in shape.split(","))
         print(json.dumps(bench_gemm_variants(M, N, K, variants=tuple(int(v) for v in vs.split(",")))), flush=True)
         return
-    if a.head:
-        for r in head_study():
+    if a.tail:
+        for r in tail_study():
             print(json.dumps(r), flush=True)
         return
     if a.gather_locality:
@@ -187,35 +188,42 @@ def main():
 
 
 
-def head_study(rows=(2048, 16384), K=512, N=256, dev="cuda", rounds=4):
-    """Fused last layer + head (ops.linear_head) per kernel variant
-    (hip().set_head_variant: 0 double-buffered, 1 pipelined 64-row x 3 stages,
-    2 pipelined 32-row x 4 stages), interleaved; every variant checked against
-    variant 0 and an fp32 reference."""
-    from distributed_tf_serving_amd.ops import hip
-
+def tail_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
+    """DeepFM / WDL / DCN MLP tail (h1 [M, 1024] -> 512 -> 256 -> sigmoid score):
+    GEMM2 (ops.linear) + fused last layer/head (ops.linear_head) vs ONE
+    ops.mlp_tail launch, interleaved; both checked against an fp32 reference."""
     out = []
     for M in rows:
         g = torch.Generator(device="cpu").manual_seed(M)
-        x = ((torch.rand(M, K, generator=g) - 0.5)).to(torch.bfloat16).to(dev)
-        W = ((torch.rand(N, K, generator=g) - 0.5) / K ** 0.5).to(torch.bfloat16).to(dev)
-        b = (torch.rand(N, generator=g) - 0.5).to(dev)
-        hw = ((torch.rand(N, generator=g) - 0.5) * 0.1).to(dev)
+        x = (torch.rand(M, 1024, generator=g) - 0.5).to(torch.bfloat16).to(dev)
+        W2 = ((torch.rand(512, 1024, generator=g) - 0.5) / 16).to(torch.bfloat16).to(dev)
+        W3 = ((torch.rand(256, 512, generator=g) - 0.5) / 11).to(torch.bfloat16).to(dev)
+        b2 = ((torch.rand(512, generator=g) - 0.5) * 0.1).to(dev)
+        b3 = ((torch.rand(256, generator=g) - 0.5) * 0.1).to(dev)
+        hw = ((torch.rand(256, generator=g) - 0.5) * 0.1).to(dev)
         extra = (torch.rand(2, M, generator=g) - 0.5).to(dev)
-        ref = torch.sigmoid(torch.relu(x.float() @ W.float().t() + b) @ hw + extra.sum(0))
-        res = {"op": "linear_head", "M": M, "K": K, "N": N}
-        times = {v: [] for v in (0, 1, 2)}
+        W2p, W3p = ops.pack_bfrag(W2), ops.pack_bfrag(W3)
+        h2 = torch.relu(x.float() @ W2.float().t() + b2).to(torch.bfloat16).float()
+        ref = torch.sigmoid(torch.relu(h2 @ W3.float().t() + b3) @ hw + extra.sum(0))
+
+        def two():
+            return ops.linear_head(ops.linear(x, W2, b2, "relu"), W3, b3, "relu", hw, 0.0, extra=extra)
+
+        def one():
+            return ops.mlp_tail(x, W2p, b2, "relu", W3p, b3, "relu", hw, 0.0, extra=extra)
+
+        times = {"two_kernels": [], "mlp_tail": []}
         for _ in range(rounds):
-            for v in (0, 1, 2):
-                hip().set_head_variant(v)
-                times[v].append(_time(lambda: ops.linear_head(x, W, b, "relu", hw, 0.0, extra=extra), rounds=1))
-        for v in (0, 1, 2):
-            hip().set_head_variant(v)
-            y = ops.linear_head(x, W, b, "relu", hw, 0.0, extra=extra)
+            times["two_kernels"].append(_time(two, rounds=1))
+            times["mlp_tail"].append(_time(one, rounds=1))
+        res = {"op": "mlp_tail", "M": M}
+        for k, fn in (("two_kernels", two), ("mlp_tail", one)):
+            y = fn()
             torch.cuda.synchronize()
-            res[f"v{v}_us"] = round(statistics.median(times[v]), 2)
-            res[f"v{v}_maxdiff_fp32"] = float((y - ref).abs().max())
-        hip().set_head_variant(0)
+            res[f"{k}_us"] = round(statistics.median(times[k]), 2)
+            res[f"{k}_maxdiff_fp32"] = float((y - ref).abs().max())
+        flops = 2.0 * M * (1024 * 512 + 512 * 256)
+        res["mlp_tail_tflops"] = round(flops / res["mlp_tail_us"] / 1e6, 1)
         out.append(res)
     return out
 
