@@ -448,13 +448,72 @@ class FallbackPool {
   std::vector<std::thread> ts_;
 };
 
+// Predicts the event loop could not admit without blocking (every arena queued
+// or in flight: LiveServer::try_submit false) wait for a batch slot here, on a
+// few native threads, so the loop keeps serving PINGs, WINDOW_UPDATEs and the
+// replies of other connections. Bounded: past kMaxQueued the call is answered
+// RESOURCE_EXHAUSTED at once.
+class SubmitPool {
+ public:
+  static constexpr size_t kMaxQueued = 4096;
+  explicit SubmitPool(int threads) {
+    for (int i = 0; i < std::max(1, threads); ++i) ts_.emplace_back([this] { work(); });
+  }
+  ~SubmitPool() { stop(); }
+  bool push(std::function<void()> task) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_ || q_.size() >= kMaxQueued) return false;
+    q_.push_back(std::move(task));
+    ++handed_;
+    cv_.notify_one();
+    return true;
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : ts_)
+      if (t.joinable()) t.join();
+    ts_.clear();
+  }
+  int64_t handed() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return handed_;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      std::function<void()> task;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stopping and drained: queued submits still run first
+        task = std::move(q_.front());
+        q_.pop_front();
+      }
+      task();
+    }
+  }
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+  int64_t handed_ = 0;
+  std::vector<std::thread> ts_;
+};
+
 struct GrpcFront {
   py::object live;  // the LiveServer holder: outlives the front door
   std::shared_ptr<FallbackPool> fb;
+  std::shared_ptr<SubmitPool> sp;
   std::unique_ptr<dtfs::net::H2GrpcServer> h2;
   void stop() {
     py::gil_scoped_release nogil;
     if (h2) h2->stop();
+    if (sp) sp->stop();
     if (fb) fb->stop();
   }
   ~GrpcFront() {
@@ -479,12 +538,14 @@ void def_grpc_front(py::module& m) {
              if (!fallback.is_none()) f->fb = std::make_shared<FallbackPool>(fallback.cast<py::function>(), fallback_threads);
              LiveServer* srv = h.srv.get();
              std::shared_ptr<FallbackPool> fb = f->fb;
+             f->sp = std::make_shared<SubmitPool>(2);
+             std::shared_ptr<SubmitPool> sp = f->sp;
              dtfs::net::H2Config cfg;
              cfg.host = host;
              cfg.port = port;
              cfg.threads = threads;
              cfg.max_message = max_message;
-             auto handler = [srv, fb](dtfs::net::GrpcCall&& call, dtfs::net::Responder r) {
+             auto handler = [srv, fb, sp](dtfs::net::GrpcCall&& call, dtfs::net::Responder r) {
                if (call.path != kPredictPath) {
                  if (fb) fb->push(std::move(call), std::move(r));
                  else r.reply(12, "method " + call.path + " is not implemented", "");
@@ -492,8 +553,7 @@ void def_grpc_front(py::module& m) {
                }
                auto msg = std::make_shared<std::string>(std::move(call.message));
                const int64_t dl = call.deadline_us;
-               srv->submit(reinterpret_cast<const uint8_t*>(msg->data()), msg->size(), dl,
-                           [r, fb, msg, dl](Reply&& rep) {
+               dtfs::runtime::Completion done = [r, fb, msg, dl](Reply&& rep) {
                              if (rep.code == dtfs::runtime::kOk) {
                                r.reply(0, std::string(), std::move(rep.response));
                              } else if ((rep.code == dtfs::runtime::kCallerPath || rep.code == dtfs::runtime::kOversize) &&
@@ -506,7 +566,15 @@ void def_grpc_front(py::module& m) {
                              } else {
                                r.reply(rep.code >= 1000 ? 13 : rep.code, std::move(rep.message), std::string());
                              }
-                           });
+                           };
+               // never block the event loop (its other connections would stall
+               // behind this call): the fast path admits in place, a full
+               // batching queue goes to the submit pool
+               if (srv->try_submit(reinterpret_cast<const uint8_t*>(msg->data()), msg->size(), dl, done)) return;
+               auto task = [srv, msg, dl, done]() mutable {
+                 srv->submit(reinterpret_cast<const uint8_t*>(msg->data()), msg->size(), dl, std::move(done));
+               };
+               if (!sp->push(std::move(task))) r.reply(8, "batching queue is full", "");
              };
              {
                py::gil_scoped_release nogil;
@@ -528,8 +596,10 @@ void def_grpc_front(py::module& m) {
         o["dropped_replies"] = s.dropped_replies;
         o["resets"] = s.resets;
         o["protocol_errors"] = s.protocol_errors;
+        o["paused_reads"] = s.paused_reads;
         o["bytes_in"] = s.bytes_in;
         o["bytes_out"] = s.bytes_out;
+        o["blocking_submits_handed_off"] = f.sp ? f.sp->handed() : 0;
         return o;
       });
 }

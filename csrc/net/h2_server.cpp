@@ -46,6 +46,7 @@ enum : uint32_t {
   kFrameSizeError = 6,
   kRefusedStream = 7,
   kCompressionError = 9,
+  kEnhanceYourCalm = 11,
 };
 
 const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";  // 24 bytes
@@ -54,6 +55,14 @@ constexpr int64_t kOurStreamWindow = 16 << 20;             // SETTINGS_INITIAL_W
 constexpr int64_t kOurConnWindow = int64_t(1) << 30;       // connection window we grant
 constexpr int64_t kMaxWindow = (int64_t(1) << 31) - 1;
 constexpr uint64_t kListenTag = 0, kWakeTag = 1;
+// Per-connection memory bounds (a client that never finishes a header block,
+// or never reads what it asks for, must not grow the server without limit):
+// a header block (HEADERS + CONTINUATION) and its decoded list are capped at
+// SETTINGS_MAX_HEADER_LIST_SIZE (advertised; GOAWAY ENHANCE_YOUR_CALM past
+// it), and while more than kMaxOutBacklog bytes wait unsent the connection's
+// input is not read (no PING / SETTINGS acks queue up behind a stalled reader).
+constexpr uint32_t kMaxHeaderList = 64 << 10;
+constexpr size_t kMaxOutBacklog = size_t(16) << 20;
 
 uint32_t be32(const uint8_t* p) { return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3]; }
 
@@ -100,6 +109,8 @@ struct Conn {
   uint32_t peer_max_frame = 16384;
   int64_t recv_unacked = 0;
   std::deque<uint32_t> blocked;  // streams waiting for window
+  bool read_paused = false;      // out backlog over kMaxOutBacklog: EPOLLIN off
+  size_t backlog() const { return out.size() - out_off; }
 };
 
 }  // namespace
@@ -176,7 +187,16 @@ class Loop : public std::enable_shared_from_this<Loop> {
           Conn& c = *it->second;
           if (evs[i].events & (EPOLLERR | EPOLLHUP)) c.dead = true;
           if (!c.dead && (evs[i].events & EPOLLIN)) on_readable(c);
-          if (!c.dead && (evs[i].events & EPOLLOUT)) flush(c);
+          if (!c.dead && (evs[i].events & EPOLLOUT)) {
+            flush(c);
+            if (!c.dead && c.read_paused && c.backlog() <= kMaxOutBacklog / 2) {
+              // the reader caught up: resume (frames already buffered first)
+              c.read_paused = false;
+              update_events(c);
+              process(c);
+              if (!c.out.empty()) flush(c);
+            }
+          }
           if (c.dead || (c.peer_goaway && c.streams.empty() && c.out_off == c.out.size())) close_conn(tag);
         }
       }
@@ -205,8 +225,12 @@ class Loop : public std::enable_shared_from_this<Loop> {
   void set_write_interest(Conn& c, bool on) {
     if (c.want_write == on) return;
     c.want_write = on;
+    update_events(c);
+  }
+
+  void update_events(Conn& c) {
     epoll_event e{};
-    e.events = uint32_t(EPOLLIN) | (on ? uint32_t(EPOLLOUT) : 0u);
+    e.events = (c.read_paused ? 0u : uint32_t(EPOLLIN)) | (c.want_write ? uint32_t(EPOLLOUT) : 0u);
     e.data.u64 = c.id;
     epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &e);
   }
@@ -223,13 +247,15 @@ class Loop : public std::enable_shared_from_this<Loop> {
       // our SETTINGS + the connection window grant (the client's preface comes first on
       // the wire from its side; ours may be sent immediately)
       std::string& o = c->out;
-      put_frame_header(&o, 18, kSettings, 0, 0);
+      put_frame_header(&o, 24, kSettings, 0, 0);
       o.append("\x00\x03", 2);
       put_u32(&o, cfg_.max_concurrent_streams);
       o.append("\x00\x04", 2);
       put_u32(&o, uint32_t(kOurStreamWindow));
       o.append("\x00\x05", 2);
       put_u32(&o, kOurMaxFrame);
+      o.append("\x00\x06", 2);
+      put_u32(&o, kMaxHeaderList);
       put_frame_header(&o, 4, kWindowUpdate, 0, 0);
       put_u32(&o, uint32_t(kOurConnWindow - 65535));
       const uint64_t id = c->id;
@@ -328,6 +354,15 @@ class Loop : public std::enable_shared_from_this<Loop> {
 
   void process(Conn& c) {
     while (!c.dead) {
+      if (c.backlog() > kMaxOutBacklog) {  // stalled reader: stop consuming its frames
+        if (!c.read_paused) {
+          c.read_paused = true;
+          update_events(c);
+          std::lock_guard<std::mutex> lk(q_mu_);
+          ++st_.paused_reads;
+        }
+        return;
+      }
       const size_t avail = c.in.size() - c.in_off;
       const uint8_t* p = reinterpret_cast<const uint8_t*>(c.in.data()) + c.in_off;
       if (!c.preface) {
@@ -355,6 +390,7 @@ class Loop : public std::enable_shared_from_this<Loop> {
           break;
         case kContinuation:
           if (!c.block_sid || sid != c.block_sid) return goaway(c, kProtocolError, "unexpected CONTINUATION");
+          if (c.block.size() + len > kMaxHeaderList) return goaway(c, kEnhanceYourCalm, "header block too large");
           c.block.append(reinterpret_cast<const char*>(pl), len);
           if (flags & kEndHeaders) end_block(c);
           break;
@@ -443,6 +479,7 @@ class Loop : public std::enable_shared_from_this<Loop> {
     }
     if (flags & kPrioFlag) off += 5;
     if (off + pad > len) return goaway(c, kProtocolError, "HEADERS padding exceeds the frame");
+    if (len - off - pad > kMaxHeaderList) return goaway(c, kEnhanceYourCalm, "header block too large");
     c.block_sid = sid;
     c.block_end_stream = (flags & kEndStream) != 0;
     c.block.assign(reinterpret_cast<const char*>(pl + off), len - off - pad);
@@ -457,8 +494,9 @@ class Loop : public std::enable_shared_from_this<Loop> {
     c.block_sid = 0;
     std::vector<Header> hs;
     std::string err;
-    if (!c.hpack.decode(reinterpret_cast<const uint8_t*>(c.block.data()), c.block.size(), &hs, &err))
-      return goaway(c, kCompressionError, "HPACK: " + err);
+    if (!c.hpack.decode(reinterpret_cast<const uint8_t*>(c.block.data()), c.block.size(), &hs, &err,
+                        kMaxHeaderList))
+      return goaway(c, err.rfind("header list", 0) == 0 ? kEnhanceYourCalm : kCompressionError, "HPACK: " + err);
     c.block.clear();
     auto it = c.streams.find(sid);
     if (it == c.streams.end()) {
@@ -753,6 +791,7 @@ H2Stats H2GrpcServer::stats() const {
     s.dropped_replies += x.dropped_replies;
     s.resets += x.resets;
     s.protocol_errors += x.protocol_errors;
+    s.paused_reads += x.paused_reads;
     s.bytes_in += x.bytes_in;
     s.bytes_out += x.bytes_out;
   }

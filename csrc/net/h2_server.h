@@ -71,6 +71,7 @@ struct H2Config {
 struct H2Stats {
   int64_t connections = 0, open_connections = 0, calls = 0, replies = 0, dropped_replies = 0;
   int64_t resets = 0, protocol_errors = 0, bytes_in = 0, bytes_out = 0;
+  int64_t paused_reads = 0;  // connections whose input was paused behind an unread reply backlog
 };
 
 class H2GrpcServer {

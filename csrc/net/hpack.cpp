@@ -243,9 +243,18 @@ void HpackDecoder::insert(Header h) {
   dyn_.push_front(std::move(h));
 }
 
-bool HpackDecoder::decode(const uint8_t* p, size_t n, std::vector<Header>* out, std::string* err) {
+bool HpackDecoder::decode(const uint8_t* p, size_t n, std::vector<Header>* out, std::string* err, size_t max_list) {
   const uint8_t* end = p + n;
   bool field_seen = false;
+  size_t list = 0;  // RFC 7540 6.5.2 header list size: name + value + 32 per field
+  auto over = [&](const Header& h) {
+    list += h.first.size() + h.second.size() + 32;
+    if (max_list && list > max_list) {
+      *err = "header list larger than SETTINGS_MAX_HEADER_LIST_SIZE";
+      return true;
+    }
+    return false;
+  };
   while (p < end) {
     const uint8_t c = *p;
     if (c & 0x80) {  // indexed
@@ -255,6 +264,7 @@ bool HpackDecoder::decode(const uint8_t* p, size_t n, std::vector<Header>* out, 
         if (err->empty()) *err = "truncated index";
         return false;
       }
+      if (over(h)) return false;
       out->push_back(std::move(h));
       field_seen = true;
     } else if ((c & 0xe0) == 0x20) {  // dynamic table size update
@@ -292,6 +302,7 @@ bool HpackDecoder::decode(const uint8_t* p, size_t n, std::vector<Header>* out, 
         *err = "bad literal value";
         return false;
       }
+      if (over(h)) return false;
       if (incremental) insert(h);
       out->push_back(std::move(h));
       field_seen = true;

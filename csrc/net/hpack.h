@@ -24,8 +24,11 @@ class HpackDecoder {
   // max_table: the SETTINGS_HEADER_TABLE_SIZE this endpoint advertised
   explicit HpackDecoder(size_t max_table = 4096) : limit_(max_table), max_(max_table) {}
   // Decode one complete header block (HEADERS + CONTINUATION payloads).
-  // false on a compression error (a connection error: COMPRESSION_ERROR).
-  bool decode(const uint8_t* p, size_t n, std::vector<Header>* out, std::string* err);
+  // false on a compression error (a connection error: COMPRESSION_ERROR) or
+  // when the decoded list outgrows max_list bytes (0 = no bound; indexed
+  // references to large table entries make a small block decode to a large
+  // list, so the bound is checked while decoding).
+  bool decode(const uint8_t* p, size_t n, std::vector<Header>* out, std::string* err, size_t max_list = 0);
   size_t table_size() const { return size_; }
   size_t table_entries() const { return dyn_.size(); }
 

@@ -88,12 +88,21 @@ int LiveServer::bucket_for(int64_t rows) const {
 }
 
 void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Completion done) {
+  (void)admit(data, n, deadline_us, done, true);
+}
+
+bool LiveServer::try_submit(const uint8_t* data, size_t n, int64_t deadline_us, Completion& done) {
+  return admit(data, n, deadline_us, done, false);
+}
+
+bool LiveServer::admit(const uint8_t* data, size_t n, int64_t deadline_us, Completion& done, bool wait) {
   auto reject = [&](int code, std::string msg) {
     {
       std::lock_guard<std::mutex> lk(mu_);
       ++st_.rejected;
     }
     done(Reply{code, std::move(msg), std::string()});
+    return true;
   };
   // framing + signature checks on the caller's thread (parallel across callers)
   wire::PredictRequestView v;
@@ -133,7 +142,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
     t.key = cfg_.output_key;
     t.shape = {0};
     done(Reply{kOk, "", wire::encode_predict_response(spec, {t})});
-    return;
+    return true;
   }
   if (rows > max_rows_)
     return reject(kOversize, "request has " + std::to_string(rows) + " rows; a batch holds at most " +
@@ -193,7 +202,9 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
         free_.pop_front();
         continue;
       }
-      // every arena is queued or in flight: wait for one (bounded by the deadline)
+      // every arena is queued or in flight: wait for one (bounded by the deadline),
+      // or tell a caller that must not block (an event-loop thread)
+      if (!wait) return false;
       if (!blocked) {
         blocked = true;
         ++st_.blocked_submits;
@@ -263,6 +274,7 @@ void LiveServer::submit(const uint8_t* data, size_t n, int64_t deadline_us, Comp
     st_.copy_us += double(now_us() - t0);
     if (--arenas_[size_t(a)].writers == 0) cv_launch_.notify_all();
   }
+  return true;
 }
 
 Reply LiveServer::predict(const uint8_t* data, size_t n, int64_t deadline_us) {

@@ -156,6 +156,10 @@ class LiveServer {
   // steady-clock microseconds (now_us()), 0 = none; a submitter that finds
   // every arena busy waits for one until then.
   void submit(const uint8_t* data, size_t n, int64_t deadline_us, Completion done);
+  // Never blocks: false (done untouched, nothing admitted) when every arena is
+  // queued or in flight and submit() would wait for one; otherwise as submit().
+  // Event-loop callers hand a false over to a thread that may block.
+  bool try_submit(const uint8_t* data, size_t n, int64_t deadline_us, Completion& done);
   // Blocking convenience wrapper.
   Reply predict(const uint8_t* data, size_t n, int64_t deadline_us);
 
@@ -169,6 +173,7 @@ class LiveServer {
   const LiveConfig& config() const { return cfg_; }
 
  private:
+  bool admit(const uint8_t* data, size_t n, int64_t deadline_us, Completion& done, bool wait);
   struct Pending {
     int64_t off, len, rows, deadline_us, t_arrive;
     Completion done;

@@ -260,3 +260,156 @@ def test_server_cli_serves_through_the_native_front_door():
             p.kill()
             p.wait()
     assert p.returncode == 0, p.returncode
+
+
+# ---- raw HTTP/2 clients: per-connection memory bounds and a non-blocking event loop
+_PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+
+
+def _frame(ftype, flags, sid, payload=b""):
+    n = len(payload)
+    return bytes([n >> 16 & 255, n >> 8 & 255, n & 255, ftype, flags]) + sid.to_bytes(4, "big") + payload
+
+
+def _read_frames(sock, until, timeout=5.0):
+    """Frames (type, flags, sid, payload) until ``until(frame)`` is true or the peer closes."""
+    import socket as _socket
+
+    sock.settimeout(timeout)
+    buf, out = b"", []
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        while len(buf) >= 9:
+            n = int.from_bytes(buf[:3], "big")
+            if len(buf) < 9 + n:
+                break
+            f = (buf[3], buf[4], int.from_bytes(buf[5:9], "big") & 0x7FFFFFFF, buf[9:9 + n])
+            buf = buf[9 + n:]
+            out.append(f)
+            if until(f):
+                return out
+        try:
+            chunk = sock.recv(65536)
+        except (_socket.timeout, ConnectionResetError):
+            break
+        if not chunk:
+            break
+        buf += chunk
+    return out
+
+
+def _hpack_int(prefix_bits, first, v):
+    cap = (1 << prefix_bits) - 1
+    if v < cap:
+        return bytes([first | v])
+    out, v = [first | cap], v - cap
+    while v >= 128:
+        out.append(v % 128 + 128)
+        v //= 128
+    return bytes(out + [v])
+
+
+def _raw_conn(port):
+    import socket
+
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(_PREFACE + _frame(4, 0, 0))
+    return s
+
+
+def test_continuation_flood_gets_goaway_and_server_survives(front):
+    srv, fr = front
+    before = fr.stats()["protocol_errors"]
+    s = _raw_conn(fr.port)
+    s.sendall(_frame(1, 0, 1, b"\x82"))  # HEADERS without END_HEADERS
+    try:
+        for _ in range(64):  # 64 x 16 KiB: past the 64 KiB header-list cap
+            s.sendall(_frame(9, 0, 1, b"\x00" * 16384))
+    except (BrokenPipeError, ConnectionResetError):
+        pass
+    frames = _read_frames(s, lambda f: f[0] == 7)
+    s.close()
+    goaway = [f for f in frames if f[0] == 7]
+    assert goaway and int.from_bytes(goaway[0][3][4:8], "big") == 11, frames  # ENHANCE_YOUR_CALM
+    settings = [f for f in frames if f[0] == 4 and not f[1] & 1]
+    assert settings and b"\x00\x06" + (64 << 10).to_bytes(4, "big") in settings[0][3]  # MAX_HEADER_LIST_SIZE
+    assert fr.stats()["protocol_errors"] > before
+    data = SyntheticRequests(fields=F, seed=21).serialized(5)
+    ch = _channel(fr.port)
+    assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (5,)
+    ch.close()
+
+
+def test_header_list_bomb_gets_goaway(front):
+    # one 4000-byte value put in the dynamic table, then referenced 20 times: a
+    # 4 KB block that decodes to 80 KB
+    srv, fr = front
+    s = _raw_conn(fr.port)
+    block = b"\x40" + _hpack_int(7, 0, 5) + b"x-big" + _hpack_int(7, 0, 4000) + b"v" * 4000 + bytes([0x80 | 62]) * 20
+    s.sendall(_frame(1, 0x4 | 0x1, 1, block))
+    frames = _read_frames(s, lambda f: f[0] == 7)
+    s.close()
+    goaway = [f for f in frames if f[0] == 7]
+    assert goaway and int.from_bytes(goaway[0][3][4:8], "big") == 11, frames
+
+
+def test_reader_that_never_reads_is_paused_not_buffered(front):
+    # PINGs from a client that never reads its ACKs: once 16 MiB of replies wait
+    # unsent, the server stops reading that connection instead of queueing more
+    import socket
+
+    srv, fr = front
+    s = _raw_conn(fr.port)
+    s.setblocking(False)
+    ping = _frame(6, 0, 0, b"12345678") * 4096  # 69 KB of PINGs per round
+    sent, off, t0 = 0, 0, time.time()
+    while time.time() - t0 < 20 and fr.stats()["paused_reads"] == 0:
+        try:
+            n = s.send(ping[off:])  # partial sends: continue mid-frame
+            sent += n
+            off = (off + n) % len(ping)
+        except (BlockingIOError, socket.timeout):
+            time.sleep(0.01)
+    paused = fr.stats()["paused_reads"]
+    s.close()
+    assert paused >= 1, f"sent {sent} bytes of PINGs, never paused"
+    data = SyntheticRequests(fields=F, seed=22).serialized(4)
+    ch = _channel(fr.port)
+    assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (4,)
+    ch.close()
+
+
+def test_full_batching_queue_does_not_block_the_event_loop():
+    # every arena queued behind a paused server: deadline-less Predicts must not
+    # stall the loop thread - a PING on another connection of the same (only)
+    # loop is still answered, and the calls complete once steps run
+    from distributed_tf_serving_amd.serving.live import LiveScheduler
+    from distributed_tf_serving_amd.serving.server import build_engine
+
+    cfg = _cfg()
+    srv = ModelServer(cfg, device="cpu")
+    eng = build_engine(cfg, torch.device("cpu"), 3)
+    live = LiveScheduler(eng, cfg.serving, start_paused=True)
+    fr = NativeGrpcFront(srv.service, live, port=0, host="127.0.0.1", threads=1)
+    ch = _channel(fr.port)
+    data = SyntheticRequests(fields=F, seed=23).serialized(64)  # one full batch each
+    n = len(live.arenas) + 4
+    futs = [ch.unary_unary(PREDICT).future(data) for _ in range(n)]
+    t0 = time.time()
+    while fr.stats()["blocking_submits_handed_off"] == 0 and time.time() - t0 < 10:
+        time.sleep(0.02)
+    assert fr.stats()["blocking_submits_handed_off"] > 0
+    s = _raw_conn(fr.port)
+    s.sendall(_frame(6, 0, 0, b"pingpong"))
+    t1 = time.time()
+    frames = _read_frames(s, lambda f: f[0] == 6 and f[1] & 1, timeout=5.0)
+    s.close()
+    assert any(f[0] == 6 and f[1] & 1 and f[3] == b"pingpong" for f in frames), "PING not answered"
+    assert time.time() - t1 < 2.0
+    live.resume()
+    for f in futs:
+        assert _scores(f.result(timeout=60)).shape == (64,)
+    ch.close()
+    fr.stop()
+    live.close()
+    srv.stop()
