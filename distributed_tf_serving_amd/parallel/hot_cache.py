@@ -162,6 +162,8 @@ class HotRowCache:
         self.cand_score = torch.empty(0, dtype=torch.float32, device=dev)
         self.active = -1
         self.refreshes = 0
+        self.refresh_failures = 0
+        self.last_error: Optional[str] = None
         self.last_filled = 0
         self._stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._lock = threading.Lock()
@@ -295,12 +297,21 @@ class HotRowCache:
         self._stop.clear()
 
         def loop():
-            while not self._stop.wait(interval_s):
+            # a failed refresh leaves the previous hot set installed (the swap is
+            # the refresh's last store) and is retried with exponential backoff;
+            # failures and the thread's liveness are reported by describe() and
+            # the live stats (serving/monitoring.py)
+            wait = interval_s
+            while not self._stop.wait(wait):
                 try:
                     self.refresh()
+                    wait = interval_s
                 except Exception as e:  # the cache is an optimisation: keep serving
-                    print(f"[hot_cache] refresh failed: {e!r}", flush=True)
-                    return
+                    self.refresh_failures += 1
+                    self.last_error = repr(e)
+                    wait = min(60.0, max(interval_s, wait * 2))
+                    print(f"[hot_cache] refresh failed ({self.refresh_failures}), retrying in {wait:.1f} s: {e!r}",
+                          flush=True)
 
         self._thread = threading.Thread(target=loop, name="dtfs-hot-cache", daemon=True)
         self._thread.start()
@@ -311,10 +322,16 @@ class HotRowCache:
             self._thread.join(timeout=30)
             self._thread = None
 
+    @property
+    def refresher_alive(self) -> bool:
+        return self._thread is not None and self._thread.is_alive()
+
     def describe(self) -> dict:
         h, m = self.counts()
         return {"capacity_rows": self.cap, "hot_rows": int(self.keys.numel()), "refreshes": self.refreshes,
-                "hits": h, "misses": m, "hit_rate": round(h / (h + m), 4) if h + m else None}
+                "hits": h, "misses": m, "hit_rate": round(h / (h + m), 4) if h + m else None,
+                "refresh_failures": self.refresh_failures, "refresher_alive": self.refresher_alive,
+                "last_error": self.last_error}
 
 
 def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.Tensor, wts: Optional[torch.Tensor],

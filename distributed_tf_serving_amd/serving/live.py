@@ -210,6 +210,8 @@ class LiveScheduler:
             st["hot_cache_rows"] = int(cache.keys.numel())
             st["hot_cache_refreshes"] = int(cache.refreshes)
             st["hot_cache_hits"], st["hot_cache_misses"] = h, m
+            st["hot_cache_refresh_failures"] = int(cache.refresh_failures)
+            st["hot_cache_refresher_alive"] = int(cache.refresher_alive)
         # the names the monitoring endpoint reads (serving/monitoring.py)
         st.setdefault("batches", st["steps"])
         st.setdefault("batched_rows", st["rows"])

@@ -48,6 +48,8 @@ _SCHED = {
     "hot_cache_refreshes": ("hot_cache_refreshes", "replica cache refreshes", True),
     "hot_cache_hits": ("hot_cache_hits", "counted remote lookups served by the replica cache", True),
     "hot_cache_misses": ("hot_cache_misses", "counted remote lookups read from the owner's HBM", True),
+    "hot_cache_refresh_failures": ("hot_cache_refresh_failures", "replica cache refreshes that failed (retried)", True),
+    "hot_cache_refresher_alive": ("hot_cache_refresher_alive", "1 while the replica cache refresher thread runs", False),
 }
 
 

@@ -157,6 +157,37 @@ def test_cache_refresh_slot_safety_and_turnover():
     assert torch.equal(peer_gather_cpu(p, c, ids2, None, 1), peer_gather_cpu(p, None, ids2, None, 1))
 
 
+def test_refresher_retries_failures_and_reports_them(monkeypatch):
+    """A failing refresh keeps the last hot set, is counted, and is retried
+    with backoff by a refresher that stays alive (it used to exit for good on
+    the first exception, leaving a silently frozen cache)."""
+    import time
+
+    p = _local_peer()
+    c = HotRowCache(p, capacity=8, ring_cap=64, sample_every=1)
+    calls = {"n": 0}
+    real = c._refresh
+
+    def flaky():
+        calls["n"] += 1
+        if calls["n"] <= 2:
+            raise RuntimeError("injected refresh failure")
+        return real()
+
+    monkeypatch.setattr(c, "_refresh", flaky)
+    c.start(interval_s=0.01)
+    try:
+        t0 = time.time()
+        while c.refreshes == 0 and time.time() - t0 < 10:
+            time.sleep(0.01)
+        d = c.describe()
+        assert d["refresh_failures"] == 2 and d["refresher_alive"] and c.refreshes >= 1
+        assert "injected" in d["last_error"]
+    finally:
+        c.stop()
+    assert not c.describe()["refresher_alive"]
+
+
 def test_local_tables_never_cached_or_counted():
     p = _local_peer(remote=())
     assert p.remote_tables == 0
