@@ -32,29 +32,19 @@ StepRunner::StepRunner(int device, int slots) : device_(device) {
   // fan-out runner keeps one (its ingress / egress streams take the other
   // hardware queues).
   ck(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking), "hipStreamCreate(copy)");
-  // A/B knobs (env, read once): DTFS_COPY_STREAMS=1 keeps every H2D on one copy
-  // stream; DTFS_COMPUTE_PRIORITY=1 creates the compute stream at the highest
-  // priority (its hardware queue is served first when queues are shared)
-  if (const char* e = std::getenv("DTFS_COPY_STREAMS")) two_copy_streams_ = std::atoi(e) != 1;
-  const char* pe = std::getenv("DTFS_COMPUTE_PRIORITY");
-  if (pe && std::atoi(pe) == 1) {
-    int least = 0, greatest = 0;
-    ck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-    ck(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, greatest), "hipStreamCreate(compute, priority)");
-  } else {
-    ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
-  }
+  // (Round 4 A/Bs, not adopted and removed: one copy stream - no change; a
+  // highest-priority compute stream - much slower, the copy and resolve queues
+  // starve; profiles/r04_session2.md.)
+  ck(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "hipStreamCreate(compute)");
   h2d_done_.resize(slots);
   done_.resize(slots);
   used_.assign(size_t(slots), 0);
   observed_.reset(new std::atomic<bool>[size_t(slots)]);
   for (int i = 0; i < slots; ++i) observed_[i].store(false);
-  // DTFS_DONE_DEVICE_SCOPE=1 (A/B only): step-done events without the
-  // system-scope release (the scores are written to fine-grained host memory,
-  // which the L2 does not cache)
-  const char* de = std::getenv("DTFS_DONE_DEVICE_SCOPE");
-  const unsigned done_flags =
-      hipEventDisableTiming | ((de && std::atoi(de) == 1) ? hipEventDisableSystemFence : 0u);
+  // Step-done events keep the system-scope release: the head kernel writes the
+  // scores to pinned host memory, and only that release orders them before the
+  // signal the host polls (without it +1.5 %, not adopted: profiles/r04_session2.md).
+  const unsigned done_flags = hipEventDisableTiming;
   for (int i = 0; i < slots; ++i) {
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
     ck(hipEventCreateWithFlags(&done_[i], done_flags), "hipEventCreate");
@@ -148,7 +138,7 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
 void StepRunner::h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer,
                             bool alternate) {
   hipStream_t st = copy_;
-  if (alternate && two_copy_streams_) {
+  if (alternate) {
     if (!copy2_) ck(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking), "hipStreamCreate(copy2)");
     if (n_h2d_++ & 1) st = copy2_;
   }
@@ -267,14 +257,7 @@ void StepProgram::validate() const {
 // keeps its system-scope release (done_ events are created without
 // hipEventDisableSystemFence, and a bound event sets the scope of the command
 // it is bound to), so the scores the head kernel wrote to pinned host memory
-// are visible when it signals. DTFS_BIND_DONE=0 restores the marker.
-static bool bind_done_event() {
-  static const bool on = [] {
-    const char* e = std::getenv("DTFS_BIND_DONE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
+// are visible when it signals.
 
 void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_src, int64_t h2d_bytes,
                                 bool skip_varint) {
@@ -296,9 +279,8 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alias a queue and serialise the step)
   h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
-  const bool bind_done = bind_done_event();
   const ProgOp* last = p.ops.empty() ? nullptr : &p.ops.back();
-  const bool bound = bind_done && last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
+  const bool bound = last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
   for (const ProgOp& o : p.ops) {
     hipStream_t st = lanes[o.lane];
     switch (o.kind) {
@@ -354,7 +336,7 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d(slot, dst, src, nbytes, compute_, true);
-  seq->launch(compute_, done_[slot], bind_done_event(), skip_varint);
+  seq->launch(compute_, done_[slot], true, skip_varint);
   used_[slot] = 1;
 }
 
@@ -365,7 +347,7 @@ void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>
   ck(hipSetDevice(device_), "hipSetDevice");
   h2d_copies(slot, dst, copies, compute_, true);
   if (seq) {
-    seq->launch(compute_, done_[slot], bind_done_event(), skip_varint);
+    seq->launch(compute_, done_[slot], true, skip_varint);
   } else {
     ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
     ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");

@@ -166,7 +166,6 @@ class StepRunner {
   void h2d(int slot, void* dst, const void* src, int64_t nbytes, hipStream_t consumer, bool alternate);
   void h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer, bool alternate);
   hipStream_t copy2_ = nullptr;  // second H2D stream, alternated with copy_ by local steps
-  bool two_copy_streams_ = true;  // DTFS_COPY_STREAMS=1: one copy stream
   // default: the device waits (round 3, one box, 3 interleaved reps of the
   // served DeepFM step with fp32-weight 5.8 MB copies: 92.5 / 94.7 / 94.7 M
   // vs host wait 89.1 / 85.4 / 97.8 M; DLRM 66.7 vs 54.3 M with 8.6 MB copies)

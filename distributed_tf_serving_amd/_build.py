@@ -27,7 +27,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
 BUILD = os.path.join(REPO, "build", "native")
-ARCH = os.environ.get("DTFS_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # the only target (MI355X / CDNA4)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
