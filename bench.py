@@ -142,6 +142,9 @@ def parse_args():
                     help="offered load of the fixed-QPS latency run, whole node (requests/s; 0 = skip); at N > 1 "
                          "split evenly over the front-door ranks")
     ap.add_argument("--qps-seconds", type=float, default=1.0)
+    ap.add_argument("--qps-sweep", default="0.25,0.5,0.75,0.9",
+                    help="latency vs offered load: open-loop runs at these fractions of the measured capacity "
+                         "(requests/s of the throughput run), p50 / p99 each ('' = off)")
     ap.add_argument("--force-fanout", action="store_true",
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
@@ -458,6 +461,32 @@ def run_live(a, ctx, cfg, model, eng, B):
                               "p50_ms": round(float(red[0]), 3), "p99_ms": round(float(red[1]), 3),
                               "errors": int(red[2])}
         extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
+    fracs = [float(x) for x in a.qps_sweep.split(",") if x.strip()] if a.qps_sweep else []
+    if fracs and window_s > 0:
+        # the throughput run's request rate, whole node (slowest rank's window)
+        w = torch.tensor([window_s], dtype=torch.float64)
+        if ctx.is_distributed:
+            dist.all_reduce(w, op=dist.ReduceOp.MAX, group=phase)
+        cap_qps = a.steps * n_req / float(w[0]) * fronts if pool or fronts > 1 else 0.0
+        sweep = []
+        for f in fracs:
+            qps = f * cap_qps
+            sync()
+            q = {"latency_us": [], "errors": 0, "window_us": 0.0}
+            n = max(200, int(qps / fronts * a.qps_seconds))
+            if pool:
+                q = live.run_load(pool, warmup=n // 10, count=n, qps=qps / fronts, threads=a.client_threads,
+                                  timeout_us=timeout_us)
+            ach = n / (q["window_us"] * 1e-6) * fronts if q.get("window_us") else 0.0
+            red = torch.tensor([pct(q["latency_us"], 50) or 0.0, pct(q["latency_us"], 99) or 0.0,
+                                float(q["errors"]), -ach], dtype=torch.float64)
+            if ctx.is_distributed:  # slowest front door's percentiles, lowest achieved rate
+                dist.all_reduce(red, op=dist.ReduceOp.MAX, group=phase)
+            sweep.append({"load": f, "offered_qps": round(qps, 1), "achieved_qps": round(-float(red[3]), 1),
+                          "scores_per_s": round(qps * a.request_rows, 1), "p50_ms": round(float(red[0]), 3),
+                          "p99_ms": round(float(red[1]), 3), "errors": int(red[2])})
+        extra["latency_vs_load"] = {"capacity_qps": round(cap_qps, 1), "request_rows": a.request_rows,
+                                    "front_doors": fronts, "points": sweep}
     # BASELINE config 2 literally: one 512-candidate request at a time (at N > 1
     # fanned out over every GPU: the reference's topology inside one node)
     sync()
