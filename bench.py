@@ -462,19 +462,19 @@ def run_live(a, ctx, cfg, model, eng, B):
                               "errors": int(red[2])}
         extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
     fracs = [float(x) for x in a.qps_sweep.split(",") if x.strip()] if a.qps_sweep else []
-    if fracs and window_s > 0:
+    if fracs:  # every rank takes part (the collectives below); ranks without requests only follow
         # the throughput run's request rate, whole node (slowest rank's window)
         w = torch.tensor([window_s], dtype=torch.float64)
         if ctx.is_distributed:
             dist.all_reduce(w, op=dist.ReduceOp.MAX, group=phase)
-        cap_qps = a.steps * n_req / float(w[0]) * fronts if pool or fronts > 1 else 0.0
+        cap_qps = a.steps * n_req / float(w[0]) * fronts if float(w[0]) > 0 else 0.0
         sweep = []
         for f in fracs:
             qps = f * cap_qps
             sync()
             q = {"latency_us": [], "errors": 0, "window_us": 0.0}
             n = max(200, int(qps / fronts * a.qps_seconds))
-            if pool:
+            if pool and qps > 0:
                 q = live.run_load(pool, warmup=n // 10, count=n, qps=qps / fronts, threads=a.client_threads,
                                   timeout_us=timeout_us)
             ach = n / (q["window_us"] * 1e-6) * fronts if q.get("window_us") else 0.0
