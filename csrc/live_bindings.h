@@ -62,7 +62,8 @@ inline void def_step_control(py::module& m) {
           py::arg("timeout_s"))
       .def(
           "heartbeat_age", [](const StepControl& c, int r) { return double(c.heartbeat_age_us(r)) * 1e-6; },
-          py::arg("rank"), "seconds since the rank's last heartbeat")
+          py::arg("rank"), "seconds since the rank's last heartbeat (huge once its process exited)")
+      .def("process_gone", &StepControl::process_gone, py::arg("rank"), "the rank's process no longer exists")
       .def("set_closing", &StepControl::set_closing, py::arg("closing"))
       .def_property_readonly("all_closing", &StepControl::all_closing)
       .def("request_stop", &StepControl::request_stop)
@@ -229,6 +230,7 @@ inline LiveConfig live_config_from(const py::dict& d) {
   if (get("heartbeat_us")) c.heartbeat_us = d["heartbeat_us"].cast<int64_t>();
   if (get("step_timeout_us")) c.step_timeout_us = d["step_timeout_us"].cast<int64_t>();
   if (get("start_paused")) c.start_paused = d["start_paused"].cast<bool>();
+  if (get("liveness_only")) c.liveness_only = d["liveness_only"].cast<bool>();
   if (get("narrow_modulo")) c.narrow_modulo = d["narrow_modulo"].cast<int64_t>();
   if (get("narrow_wts_cols")) c.narrow_wts_cols = d["narrow_wts_cols"].cast<int64_t>();
   return c;

@@ -27,7 +27,7 @@ std::string shape_str(const std::vector<int64_t>& s) {
 
 LiveServer::LiveServer(StepBackend* backend, LiveConfig cfg, std::vector<std::pair<uint8_t*, int64_t>> arenas,
                        StepControl* ctl)
-    : backend_(backend), cfg_(std::move(cfg)), ctl_(ctl) {
+    : backend_(backend), cfg_(std::move(cfg)), ctl_(ctl), agree_(cfg_.liveness_only ? nullptr : ctl) {
   if (!backend_) throw std::invalid_argument("null StepBackend");
   const auto& bk = backend_->buckets();
   if (bk.empty() || !std::is_sorted(bk.begin(), bk.end()) || bk.front() <= 0)
@@ -366,7 +366,7 @@ void LiveServer::launcher_loop() {
       // open batch (fuller steps under load)
       auto slot_free = [&] { return inflight_ < cfg_.depth && !slot_busy_[size_t(next_slot_)]; };
       auto drained = [&] { return closing_ && sealed_.empty() && (open_ < 0 || arenas_[size_t(open_)].pend.empty()); };
-      if (!ctl_) {
+      if (!agree_) {
         cv_launch_.wait(lk, [&] { return broken_ || (!paused_ && (drained() || slot_free())) || (paused_ && closing_); });
         if (paused_ && closing_) break;  // never started: nothing was launched
         if (broken_ || !slot_free()) break;
@@ -391,7 +391,7 @@ void LiveServer::launcher_loop() {
           if (closing_ || idle || now >= o.t_first + cfg_.batch_timeout_us) local = true;
           else wake = o.t_first + cfg_.batch_timeout_us;
         }
-        if (!ctl_) {
+        if (!agree_) {
           if (!sealed_.empty()) {
             a = sealed_.front();
             sealed_.pop_front();
@@ -417,13 +417,13 @@ void LiveServer::launcher_loop() {
           k = uint64_t(steps_launched_);
           if (drained() && !closing_posted_) {
             closing_posted_ = true;
-            ctl_->set_closing(true);
+            agree_->set_closing(true);
           }
-          if (closing_posted_ && ctl_->all_closing() && ctl_->proposed() <= k) {
+          if (closing_posted_ && agree_->all_closing() && agree_->proposed() <= k) {
             stop = true;
             break;
           }
-          remote = ctl_->proposed() > k;
+          remote = agree_->proposed() > k;
           if ((remote || local) && slot_free()) {
             if (!sealed_.empty()) {
               a = sealed_.front();
@@ -452,17 +452,17 @@ void LiveServer::launcher_loop() {
         }
         // nothing to launch yet: sleep until a submit / slot release / the
         // batch timeout, or (cluster) a proposal, which the watcher relays
-        if (ctl_ && !(remote || local)) {
+        if (agree_ && !(remote || local)) {
           launcher_idle_.store(true, std::memory_order_seq_cst);
-          ctl_->set_idle(true);
+          agree_->set_idle(true);
           // re-check after announcing idleness (seq_cst against propose())
-          if (ctl_->proposed() <= k && !broken_) {
+          if (agree_->proposed() <= k && !broken_) {
             if (wake > 0) cv_launch_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
             else cv_launch_.wait_for(lk, std::chrono::microseconds(cfg_.heartbeat_us));
           }
-          ctl_->set_idle(false);
+          agree_->set_idle(false);
           launcher_idle_.store(false, std::memory_order_seq_cst);
-        } else if (ctl_) {
+        } else if (agree_) {
           // a step to launch but no free slot / arena yet: release() notifies
           cv_launch_.wait_for(lk, std::chrono::microseconds(cfg_.heartbeat_us));
         } else if (wake > 0) {
@@ -484,16 +484,16 @@ void LiveServer::launcher_loop() {
       ++steps_launched_;
     }
     int agreed = -1;
-    if (ctl_) {
+    if (agree_) {
       // agree on step k's bucket with every rank (step_control.h)
       const int mine = arena_rows > 0 ? bucket_for(arena_rows) : 0;
       std::string gerr;
       int b = -1;
       try {
         trace::Range tr("live_agree");
-        if (!remote) ctl_->propose(k);
-        ctl_->post(k, mine);
-        b = ctl_->gather(k, cfg_.step_timeout_us, &gerr);
+        if (!remote) agree_->propose(k);
+        agree_->post(k, mine);
+        b = agree_->gather(k, cfg_.step_timeout_us, &gerr);
       } catch (const std::exception& e) {
         gerr = e.what();
       }
@@ -501,7 +501,7 @@ void LiveServer::launcher_loop() {
         const std::string why = "step agreement failed: " + (b >= nb ? std::string("bucket out of range") : gerr);
         fail_all(pend, kUnavailable, "server unavailable: " + why);
         release(a, slot);
-        ctl_->mark_broken(ctl_->rank());
+        agree_->mark_broken(agree_->rank());
         go_broken(why);
         break;
       }
@@ -532,10 +532,10 @@ void LiveServer::launcher_loop() {
                                 cfg_.varint_chunks, cfg_.narrow_wts_cols, narrow_id_bytes());
     } catch (const std::exception& e) {
       fail_all(live, kInternal, std::string("batch build failed: ") + e.what());
-      if (ctl_) {  // the other ranks launch step k: this rank cannot skip it
+      if (agree_) {  // the other ranks launch step k: this rank cannot skip it
         const std::string why = std::string("batch build failed in a cluster step: ") + e.what();
         release(a, slot);
-        ctl_->mark_broken(ctl_->rank());
+        agree_->mark_broken(agree_->rank());
         go_broken(why);
         break;
       }
@@ -547,7 +547,7 @@ void LiveServer::launcher_loop() {
       continue;
     }
     const int64_t t1 = now_us();
-    if (batch.n_valid == 0 && !ctl_) {
+    if (batch.n_valid == 0 && !agree_) {
       // nothing to compute: every request was malformed (or none left)
       for (size_t i = 0; i < live.size(); ++i)
         if (live[i].done) live[i].done(Reply{kInvalidArgument, batch.errors[i], std::string()});
@@ -560,7 +560,7 @@ void LiveServer::launcher_loop() {
       release(a, slot);
       continue;
     }
-    const int b = ctl_ ? agreed : bucket_for(batch.total_rows);
+    const int b = agree_ ? agreed : bucket_for(batch.total_rows);
     try {
       trace::Range tr("live_launch");
       backend_->launch(slot, b, ar.base, batch);
@@ -568,7 +568,7 @@ void LiveServer::launcher_loop() {
       const std::string why = std::string("step launch failed: ") + e.what();
       fail_all(live, kUnavailable, why);
       release(a, slot);
-      if (ctl_) ctl_->mark_broken(ctl_->rank());
+      if (agree_) agree_->mark_broken(agree_->rank());
       go_broken(why);
       break;
     }
@@ -589,7 +589,7 @@ void LiveServer::launcher_loop() {
     cv_done_.notify_all();
     cv_space_.notify_all();
   }
-  if (ctl_ && !closing_posted_) ctl_->set_closing(true);
+  if (agree_ && !closing_posted_) agree_->set_closing(true);
   // whatever is still queued will not be launched
   std::vector<Pending> orphans;
   {
@@ -624,8 +624,10 @@ void LiveServer::watcher_loop() {
         const int silent = ctl_->silent_peer(cfg_.peer_timeout_us);
         if (silent >= 0) {
           ctl_->mark_broken(ctl_->rank());
-          go_broken("rank " + std::to_string(silent) + " stopped answering (no heartbeat for " +
-                    std::to_string(cfg_.peer_timeout_us / 1000) + " ms)");
+          go_broken(ctl_->process_gone(silent)
+                        ? "rank " + std::to_string(silent) + " exited"
+                        : "rank " + std::to_string(silent) + " stopped answering (no heartbeat for " +
+                              std::to_string(cfg_.peer_timeout_us / 1000) + " ms)");
         }
       }
     }

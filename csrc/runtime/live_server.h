@@ -102,6 +102,11 @@ struct LiveConfig {
   // is older than peer_timeout_us breaks the cluster; heartbeat_us is the
   // watcher's period.
   int64_t peer_timeout_us = 5'000'000;
+  // liveness_only: the StepControl only carries heartbeats and the broken flag
+  // (ranks whose steps have no collectives but read each other's memory: the
+  // sharded DLRM's peer exchange maps every owner's tables by IPC). Steps are
+  // not agreed; a silent peer still breaks this server (UNAVAILABLE).
+  bool liveness_only = false;
   int64_t heartbeat_us = 20'000;
   // Launch nothing until resume() (requests are admitted and queue): a server
   // whose step issues torch.distributed collectives from the launcher thread
@@ -205,7 +210,8 @@ class LiveServer {
 
   StepBackend* backend_;
   LiveConfig cfg_;
-  StepControl* ctl_ = nullptr;
+  StepControl* ctl_ = nullptr;    // heartbeats + the cluster's broken flag (watcher thread)
+  StepControl* agree_ = nullptr;  // ctl_ unless liveness_only: every step agreed with the other ranks
   int64_t max_rows_ = 0;
   int64_t arena_budget_ = 0;  // payload bytes a batch may plan for (see need_of)
 

@@ -4,6 +4,7 @@
 #include <linux/futex.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <signal.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -76,8 +77,14 @@ StepControl::StepControl(const std::string& name, int world, int rank, bool crea
     }
   }
   attach_us_ = now_us();
+  s_->ranks[rank_].pid.store(int32_t(getpid()), std::memory_order_release);
   s_->ranks[rank_].attached.store(1, std::memory_order_release);
   heartbeat();
+}
+
+bool StepControl::process_gone(int r) const {
+  const int32_t pid = s_->ranks[r].pid.load(std::memory_order_acquire);
+  return pid > 0 && ::kill(pid, 0) != 0 && errno == ESRCH;  // signal 0: existence probe only
 }
 
 StepControl::~StepControl() {
@@ -177,6 +184,7 @@ void StepControl::heartbeat() { s_->ranks[rank_].heartbeat_us.store(now_us(), st
 
 int64_t StepControl::heartbeat_age_us(int r) const {
   if (r < 0 || r >= world_) throw std::out_of_range("step control: rank out of range");
+  if (r != rank_ && process_gone(r)) return INT64_MAX / 4;
   int64_t hb = s_->ranks[r].heartbeat_us.load(std::memory_order_acquire);
   if (hb == 0) hb = attach_us_;
   return now_us() - hb;
@@ -186,6 +194,7 @@ int StepControl::silent_peer(int64_t timeout_us) const {
   const int64_t now = now_us();
   for (int r = 0; r < world_; ++r) {
     if (r == rank_) continue;
+    if (process_gone(r)) return r;
     int64_t hb = s_->ranks[r].heartbeat_us.load(std::memory_order_acquire);
     if (hb == 0) hb = attach_us_;  // not attached yet: give it the timeout from our start
     if (now - hb > timeout_us) return r;

@@ -41,6 +41,7 @@ struct alignas(64) CtlRank {
   std::atomic<int64_t> heartbeat_us;      // CLOCK_MONOTONIC microseconds; 0 = not started
   std::atomic<uint32_t> closing;          // this rank stopped admitting and has nothing queued
   std::atomic<uint32_t> attached;
+  std::atomic<int32_t> pid;               // the rank's process: a peer whose process is gone is dead at once
 };
 
 struct CtlShared {
@@ -95,8 +96,13 @@ class StepControl {
   // First peer whose heartbeat is older than timeout_us (-1: all alive). A peer
   // that never started is judged from `since_us` (this rank's attach time).
   int silent_peer(int64_t timeout_us) const;
-  // Microseconds since rank r's last heartbeat (its attach time if it never beat).
+  // Microseconds since rank r's last heartbeat (its attach time if it never beat);
+  // "forever" once r's process has exited (all ranks of a node share a PID
+  // namespace: a dead rank is seen within one watcher period, not after the
+  // peer timeout - the peer exchange's readers must stop loading from its store).
   int64_t heartbeat_age_us(int r) const;
+  // Rank r's process no longer exists.
+  bool process_gone(int r) const;
 
   void set_closing(bool v);
   bool all_closing() const;

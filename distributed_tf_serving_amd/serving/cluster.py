@@ -15,6 +15,17 @@ that fan-out moves inside one node, onto the native live server of every rank
               (RCCL / the one-shot peer kernel) and gathers the scores back.
 ``alltoall``  every rank is a front door (gRPC port + rank); each rank's rows
               are split over all GPUs and the scores return to it.
+``local``     every rank is a front door and scores its own requests on its
+              own GPU. With a sharded-table model (DLRM, BASELINE config 4) the
+              tables live sharded over the ranks and each rank's steps read the
+              other ranks' shards where they live (the peer exchange:
+              IPC-mapped stores, parallel/embedding_sharding.py): no collective
+              in the step, but every rank depends on every table owner. The
+              step control then carries liveness only (heartbeats + the broken
+              flag, no step agreement): a dead owner turns every rank's requests
+              into UNAVAILABLE within ``control_timeout_s``, and ``--recover``
+              re-plans the tables over the survivors (their rows are rebuilt
+              from the tables' hashed initialisation, so scores do not change).
 
 Steps are agreed through a shared-memory step control (parallel/control.py,
 csrc/runtime/step_control.h): a step runs only when some rank has requests
@@ -116,8 +127,8 @@ class ClusterServer:
     # -- construction -------------------------------------------------------------
     @property
     def serves(self) -> bool:
-        """This rank is a front door (rank 0; every rank in alltoall mode)."""
-        return self.rank == 0 or self.mode == "alltoall"
+        """This rank is a front door (rank 0; every rank in alltoall / local mode)."""
+        return self.rank == 0 or self.mode in ("alltoall", "local")
 
     def _module(self):
         from ..ops import hip, native
@@ -142,10 +153,13 @@ class ClusterServer:
             if not eng.self_check(B, seed=self.epoch):
                 raise RuntimeError("fan-out self-check failed: the native step's scores differ from a local forward")
         ctl = None
-        if world > 1 and eng.lockstep:
+        # lockstep engines agree every step; independent ranks (local mode:
+        # the peer exchange's table owners) share the segment for liveness only
+        liveness_only = world > 1 and not eng.lockstep and mode == "local"
+        if world > 1 and (eng.lockstep or liveness_only):
             ctl = create_control(self._module(), world, ctx.rank, store=store,
                                  prefix=f"dtfs/ctl/cluster/{self.epoch}")
-        servable = build_servable(self.cfg, slots=self.slots, engine=eng, control=ctl)
+        servable = build_servable(self.cfg, slots=self.slots, engine=eng, control=ctl, liveness_only=liveness_only)
         with self._lock:
             self.engine, self.ctl, self.sched, self.ctx = eng, ctl, servable.scheduler, ctx
             self.rank, self.world = (ctx.rank, world) if world > 1 else (0, 1)
@@ -344,8 +358,10 @@ class ClusterServer:
 def main(argv=None):
     ap = argparse.ArgumentParser(description="multi-GPU CTR model server (rank 0 = PredictionService front door)")
     ap.add_argument("--preset", default="deepfm_fanout4")
-    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall"],
-                    help="scatter: rank 0 is the only front door; alltoall: every rank serves on port + rank")
+    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall", "local"],
+                    help="scatter: rank 0 is the only front door; alltoall: every rank serves on port + rank; "
+                         "local: every rank serves its own requests on port + rank (sharded DLRM: tables read "
+                         "where they live, config 4)")
     ap.add_argument("--port", type=int, default=9999)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--grpc-workers", type=int, default=32)
@@ -377,7 +393,7 @@ def main(argv=None):
         if not a.no_gc_freeze:  # every rank, after warm-up, before traffic
             tune_for_serving()
         if srv.serves:
-            p = a.port + (srv.rank if a.mode == "alltoall" else 0)
+            p = a.port + (srv.rank if a.mode in ("alltoall", "local") else 0)
             if a.front == "native":
                 port = srv.start_native_grpc(p, a.host, a.front_threads)
                 if a.monitoring_port is not None and srv.rank == 0:

@@ -49,11 +49,16 @@ class LiveScheduler:
     def __init__(self, engine, serving_cfg, buckets: Optional[Sequence[int]] = None, n_arenas: Optional[int] = None,
                  depth: Optional[int] = None, control=None, step_timeout_s: float = 10.0,
                  model_name: Optional[str] = None, version: Optional[int] = None, start_paused: bool = False,
-                 narrow: Optional[bool] = None, peer_timeout_s: float = 5.0):
+                 narrow: Optional[bool] = None, peer_timeout_s: float = 5.0, liveness_only: bool = False):
         """``control``: the job's StepControl (parallel/control.py) when the
         step has collectives (fan-out, sharded tables): every step is then
         agreed with the other ranks - launched only when some rank has work,
-        at the largest bucket any rank needs (csrc/runtime/step_control.h)."""
+        at the largest bucket any rank needs (csrc/runtime/step_control.h).
+        ``liveness_only``: the control only carries heartbeats and the broken
+        flag - steps are this rank's own (no collectives in them) but read the
+        other ranks' memory (the sharded DLRM's peer exchange), so a silent peer
+        must still fail requests UNAVAILABLE instead of letting them read a dead
+        owner's tables."""
         if engine.ingest != "arena":
             raise ValueError("the live server needs an arena-ingest FanoutEngine")
         sc = serving_cfg
@@ -106,6 +111,7 @@ class LiveScheduler:
             max_pending=max(64, sc.max_queued_rows // max(1, min(self.buckets))),
             step_timeout_us=int(step_timeout_s * 1e6), peer_timeout_us=int(peer_timeout_s * 1e6),
             start_paused=start_paused, narrow_modulo=self.narrow_modulo, narrow_wts_cols=self.narrow_wts_cols,
+            liveness_only=bool(liveness_only and control is not None),
             caller_outputs=["sorted_prediction", "sorted_index"])  # service.RANKED_OUTPUTS
         if engine.cuda:
             from ..ops import hip

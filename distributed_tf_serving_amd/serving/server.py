@@ -106,9 +106,11 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
 
 
 def build_servable(cfg: Config, device=None, version: Optional[int] = None, slots: int = 3,
-                   engine: Optional[FanoutEngine] = None, control=None) -> Servable:
+                   engine: Optional[FanoutEngine] = None, control=None, liveness_only: bool = False) -> Servable:
     """``control``: the job's StepControl (parallel/control.py) when the
-    engine's step has collectives (every rank's live server agrees on it)."""
+    engine's step has collectives (every rank's live server agrees on it), or
+    with ``liveness_only`` for ranks that serve independently but read each
+    other's memory (heartbeats + broken flag only)."""
     sc = cfg.serving
     eng = engine or build_engine(cfg, device, slots)
     model = eng.ex.model
@@ -118,7 +120,8 @@ def build_servable(cfg: Config, device=None, version: Optional[int] = None, slot
             raise ValueError("a multi-rank engine with collectives in its step needs a StepControl")
         sched = LiveScheduler(eng, sc, version=sc.version if version is None else version,
                               step_timeout_s=sc.step_timeout_s, control=control,
-                              peer_timeout_s=getattr(sc, "peer_timeout_s", 5.0), start_paused=control is not None)
+                              peer_timeout_s=getattr(sc, "peer_timeout_s", 5.0), start_paused=control is not None,
+                              liveness_only=liveness_only)
     else:
         sched = BatchingScheduler(eng, max_batch_rows=sc.max_batch_rows, batch_timeout_us=sc.batch_timeout_us,
                                   max_queued_rows=sc.max_queued_rows, depth=max(1, slots - 1), name=sc.model_name,

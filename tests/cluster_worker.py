@@ -22,7 +22,10 @@ if REPO not in sys.path:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall"])
+    ap.add_argument("--mode", default="scatter", choices=["scatter", "alltoall", "local"])
+    ap.add_argument("--preset", default="deepfm", choices=["deepfm", "dlrm"],
+                    help="dlrm: BASELINE config 4 scaled down - tables sharded over the ranks, read where they "
+                         "live (peer exchange), checked against the unsharded model")
     ap.add_argument("--out", required=True)
     ap.add_argument("--grpc-port", type=int, default=0, help="> 0: also serve gRPC on port + rank and query it")
     ap.add_argument("--front", default="native", choices=["native", "grpcio"],
@@ -49,10 +52,23 @@ def main():
     ctx = init_from_env(timeout_s=120)
     rank = ctx.rank
     gpu = ctx.device.type == "cuda"
-    cfg = load_preset("deepfm_1gpu")
-    cfg.model.vocab_size = 100_000
-    if not gpu:  # small enough for gloo on a CPU test box
-        cfg.model.embed_dim, cfg.model.mlp_dims = 16, (32, 16)
+    ref = None  # the scores every request must match (default: the served model's own forward)
+    if a.preset == "dlrm":
+        from distributed_tf_serving_amd.models import build_model
+
+        cfg = load_preset("dlrm_sharded8")
+        cfg.model.table_rows = 5000
+        cfg.model.embedding_exchange = "peer"
+        cfg.model.hot_cache_rows = 1024
+        if not gpu:
+            cfg.model.bottom_mlp, cfg.model.mlp_dims = (32, 64), (64, 32)
+        ref = build_model(cfg.model, ctx.device)  # unsharded: the same hashed tables, materialised
+    else:
+        cfg = load_preset("deepfm_1gpu")
+        cfg.model.vocab_size = 100_000
+        if not gpu:  # small enough for gloo on a CPU test box
+            cfg.model.embed_dim, cfg.model.mlp_dims = 16, (32, 16)
+    cfg.serving.model_name = "DCN"
     cfg.serving.device = "cuda" if gpu else "cpu"
     cfg.serving.max_batch_rows = 768
     cfg.serving.allowed_batch_sizes = (96, 768)  # divisible by 1, 2, 3
@@ -71,14 +87,14 @@ def main():
         if srv.serves:
             from distributed_tf_serving_amd.serving.errors import ServingError
 
-            model = srv.registry.resolve("DCN").model
+            model = ref or srv.registry.resolve("DCN").model
             synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=7 + rank)
             outcomes, diffs = [], []
             t_end = time.monotonic() + 70
             injected = False
             while time.monotonic() < t_end:
                 n_ok = outcomes.count("ok")
-                if a.mode == "alltoall" and rank == a.kill_rank and n_ok >= a.kill_after:
+                if a.mode in ("alltoall", "local") and rank == a.kill_rank and n_ok >= a.kill_after:
                     os._exit(17)
                 if rank == a.inject_comm_error and n_ok >= a.kill_after and not injected:
                     time.sleep(0.3)  # the front door is idle when the error arrives
@@ -103,12 +119,14 @@ def main():
                        world_after=srv.world)
             with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
                 json.dump(res, f)  # before stop(): a survivor's peers may already be gone
-            # alltoall: every front door keeps its live server up (joining the
-            # others' steps) until all of this epoch's front doors are done
+            # alltoall / local: every front door keeps its live server up (joining
+            # the others' steps; local: its table shards stay mapped by the
+            # others) until all of this epoch's front doors are done
             key = f"test/done/{srv.epoch}"
             srv._store.add(key, 1)
             t_wait = time.monotonic() + 60
-            while srv.mode == "alltoall" and srv._store.add(key, 0) < srv.world and time.monotonic() < t_wait:
+            while srv.mode in ("alltoall", "local") and srv._store.add(key, 0) < srv.world and \
+                    time.monotonic() < t_wait:
                 time.sleep(0.05)
             srv.stop()
         else:
@@ -121,7 +139,7 @@ def main():
     srv = ClusterServer(cfg, ctx, mode=a.mode, control_timeout_s=20, step_timeout_s=20, follower_fault=fault)
     res = {"rank": rank, "serves": srv.serves}
     if srv.serves:
-        model = srv.registry.resolve("DCN").model
+        model = ref or srv.registry.resolve("DCN").model
         synth = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=100 + rank)
         reqs = []
         for i in range(a.requests):
@@ -148,7 +166,7 @@ def main():
 
             # alltoall: every rank is a front door; an ephemeral port each (port + rank
             # could collide with the rendezvous / RCCL sockets)
-            p = 0 if a.mode == "alltoall" else a.grpc_port
+            p = 0 if a.mode in ("alltoall", "local") else a.grpc_port
             port = (srv.start_native_grpc(p, host="127.0.0.1") if a.front == "native"
                     else srv.start_grpc(p, host="127.0.0.1"))
             be = GrpcBackend(f"127.0.0.1:{port}")

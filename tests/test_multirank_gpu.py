@@ -179,3 +179,48 @@ def test_cluster_recovers_over_surviving_ranks_sharing_one_gpu(tmp_path):
     assert r0["recoveries"] == 1 and r0["world_after"] == 2 and r0["max_diff"] < 1e-4, r0
     r1 = json.load(open(tmp_path / "rank1.json"))
     assert r1["recoveries"] == 1 and r1["world_after"] == 2, r1
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_local_cluster_sharded_dlrm_ranks_sharing_one_gpu(tmp_path, n):
+    """BASELINE config 4 served as a cluster on hardware: every rank is a front
+    door over the sharded DLRM (tables read where they live through IPC-mapped
+    stores, no collective in the step); in-process and gRPC scores equal the
+    unsharded model's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tests/cluster_worker.py",
+           "--mode", "local", "--preset", "dlrm", "--out", str(tmp_path), "--grpc-port", str(_port())]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    errs = {f.name: f.read_text()[-3000:] for f in sorted(tmp_path.glob("rank*.err"))}
+    assert p.returncode == 0, (errs, p.stdout[-2000:], p.stderr[-2000:])
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
+    for r in res:
+        assert r["serves"] and r["max_diff"] < 1e-3 and r["grpc_max_diff"] < 1e-3, r
+        assert r["idle_steps"] == 0 and not r["broken"], r
+
+
+def test_local_cluster_dead_table_owner_sharing_one_gpu(tmp_path):
+    """A table owner of the peer exchange dies (rank 2 of 3, one shared GPU).
+    Its IPC-exported stores stay valid for the importers (the dma-buf import
+    holds its own reference to the memory: no GPU fault for the steps already
+    in flight), the survivors see the process gone within one watcher period,
+    answer UNAVAILABLE, re-plan the tables over ranks 0-1 and serve the
+    unsharded model's scores again."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_cluster_server import spawn_launched
+
+    procs, outs = spawn_launched(3, ["--mode", "local", "--preset", "dlrm", "--out", str(tmp_path), "--kill-rank",
+                                     "2", "--kill-after", "3"],
+                                 dict(DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100"), timeout=110)
+    assert procs[2].returncode == 17, outs[2][-2000:]
+    for r in (0, 1):
+        f = tmp_path / f"rank{r}.json"
+        assert f.exists(), outs[r][-3000:]
+        res = json.load(open(f))
+        out = res["outcomes"]
+        assert "UNAVAILABLE" in out and out[-5:] == ["ok"] * 5, out
+        assert res["recoveries"] == 1 and res["world_after"] == 2 and res["max_diff"] < 1e-3, res

@@ -149,14 +149,22 @@ def test_deadline_exceeded_on_the_client_and_server_survives(front):
     synth = SyntheticRequests(fields=F, seed=14)
     data = synth.serialized(8)
     # a 100 us deadline expires before (or while) the call is served - unless
-    # the in-process server answers inside it, so try a few times
+    # an idle server answers inside it (it can, on an idle host): each try is
+    # queued behind a burst of full batches on another channel
+    busy = _channel(fr.port)
+    big = synth.serialized(64)
     codes = []
     for _ in range(20):
+        burst = [busy.unary_unary(PREDICT).future(big) for _ in range(16)]
         try:
             assert _scores(ch.unary_unary(PREDICT)(data, timeout=1e-4)).shape == (8,)
         except grpc.RpcError as e:
             codes.append(e.code())
+        for f in burst:
+            f.result(timeout=60)
+        if codes:
             break
+    busy.close()
     assert codes == [grpc.StatusCode.DEADLINE_EXCEEDED], codes
     # the connection and the server keep working after the cancelled stream
     assert _scores(ch.unary_unary(PREDICT)(data, timeout=20)).shape == (8,)

@@ -94,3 +94,34 @@ def test_timeout_liveness_and_broken_flag():
     with pytest.raises(RuntimeError):
         native().StepControl(name, 2, 1, False)  # unlinked: nobody can attach any more
     del store, pfx
+
+
+def _attach_and_exit(name):
+    from distributed_tf_serving_amd.ops import native as _native
+
+    c = _native().StepControl(name, 2, 1, False)
+    c.heartbeat()
+    os._exit(0)  # no close: the segment keeps this rank's last heartbeat and pid
+
+
+def test_exited_peer_is_dead_at_once():
+    """A rank whose process exited is reported by silent_peer / heartbeat_age
+    immediately (pid probe), not after the peer timeout: the peer exchange's
+    readers stop loading from a dead owner's store within one watcher period."""
+    import time
+    import uuid
+
+    name = f"/dtfs_t_{uuid.uuid4().hex[:8]}"
+    c0 = native().StepControl(name, 2, 0, True)
+    try:
+        p = mp.get_context("spawn").Process(target=_attach_and_exit, args=(name,))
+        p.start()
+        p.join(timeout=60)
+        assert p.exitcode == 0
+        t0 = time.monotonic()
+        assert c0.silent_peer(3600.0) == 1  # an hour's timeout: the pid probe decides
+        assert c0.process_gone(1) and not c0.process_gone(0)
+        assert c0.heartbeat_age(1) > 1e6
+        assert time.monotonic() - t0 < 1.0
+    finally:
+        c0.unlink()
