@@ -128,6 +128,12 @@ def parse_args():
     ap.add_argument("--cache-learn-rounds", type=int, default=6,
                     help="peer exchange: untimed (max(8, warmup)-step run + cache refresh) rounds before the clock "
                          "(a server refreshes every second)")
+    ap.add_argument("--cache-refresh-s", type=float, default=0.0,
+                    help="peer exchange: > 0 keeps the background refresher running (this period) through the "
+                         "timed run, so the clock covers the refreshes' cost")
+    ap.add_argument("--stream-pool", type=int, default=4096,
+                    help="peer exchange: distinct pre-serialized requests per rank (a long, non-repeating stream "
+                         "for the replica cache to learn; --pool for every other model)")
     ap.add_argument("--small-buckets", default=None,
                     help="extra padding buckets (rows per GPU) below the full step, so a lightly loaded server "
                          "runs a step sized to what is queued (TF-Serving allowed_batch_sizes; at N > 1 every "
@@ -279,7 +285,8 @@ def request_pool(a, ctx, eng, B, F):
         synth = SyntheticRequests(fields=F, dist="reference")
         return ([synth.serialized(a.request_rows, raw=False)] if rows_in else []), n_req
     synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank)
-    n = max(1, a.pool) if n_req else 0
+    peer = getattr(getattr(getattr(eng.ex, "model", None), "emb", None), "peer", None) is not None
+    n = max(1, a.stream_pool if peer else a.pool) if n_req else 0
     return [synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n)], n_req
 
 
@@ -428,6 +435,8 @@ def run_live(a, ctx, cfg, model, eng, B):
             cache.refresh()
         sync()
         cache.reset_counts()
+        if a.cache_refresh_s > 0:  # the serving configuration: refreshes run while the clock does
+            cache.start(a.cache_refresh_s)
     steps0 = live.stats()["steps"]
     if pool:
         r = live.run_load(pool, warmup=untimed * n_req, count=a.steps * n_req, concurrency=conc,
@@ -550,6 +559,8 @@ def run_live(a, ctx, cfg, model, eng, B):
         per = {k: round(st[k] / max(1, st["steps"]), 1) for k in ("copy_us", "build_us", "launch_us", "wait_us",
                                                                   "encode_us")}
         print(json.dumps({"server_us_per_step": per, "stats": st}), file=sys.stderr, flush=True)
+    if cache is not None:
+        cache.stop()  # the background refresher (--cache-refresh-s)
     live.close()  # cluster: returns once every rank has closed
     sync()
     return window_s, extra
@@ -735,7 +746,8 @@ def main():
                 "encoding": a.encoding,
                 "path": ("served: native live server (batching, arena copy, parse, step, encode) driven by "
                          "in-process native client threads"),
-                "two_lane_buckets": sorted(eng._program_buckets),  # steps run as a two-lane program
+                # steps run as a two-lane program (fan-out: resolve pass on the ingress lane)
+                "two_lane_buckets": sorted(set(eng._program_buckets) | {k[0] for k, v in eng._split.items() if v}),
                 # CUs of the program's aux lane (0: unmasked; step_runner.cpp ensure_aux_stream)
                 "aux_lane_cus": int(getattr(getattr(eng, "_runner", None), "aux_cus", 0) or 0),
             },

@@ -327,7 +327,8 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
                                       c10::optional<torch::Tensor> wts, int64_t B, int64_t F, int64_t modulo,
                                       double bias, torch::Tensor W, torch::Tensor b, int64_t act, bool fm2,
                                       c10::optional<torch::Tensor> cross_w, c10::optional<torch::Tensor> cross_c,
-                                      c10::optional<std::vector<torch::Tensor>> resolved) {
+                                      c10::optional<std::vector<torch::Tensor>> resolved,
+                                      c10::optional<torch::Tensor> Wp) {
   check_dev(table, "table");
   check_dev(W, "W");
   check_dev(b, "b");
@@ -383,6 +384,18 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
   const torch::Tensor &rows_t = r[0], &wts_t = r[1], &parts = r[2];
   if (B == 0) return {h, parts};
   auto st = cur_stream(table);
+  if (Wp && dtfs::gemm_gather1w_ok(Mp, int(N), int(F), cross)) {
+    // one wave per SIMD, B from registers (csrc/kernels/gather_gemm.hip)
+    check_dev(*Wp, "Wp");
+    check_same_dev(table, *Wp, "Wp");
+    TORCH_CHECK(Wp->scalar_type() == torch::kBFloat16 && Wp->numel() == W.numel() && Wp->is_contiguous(),
+                "Wp must be W packed in MFMA fragment order (ops.pack_bfrag)");
+    check_hip(dtfs::launch_gemm_gather1w(table.data_ptr(), V, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), Mp,
+                                         int(F), Wp->data_ptr(), b.data_ptr<float>(), h.data_ptr(), N,
+                                         fm2 ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st),
+              "gemm_gather1w");
+    return {h, parts};
+  }
   check_hip(dtfs::launch_gemm_gather(table.data_ptr(), V, rows_t.data_ptr<int32_t>(), wts_t.data_ptr<float>(), Mp,
                                      int(F), W.data_ptr(), b.data_ptr<float>(), h.data_ptr(), N,
                                      (fm2 || cross) ? parts.data_ptr<float>() : nullptr, int(B), int(N), int(act), st,
@@ -1485,6 +1498,10 @@ dtfs::runtime::LoopSlot loop_slot_from(const py::dict& d, std::vector<py::object
       s.fan.forward_seq = &d["forward_seq"].cast<dtfs::runtime::KernelSequence&>();
     if (d.contains("ingress_seq") && !d["ingress_seq"].is_none())
       s.fan.ingress_seq = &d["ingress_seq"].cast<dtfs::runtime::KernelSequence&>();
+    if (d.contains("resolve_exec") && !d["resolve_exec"].is_none())
+      s.fan.resolve = reinterpret_cast<hipGraphExec_t>(d["resolve_exec"].cast<uintptr_t>());
+    if (d.contains("resolve_seq") && !d["resolve_seq"].is_none())
+      s.fan.resolve_seq = &d["resolve_seq"].cast<dtfs::runtime::KernelSequence&>();
   } else {
     s.h2d_dst = dst.data_ptr();
     s.h2d_cap = int64_t(dst.nbytes());
@@ -1588,6 +1605,7 @@ class GpuBackend : public dtfs::runtime::StepBackend {
       dtfs::runtime::FanoutStep f = s.fan;
       f.h2d_src = arena;
       f.h2d_bytes = nbytes;
+      f.skip_varint = batch.n_gpu_varint == 0;
       runner_->launch_fanout(slot, f);
     } else {
       if (nbytes > s.h2d_cap) throw std::runtime_error("batch larger than the device arena");
@@ -1670,7 +1688,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("embed_gemm", &embed_gemm, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"), py::arg("wts"),
         py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W"), py::arg("b"), py::arg("act"),
         py::arg("fm2"), py::arg("cross_w") = py::none(), py::arg("cross_c") = py::none(),
-        py::arg("resolved") = py::none());
+        py::arg("resolved") = py::none(), py::arg("Wp") = py::none());
   m.def("embed_gemm_resolve", &embed_gemm_resolve, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"),
         py::arg("wts"), py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("n_parts"),
         "gather-GEMM front half (K1 resolve) -> (rows_t, wts_t, parts) for embed_gemm(resolved=...)");
@@ -1768,7 +1786,7 @@ PYBIND11_MODULE(_hip, m) {
           [](dtfs::runtime::StepRunner& r, int slot, torch::Tensor h2d_dst, torch::Tensor h2d_src, int64_t h2d_bytes,
              uintptr_t ingress_exec, dtfs::comm::RcclComm& cin, int mode, torch::Tensor send, torch::Tensor recv,
              uintptr_t forward_exec, dtfs::comm::RcclComm& cout, torch::Tensor scores, torch::Tensor back,
-             torch::Tensor h_out, int64_t d2h_bytes) {
+             torch::Tensor h_out, int64_t d2h_bytes, uintptr_t resolve_exec) {
             TORCH_CHECK(h2d_src.device().is_cpu() && h2d_src.is_pinned(), "h2d_src must be pinned host memory");
             TORCH_CHECK(h2d_bytes >= 0 && h2d_bytes <= int64_t(h2d_dst.nbytes()) &&
                             h2d_bytes <= int64_t(h2d_src.nbytes()),
@@ -1777,11 +1795,12 @@ PYBIND11_MODULE(_hip, m) {
                                       h_out, d2h_bytes);
             s.h2d_src = h2d_src.data_ptr();
             s.h2d_bytes = h2d_bytes;
+            s.resolve = reinterpret_cast<hipGraphExec_t>(resolve_exec);
             r.launch_fanout(slot, s);
           },
           py::arg("slot"), py::arg("h2d_dst"), py::arg("h2d_src"), py::arg("h2d_bytes"), py::arg("ingress_exec"),
           py::arg("cin"), py::arg("mode"), py::arg("send"), py::arg("recv"), py::arg("forward_exec"), py::arg("cout"),
-          py::arg("scores"), py::arg("back"), py::arg("h_out"), py::arg("d2h_bytes"))
+          py::arg("scores"), py::arg("back"), py::arg("h_out"), py::arg("d2h_bytes"), py::arg("resolve_exec") = 0)
       .def(
           "launch_program",
           [](dtfs::runtime::StepRunner& r, int slot, py::dict program, torch::Tensor h2d_src, int64_t h2d_bytes) {

@@ -142,6 +142,13 @@ hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_
                               int N, int epi, hipStream_t st, const float* cross_w = nullptr,
                               const float* cross_c = nullptr, int cross_n = 0);
 
+// The same op, one wave per SIMD (gather_gemm.hip): Wp = W in MFMA fragment
+// order (ops.pack_bfrag), N % 512 == 0, Mp % 128 == 0; no cross network.
+bool gemm_gather1w_ok(int64_t Mp, int N, int F, bool cross);
+hipError_t launch_gemm_gather1w(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
+                                int F, const void* Wp, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
+                                int N, int epi, hipStream_t st);
+
 // K3b/K4: C = epi(A[M,K] . W[N,K]^T); epi: 0 none, 1 relu, 2 sigmoid, 3 cross.
 hipError_t launch_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, const float* sa,
                        const float* sw, void* C, int64_t ldc, bool out_f32, const void* X0, const void* XL,

@@ -188,10 +188,13 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   // shares a hardware queue (GPU_MAX_HW_QUEUES = 4) and serialises the step
   // (329 vs 187 us per step measured)
   h2d(slot, s.h2d_dst, s.h2d_src, s.h2d_bytes, ingress_, false);
-  if (s.ingress_seq) s.ingress_seq->launch(ingress_);
+  if (s.ingress_seq) s.ingress_seq->launch(ingress_, nullptr, false, s.skip_varint);
   else if (s.ingress) ck(hipGraphLaunch(s.ingress, ingress_), "hipGraphLaunch(ingress)");
   if (s.mode == 0) s.cin->alltoall(s.send, s.recv, s.in_bytes, ingress_);
   else s.cin->scatter(s.send, s.recv, s.in_bytes, 0, ingress_);
+  // the forward's resolve pass on this lane: step k+1's runs beside step k's forward
+  if (s.resolve_seq) s.resolve_seq->launch(ingress_);
+  else if (s.resolve) ck(hipGraphLaunch(s.resolve, ingress_), "hipGraphLaunch(resolve)");
   ck(hipEventRecord(in_done_[slot], ingress_), "hipEventRecord(in)");
   // compute: the forward graph
   ck(hipStreamWaitEvent(compute_, in_done_[slot], 0), "hipStreamWaitEvent(compute)");

@@ -53,6 +53,14 @@ struct FanoutStep {
   // optional: replay these instead of launching the graphs (same kernels)
   const KernelSequence* ingress_seq = nullptr;
   const KernelSequence* forward_seq = nullptr;
+  // optional: the forward's front half (the gather-GEMM's resolve pass) on the
+  // ingress lane right after the row exchange, so step k+1's resolve runs
+  // beside step k's forward (the local two-lane program's split, fan-out form)
+  hipGraphExec_t resolve = nullptr;
+  const KernelSequence* resolve_seq = nullptr;
+  // no request of the step carries packed varint ids: the ingress sequence
+  // leaves out the arena varint-decode kernel
+  bool skip_varint = false;
 };
 
 // A step as a short program over two device lanes - the compute stream and

@@ -175,7 +175,8 @@ class WideDeep(CTRModel):
     def _gg_front(self, ids, wts, resolved=None):
         first = self.mlp.layers[0]
         h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
-                                 first.bias, first.act, fm2=False, resolved=resolved)
+                                 first.bias, first.act, fm2=False, resolved=resolved,
+                                 packed_w=first.packed)
         return h, wide, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):
@@ -217,7 +218,8 @@ class DeepFM(CTRModel):
         # K1 + K2 inside the first layer's GEMM: x never reaches HBM
         first = self.mlp.layers[0]
         h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
-                               first.bias, first.act, fm2=True, resolved=resolved)
+                               first.bias, first.act, fm2=True, resolved=resolved,
+                               packed_w=first.packed)
         return h, fm, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):

@@ -440,7 +440,7 @@ def embed_gemm_resolve(table: torch.Tensor, ids, wts: Optional[torch.Tensor], li
 
 def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
                bias: float, W: torch.Tensor, b: torch.Tensor, act: str = "relu",
-               fm2: bool = True, cross=None, resolved=None) -> Tuple[torch.Tensor, torch.Tensor]:
+               fm2: bool = True, cross=None, resolved=None, packed_w=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """K1 fused into the first MLP layer (K4): returns
       h     = act(x W^T + b) bf16 [B, N], x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)),
       parts = fp32 [1 + fm2, >= B]: row 0 = bias + sum_f lin[row] w, row 1 the
@@ -449,6 +449,10 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
     network's logit x_L . head_w instead (the GPU takes the folded weights,
     ``cross_consts = cross_v1_consts(w, b, head_w)``, as ``cross[3]`` when given).
     ``resolved``: the front half from :func:`embed_gemm_resolve` (GPU only).
+    ``packed_w``: a callable returning W in MFMA fragment order
+    (:func:`pack_bfrag`, e.g. ``Dense.packed``); with it (and GG1W, N % 512 ==
+    0, no cross network) the GPU runs the one-wave-per-SIMD form
+    (csrc/kernels/gather_gemm.hip: B straight into registers).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
     table rows straight into the GEMM's LDS tiles); on the CPU the unfused math."""
     m = int(modulo) if modulo > 0 else table.shape[0]
@@ -459,11 +463,13 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
         if cross is not None:
             xw, xc = cross[3] if len(cross) > 3 and cross[3] is not None else cross_v1_consts(*cross[:3])
         r = list(resolved) if resolved is not None else None
+        wp = packed_w() if packed_w is not None and GG1W and cross is None and W.shape[0] % 512 == 0 else None
         if isinstance(ids, ArenaRows):
             return tuple(hip().embed_gemm(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias),
-                                          W, b, a, fm2, xw, xc, r))
+                                          W, b, a, fm2, xw, xc, r, wp))
         return tuple(hip().embed_gemm(table, lin, None, _rows(ids), None if wts is None else _rows(wts),
-                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2, xw, xc, r))
+                                      int(ids.shape[0]), int(ids.shape[1]), m, float(bias), W, b, a, fm2, xw, xc, r,
+                                      wp))
     if cross is not None:
         x, logit = embed_cross(table, ids, wts, m, cross[0], cross[1], cross[2])
         first = torch.full((1, x.shape[0]), float(bias), dtype=torch.float32)
@@ -702,6 +708,9 @@ def pack_bfrag(W: torch.Tensor) -> torch.Tensor:
 # not an environment knob: microbenchmarks and tests flip it in-process.
 MLP_TAIL = True
 MLP_TAIL_MIN_ROWS = 8192
+# embed_gemm's one-wave-per-SIMD gather-GEMM (gather_gemm.hip) when the
+# caller hands it packed weights; False = the 8-phase kernel (gemm.hip).
+GG1W = True
 
 
 def mlp_tail_ok(x: torch.Tensor, l2, l3) -> bool:

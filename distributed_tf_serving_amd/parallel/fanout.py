@@ -165,6 +165,7 @@ class FanoutEngine:
         self.program_active = False
         self._program_buckets: set = set()  # buckets whose step is a two-lane program
         self._ingress_graph: Dict[Tuple[int, int], object] = {}
+        self._split: Dict[Tuple[int, int], object] = {}  # two-lane fan-out forward (_capture_split)
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
         self._native_disabled = False
@@ -286,6 +287,7 @@ class FanoutEngine:
                 self.ex.prepare(B, s)
             if native:
                 self._capture_ingress(B, s)
+                self._capture_split(B, s)
         # a failed self-check disables the native path for good (every rank agreed)
         self.native_fanout_active = native and not self._native_disabled
 
@@ -400,10 +402,53 @@ class FanoutEngine:
         g.instantiate()
         self._ingress_graph[key] = g
 
+    def _capture_split(self, B: int, slot: int):
+        """The fan-out step's two-lane forward: (resolve graph, rest-of-forward
+        graph, scores) when the model's first layer is the gather-GEMM on these
+        rows, else None. The StepRunner launches the resolve pass on the
+        ingress lane right after the row exchange, so step k+1's resolve runs
+        beside step k's gather-GEMM / tail on the compute lane - the local
+        two-lane program's split (CTRModel.build_program) in fan-out form."""
+        key = (B, slot)
+        if key in self._split:
+            return self._split[key]
+        m = self.ex.model
+        buf = self.ex.input_buffer(B, slot)
+        ids, wts = self.layout.ids(buf), self.layout.wts(buf)
+        res = None
+        if (self.cuda and self.ex.use_graphs and os.environ.get("DTFS_RESOLVE_LANE", "1") == "1"
+                and getattr(m, "resolve_lane", False) and m._resolve_applies(ids, wts)):
+            st: dict = {}
+            side = torch.cuda.Stream(self.dev)
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):  # warm-up (packs weights, allocates outside the capture)
+                m._forward(ids, wts, resolved=m._resolve(ids, wts))
+            side.synchronize()
+            pool = torch.cuda.graph_pool_handle()
+            g_res = torch.cuda.CUDAGraph(keep_graph=True)
+            with torch.cuda.graph(g_res, pool=pool, stream=side):
+                st["resolved"] = m._resolve(ids, wts)
+            g_res.instantiate()
+            g_fwd = torch.cuda.CUDAGraph(keep_graph=True)
+            with torch.cuda.graph(g_fwd, pool=pool, stream=side):
+                st["scores"] = m._forward(ids, wts, resolved=st["resolved"])
+            g_fwd.instantiate()
+            res = (g_res, g_fwd, st["scores"], st)
+        self._split[key] = res
+        return res
+
+    def _forward_parts(self, B: int, slot: int):
+        """(resolve graph or None, forward graph, device scores) of a fan-out step."""
+        sp = self._capture_split(B, slot)
+        if sp is not None:
+            return sp[0], sp[1], sp[2]
+        self.ex.prepare(B, slot)
+        return None, self.ex._graphs[(B, slot)], self.ex._out[(B, slot)]
+
     def _launch_native_fanout(self, B: int, slot: int, h_in, h_out, rows: int, t0: float,
                               nbytes: Optional[int]) -> StepHandle:
         key = (B, slot)
-        self.ex.prepare(B, slot)
+        g_res, g_fwd, scores = self._forward_parts(B, slot)
         self._capture_ingress(B, slot)
         self.runner()
         send, back = self._send_buf(B, slot), self._back_buf(B, slot)
@@ -417,7 +462,8 @@ class FanoutEngine:
         self._runner.launch_fanout(
             slot, dst, h_in, h2d, ing.raw_cuda_graph_exec() if ing is not None else 0,
             self._cin, 0 if self.mode == "alltoall" else 1, send, self.ex.input_buffer(B, slot),
-            self.ex._graphs[key].raw_cuda_graph_exec(), self._cout, self.ex._out[key], back, h_out, rows * 4)
+            g_fwd.raw_cuda_graph_exec(), self._cout, scores, back, h_out, rows * 4,
+            g_res.raw_cuda_graph_exec() if g_res is not None else 0)
         return StepHandle(B=B, slot=slot, host_out=h_out[:rows], event=_RunnerEvent(self._runner, slot,
                                                                                    (self._cin, self._cout)),
                           t_submit=t0, timeout_s=self.step_timeout_s)
@@ -531,17 +577,17 @@ class FanoutEngine:
                                 h_out=h_out))
             elif self.native_fanout_active:
                 key = (B, s)
-                self.ex.prepare(B, s)
+                g_res, fwd, scores = self._forward_parts(B, s)
                 self._capture_ingress(B, s)
                 ing = self._ingress_graph.get(key)
-                fwd = self.ex._graphs[key]
                 out.append(dict(
                     fanout=True, h2d_dst=self.dev_arena(s),
                     ingress_exec=ing.raw_cuda_graph_exec() if ing is not None else 0, ingress_seq=seq(ing),
                     cin=self._cin, cout=self._cout, mode=0 if self.mode == "alltoall" else 1,
                     send=self._send_buf(B, s), recv=self.ex.input_buffer(B, s),
-                    forward_exec=fwd.raw_cuda_graph_exec(), forward_seq=seq(fwd), scores=self.ex._out[key],
-                    back=self._back_buf(B, s), h_out=h_out, d2h_bytes=rows * 4))
+                    forward_exec=fwd.raw_cuda_graph_exec(), forward_seq=seq(fwd), scores=scores,
+                    resolve_exec=g_res.raw_cuda_graph_exec() if g_res is not None else None,
+                    resolve_seq=seq(g_res), back=self._back_buf(B, s), h_out=h_out, d2h_bytes=rows * 4))
             else:
                 raise RuntimeError("no native step path for this engine (graphs disabled or fan-out fell back)")
         return out

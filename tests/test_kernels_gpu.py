@@ -837,6 +837,27 @@ def test_embed_gemm_matches_fp32_reference(cuda, B, ids32, fm2):
     _close(parts[:, :B].sum(0), fmg, 1e-5, 1e-5, "FM partials vs the gather kernel's FM")
 
 
+@pytest.mark.parametrize("B,F,N,fm2", [(1, 43, 1024, True), (300, 1, 512, False), (4099, 3, 1024, True),
+                                       (16384, 43, 1024, True), (16384, 43, 1024, False), (2048, 26, 2048, True),
+                                       (1000, 7, 1536, False)])
+def test_gather_gemm_one_wave_form(cuda, B, F, N, fm2):
+    """The one-wave-per-SIMD gather-GEMM (gather_gemm.hip: packed W straight
+    into registers, 6-slot A ring, scale pass one tile ahead) vs the fp32
+    reference and vs the 8-phase kernel, over field counts below / above its
+    prefetch depths and 1-4 column tiles (FM rows owned by tiles 0-1)."""
+    V, bias = 30_000, -0.5
+    table, lin, W, b, ids, wts = _gather_gemm_case(B, F=F, V=V, N=N, seed=B + F)
+    d = [t.to(cuda) for t in (table, lin, W, b, ids, wts)]
+    Wp = ops.pack_bfrag(d[2])
+    h, parts = ops.embed_gemm(d[0], d[4], d[5], d[1], V, bias, d[2], d[3], "relu", fm2=fm2, packed_w=lambda: Wp)
+    h_ref, fm_ref = _gather_gemm_ref(table, lin, W, b, ids, wts, V, bias, fm2)
+    _close(h, h_ref, 2e-2, 2e-3, "one-wave gather-GEMM h vs fp32")
+    _close(parts[:, :B].sum(0), fm_ref, 1e-4, 1e-4, "one-wave FM partials vs fp32")
+    h8, p8 = ops.embed_gemm(d[0], d[4], d[5], d[1], V, bias, d[2], d[3], "relu", fm2=fm2)
+    _close(h, h8, 1e-2, 1e-4, "one-wave vs 8-phase gather-GEMM")
+    _close(parts[:, :B].sum(0), p8[:, :B].sum(0), 1e-5, 1e-5, "one-wave vs 8-phase FM partials")
+
+
 def test_embed_gemm_narrow_exchange_rows(cuda):
     """The candidate fan-out hands the forward its exchanged rows as strided
     views of [int32 row x F | fp32 weight x F] (serving/packing.py narrow

@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--gemm-variants", action="store_true")
     ap.add_argument("--embed-study", action="store_true")
     ap.add_argument("--gather-gemm", action="store_true", help="K1 fused into K4 vs gather + GEMM")
+    ap.add_argument("--gg-id-space", type=int, default=1 << 40, help="--gather-gemm: ids drawn (zipf) from [0, this)")
+    ap.add_argument("--gg-rows", default="2048,4096,8192,16384", help="--gather-gemm: row counts")
     ap.add_argument("--gather-locality", action="store_true",
                     help="gather-GEMM time by where the table rows come from (L2 / MALL / HBM)")
     ap.add_argument("--variants", default="", help="M,N,K:v1,v2,... interleaved A/B of GEMM variants")
@@ -160,7 +162,7 @@ def main():
         for r in gather_locality_study():
             print(json.dumps(r), flush=True)
     if a.gather_gemm:
-        for r in gather_gemm_study():
+        for r in gather_gemm_study(rows=tuple(int(x) for x in a.gg_rows.split(",")), id_space=a.gg_id_space):
             print(json.dumps(r), flush=True)
         return
     if a.embed_study:
@@ -228,7 +230,7 @@ def tail_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
     return out
 
 
-def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024, dev="cuda"):
+def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024, dev="cuda", id_space=1 << 40):
     """K1 fused into K4 vs the separate gather + GEMM at the DeepFM serving
     shape (Zipf ids, 1M x 64 table): resolve + gather-GEMM vs embed(x, FM) +
     8-phase GEMM, interleaved rounds; also each half alone."""
@@ -240,7 +242,7 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
     b = torch.randn(N, device=dev) * 0.01
     out = []
     for B in rows:
-        ids_np, wts_np = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
+        ids_np, wts_np = SyntheticRequests(fields=F, id_space=id_space, dist="zipf", seed=B).arrays(B)
         ids, wts = torch.from_numpy(ids_np).to(dev), torch.from_numpy(wts_np).to(dev)
 
         def unfused():
@@ -253,19 +255,33 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
         def fused_nofm():
             return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=False)
 
+        Wp = ops.pack_bfrag(W)
+        res = ops.embed_gemm_resolve(table, ids, wts, lin, V, 0.0, True)
+
+        def gg8():  # the GEMM half alone, 8-phase (gemm.hip)
+            return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=True, resolved=res)
+
+        def gg1w():  # the GEMM half alone, one wave per SIMD (gather_gemm.hip)
+            return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=True, resolved=res,
+                                  packed_w=lambda: Wp)
+
+        torch.testing.assert_close(gg1w()[0].float(), gg8()[0].float(), atol=1e-2, rtol=1e-2)
         x, _ = ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True, want_fm=True, fm2=True)
-        t = {k: [] for k in ("unfused", "fused", "embed", "gemm", "fused_nofm")}
+        t = {k: [] for k in ("unfused", "fused", "embed", "gemm", "fused_nofm", "gg8", "gg1w")}
         for _ in range(5):  # interleaved
+            t["gg8"].append(_time(gg8, 20, 1))
+            t["gg1w"].append(_time(gg1w, 20, 1))
             t["unfused"].append(_time(unfused, 20, 1))
             t["fused"].append(_time(fused, 20, 1))
             t["fused_nofm"].append(_time(fused_nofm, 20, 1))
             t["embed"].append(_time(lambda: ops.embed(table, ids, wts, lin=lin, modulo=V, want_x=True,
                                                       want_fm=True, fm2=True), 20, 1))
             t["gemm"].append(_time(lambda: ops.linear(x, W, b, "relu"), 20, 1))
-        r = {"op": "gather_gemm", "B": B, "N": N, "K": F * 64}
+        r = {"op": "gather_gemm", "B": B, "N": N, "K": F * 64, "id_space": id_space}
         for k, v in t.items():
             r[f"{k}_us"] = round(statistics.median(v), 2)
         r["fused_tflops"] = round(2.0 * B * N * F * 64 / r["fused_us"] / 1e6, 1)
+        r["gg1w_tflops"] = round(2.0 * B * N * F * 64 / r["gg1w_us"] / 1e6, 1)
         out.append(r)
     return out
 
