@@ -147,6 +147,17 @@ def build_native(verbose=False, force=False, sanitize=False) -> str:
     return out
 
 
+def _file_flags(src: str):
+    """Per-kernel-file compiler flags: a ``// hipcc-flags: ...`` line in the
+    file's first 60 lines (e.g. gather_gemm.hip turns SLP vectorisation off:
+    packed f32 VALU beside MFMAs costs more issue cycles than scalar)."""
+    with open(src) as f:
+        for _, line in zip(range(60), f):
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def build_hip(verbose=False, force=False) -> str:
     tdir, tinc, tlib, abi = _torch_paths()
     out = os.path.join(PKG_DIR, "_hip" + EXT_SUFFIX)
@@ -164,7 +175,7 @@ def build_hip(verbose=False, force=False) -> str:
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _stale(obj, src, hdr):
-            jobs.append([HIPCC, *dev_flags, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *dev_flags, *_file_flags(src), "-c", src, "-o", obj])
     for s in HIP_HOST_SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(odir, s.replace("/", "_") + ".o")

@@ -176,7 +176,7 @@ class WideDeep(CTRModel):
         first = self.mlp.layers[0]
         h, wide = ops.embed_gemm(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, first.weight,
                                  first.bias, first.act, fm2=False, resolved=resolved,
-                                 packed_w=first.packed)
+                                 packed_w=lambda: first.packed("32"))
         return h, wide, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):
@@ -219,7 +219,7 @@ class DeepFM(CTRModel):
         first = self.mlp.layers[0]
         h, fm = ops.embed_gemm(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, first.weight,
                                first.bias, first.act, fm2=True, resolved=resolved,
-                               packed_w=first.packed)
+                               packed_w=lambda: first.packed("32"))
         return h, fm, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):

@@ -117,15 +117,19 @@ class Dense(nn.Module):
         self.register_buffer("w_scale", sw.contiguous(), persistent=False)
         self.fp8 = True
 
-    def packed(self) -> torch.Tensor:
-        """The weight in MFMA fragment order (ops.pack_bfrag) for the fused MLP
-        tail, re-packed whenever the weight changed (load_state_dict bumps its
-        version). Built by the eager warm-up that precedes every graph capture."""
+    def packed(self, layout: str = "16") -> torch.Tensor:
+        """The weight in MFMA fragment order - "16": ops.pack_bfrag (the fused
+        MLP tail's 16x16x32 B operand), "32": ops.pack_frag32 (the gather-GEMM's
+        32x32x16 A operand) - re-packed whenever the weight changed
+        (load_state_dict bumps its version). Built by the eager warm-up that
+        precedes every graph capture."""
         key = (self.weight.data_ptr(), self.weight._version)
-        cached = getattr(self, "_packed", None)
+        cache = self.__dict__.setdefault("_packed", {})
+        cached = cache.get(layout)
         if cached is None or cached[0] != key:
-            cached = (key, ops.pack_bfrag(self.weight.detach()))
-            self._packed = cached
+            w = self.weight.detach()
+            cached = (key, ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w))
+            cache[layout] = cached
         return cached[1]
 
     def forward(self, x: torch.Tensor, xq=None) -> torch.Tensor:

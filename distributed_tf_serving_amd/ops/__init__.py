@@ -449,8 +449,8 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
     network's logit x_L . head_w instead (the GPU takes the folded weights,
     ``cross_consts = cross_v1_consts(w, b, head_w)``, as ``cross[3]`` when given).
     ``resolved``: the front half from :func:`embed_gemm_resolve` (GPU only).
-    ``packed_w``: a callable returning W in MFMA fragment order
-    (:func:`pack_bfrag`, e.g. ``Dense.packed``); with it (and GG1W, N % 512 ==
+    ``packed_w``: a callable returning W in 32x32x16 MFMA fragment order
+    (:func:`pack_frag32`, e.g. ``lambda: dense.packed("32")``); with it (and GG1W, N % 512 ==
     0, no cross network) the GPU runs the one-wave-per-SIMD form
     (csrc/kernels/gather_gemm.hip: B straight into registers).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
@@ -701,6 +701,17 @@ def pack_bfrag(W: torch.Tensor) -> torch.Tensor:
     if N % 16 or K % 64:
         raise ValueError(f"pack_bfrag needs N % 16 == 0 and K % 64 == 0, got {tuple(W.shape)}")
     return W.reshape(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous()
+
+
+def pack_frag32(W: torch.Tensor) -> torch.Tensor:
+    """bf16 weights [N, K] -> the A-operand fragment order of
+    v_mfma_f32_32x32x16_bf16 (csrc/kernels/gather_gemm.hip): block (n32, k64,
+    s) is 64 lanes x 8 values, lane (r, h) = (l & 31, l >> 5) holding
+    W[32 n32 + r, 64 k64 + 16 s + 8 h + e] - 1 KiB contiguous per fragment."""
+    N, K = W.shape
+    if N % 32 or K % 64:
+        raise ValueError(f"pack_frag32 needs N % 32 == 0 and K % 64 == 0, got {tuple(W.shape)}")
+    return W.reshape(N // 32, 32, K // 64, 4, 2, 8).permute(0, 2, 3, 4, 1, 5).contiguous()
 
 
 # The fused MLP tail replaces GEMM2 + the fused last-layer/head kernel at or

@@ -10,6 +10,7 @@ weights, and checks that an idle cluster launches no steps. Each rank writes
 """
 import argparse
 import concurrent.futures as cf
+import faulthandler
 import json
 import os
 import sys
@@ -196,6 +197,7 @@ def main():
 
 
 if __name__ == "__main__":
+    faulthandler.enable()  # a native abort (SIGABRT / SIGSEGV) still names the Python frame it hit
     try:
         main()
     except BaseException:

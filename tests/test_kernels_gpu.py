@@ -848,7 +848,7 @@ def test_gather_gemm_one_wave_form(cuda, B, F, N, fm2):
     V, bias = 30_000, -0.5
     table, lin, W, b, ids, wts = _gather_gemm_case(B, F=F, V=V, N=N, seed=B + F)
     d = [t.to(cuda) for t in (table, lin, W, b, ids, wts)]
-    Wp = ops.pack_bfrag(d[2])
+    Wp = ops.pack_frag32(d[2])
     h, parts = ops.embed_gemm(d[0], d[4], d[5], d[1], V, bias, d[2], d[3], "relu", fm2=fm2, packed_w=lambda: Wp)
     h_ref, fm_ref = _gather_gemm_ref(table, lin, W, b, ids, wts, V, bias, fm2)
     _close(h, h_ref, 2e-2, 2e-3, "one-wave gather-GEMM h vs fp32")

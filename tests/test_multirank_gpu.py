@@ -195,7 +195,8 @@ def test_local_cluster_sharded_dlrm_ranks_sharing_one_gpu(tmp_path, n):
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     errs = {f.name: f.read_text()[-3000:] for f in sorted(tmp_path.glob("rank*.err"))}
-    assert p.returncode == 0, (errs, p.stdout[-2000:], p.stderr[-2000:])
+    written = sorted(f.name for f in tmp_path.glob("rank*.json"))  # how far the ranks got
+    assert p.returncode == 0, (errs, written, p.stdout[-2000:], p.stderr[-4000:])
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
     for r in res:
         assert r["serves"] and r["max_diff"] < 1e-3 and r["grpc_max_diff"] < 1e-3, r

@@ -51,6 +51,31 @@ def test_pack_bfrag_layout_and_round_trip():
         ops.pack_bfrag(W[:, :100])
 
 
+def test_pack_frag32_layout():
+    # fragment (n32, k64, s), lane (r, h), value e = W[32 n32 + r, 64 k64 + 16 s + 8 h + e]
+    N, K = 96, 192
+    W = torch.arange(N * K, dtype=torch.float32).view(N, K).to(torch.bfloat16)
+    P = ops.pack_frag32(W).view(N // 32, K // 64, 4, 64, 8)
+    for n32, k64, s, lane in ((0, 0, 0, 0), (2, 1, 3, 37), (1, 2, 1, 63), (2, 2, 2, 31), (0, 1, 0, 32)):
+        r, h = lane & 31, lane >> 5
+        want = W[32 * n32 + r, 64 * k64 + 16 * s + 8 * h: 64 * k64 + 16 * s + 8 * h + 8]
+        assert torch.equal(P[n32, k64, s, lane], want)
+    with pytest.raises(ValueError):
+        ops.pack_frag32(W[:80])
+
+
+def test_dense_packed_layouts_are_cached_per_layout():
+    from distributed_tf_serving_amd.models.layers import Dense
+
+    d = Dense(128, 64, "relu", torch.bfloat16, "cpu", torch.Generator().manual_seed(0))
+    p16, p32 = d.packed("16"), d.packed("32")
+    assert torch.equal(p16, ops.pack_bfrag(d.weight)) and torch.equal(p32, ops.pack_frag32(d.weight))
+    assert d.packed("32") is p32
+    with torch.no_grad():
+        d.weight.add_(1.0)  # bumps the version: both layouts are re-packed
+    assert torch.equal(d.packed("32"), ops.pack_frag32(d.weight)) and d.packed("16") is not p16
+
+
 def test_mlp_tail_only_on_gpu_shapes():
     from distributed_tf_serving_amd.config import ModelConfig
     from distributed_tf_serving_amd.models import build_model

@@ -1,8 +1,9 @@
 // Diagnostic build of the one-wave-per-SIMD gather-GEMM (gemm_gather1w_kernel,
 // csrc/kernels/gather_gemm.hip) with s_memtime stamps (DTFS_GG1W_STAMPS): where
-// does one K tile spend its cycles - step 0 (A fragments streaming in), steps
-// 1-3 (B waits + A DMAs), step 4 (scale reads + ring DMA), steps 5-6 (scale
-// pass writes), step 7 - against the 128 x 16 = 2048 MFMA cycles it carries?
+// does one K tile spend its cycles - step 0 (fragment waits, scale reads, A
+// DMAs), step 1 (scale writes, A DMAs), step 2 (scale writes, rows), the
+// barrier, step 3 (MFMAs + next tile's fragment reads, then W loads + ring DMA)
+// - against the 64 x 32 = 2048 MFMA cycles it carries?
 // DeepFM's first layer: F = 43 fields x 64 dims -> 1024, FM on.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o gg1w_stamps gg1w_stamps.hip
 // Arguments: "hot" draws every row from the first 256 table rows (L2-resident)
@@ -94,8 +95,8 @@ int main(int argc, char** argv) {
       }
     printf("{\"kernel\": \"gemm_gather1w (FM%s)\", \"M\": %d, \"N\": %d, \"F\": %d, \"blocks\": %d, \"event_us\": %.2f, "
            "\"median_cycles\": {\"prologue\": %.0f, \"loop\": %.0f, \"loop_per_k_tile\": %.0f, \"epilogue\": %.0f, "
-           "\"sampled_tile\": %.0f, \"step0\": %.0f, \"steps1_3\": %.0f, \"step4\": %.0f, \"step5\": %.0f, "
-           "\"step6\": %.0f, \"step7\": %.0f}}\n",
+           "\"sampled_tile\": %.0f, \"step0\": %.0f, \"step1\": %.0f, \"step2\": %.0f, \"barrier\": %.0f, "
+           "\"step3\": %.0f, \"unused\": %.0f}}\n",
            hot ? ", L2-hot rows" : "", M, N, F, nb, ms * 1e3 / 20, med(pro), med(loop), med(loop) / F, med(epi),
            med(tile), med(seg[0]), med(seg[1]), med(seg[2]), med(seg[3]), med(seg[4]), med(seg[5]));
   }

@@ -255,7 +255,7 @@ def gather_gemm_study(rows=(2048, 4096, 8192, 16384), F=43, V=1_000_000, N=1024,
         def fused_nofm():
             return ops.embed_gemm(table, ids, wts, lin, V, 0.0, W, b, "relu", fm2=False)
 
-        Wp = ops.pack_bfrag(W)
+        Wp = ops.pack_frag32(W)
         res = ops.embed_gemm_resolve(table, ids, wts, lin, V, 0.0, True)
 
         def gg8():  # the GEMM half alone, 8-phase (gemm.hip)
