@@ -384,7 +384,7 @@ std::vector<torch::Tensor> embed_gemm(torch::Tensor table, c10::optional<torch::
   const torch::Tensor &rows_t = r[0], &wts_t = r[1], &parts = r[2];
   if (B == 0) return {h, parts};
   auto st = cur_stream(table);
-  if (Wp && dtfs::gemm_gather1w_ok(Mp, int(N), int(F), cross)) {
+  if (Wp && dtfs::gemm_gather1w_ok(Mp, int(N), int(F), cross, V)) {
     // one wave per SIMD, B from registers (csrc/kernels/gather_gemm.hip)
     check_dev(*Wp, "Wp");
     check_same_dev(table, *Wp, "Wp");

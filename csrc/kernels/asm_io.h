@@ -52,6 +52,19 @@ __device__ __forceinline__ void lds_write16(uint8_t* p, const i32x4& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
 
+// SGPR base + 32-bit per-lane byte offset: the uniform part of an address
+// stays in scalar registers (no 64-bit VALU adds, one VGPR per address)
+__device__ __forceinline__ void lds_dma16_s(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ bf16x8 gload16_s(const void* sbase, uint32_t voff) {
+  bf16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase));
+  return v;
+}
+
 // 16 bytes per lane global -> registers
 __device__ __forceinline__ bf16x8 gload16(const void* g) {
   bf16x8 v;

@@ -180,26 +180,29 @@ __global__ void __launch_bounds__(256, 1) gemm_gather1w_kernel(const uint8_t* __
     const uint32_t base = rring_lds + (u & (RI - 1)) * RING + idx_off;
     sfor<4>([&](auto k) { aidx[k] = lds_read4_at<32 * k>(base); });
   };
-  auto stage_a = [&](int u, int k) {  // 1 op; aidx of tile u landed
+  auto stage_a = [&](int u, int k) {  // 1 op; aidx of tile u landed (table < 4 GiB: a 32-bit offset)
     const int rr = min(max(aidx[k], 0), Vm1);
-    lds_dma16(table + int64_t(rr) * 128 + a_src, aring_w + (u & (NS - 1)) * SLOT + k * 1024);
+    lds_dma16_s(table, uint32_t(rr) * 128u + a_src, aring_w + (u & (NS - 1)) * SLOT + k * 1024);
   };
   // W fragments of wave w (the MFMA's A operand, 32 columns x 16 K each):
   // packed blocks n0 / 32 + 4 w + jn, layout [N/32][F][4][64][8] (ops.pack_frag32)
-  const bf16x8* wpw = Wp + int64_t(n0 / 32 + 4 * w) * F * 4 * 64 + lane;
+  // (the fragment's address is uniform but for the lane's 16 bytes: SGPR base)
+  const bf16x8* wpw = Wp + int64_t(n0 / 32 + 4 * w) * F * 4 * 64;
+  const uint32_t w_lane = 16 * lane;
   bf16x8 wf[4][4];
   auto load_w1 = [&](int u, int jn, int s) {  // 1 op
-    wf[jn][s] = gload16(wpw + ((int64_t(jn) * F + min(u, F - 1)) * 4 + s) * 64);
+    wf[jn][s] = gload16_s(wpw + ((int64_t(jn) * F + min(u, F - 1)) * 4 + s) * 64, w_lane);
   };
 
   // ---- x fragments (the MFMA's B operand): row 32 im + r32, K 16 s + 8 h ..
   // +7 = logical chunk 2 s + h, physical (2 s + h) ^ (r32 & 7)
   bf16x8 xf[4][4];
-  uint32_t xo[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) xo[s] = r32 * 128 + (((2 * s + h) ^ (r32 & 7)) << 4);
+  // chunk (2 s + h) ^ (r32 & 7) = ((h ^ (r32 & 1)) | 2 (s ^ ((r32 >> 1) & 3))):
+  // bits 5-6 of the byte offset are s ^ ((r32 >> 1) & 3), so one register
+  // holds the s = 0 offset and K step s XORs (s << 5) into it
+  const uint32_t xo0 = r32 * 128 + ((h ^ (r32 & 1)) << 4) + (((r32 >> 1) & 3) << 5);
   auto read_xs = [&](int u, int s) {  // 4 ops: K step s of all 4 row blocks
-    const uint32_t a = aring_lds + (u & (NS - 1)) * SLOT + xo[s];
+    const uint32_t a = aring_lds + (u & (NS - 1)) * SLOT + (xo0 ^ uint32_t(s << 5));
     sfor<4>([&](auto im) { xf[im][s] = lds_read16_at<4096 * im>(a); });
   };
   // ---- scale pass: thread T rescales logical chunk T & 7 of rows (T >> 3) +
@@ -364,6 +367,27 @@ __global__ void __launch_bounds__(256, 1) gemm_gather1w_kernel(const uint8_t* __
       mfma1(jn, (2 * k) & 3, k >> 1);
       mfma1(jn, (2 * k + 1) & 3, k >> 1);
     };
+    if constexpr (FM) {
+      // the FM sums are complete once tile F-1 is scaled (during tile F-2):
+      // the last tile stores the partials, so none of their registers live
+      // past the loop (there the allocator spilled accumulators to scratch)
+      if (t == F - 1) {
+        const int sc_ce = T & 7, sc_r0e = T >> 3;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          float part = -fsq[a];
+#pragma unroll
+          for (int d = 0; d < 8; ++d) part += fs[a][d] * fs[a][d];
+          part += __shfl_xor(part, 1, 64);
+          part += __shfl_xor(part, 2, 64);
+          part += __shfl_xor(part, 4, 64);
+          if (tn < 2 && sc_ce == 0) fm_part[Mp + m0 + sc_r0e + 32 * (2 * tn + a)] = 0.5f * part;
+        }
+        // the shuffles are LDS ops the compiler tracks: retire them here, or
+        // it drains lgkmcnt in the middle of step 0 on every tile
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      }
+    }
     // step 0: A(t)'s fragments land K step by K step; G3(t-1)
     wait_vm4<12>(wf[0]);
     G1_T(2);
@@ -439,67 +463,73 @@ __global__ void __launch_bounds__(256, 1) gemm_gather1w_kernel(const uint8_t* __
 #undef WAIT_XS
   // the trailing (re-staged, unread) loads land before the LDS is reused / the waves exit
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // Lane-derived indices of the tail are recomputed here from a volatile read
+  // of the lane id (not CSE'd with the prologue's): kept live across the loop,
+  // the register allocator spilled them to scratch - and a scratch-using
+  // kernel faulted (memory aperture violation) once captured into the served
+  // step's HIP graph. Scratch-free is checked by test_kernels_gpu.
+  int lane_e;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+  int tid_e;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_e) : "v"(lane_e));
+  tid_e += 64 * w;
+  const int r32e = lane_e & 31, he = lane_e >> 5, sc_ce = tid_e & 7, sc_r0e = tid_e >> 3;
   __syncthreads();
 
   // ---- epilogue: bias + act -> bf16, staged through LDS, written as whole 1 KiB rows
   {
     const float lo = relu ? 0.f : -__builtin_huge_valf();
 #pragma unroll
-    for (int jn = 0; jn < 4; ++jn)
+    for (int jn = 0; jn < 4; ++jn) {
+      f32x4 b4[4];
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int n = 128 * w + 32 * jn + 8 * g4 + 4 * h;
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + n0 + n);
+      for (int g4 = 0; g4 < 4; ++g4)
+        b4[g4] = *reinterpret_cast<const f32x4*>(bias + n0 + 128 * w + 32 * jn + 8 * g4 + 4 * he);
 #pragma unroll
-        for (int im = 0; im < 4; ++im) {
-          const int m = 32 * im + r32;
+      for (int im = 0; im < 4; ++im) {
+        // a whole 16-register accumulator at a time (sub-register pieces made
+        // the allocator shuffle AGPRs at the loop exit, through scratch)
+        const f32x16 av = acc[jn][im];
+        const int m = 32 * im + r32e;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int n = 128 * w + 32 * jn + 8 * g4 + 4 * he;
           bf16x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[jn][im][4 * g4 + e] + b4[e], lo));
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(av[4 * g4 + e] + b4[g4][e], lo));
           *reinterpret_cast<bf16x4*>(smem + m * SP + n * 2) = o;
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
+    }
   }
   __syncthreads();
 #pragma unroll 4
   for (int r = w; r < BM; r += 4) {
     const int m = m0 + r;
     if (m < M)
-      *reinterpret_cast<bf16x8*>(C + int64_t(m) * ldc + n0 + 8 * lane) =
-          *reinterpret_cast<const bf16x8*>(smem + r * SP + 16 * lane);
+      *reinterpret_cast<bf16x8*>(C + int64_t(m) * ldc + n0 + 8 * lane_e) =
+          *reinterpret_cast<const bf16x8*>(smem + r * SP + 16 * lane_e);
   }
 #ifdef DTFS_GG1W_STAMPS
   G1_AT(10);
-  if (lane == 0 && blockIdx.x < 4096)
+  if (lane_e == 0 && blockIdx.x < 4096)
     for (int k = 0; k < 12; ++k) g_gg1w_stamps[blockIdx.x][w][k] = g1_s[k];
 #endif
-  if constexpr (FM) {
-    if (tn < 2) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        float part = -fsq[a];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) part += fs[a][d] * fs[a][d];
-        part += __shfl_xor(part, 1, 64);
-        part += __shfl_xor(part, 2, 64);
-        part += __shfl_xor(part, 4, 64);
-        if (sc_c == 0) fm_part[Mp + m0 + sc_r0 + 32 * (2 * tn + a)] = 0.5f * part;
-      }
-    }
-  }
 }
 
 }  // namespace kern
 
-bool gemm_gather1w_ok(int64_t Mp, int N, int F, bool cross) {
-  return !cross && N % 512 == 0 && Mp % 128 == 0 && F >= 1 && F <= 4096;
+bool gemm_gather1w_ok(int64_t Mp, int N, int F, bool cross, int64_t V) {
+  // V <= 2^25: table row offsets (128 B rows) fit the 32-bit DMA offset
+  return !cross && N % 512 == 0 && Mp % 128 == 0 && F >= 1 && F <= 4096 && V >= 1 && V <= (int64_t(1) << 25);
 }
 
 hipError_t launch_gemm_gather1w(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                                 int F, const void* Wp, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                                 int N, int epi, hipStream_t st) {
   if (M == 0) return hipSuccess;
-  if (!gemm_gather1w_ok(Mp, N, F, false) || Mp < M || V < 1 || V > (int64_t(1) << 31) || ldc < N || ldc % 8 != 0 ||
+  if (!gemm_gather1w_ok(Mp, N, F, false, V) || Mp < M || ldc < N || ldc % 8 != 0 ||
       (fm_part && N < 1024) || !table || !rows_t || !wts_t || !Wp || !C || !bias)
     return hipErrorInvalidValue;
   const int grid = int(Mp / 128) * (N / 512);

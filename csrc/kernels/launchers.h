@@ -143,8 +143,9 @@ hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_
                               const float* cross_c = nullptr, int cross_n = 0);
 
 // The same op, one wave per SIMD (gather_gemm.hip): Wp = W in MFMA fragment
-// order (ops.pack_bfrag), N % 512 == 0, Mp % 128 == 0; no cross network.
-bool gemm_gather1w_ok(int64_t Mp, int N, int F, bool cross);
+// order (ops.pack_frag32), N % 512 == 0, Mp % 128 == 0, V <= 2^25 table rows;
+// no cross network.
+bool gemm_gather1w_ok(int64_t Mp, int N, int F, bool cross, int64_t V);
 hipError_t launch_gemm_gather1w(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp,
                                 int F, const void* Wp, const float* bias, void* C, int64_t ldc, float* fm_part, int M,
                                 int N, int epi, hipStream_t st);

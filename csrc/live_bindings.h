@@ -18,6 +18,7 @@
 
 #include "net/h2_server.h"
 #include "runtime/batcher.h"
+#include "runtime/numa.h"
 #include "runtime/live_server.h"
 #include "runtime/loadgen.h"
 #include "runtime/shared_scatter.h"
@@ -102,9 +103,27 @@ using ScatterClass = py::class_<SharedScatter, std::shared_ptr<SharedScatter>>;
 inline ScatterClass def_shared_scatter(py::module& m) {
   ScatterClass c(m, "SharedScatter", py::module_local(),
                  "Scatter fan-out through rank 0's shared request arenas (one node; runtime/shared_scatter.h)");
-  c.def(py::init<std::string, int, int, bool, int64_t, int, int64_t, int, int64_t, int>(), py::arg("name"),
-        py::arg("world"), py::arg("rank"), py::arg("create"), py::arg("fields") = 0, py::arg("n_arenas") = 0,
-        py::arg("arena_cap") = 0, py::arg("slots") = 0, py::arg("out_floats") = 0, py::arg("node") = -1)
+  c.def(py::init<std::string, int, int, bool, int64_t, int, int64_t, int, int64_t, int, std::vector<int>, int64_t>(),
+        py::arg("name"), py::arg("world"), py::arg("rank"), py::arg("create"), py::arg("fields") = 0,
+        py::arg("n_arenas") = 0, py::arg("arena_cap") = 0, py::arg("slots") = 0, py::arg("out_floats") = 0,
+        py::arg("node") = -1, py::arg("rank_nodes") = std::vector<int>(), py::arg("expected_payload") = 0)
+      .def(
+          "placement",
+          [](const SharedScatter& s) {
+            py::list l;
+            for (const auto& sl : s.placement())
+              l.append(py::dict(py::arg("lo") = sl.lo, py::arg("hi") = sl.hi, py::arg("node") = sl.node,
+                                py::arg("rank") = sl.rank, py::arg("bound") = sl.bound));
+            return l;
+          },
+          "per-rank NUMA slices of the arenas placed at creation: [{lo, hi, node, rank, bound}] (segment offsets)")
+      .def(
+          "page_node",
+          [](const SharedScatter& s, int64_t off) {
+            TORCH_CHECK(off >= 0 && size_t(off) < s.bytes(), "offset outside the segment");
+            return dtfs::runtime::page_numa_node(static_cast<const uint8_t*>(s.base()) + off);
+          },
+          py::arg("offset"), "NUMA node of the page at a segment offset (-1 untouched / unknown)")
       .def_property_readonly("world", &SharedScatter::world)
       .def_property_readonly("rank", &SharedScatter::rank)
       .def_property_readonly("n_arenas", &SharedScatter::n_arenas)

@@ -128,8 +128,33 @@ std::vector<ShareCopy> share_copies(const uint8_t* arena, const RankShare& s, ui
   return c;
 }
 
+std::vector<NodeSlice> scatter_placement(int64_t arenas_off, int n_arenas, int64_t arena_stride, int64_t payload_off,
+                                         int64_t expected_payload, const std::vector<int>& rank_nodes) {
+  std::vector<NodeSlice> out;
+  const int world = int(rank_nodes.size());
+  if (world < 2 || expected_payload <= 0 || n_arenas < 1) return out;
+  const int64_t cap = arena_stride - payload_off;  // payload bytes an arena can hold
+  const int64_t used = std::min(expected_payload, cap);
+  for (int i = 0; i < n_arenas; ++i) {
+    const int64_t p0 = arenas_off + int64_t(i) * arena_stride + payload_off;
+    for (int r = 1; r < world; ++r) {
+      const int nd = rank_nodes[size_t(r)];
+      if (nd < 0 || nd == rank_nodes[0]) continue;  // rank 0's node already holds the segment
+      // whole pages only: the boundary page stays with the lower share
+      int64_t lo = page_up(p0 + used * r / world);
+      int64_t hi = r == world - 1 ? arenas_off + int64_t(i + 1) * arena_stride : page_up(p0 + used * (r + 1) / world);
+      hi = std::min(hi, arenas_off + int64_t(i + 1) * arena_stride);
+      if (hi <= lo) continue;
+      if (!out.empty() && out.back().node == nd && out.back().hi == lo) out.back().hi = hi;  // neighbours on one node
+      else out.push_back(NodeSlice{lo, hi, nd, r, false});
+    }
+  }
+  return out;
+}
+
 SharedScatter::SharedScatter(const std::string& name, int world, int rank, bool create, int64_t fields, int n_arenas,
-                             int64_t arena_cap, int slots, int64_t out_floats, int node)
+                             int64_t arena_cap, int slots, int64_t out_floats, int node,
+                             const std::vector<int>& rank_nodes, int64_t expected_payload)
     : name_(name), rank_(rank) {
   if (world < 1 || world > kScatterMaxRanks) throw std::invalid_argument("shared scatter: world must be in [1, 16]");
   if (rank < 0 || rank >= world) throw std::invalid_argument("shared scatter: bad rank");
@@ -169,6 +194,18 @@ SharedScatter::SharedScatter(const std::string& name, int world, int rank, bool 
     // rank 0 writes every request into these pages: place them on its node
     // before anything touches them (best effort)
     if (node >= 0) bind_range_to_node(p, bytes_, node);
+    if (!rank_nodes.empty()) {
+      if (int(rank_nodes.size()) != world) {
+        munmap(p, bytes_);
+        shm_unlink(name.c_str());
+        throw std::invalid_argument("shared scatter: rank_nodes needs one node per rank");
+      }
+      // then each rank's share of every arena on that rank's node (before
+      // anything touches the pages; best effort like the segment's own)
+      placement_ = scatter_placement(arenas_off, n_arenas, page_up(arena_cap), kArenaPayloadOff, expected_payload,
+                                     rank_nodes);
+      for (auto& sl : placement_) sl.bound = bind_range_to_node(static_cast<uint8_t*>(p) + sl.lo, size_t(sl.hi - sl.lo), sl.node);
+    }
     s_ = new (p) ScatterShared();
     s_->world = world;
     s_->n_arenas = n_arenas;

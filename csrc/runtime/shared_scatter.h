@@ -92,13 +92,32 @@ void compute_shares(const uint8_t* arena, int64_t capacity, int64_t fields, int 
 // header (total_rows = s.rows, GPU varint decode off).
 std::vector<ShareCopy> share_copies(const uint8_t* arena, const RankShare& s, uint8_t* hdr_stage);
 
+// NUMA placement of the shared arenas, per rank: requests are appended in row
+// order and shares are contiguous row ranges, so rank r's bytes of a full batch
+// sit at about payload [r S, (r + 1) S), S = expected_payload / world. Those
+// pages go on the NUMA node of the GPU that DMAs them (rank 0's thread writes
+// them once across the socket link instead of that GPU reading them across it
+// every step). Byte offsets are segment-relative, page-aligned.
+struct NodeSlice {
+  int64_t lo = 0, hi = 0;
+  int node = -1;
+  int rank = -1;
+  bool bound = false;  // mbind succeeded (false: one-node machine / no NUMA support)
+};
+std::vector<NodeSlice> scatter_placement(int64_t arenas_off, int n_arenas, int64_t arena_stride, int64_t payload_off,
+                                         int64_t expected_payload, const std::vector<int>& rank_nodes);
+
 class SharedScatter {
  public:
   // create (rank 0): the segment sized for n_arenas arenas of arena_cap bytes
   // and `slots` outputs of out_floats fp32 scores; node >= 0 places its pages
-  // on that NUMA node. attach (rank > 0): map an existing segment.
+  // on that NUMA node, then rank_nodes (one node per rank, -1 unknown) and
+  // expected_payload (bytes of a full batch) place each rank's share of every
+  // arena on its own node (scatter_placement). attach (rank > 0): map an
+  // existing segment.
   SharedScatter(const std::string& name, int world, int rank, bool create, int64_t fields = 0, int n_arenas = 0,
-                int64_t arena_cap = 0, int slots = 0, int64_t out_floats = 0, int node = -1);
+                int64_t arena_cap = 0, int slots = 0, int64_t out_floats = 0, int node = -1,
+                const std::vector<int>& rank_nodes = {}, int64_t expected_payload = 0);
   ~SharedScatter();
   SharedScatter(const SharedScatter&) = delete;
   SharedScatter& operator=(const SharedScatter&) = delete;
@@ -120,6 +139,8 @@ class SharedScatter {
   void set_on_unmap(std::function<void(void*, size_t)> f) { on_unmap_ = std::move(f); }
   bool all_attached() const;
   void unlink();
+  // create side: the per-rank slices placed at creation (empty on attach)
+  const std::vector<NodeSlice>& placement() const { return placement_; }
 
   // The step index of the next launch on this rank (every rank launches every
   // step in the same order, so the counters agree).
@@ -150,6 +171,7 @@ class SharedScatter {
   std::atomic<uint64_t> next_step_{0};
   std::atomic<int64_t> h2d_bytes_{0}, h2d_steps_{0};
   std::function<void(void*, size_t)> on_unmap_;
+  std::vector<NodeSlice> placement_;
 };
 
 }  // namespace runtime

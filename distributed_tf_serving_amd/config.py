@@ -50,10 +50,12 @@ class ModelConfig:
     multi_hot: int = 1                # dlrm: ids per sparse table (> 1: weighted sum-pooled bag, K1b)
     # dlrm tables sharded over ranks: "alltoall" (ids + rows through RCCL),
     # "peer" (rows loaded from the owner's HBM over xGMI, hot remote rows from a
-    # per-rank replica cache of hot_cache_rows rows; parallel/hot_cache.py) or
+    # per-rank replica cache of hot_cache_rows rows - -1: a quarter of the
+    # free device memory, capped at the remote rows; 0: no cache;
+    # parallel/hot_cache.py) or
     # "auto" (peer on GPUs that can all load from each other, else alltoall)
     embedding_exchange: str = "auto"
-    hot_cache_rows: int = 1 << 20
+    hot_cache_rows: int = -1
     param_dtype: str = "bf16"         # storage dtype of embeddings + dense weights
     gemm_dtype: str = "bf16"          # bf16 | fp8 (dcn_v2 towers on CDNA4 fp8 MFMA)
     seed: int = 1234

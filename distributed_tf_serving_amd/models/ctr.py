@@ -109,9 +109,9 @@ class CTRModel(nn.Module):
 
     # A local GPU step as a two-lane program (parallel/step_program.py): the
     # gather-GEMM's resolve pass of step k+1 runs on the aux lane right after
-    # its H2D, while the compute lane finishes step k (default for the
-    # gather-GEMM buckets; DTFS_RESOLVE_LANE=0 turns it off, parallel/fanout.py
-    # _program_enabled).
+    # its H2D, while the compute lane finishes step k (DTFS_RESOLVE_LANE=1;
+    # off by default since the one-wave gather-GEMM leaves it no registers to
+    # co-run in, parallel/fanout.py _program_enabled).
     resolve_lane = False
 
     def build_program(self, ids, wts, B: int, bufs: dict, out: Optional[torch.Tensor] = None,

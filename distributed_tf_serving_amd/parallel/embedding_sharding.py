@@ -269,7 +269,7 @@ class ShardedEmbedding(nn.Module):
             self.peer = hot_cache.PeerTables(stores, owner, [lay[owner[t]][1][t] for t in range(T)],
                                              [plan.tables[t].rows for t in range(T)], self.rank,
                                              chunk_shift=hot_cache.CHUNK_SHIFT if peer else None)
-            if peer and cache_rows > 0 and self.peer.remote_tables:
+            if peer and cache_rows != 0 and self.peer.remote_tables:  # < 0: sized from free HBM
                 self.cache = hot_cache.HotRowCache(self.peer, cache_rows, sample_every=cache_sample_every)
         i64 = dict(dtype=torch.int64, device=dev)
         # table-wise route: slot (s, j) <- table tw_by_rank[s][j] (pad: column 0, row 0 of s)
@@ -491,7 +491,7 @@ class ShardedDLRM(nn.Module):
         self.dense.gen = None
         self.emb = ShardedEmbedding(self.plan, ctx, cfg.seed, self.dense.table_bound, DTYPES[cfg.param_dtype],
                                     device, group, col_base=cfg.num_dense, hot=self.hot, exchange=exchange,
-                                    cache_rows=int(getattr(cfg, "hot_cache_rows", 0)))
+                                    cache_rows=int(getattr(cfg, "hot_cache_rows", -1)))
         self.device_ = torch.device(device)
 
     def signature(self):

@@ -296,16 +296,18 @@ class FanoutEngine:
         if not (self.cuda and self.mode == "local" and self.native_launch and self.ingest == "arena"):
             return False
         # embedding-parallel models: the exchange is the program. Local
-        # gather-GEMM steps run as one too (DTFS_RESOLVE_LANE=0 turns it
-        # off): the resolve pass of step k+1 on the aux lane right after its
-        # H2D, the compute lane waiting only for that - 108.4 vs 104.5 M
-        # scores/s interleaved on one box (profiles/r04_session2.md). (A
-        # cross-step overlapped GATHER slowed the fused head 12.6 -> 61 us,
-        # profiles/step_overlap.md; the resolve pass is a tenth of its bytes.)
+        # gather-GEMM steps can run as one too (DTFS_RESOLVE_LANE=1): the
+        # resolve pass of step k+1 on the aux lane right after its H2D, the
+        # compute lane waiting only for that - 108.4 vs 104.5 M scores/s with
+        # round 4's 8-phase gather-GEMM (profiles/r04_session2.md). Off by
+        # default since round 5: the one-wave gather-GEMM holds every
+        # register of every SIMD, the aux lane's resolve cannot co-run (86 us
+        # mean, starved) and the one-stream step measured 131.0 / 130.3 vs
+        # 129.9 / 123.2 M interleaved (profiles/r05_gg1w.md).
         m = self.ex.model
         if getattr(m, "supports_program", False):
             return True
-        if os.environ.get("DTFS_RESOLVE_LANE", "1") != "1" or not getattr(m, "resolve_lane", False):
+        if os.environ.get("DTFS_RESOLVE_LANE", "0") != "1" or not getattr(m, "resolve_lane", False):
             return False
         # only the buckets whose step runs the gather-GEMM (smaller steps keep
         # the one-stream step: no cross-lane hop on the light-load path)
@@ -416,7 +418,9 @@ class FanoutEngine:
         buf = self.ex.input_buffer(B, slot)
         ids, wts = self.layout.ids(buf), self.layout.wts(buf)
         res = None
-        if (self.cuda and self.ex.use_graphs and os.environ.get("DTFS_RESOLVE_LANE", "1") == "1"
+        # off by default like the local program: 122.0 / 121.5 (on) vs 122.3 /
+        # 123.0 M (off) interleaved with the one-wave gather-GEMM (profiles/r05_gg1w.md)
+        if (self.cuda and self.ex.use_graphs and os.environ.get("DTFS_RESOLVE_LANE", "0") == "1"
                 and getattr(m, "resolve_lane", False) and m._resolve_applies(ids, wts)):
             st: dict = {}
             side = torch.cuda.Stream(self.dev)

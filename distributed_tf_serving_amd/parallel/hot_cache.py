@@ -124,6 +124,29 @@ class PeerTables:
         return out
 
 
+# Bytes of device memory one cached row costs: the bf16 row + its share of the
+# two {key, slot} index buffers (2 x 2 entries x 16 B at the 50 % load factor)
+# + the hot-set / candidate arrays of a refresh.
+CACHE_BYTES_PER_ROW = 2 * D + 64 + 32
+
+
+def auto_capacity(peer: "PeerTables", free_bytes: Optional[int] = None, fraction: float = 0.25,
+                  floor: int = 1 << 16) -> int:
+    """Default replica-cache capacity: ``fraction`` of the device memory still
+    free once the tables are placed, capped at the remote rows there are to
+    cache. MI355X: ~250 GB free beside a 2 x 38 GB sharded DLRM -> room for
+    every remote row of the round-4 rehearsal tables; the cap keeps small
+    models from reserving memory they cannot use."""
+    remote_rows = int(sum(int(r) for r, rem in zip(peer.rows, peer.tremote_cpu.tolist()) if rem))
+    if remote_rows == 0:
+        return 0
+    if free_bytes is None:
+        dev = peer.trows.device
+        free_bytes = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else 1 << 30
+    fit = int(fraction * free_bytes) // CACHE_BYTES_PER_ROW
+    return max(min(floor, remote_rows), min(remote_rows, fit))
+
+
 class HotRowCache:
     """This rank's replica of hot rows of tables owned by other ranks.
 
@@ -141,9 +164,12 @@ class HotRowCache:
     it keeps at most ``fill`` x capacity rows hot so there are free slots for
     the next turnover."""
 
-    def __init__(self, peer: PeerTables, capacity: int, ring_cap: int = 1 << 20, sample_every: int = 8,
+    def __init__(self, peer: PeerTables, capacity: Optional[int] = -1, ring_cap: int = 1 << 20, sample_every: int = 8,
                  decay: float = 0.5, fill: float = 0.75):
         self.peer = peer
+        self.sized = "explicit"
+        if capacity is None or int(capacity) < 0:  # auto: from the free device memory
+            capacity, self.sized = auto_capacity(peer), "auto (a quarter of free device memory, capped at the remote rows)"
         self.cap = max(1, int(capacity))
         self.H = _next_pow2(2 * self.cap)
         self.sample_every, self.decay, self.fill = int(sample_every), float(decay), float(fill)
@@ -328,7 +354,8 @@ class HotRowCache:
 
     def describe(self) -> dict:
         h, m = self.counts()
-        return {"capacity_rows": self.cap, "hot_rows": int(self.keys.numel()), "refreshes": self.refreshes,
+        return {"capacity_rows": self.cap, "sized": self.sized, "hot_rows": int(self.keys.numel()),
+                "refreshes": self.refreshes,
                 "hits": h, "misses": m, "hit_rate": round(h / (h + m), 4) if h + m else None,
                 "refresh_failures": self.refresh_failures, "refresher_alive": self.refresher_alive,
                 "last_error": self.last_error}

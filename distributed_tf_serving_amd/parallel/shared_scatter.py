@@ -25,15 +25,24 @@ from .control import default_store
 
 def create_shared_scatter(module, world: int, rank: int, fields: int, n_arenas: int, arena_cap: int, slots: int,
                           out_floats: int, store=None, prefix: str = "dtfs/scatter/0", node: int = -1,
-                          register: bool = False, timeout_s: float = 60.0):
+                          register: bool = False, timeout_s: float = 60.0, expected_payload: int = 0):
     """A SharedScatter of ``module`` (``_hip`` for GPU ranks, which also
     register the mapping with their device, ``_native`` for CPU ranks).
-    Not a collective: every rank calls it with the same ``prefix``."""
+    Not a collective: every rank calls it with the same ``prefix``.
+    ``node``: this rank's NUMA node (-1 unknown). Every rank publishes its node;
+    rank 0 places the segment on its own and, with ``expected_payload`` (bytes
+    of a full batch), each rank's share of every arena on that rank's node
+    (runtime/shared_scatter.h scatter_placement)."""
     store = store if store is not None else default_store()
     name_key, att_key = f"{prefix}/name", f"{prefix}/attached"
+    store.set(f"{prefix}/node/{rank}", str(int(node)))
     if rank == 0:
+        keys = [f"{prefix}/node/{r}" for r in range(world)]
+        store.wait(keys, datetime.timedelta(seconds=timeout_s))
+        rank_nodes = [int(store.get(k).decode()) for k in keys]
         name = f"/dtfs-sct-{os.getpid()}-{secrets.token_hex(6)}"
-        seg = module.SharedScatter(name, world, 0, True, fields, n_arenas, arena_cap, slots, out_floats, node)
+        seg = module.SharedScatter(name, world, 0, True, fields, n_arenas, arena_cap, slots, out_floats, node,
+                                   rank_nodes if expected_payload > 0 else [], int(expected_payload))
         store.set(name_key, name)
     else:
         store.wait([name_key], datetime.timedelta(seconds=timeout_s))
@@ -64,6 +73,10 @@ def scatter_for_engine(ctx, fields: int, arena_cap: int, slots: int, max_rows_pe
     from ..utils.affinity import current_node
 
     cuda = ctx.device.type == "cuda"
+    # a full batch's request bytes (raw tensor_content: 8 B id + 4 B weight per
+    # feature, + framing): where each rank's share of an arena will sit
+    expected = ctx.world * max_rows_per_rank * (12 * fields + 16)
     return create_shared_scatter(hip() if cuda else native(), ctx.world, ctx.rank, fields, n_arenas or slots + 3,
                                  arena_cap, slots, ctx.world * max_rows_per_rank, store=store,
-                                 prefix=f"dtfs/scatter/{tag}", node=current_node() if cuda else -1, register=cuda)
+                                 prefix=f"dtfs/scatter/{tag}", node=current_node() if cuda else -1, register=cuda,
+                                 expected_payload=expected)

@@ -73,7 +73,7 @@ def test_bench_scatter_mode_rccl_path_world2():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n,mode", [(4, "alltoall"), (8, "alltoall"), (4, "scatter"), (4, "local")])
+@pytest.mark.parametrize("n,mode", [(4, "alltoall"), (8, "alltoall"), (4, "scatter"), (8, "scatter"), (4, "local")])
 def test_bench_more_ranks(n, mode):
     """World 4 and 8 over gloo, with requests (20 rows) that do not divide by
     the world size: every rank must finish the same lockstep steps (no hang)
@@ -111,6 +111,20 @@ def test_bench_sharded_dlrm_peer_exchange_world2():
     assert c["hot_rows"] > 0 and c["refreshes"] == 2 and c["remote_lookups_per_step"] > 0
     assert 0.0 < c["hit_rate"] <= 1.0 and 0.0 <= c["hit_rate_fresh_stream"] <= 1.0
     assert c["xgmi_bytes_per_step_per_rank"] < ex["bytes_per_step_per_rank"]
+    assert out.get("requests_failed", 0) == 0
+
+
+@pytest.mark.slow
+def test_bench_sharded_dlrm_peer_exchange_world8():
+    """The 8-rank shape of config 4 rehearsed over gloo: 26 tables placed on 8
+    ranks, every rank loading from 7 peers' stores, caches sized automatically
+    (capped at the remote rows), whole-job rate over 8 ranks."""
+    out = _run_bench(8, ("--model", "dlrm", "--table-rows", "2000", "--exchange", "peer", "--cache-learn-rounds", "1",
+                         "--request-rows", "20", "--requests-per-gpu", "2"))
+    par = out["config"]["parallelism"]
+    assert "embedding-mp8" in par and out["n_gpus"] == 8 and out["config"]["global_batch"] == 8 * 40, par
+    c = out["embedding_exchange"]["hot_row_cache"]
+    assert c is not None and c["sized"].startswith("auto") and c["capacity_rows"] > 0
     assert out.get("requests_failed", 0) == 0
 
 

@@ -125,6 +125,24 @@ def test_chunked_store_rows():
         PeerTables([[torch.zeros(8, 64), torch.zeros(16, 64)]], [0], [0], [20], rank=0, chunk_shift=4)
 
 
+def test_auto_capacity_from_free_memory():
+    """Default capacity: a quarter of the free device memory at
+    CACHE_BYTES_PER_ROW a row, capped at the remote rows (floor 64 k or all of
+    them); no remote table, no cache."""
+    from distributed_tf_serving_amd.parallel.hot_cache import CACHE_BYTES_PER_ROW, auto_capacity
+
+    p = _local_peer(T=4, rows=50, remote=(1, 3))
+    assert auto_capacity(p, free_bytes=1 << 40) == 100  # capped: 2 remote tables x 50 rows
+    assert auto_capacity(_local_peer(remote=())) == 0
+    big = _local_peer(T=2, rows=50, remote=(1,))
+    big.rows = [50, 10 ** 9]  # a billion-row remote table (the stores stay small: capacity math only)
+    assert auto_capacity(big, free_bytes=4 * CACHE_BYTES_PER_ROW * 10 ** 6) == 10 ** 6
+    assert auto_capacity(big, free_bytes=0) == 1 << 16  # the floor
+    c = HotRowCache(p, capacity=-1, ring_cap=64)
+    assert c.cap == 100 and c.describe()["sized"].startswith("auto")
+    assert HotRowCache(p, capacity=8, ring_cap=64).describe()["sized"] == "explicit"
+
+
 def test_cache_refresh_slot_safety_and_turnover():
     p = _local_peer()
     c = HotRowCache(p, capacity=8, ring_cap=64, sample_every=1, fill=0.75)

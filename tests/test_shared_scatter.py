@@ -118,3 +118,46 @@ def test_gpu_varint_arena_is_refused():
     lay.build(ar, lay.place(ar, reqs))
     with pytest.raises(Exception, match="varint"):
         native().SharedScatter.shares(ar, F, 2, 8)
+
+
+def test_numa_placement_puts_each_share_on_its_reader_node():
+    """Per-rank NUMA slices of the shared arenas (a 2-socket node: ranks 0-1
+    on node 0, ranks 2-3 on node 1): rank r's share of every arena, about
+    payload [r S, (r + 1) S) of a full batch, is bound to r's node - the last
+    rank's slice runs to the arena's end; nothing is bound for ranks on rank
+    0's node. On a one-node machine the binding reports failure (best effort)
+    and the segment serves as before."""
+    F, world, B = 6, 4, 64
+    lay = ArenaLayout(F, max_rows=world * B, gpu_varint=False)
+    name = f"/dtfs-test-sct-{os.getpid()}-{secrets.token_hex(4)}"
+    expected = world * B * (12 * F + 16)
+    seg = native().SharedScatter(name, world, 0, True, F, 3, lay.capacity, 2, world * B, -1, [0, 0, 1, 1], expected)
+    try:
+        pl = seg.placement()
+        page = 4096
+        stride = -(-lay.capacity // page) * page
+        payload_off = 64 + 32 * 1024  # kArenaPayloadOff: header + request descriptors
+        up = lambda x: -(-x // page) * page  # noqa: E731
+        # per arena: ranks 2 and 3 (both node 1) merge into one slice from rank 2's
+        # first page to the arena's end
+        assert len(pl) == 3 and all(s["node"] == 1 and s["rank"] == 2 for s in pl), pl
+        for s in pl:
+            a0 = s["hi"] - stride  # the arena's start (its slice ends at the arena's end)
+            assert a0 % page == 0 and s["lo"] - a0 == up(payload_off + expected * 2 // world)
+        n_nodes = native().numa_node_count()
+        if n_nodes < 2:
+            assert not any(s["bound"] for s in pl)  # no node 1 here
+        else:
+            assert all(s["bound"] for s in pl)
+            seg.arena(0)[pl[0]["lo"] - (pl[0]["hi"] - stride):].fill_(1)  # first touch places the pages
+            assert seg.page_node(pl[0]["lo"]) == 1
+        # every rank on node 0, or no expected payload: nothing placed
+        name2 = name + "b"
+        seg2 = native().SharedScatter(name2, world, 0, True, F, 3, lay.capacity, 2, world * B, -1, [0, 0, 0, 0],
+                                      expected)
+        assert seg2.placement() == []
+        seg2.unlink()
+        with pytest.raises(Exception):  # one node per rank
+            native().SharedScatter(name + "c", world, 0, True, F, 3, lay.capacity, 2, world * B, -1, [0, 1], expected)
+    finally:
+        seg.unlink()

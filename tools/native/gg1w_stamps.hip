@@ -33,6 +33,9 @@ static double med(std::vector<double> v) {
 
 int main(int argc, char** argv) {
   const bool hot = argc > 1 && std::string(argv[1]) == "hot";
+  // "graph": the launches go through a captured HIP graph on a non-blocking
+  // stream (the served step's way; the kernel's scratch use is reported)
+  const bool graph = argc > 1 && std::string(argv[1]) == "graph";
   const int F = 43, N = 1024, V = 1 << 20, K = F * 64;
   void *table, *W, *C;
   float *bias, *fm, *wts;
@@ -59,6 +62,24 @@ int main(int argc, char** argv) {
     }
     (void)hipMemcpy(rows, r.data(), r.size() * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(wts, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  }
+  if (graph) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&dtfs::kern::gemm_gather1w_kernel<true>));
+    printf("{\"kernel\": \"gemm_gather1w<FM>\", \"scratch_bytes_per_lane\": %zu}\n", fa.localSizeBytes);
+    hipStream_t st;
+    (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    (void)hipStreamBeginCapture(st, hipStreamCaptureModeGlobal);
+    for (int i = 0; i < 4; ++i)
+      (void)dtfs::launch_gemm_gather1w(table, V, rows, wts, 16384, F, W, bias, C, N, fm, 16384, N, 1, st);
+    (void)hipStreamEndCapture(st, &g);
+    (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    for (int i = 0; i < 5; ++i) (void)hipGraphLaunch(ge, st);
+    const hipError_t e = hipStreamSynchronize(st);
+    printf("{\"graph_replays\": 5, \"status\": \"%s\"}\n", hipGetErrorString(e));
+    return e == hipSuccess ? 0 : 1;
   }
   for (int M : {2048, 16384}) {
     auto run = [&] {
