@@ -109,6 +109,9 @@ def parse_args():
                     help="N > 1: alltoall = every request fanned out over all GPUs (config 3, default); local = "
                          "one independent replica per GPU (default for dlrm: its tables are sharded instead and "
                          "every step exchanges embeddings); scatter = rank 0 is the only front door")
+    ap.add_argument("--feature-weights", default="uniform", choices=["uniform", "ones"],
+                    help="request feature weights: uniform in (0, 1] (default) or all 1.0 as the reference client "
+                         "sends them (DCNClient.java:67-73; host narrowing then ships no weight bytes)")
     ap.add_argument("--encoding", default="raw", choices=["raw", "packed"],
                     help="raw = tensor_content; packed = int64_val/float_val like the reference client")
     ap.add_argument("--decode-threads", type=int, default=4,
@@ -284,7 +287,8 @@ def request_pool(a, ctx, eng, B, F):
     if a.reference_workload:  # every candidate ids 1..43, weights 1.0 (DCNClient.java:57-74)
         synth = SyntheticRequests(fields=F, dist="reference")
         return ([synth.serialized(a.request_rows, raw=False)] if rows_in else []), n_req
-    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank)
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank,
+                              weights=a.feature_weights)
     peer = getattr(getattr(getattr(eng.ex, "model", None), "emb", None), "peer", None) is not None
     n = max(1, a.stream_pool if peer else a.pool) if n_req else 0
     return [synth.serialized(a.request_rows, raw=(a.encoding == "raw")) for _ in range(n)], n_req
@@ -508,7 +512,7 @@ def run_live(a, ctx, cfg, model, eng, B):
     sync()
     st = live.stats()
     keys = ("steps", "full_steps", "timeout_steps", "eager_steps", "empty_steps", "proposed_steps", "joined_steps",
-            "blocked_submits", "narrowed")
+            "blocked_submits", "narrowed", "narrowed_wts_bf16", "narrowed_wts_implicit")
     extra["server"] = {k: st[k] for k in keys}
     extra["server"]["steps_in_throughput_run"] = st_load["steps"]
     if control is not None:
@@ -734,7 +738,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
             "dtype": dtype_label(cfg),
-            "data": "synthetic (zipf feature ids over 2^40, uniform weights; random-init weights)",
+            "data": ("synthetic (zipf feature ids over 2^40, " +
+                     ("feature weights 1.0 as the reference client sends them" if a.feature_weights == "ones"
+                      else "uniform weights") + "; random-init weights)"),
             "config": {
                 "model": describe_model(cfg),
                 "global_batch": world * B,

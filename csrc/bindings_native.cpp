@@ -792,6 +792,18 @@ PYBIND11_MODULE(_native, m) {
         return out.narrow(0, 0, 3 * src.numel());
       },
       py::arg("ids"), py::arg("modulo"), "Host K0: int64 ids -> 3-byte little-endian rows (id mod modulo <= 2^24).");
+  m.def(
+      "classify_weights",
+      [](torch::Tensor wts, int64_t wcols) {
+        TORCH_CHECK(wts.device().is_cpu() && wts.scalar_type() == torch::kFloat32 && wts.dim() == 2,
+                    "wts must be CPU fp32 [rows, fields]");
+        TORCH_CHECK(wcols >= 1 && wcols <= wts.size(1), "wcols must be in [1, fields]");
+        auto src = wts.contiguous();
+        return runtime::classify_weights(reinterpret_cast<const uint8_t*>(src.data_ptr()), src.size(0), src.size(1),
+                                         wcols);
+      },
+      py::arg("wts"), py::arg("wcols"),
+      "Host K0: the cheapest exact form of a request's first wcols weights per row (0 fp32, 1 bf16, 2 all 1.0).");
   m.def("now_us", &runtime::now_us);
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); }, py::arg("name"));

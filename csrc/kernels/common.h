@@ -92,12 +92,20 @@ __device__ __forceinline__ int arena_narrow_idb(const uint8_t* arena) {
   return *reinterpret_cast<const int32_t*>(arena + 40) == 3 ? 3 : 4;
 }
 
+// Row-table wts_off of a narrowed row, bits 31..30: how its weights travel
+// (runtime/narrow.h WtsKind): fp32, bf16 (every weight of the request was
+// exactly a bf16 value) or none (every weight was 1.0, the reference client's
+// requests, DCNClient.java:67-73). Bits 29..0: the payload offset.
+constexpr uint32_t kWtsOffMask = 0x3fffffffu;
+constexpr int kWtsF32 = 0, kWtsBf16 = 1, kWtsOnes = 2;
+
 struct ArenaRow {
   const uint8_t* ids;  // 8 * F bytes of int64 ids (narrow: idb * F bytes of rows), or nullptr (padding row)
-  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: 4 * wcols, 4-byte aligned)
+  const uint8_t* wts;  // 4 * F bytes of fp32 weights (narrow: wcols weights of kind wkind)
   bool narrow;
   int wcols;  // narrow rows: weights present (arena_narrow_wcols)
   int idb;    // narrow rows: bytes per id (arena_narrow_idb)
+  int wkind = kWtsF32;  // narrow rows: kWtsF32 / kWtsBf16 / kWtsOnes
 };
 
 // Table row of feature f of a narrowed row: int32, or 3 packed bytes (the
@@ -107,6 +115,25 @@ __device__ __forceinline__ int64_t arena_narrow_id(const ArenaRow& ar, int f) {
   return int64_t(reinterpret_cast<const int32_t*>(ar.ids)[f]);
 }
 
+// Weight f of a narrowed row (0 past the columns the row carries).
+__device__ __forceinline__ float arena_narrow_w(const ArenaRow& ar, int f) {
+  if (f >= ar.wcols) return 0.f;
+  if (ar.wkind == kWtsOnes) return 1.f;
+  if (ar.wkind == kWtsBf16) return __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(ar.wts)[f]) << 16);
+  return reinterpret_cast<const float*>(ar.wts)[f];
+}
+
+// A row-table entry {ids_off, wts_off} of the payload -> the row.
+__device__ __forceinline__ ArenaRow arena_row_at(const uint8_t* payload, int2 o, int wcols, int idb) {
+  ArenaRow r{payload + (o.x & 0x7fffffff), payload + (uint32_t(o.y) & kWtsOffMask), o.x < 0, kArenaAllWeights, 4};
+  if (r.narrow) {
+    r.wcols = wcols;
+    r.idb = idb;
+    r.wkind = int(uint32_t(o.y) >> 30);
+  }
+  return r;
+}
+
 __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payload_off, int64_t r) {
   const int64_t total = *reinterpret_cast<const int64_t*>(arena + 8);
   ArenaRow out{nullptr, nullptr, false, kArenaAllWeights, 4};
@@ -114,13 +141,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
     const uint8_t* payload = arena + payload_off;
     const int64_t rt = *reinterpret_cast<const int64_t*>(arena + 16);
     const int2 o = reinterpret_cast<const int2*>(payload + rt)[r];
-    out.narrow = o.x < 0;
-    out.ids = payload + (o.x & 0x7fffffff);
-    out.wts = payload + o.y;
-    if (out.narrow) {
-      out.wcols = arena_narrow_wcols(arena);
-      out.idb = arena_narrow_idb(arena);
-    }
+    out = arena_row_at(payload, o, arena_narrow_wcols(arena), arena_narrow_idb(arena));
   }
   return out;
 }
@@ -129,7 +150,7 @@ __device__ __forceinline__ ArenaRow arena_row(const uint8_t* arena, int64_t payl
 __device__ __forceinline__ void arena_feature(const ArenaRow& ar, int f, int64_t& id, float& w) {
   if (ar.narrow) {
     id = arena_narrow_id(ar, f);
-    w = f < ar.wcols ? reinterpret_cast<const float*>(ar.wts)[f] : 0.f;
+    w = arena_narrow_w(ar, f);
   } else {
     id = int64_t(load_u64_unaligned(ar.ids + 8 * f));
     w = __uint_as_float(load_u32_unaligned(ar.wts + 4 * f));

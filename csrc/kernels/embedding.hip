@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) embed_pipe_kernel(EmbedArgs a, uint64_t m
     id = 0;
     w = 0.f;
     if (!ok) return;
-    const ArenaRow ar{a_payload + (d.x & 0x7fffffff), a_payload + d.y, d.x < 0, a_wcols, a_idb};
+    const ArenaRow ar = arena_row_at(a_payload, d, a_wcols, a_idb);
     arena_feature(ar, lane, id, w);
   };
   // stage 2: hash -> table row (clamped), weight (0 for rows another shard owns)
@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(256) embed_resolve_kernel(EmbedArgs a, uint64_
     if constexpr (ARENA) {
       if (b < a.B && b < a_rows) {
         const int2 d = s_desc[r];
-        const ArenaRow ar{payload + (d.x & 0x7fffffff), payload + d.y, d.x < 0, a_wcols, a_idb};
+        const ArenaRow ar = arena_row_at(payload, d, a_wcols, a_idb);
         arena_feature(ar, f, id[k], w[k]);
       }
     } else if (b < a.B) {

@@ -29,16 +29,14 @@ __global__ void __launch_bounds__(256) unpack_arena_kernel(const uint8_t* __rest
   const ArenaRow src = arena_row(arena, kArenaPayloadOff, r);
   int64_t* dst = packed + int64_t(r) * W;
   if (src.narrow) {  // host-narrowed row: int32 rows -> int64, fp32 weights (packed as 2 per word)
-    const int fw = min(F, src.wcols);  // weights the row carries (the rest are 0)
     for (int c = lane; c < W; c += 64) {
       uint64_t v = 0;
       if (c < F) {
         v = uint64_t(arena_narrow_id(src, c));
       } else {
         const int f0 = 2 * (c - F);
-        const uint32_t* wb = reinterpret_cast<const uint32_t*>(src.wts);
-        const uint32_t lo = f0 < fw ? wb[f0] : 0u;
-        const uint32_t hi = f0 + 1 < fw ? wb[f0 + 1] : 0u;
+        const uint32_t lo = f0 < F ? __float_as_uint(arena_narrow_w(src, f0)) : 0u;
+        const uint32_t hi = f0 + 1 < F ? __float_as_uint(arena_narrow_w(src, f0 + 1)) : 0u;
         v = (uint64_t(hi) << 32) | lo;
       }
       dst[c] = int64_t(v);

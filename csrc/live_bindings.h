@@ -372,6 +372,8 @@ void def_live_methods(py::class_<H>& c) {
             o["eager_steps"] = s.eager_steps;
             o["blocked_submits"] = s.blocked_submits;
             o["narrowed"] = s.narrowed;
+            o["narrowed_wts_bf16"] = s.narrowed_wts_bf16;
+            o["narrowed_wts_implicit"] = s.narrowed_wts_implicit;
             o["proposed_steps"] = s.proposed_steps;
             o["joined_steps"] = s.joined_steps;
             o["copy_us"] = s.copy_us;

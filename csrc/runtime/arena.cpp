@@ -1,4 +1,5 @@
 #include "arena.h"
+#include "narrow.h"
 
 #include <algorithm>
 #include <climits>
@@ -87,11 +88,12 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
     const ArenaItem& it = items[i];
     if (it.narrow) {
       const int64_t ne = it.rows * fields;
-      const int64_t nw = it.rows * wcols;
+      const int64_t nwb = it.rows * wcols * wts_bytes_per(it.wkind);
       if (it.rows < 0 || it.ids_off < 0 || it.wts_off < 0 || it.ids_off % 4 || it.wts_off % 4 ||
-          it.ids_off + idb * ne + 4 > cap || it.wts_off + 4 * nw > cap)
+          it.wkind < kWtsF32 || it.wkind > kWtsOnes || it.ids_off + idb * ne + 4 > cap || it.wts_off + nwb > cap ||
+          it.wts_off >= (int64_t(1) << kWtsKindShift))
         throw std::invalid_argument("narrow request outside arena");
-      end = std::max(end, std::max(it.ids_off + idb * ne + 4, it.wts_off + 4 * nw));  // +4: a reader's 4-byte load of the last 3-byte id
+      end = std::max(end, std::max(it.ids_off + idb * ne + 4, it.wts_off + nwb));  // +4: a reader's 4-byte load of the last 3-byte id
       continue;
     }
     spans[i] = {it.off, it.len};
@@ -164,7 +166,7 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
         continue;
       }
       desc[4 * nd + 0] = items[i].ids_off | kNarrowFlag;
-      desc[4 * nd + 1] = items[i].wts_off;
+      desc[4 * nd + 1] = items[i].wts_off | (int64_t(items[i].wkind) << kWtsKindShift);
       desc[4 * nd + 2] = rows;
       desc[4 * nd + 3] = row;
       ++nd;
@@ -312,9 +314,11 @@ ArenaBatch arena_build_items(uint8_t* base, int64_t capacity, const std::vector<
     const int64_t io = desc[4 * d + 0], wo = desc[4 * d + 1], rows = desc[4 * d + 2], r0 = desc[4 * d + 3];
     if (io & kNarrowFlag) {
       const int64_t ni = io & ~kNarrowFlag;
+      const int64_t kind = wo >> kWtsKindShift, w0 = wo & ((int64_t(1) << kWtsKindShift) - 1);
+      const int64_t wrow = wts_bytes_per(int(kind)) * wcols;
       for (int64_t r = 0; r < rows; ++r) {
         tab[2 * (r0 + r) + 0] = int32_t(uint32_t(ni + r * idb * fields) | 0x80000000u);
-        tab[2 * (r0 + r) + 1] = int32_t(wo + r * 4 * wcols);
+        tab[2 * (r0 + r) + 1] = int32_t(uint32_t(w0 + r * wrow) | uint32_t(kind << kWtsKindShift));
       }
       continue;
     }
@@ -357,8 +361,9 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
     std::memcpy(e, payload + rt + 8 * row, 8);
     const bool narrow = e[0] < 0;
     const uint8_t* ip = payload + int64_t(uint32_t(e[0]) & 0x7fffffffu);
-    const uint8_t* wp = payload + e[1];
-    if (narrow) {  // int32 / 3-byte rows -> int64, fp32 weights as they are
+    const int wkind = narrow ? int(uint32_t(e[1]) >> kWtsKindShift) : kWtsF32;
+    const uint8_t* wp = payload + (narrow ? int64_t(uint32_t(e[1]) & ((1u << kWtsKindShift) - 1)) : int64_t(e[1]));
+    if (narrow) {  // int32 / 3-byte rows -> int64, weights back to fp32
       for (int64_t f = 0; f < fields; ++f) {
         int32_t id = 0;
         if (idb == 3) {
@@ -369,7 +374,20 @@ void arena_unpack_cpu(const uint8_t* base, uint8_t* dst, int64_t B, int64_t W, i
         const int64_t id64 = id;
         std::memcpy(dst + row * W * 8 + 8 * f, &id64, 8);
       }
-      std::memcpy(dst + row * W * 8 + 8 * fields, wp, size_t(4 * wcols));  // dropped columns stay 0
+      uint8_t* dw = dst + row * W * 8 + 8 * fields;  // dropped columns stay 0
+      if (wkind == kWtsF32) {
+        std::memcpy(dw, wp, size_t(4 * wcols));
+      } else {
+        for (int64_t c = 0; c < wcols; ++c) {
+          uint32_t v = 0x3f800000u;  // kWtsOnes: 1.0
+          if (wkind == kWtsBf16) {
+            uint16_t h;
+            std::memcpy(&h, wp + 2 * c, 2);
+            v = uint32_t(h) << 16;
+          }
+          std::memcpy(dw + 4 * c, &v, 4);
+        }
+      }
       continue;
     }
     std::memcpy(dst + row * W * 8, ip, size_t(8 * fields));

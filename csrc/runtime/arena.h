@@ -58,14 +58,15 @@ using Span = std::pair<int64_t, int64_t>;  // (payload offset, length)
 
 // One request of a batch: a serialized PredictRequest span (parsed here), or
 // a request whose candidate features the submitting thread already narrowed
-// into the payload (runtime/narrow.h: int32 table rows at ids_off, bf16
-// weights at wts_off; payload-relative). A narrow request's row-table entries
+// into the payload (runtime/narrow.h: int32 / 3-byte table rows at ids_off,
+// weights of kind wkind - fp32, bf16 or none - at wts_off; payload-relative). A narrow request's row-table entries
 // carry bit 31 of ids_off (the GPU reads 4 + 2 bytes per feature there) and
 // its descriptor's ids_off carries kNarrowFlag.
 struct ArenaItem {
   int64_t off = 0, len = 0;
   bool narrow = false;
   int64_t rows = 0, ids_off = 0, wts_off = 0;
+  int wkind = 0;  // narrow: how the weights travel (runtime/narrow.h WtsKind)
 };
 constexpr int64_t kNarrowFlag = int64_t(1) << 62;
 

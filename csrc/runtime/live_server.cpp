@@ -162,6 +162,8 @@ bool LiveServer::admit(const uint8_t* data, size_t n, int64_t deadline_us, Compl
   }
   const bool narrow = ids_src && wts_src;
   const int64_t wcols = cfg_.narrow_wts_cols > 0 ? cfg_.narrow_wts_cols : cfg_.fields;  // narrow weights kept per row
+  // the cheapest exact form of this request's weights (all 1.0: none travel)
+  const int wkind = narrow ? classify_weights(wts_src, rows, cfg_.fields, wcols) : kWtsF32;
   const int64_t idb = narrow_id_bytes();  // 3-byte rows for tables of <= 2^24 rows
   const int64_t ids_bytes = idb == 3 ? 3 * ne + kNarrow24Slack : 4 * ne;
   const int64_t need = narrow ? align64(ids_bytes) + align64(4 * rows * wcols) + 8 * rows + 256 : need_of(int64_t(n), rows);
@@ -231,8 +233,11 @@ bool LiveServer::admit(const uint8_t* data, size_t n, int64_t deadline_us, Compl
       p.narrow = true;
       p.ids_off = align64(o.used);
       p.wts_off = align64(p.ids_off + ids_bytes);
-      o.used = p.wts_off + 4 * rows * wcols;
+      p.wkind = wkind;
+      o.used = p.wts_off + wts_bytes_per(wkind) * rows * wcols;
       ++st_.narrowed;
+      if (wkind == kWtsBf16) ++st_.narrowed_wts_bf16;
+      if (wkind == kWtsOnes) ++st_.narrowed_wts_implicit;
     } else {
       off = p.off = o.used;
       o.used += align8(int64_t(n));
@@ -260,12 +265,8 @@ bool LiveServer::admit(const uint8_t* data, size_t n, int64_t deadline_us, Compl
   if (narrow) {  // ... narrowed on the way (K0 on the host)
     if (idb == 3) narrow_ids24(ids_src, payload + pend_ids, ne, cfg_.narrow_modulo);
     else narrow_ids(ids_src, reinterpret_cast<int32_t*>(payload + pend_ids), ne, cfg_.narrow_modulo);
-    if (wcols == cfg_.fields) {
-      std::memcpy(payload + pend_wts, wts_src, size_t(4 * ne));  // fp32 weights travel as they are
-    } else {  // only the weight columns the model reads
-      for (int64_t r = 0; r < rows; ++r)
-        std::memcpy(payload + pend_wts + 4 * r * wcols, wts_src + 4 * r * cfg_.fields, size_t(4 * wcols));
-    }
+    // only the weight columns the model reads, in the cheapest exact form
+    store_weights(wts_src, rows, cfg_.fields, wcols, wkind, payload + pend_wts);
   } else {
     std::memcpy(payload + off, data, n);
   }
@@ -523,6 +524,7 @@ void LiveServer::launcher_loop() {
       it.rows = p.rows;
       it.ids_off = p.ids_off;
       it.wts_off = p.wts_off;
+      it.wkind = p.wkind;
     }
     Arena& ar = arenas_[size_t(a)];
     ArenaBatch batch;

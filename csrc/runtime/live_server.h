@@ -133,6 +133,8 @@ struct LiveStats {
   int64_t submitted = 0, rejected = 0, completed = 0, failed = 0, expired = 0;
   int64_t steps = 0, rows = 0, padded_rows = 0, empty_steps = 0;
   int64_t full_steps = 0, timeout_steps = 0, eager_steps = 0, blocked_submits = 0, narrowed = 0;
+  // narrowed requests whose weights travelled as bf16 (all exact) / not at all (all 1.0)
+  int64_t narrowed_wts_bf16 = 0, narrowed_wts_implicit = 0;
   // cluster mode: steps this rank proposed / joined with a batch of its own /
   // joined with nothing queued (empty_steps counts those too)
   int64_t proposed_steps = 0, joined_steps = 0;
@@ -183,7 +185,8 @@ class LiveServer {
     int64_t off, len, rows, deadline_us, t_arrive;
     Completion done;
     bool narrow = false;
-    int64_t ids_off = 0, wts_off = 0;  // narrow: payload offsets of the 3-byte / int32 rows and fp32 weights
+    int64_t ids_off = 0, wts_off = 0;  // narrow: payload offsets of the 3-byte / int32 rows and the weights
+    int wkind = 0;                     // narrow: WtsKind of the weights (runtime/narrow.h)
   };
   struct Arena {
     uint8_t* base = nullptr;

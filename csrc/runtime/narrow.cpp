@@ -87,6 +87,42 @@ __attribute__((target("avx2"))) void pack24_avx2(const int32_t* rows, uint8_t* d
 
 }  // namespace
 
+int classify_weights(const uint8_t* src, int64_t rows, int64_t fields, int64_t wcols) {
+  bool ones = true, bf16 = true;
+  for (int64_t r = 0; r < rows && (ones || bf16); ++r) {
+    const uint8_t* p = src + 4 * r * fields;
+    uint32_t all = 0, low = 0;
+    for (int64_t c = 0; c < wcols; ++c) {
+      uint32_t v;
+      std::memcpy(&v, p + 4 * c, 4);
+      all |= v ^ 0x3f800000u;  // 1.0f
+      low |= v & 0xffffu;
+    }
+    ones = ones && all == 0;
+    bf16 = bf16 && low == 0;
+  }
+  return ones ? kWtsOnes : bf16 ? kWtsBf16 : kWtsF32;
+}
+
+void store_weights(const uint8_t* src, int64_t rows, int64_t fields, int64_t wcols, int kind, uint8_t* dst) {
+  if (kind == kWtsOnes) return;
+  if (kind == kWtsF32) {
+    if (wcols == fields) {
+      std::memcpy(dst, src, size_t(4 * rows * fields));
+    } else {
+      for (int64_t r = 0; r < rows; ++r) std::memcpy(dst + 4 * r * wcols, src + 4 * r * fields, size_t(4 * wcols));
+    }
+    return;
+  }
+  uint16_t* d = reinterpret_cast<uint16_t*>(dst);  // bf16: the high half of each (exact) fp32
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t c = 0; c < wcols; ++c) {
+      uint32_t v;
+      std::memcpy(&v, src + 4 * (r * fields + c), 4);
+      d[r * wcols + c] = uint16_t(v >> 16);
+    }
+}
+
 void narrow_ids(const uint8_t* src, int32_t* dst, int64_t n, int64_t modulo) {
   if (g_avx2) narrow_ids_avx2(src, dst, n, modulo);
   else narrow_ids_scalar(src, dst, n, modulo);

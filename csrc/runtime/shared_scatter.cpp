@@ -102,7 +102,12 @@ void compute_shares(const uint8_t* arena, int64_t capacity, int64_t fields, int 
       const bool narrow = x < 0;
       const int64_t ids_off = int64_t(uint32_t(x) & 0x7fffffffu);
       add(ids_off, narrow ? idb * fields + kNarrow24Slack : 8 * fields, last_ids);
-      add(int64_t(y), 4 * (narrow ? wcols : fields), last_wts);
+      if (narrow) {  // weights of kind y >> 30 (none for all-ones requests)
+        const int64_t wb = wts_bytes_per(int(uint32_t(y) >> kWtsKindShift)) * wcols;
+        if (wb > 0) add(int64_t(uint32_t(y) & ((1u << kWtsKindShift) - 1)), wb, last_wts);
+      } else {
+        add(int64_t(y), 4 * fields, last_wts);
+      }
     }
     s.n_ranges = merge_ranges(iv, s.r);
   }

@@ -8,6 +8,9 @@ Modes:
 ``uniform``    ids uniform over ``id_space``.
 ``zipf``       per-field Zipf(a) popularity over ``id_space`` (realistic CTR
                skew: a few hot ids, a long tail), weights uniform in (0, 1].
+
+``weights="ones"`` gives the uniform / zipf modes the reference client's
+feature weights (every one 1.0, DCNClient.java:67-73) instead.
 """
 from __future__ import annotations
 
@@ -25,9 +28,12 @@ _GOLD = np.uint64(0x9E3779B97F4A7C15)
 class SyntheticRequests:
     def __init__(self, fields: int = 43, id_space: int = 1_000_000, dist: str = "zipf", zipf_a: float = 1.1,
                  seed: int = 0, model_name: str = "DCN", signature_name: str = "serving_default",
-                 ids_key: str = "feat_ids", wts_key: str = "feat_wts"):
+                 ids_key: str = "feat_ids", wts_key: str = "feat_wts", weights: str = "uniform"):
         if dist not in ("reference", "uniform", "zipf"):
             raise ValueError(f"unknown id distribution {dist!r}")
+        if weights not in ("uniform", "ones"):
+            raise ValueError(f"unknown feature weights {weights!r}")
+        self.weights = weights
         self.F, self.space, self.dist, self.a = fields, int(id_space), dist, zipf_a
         self.rng = np.random.default_rng(seed)
         self.model_name, self.signature_name = model_name, signature_name
@@ -47,6 +53,8 @@ class SyntheticRequests:
             with np.errstate(over="ignore"):
                 h = (rank * _GOLD) ^ field_salt[None, :]
             ids = (h % np.uint64(self.space)).astype(np.int64)
+        if self.weights == "ones":
+            return ids, np.ones((rows, F), dtype=np.float32)
         wts = self.rng.random((rows, F), dtype=np.float32)
         wts = np.where(wts == 0, np.float32(1.0), wts)
         return ids, wts

@@ -152,6 +152,38 @@ def test_gather_gemm_served_steps_match_eager_forward():
         srv.stop()
 
 
+@pytest.mark.parametrize("kind", ["ones", "bf16", "mixed"])
+def test_served_weight_kinds_match_eager_forward(server, kind):
+    """Host narrowing ships all-1.0 weights as nothing and bf16-exact weights
+    as bf16 (the GPU readers widen them back, csrc/kernels/common.h
+    arena_narrow_w): scores equal the eager forward of the request's fp32
+    weights, including a 2048-row gather-GEMM batch mixing every kind."""
+    model = server.registry.resolve("DCN").model
+    live = server.registry.resolve("DCN").scheduler
+    st0 = live.stats()
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=31)
+    reqs = []
+    for i in range(12):
+        ids, wts = synth.arrays([512, 1, 100, 37, 300, 512][i % 6])
+        k = kind if kind != "mixed" else ["ones", "bf16", "f32"][i % 3]
+        if k == "ones":
+            wts = np.ones_like(wts)
+        elif k == "bf16":
+            wts = torch.from_numpy(wts).to(torch.bfloat16).float().numpy()
+        t = [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(np.ascontiguousarray(wts)))]
+        reqs.append((native().encode_predict_request("DCN", "serving_default", None, t, True), ids, wts))
+    with cf.ThreadPoolExecutor(12) as pool:
+        outs = list(pool.map(lambda r: server.service.predict_bytes(r[0], 30.0), reqs))
+    for (data, ids, wts), resp in zip(reqs, outs):
+        want = model(torch.from_numpy(ids).cuda(), torch.from_numpy(wts).cuda()).float().cpu().numpy()
+        np.testing.assert_allclose(_scores(resp), want, atol=2e-5)
+    st = live.stats()
+    if kind in ("ones", "mixed"):
+        assert st["narrowed_wts_implicit"] > st0["narrowed_wts_implicit"]
+    if kind in ("bf16", "mixed"):
+        assert st["narrowed_wts_bf16"] > st0["narrowed_wts_bf16"]
+
+
 def test_one_hot_dlrm_served_from_narrow_arena_matches_eager():
     """One-hot DLRM on the GPU live server: host-narrowed requests carry only
     the 13 dense weights, the fused bottom MLP and the fused gather +

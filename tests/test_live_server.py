@@ -329,6 +329,50 @@ def test_live_server_narrowed_ingest_matches_fp32_forward_for_every_encoding():
     live.close()
 
 
+def test_live_server_narrowed_weights_travel_in_their_cheapest_exact_form():
+    """Host narrowing picks each request's weight form: all 1.0 (the reference
+    client's requests, DCNClient.java:67-73) -> no weight bytes at all, every
+    weight exactly a bf16 value -> bf16, else fp32. Mixed in one batch, every
+    request scores exactly like the fp32 forward of its own weights, and the
+    arena carries fewer bytes for the cheaper forms."""
+    cfg = _cfg(max_rows=64, buckets=(8, 64))
+    cfg.model.vocab_size = 100_000
+    eng = _engine(cfg)
+    live = LiveScheduler(eng, cfg.serving, narrow=True)
+    synth = SyntheticRequests(fields=F, id_space=1 << 40, dist="zipf", seed=21)
+    model = eng.ex.model
+    reqs = []
+    for rows, kind in ((5, "ones"), (17, "bf16"), (9, "f32"), (30, "ones"), (3, "bf16")):
+        ids, wts = synth.arrays(rows)
+        if kind == "ones":
+            wts = np.ones_like(wts)
+        elif kind == "bf16":
+            wts = torch.from_numpy(wts).to(torch.bfloat16).float().numpy()
+        t = [("feat_ids", torch.from_numpy(ids)), ("feat_wts", torch.from_numpy(np.ascontiguousarray(wts)))]
+        reqs.append((native().encode_predict_request("DCN", "", None, t, True), ids, wts))
+    with cf.ThreadPoolExecutor(5) as pool:
+        outs = list(pool.map(lambda r: live.predict_bytes(r[0], 10.0), reqs))
+    for (raw, ids, wts), out in zip(reqs, outs):
+        want = model(torch.from_numpy(ids), torch.from_numpy(wts)).numpy()
+        np.testing.assert_allclose(_scores(out), want, atol=1e-5)
+    st = live.stats()
+    assert st["narrowed"] == 5 and st["narrowed_wts_implicit"] == 2 and st["narrowed_wts_bf16"] == 2, st
+    live.close()
+
+
+def test_weight_kind_classification():
+    """runtime/narrow.cpp classify_weights: all 1.0 -> 2 (implicit), all exact
+    bf16 -> 1, else 0 - over the columns the model reads only."""
+    vals = np.array([[1.0, 1.0, 1.0], [0.5, -2.0, 0.375]], dtype=np.float32)
+    assert native().classify_weights(torch.from_numpy(np.ones((4, 3), np.float32)), 3) == 2
+    assert native().classify_weights(torch.from_numpy(vals[1:].copy()), 3) == 1
+    assert native().classify_weights(torch.from_numpy(np.full((2, 3), 0.1, np.float32)), 3) == 0
+    # only the columns the model reads decide: a non-bf16 value beyond wcols does not matter
+    mixed = np.array([[1.0, 1.0, 0.1]], dtype=np.float32)
+    assert native().classify_weights(torch.from_numpy(mixed), 2) == 2 and native().classify_weights(
+        torch.from_numpy(mixed), 3) == 0
+
+
 def test_live_server_narrow_weight_columns_for_one_hot_dlrm():
     """One-hot DLRM reads only its 13 dense weights: host-narrowed requests
     carry just those (the arena header tells the readers), and the served
