@@ -520,7 +520,8 @@ def run_live(a, ctx, cfg, model, eng, B):
         t0 = st["steps"]
         time.sleep(0.05)
         extra["server"]["idle_steps_per_s"] = round((live.stats()["steps"] - t0) / 0.05, 1)
-    extra["ingest"] = ("host-narrowed int32 rows + fp32 weights (K0 on the submitting thread)" if live.narrow_modulo
+    extra["ingest"] = ("host-narrowed 3-byte / int32 rows + weights in their cheapest exact form (fp32, bf16, or none "
+                       "when all 1.0; K0 on the submitting thread)" if live.narrow_modulo
                        else "raw request bytes, unpacked on the GPU")
     if hasattr(model, "exchange_bytes"):  # sharded tables: the embedding exchange of one step, per rank
         extra["embedding_exchange"] = {
