@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstring>
 #include <deque>
 #include <stdexcept>
@@ -110,6 +111,12 @@ struct Conn {
   int64_t recv_unacked = 0;
   std::deque<uint32_t> blocked;  // streams waiting for window
   bool read_paused = false;      // out backlog over kMaxOutBacklog: EPOLLIN off
+  // lingering close after our GOAWAY: the GOAWAY goes out, then our write side
+  // shuts (FIN) and what the peer still sends is read and dropped until it
+  // closes or the deadline passes. Closing a socket with unread input sends an
+  // RST, which can destroy the GOAWAY in the peer's receive queue.
+  bool closing = false, shut_wr = false;
+  std::chrono::steady_clock::time_point close_by{};
   size_t backlog() const { return out.size() - out_off; }
 };
 
@@ -186,10 +193,17 @@ class Loop : public std::enable_shared_from_this<Loop> {
           if (it == conns_.end()) continue;
           Conn& c = *it->second;
           if (evs[i].events & (EPOLLERR | EPOLLHUP)) c.dead = true;
+          if (!c.dead && c.closing) {
+            if (evs[i].events & EPOLLOUT) flush(c);
+            if (!c.dead && (evs[i].events & EPOLLIN)) discard_input(c);
+            if (!c.dead) shut_when_flushed(c);
+            if (c.dead) close_conn(tag);
+            continue;
+          }
           if (!c.dead && (evs[i].events & EPOLLIN)) on_readable(c);
           if (!c.dead && (evs[i].events & EPOLLOUT)) {
             flush(c);
-            if (!c.dead && c.read_paused && c.backlog() <= kMaxOutBacklog / 2) {
+            if (!c.dead && !c.closing && c.read_paused && c.backlog() <= kMaxOutBacklog / 2) {
               // the reader caught up: resume (frames already buffered first)
               c.read_paused = false;
               update_events(c);
@@ -197,10 +211,12 @@ class Loop : public std::enable_shared_from_this<Loop> {
               if (!c.out.empty()) flush(c);
             }
           }
-          if (c.dead || (c.peer_goaway && c.streams.empty() && c.out_off == c.out.size())) close_conn(tag);
+          if (c.dead || (!c.closing && c.peer_goaway && c.streams.empty() && c.out_off == c.out.size()))
+            close_conn(tag);
         }
       }
       drain_replies();
+      reap_closing();
     }
     // graceful-ish stop: GOAWAY to every client, then close
     for (auto& kv : conns_) {
@@ -311,10 +327,44 @@ class Loop : public std::enable_shared_from_this<Loop> {
     put_u32(&c.out, c.last_sid);
     put_u32(&c.out, code);
     c.out.append(why);
+    c.closing = true;
+    c.close_by = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+    c.streams.clear();  // replies still in the handler are dropped
+    c.blocked.clear();
+    if (c.read_paused) {
+      c.read_paused = false;
+      update_events(c);
+    }
     flush(c);
-    c.dead = true;
+    if (!c.dead) shut_when_flushed(c);
     std::lock_guard<std::mutex> lk(q_mu_);
     ++st_.protocol_errors;
+  }
+
+  void shut_when_flushed(Conn& c) {
+    if (!c.shut_wr && c.out_off == c.out.size()) {
+      ::shutdown(c.fd, SHUT_WR);
+      c.shut_wr = true;
+    }
+  }
+
+  void discard_input(Conn& c) {
+    char buf[16384];
+    for (;;) {
+      const ssize_t r = ::recv(c.fd, buf, sizeof(buf), 0);
+      if (r > 0) continue;
+      if (r < 0 && errno == EINTR) continue;
+      if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) c.dead = true;
+      return;
+    }
+  }
+
+  void reap_closing() {
+    const auto now = std::chrono::steady_clock::now();
+    std::vector<uint64_t> done;
+    for (auto& kv : conns_)
+      if (kv.second->closing && now >= kv.second->close_by) done.push_back(kv.first);
+    for (uint64_t id : done) close_conn(id);
   }
 
   void rst(Conn& c, uint32_t sid, uint32_t code) {
@@ -353,7 +403,7 @@ class Loop : public std::enable_shared_from_this<Loop> {
   }
 
   void process(Conn& c) {
-    while (!c.dead) {
+    while (!c.dead && !c.closing) {
       if (c.backlog() > kMaxOutBacklog) {  // stalled reader: stop consuming its frames
         if (!c.read_paused) {
           c.read_paused = true;

@@ -351,30 +351,17 @@ class DCNv2(CTRModel):
             return ops.linear_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0=x0, xl=xl)
         return ops.cross_v2(x0, xl, layer.weight, layer.bias)
 
-    # The fp8 gather of step k+1 on the aux lane while step k's cross GEMMs run
-    # (the two-lane step program of CTRModel.build_program) measured no gain:
-    # 26.86 / 26.85 vs 27.13 / 26.99 M scores/s one-stream, interleaved
-    # (profiles/r04_session2.md) - the cross GEMMs hold every CU, so the gather
-    # only moves, it does not overlap. The hooks stay for A/B (set it True).
-    resolve_lane = False
-
-    def _resolve_applies(self, ids, wts) -> bool:
-        on_gpu = ids.arena.is_cuda if isinstance(ids, ops.ArenaRows) else ids.is_cuda
-        return (on_gpu and self.fp8 and not self.low_rank and self.cfg.num_fields <= 64
-                and ids.shape[0] >= 8192)
-
-    def _resolve(self, ids, wts):
-        x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
-        return x0, tuple(q0)
+    # (no resolve lane: the fp8 gather of step k+1 on the aux lane beside step
+    # k's cross GEMMs measured no gain, 26.86 / 26.85 vs 27.13 / 26.99 M
+    # one-stream, profiles/r04_session2.md - the cross GEMMs hold every CU;
+    # the hooks were removed in round 5)
 
     def _forward(self, ids, wts, out=None, resolved=None):
         # fp8 towers: x0 is quantised once, for the first cross layer AND the
         # first MLP layer (both read it) - by the gather itself, which holds each
         # row in one wave's registers (ops.embed_fp8; no separate quant pass)
         fp8_full = self.fp8 and not self.low_rank
-        if resolved is not None:  # gathered on the aux lane (resolve_lane)
-            x0, q0 = resolved
-        elif fp8_full and self.cfg.num_fields <= 64:
+        if fp8_full and self.cfg.num_fields <= 64:
             x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
             q0 = tuple(q0)
         else:
@@ -399,7 +386,8 @@ class DCNv2(CTRModel):
                 last = i == L - 1
                 if fused:
                     z, cross_logit = ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, xl,
-                                                        want_z=not last, head_w=self.head_wc if last else None)
+                                                        want_z=not last, head_w=self.head_wc if last else None,
+                                                        packed_w=lambda layer=layer: layer.packed("mx"))
                     if not last:
                         q, sx = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
                 else:
@@ -527,28 +515,12 @@ class DLRM(CTRModel):
         and the interaction's gather)."""
         return self.hot == 1 and self.emb is not None and self._bottom_fused()
 
-    # Step k+1's bottom MLP + gathered interaction on the aux lane while step
-    # k's top MLP runs (the two-lane program of CTRModel.build_program)
-    # measured slower: 100.2 / 100.5 vs 106.1 / 107.0 M scores/s one-stream,
-    # interleaved (profiles/r04_session2.md). The hooks stay for A/B.
-    resolve_lane = False
-
-    def _resolve_applies(self, ids, wts) -> bool:
-        arena = isinstance(ids, ops.ArenaRows)
-        on_gpu = ids.arena.is_cuda if arena else ids.is_cuda
-        return on_gpu and self.hot == 1 and self.emb is not None and ids.shape[0] >= 8192
-
-    def _resolve(self, ids, wts):
-        """Bottom MLP + the one-hot gather fused into the dot interaction: the
-        top MLP's input z."""
-        arena = isinstance(ids, ops.ArenaRows)
-        dense_out = self.bottom_out(ids if arena else wts)
-        return ops.dot_interaction_gather(dense_out, self.emb, ids if arena else self.sparse_ids(ids), self.modulo_f,
-                                          self.offset_f, self.inter_cols, id_col0=self.cfg.num_dense)
+    # (no resolve lane: step k+1's bottom MLP + gathered interaction on the
+    # aux lane beside step k's top MLP measured slower, 100.2 / 100.5 vs
+    # 106.1 / 107.0 M one-stream, profiles/r04_session2.md; hooks removed in
+    # round 5)
 
     def _forward(self, ids, wts, out=None, resolved=None):
-        if resolved is not None:  # z from the aux lane (resolve_lane)
-            return self.top.forward_head(resolved, self.head_w, self.head_b, out=out)
         arena = isinstance(ids, ops.ArenaRows)
         dense_out = self.bottom_out(ids if arena else wts)
         if self.hot == 1 and self.emb is not None and (arena or ids.is_cuda):

@@ -120,15 +120,23 @@ class Dense(nn.Module):
     def packed(self, layout: str = "16") -> torch.Tensor:
         """The weight in MFMA fragment order - "16": ops.pack_bfrag (the fused
         MLP tail's 16x16x32 B operand), "32": ops.pack_frag32 (the gather-GEMM's
-        32x32x16 A operand) - re-packed whenever the weight changed
+        32x32x16 A operand), "mx": ops.pack_mx_frag of the e4m3 copy (the
+        one-wave cross GEMM) - re-packed whenever the weight changed
         (load_state_dict bumps its version). Built by the eager warm-up that
         precedes every graph capture."""
         key = (self.weight.data_ptr(), self.weight._version)
         cache = self.__dict__.setdefault("_packed", {})
         cached = cache.get(layout)
         if cached is None or cached[0] != key:
-            w = self.weight.detach()
-            cached = (key, ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w))
+            if layout == "mx":  # the fp8 copy, MX-fp8 fragment order (cross_gemm.hip)
+                key = (self.w_fp8.data_ptr(), self.w_fp8._version)
+                cached = cache.get(layout)
+                if cached is not None and cached[0] == key:
+                    return cached[1]
+                cached = (key, ops.pack_mx_frag(self.w_fp8))
+            else:
+                w = self.weight.detach()
+                cached = (key, ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w))
             cache[layout] = cached
         return cached[1]
 
@@ -169,13 +177,17 @@ class MLP(nn.Module):
         head run as ONE kernel (ops.mlp_tail: 64-row workgroups, h2 kept in LDS,
         weights loaded in MFMA fragment order straight into registers).
         ``start``: x is already the output of layers[:start]."""
-        rest = self.layers[start:]
-        if len(rest) == 2 and x.is_cuda and xq is None and ops.mlp_tail_ok(x, rest[0], rest[1]):
-            l2, l3 = rest
+        n = len(self.layers)
+        k = start
+        while n - k > 2:  # the layers in front of the tail (DCN-v2: the fp8 first layer)
+            x = self.layers[k](x, xq if k == start else None)
+            k += 1
+        if n - k == 2 and x.is_cuda and (xq is None or k > start) and ops.mlp_tail_ok(x, *self.layers[k:]):
+            l2, l3 = self.layers[k:]
             return ops.mlp_tail(x, l2.packed(), l2.bias, l2.act, l3.packed(), l3.bias, l3.act, head_w, head_b,
                                 extra=extra, sigmoid=sigmoid, out=out)
-        for k, layer in enumerate(self.layers[start:-1], start):
-            x = layer(x, xq if k == 0 else None)
+        for j in range(k, n - 1):
+            x = self.layers[j](x, xq if j == start else None)
         last = self.layers[-1]
         if x.is_cuda and not last.fp8 and last.act in ("relu", "none") and ops.linear_head_ok(x, last.weight):
             return ops.linear_head(x, last.weight, last.bias, last.act, head_w, head_b, extra=extra, sigmoid=sigmoid,

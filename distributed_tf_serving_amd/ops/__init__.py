@@ -292,16 +292,38 @@ def cross_gemm_fits(M: int, N: int) -> bool:
     return -(-M // 256) * -(-N // 256) >= 256 and N % 8 == 0
 
 
+# cross_gemm_fp8 runs the one-wave-per-SIMD kernel (csrc/kernels/cross_gemm.hip)
+# when the caller hands it W packed in MX fragment order; False = the 8-phase form.
+# Off: bit-equal but slower so far (16384 x 2752 x 2816: 150 vs 123 us a layer,
+# tools.studies.microbench --dcn, profiles/r05_dcn_cross1w.md).
+CROSS1W = False
+
+
+def pack_mx_frag(Wq: torch.Tensor) -> torch.Tensor:
+    """e4m3 weights [N, K] -> the A-operand fragment order of
+    v_mfma_scale_f32_16x16x128_f8f6f4 (csrc/kernels/cross_gemm.hip): block
+    (n16, k128, half) is 64 lanes x 16 bytes, lane (r, q) = (l & 15, l >> 4)
+    holding row 16 n16 + r, K bytes 128 k128 + 64 half + 16 q .. +16. uint8."""
+    N, K = Wq.shape
+    if N % 16 or K % 128:
+        raise ValueError(f"pack_mx_frag needs N % 16 == 0 and K % 128 == 0, got {tuple(Wq.shape)}")
+    u = Wq.contiguous().view(torch.uint8)
+    return u.reshape(N // 16, 16, K // 128, 2, 4, 16).permute(0, 2, 3, 4, 1, 5).contiguous().view(-1)
+
+
 def cross_gemm_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
                    b: Optional[torch.Tensor], x0: torch.Tensor, xl: torch.Tensor, want_z: bool = True,
-                   head_w: Optional[torch.Tensor] = None):
+                   head_w: Optional[torch.Tensor] = None, packed_w=None):
     """One DCN-v2 cross layer in one launch (csrc/kernels/gemm.hip
     cross_staged_epilogue): y = bf16(xq Wq^T * sx * sw + b), z = bf16(x0 * y + xl).
-    Returns (z or None, dot or None) with dot = fp32 [ceil(N / 256), M] partial
-    cross logits z[:, 256 t:256 t + 256] . head_w[256 t:256 t + 256] (a head
-    ``extra``). The same rounding as linear_fp8 + cross_combine."""
+    Returns (z or None, dot or None) with dot = fp32 [tiles, M] partial cross
+    logits z[:, T t:T t + T] . head_w[T t:T t + T] (a head ``extra``; T = 256,
+    or 512 for the one-wave form). The same rounding as linear_fp8 +
+    cross_combine. ``packed_w``: a callable returning :func:`pack_mx_frag` of
+    Wq - with it (and CROSS1W) the GPU runs csrc/kernels/cross_gemm.hip."""
     if xq.is_cuda:
-        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w)
+        wp = packed_w() if packed_w is not None and CROSS1W else None
+        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w, wp)
         return (z if want_z else None), (d if head_w is not None else None)
     y = linear_fp8(xq, sx, Wq, sw, b)
     zb = (x0.float() * y.float() + xl.float()).to(torch.bfloat16)

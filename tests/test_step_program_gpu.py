@@ -192,50 +192,3 @@ def test_resolve_lane_program_engine_and_live_server(cuda, monkeypatch):
             assert (got - want).abs().max().item() < 5e-3  # 512-row forward vs rows inside a 16384-row step
     finally:
         live.close()
-
-
-def test_dcn_v2_fp8_gather_resolved_on_another_stream_is_identical(cuda):
-    """DCN-v2's resolve lane: the fp8 gather (x0 + its e4m3 copy) run on a
-    second stream and handed to the forward gives the scores of the one-stream
-    forward, bit for bit."""
-    cfg = ModelConfig(family="dcn_v2", num_fields=43, vocab_size=100_003, embed_dim=64, num_cross_layers=3,
-                      mlp_dims=(1024, 512, 256), gemm_dtype="fp8")
-    m = build_model(cfg, cuda)
-    g = torch.Generator().manual_seed(21)
-    B = 8192
-    ids = torch.randint(0, 10**9, (B, 43), generator=g).to(cuda)
-    wts = torch.rand(B, 43, generator=g).to(cuda)
-    assert m._resolve_applies(ids, wts)  # the hooks (the lane itself is off for DCN-v2: no gain)
-    assert not m._resolve_applies(ids[:4096], wts[:4096])  # small buckets keep the one-stream step
-    with torch.no_grad():
-        want = m._forward(ids, wts)
-        s = torch.cuda.Stream(cuda)
-        with torch.cuda.stream(s):
-            r = m._resolve(ids, wts)
-        torch.cuda.current_stream(cuda).wait_stream(s)
-        got = m._forward(ids, wts, resolved=r)
-    torch.cuda.synchronize()
-    assert torch.equal(got, want)
-
-
-def test_dlrm_interaction_resolved_on_another_stream_is_identical(cuda):
-    """DLRM's resolve lane: bottom MLP + gathered dot interaction run on a
-    second stream and handed to the top MLP give the one-stream scores, bit
-    for bit."""
-    cfg = _cfg()
-    m = build_model(cfg, cuda)
-    g = torch.Generator().manual_seed(23)
-    B = 8192
-    ids = torch.randint(0, 10**9, (B, cfg.num_fields), generator=g).to(cuda)
-    wts = torch.rand(B, cfg.num_fields, generator=g).to(cuda)
-    # the hooks (the lane itself is off for DLRM: slower)
-    assert m._resolve_applies(ids, wts) and not m._resolve_applies(ids[:2048], wts[:2048])
-    with torch.no_grad():
-        want = m._forward(ids, wts)
-        s = torch.cuda.Stream(cuda)
-        with torch.cuda.stream(s):
-            z = m._resolve(ids, wts)
-        torch.cuda.current_stream(cuda).wait_stream(s)
-        got = m._forward(ids, wts, resolved=z)
-    torch.cuda.synchronize()
-    assert torch.equal(got, want)

@@ -141,8 +141,14 @@ def main():
                     help="MLP tail 1024 -> 512 -> 256 -> score: GEMM2 + fused head vs the one-kernel tail")
     ap.add_argument("--serving", action="store_true",
                     help="the serving-step GEMM shapes (DeepFM 16384 rows, DCN-v2 8192 rows) vs hipBLASLt")
+    ap.add_argument("--dcn", action="store_true",
+                    help="DCN-v2 fp8: 8-phase vs one-wave cross layer, and graph-captured forwards per variant")
+    ap.add_argument("--dcn-rows", default="2048,8192,16384")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.dcn:
+        dcn_study(rows=tuple(int(x) for x in a.dcn_rows.split(",")))
+        return
     if a.serving:
         for s in ((16384, 1024, 2752), (16384, 512, 1024), (16384, 256, 512), (8192, 2752, 2752),
                   (8192, 1024, 2752)):
@@ -227,6 +233,77 @@ def tail_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
         flops = 2.0 * M * (1024 * 512 + 512 * 256)
         res["mlp_tail_tflops"] = round(flops / res["mlp_tail_us"] / 1e6, 1)
         out.append(res)
+    return out
+
+
+def dcn_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
+    """DCN-v2 fp8 (preset dcn_v2_fp8): one cross layer on the 8-phase fused
+    kernel vs the one-wave MX kernel (cross_gemm.hip), then the whole forward
+    as a captured graph with each of (CROSS1W, MLP_TAIL) on / off - interleaved
+    rounds, every variant's scores against the all-off one."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.config import load_preset
+    from distributed_tf_serving_amd.models import build_model
+
+    cfg = load_preset("dcn_v2_fp8").model
+    m = build_model(cfg, dev)
+    out = []
+    for B in rows:
+        ids_np, wts_np = SyntheticRequests(fields=cfg.num_fields, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
+        ids, wts = torch.from_numpy(ids_np).to(dev), torch.from_numpy(wts_np).to(dev)
+        # one cross layer alone (the middle one: writes z)
+        x0 = (torch.randn(B, m.d, device=dev) * 0.5).to(torch.bfloat16)
+        q, sx = ops.quant_rows_fp8(x0, ops.FP8_K_PAD)
+        layer = m.cross[1]
+        Wp = layer.packed("mx")
+
+        def c8():
+            return ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, x0, want_z=True)
+
+        def c1w():
+            return ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, x0, want_z=True,
+                                      packed_w=lambda: Wp)
+
+        z8, z1 = c8()[0], c1w()[0]
+        torch.cuda.synchronize()
+        r = {"op": "dcn_v2", "B": B, "cross_z_maxdiff": float((z8.float() - z1.float()).abs().max())}
+        tc = {"cross8": [], "cross1w": []}
+        for _ in range(rounds):
+            tc["cross8"].append(_time(c8, 20, 1))
+            tc["cross1w"].append(_time(c1w, 20, 1))
+        for k, v in tc.items():
+            r[f"{k}_us"] = round(statistics.median(v), 2)
+        flops = 2.0 * B * m.d * q.shape[1]
+        r["cross1w_tflops"] = round(flops / r["cross1w_us"] / 1e6, 1)
+        # the whole forward, captured per variant
+        graphs, ys = {}, {}
+        for c1 in (False, True):
+            for tail in (False, True):
+                ops.CROSS1W, ops.MLP_TAIL = c1, tail
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    for _ in range(2):
+                        m(ids, wts)
+                torch.cuda.current_stream().wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    y = m(ids, wts)
+                graphs[(c1, tail)], ys[(c1, tail)] = g, y
+        ops.CROSS1W, ops.MLP_TAIL = True, True
+        tg = {k: [] for k in graphs}
+        for _ in range(rounds):
+            for k, g in graphs.items():
+                tg[k].append(_time(g.replay, 20, 1))
+        torch.cuda.synchronize()
+        base = ys[(False, False)].float()
+        for (c1, tail), v in tg.items():
+            tag = f"graph_cross1w{int(c1)}_tail{int(tail)}"
+            r[f"{tag}_us"] = round(statistics.median(v), 1)
+            r[f"{tag}_maxdiff"] = float((ys[(c1, tail)].float() - base).abs().max())
+        out.append(r)
+        print(json.dumps(r), flush=True)
+        del graphs, ys
     return out
 
 
