@@ -224,7 +224,15 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
       fence();
     }
   }
+  // Retire the trailing prefetches before ANY epilogue instruction: the
+  // compiler takes an asm load's output as written when the asm ends, so the
+  // registers of the last (clamped, dead) prefetches are free to it after the
+  // loop - without the sched_barrier it hoisted epilogue address math above the
+  // wait into a W-fragment register still being loaded, a late return replaced
+  // the address and the GPU faulted (memory aperture violation, graph replays
+  // only). tests/test_kernel_resources.py runs tools/isa_hazards.py on this.
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
 
   // ---- epilogue: y = bf16(acc * sa * sw + b) staged in LDS ...

@@ -463,6 +463,9 @@ __global__ void __launch_bounds__(256, 1) gemm_gather1w_kernel(const uint8_t* __
 #undef WAIT_XS
   // the trailing (re-staged, unread) loads land before the LDS is reused / the waves exit
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // nothing of the tail above the wait: the registers of the dead trailing
+  // prefetches are free to the compiler after the loop (see cross_gemm.hip)
+  __builtin_amdgcn_sched_barrier(0);
   // Lane-derived indices of the tail are recomputed here from a volatile read
   // of the lane id (not CSE'd with the prologue's): kept live across the loop,
   // the register allocator spilled them to scratch - and a scratch-using

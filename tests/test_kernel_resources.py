@@ -21,16 +21,19 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 
 
-def _resources(src: str):
-    """{kernel symbol: {"scratch": bytes/lane, "vgprs": n, "agprs": n, "lds": bytes}}"""
-    path = os.path.join(REPO, "csrc", "kernels", src)
-    flags = []
+def _flags(path):
     with open(path) as f:
         for _, line in zip(range(60), f):
             if line.startswith("// hipcc-flags:"):
-                flags = line.split(":", 1)[1].split()
+                return line.split(":", 1)[1].split()
+    return []
+
+
+def _resources(src: str):
+    """{kernel symbol: {"scratch": bytes/lane, "vgprs": n, "agprs": n, "lds": bytes}}"""
+    path = os.path.join(REPO, "csrc", "kernels", src)
     out = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c", path,
-                          "-o", os.devnull, "-I" + os.path.join(REPO, "csrc"), *flags,
+                          "-o", os.devnull, "-I" + os.path.join(REPO, "csrc"), *_flags(path),
                           "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     res, cur = {}, None
@@ -47,12 +50,36 @@ def _resources(src: str):
     return res
 
 
-@pytest.mark.parametrize("src", ["gather_gemm.hip", "mlp_tail.hip"])
+@pytest.mark.parametrize("src", ["gather_gemm.hip", "mlp_tail.hip", "cross_gemm.hip"])
 def test_one_wave_kernels_are_scratch_free(src):
     res = _resources(src)
     assert res, f"no kernels found in {src}"
     for name, r in res.items():
         assert r.get("scratch") == 0, f"{src}: {name} spills {r.get('scratch')} bytes/lane to scratch"
+
+
+@pytest.mark.parametrize("src", ["gather_gemm.hip", "mlp_tail.hip", "cross_gemm.hip", "gemm.hip", "embedding.hip"])
+def test_inline_asm_loads_have_no_register_hazards(src, tmp_path):
+    """No instruction touches a register an inline-asm load is still filling
+    (tools/isa_hazards.py on the compiled gfx950 code): the round-5 one-wave
+    cross kernel faulted the GPU in graph replays because the compiler had put
+    epilogue address math into a register of a prefetch still in flight."""
+    import sys
+
+    sys.path.insert(0, REPO)
+    from tools import isa_hazards
+
+    path = os.path.join(REPO, "csrc", "kernels", src)
+    asm = str(tmp_path / "k.s")
+    out = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", path,
+                          "-o", asm, "-I" + os.path.join(REPO, "csrc"), *_flags(path)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    with open(asm) as f:
+        kernels = isa_hazards.parse_kernels(f.read().splitlines())
+    bad = {name: isa_hazards.check(instrs) for name, instrs in kernels.items()}
+    bad = {k: v[:3] for k, v in bad.items() if v}
+    assert not bad, bad
 
 
 def test_gather_gemm_uses_one_wave_per_simd_budget():
