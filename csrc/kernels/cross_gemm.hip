@@ -61,6 +61,40 @@ __device__ __forceinline__ f32x4 mx16(const i32x4& alo, const i32x4& ahi, const 
 
 constexpr int kCx1wBM = 128, kCx1wBN = 512;
 
+// Diagnostic build only (tools/native/cross1w_stamps.hip defines it): s_memtime
+// stamps of one K tile in the middle of the loop (top, after steps 0, 1, 2, the
+// barrier, step 3) plus entry / prologue / loop / epilogue, written by lane 0
+// of each wave at the end.
+#ifdef DTFS_CROSS1W_STAMPS
+__device__ unsigned long long g_cross1w_stamps[4096][4][10];
+__device__ unsigned long long g_cross1w_tiles[4096][4][32];  // top of every K tile (t < 32)
+#define C1_TILE()                                                                       \
+  do {                                                                                  \
+    const unsigned long long c1_now = __builtin_amdgcn_s_memtime();                     \
+    if (lane == 0 && blockIdx.x < 4096 && t < 32) g_cross1w_tiles[blockIdx.x][w][t] = c1_now; \
+  } while (0)
+#define C1_T(k)                                             \
+  do {                                                      \
+    if (t == c1_t) c1_s[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define C1_AT(k) c1_s[k] = __builtin_amdgcn_s_memtime()
+#else
+#define C1_T(k) \
+  do {          \
+  } while (0)
+#define C1_AT(k) \
+  do {           \
+  } while (0)
+#define C1_TILE() \
+  do {            \
+  } while (0)
+#endif
+// Ablations for the stamps tool only (wrong results): bit 0 drops the W
+// loads, 1 the A DMAs, 2 the LDS fragment reads, 3 the per-tile barrier.
+#ifndef CX_ABL
+#define CX_ABL 0
+#endif
+
 __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restrict__ A, int64_t lda,
                                                          const uint8_t* __restrict__ Wp, const float* __restrict__ bias,
                                                          const float* __restrict__ sa, const float* __restrict__ sw,
@@ -68,6 +102,11 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
                                                          const bf16* __restrict__ X0, const bf16* __restrict__ XL,
                                                          int64_t ldx, const float* __restrict__ hw,
                                                          float* __restrict__ dot, int64_t ldd, int M, int N, int K) {
+#ifdef DTFS_CROSS1W_STAMPS
+  unsigned long long c1_s[10] = {};
+  const int c1_t = K / 256;
+#endif
+  C1_AT(0);
   constexpr int BM = kCx1wBM, BN = kCx1wBN;
   constexpr int NS = 4;           // ring slots: tile t+1 (fragments), t+2 / t+3 (DMA in flight), t (free)
   constexpr int SLOT = BM * 128;  // 16 KiB
@@ -114,6 +153,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   i32x4 xf[8][2];
   const uint32_t xo_lo = fr * 128 + ((fq ^ (fr & 7)) << 4), xo_hi = fr * 128 + (((fq + 4) ^ (fr & 7)) << 4);
   auto read_x = [&](int u, int i) {  // 2 ops
+    if (CX_ABL & 4) return;
     const uint32_t s = ring + (u & (NS - 1)) * SLOT + 2048 * i;
     xf[i][0] = cread16<0>(s + xo_lo);
     xf[i][1] = cread16<0>(s + xo_hi);
@@ -140,8 +180,11 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   // for W(t, s) at the top of step s counts the ops issued after it: 12, 10,
   // 10, 12.
   auto vm_op = [&](int t, int g, int i) {
-    if (i < 4) load_w1(g == 3 ? t : t + 1, 2 * g + (i >> 1), i & 1);
-    else stage_a(t + 3, 2 * g + (i - 4));
+    if (i < 4) {
+      if (!(CX_ABL & 1)) load_w1(g == 3 ? t : t + 1, 2 * g + (i >> 1), i & 1);
+    } else if (!(CX_ABL & 2)) {
+      stage_a(t + 3, 2 * g + (i - 4));
+    }
   };
 
   // ---- prologue: A(0), A(1); then G0(-1), G1(-1), G2(-1) (W(0, blocks 0-5),
@@ -158,9 +201,12 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   barrier();
 #pragma unroll
   for (int i = 0; i < 6; ++i) read_x(0, i);
+  C1_AT(1);
 
 #pragma unroll 1
   for (int t = 0; t < KT; ++t) {
+    C1_T(2);
+    C1_TILE();
     // step 0 (column blocks 0, 1): fragments 6, 7 of A(t) read after pair 1
     cwait_vm4<12>(*reinterpret_cast<i32x4(*)[4]>(&wf[0][0]));
     cwait_lgkm2<10>(xf[0][0], xf[0][1]);
@@ -193,6 +239,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     cwait_lgkm2<0>(xf[7][0], xf[7][1]);
     pair(0, 7);
     fence();
+    C1_T(3);
     // step 1 (blocks 2, 3): G0(t)
     cwait_vm4<10>(*reinterpret_cast<i32x4(*)[4]>(&wf[2][0]));
 #pragma unroll
@@ -201,6 +248,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
       if (k >= 1 && k <= 6) vm_op(t, 0, k - 1);
       fence();
     }
+    C1_T(4);
     // step 2 (blocks 4, 5): G1(t)
     cwait_vm4<10>(*reinterpret_cast<i32x4(*)[4]>(&wf[4][0]));
 #pragma unroll
@@ -209,10 +257,12 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
       if (k >= 1 && k <= 6) vm_op(t, 1, k - 1);
       fence();
     }
+    C1_T(5);
     // fragments of A(t) read (6 / 7 in step 0) and A(t+1) landed for every
     // wave (this step's wait retired G1(t-2)): one barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
+    if (!(CX_ABL & 8)) barrier();
+    C1_T(6);
     // step 3 (blocks 6, 7): G2(t); fragments 0-5 of A(t+1), each two pairs
     // after its registers' last MFMA
     cwait_vm4<12>(*reinterpret_cast<i32x4(*)[4]>(&wf[6][0]));
@@ -223,7 +273,9 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
       if (k >= 1 && k <= 4) vm_op(t, 2, k - 1);
       fence();
     }
+    C1_T(7);
   }
+  C1_AT(8);
   // Retire the trailing prefetches before ANY epilogue instruction: the
   // compiler takes an asm load's output as written when the asm ends, so the
   // registers of the last (clamped, dead) prefetches are free to it after the
@@ -235,7 +287,37 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
 
-  // ---- epilogue: y = bf16(acc * sa * sw + b) staged in LDS ...
+  // ---- epilogue. Wave w owns rows w, w + 4, .. (32 of them), lane l the
+  // tile's columns 8 l .. 8 l + 7. Its x0 / xl row segments are loaded 16 rows
+  // at a time: row by row, every row waited out a whole memory round trip (the
+  // epilogue took 43 k cycles, half the K loop's 84 k -
+  // tools/native/cross1w_stamps.hip). (Loading the first batch before the y
+  // staging spills at 512 registers.)
+  int lane_e;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+  const int n = n0 + 8 * lane_e;
+  const bool col_ok = n < N;  // N % 16 == 0: a lane's 8 columns exist together
+  const int nr = min(n, N - 8);
+  const bool same = XL == X0;
+  constexpr int RB = 16;  // rows per batch (2 batches of the wave's 32)
+  bf16x8 xv[RB], lv[RB];
+  auto load_x0 = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int mc = min(m0 + w + 4 * (RB * b + i), M - 1);
+      xv[i] = *reinterpret_cast<const bf16x8*>(X0 + int64_t(mc) * ldx + nr);
+    }
+  };
+  auto load_xl = [&](int b) {
+    if (!same) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int mc = min(m0 + w + 4 * (RB * b + i), M - 1);
+        lv[i] = *reinterpret_cast<const bf16x8*>(XL + int64_t(mc) * ldx + nr);
+      }
+    }
+  };
+  // y = bf16(acc * sa * sw + b) staged in LDS
   {
     float sam[8];
 #pragma unroll
@@ -257,14 +339,8 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     }
   }
   __syncthreads();
-  // ... then z = bf16(x0 * y + xl) by whole rows: wave w owns rows w, w + 4, ..;
-  // lane l the tile's columns 8 l .. 8 l + 7
+  // ... then z = bf16(x0 * y + xl), written whole and / or dotted with hw
   {
-    int lane_e;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
-    const int n = n0 + 8 * lane_e;
-    const bool col_ok = n < N;  // N % 16 == 0: a lane's 8 columns exist together
-    const int nr = min(n, N - 8);
     float w8[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) w8[e] = 0.f;
@@ -274,28 +350,42 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) w8[e] = a[e], w8[e + 4] = b[e];
     }
-    const bool same = XL == X0;
-#pragma unroll 2
-    for (int r = w; r < BM; r += 4) {
-      const int m = m0 + r;
-      const int mc = min(m, M - 1);
-      const bf16x8 x0v = *reinterpret_cast<const bf16x8*>(X0 + int64_t(mc) * ldx + nr);
-      const bf16x8 l8 = same ? x0v : *reinterpret_cast<const bf16x8*>(XL + int64_t(mc) * ldx + nr);
-      const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(smem + r * SP + 16 * lane_e);
-      bf16x8 z8;
-      float d = 0.f;
+#pragma unroll 1
+    for (int b = 0; b < 32 / RB; ++b) {
+      load_x0(b);
+      load_xl(b);
+      float d[RB];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        z8[e] = f2bf(bf2f(x0v[e]) * bf2f(y8[e]) + bf2f(l8[e]));
-        d += bf2f(z8[e]) * w8[e];
+      for (int i = 0; i < RB; ++i) {
+        const int r = w + 4 * (RB * b + i);
+        const int m = m0 + r;
+        const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(smem + r * SP + 16 * lane_e);
+        const bf16x8 l8 = same ? xv[i] : lv[i];
+        bf16x8 z8;
+        d[i] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          z8[e] = f2bf(bf2f(xv[i][e]) * bf2f(y8[e]) + bf2f(l8[e]));
+          d[i] += bf2f(z8[e]) * w8[e];
+        }
+        if (Z && col_ok && m < M) *reinterpret_cast<bf16x8*>(Z + int64_t(m) * ldz + n) = z8;
       }
-      if (Z && col_ok && m < M) *reinterpret_cast<bf16x8*>(Z + int64_t(m) * ldz + n) = z8;
       if (dot) {
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (lane_e == 0 && m < M) dot[int64_t(tn) * ldd + m] = d;
+        for (int i = 0; i < RB; ++i) {
+          float v = d[i];
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+          const int m = m0 + w + 4 * (RB * b + i);
+          if (lane_e == 0 && m < M) dot[int64_t(tn) * ldd + m] = v;
+        }
       }
     }
+#ifdef DTFS_CROSS1W_STAMPS
+    C1_AT(9);
+    if (lane_e == 0 && blockIdx.x < 4096)
+      for (int k = 0; k < 10; ++k) g_cross1w_stamps[blockIdx.x][w][k] = c1_s[k];
+#endif
   }
 }
 
