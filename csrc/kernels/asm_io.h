@@ -59,6 +59,13 @@ __device__ __forceinline__ void lds_dma16_s(const void* sbase, uint32_t voff, ui
                : "memory", "m0");
 }
 
+// 4 bytes per lane into LDS at M0 + 4 lane: a cache-line touch with no
+// register destination (nothing for the compiler to reuse while it is in flight)
+__device__ __forceinline__ void lds_dma4_s(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ bf16x8 gload16_s(const void* sbase, uint32_t voff) {
   bf16x8 v;
   asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase));

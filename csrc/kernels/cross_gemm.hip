@@ -94,6 +94,12 @@ __device__ unsigned long long g_cross1w_tiles[4096][4][32];  // top of every K t
 #ifndef CX_ABL
 #define CX_ABL 0
 #endif
+// W touches (off): two cache-line touch loads per wave per K tile pulling the
+// wave's W fragments of tile t+3 toward the L2 while tile t runs. Measured no
+// gain (3871 vs 3801 cycles per K tile at 16384 rows, 187 vs 181 us).
+#ifndef CX_TOUCH
+#define CX_TOUCH 0
+#endif
 
 __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restrict__ A, int64_t lda,
                                                          const uint8_t* __restrict__ Wp, const float* __restrict__ bias,
@@ -152,6 +158,17 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   // ---- x fragments: row 16 i + fr, chunks fq and fq + 4 (physical ^ (row & 7))
   i32x4 xf[8][2];
   const uint32_t xo_lo = fr * 128 + ((fq ^ (fr & 7)) << 4), xo_hi = fr * 128 + (((fq + 4) ^ (fr & 7)) << 4);
+  // touch i (0, 1) of tile u: lane l -> fragment chunk l >> 2 (block j, half
+  // h), cache lines 2 (l & 3) + i of its 8; into a dead LDS corner (the
+  // epilogue's staging area, idle during the loop)
+  const uint32_t touch_off = [&] {
+    const int c = lane >> 2, jb = min(n0 / 16 + 8 * w + (c >> 1), nblk - 1);
+    return uint32_t(((jb * KT) * 2 + (c & 1)) * 1024 + ((lane & 3) * 2) * 128);
+  }();
+  const uint32_t touch_lds = ring + NS * SLOT + 256 * w;
+  auto touch_w = [&](int u, int i) {  // 1 op
+    lds_dma4_s(Wp + int64_t(min(u, KT - 1)) * 2048 + 128 * i, touch_off, touch_lds);
+  };
   auto read_x = [&](int u, int i) {  // 2 ops
     if (CX_ABL & 4) return;
     const uint32_t s = ring + (u & (NS - 1)) * SLOT + 2048 * i;
@@ -179,9 +196,13 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   // + A(t+3, k = 0, 1 / 2, 3); G3(t-1) goes out in step 0 of tile t. The wait
   // for W(t, s) at the top of step s counts the ops issued after it: 12, 10,
   // 10, 12.
+  // G2 also carries the two W touches of tile t+3 (CX_TOUCH): waits 14, 12, 12, 12.
+  constexpr int TCH = CX_TOUCH ? 2 : 0;
   auto vm_op = [&](int t, int g, int i) {
     if (i < 4) {
       if (!(CX_ABL & 1)) load_w1(g == 3 ? t : t + 1, 2 * g + (i >> 1), i & 1);
+    } else if (g == 2) {
+      if (!(CX_ABL & 1)) touch_w(t + 3, i - 4);
     } else if (!(CX_ABL & 2)) {
       stage_a(t + 3, 2 * g + (i - 4));
     }
@@ -196,8 +217,9 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
 #pragma unroll
   for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int i = 0; i < (g == 2 ? 4 : 6); ++i) vm_op(-1, g, i);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // A(0), A(1) landed (this wave's share)
+    for (int i = 0; i < (g == 2 ? 4 + TCH : 6); ++i) vm_op(-1, g, i);
+  // A(0), A(1) landed (this wave's share)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 + TCH) : "memory");
   barrier();
 #pragma unroll
   for (int i = 0; i < 6; ++i) read_x(0, i);
@@ -208,7 +230,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     C1_T(2);
     C1_TILE();
     // step 0 (column blocks 0, 1): fragments 6, 7 of A(t) read after pair 1
-    cwait_vm4<12>(*reinterpret_cast<i32x4(*)[4]>(&wf[0][0]));
+    cwait_vm4<12 + TCH>(*reinterpret_cast<i32x4(*)[4]>(&wf[0][0]));
     cwait_lgkm2<10>(xf[0][0], xf[0][1]);
     pair(0, 0);
     fence();
@@ -241,7 +263,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     fence();
     C1_T(3);
     // step 1 (blocks 2, 3): G0(t)
-    cwait_vm4<10>(*reinterpret_cast<i32x4(*)[4]>(&wf[2][0]));
+    cwait_vm4<10 + TCH>(*reinterpret_cast<i32x4(*)[4]>(&wf[2][0]));
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pair(1, k);
@@ -250,7 +272,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     }
     C1_T(4);
     // step 2 (blocks 4, 5): G1(t)
-    cwait_vm4<10>(*reinterpret_cast<i32x4(*)[4]>(&wf[4][0]));
+    cwait_vm4<10 + TCH>(*reinterpret_cast<i32x4(*)[4]>(&wf[4][0]));
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pair(2, k);
@@ -270,7 +292,7 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
     for (int k = 0; k < 8; ++k) {
       if (k >= 2) read_x(t + 1, k - 2);
       pair(3, k);
-      if (k >= 1 && k <= 4) vm_op(t, 2, k - 1);
+      if (k >= 1 && k <= 4 + TCH) vm_op(t, 2, k - 1);
       fence();
     }
     C1_T(7);
@@ -299,21 +321,22 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
   const bool col_ok = n < N;  // N % 16 == 0: a lane's 8 columns exist together
   const int nr = min(n, N - 8);
   const bool same = XL == X0;
-  constexpr int RB = 16;  // rows per batch (2 batches of the wave's 32)
-  bf16x8 xv[RB], lv[RB];
-  auto load_x0 = [&](int b) {
+  // x0 / xl rows in batches of RB, two batches in registers: batch b + 1 is
+  // loaded before batch b is computed and stored (vmcnt retires in order,
+  // stores included: loads issued behind a batch's stores would wait for them)
+  constexpr int RB = 8, NB = 32 / RB;
+  bf16x8 xv[2][RB], lv[2][RB];
+  auto load_rows = [&](int b) {
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       const int mc = min(m0 + w + 4 * (RB * b + i), M - 1);
-      xv[i] = *reinterpret_cast<const bf16x8*>(X0 + int64_t(mc) * ldx + nr);
+      xv[b & 1][i] = *reinterpret_cast<const bf16x8*>(X0 + int64_t(mc) * ldx + nr);
     }
-  };
-  auto load_xl = [&](int b) {
     if (!same) {
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         const int mc = min(m0 + w + 4 * (RB * b + i), M - 1);
-        lv[i] = *reinterpret_cast<const bf16x8*>(XL + int64_t(mc) * ldx + nr);
+        lv[b & 1][i] = *reinterpret_cast<const bf16x8*>(XL + int64_t(mc) * ldx + nr);
       }
     }
   };
@@ -350,22 +373,23 @@ __global__ void __launch_bounds__(256, 1) cross1w_kernel(const uint8_t* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) w8[e] = a[e], w8[e + 4] = b[e];
     }
-#pragma unroll 1
-    for (int b = 0; b < 32 / RB; ++b) {
-      load_x0(b);
-      load_xl(b);
+    load_rows(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b + 1 < NB) load_rows(b + 1);
       float d[RB];
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         const int r = w + 4 * (RB * b + i);
         const int m = m0 + r;
         const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(smem + r * SP + 16 * lane_e);
-        const bf16x8 l8 = same ? xv[i] : lv[i];
+        const bf16x8 x8 = xv[b & 1][i];
+        const bf16x8 l8 = same ? x8 : lv[b & 1][i];
         bf16x8 z8;
         d[i] = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          z8[e] = f2bf(bf2f(xv[i][e]) * bf2f(y8[e]) + bf2f(l8[e]));
+          z8[e] = f2bf(bf2f(x8[e]) * bf2f(y8[e]) + bf2f(l8[e]));
           d[i] += bf2f(z8[e]) * w8[e];
         }
         if (Z && col_ok && m < M) *reinterpret_cast<bf16x8*>(Z + int64_t(m) * ldz + n) = z8;
