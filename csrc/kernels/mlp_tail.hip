@@ -33,6 +33,13 @@
 namespace dtfs {
 namespace kern {
 
+// Ablations for tools/native/tail_ablate.hip only (wrong results): bit 0
+// drops GEMM2's B loads in the K loop, 1 its A DMAs, 2 the per-tile barrier,
+// 3 GEMM3 and the head.
+#ifndef TAIL_ABL
+#define TAIL_ABL 0
+#endif
+
 namespace {
 // A ring tile: 64 rows x 128 bytes, 16-byte chunk c of row r at c ^ ((r >> 1) & 7)
 __device__ __forceinline__ int tail_swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -126,11 +133,11 @@ __global__ void __launch_bounds__(512) mlp_tail_kernel(const bf16* __restrict__ 
   // iteration kt + LEAD - NS <= kt - 2, which every wave finished before the
   // barrier of iteration kt - 1 (NS >= LEAD + 2).
   auto body = [&](int kt, const bf16x8(&bc)[TJ2][2], bf16x8(&bn)[TJ2][2]) {
-    load_b2(bn, kt + 1);
-    stage_a(kt + LEAD);
+    if (!(TAIL_ABL & 1)) load_b2(bn, kt + 1);
+    if (!(TAIL_ABL & 2)) stage_a(kt + LEAD);
     static_assert(TJ2 == 4, "vmcnt below counts 1 + 2 * TJ2 + 1 = 10 ops");
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(TAIL_ABL & 4)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint8_t* as = ring + (kt % NS) * SLOT;
     bf16x8 fa[2][4];
@@ -192,6 +199,10 @@ __global__ void __launch_bounds__(512) mlp_tail_kernel(const bf16* __restrict__ 
     }
   }
   __syncthreads();
+  if (TAIL_ABL & 8) {
+    if (threadIdx.x < BM && m0 + int(threadIdx.x) < M) y[m0 + threadIdx.x] = bf2f(*reinterpret_cast<const bf16*>(h2s + threadIdx.x * H2P));
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NK2 / 2; ++t)
 #pragma unroll
