@@ -122,7 +122,9 @@ class CTRModel(nn.Module):
         if self.resolve_lane and self._resolve_applies(ids, wts):
             # (gating step k+1's resolve on step k's tower - so it runs beside the
             # head instead of GEMM2 - measured no better: 105.4 vs 106.1 / 104.0 M
-            # serial on one box, profiles/r04_session2.md)
+            # serial on one box, profiles/r04_session2.md; round 5, gated behind
+            # the one-wave gather-GEMM to run beside the fused MLP tail: 107.9 /
+            # 112.8 vs 126.1 / 126.1 M one-stream, interleaved on one box)
             def resolve():
                 st["resolved"] = self._resolve(ids, wts)
 
