@@ -292,11 +292,6 @@ def cross_gemm_fits(M: int, N: int) -> bool:
     return -(-M // 256) * -(-N // 256) >= 256 and N % 8 == 0
 
 
-# cross_gemm_fp8 runs the one-wave-per-SIMD kernel (csrc/kernels/cross_gemm.hip)
-# when the caller hands it W packed in MX fragment order; False = the 8-phase form.
-# Off: bit-equal but slower so far (16384 x 2752 x 2816: 150 vs 123 us a layer,
-# tools.studies.microbench --dcn, profiles/r05_dcn_cross1w.md).
-CROSS1W = False
 
 
 def pack_mx_frag(Wq: torch.Tensor) -> torch.Tensor:
@@ -320,9 +315,11 @@ def cross_gemm_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: tor
     logits z[:, T t:T t + T] . head_w[T t:T t + T] (a head ``extra``; T = 256,
     or 512 for the one-wave form). The same rounding as linear_fp8 +
     cross_combine. ``packed_w``: a callable returning :func:`pack_mx_frag` of
-    Wq - with it (and CROSS1W) the GPU runs csrc/kernels/cross_gemm.hip."""
+    Wq - with it the GPU runs the one-wave kernel csrc/kernels/cross_gemm.hip
+    (bit-equal, slower than the 8-phase form: the served DCN-v2 does not pass
+    it, models.ctr.DCNv2.one_wave_cross; profiles/r05_dcn_cross1w.md)."""
     if xq.is_cuda:
-        wp = packed_w() if packed_w is not None and CROSS1W else None
+        wp = packed_w() if packed_w is not None else None
         z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w, wp)
         return (z if want_z else None), (d if head_w is not None else None)
     y = linear_fp8(xq, sx, Wq, sw, b)

@@ -371,7 +371,7 @@ def test_cross_gemm_fp8_staged_epilogue(cuda, M, N, same):
 
 
 @pytest.mark.parametrize("M,N,same", [(700, 2752, False), (4100, 2752, True), (128, 512, False), (1030, 1040, True)])
-def test_cross_gemm_one_wave_form(cuda, M, N, same, monkeypatch):
+def test_cross_gemm_one_wave_form(cuda, M, N, same):
     """The one-wave-per-SIMD MX-fp8 cross layer (cross_gemm.hip: W packed in
     fragment order straight into registers, 128 x 512 tiles): z bit for bit the
     plain fp8 GEMM + cross_combine's, partial logits per 512-column tile summing
@@ -387,7 +387,6 @@ def test_cross_gemm_one_wave_form(cuda, M, N, same, monkeypatch):
     dq, dsx, dW, dsw, db, dx0, dhw = (t.to(cuda) for t in (q, sx, Wq, sw, b, x0, hw))
     dxl = dx0 if same else xl.to(cuda)
     Wp = ops.pack_mx_frag(dW)
-    monkeypatch.setattr(ops, "CROSS1W", True)
     z, d = ops.cross_gemm_fp8(dq, dsx, dW, dsw, db, dx0, dxl, want_z=True, head_w=dhw, packed_w=lambda: Wp)
     z2, d2 = ops.cross_gemm_fp8(dq, dsx, dW, dsw, db, dx0, dxl, want_z=False, head_w=dhw, packed_w=lambda: Wp)
     y = ops.linear_fp8(dq, dsx, dW, dsw, db)

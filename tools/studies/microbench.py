@@ -239,7 +239,7 @@ def tail_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
 def dcn_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
     """DCN-v2 fp8 (preset dcn_v2_fp8): one cross layer on the 8-phase fused
     kernel vs the one-wave MX kernel (cross_gemm.hip), then the whole forward
-    as a captured graph with each of (CROSS1W, MLP_TAIL) on / off - interleaved
+    as a captured graph with each of (one-wave cross kernel, MLP_TAIL) on / off - interleaved
     rounds, every variant's scores against the all-off one."""
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.config import load_preset
@@ -279,7 +279,7 @@ def dcn_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
         graphs, ys = {}, {}
         for c1 in (False, True):
             for tail in (False, True):
-                ops.CROSS1W, ops.MLP_TAIL = c1, tail
+                m.one_wave_cross, ops.MLP_TAIL = c1, tail
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
@@ -290,7 +290,7 @@ def dcn_study(rows=(2048, 8192, 16384), dev="cuda", rounds=5):
                 with torch.cuda.graph(g):
                     y = m(ids, wts)
                 graphs[(c1, tail)], ys[(c1, tail)] = g, y
-        ops.CROSS1W, ops.MLP_TAIL = True, True
+        m.one_wave_cross, ops.MLP_TAIL = False, True
         tg = {k: [] for k in graphs}
         for _ in range(rounds):
             for k, g in graphs.items():
