@@ -56,7 +56,7 @@ def parse_kernels(lines):
             in_asm = False
         line = raw.split(";")[0].rstrip()
         m = re.match(r"^([A-Za-z_.$][\w.$]*):", line)
-        if m and not line.startswith("."):
+        if m:  # a label at column 0: a kernel symbol, or a local .L / $ label
             label = m.group(1)
             if not label.startswith(".L") and not label.startswith("$"):
                 name = label
