@@ -401,6 +401,53 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const bf16* __restrict_
   }
 }
 
+// The same quantisation, each lane owning 16 consecutive columns (two 16-byte
+// loads, ONE 16-byte store of 16 e4m3 values instead of two 8-byte ones);
+// K, Kq multiples of 16, 16-byte aligned rows. Bit-equal to quant_rows_kernel.
+template <int MAXP>
+__global__ void __launch_bounds__(256) quant_rows16_kernel(const bf16* __restrict__ x, int64_t ldx, int M, int K,
+                                                           uint8_t* __restrict__ q, int64_t ldq,
+                                                           float* __restrict__ scale, int Kq) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int np = K / 16;
+  for (int p = np + lane; p < Kq / 16; p += 64) *reinterpret_cast<int4*>(q + m * ldq + p * 16) = make_int4(0, 0, 0, 0);
+  float v[MAXP][16];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXP; ++c) {
+    const int p = lane + c * 64;
+    if (p < np) {
+      const bf16x8 t0 = *reinterpret_cast<const bf16x8*>(x + m * ldx + p * 16);
+      const bf16x8 t1 = *reinterpret_cast<const bf16x8*>(x + m * ldx + p * 16 + 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[c][j] = bf2f(t0[j]);
+        v[c][j + 8] = bf2f(t1[j]);
+        amax = fmaxf(amax, fmaxf(fabsf(v[c][j]), fabsf(v[c][j + 8])));
+      }
+    }
+  }
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (lane == 0) scale[m] = s;
+#pragma unroll
+  for (int c = 0; c < MAXP; ++c) {
+    const int p = lane + c * 64;
+    if (p < np) {
+      int o[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        o[d] = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4 * d] * inv, v[c][4 * d + 1] * inv, 0, false);
+        o[d] = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4 * d + 2] * inv, v[c][4 * d + 3] * inv, o[d], true);
+      }
+      *reinterpret_cast<int4*>(q + m * ldq + p * 16) = make_int4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 // DCN-v2 cross combine, the second half of a split cross layer: the GEMM
 // writes y = xl W^T + b (plain bf16 epilogue, so the big 8-phase tile can run
 // it), then one wave per row computes z = x0 * y + xl (fp32, rounded to bf16)
@@ -603,10 +650,21 @@ hipError_t launch_quant_rows_fp8(const void* x, int64_t ldx, int M, int K, void*
   if (M == 0) return hipSuccess;
   if (Kq <= 0) Kq = K;
   if (K % 8 || Kq % 8 || Kq < K || ldq < Kq) return hipErrorInvalidValue;
-  const int chunks = (K / 8 + 63) / 64;
   dim3 grid((M + 3) / 4), block(256);
   const bf16* xi = static_cast<const bf16*>(x);
   uint8_t* qo = static_cast<uint8_t*>(q);
+  // 16 columns per lane when the rows allow 16-byte accesses: bit-equal, 21.5 vs
+  // 22.9 us at 16384 x 2752 (tools/native/quant_ab.hip)
+  const int pairs = (K / 16 + 63) / 64;
+  if (K % 16 == 0 && Kq % 16 == 0 && ldx % 8 == 0 && ldq % 16 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(q) % 16 == 0 && pairs >= 1 && pairs <= 4) {
+#define Q16_CASE(C)                                                                                       \
+  case C: hipLaunchKernelGGL(quant_rows16_kernel<C>, grid, block, 0, st, xi, ldx, M, K, qo, ldq, scale, Kq); break;
+    switch (pairs) { Q16_CASE(1) Q16_CASE(2) Q16_CASE(3) Q16_CASE(4) }
+#undef Q16_CASE
+    return hipGetLastError();
+  }
+  const int chunks = (K / 8 + 63) / 64;
 #define Q_CASE(C)                                                                                   \
   case C: hipLaunchKernelGGL(quant_rows_kernel<C>, grid, block, 0, st, xi, ldx, M, K, qo, ldq, scale, Kq); break;
   switch (chunks) {
