@@ -180,7 +180,16 @@ def main():
             be.close()
             res["grpc_max_diff"] = max(gd)
     dist.barrier(group=phase)  # every front door is done: the cluster is idle now
+    # let the last step's bookkeeping land (a rank that joined a peer's final
+    # step may count it a moment after that peer's front door answered; under
+    # a loaded CPU that moment can exceed the window below)
     st0 = srv.sched.stats()["steps"]
+    for _ in range(40):
+        time.sleep(0.05)
+        st1 = srv.sched.stats()["steps"]
+        if st1 == st0:
+            break
+        st0 = st1
     time.sleep(0.3)
     res["idle_steps"] = srv.sched.stats()["steps"] - st0
     res["stats"] = {k: v for k, v in srv.sched.stats().items() if isinstance(v, (int, float))}
