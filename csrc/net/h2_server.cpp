@@ -201,21 +201,13 @@ class Loop : public std::enable_shared_from_this<Loop> {
             continue;
           }
           if (!c.dead && (evs[i].events & EPOLLIN)) on_readable(c);
-          if (!c.dead && (evs[i].events & EPOLLOUT)) {
-            flush(c);
-            if (!c.dead && !c.closing && c.read_paused && c.backlog() <= kMaxOutBacklog / 2) {
-              // the reader caught up: resume (frames already buffered first)
-              c.read_paused = false;
-              update_events(c);
-              process(c);
-              if (!c.out.empty()) flush(c);
-            }
-          }
+          if (!c.dead && (evs[i].events & EPOLLOUT)) flush(c);
           if (c.dead || (!c.closing && c.peer_goaway && c.streams.empty() && c.out_off == c.out.size()))
             close_conn(tag);
         }
       }
       drain_replies();
+      resume_paused();
       reap_closing();
     }
     // graceful-ish stop: GOAWAY to every client, then close
@@ -320,6 +312,36 @@ class Loop : public std::enable_shared_from_this<Loop> {
       }
       set_write_interest(c, true);
     }
+    // Every flush, from whichever call site (readiness, drain_replies, goaway):
+    // a closing connection sends its FIN once the GOAWAY is out, and a
+    // connection whose reads were paused resumes once the reader caught up.
+    // Resuming only from the EPOLLOUT branch hung a connection whose backlog
+    // drained inside drain_replies (no EPOLLIN, no EPOLLOUT interest left).
+    if (c.closing) {
+      shut_when_flushed(c);
+    } else if (c.read_paused && c.backlog() <= kMaxOutBacklog / 2) {
+      c.read_paused = false;
+      update_events(c);
+      resume_.push_back(c.id);  // frames already buffered: processed by resume_paused()
+    }
+  }
+
+  // Connections whose reads resumed: parse the frames they buffered while
+  // paused (outside flush(), which process() paths call).
+  void resume_paused() {
+    while (!resume_.empty()) {
+      std::vector<uint64_t> ids;
+      ids.swap(resume_);
+      for (uint64_t id : ids) {
+        auto it = conns_.find(id);
+        if (it == conns_.end()) continue;
+        Conn& c = *it->second;
+        if (c.dead || c.closing || c.read_paused) continue;
+        process(c);
+        if (!c.dead && !c.out.empty()) flush(c);
+        if (c.dead) close_conn(id);
+      }
+    }
   }
 
   void goaway(Conn& c, uint32_t code, const std::string& why) {
@@ -329,6 +351,7 @@ class Loop : public std::enable_shared_from_this<Loop> {
     c.out.append(why);
     c.closing = true;
     c.close_by = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+    closing_.push_back(c.id);
     c.streams.clear();  // replies still in the handler are dropped
     c.blocked.clear();
     if (c.read_paused) {
@@ -359,12 +382,22 @@ class Loop : public std::enable_shared_from_this<Loop> {
     }
   }
 
+  // Lingering closes past their deadline (only the connections in closing_,
+  // not every connection on every loop iteration).
   void reap_closing() {
+    if (closing_.empty()) return;
     const auto now = std::chrono::steady_clock::now();
-    std::vector<uint64_t> done;
-    for (auto& kv : conns_)
-      if (kv.second->closing && now >= kv.second->close_by) done.push_back(kv.first);
-    for (uint64_t id : done) close_conn(id);
+    size_t keep = 0;
+    for (uint64_t id : closing_) {
+      auto it = conns_.find(id);
+      if (it == conns_.end()) continue;  // closed already
+      if (now >= it->second->close_by) {
+        close_conn(id);
+      } else {
+        closing_[keep++] = id;
+      }
+    }
+    closing_.resize(keep);
   }
 
   void rst(Conn& c, uint32_t sid, uint32_t code) {
@@ -753,6 +786,8 @@ class Loop : public std::enable_shared_from_this<Loop> {
   int lfd_, ep_ = -1, efd_ = -1;
   uint64_t next_id_;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
+  std::vector<uint64_t> resume_;   // reads resumed in flush(): buffered frames to process
+  std::vector<uint64_t> closing_;  // lingering closes (GOAWAY sent), reaped at close_by
   mutable std::mutex q_mu_;
   std::vector<Posted> q_;
   bool stop_ = false;

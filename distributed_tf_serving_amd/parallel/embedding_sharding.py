@@ -303,6 +303,18 @@ class ShardedEmbedding(nn.Module):
         # where table t of (local candidate) b lands after the exchange, per bucket B
         self._maps: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 
+    def release_peers(self) -> None:
+        """Unmap the other ranks' stores (GPU: closes their IPC mappings now;
+        CPU: drops the shared-memory views). The device is drained first so no
+        kernel still reads them; the lookup cannot run afterwards."""
+        p = self.peer
+        if p is None or self.world == 1 or getattr(self, "peers_released", False):
+            return
+        if self.store.is_cuda:
+            torch.cuda.synchronize(self.store.device)
+        p.stores = [chunks if r == self.rank else [] for r, chunks in enumerate(p.stores)]
+        self.peers_released = True
+
     def local_bytes(self) -> int:
         return sum(c.numel() * c.element_size() for c in [self.store, *self.store_chunks])
 
@@ -524,6 +536,14 @@ class ShardedDLRM(nn.Module):
     def stop_cache(self) -> None:
         if self.emb.cache is not None:
             self.emb.cache.stop()
+
+    def release(self) -> None:
+        """Shutdown, once no step can run any more (the live server drained):
+        stop the replica-cache refresher and unmap every peer's store here, in
+        program order, instead of from interpreter-teardown deleters racing a
+        still-running refresher (the round-5 SIGABRT at cluster exit)."""
+        self.stop_cache()
+        self.emb.release_peers()
 
     def narrow_weight_cols(self) -> int:
         """One-hot: only the dense features' weights are read (the request

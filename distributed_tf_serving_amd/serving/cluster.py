@@ -350,9 +350,15 @@ class ClusterServer:
         if self.ctl is not None and self.rank == 0:
             self.ctl.request_stop()  # followers close their live servers too
         if self.registry is not None:
-            self.registry.close()  # drains this rank's live server: every launched step completes
+            # drains this rank's live server (every launched step completes),
+            # then stops the replica-cache refresher and unmaps the peers'
+            # stores (LiveScheduler.close -> ShardedDLRM.release)
+            self.registry.close()
         elif self.sched is not None:
             self.sched.close()
+        wd = getattr(self, "_watchdog", None)
+        if wd is not None and wd is not threading.current_thread():
+            wd.join(timeout=10)
 
 
 def main(argv=None):

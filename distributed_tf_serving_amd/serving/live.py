@@ -235,4 +235,7 @@ class LiveScheduler:
         return bool(self.srv.broken)
 
     def close(self) -> None:
-        self.srv.close()
+        self.srv.close()  # every launched step has completed
+        release = getattr(self.eng.ex.model, "release", None)
+        if release is not None:  # replica-cache refresher + IPC-mapped peer stores
+            release()

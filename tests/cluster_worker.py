@@ -14,6 +14,7 @@ import faulthandler
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -200,13 +201,21 @@ def main():
         res["followed"] = srv.serve_follower()
         srv.stop()
     res["broken"] = bool(srv.broken)
+    # stop() joins the watchdog and the replica-cache refresher: nothing of the
+    # server may still run (and touch peer memory) while the process exits
+    res["threads_after_stop"] = [t.name for t in threading.enumerate() if t.name.startswith("dtfs-")]
     with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.barrier(group=phase)
 
 
 if __name__ == "__main__":
-    faulthandler.enable()  # a native abort (SIGABRT / SIGSEGV) still names the Python frame it hit
+    _out = next((sys.argv[i + 1] for i, x in enumerate(sys.argv[:-1]) if x == "--out"), None)
+    # a native abort (SIGABRT / SIGSEGV) still names the Python frame of every
+    # thread: into rank<r>.fault, where the test reads it (torchrun's failure
+    # summary keeps only the signal)
+    _fault = open(os.path.join(_out, f"rank{os.environ.get('RANK', '?')}.fault"), "w") if _out else sys.stderr
+    faulthandler.enable(file=_fault, all_threads=True)
     try:
         main()
     except BaseException:

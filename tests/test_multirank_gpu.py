@@ -22,6 +22,18 @@ def _port():
         return s.getsockname()[1]
 
 
+def _rank_errors(out) -> dict:
+    """What tests/cluster_worker.py left behind on failure: each rank's Python
+    traceback (rank<r>.err) and its faulthandler dump of every thread on a
+    native abort (rank<r>.fault, empty when the rank exited cleanly)."""
+    errs = {}
+    for f in sorted(out.glob("rank*.err")) + sorted(out.glob("rank*.fault")):
+        txt = f.read_text()
+        if txt.strip():
+            errs[f.name] = txt[-3000:]
+    return errs
+
+
 @pytest.mark.parametrize("n,mode,peer,scatter_path", [
     (2, "alltoall", 0, "shared"), (3, "alltoall", 0, "shared"), (2, "scatter", 0, "shared"),
     (3, "scatter", 0, "shared"), (2, "scatter", 0, "rccl"), (2, "local", 0, "shared"),
@@ -148,7 +160,7 @@ def test_native_cluster_server_ranks_sharing_one_gpu(tmp_path, n, mode):
            "--mode", mode, "--out", str(tmp_path), "--grpc-port", str(_port())]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
-    errs = {f.name: f.read_text()[-3000:] for f in sorted(tmp_path.glob("rank*.err"))}
+    errs = _rank_errors(tmp_path)
     assert p.returncode == 0, (errs, p.stdout[-2000:], p.stderr[-2000:])
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
     fronts = [r for r in res if r["serves"]]
@@ -194,13 +206,14 @@ def test_local_cluster_sharded_dlrm_ranks_sharing_one_gpu(tmp_path, n):
            "--mode", "local", "--preset", "dlrm", "--out", str(tmp_path), "--grpc-port", str(_port())]
     env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
-    errs = {f.name: f.read_text()[-3000:] for f in sorted(tmp_path.glob("rank*.err"))}
+    errs = _rank_errors(tmp_path)
     written = sorted(f.name for f in tmp_path.glob("rank*.json"))  # how far the ranks got
     assert p.returncode == 0, (errs, written, p.stdout[-2000:], p.stderr[-4000:])
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
     for r in res:
         assert r["serves"] and r["max_diff"] < 1e-3 and r["grpc_max_diff"] < 1e-3, r
         assert r["idle_steps"] == 0 and not r["broken"], r
+        assert r["threads_after_stop"] == [], r["threads_after_stop"]
 
 
 def test_local_cluster_dead_table_owner_sharing_one_gpu(tmp_path):

@@ -387,6 +387,55 @@ def test_reader_that_never_reads_is_paused_not_buffered(front):
     ch.close()
 
 
+def test_paused_reader_resumes_on_the_same_connection(front):
+    # a connection paused for its 16 MiB reply backlog must resume
+    # reading once the client drains its socket, whichever flush emptied the
+    # backlog - its next PING on the SAME connection is answered
+    import socket
+
+    srv, fr = front
+    s = _raw_conn(fr.port)
+    s.setblocking(False)
+    ping = _frame(6, 0, 0, b"12345678") * 4096
+    before = fr.stats()["paused_reads"]
+    off, t0 = 0, time.time()
+    while time.time() - t0 < 20 and fr.stats()["paused_reads"] == before:
+        try:
+            off = (off + s.send(ping[off:])) % len(ping)
+        except (BlockingIOError, socket.timeout):
+            time.sleep(0.01)
+    assert fr.stats()["paused_reads"] > before, "never paused"
+    # drain every reply (frame-aligned) while finishing the partial PING frame,
+    # then ask once more on the same connection
+    tail = ping[off:] if off else b""
+    buf, drained, asked, got = b"", 0, False, False
+    t0 = time.time()
+    while time.time() - t0 < 40 and not got:
+        try:
+            chunk = s.recv(1 << 20)
+            if not chunk:
+                break
+            buf += chunk
+            drained += len(chunk)
+        except BlockingIOError:
+            time.sleep(0.002)
+        while len(buf) >= 9 and len(buf) >= 9 + int.from_bytes(buf[:3], "big"):
+            n = int.from_bytes(buf[:3], "big")
+            if buf[3] == 6 and buf[4] & 1 and buf[9:9 + n] == b"resumed!":
+                got = True
+            buf = buf[9 + n:]
+        if tail:
+            try:
+                tail = tail[s.send(tail):]
+            except BlockingIOError:
+                pass
+        elif not asked and drained > (8 << 20):
+            s.send(_frame(6, 0, 0, b"resumed!"))  # 17 bytes: fits the drained socket buffer
+            asked = True
+    s.close()
+    assert asked and got, (asked, drained, "no PING ACK after the reader drained: reads never resumed")
+
+
 def test_full_batching_queue_does_not_block_the_event_loop():
     # every arena queued behind a paused server: deadline-less Predicts must not
     # stall the loop thread - a PING on another connection of the same (only)
