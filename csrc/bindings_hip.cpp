@@ -1165,6 +1165,73 @@ torch::Tensor mlp_tail(torch::Tensor X, torch::Tensor W2p, torch::Tensor b2, int
   return y;
 }
 
+// K1 + K2 + K4 x 3 + K6: the whole DeepFM / Wide&Deep tower after the resolve
+// pass in one launch (gather_mlp.hip): 64 rows x all 1024 h1 columns per
+// workgroup, h1 / h2 kept in LDS. W1p / W2p / W3p: ops.pack_frag32 of the three
+// weights. ``fm``: add the second-order FM term of each row (DeepFM). Returns the
+// scores (fp32 [B], or ``out``: device or pinned host memory).
+torch::Tensor gather_mlp(torch::Tensor table, c10::optional<torch::Tensor> lin, c10::optional<torch::Tensor> arena,
+                         c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts, int64_t B, int64_t F,
+                         int64_t modulo, double bias, torch::Tensor W1p, torch::Tensor b1, torch::Tensor W2p,
+                         torch::Tensor b2, int64_t act2, torch::Tensor W3p, torch::Tensor b3, int64_t act3,
+                         torch::Tensor hw, double hbias, bool fm, bool sigmoid,
+                         c10::optional<std::vector<torch::Tensor>> resolved, c10::optional<torch::Tensor> out) {
+  check_dev(table, "table");
+  for (auto* t : {&W1p, &b1, &W2p, &b2, &W3p, &b3, &hw}) {
+    check_dev(*t, "gather_mlp operand");
+    check_same_dev(table, *t, "gather_mlp operand");
+  }
+  TORCH_CHECK(table.scalar_type() == torch::kBFloat16 && table.dim() == 2 && table.size(1) == 64 &&
+                  table.is_contiguous(),
+              "gather_mlp: table must be contiguous bf16 [V, 64]");
+  const int64_t V = table.size(0);
+  TORCH_CHECK(F >= 1 && F <= 64, "gather_mlp handles 1..64 fields");
+  TORCH_CHECK(modulo > 0 && modulo <= V, "modulo must be in (0, table rows]");
+  for (auto* t : {&W1p, &W2p, &W3p})
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->is_contiguous(), "W1p / W2p / W3p: contiguous bf16 (pack_frag32)");
+  TORCH_CHECK(b1.scalar_type() == torch::kFloat32 && b1.numel() == 1024 && b2.scalar_type() == torch::kFloat32 &&
+                  b2.numel() == 512 && b3.scalar_type() == torch::kFloat32 && b3.numel() == 256 &&
+                  hw.scalar_type() == torch::kFloat32 && hw.numel() == 256,
+              "gather_mlp covers 64F -> 1024 -> 512 -> 256 -> 1 (fp32 biases / head weights)");
+  TORCH_CHECK(W1p.numel() == 1024 * 64 * F && W2p.numel() == 512 * 1024 && W3p.numel() == 256 * 512,
+              "packed weight sizes");
+  TORCH_CHECK((act2 == 0 || act2 == 1) && (act3 == 0 || act3 == 1), "act must be 0 (none) or 1 (relu)");
+  if (lin) {
+    check_dev(*lin, "lin");
+    TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
+  }
+  TORCH_CHECK(dtfs::gather_mlp_ok((B + 255) / 256 * 256, 1024, int(64 * F), 512, 256, int(F), V),
+              "gather_mlp: shape outside the kernel's range");
+  dtfs::EmbedArgs a;
+  embed_gemm_inputs(table, arena, ids, wts, B, F, a);
+  c10::DeviceGuard g(table.device());
+  const int64_t Mp = (B + 255) / 256 * 256;
+  const int64_t n_parts = fm ? 2 : 1;  // the resolve pass's shape (row 1 unused here)
+  std::vector<torch::Tensor> r;
+  if (resolved) {
+    r = *resolved;
+    TORCH_CHECK(r.size() == 3, "resolved = (rows_t, wts_t, parts)");
+    TORCH_CHECK(r[0].scalar_type() == torch::kInt32 && r[0].dim() == 2 && r[0].size(0) == F && r[0].size(1) == Mp &&
+                    r[0].is_contiguous() && r[1].scalar_type() == torch::kFloat32 && r[1].sizes() == r[0].sizes() &&
+                    r[1].is_contiguous() && r[2].scalar_type() == torch::kFloat32 && r[2].dim() == 2 &&
+                    r[2].size(1) == Mp && r[2].is_contiguous(),
+                "resolved tensors do not match this gather_mlp's shape");
+    for (const auto& t : r) check_same_dev(table, t, "resolved");
+  } else {
+    r = embed_gemm_resolve_into(table, lin, a, B, F, modulo, bias, n_parts);
+  }
+  torch::Tensor y;
+  float* yp = score_out(table, B, out, y);
+  if (B == 0) return y;
+  check_hip(dtfs::launch_gather_mlp(table.data_ptr(), V, r[0].data_ptr<int32_t>(), r[1].data_ptr<float>(), Mp, int(F),
+                                    W1p.data_ptr(), b1.data_ptr<float>(), W2p.data_ptr(), b2.data_ptr<float>(),
+                                    int(act2), W3p.data_ptr(), b3.data_ptr<float>(), int(act3), hw.data_ptr<float>(),
+                                    float(hbias), r[2].data_ptr<float>(), fm, int(B), sigmoid ? 2 : 0, yp,
+                                    cur_stream(table)),
+            "gather_mlp");
+  return y;
+}
+
 // ---------------------------------------------------------------- K0 ingest
 void unpack_arena(torch::Tensor arena, torch::Tensor packed, int64_t fields, int64_t narrow_modulo) {
   check_dev(arena, "arena");
@@ -1752,6 +1819,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mlp_tail", &mlp_tail, py::arg("X"), py::arg("W2p"), py::arg("b2"), py::arg("act2"), py::arg("W3p"),
         py::arg("b3"), py::arg("act3"), py::arg("hw"), py::arg("hbias") = 0.0, py::arg("extra") = py::none(),
         py::arg("sigmoid") = true, py::arg("out") = py::none());
+  m.def("gather_mlp", &gather_mlp, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"),
+        py::arg("wts"), py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W1p"), py::arg("b1"),
+        py::arg("W2p"), py::arg("b2"), py::arg("act2"), py::arg("W3p"), py::arg("b3"), py::arg("act3"), py::arg("hw"),
+        py::arg("hbias"), py::arg("fm"), py::arg("sigmoid") = true, py::arg("resolved") = py::none(),
+        py::arg("out") = py::none(),
+        "DeepFM / Wide&Deep tower in one launch: gather + FM + 3 MLP layers + head (gather_mlp.hip)");
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");

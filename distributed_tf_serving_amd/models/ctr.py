@@ -99,6 +99,17 @@ class CTRModel(nn.Module):
                 and first.act in ("relu", "none") and first.k == first.in_dim
                 and ops.embed_gemm_ok(self.emb, first.weight, int(ids.shape[0]), fm2))
 
+    def _gather_mlp(self, ids, wts, fm2: bool) -> bool:
+        """The whole tower runs as ONE kernel (ops.gather_mlp: gather + FM + the
+        three MLP layers + head, h1 / h2 in LDS): the gather-GEMM applies and
+        the tower is 64F -> 1024 -> 512 -> 256 on a batch that fills the GPU."""
+        return (self.use_gather_mlp and self._gather_gemm(ids, wts, fm2)
+                and ops.gather_mlp_ok(self.emb, self.mlp.layers, int(ids.shape[0])))
+
+    # module-level A/B switch for studies (tools/studies): False keeps the
+    # two-kernel form (gather-GEMM + MLP tail)
+    use_gather_mlp = True
+
     def _resolve_applies(self, ids, wts) -> bool:
         """The step runs the gather-GEMM (so its resolve pass can move to the aux lane)."""
         return False
@@ -182,6 +193,9 @@ class WideDeep(CTRModel):
         return h, wide, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):
+        if self._gather_mlp(ids, wts, fm2=False):  # the whole tower in one launch
+            return ops.gather_mlp(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, self.mlp.layers,
+                                  self.head_w, self.head_b, fm=False, resolved=resolved, out=out)
         if self._gather_gemm(ids, wts, fm2=False):
             h, wide, hw, hb = self._gg_front(ids, wts, resolved)
             return self.mlp.forward_head(h, hw, hb, extra=wide, out=out, start=1)
@@ -225,6 +239,9 @@ class DeepFM(CTRModel):
         return h, fm, self.head_w, self.head_b
 
     def _forward(self, ids, wts, out=None, resolved=None):
+        if self._gather_mlp(ids, wts, fm2=True):  # the whole tower in one launch
+            return ops.gather_mlp(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, self.mlp.layers,
+                                  self.head_w, self.head_b, fm=True, resolved=resolved, out=out)
         if self._gather_gemm(ids, wts, fm2=True):
             h, fm, hw, hb = self._gg_front(ids, wts, resolved)
             return self.mlp.forward_head(h, hw, hb, extra=fm, out=out, start=1)

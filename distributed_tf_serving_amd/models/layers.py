@@ -133,10 +133,17 @@ class Dense(nn.Module):
                 cached = cache.get(layout)
                 if cached is not None and cached[0] == key:
                     return cached[1]
-                cached = (key, ops.pack_mx_frag(self.w_fp8))
+                fresh = ops.pack_mx_frag(self.w_fp8)
             else:
                 w = self.weight.detach()
-                cached = (key, ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w))
+                fresh = ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w)
+            if cached is not None and cached[1].shape == fresh.shape and cached[1].dtype == fresh.dtype:
+                # a weight changed in place: re-pack INTO the buffer captured HIP
+                # graphs already read (a new allocation would leave them serving
+                # the old weights)
+                cached[1].copy_(fresh)
+                fresh = cached[1]
+            cached = (key, fresh)
             cache[layout] = cached
         return cached[1]
 

@@ -762,6 +762,44 @@ def mlp_tail(x: torch.Tensor, W2p: torch.Tensor, b2: torch.Tensor, act2: str, W3
     return hip().mlp_tail(x, W2p, b2, _ACTS[act2], W3p, b3, _ACTS[act3], hw, float(hbias), extra, sigmoid, out)
 
 
+# The whole DeepFM / Wide&Deep tower as one kernel (gather_mlp.hip) at or above
+# this many rows (16384 rows = one 64-row workgroup per CU).
+GATHER_MLP_MIN_ROWS = 8192
+
+
+def gather_mlp_ok(table: torch.Tensor, layers, rows: int) -> bool:
+    """Shapes the one-launch tower covers: bf16 64-wide table of <= 2^25 rows,
+    bf16 layers 64F -> 1024 (ReLU) -> 512 -> 256, enough rows to fill the GPU."""
+    if len(layers) != 3 or rows < GATHER_MLP_MIN_ROWS:
+        return False
+    l1, l2, l3 = layers
+    return (table.is_cuda and table.dtype == torch.bfloat16 and table.dim() == 2 and table.shape[1] == 64
+            and table.shape[0] <= 2 ** 25 and not any(l.fp8 for l in layers)
+            and tuple(l1.weight.shape) == (1024, l1.in_dim) and l1.k == l1.in_dim and l1.in_dim % 64 == 0
+            and 1 <= l1.in_dim // 64 <= 64 and tuple(l2.weight.shape) == (512, 1024)
+            and tuple(l3.weight.shape) == (256, 512) and l1.act == "relu" and l2.act in ("relu", "none")
+            and l3.act in ("relu", "none"))
+
+
+def gather_mlp(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
+               bias: float, layers, hw: torch.Tensor, hbias: float, fm: bool, sigmoid: bool = True,
+               resolved=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K1 + K2 + K4 x 3 + K6 in one launch (GPU): the scores of a DeepFM
+    (``fm``) or Wide&Deep tower, out_act(mlp(x) . hw + hbias + first-order
+    (+ FM)), x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)). h1 and h2 stay in
+    the CU's LDS (csrc/kernels/gather_mlp.hip). ``resolved``: the front half
+    from :func:`embed_gemm_resolve`; ``out``: device or pinned host scores."""
+    l1, l2, l3 = layers
+    m = int(modulo) if modulo > 0 else table.shape[0]
+    args = (l1.packed("32"), l1.bias, l2.packed("32"), l2.bias, _ACTS[l2.act], l3.packed("32"), l3.bias,
+            _ACTS[l3.act], hw, float(hbias), bool(fm), bool(sigmoid), list(resolved) if resolved is not None else None,
+            out)
+    if isinstance(ids, ArenaRows):
+        return hip().gather_mlp(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias), *args)
+    return hip().gather_mlp(table, lin, None, _rows(ids), None if wts is None else _rows(wts), int(ids.shape[0]),
+                            int(ids.shape[1]), m, float(bias), *args)
+
+
 def unpack_bfrag(Wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
     """Inverse of :func:`pack_bfrag` (tests)."""
     return Wp.reshape(N // 16, K // 64, 2, 4, 16, 8).permute(0, 4, 1, 2, 3, 5).reshape(N, K)

@@ -897,6 +897,85 @@ def test_gather_gemm_one_wave_form(cuda, B, F, N, fm2):
     _close(parts[:, :B].sum(0), p8[:, :B].sum(0), 1e-5, 1e-5, "one-wave vs 8-phase FM partials")
 
 
+class _Layer:
+    """The attributes ops.gather_mlp reads off a models.layers.Dense."""
+
+    def __init__(self, W, b, act):
+        self.weight, self.bias, self.act, self.fp8 = W, b, act, False
+        self.in_dim = self.k = W.shape[1]
+
+    def packed(self, layout):
+        assert layout == "32"
+        return ops.pack_frag32(self.weight)
+
+
+@pytest.mark.parametrize("B,F,fm,act3", [(8192, 43, True, "relu"), (16421, 43, True, "none"),
+                                          (16384, 43, False, "relu"), (9000, 7, True, "relu"),
+                                          (8192, 1, False, "none"), (8300, 64, True, "relu")])
+def test_gather_mlp_tower_vs_fp32(cuda, B, F, fm, act3):
+    """The whole DeepFM / Wide&Deep tower in one launch (gather_mlp.hip: 64 rows
+    x all 1024 h1 columns per workgroup, h1 / h2 in LDS) vs the fp32 torch math
+    (h1 and h2 rounded to bf16 like every GPU path), over field counts below /
+    above the rings' depths and row counts that are not a multiple of 64; and
+    vs the two-kernel form it replaces (one-wave gather-GEMM + MLP tail)."""
+    V, bias = 30_000, -0.25
+    table, lin, W1, b1, ids, wts = _gather_gemm_case(B, F=F, V=V, N=1024, seed=B + F)
+    g = torch.Generator().manual_seed(B * 7 + F)
+    W2 = (torch.randn(512, 1024, generator=g) / 32).to(torch.bfloat16)
+    W3 = (torch.randn(256, 512, generator=g) / 512 ** 0.5).to(torch.bfloat16)
+    b2, b3 = torch.randn(512, generator=g) * 0.1, torch.randn(256, generator=g) * 0.1
+    hw = torch.randn(256, generator=g) * 0.05
+    d = [t.to(cuda) for t in (table, lin, W1, b1, ids, wts, W2, b2, W3, b3, hw)]
+    layers = [_Layer(d[2], d[3], "relu"), _Layer(d[6], d[7], "relu"), _Layer(d[8], d[9], act3)]
+    assert ops.gather_mlp_ok(d[0], layers, B)
+    y = ops.gather_mlp(d[0], d[4], d[5], d[1], V, bias, layers, d[10], 0.2, fm=fm)
+    h1, first = _gather_gemm_ref(table, lin, W1, b1, ids, wts, V, bias, fm)
+    ref = _mlp_tail_ref(h1.to(torch.bfloat16), W2, b2, "relu", W3, b3, act3, hw, 0.2, first, True)
+    # h1 / h2 are bf16: a ReLU / rounding boundary flip moves a logit by ~1e-3
+    _close(y, ref, 2e-3, 2e-3, f"gather_mlp {B} x {F} fm={fm} vs fp32")
+    h, parts = ops.embed_gemm(d[0], d[4], d[5], d[1], V, bias, d[2], d[3], "relu", fm2=fm,
+                              packed_w=lambda: ops.pack_frag32(d[2]))
+    y2 = ops.mlp_tail(h, ops.pack_bfrag(d[6]), d[7], "relu", ops.pack_bfrag(d[8]), d[9], act3, d[10], 0.2, parts, True)
+    _close(y, y2, 2e-3, 2e-3, "gather_mlp vs gather-GEMM + MLP tail")
+    # the resolve pass done earlier (another lane) and scores into pinned host memory
+    r = ops.embed_gemm_resolve(d[0], d[4], d[5], d[1], V, bias, fm)
+    out = torch.zeros(B, dtype=torch.float32).pin_memory()
+    y3 = ops.gather_mlp(d[0], d[4], d[5], d[1], V, bias, layers, d[10], 0.2, fm=fm, resolved=r, out=out)
+    torch.cuda.synchronize()
+    assert y3.data_ptr() == out.data_ptr()
+    _close(out, y, 0, 0, "resolved + pinned out vs one call")
+
+
+def test_gather_mlp_model_path_and_weight_update(cuda):
+    """DeepFM / Wide&Deep at a GPU-filling batch take the one-launch tower; the
+    scores equal the two-kernel form's, and an in-place weight update reaches
+    the packed copy the kernel (and any captured graph) reads."""
+    for family in ("deepfm", "wdl"):
+        m = build_model(ModelConfig(family=family, vocab_size=20000), cuda)
+        ids = torch.randint(0, 1 << 40, (16384, 43)).to(cuda)
+        wts = torch.rand(16384, 43).to(cuda)
+        assert m._gather_mlp(ids, wts, fm2=family == "deepfm")
+        y = m(ids, wts)
+        try:
+            type(m).use_gather_mlp = False
+            want = m(ids, wts)
+        finally:
+            type(m).use_gather_mlp = True
+        _close(y, want, 2e-3, 2e-3, f"{family}: gather_mlp vs two kernels")
+        l2 = m.mlp.layers[1]
+        packed = l2.packed("32")
+        with torch.no_grad():
+            l2.weight.mul_(0.5)
+        y2 = m(ids, wts)
+        assert l2.packed("32").data_ptr() == packed.data_ptr()  # re-packed in place
+        try:
+            type(m).use_gather_mlp = False
+            want2 = m(ids, wts)
+        finally:
+            type(m).use_gather_mlp = True
+        _close(y2, want2, 2e-3, 2e-3, f"{family}: after a weight update")
+
+
 def test_embed_gemm_narrow_exchange_rows(cuda):
     """The candidate fan-out hands the forward its exchanged rows as strided
     views of [int32 row x F | fp32 weight x F] (serving/packing.py narrow
