@@ -411,6 +411,8 @@ def run_live(a, ctx, cfg, model, eng, B):
     live = LiveScheduler(eng, sc, buckets=buckets, depth=a.slots, control=control, step_timeout_s=a.step_timeout_s,
                          start_paused=control is not None, narrow=not a.no_narrow, peer_timeout_s=a.step_timeout_s)
     extra = {}
+    if eng.self_checks:  # every bucket's fan-out step vs a local forward of the same rows, at start-up
+        extra["self_check"] = {"atol": 1e-5, "buckets": eng.self_checks}
     if world == 1 and pool:
         extra["fp32_check"] = fp32_check(cfg, model, live, pool[0])
     # phase barriers of the main thread: a CPU group of their own (the step's

@@ -168,6 +168,7 @@ class FanoutEngine:
         self._split: Dict[Tuple[int, int], object] = {}  # two-lane fan-out forward (_capture_split)
         self._seqs: Dict[int, object] = {}
         self.native_fanout_active = False
+        self.self_checks: list = []  # self_check() results: {bucket, rows, max_abs_diff}
         self._native_disabled = False
         self.layout = executor.layout
         self.dev = executor.device
@@ -512,6 +513,8 @@ class FanoutEngine:
                 diff = (got - want).abs().max().item()
                 ok = bool(diff <= atol)
                 err = f"max |diff| {diff:.3g}"
+                # kept for the run's report (bench.py JSON "self_check")
+                self.self_checks.append({"bucket": int(B), "rows": int(rows), "max_abs_diff": float(diff)})
         except Exception as e:  # surfaced through the agreement below
             ok, err = False, repr(e)
         if not ok:

@@ -86,6 +86,22 @@ def test_bench_more_ranks(n, mode):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("n,model", [(8, "dcn_v2"), (3, "dcn_v2"), (8, "deepfm")])
+def test_bench_alltoall_fanout_exact_vs_local(n, model):
+    """BASELINE config 5 (DCN-v2, fp8 towers) and config 3 (DeepFM) fanned out
+    over n gloo ranks in alltoall mode (every rank a front door, its rows split
+    over all ranks as narrow exchange rows): at start-up every bucket's fan-out
+    step scores exactly like a local forward of the same rows on every rank,
+    and the served run fails no request."""
+    out = _run_bench(n, ("--model", model, "--mode", "alltoall", "--request-rows", "24", "--requests-per-gpu", "2",
+                         "--small-buckets", "", "--qps", "0", "--qps-sweep", ""))
+    assert out["n_gpus"] == n and out.get("requests_failed", 0) == 0
+    assert "alltoall" in out["config"]["parallelism"], out["config"]["parallelism"]
+    sc = out["self_check"]
+    assert sc["buckets"] and all(b["max_abs_diff"] <= 1e-5 and b["rows"] > 0 for b in sc["buckets"]), sc
+
+
+@pytest.mark.slow
 def test_bench_sharded_dlrm_world2():
     """DLRM with tables sharded over 2 gloo ranks: every step is the eager step
     program (ids all-to-all, owner gather, embeddings all-to-all) in lockstep."""

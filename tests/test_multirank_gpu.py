@@ -73,6 +73,35 @@ def test_bench_ranks_sharing_one_gpu(n, mode, peer, scatter_path):
         assert len(per) == n and min(per) > 0.5 * max(per), per
 
 
+@pytest.mark.parametrize("n,peer", [(2, 0), (3, 0), (3, 262144)])
+def test_bench_dcn_v2_alltoall_ranks_sharing_one_gpu(n, peer):
+    """BASELINE config 5 through the candidate fan-out on hardware (verdict r5
+    #1/#4): DCN-v2 with fp8 towers, alltoall over n ranks sharing the GPU. Each
+    rank's rows cross to the others as narrow exchange rows and feed the fp8
+    gather, the quant passes and the split cross path; every bucket's fan-out
+    step scores exactly like a local forward at start-up, no request fails."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
+           "--model", "dcn_v2", "--mode", "alltoall", "--steps", "20", "--warmup", "4", "--prime-steps", "10",
+           "--requests-per-gpu", "4", "--request-rows", "96", "--pool", "8", "--client-threads", "2",
+           "--qps", "200", "--qps-seconds", "0.4", "--qps-sweep", "", "--small-buckets", "96",
+           "--step-timeout-s", "20"]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="2", DTFS_HANG_DUMP_S="100",
+               DTFS_PEER_COMM=str(peer))
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == n and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    assert "native C++ step" in out["config"]["parallelism"], out["config"]["parallelism"]
+    assert out["server"]["idle_steps_per_s"] == 0, out["server"]
+    sc = out["self_check"]["buckets"]
+    assert len(sc) == 2 and all(b["max_abs_diff"] <= 1e-5 for b in sc), sc
+
+
 @pytest.mark.parametrize("n,peer", [(2, 0), (3, 0), (3, 1 << 20)])
 def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
     """BASELINE config 4 shape on N ranks: DLRM tables sharded table-wise over
