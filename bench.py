@@ -128,9 +128,12 @@ def parse_args():
                          "HBM over xGMI behind a per-rank hot-row replica cache (default: the preset's)")
     ap.add_argument("--hot-cache-rows", type=int, default=None,
                     help="peer exchange: replica cache rows per rank (default: the config's; 0 = no cache)")
-    ap.add_argument("--cache-learn-rounds", type=int, default=6,
-                    help="peer exchange: untimed (max(8, warmup)-step run + cache refresh) rounds before the clock "
-                         "(a server refreshes every second)")
+    ap.add_argument("--cache-learn-rounds", type=int, default=2,
+                    help="peer exchange: untimed learning rounds before the clock, each a pass over the request "
+                         "pool with every candidate's remote keys sampled, then a cache refresh (a server "
+                         "refreshes every second)")
+    ap.add_argument("--cache-learn-requests", type=int, default=0,
+                    help="peer exchange: requests per learning round (0: the whole request pool)")
     ap.add_argument("--cache-refresh-s", type=float, default=0.0,
                     help="peer exchange: > 0 keeps the background refresher running (this period) through the "
                          "timed run, so the clock covers the refreshes' cost")
@@ -318,6 +321,36 @@ def fresh_hit_rate(cfg, model, ctx, rows: int = 32768) -> float:
     return round(hit / tot, 4) if tot else 0.0
 
 
+def cache_oracle(a, cfg, model, ctx, n_pool: int, extra_k=()) -> dict:
+    """Hit rate of the EXACT top-k remote keys of the served request pool (the
+    same generator and seed as request_pool; every request equally likely): an
+    upper bound for any hot set of k rows on this stream, at k = 1 M / 8 M /
+    64 M and the cache's capacity / installed rows (extra_k)."""
+    import numpy as np
+
+    from distributed_tf_serving_amd.parallel.hot_cache import KEY_SHIFT
+
+    peer = model.emb.peer
+    hot, col0 = int(getattr(model, "hot", 1)), cfg.num_dense
+    synth = SyntheticRequests(fields=cfg.num_fields, id_space=1 << 40, dist="zipf", seed=1000 + ctx.rank,
+                              weights=a.feature_weights)
+    remote = [t for t in range(peer.T) if bool(peer.tremote_cpu[t])]
+    keys = []
+    for _ in range(n_pool):
+        ids, _ = synth.arrays(a.request_rows)
+        for t in remote:
+            v = ids[:, col0 + t * hot:col0 + (t + 1) * hot].astype(np.int64) % np.int64(peer.rows[t])
+            keys.append((np.int64(t) << KEY_SHIFT) | v.reshape(-1))
+    if not keys:
+        return {}
+    _, counts = np.unique(np.concatenate(keys), return_counts=True)
+    counts = np.sort(counts)[::-1]
+    csum, total = np.cumsum(counts), float(counts.sum())
+    ks = sorted({1 << 20, 8 << 20, 64 << 20, *[int(k) for k in extra_k if k > 0]})
+    return {"distinct_keys": int(counts.size), "lookups": int(total),
+            "hit_rate_at": {str(k): round(float(csum[min(k, counts.size) - 1]) / total, 4) for k in ks}}
+
+
 def fp32_check(cfg, model, live, request: bytes) -> dict:
     """Scores of one served request vs an fp32 forward of the same weights on
     the CPU (the ops' reference math)."""
@@ -432,13 +465,25 @@ def run_live(a, ctx, cfg, model, eng, B):
     timeout_us = int(a.step_timeout_s * 1e6)
     cache = getattr(model, "cache", None)
     if cache is not None and pool:
-        # peer exchange: serve a few steps so the kernels sample the stream,
-        # then install the hot set (the refresher is off while the clock runs:
-        # a synthetic stream's hot set does not drift)
+        # peer exchange: serve the request pool with every candidate's remote
+        # keys sampled (the kernels read the period from the cache descriptor,
+        # the captured graphs stay), installing the hot set after each pass;
+        # then back to sampling every sample_every-th candidate (the refresher
+        # is off while the clock runs: a synthetic stream's hot set does not drift)
+        cache.set_sample_period(1)
+        per_pass = a.cache_learn_requests if a.cache_learn_requests > 0 else max(max(8, a.warmup) * n_req, len(pool))
+        # no more keys per refresh than the ring holds
+        keys_per_req = a.request_rows * max(1, model.emb.peer.remote_tables) * int(getattr(model, "hot", 1))
+        chunk = max(n_req, min(per_pass, cache.ring.numel() // max(1, keys_per_req)))
         for _ in range(a.cache_learn_rounds):
-            live.run_load(pool, warmup=0, count=max(8, a.warmup) * n_req, concurrency=conc,
-                          threads=a.client_threads, timeout_us=timeout_us)
-            cache.refresh()
+            done = 0
+            while done < per_pass:
+                n = min(chunk, per_pass - done)
+                live.run_load(pool, warmup=0, count=n, concurrency=conc, threads=a.client_threads,
+                              timeout_us=timeout_us)
+                cache.refresh()
+                done += n
+        cache.set_sample_period(0)
         sync()
         cache.reset_counts()
         if a.cache_refresh_s > 0:  # the serving configuration: refreshes run while the clock does
@@ -547,6 +592,9 @@ def run_live(a, ctx, cfg, model, eng, B):
                 "counted_every": cache.count_scale,
                 # the pool repeats: the same hot set on a fresh draw of the stream
                 "hit_rate_fresh_stream": fresh_hit_rate(cfg, model, ctx),
+                # exact top-k of the served pool's remote-key frequencies: the best
+                # any hot set of k rows can do on this stream
+                "oracle": cache_oracle(a, cfg, model, ctx, len(pool), [cache.cap, int(cache.keys.numel())]),
             }
     if eng.scatter is not None:
         # shared-arena scatter: host->device bytes this rank copied per step (its

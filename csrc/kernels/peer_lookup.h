@@ -83,8 +83,16 @@ __device__ __forceinline__ const bf16* peer_row(const PeerLookupArgs& p, const C
 // both. Counting a subset keeps the counters' atomics (one per wave and kind,
 // on 128 addresses) off most waves - counting every lookup cost ~3 us per
 // 16384-candidate step (tools/studies/peer_lookup_bench.py).
+// The sampling period: word 1 of the cache descriptor when > 0 (set by the
+// host between steps - HotRowCache.set_sample_period: every candidate while
+// the cache learns, the captured graphs unchanged), else sample_every.
+__device__ __forceinline__ int64_t peer_sample_period(const PeerLookupArgs& p) {
+  const int64_t dyn = p.cache ? p.cache[1] : 0;
+  return dyn > 0 ? dyn : int64_t(p.sample_every);
+}
 __device__ __forceinline__ bool peer_sampled(const PeerLookupArgs& p, int64_t b) {
-  return p.sample_every <= 1 || b % p.sample_every == 0;
+  const int64_t sp = peer_sample_period(p);
+  return sp <= 1 || b % sp == 0;
 }
 __device__ __forceinline__ bool peer_counted(const PeerLookupArgs& p, int64_t b) {
   return p.sample_every <= 1 || b % p.sample_every == p.sample_every / 2;

@@ -155,8 +155,10 @@ class HotRowCache:
     capacity; one 16-byte load per probe): one serves the steps while
     :meth:`refresh` rebuilds the other.
     ``desc`` (int64 [5], read by the kernels at their start) = {active index,
-    0, H - 1, rows, capacity}: a refresh changes only its first word (one
-    8-byte store), so a kernel sees the old index or the new one, whole.
+    sample period, H - 1, rows, capacity}: a refresh changes only its first
+    word (one 8-byte store), so a kernel sees the old index or the new one,
+    whole; the sample period (0 = ``sample_every``) lets a learning phase
+    sample every candidate without re-capturing the step's graphs.
 
     Slot safety: :meth:`refresh` first waits for the device (every step that
     could still read the index replaced by the previous refresh is done); the
@@ -164,8 +166,8 @@ class HotRowCache:
     it keeps at most ``fill`` x capacity rows hot so there are free slots for
     the next turnover."""
 
-    def __init__(self, peer: PeerTables, capacity: Optional[int] = -1, ring_cap: int = 1 << 20, sample_every: int = 8,
-                 decay: float = 0.5, fill: float = 0.75):
+    def __init__(self, peer: PeerTables, capacity: Optional[int] = -1, ring_cap: Optional[int] = None,
+                 sample_every: int = 8, decay: float = 0.5, fill: float = 0.75):
         self.peer = peer
         self.sized = "explicit"
         if capacity is None or int(capacity) < 0:  # auto: from the free device memory
@@ -175,6 +177,11 @@ class HotRowCache:
         self.sample_every, self.decay, self.fill = int(sample_every), float(decay), float(fill)
         dev = peer.trows.device
         self.device = dev
+        if ring_cap is None:
+            # the ring holds the keys sampled between two refreshes: 16 M on a
+            # GPU (128 MB of its 288 GB) so a learning phase that samples every
+            # candidate of tens of steps loses none; small on the CPU
+            ring_cap = (1 << 24) if dev.type == "cuda" else (1 << 16)
         i64 = dict(dtype=torch.int64, device=dev)
         self.rows = torch.zeros(self.cap, D, dtype=peer.dtype, device=dev)
         self.index = [torch.full((self.H, 2), -1, **i64) for _ in range(2)]  # {key, slot} entries
@@ -187,6 +194,7 @@ class HotRowCache:
         self.cand_keys = torch.empty(0, **i64)     # candidates with decayed counts
         self.cand_score = torch.empty(0, dtype=torch.float32, device=dev)
         self.active = -1
+        self.sample_period = 0
         self.refreshes = 0
         self.refresh_failures = 0
         self.last_error: Optional[str] = None
@@ -220,6 +228,13 @@ class HotRowCache:
 
     def reset_counts(self) -> None:
         self.stats.zero_()
+
+    def set_sample_period(self, n: int = 0) -> None:
+        """Sample the remote keys of every n-th candidate from the next step
+        on (n = 1: all; 0: back to ``sample_every``). Kernels read it from the
+        descriptor, so captured graphs need no re-capture."""
+        self.desc[1:2].fill_(int(n))
+        self.sample_period = int(n)
 
     # -- CPU reference of the kernels' cache side ---------------------------------
     def lookup_cpu(self, keys: torch.Tensor) -> torch.Tensor:
@@ -379,7 +394,8 @@ def peer_gather_cpu(peer: PeerTables, cache: Optional[HotRowCache], ids: torch.T
             rows[hit] = cache.rows.cpu()[slot[hit]].float()
         b = torch.arange(B, dtype=torch.int64).repeat_interleave(T * hot)
         n = cache.sample_every
-        sampled = (b % n == 0) if n > 1 else torch.ones_like(b, dtype=torch.bool)
+        sp = cache.sample_period if cache.sample_period > 0 else n  # the kernels' peer_sample_period
+        sampled = (b % sp == 0) if sp > 1 else torch.ones_like(b, dtype=torch.bool)
         counted = (b % n == n // 2) if n > 1 else torch.ones_like(b, dtype=torch.bool)
         cache.count_cpu(int((hit & counted).sum()), int((remote & ~hit & counted).sum()))
         if n > 0:
