@@ -1342,8 +1342,7 @@ std::vector<torch::Tensor> cross_combine(torch::Tensor y, torch::Tensor x0, torc
 // them). Same rounding as linear_fp8 (plain) + cross_combine.
 std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, torch::Tensor Wq, torch::Tensor sw,
                                           c10::optional<torch::Tensor> bias, torch::Tensor x0, torch::Tensor xl,
-                                          bool want_z, c10::optional<torch::Tensor> head_w,
-                                          c10::optional<torch::Tensor> Wp) {
+                                          bool want_z, c10::optional<torch::Tensor> head_w) {
   check_dev(q, "q");
   check_same_dev(q, Wq, "Wq");
   TORCH_CHECK(q.scalar_type() == torch::kFloat8_e4m3fn && Wq.scalar_type() == torch::kFloat8_e4m3fn && q.dim() == 2 &&
@@ -1377,14 +1376,7 @@ std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, tor
   }
   TORCH_CHECK(want_z || hw, "nothing to produce");
   c10::DeviceGuard g(q.device());
-  // one wave per SIMD when W comes packed in MX fragment order (cross_gemm.hip)
-  const bool one_wave = Wp && dtfs::cross1w_ok(int(M), int(N), int(K));
-  if (one_wave) {
-    check_same_dev(q, *Wp, "Wp");
-    TORCH_CHECK(Wp->scalar_type() == torch::kUInt8 && Wp->numel() == N * K && Wp->is_contiguous(),
-                "Wp must be Wq packed in MX fragment order (ops.pack_mx_frag)");
-  }
-  const int64_t tiles_n = one_wave ? dtfs::cross1w_tiles_n(int(N)) : (N + 255) / 256;
+  const int64_t tiles_n = (N + 255) / 256;
   torch::Tensor z, dot;
   if (want_z) z = torch::empty({M, N}, x0.options());
   if (hw) dot = torch::empty({tiles_n, M}, x0.options().dtype(torch::kFloat32));
@@ -1407,10 +1399,6 @@ std::vector<torch::Tensor> cross_gemm_fp8(torch::Tensor q, torch::Tensor sx, tor
   a.M = int(M);
   a.N = int(N);
   a.K = int(K);
-  if (one_wave) {
-    check_hip(dtfs::launch_cross1w(a, Wp->data_ptr(), cur_stream(q)), "cross1w");
-    return {z, dot};
-  }
   check_hip(dtfs::launch_cross_gemm_fp8(a, cur_stream(q)), "cross_gemm_fp8");
   return {z, dot};
 }
@@ -1838,8 +1826,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dot_interaction_gather_arena", &dot_interaction_gather_arena, py::arg("dense"), py::arg("table"),
         py::arg("arena"), py::arg("id_col0"), py::arg("modulo_f"), py::arg("offset_f"), py::arg("out_cols") = 0);
   m.def("cross_gemm_fp8", &cross_gemm_fp8, py::arg("q"), py::arg("sx"), py::arg("Wq"), py::arg("sw"), py::arg("bias"),
-        py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none(),
-        py::arg("Wp") = py::none());
+        py::arg("x0"), py::arg("xl"), py::arg("want_z") = true, py::arg("head_w") = py::none());
   m.def("cross_combine", &cross_combine, py::arg("y"), py::arg("x0"), py::arg("xl"), py::arg("want_z") = true,
         py::arg("k_pad") = 0, py::arg("head_w") = py::none(),
         "split DCN-v2 cross layer: z = x0*y + xl, optionally quantised (e4m3 + row scale) and/or dotted with head_w");

@@ -238,12 +238,9 @@ struct CrossGemmArgs {
   int M = 0, N = 0, K = 0;
 };
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& args, hipStream_t st);
-// The same layer, one wave per SIMD (cross_gemm.hip): W packed in MX fragment
-// order (ops.pack_mx_frag) instead of args.W, 128 x 512 tiles, dot partials
-// per 512-column tile [cross1w_tiles_n(N)][ldd]; N % 16 == 0, K % 128 == 0.
-bool cross1w_ok(int M, int N, int K);
-int cross1w_tiles_n(int N);
-hipError_t launch_cross1w(const CrossGemmArgs& args, const void* Wp, hipStream_t st);
+// (The rejected one-wave-per-SIMD form of this layer, 128 x 512 tiles with W
+// in MX fragment order, lives in tools/native/cross_gemm_1w.hip with its stamp
+// study; profiles/r05_dcn_cross1w.md.)
 
 // Peer lookup (kernels/peer_lookup.h): table-wise sharded tables read
 // one-sidedly where they live. A rank's store is a list of chunks of 2^shift

@@ -321,11 +321,6 @@ class DCNv2(CTRModel):
     family = "dcn_v2"
     supports_arena = True
 
-    # the one-wave MX cross kernel (csrc/kernels/cross_gemm.hip) instead of the
-    # 8-phase form: bit-equal, measured slower (profiles/r05_dcn_cross1w.md) -
-    # off; tools.studies.microbench --dcn flips it per instance
-    one_wave_cross = False
-
     def __init__(self, cfg: ModelConfig, device="cpu"):
         super().__init__(cfg, device)
         V, D, F, L = cfg.vocab_size, cfg.embed_dim, cfg.num_fields, cfg.num_cross_layers
@@ -410,9 +405,7 @@ class DCNv2(CTRModel):
                 last = i == L - 1
                 if fused:
                     z, cross_logit = ops.cross_gemm_fp8(q, sx, layer.w_fp8, layer.w_scale, layer.bias, x0, xl,
-                                                        want_z=not last, head_w=self.head_wc if last else None,
-                                                        packed_w=(lambda layer=layer: layer.packed("mx"))
-                                                        if self.one_wave_cross else None)
+                                                        want_z=not last, head_w=self.head_wc if last else None)
                     if not last:
                         q, sx = ops.quant_rows_fp8(z, ops.FP8_K_PAD)
                 else:

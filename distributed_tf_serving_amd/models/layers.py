@@ -120,23 +120,15 @@ class Dense(nn.Module):
     def packed(self, layout: str = "16") -> torch.Tensor:
         """The weight in MFMA fragment order - "16": ops.pack_bfrag (the fused
         MLP tail's 16x16x32 B operand), "32": ops.pack_frag32 (the gather-GEMM's
-        32x32x16 A operand), "mx": ops.pack_mx_frag of the e4m3 copy (the
-        one-wave cross GEMM) - re-packed whenever the weight changed
+        and the one-launch tower's 32x32x16 A operand) - re-packed whenever the weight changed
         (load_state_dict bumps its version). Built by the eager warm-up that
         precedes every graph capture."""
         key = (self.weight.data_ptr(), self.weight._version)
         cache = self.__dict__.setdefault("_packed", {})
         cached = cache.get(layout)
         if cached is None or cached[0] != key:
-            if layout == "mx":  # the fp8 copy, MX-fp8 fragment order (cross_gemm.hip)
-                key = (self.w_fp8.data_ptr(), self.w_fp8._version)
-                cached = cache.get(layout)
-                if cached is not None and cached[0] == key:
-                    return cached[1]
-                fresh = ops.pack_mx_frag(self.w_fp8)
-            else:
-                w = self.weight.detach()
-                fresh = ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w)
+            w = self.weight.detach()
+            fresh = ops.pack_bfrag(w) if layout == "16" else ops.pack_frag32(w)
             if cached is not None and cached[1].shape == fresh.shape and cached[1].dtype == fresh.dtype:
                 # a weight changed in place: re-pack INTO the buffer captured HIP
                 # graphs already read (a new allocation would leave them serving

@@ -294,33 +294,16 @@ def cross_gemm_fits(M: int, N: int) -> bool:
 
 
 
-def pack_mx_frag(Wq: torch.Tensor) -> torch.Tensor:
-    """e4m3 weights [N, K] -> the A-operand fragment order of
-    v_mfma_scale_f32_16x16x128_f8f6f4 (csrc/kernels/cross_gemm.hip): block
-    (n16, k128, half) is 64 lanes x 16 bytes, lane (r, q) = (l & 15, l >> 4)
-    holding row 16 n16 + r, K bytes 128 k128 + 64 half + 16 q .. +16. uint8."""
-    N, K = Wq.shape
-    if N % 16 or K % 128:
-        raise ValueError(f"pack_mx_frag needs N % 16 == 0 and K % 128 == 0, got {tuple(Wq.shape)}")
-    u = Wq.contiguous().view(torch.uint8)
-    return u.reshape(N // 16, 16, K // 128, 2, 4, 16).permute(0, 2, 3, 4, 1, 5).contiguous().view(-1)
-
-
 def cross_gemm_fp8(xq: torch.Tensor, sx: torch.Tensor, Wq: torch.Tensor, sw: torch.Tensor,
                    b: Optional[torch.Tensor], x0: torch.Tensor, xl: torch.Tensor, want_z: bool = True,
-                   head_w: Optional[torch.Tensor] = None, packed_w=None):
+                   head_w: Optional[torch.Tensor] = None):
     """One DCN-v2 cross layer in one launch (csrc/kernels/gemm.hip
     cross_staged_epilogue): y = bf16(xq Wq^T * sx * sw + b), z = bf16(x0 * y + xl).
     Returns (z or None, dot or None) with dot = fp32 [tiles, M] partial cross
-    logits z[:, T t:T t + T] . head_w[T t:T t + T] (a head ``extra``; T = 256,
-    or 512 for the one-wave form). The same rounding as linear_fp8 +
-    cross_combine. ``packed_w``: a callable returning :func:`pack_mx_frag` of
-    Wq - with it the GPU runs the one-wave kernel csrc/kernels/cross_gemm.hip
-    (bit-equal, slower than the 8-phase form: the served DCN-v2 does not pass
-    it, models.ctr.DCNv2.one_wave_cross; profiles/r05_dcn_cross1w.md)."""
+    logits z[:, T t:T t + T] . head_w[T t:T t + T] (a head ``extra``; T = 256).
+    The same rounding as linear_fp8 + cross_combine."""
     if xq.is_cuda:
-        wp = packed_w() if packed_w is not None else None
-        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w, wp)
+        z, d = hip().cross_gemm_fp8(xq, sx, Wq, sw, b, x0, xl, want_z, head_w)
         return (z if want_z else None), (d if head_w is not None else None)
     y = linear_fp8(xq, sx, Wq, sw, b)
     zb = (x0.float() * y.float() + xl.float()).to(torch.bfloat16)
@@ -469,7 +452,7 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
     ``cross_consts = cross_v1_consts(w, b, head_w)``, as ``cross[3]`` when given).
     ``resolved``: the front half from :func:`embed_gemm_resolve` (GPU only).
     ``packed_w``: a callable returning W in 32x32x16 MFMA fragment order
-    (:func:`pack_frag32`, e.g. ``lambda: dense.packed("32")``); with it (and GG1W, N % 512 ==
+    (:func:`pack_frag32`, e.g. ``lambda: dense.packed("32")``); with it (N % 512 ==
     0, no cross network) the GPU runs the one-wave-per-SIMD form
     (csrc/kernels/gather_gemm.hip: B straight into registers).
     On the GPU x never exists in HBM (csrc/kernels/gemm.hip gemm_gather_kernel reads
@@ -482,7 +465,7 @@ def embed_gemm(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optio
         if cross is not None:
             xw, xc = cross[3] if len(cross) > 3 and cross[3] is not None else cross_v1_consts(*cross[:3])
         r = list(resolved) if resolved is not None else None
-        wp = packed_w() if packed_w is not None and GG1W and cross is None and W.shape[0] % 512 == 0 else None
+        wp = packed_w() if packed_w is not None and cross is None and W.shape[0] % 512 == 0 else None
         if isinstance(ids, ArenaRows):
             return tuple(hip().embed_gemm(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias),
                                           W, b, a, fm2, xw, xc, r, wp))
@@ -734,19 +717,14 @@ def pack_frag32(W: torch.Tensor) -> torch.Tensor:
 
 
 # The fused MLP tail replaces GEMM2 + the fused last-layer/head kernel at or
-# above this many rows (one 64-row workgroup per CU at 16384). A module flag,
-# not an environment knob: microbenchmarks and tests flip it in-process.
-MLP_TAIL = True
+# above this many rows (one 64-row workgroup per CU at 16384).
 MLP_TAIL_MIN_ROWS = 8192
-# embed_gemm's one-wave-per-SIMD gather-GEMM (gather_gemm.hip) when the
-# caller hands it packed weights; False = the 8-phase kernel (gemm.hip).
-GG1W = True
 
 
 def mlp_tail_ok(x: torch.Tensor, l2, l3) -> bool:
     """Shapes the fused two-layer tail + head kernel covers: bf16 [M, 1024] ->
     512 -> 256 -> score, ReLU / linear layers, enough rows to fill the GPU."""
-    return (MLP_TAIL and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
             and x.shape[1] == 1024 and x.shape[0] >= MLP_TAIL_MIN_ROWS
             and not l2.fp8 and not l3.fp8 and tuple(l2.weight.shape) == (512, 1024)
             and tuple(l3.weight.shape) == (256, 512) and l2.act in ("relu", "none") and l3.act in ("relu", "none"))

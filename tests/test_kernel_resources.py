@@ -50,7 +50,7 @@ def _resources(src: str):
     return res
 
 
-@pytest.mark.parametrize("src", ["gather_gemm.hip", "gather_mlp.hip", "mlp_tail.hip", "cross_gemm.hip"])
+@pytest.mark.parametrize("src", ["gather_gemm.hip", "gather_mlp.hip", "mlp_tail.hip"])
 def test_one_wave_kernels_are_scratch_free(src):
     res = _resources(src)
     assert res, f"no kernels found in {src}"
@@ -58,7 +58,7 @@ def test_one_wave_kernels_are_scratch_free(src):
         assert r.get("scratch") == 0, f"{src}: {name} spills {r.get('scratch')} bytes/lane to scratch"
 
 
-@pytest.mark.parametrize("src", ["gather_gemm.hip", "gather_mlp.hip", "mlp_tail.hip", "cross_gemm.hip", "gemm.hip", "embedding.hip"])
+@pytest.mark.parametrize("src", ["gather_gemm.hip", "gather_mlp.hip", "mlp_tail.hip", "gemm.hip", "embedding.hip"])
 def test_inline_asm_loads_have_no_register_hazards(src, tmp_path):
     """No instruction touches a register an inline-asm load is still filling
     (tools/isa_hazards.py on the compiled gfx950 code): the round-5 one-wave

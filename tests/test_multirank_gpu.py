@@ -102,6 +102,32 @@ def test_bench_dcn_v2_alltoall_ranks_sharing_one_gpu(n, peer):
     assert len(sc) == 2 and all(b["max_abs_diff"] <= 1e-5 for b in sc), sc
 
 
+def test_bench_eight_ranks_sharing_one_gpu():
+    """The 8-GPU node's world size on hardware (verdict r5 #5): 8 ranks share
+    the box's GPU, an 8-rank RCCL communicator pair, the 8-rank step control
+    and the alltoall fan-out; every bucket's fan-out step equals a local
+    forward on every rank, no request fails, an idle cluster steps nothing.
+    (scripts/gpu_rehearsal8.sh runs the scatter / peer-exchange DLRM / DCN-v2
+    forms too: profiles/r06_rehearsal8_and_reference.log.)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "8",
+           "--steps", "10", "--warmup", "2", "--prime-steps", "5", "--requests-per-gpu", "4", "--request-rows", "64",
+           "--pool", "4", "--client-threads", "1", "--qps", "0", "--qps-sweep", "", "--small-buckets", "64",
+           "--mode", "alltoall", "--step-timeout-s", "60"]
+    env = dict(os.environ, DTFS_SHARE_GPU="1", DTFS_HOST_THREADS="1", DTFS_HANG_DUMP_S="140")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 8 and out["value"] > 0 and out.get("requests_failed", 0) == 0
+    assert "candidate-dp8" in out["config"]["parallelism"] and "native C++ step" in out["config"]["parallelism"]
+    assert out["server"]["idle_steps_per_s"] == 0, out["server"]
+    assert all(b["max_abs_diff"] <= 1e-5 for b in out["self_check"]["buckets"]), out["self_check"]
+
+
 @pytest.mark.parametrize("n,peer", [(2, 0), (3, 0), (3, 1 << 20)])
 def test_bench_sharded_dlrm_ranks_sharing_one_gpu(n, peer):
     """BASELINE config 4 shape on N ranks: DLRM tables sharded table-wise over

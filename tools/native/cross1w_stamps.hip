@@ -4,10 +4,10 @@
 // G3 W loads, fragments 6 / 7), step 1 (G0: W + A DMAs), step 2 (G1), the
 // barrier, step 3 (G2 + the next tile's fragments) - against the 64 x 32 =
 // 2048 MFMA cycles it carries? DCN-v2 cross shape: N = 2752, K = 2816.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -I csrc -o cross1w_stamps cross1w_stamps.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -I ../../csrc/kernels -o cross1w_stamps cross1w_stamps.hip
 // Arguments: M values (default 2048 16384).
 #define DTFS_CROSS1W_STAMPS 1
-#include "../../csrc/kernels/cross_gemm.hip"
+#include "cross_gemm_1w.hip"
 
 #include <algorithm>
 #include <cstdio>

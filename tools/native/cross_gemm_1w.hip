@@ -21,10 +21,20 @@
 //     gather_gemm.hip), counted vmcnt / lgkmcnt waits, one barrier per tile;
 //   * epilogue: y staged through LDS, then x0 / xl / z as whole 1 KiB row
 //     segments.
+//
+// NOT part of the served build (rejected: 137-149 vs 122-125 us per layer at
+// 16384 rows against the 8-phase form, profiles/r05_dcn_cross1w.md). Kept here
+// for tools/native/cross1w_stamps.hip; build with -I csrc/kernels.
 // hipcc-flags: -fno-slp-vectorize
 #include "asm_io.h"
 #include "common.h"
 #include "launchers.h"
+
+namespace dtfs {
+bool cross1w_ok(int M, int N, int K);
+int cross1w_tiles_n(int N);
+hipError_t launch_cross1w(const CrossGemmArgs& args, const void* Wp, hipStream_t st);
+}  // namespace dtfs
 
 namespace dtfs {
 namespace kern {
