@@ -472,9 +472,10 @@ def run_live(a, ctx, cfg, model, eng, B):
         # is off while the clock runs: a synthetic stream's hot set does not drift)
         cache.set_sample_period(1)
         per_pass = a.cache_learn_requests if a.cache_learn_requests > 0 else max(max(8, a.warmup) * n_req, len(pool))
-        # no more keys per refresh than the ring holds
+        # at most half the ring's keys per refresh: pushes land in 64 segments
+        # by block, and a segment that wraps overwrites keys not yet counted
         keys_per_req = a.request_rows * max(1, model.emb.peer.remote_tables) * int(getattr(model, "hot", 1))
-        chunk = max(n_req, min(per_pass, cache.ring.numel() // max(1, keys_per_req)))
+        chunk = max(n_req, min(per_pass, cache.ring.numel() // max(1, 2 * keys_per_req)))
         for _ in range(a.cache_learn_rounds):
             done = 0
             while done < per_pass:

@@ -6,8 +6,10 @@
 
 #include <torch/extension.h>
 
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <memory>
 #include <string>
 #include <vector>
@@ -342,6 +344,11 @@ void def_live_methods(py::class_<H>& c) {
             }
             py::dict o;
             o["latency_us"] = r.latency_us;
+            // [n, 6] float32: sched_lag, admit, batch, step, encode, deliver (loadgen.h Stages)
+            py::array_t<float> stg({py::ssize_t(r.stages_us.size()), py::ssize_t(dtfs::runtime::kStages)});
+            if (!r.stages_us.empty())
+              std::memcpy(stg.mutable_data(), r.stages_us.data(), r.stages_us.size() * sizeof(dtfs::runtime::Stages));
+            o["stages_us"] = stg;
             o["submitted"] = r.submitted;
             o["ok"] = r.ok;
             o["errors"] = r.errors;

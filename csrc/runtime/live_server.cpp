@@ -699,6 +699,10 @@ void LiveServer::completer_loop() {
           r.response = wire::encode_predict_response(spec, {t});
           ++n_ok;
         }
+        r.t_arrive = p.t_arrive;
+        r.t_launch = f.t_launch;
+        r.t_done = t1;
+        r.t_encoded = now_us();
         if (p.done) p.done(std::move(r));
         p.done = nullptr;
       }

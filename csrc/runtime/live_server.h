@@ -62,6 +62,11 @@ struct Reply {
   int code = kOk;
   std::string message;
   std::string response;  // serialized PredictResponse when code == kOk
+  // steady-clock microseconds (now_us()) of the request's life in the server,
+  // 0 when it never got there: admitted into an arena, its step launched, the
+  // step seen done by the completer, its response encoded. The load generator
+  // splits each latency into these stages (where a tail request waited).
+  int64_t t_arrive = 0, t_launch = 0, t_done = 0, t_encoded = 0;
 };
 using Completion = std::function<void(Reply&&)>;
 

@@ -66,7 +66,11 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   int64_t completed = 0;
   double t_open = 0, t_close = 0;
   std::vector<double> lat_sched;  // open loop: by request index
-  if (open_loop) lat_sched.assign(size_t(spec.warmup + spec.count), -1.0);
+  std::vector<Stages> stg_sched;
+  if (open_loop) {
+    lat_sched.assign(size_t(spec.warmup + spec.count), -1.0);
+    stg_sched.assign(size_t(spec.warmup + spec.count), Stages{});
+  }
   res.latency_us.reserve(size_t(spec.count));
   WorkQ work;
   std::atomic<int64_t> next{0};
@@ -80,8 +84,13 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   // then did next.fetch_add / work.push: the waiter could wake in between and
   // return, a use-after-return on the completer thread.)
   int running = 0;
-  auto on_done = [&](int64_t i, int64_t t_sched, Reply&& r) {
+  auto on_done = [&](int64_t i, int64_t t_sched, int64_t t_pop, Reply&& r) {
     const int64_t t = now_us();
+    Stages sg{};
+    if (r.code == kOk && r.t_arrive > 0 && r.t_encoded > 0) {
+      sg = {float(t_pop - t_sched), float(r.t_arrive - t_pop), float(r.t_launch - r.t_arrive),
+            float(r.t_done - r.t_launch), float(r.t_encoded - r.t_done), float(t - r.t_encoded)};
+    }
     bool push_token = false, last = false;
     {
       std::lock_guard<std::mutex> lk(mu);
@@ -96,13 +105,18 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
         }
       }
       if (open_loop) {
-        if (i >= spec.warmup && i < spec.warmup + spec.count) lat_sched[size_t(i)] = double(t - t_sched);
+        if (i >= spec.warmup && i < spec.warmup + spec.count) {
+          lat_sched[size_t(i)] = double(t - t_sched);
+          stg_sched[size_t(i)] = sg;
+        }
         if (completed == spec.warmup + spec.count) t_close = double(t);
       } else {
         // closed loop: the window is counted in completions, whatever their order
         if (completed == spec.warmup) t_open = double(t);
-        if (completed > spec.warmup && completed <= spec.warmup + spec.count)
+        if (completed > spec.warmup && completed <= spec.warmup + spec.count) {
           res.latency_us.push_back(double(t - t_sched));
+          res.stages_us.push_back(sg);
+        }
         if (completed == spec.warmup + spec.count) t_close = double(t);
         push_token = true;
       }
@@ -127,11 +141,12 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
       std::pair<int64_t, int64_t> w;
       while (work.pop(&w)) {
         const int64_t i = w.first;
-        const int64_t t_sched = open_loop ? w.second : now_us();
+        const int64_t t_pop = now_us();
+        const int64_t t_sched = open_loop ? w.second : t_pop;
         const std::string& r = reqs[size_t(i % P)];
         const int64_t dl = spec.timeout_us > 0 ? t_sched + spec.timeout_us : 0;
         srv.submit(reinterpret_cast<const uint8_t*>(r.data()), r.size(), dl,
-                   [&on_done, i, t_sched](Reply&& rep) { on_done(i, t_sched, std::move(rep)); });
+                   [&on_done, i, t_sched, t_pop](Reply&& rep) { on_done(i, t_sched, t_pop, std::move(rep)); });
       }
     });
   }
@@ -170,7 +185,10 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   res.window_us = t_close - t_open;
   if (open_loop) {
     for (int64_t i = spec.warmup; i < spec.warmup + spec.count; ++i)
-      if (lat_sched[size_t(i)] >= 0) res.latency_us.push_back(lat_sched[size_t(i)]);
+      if (lat_sched[size_t(i)] >= 0) {
+        res.latency_us.push_back(lat_sched[size_t(i)]);
+        res.stages_us.push_back(stg_sched[size_t(i)]);
+      }
   }
   return res;
 }

@@ -10,6 +10,7 @@
 // fixed QPS" needs (the reference has no such mode).
 #pragma once
 
+#include <array>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -33,8 +34,18 @@ struct LoadSpec {
                                     // after its completion is counted (run_load must still wait for it)
 };
 
+// Stages of one request's latency (us), in order: sched_lag (open loop: the
+// submitting thread picked it up late), admit (until admitted into an arena:
+// a full server blocks here), batch (admitted -> its step launched: batching
+// wait + build + launch), step (launched -> the completer saw it done: the GPU
+// step and the steps ahead of it), encode (the batch's responses up to this
+// one), deliver (encoded -> the client's callback ran).
+constexpr int kStages = 6;
+using Stages = std::array<float, kStages>;
+
 struct LoadResult {
   std::vector<double> latency_us;  // timed requests (closed loop: completion order; open loop: by schedule)
+  std::vector<Stages> stages_us;   // the same requests' stages, same order (OK replies only: else zeros)
   int64_t submitted = 0, ok = 0, errors = 0;
   double window_us = 0;            // timed window: first to last timed completion boundary
   double wall_us = 0;
