@@ -419,6 +419,25 @@ def fp32_check_dlrm_sparse(cfg, model, live, request: bytes) -> dict:
             "rows": int(got.numel()), "reference": f"sparse: {B * Tn * hot} referenced table rows rebuilt on the CPU"}
 
 
+STAGES = ("sched_lag", "admit", "batch", "step", "encode", "deliver")  # csrc/runtime/loadgen.h Stages
+
+
+def stage_breakdown(r: dict):
+    """Where the requests of a load run spent their latency (this rank's front
+    door): each stage's p50 / p99, and its mean over the requests at or above
+    the run's p99 latency - the tail's own breakdown."""
+    lat = np.asarray(r.get("latency_us", []), dtype=np.float64)
+    st = np.asarray(r.get("stages_us", np.zeros((0, len(STAGES)))), dtype=np.float64)
+    if lat.size == 0 or st.shape != (lat.size, len(STAGES)):
+        return None
+    tail = st[lat >= np.percentile(lat, 99)]
+    r1 = lambda v: round(float(v), 1)  # noqa: E731
+    return {"p50_us": {k: r1(np.percentile(st[:, i], 50)) for i, k in enumerate(STAGES)},
+            "p99_us": {k: r1(np.percentile(st[:, i], 99)) for i, k in enumerate(STAGES)},
+            "tail_mean_us": {k: r1(tail[:, i].mean()) for i, k in enumerate(STAGES)} if len(tail) else None,
+            "tail_requests": int(len(tail))}
+
+
 def pct(lat_us, q):
     return round(float(np.percentile(lat_us, q)) * 1e-3, 3) if len(lat_us) else None
 
@@ -520,7 +539,7 @@ def run_live(a, ctx, cfg, model, eng, B):
         extra["fixed_qps"] = {"qps": a.qps, "front_doors": fronts, "request_rows": a.request_rows,
                               "scores_per_s": round(a.qps * a.request_rows, 1),
                               "p50_ms": round(float(red[0]), 3), "p99_ms": round(float(red[1]), 3),
-                              "errors": int(red[2])}
+                              "errors": int(red[2]), "stages": stage_breakdown(q)}
         extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
     fracs = [float(x) for x in a.qps_sweep.split(",") if x.strip()] if a.qps_sweep else []
     if fracs:  # every rank takes part (the collectives below); ranks without requests only follow
@@ -545,7 +564,7 @@ def run_live(a, ctx, cfg, model, eng, B):
                 dist.all_reduce(red, op=dist.ReduceOp.MAX, group=phase)
             sweep.append({"load": f, "offered_qps": round(qps, 1), "achieved_qps": round(-float(red[3]), 1),
                           "scores_per_s": round(qps * a.request_rows, 1), "p50_ms": round(float(red[0]), 3),
-                          "p99_ms": round(float(red[1]), 3), "errors": int(red[2])})
+                          "p99_ms": round(float(red[1]), 3), "errors": int(red[2]), "stages": stage_breakdown(q)})
         extra["latency_vs_load"] = {"capacity_qps": round(cap_qps, 1), "request_rows": a.request_rows,
                                     "front_doors": fronts, "points": sweep}
     # BASELINE config 2 literally: one 512-candidate request at a time (at N > 1
