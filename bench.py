@@ -438,6 +438,39 @@ def stage_breakdown(r: dict):
             "tail_requests": int(len(tail))}
 
 
+def host_sched_counters() -> dict:
+    """Host-side scheduling counters of this process (what a latency tail
+    caused by the host looks like): the cgroup's CPU quota and throttling
+    (cgroup v2 cpu.max / cpu.stat), the process's CPU time and its voluntary /
+    involuntary context switches (getrusage). Diff two readings."""
+    import resource
+
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        out["cpu_quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for ln in f:
+                k, v = ln.split()
+                if k in ("nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out.update(cpu_s=ru.ru_utime + ru.ru_stime, nvcsw=ru.ru_nvcsw, nivcsw=ru.ru_nivcsw, wall_s=time.monotonic())
+    return out
+
+
+def host_sched_delta(a: dict, b: dict) -> dict:
+    d = {k: b[k] - a[k] for k in b if k in a and k != "cpu_quota_cpus" and b[k] is not None and a[k] is not None}
+    wall = d.pop("wall_s", 0.0)
+    d["cpus_busy"] = round(d.pop("cpu_s", 0.0) / wall, 2) if wall > 0 else None
+    d["wall_s"] = round(wall, 2)
+    d["cpu_quota_cpus"] = b.get("cpu_quota_cpus")
+    return d
+
+
 def pct(lat_us, q):
     return round(float(np.percentile(lat_us, q)) * 1e-3, 3) if len(lat_us) else None
 
@@ -542,6 +575,7 @@ def run_live(a, ctx, cfg, model, eng, B):
                               "errors": int(red[2]), "stages": stage_breakdown(q)}
         extra["p50_at_fixed_qps_ms"] = extra["fixed_qps"]["p50_ms"]
     fracs = [float(x) for x in a.qps_sweep.split(",") if x.strip()] if a.qps_sweep else []
+    hs0 = host_sched_counters()
     if fracs:  # every rank takes part (the collectives below); ranks without requests only follow
         # the throughput run's request rate, whole node (slowest rank's window)
         w = torch.tensor([window_s], dtype=torch.float64)
@@ -566,7 +600,9 @@ def run_live(a, ctx, cfg, model, eng, B):
                           "scores_per_s": round(qps * a.request_rows, 1), "p50_ms": round(float(red[0]), 3),
                           "p99_ms": round(float(red[1]), 3), "errors": int(red[2]), "stages": stage_breakdown(q)})
         extra["latency_vs_load"] = {"capacity_qps": round(cap_qps, 1), "request_rows": a.request_rows,
-                                    "front_doors": fronts, "points": sweep}
+                                    "front_doors": fronts, "points": sweep,
+                                    # this rank's host over the sweep: cgroup throttling, CPU use, preemptions
+                                    "host": host_sched_delta(hs0, host_sched_counters())}
     # BASELINE config 2 literally: one 512-candidate request at a time (at N > 1
     # fanned out over every GPU: the reference's topology inside one node)
     sync()
