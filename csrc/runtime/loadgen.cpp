@@ -134,44 +134,58 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
   };
 
   std::vector<std::thread> subs;
+  std::vector<int64_t> due;  // open loop: request i's send time
   const int T = std::max(1, spec.threads);
   const double wall0 = double(now_us());
-  for (int s = 0; s < T; ++s) {
-    subs.emplace_back([&] {
-      std::pair<int64_t, int64_t> w;
-      while (work.pop(&w)) {
-        const int64_t i = w.first;
-        const int64_t t_pop = now_us();
-        const int64_t t_sched = open_loop ? w.second : t_pop;
-        const std::string& r = reqs[size_t(i % P)];
-        const int64_t dl = spec.timeout_us > 0 ? t_sched + spec.timeout_us : 0;
-        srv.submit(reinterpret_cast<const uint8_t*>(r.data()), r.size(), dl,
-                   [&on_done, i, t_sched, t_pop](Reply&& rep) { on_done(i, t_sched, t_pop, std::move(rep)); });
-      }
-    });
-  }
-  if (spec.warmup == 0) t_open = double(now_us());
+  auto submit_one = [&](int64_t i, int64_t t_sched, int64_t t_pop) {
+    const std::string& r = reqs[size_t(i % P)];
+    const int64_t dl = spec.timeout_us > 0 ? t_sched + spec.timeout_us : 0;
+    srv.submit(reinterpret_cast<const uint8_t*>(r.data()), r.size(), dl,
+               [&on_done, i, t_sched, t_pop](Reply&& rep) { on_done(i, t_sched, t_pop, std::move(rep)); });
+  };
   if (!open_loop) {
+    for (int s = 0; s < T; ++s) {
+      subs.emplace_back([&] {
+        std::pair<int64_t, int64_t> w;
+        while (work.pop(&w)) {
+          const int64_t t_pop = now_us();
+          submit_one(w.first, t_pop, t_pop);
+        }
+      });
+    }
+    if (spec.warmup == 0) t_open = double(now_us());
     for (int c = 0; c < C && c < total; ++c) work.push(next.fetch_add(1), 0);
   } else {
-    // schedule thread: request i is due at t0 + i / qps (uniform) or at
-    // exponential gaps; everything due is queued whenever it wakes, so a late
-    // wake-up sends a burst instead of drifting the offered rate
+    // request i is due at t0 + i / qps (uniform) or at exponential gaps. No
+    // shared queue: submitter s owns requests s, s + T, s + 2T, ... and sends
+    // each when it is due (sleeping when it is far, yielding when near). One
+    // schedule thread pushing every request through a condition variable fell
+    // behind at ~250 k requests/s: its lag showed up as a 10 ms latency tail
+    // at 90 % of DeepFM's capacity (profiles/r06_latency_stages.md).
+    due.assign(static_cast<size_t>(total), 0);  // outlives this block: the submitters read it
     std::mt19937_64 rng(spec.seed);
     std::exponential_distribution<double> expo(spec.qps);
     const double t0 = double(now_us()) + 1000.0;
     double t_next = t0;
     for (int64_t i = 0; i < total; ++i) {
-      if (i == spec.warmup) t_open = t_next;
-      for (;;) {
-        const double now = double(now_us());
-        if (now >= t_next) break;
-        const double gap = t_next - now;
-        if (gap > 200) std::this_thread::sleep_for(std::chrono::microseconds(int64_t(gap - 100)));
-        else std::this_thread::yield();
-      }
-      work.push(i, int64_t(t_next));
+      due[size_t(i)] = int64_t(t_next);
       t_next += spec.poisson ? expo(rng) * 1e6 : 1e6 / spec.qps;
+    }
+    t_open = double(due[size_t(std::min<int64_t>(spec.warmup, total - 1))]);
+    for (int s = 0; s < T; ++s) {
+      subs.emplace_back([&, s] {
+        for (int64_t i = s; i < total; i += T) {
+          const int64_t t_sched = due[size_t(i)];
+          for (;;) {
+            const int64_t now = now_us();
+            if (now >= t_sched) break;
+            const int64_t gap = t_sched - now;
+            if (gap > 200) std::this_thread::sleep_for(std::chrono::microseconds(gap - 100));
+            else std::this_thread::yield();
+          }
+          submit_one(i, t_sched, now_us());
+        }
+      });
     }
   }
   {
