@@ -157,11 +157,14 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
     for (int c = 0; c < C && c < total; ++c) work.push(next.fetch_add(1), 0);
   } else {
     // request i is due at t0 + i / qps (uniform) or at exponential gaps. No
-    // shared queue: submitter s owns requests s, s + T, s + 2T, ... and sends
-    // each when it is due (sleeping when it is far, yielding when near). One
-    // schedule thread pushing every request through a condition variable fell
-    // behind at ~250 k requests/s: its lag showed up as a 10 ms latency tail
-    // at 90 % of DeepFM's capacity (profiles/r06_latency_stages.md).
+    // shared queue and no schedule thread: each submitter claims the next
+    // request (one atomic increment), waits until it is due and sends it, so
+    // a submitter that stalls (preempted, a slow copy) holds up one request
+    // while the others take the following ones. (One schedule thread pushing
+    // every request through a condition variable fell behind at ~250 k
+    // requests/s, and submitters that each owned every T-th request drained a
+    // stall alone: both showed up as 10-50 ms latency tails at 75-90 % of
+    // DeepFM's capacity, profiles/r06_latency_stages.md.)
     due.assign(static_cast<size_t>(total), 0);  // outlives this block: the submitters read it
     std::mt19937_64 rng(spec.seed);
     std::exponential_distribution<double> expo(spec.qps);
@@ -173,8 +176,10 @@ LoadResult run_load(LiveServer& srv, const std::vector<std::string>& reqs, const
     }
     t_open = double(due[size_t(std::min<int64_t>(spec.warmup, total - 1))]);
     for (int s = 0; s < T; ++s) {
-      subs.emplace_back([&, s] {
-        for (int64_t i = s; i < total; i += T) {
+      subs.emplace_back([&] {
+        for (;;) {
+          const int64_t i = next.fetch_add(1);
+          if (i >= total) break;
           const int64_t t_sched = due[size_t(i)];
           for (;;) {
             const int64_t now = now_us();
