@@ -1165,17 +1165,16 @@ torch::Tensor mlp_tail(torch::Tensor X, torch::Tensor W2p, torch::Tensor b2, int
   return y;
 }
 
-// K1 + K2 + K4 x 3 + K6: the whole DeepFM / Wide&Deep tower after the resolve
-// pass in one launch (gather_mlp.hip): 64 rows x all 1024 h1 columns per
+// K1 + K2 + K4 x 3 + K6: the whole DeepFM / Wide&Deep tower in one launch,
+// the resolve pass included (gather_mlp.hip): 64 rows x all 1024 h1 columns per
 // workgroup, h1 / h2 kept in LDS. W1p / W2p / W3p: ops.pack_frag32 of the three
-// weights. ``fm``: add the second-order FM term of each row (DeepFM). Returns the
-// scores (fp32 [B], or ``out``: device or pinned host memory).
+// weights. ``fm``: add the second-order FM term of each row (DeepFM). Returns
+// the scores (fp32 [B], or ``out``: device or pinned host memory).
 torch::Tensor gather_mlp(torch::Tensor table, c10::optional<torch::Tensor> lin, c10::optional<torch::Tensor> arena,
                          c10::optional<torch::Tensor> ids, c10::optional<torch::Tensor> wts, int64_t B, int64_t F,
                          int64_t modulo, double bias, torch::Tensor W1p, torch::Tensor b1, torch::Tensor W2p,
                          torch::Tensor b2, int64_t act2, torch::Tensor W3p, torch::Tensor b3, int64_t act3,
-                         torch::Tensor hw, double hbias, bool fm, bool sigmoid,
-                         c10::optional<std::vector<torch::Tensor>> resolved, c10::optional<torch::Tensor> out) {
+                         torch::Tensor hw, double hbias, bool fm, bool sigmoid, c10::optional<torch::Tensor> out) {
   check_dev(table, "table");
   for (auto* t : {&W1p, &b1, &W2p, &b2, &W3p, &b3, &hw}) {
     check_dev(*t, "gather_mlp operand");
@@ -1196,38 +1195,30 @@ torch::Tensor gather_mlp(torch::Tensor table, c10::optional<torch::Tensor> lin, 
   TORCH_CHECK(W1p.numel() == 1024 * 64 * F && W2p.numel() == 512 * 1024 && W3p.numel() == 256 * 512,
               "packed weight sizes");
   TORCH_CHECK((act2 == 0 || act2 == 1) && (act3 == 0 || act3 == 1), "act must be 0 (none) or 1 (relu)");
+  TORCH_CHECK(B >= 0 && B < (int64_t(1) << 31), "gather_mlp: row count");
   if (lin) {
     check_dev(*lin, "lin");
     TORCH_CHECK(lin->scalar_type() == torch::kFloat32 && lin->numel() == V, "lin must be fp32 [V]");
   }
-  TORCH_CHECK(dtfs::gather_mlp_ok((B + 255) / 256 * 256, 1024, int(64 * F), 512, 256, int(F), V),
+  TORCH_CHECK(dtfs::gather_mlp_ok((B + 63) / 64 * 64, 1024, int(64 * F), 512, 256, int(F), V),
               "gather_mlp: shape outside the kernel's range");
   dtfs::EmbedArgs a;
   embed_gemm_inputs(table, arena, ids, wts, B, F, a);
+  a.table = table.data_ptr();
+  a.lin = lin ? lin->data_ptr<float>() : nullptr;
+  a.B = int(B);
+  a.F = int(F);
+  a.D = 64;
+  a.V = V;
+  a.modulo = modulo;
+  a.bias = float(bias);
   c10::DeviceGuard g(table.device());
-  const int64_t Mp = (B + 255) / 256 * 256;
-  const int64_t n_parts = fm ? 2 : 1;  // the resolve pass's shape (row 1 unused here)
-  std::vector<torch::Tensor> r;
-  if (resolved) {
-    r = *resolved;
-    TORCH_CHECK(r.size() == 3, "resolved = (rows_t, wts_t, parts)");
-    TORCH_CHECK(r[0].scalar_type() == torch::kInt32 && r[0].dim() == 2 && r[0].size(0) == F && r[0].size(1) == Mp &&
-                    r[0].is_contiguous() && r[1].scalar_type() == torch::kFloat32 && r[1].sizes() == r[0].sizes() &&
-                    r[1].is_contiguous() && r[2].scalar_type() == torch::kFloat32 && r[2].dim() == 2 &&
-                    r[2].size(1) == Mp && r[2].is_contiguous(),
-                "resolved tensors do not match this gather_mlp's shape");
-    for (const auto& t : r) check_same_dev(table, t, "resolved");
-  } else {
-    r = embed_gemm_resolve_into(table, lin, a, B, F, modulo, bias, n_parts);
-  }
   torch::Tensor y;
   float* yp = score_out(table, B, out, y);
   if (B == 0) return y;
-  check_hip(dtfs::launch_gather_mlp(table.data_ptr(), V, r[0].data_ptr<int32_t>(), r[1].data_ptr<float>(), Mp, int(F),
-                                    W1p.data_ptr(), b1.data_ptr<float>(), W2p.data_ptr(), b2.data_ptr<float>(),
+  check_hip(dtfs::launch_gather_mlp(a, W1p.data_ptr(), b1.data_ptr<float>(), W2p.data_ptr(), b2.data_ptr<float>(),
                                     int(act2), W3p.data_ptr(), b3.data_ptr<float>(), int(act3), hw.data_ptr<float>(),
-                                    float(hbias), r[2].data_ptr<float>(), fm, int(B), sigmoid ? 2 : 0, yp,
-                                    cur_stream(table)),
+                                    float(hbias), fm, sigmoid ? 2 : 0, yp, cur_stream(table)),
             "gather_mlp");
   return y;
 }
@@ -1810,9 +1801,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gather_mlp", &gather_mlp, py::arg("table"), py::arg("lin"), py::arg("arena"), py::arg("ids"),
         py::arg("wts"), py::arg("B"), py::arg("F"), py::arg("modulo"), py::arg("bias"), py::arg("W1p"), py::arg("b1"),
         py::arg("W2p"), py::arg("b2"), py::arg("act2"), py::arg("W3p"), py::arg("b3"), py::arg("act3"), py::arg("hw"),
-        py::arg("hbias"), py::arg("fm"), py::arg("sigmoid") = true, py::arg("resolved") = py::none(),
-        py::arg("out") = py::none(),
-        "DeepFM / Wide&Deep tower in one launch: gather + FM + 3 MLP layers + head (gather_mlp.hip)");
+        py::arg("hbias"), py::arg("fm"), py::arg("sigmoid") = true, py::arg("out") = py::none(),
+        "DeepFM / Wide&Deep tower in one launch: resolve + gather + FM + 3 MLP layers + head (gather_mlp.hip)");
   m.def("set_embed_wave_cap", &dtfs::set_embed_wave_cap, py::arg("waves"), py::arg("rows_in_flight") = 1,
         "pipelined embedding gather geometry: resident-wave cap (0 = one row per wave) and rows in flight per "
         "wave (1 or 2); tuning sweeps and tests");

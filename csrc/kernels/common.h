@@ -52,6 +52,18 @@ __device__ __forceinline__ int64_t hash_row(int64_t id, int64_t modulo) {
   return r < 0 ? r + modulo : r;
 }
 
+// u mod m for m < 2^32 with magic = floor((2^64 - 1) / m): q = mulhi(u, magic)
+// is floor(u/m) or one less, so one conditional subtract finishes it (the
+// 64-bit software modulo of hash_row costs ~100 instructions).
+__device__ __forceinline__ int64_t hash_row_magic(int64_t id, int64_t m, uint64_t magic) {
+  const uint64_t u = id < 0 ? uint64_t(0) - uint64_t(id) : uint64_t(id);
+  const uint64_t q = __umul64hi(u, magic);
+  uint64_t r = u - q * uint64_t(m);
+  if (r >= uint64_t(m)) r -= uint64_t(m);
+  if (id < 0 && r) r = uint64_t(m) - r;  // python-style non-negative modulo
+  return int64_t(r);
+}
+
 // Unaligned little-endian loads from byte-addressed buffers (protobuf
 // tensor_content has no alignment): aligned dword loads + v_alignbyte funnel
 // shifts instead of byte loads. Reads only the dwords the value overlaps.

@@ -194,16 +194,7 @@ __global__ void __launch_bounds__(256) embed_kernel(EmbedArgs a) {
 // the id fetch hides under the gather. The id -> row hash uses a multiply-high
 // reciprocal (host-computed) instead of the 64-bit software modulo.
 
-// u mod m for m < 2^32 with magic = floor((2^64 - 1) / m): q = mulhi(u, magic)
-// is floor(u/m) or one less, so one conditional subtract finishes it.
-__device__ __forceinline__ int64_t hash_row_magic(int64_t id, int64_t m, uint64_t magic) {
-  const uint64_t u = id < 0 ? uint64_t(0) - uint64_t(id) : uint64_t(id);
-  const uint64_t q = __umul64hi(u, magic);
-  uint64_t r = u - q * uint64_t(m);
-  if (r >= uint64_t(m)) r -= uint64_t(m);
-  if (id < 0 && r) r = uint64_t(m) - r;  // python-style non-negative modulo
-  return int64_t(r);
-}
+// (hash_row_magic: common.h)
 
 // K3 in the gather (DCN v1, CROSS): x_{l+1} = x0 (x_l . w_l) + b_l + x_l keeps
 // every x_l in span{x0, b_0 + .. + b_{l-1}}: x_l = alpha_l x0 + beta_l with

@@ -5,7 +5,7 @@
 //   h1 = relu(sum_f bf16(w[m,f] T[row(m,f)]) . W1[:, 64f..64f+63]^T + b1)  bf16, LDS
 //   h2 = act2(h1 W2^T + b2)                                                 bf16, LDS
 //   h3 = act3(h2 W3^T + b3)                                                 fp32, registers
-//   y[m] = sigmoid(h3[m] . hw + hbias + first[m] (+ FM(m)))
+//   y[m] = sigmoid(h3[m] . hw + hbias + first-order(m) (+ FM(m)))
 //
 // Round 5 ran this as two kernels (gather_gemm.hip 128 x 512 tiles + mlp_tail.hip):
 // 89 + 28 us per 16384-row step, h1 (32 MiB) written to HBM by the first and read
@@ -180,39 +180,40 @@ __device__ __forceinline__ void tail_gemm(const bf16x8* __restrict__ Wb, uint32_
 
 template <bool FM>
 __global__ void __launch_bounds__(256, 1)
-    gather_mlp_kernel(const uint8_t* __restrict__ table, int Vm1, const int32_t* __restrict__ rows_t,
-                      const float* __restrict__ wts_t, int64_t Mp, int F, const bf16x8* __restrict__ W1p,
+    gather_mlp_kernel(EmbedArgs ea, uint64_t magic, int F, const bf16x8* __restrict__ W1p,
                       const float* __restrict__ b1, const bf16x8* __restrict__ W2p, const float* __restrict__ b2,
                       int act2, const bf16x8* __restrict__ W3p, const float* __restrict__ b3, int act3,
-                      const float* __restrict__ hw, float hbias, const float* __restrict__ first, int M, int out_act,
-                      float* __restrict__ y) {
+                      const float* __restrict__ hw, float hbias, int M, int out_act, float* __restrict__ y) {
   constexpr int BM = 64;
   constexpr int N1 = 1024, N2 = 512, N3 = 256;
   constexpr int NS = 4;   // A ring slots: tile t+1 (scale pass, then fragments), t+2 / t+3 (DMA), t (free)
-  constexpr int RI = 8;   // rows / weights ring slots
-  constexpr int LR = 6;   // ring lead (tiles)
   constexpr int SLOT = BM * 128;
-  constexpr int RING = 1024;  // per tile: 64 int32 table rows | 64 fp32 weights | (a copy of both)
+  constexpr int FMAX = 64;
+  constexpr int TROWS = NS * SLOT, TWTS = TROWS + FMAX * BM * 4;  // resolved rows / weights [F][64], field-major
   constexpr int H1P = N1 * 2, H2P = N2 * 2;
-  constexpr int HOFF = BM * H1P;           // head partials [4][64] fp32, then the FM terms [64]
-  constexpr int BOFF = HOFF + 4 * BM * 4 + BM * 4;  // b1 | b2 | b3 | hw, fp32, staged once
+  constexpr int HOFF = BM * H1P;  // head partials [4][64] fp32, the FM terms [64], the first-order terms [64]
+  constexpr int BOFF = HOFF + 4 * BM * 4 + 2 * BM * 4;  // b1 | b2 | b3 | hw, fp32, staged once
   constexpr int SMEM = BOFF + (N1 + N2 + N3 + N3) * 4;
-  static_assert(NS * SLOT + RI * RING <= HOFF, "the K loop's rings live inside the h1 tile");
+  static_assert(TWTS + FMAX * BM * 4 <= HOFF, "the K loop's ring and row tables live inside the h1 tile");
+  const uint8_t* const table = static_cast<const uint8_t*>(ea.table);
+  const int Vm1 = int(ea.V - 1);
 #ifdef DTFS_GM_STAMPS
   unsigned long long gm_s[16] = {};
   const int gm_t = F / 2;
 #endif
   GM_AT(0);
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
-  uint8_t* const rring = smem + NS * SLOT;
+  int32_t* const rows_l = reinterpret_cast<int32_t*>(smem + TROWS);
+  float* const wts_l = reinterpret_cast<float*>(smem + TWTS);
   float* const red = reinterpret_cast<float*>(smem + HOFF);
   float* const fmv = red + 4 * BM;
+  float* const firstv = fmv + BM;
   float* const b1s = reinterpret_cast<float*>(smem + BOFF);
   float* const b2s = b1s + N1;
   float* const b3s = b2s + N2;
   float* const hws = b3s + N3;
   const uint32_t aring_lds = lds_addr(smem);
-  const uint32_t rring_lds = lds_addr(rring);
+  const uint32_t rows_lds = lds_addr(rows_l), wts_lds = lds_addr(wts_l);
 
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
   const int T = threadIdx.x;
@@ -221,13 +222,6 @@ __global__ void __launch_bounds__(256, 1)
   const int r32 = lane & 31, h = lane >> 5;
 
   // ---- staging (VMEM: every wave issues the same number per tile)
-  auto stage_ring = [&](int u) {  // 1 op: lanes 0-15 the rows, 16-31 the weights of tile u (32-63 a copy)
-    const int uc = min(u, F - 1);
-    const int l = lane & 31;
-    const void* g = l < 16 ? static_cast<const void*>(rows_t + int64_t(uc) * Mp + m0 + 4 * l)
-                           : static_cast<const void*>(wts_t + int64_t(uc) * Mp + m0 + 4 * (l - 16));
-    lds_dma16(g, rring_lds + (u & (RI - 1)) * RING);
-  };
   // A tile u: wave w DMAs rows R = 16 w + 8 k + (lane >> 3), k = 0..1 (1 KiB
   // each); lane i lands at +16 i = physical chunk lane & 7 of row R, which
   // holds logical chunk (lane & 7) ^ (R & 7)
@@ -236,8 +230,8 @@ __global__ void __launch_bounds__(256, 1)
   const uint32_t aring_w = aring_lds + 16 * w * 128;
   const uint32_t idx_off = 4 * arow0;
   int aidx[2];
-  auto read_idx = [&](int u) {  // 2 LDS ops
-    const uint32_t base = rring_lds + (u & (RI - 1)) * RING + idx_off;
+  auto read_idx = [&](int u) {  // 2 LDS ops (tiles past the last re-read it: branch-free loop)
+    const uint32_t base = rows_lds + min(u, F - 1) * (BM * 4) + idx_off;
     aidx[0] = ds_read4_at<0>(base);
     aidx[1] = ds_read4_at<32>(base);
   };
@@ -276,7 +270,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int d = 0; d < 8; ++d) fs[a][d] = 0.f;
   auto scale_read = [&](int u) {  // 4 ops
     const uint32_t base = aring_lds + (u & (NS - 1)) * SLOT + sc_off;
-    const uint32_t wb = rring_lds + (u & (RI - 1)) * RING + 256 + 4 * sc_r0;
+    const uint32_t wb = wts_lds + min(u, F - 1) * (BM * 4) + 4 * sc_r0;
     sv[0] = ds_read16i_at<0>(base);
     swt[0] = ds_read4_at<0>(wb);
     sv[1] = ds_read16i_at<4096>(base);
@@ -328,18 +322,18 @@ __global__ void __launch_bounds__(256, 1)
   // ---- VMEM per tile t, one op after each MFMA pair of the step after the
   // one that last read the registers it refills (op i of a W group refills
   // wf[jn = 2 g' + (i & 1)][s = i >> 1], last read by pair i of its step):
-  //   step 0: W(t, 6..7) x 8, ring(t + 5)
+  //   step 0: W(t, 6..7) x 8
   //   step 1: W(t+1, 0..1) x 8, A(t+3, 0)
   //   step 2: W(t+1, 2..3) x 8, A(t+3, 1)
   //   step 3: W(t+1, 4..5) x 8
   // so the counted wait for W(t, 2 st .. 2 st + 1) at the top of step st is
-  // vmcnt 18, 18, 18, 19 (the ops issued after it, in order). vmcnt retires in
+  // vmcnt 18, 17, 17, 18 (the ops issued after it, in order). vmcnt retires in
   // issue order: step 2's wait retires A(t+2) (issued at tile t-1) before the
-  // tile's barrier; step 1's wait retires ring(t+4) long before read_idx(t+4).
+  // tile's barrier. The rows / weights of every tile are resolved into LDS by
+  // the prologue (no rows ring).
   auto vm_op = [&](int t, int g, int i) {
     if (g == 3) {
-      if (i < 8) load_w1(t, 6 + (i & 1), i >> 1);
-      else stage_ring(t + 5);
+      load_w1(t, 6 + (i & 1), i >> 1);
     } else if (i < 8) {
       load_w1(t + 1, 2 * g + (i & 1), i >> 1);
     } else {
@@ -355,13 +349,58 @@ __global__ void __launch_bounds__(256, 1)
     reinterpret_cast<f32x4*>(b3s)[T] = reinterpret_cast<const f32x4*>(b3)[T];
     reinterpret_cast<f32x4*>(hws)[T] = reinterpret_cast<const f32x4*>(hw)[T];
   }
-  // ---- prologue: rings 0..4; A(0), A(1); then steps 1-3's groups of tile -1
-  // in the loop's order, so the loop's counted waits hold from the first tile;
-  // A(0) scaled; idx(3) read; K steps 0-2 of A(0)'s fragments in flight as step
-  // 3 of a tile leaves them
-  for (int u = 0; u < LR - 1; ++u) stage_ring(u);
+  // ---- resolve (K0 + the gather's front half, in the kernel: no resolve pass,
+  // no kernel boundary): this workgroup's 64 rows x F fields -> clamped table
+  // rows and weights, field-major in LDS, plus each row's first-order term
+  // bias + sum_f lin[row] w. Thread T: row T & 63, fields T >> 6, +4, +8, ...;
+  // every id / weight load of a thread goes out before the first use, then
+  // every lin load: two dependent round trips after the row descriptor.
+  {
+    constexpr int KR = FMAX / 4;
+    const int rr = T & 63, f0 = T >> 6;
+    const int b = m0 + rr;
+    ArenaRow ar{nullptr, nullptr, false, kArenaAllWeights, 4};
+    if (ea.arena && b < ea.B) ar = arena_row(static_cast<const uint8_t*>(ea.arena), kArenaPayloadOff, b);
+    int64_t id[KR];
+    float wv[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int f = f0 + 4 * k;
+      id[k] = 0;
+      wv[k] = 0.f;
+      if (f < F && b < ea.B) {
+        if (ea.arena) {
+          if (ar.ids) arena_feature(ar, f, id[k], wv[k]);
+        } else {
+          id[k] = ea.ids64 ? static_cast<const int64_t*>(ea.ids)[int64_t(b) * ea.ids_ld + f]
+                           : int64_t(static_cast<const int32_t*>(ea.ids)[int64_t(b) * ea.ids_ld + f]);
+          wv[k] = !ea.wts ? 1.f
+                  : ea.wts16 ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(ea.wts)[int64_t(b) * ea.wts_ld + f]) << 16)
+                             : static_cast<const float*>(ea.wts)[int64_t(b) * ea.wts_ld + f];
+        }
+      }
+    }
+    float lsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int f = f0 + 4 * k;
+      if (f < F) {
+        int64_t g = magic ? hash_row_magic(id[k], ea.modulo, magic) : hash_row(id[k], ea.modulo);
+        g = g < 0 ? 0 : (g > Vm1 ? Vm1 : g);  // memory safety whatever the ids say
+        rows_l[f * BM + rr] = int32_t(g);
+        wts_l[f * BM + rr] = wv[k];
+        if (ea.lin) lsum += ea.lin[g] * wv[k];
+      }
+    }
+    red[f0 * BM + rr] = lsum;
+  }
+  __syncthreads();
+  if (T < BM) firstv[T] = ea.bias + red[T] + red[BM + T] + red[2 * BM + T] + red[3 * BM + T];
+  // ---- prologue: A(0), A(1); then steps 1-3's groups of tile -1 in the
+  // loop's order, so the loop's counted waits hold from the first tile; A(0)
+  // scaled; idx(3) read; K steps 0-2 of A(0)'s fragments in flight as step 3
+  // of a tile leaves them
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  barrier();
   read_idx(0);
   wait_idx();
   stage_a(0, 0);
@@ -444,11 +483,10 @@ __global__ void __launch_bounds__(256, 1)
     fence();
     pair(0, 7);
     vm_op(t, 3, 7);
-    vm_op(t, 3, 8);
     fence();
     GM_T(3);
     // step 1: the scale pass's chunk of rows r (q = 0); W(t+1, 0..1), A(t+3, 0)
-    wait_vm8<18>(wf[2], wf[3]);
+    wait_vm8<17>(wf[2], wf[3]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pair(1, k);
@@ -460,7 +498,7 @@ __global__ void __launch_bounds__(256, 1)
     }
     GM_T(4);
     // step 2: rows r + 32 (q = 1); W(t+1, 2..3), A(t+3, 1); then the rows of A(t+4)
-    wait_vm8<18>(wf[4], wf[5]);
+    wait_vm8<17>(wf[4], wf[5]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pair(2, k);
@@ -478,7 +516,7 @@ __global__ void __launch_bounds__(256, 1)
     GM_T(6);
     // step 3: K steps 0-2 of A(t+1) stream in, each two pairs after its
     // registers' last use; W(t+1, 4..5)
-    wait_vm8<19>(wf[6], wf[7]);
+    wait_vm8<18>(wf[6], wf[7]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (k == 4) read_xs(t + 1, 0);
@@ -603,7 +641,7 @@ __global__ void __launch_bounds__(256, 1)
   if (tid_e < BM) {
     const int m = m0 + tid_e;
     if (m < M) {
-      float s = hbias + first[m];
+      float s = hbias + firstv[tid_e];
       if constexpr (FM) s += fmv[tid_e];
 #pragma unroll
       for (int ww = 0; ww < 4; ++ww) s += red[ww * BM + tid_e];
@@ -620,29 +658,28 @@ __global__ void __launch_bounds__(256, 1)
 }  // namespace kern
 
 bool gather_mlp_ok(int64_t Mp, int N1, int K1, int N2, int N3, int F, int64_t V) {
-  return N1 == 1024 && N2 == 512 && N3 == 256 && K1 == 64 * F && Mp % 64 == 0 && F >= 1 && F <= 4096 && V >= 1 &&
+  return N1 == 1024 && N2 == 512 && N3 == 256 && K1 == 64 * F && Mp % 64 == 0 && F >= 1 && F <= 64 && V >= 1 &&
          V <= (int64_t(1) << 25);
 }
 
-hipError_t launch_gather_mlp(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp, int F,
-                             const void* W1p, const float* b1, const void* W2p, const float* b2, int act2,
-                             const void* W3p, const float* b3, int act3, const float* hw, float hbias,
-                             const float* first, bool fm, int M, int out_act, float* y, hipStream_t st) {
-  if (M == 0) return hipSuccess;
-  if (!gather_mlp_ok(Mp, 1024, 64 * F, 512, 256, F, V) || Mp < M || !table || !rows_t || !wts_t || !W1p || !b1 ||
-      !W2p || !b2 || !W3p || !b3 || !hw || !first || !y)
+hipError_t launch_gather_mlp(const EmbedArgs& a, const void* W1p, const float* b1, const void* W2p, const float* b2,
+                             int act2, const void* W3p, const float* b3, int act3, const float* hw, float hbias,
+                             bool fm, int out_act, float* y, hipStream_t st) {
+  if (a.B == 0) return hipSuccess;
+  const int64_t Mp = (int64_t(a.B) + 63) / 64 * 64;
+  if (!gather_mlp_ok(Mp, 1024, 64 * a.F, 512, 256, a.F, a.V) || a.B < 0 || a.modulo <= 0 || !a.table ||
+      (!a.arena && !a.ids) || a.modulo_f || a.shard_lo_f || !W1p || !b1 || !W2p || !b2 || !W3p || !b3 || !hw || !y)
     return hipErrorInvalidValue;
+  const uint64_t magic = a.modulo < (int64_t(1) << 32) ? ~uint64_t(0) / uint64_t(a.modulo) : 0;
   const int grid = int(Mp / 64);
   if (fm)
-    hipLaunchKernelGGL((kern::gather_mlp_kernel<true>), dim3(grid), dim3(256), 0, st,
-                       static_cast<const uint8_t*>(table), int(V - 1), rows_t, wts_t, Mp, F,
+    hipLaunchKernelGGL((kern::gather_mlp_kernel<true>), dim3(grid), dim3(256), 0, st, a, magic, a.F,
                        static_cast<const kern::bf16x8*>(W1p), b1, static_cast<const kern::bf16x8*>(W2p), b2, act2,
-                       static_cast<const kern::bf16x8*>(W3p), b3, act3, hw, hbias, first, M, out_act, y);
+                       static_cast<const kern::bf16x8*>(W3p), b3, act3, hw, hbias, a.B, out_act, y);
   else
-    hipLaunchKernelGGL((kern::gather_mlp_kernel<false>), dim3(grid), dim3(256), 0, st,
-                       static_cast<const uint8_t*>(table), int(V - 1), rows_t, wts_t, Mp, F,
+    hipLaunchKernelGGL((kern::gather_mlp_kernel<false>), dim3(grid), dim3(256), 0, st, a, magic, a.F,
                        static_cast<const kern::bf16x8*>(W1p), b1, static_cast<const kern::bf16x8*>(W2p), b2, act2,
-                       static_cast<const kern::bf16x8*>(W3p), b3, act3, hw, hbias, first, M, out_act, y);
+                       static_cast<const kern::bf16x8*>(W3p), b3, act3, hw, hbias, a.B, out_act, y);
   return hipGetLastError();
 }
 

@@ -171,16 +171,17 @@ hipError_t launch_mlp_tail(const void* X, int64_t ldx, int M, int K1, const void
                            int N2, const void* W3p, const float* b3, int act3, int N3, const float* hw, float hbias,
                            const float* extra, int extra_n, int64_t extra_ld, int out_act, float* y, hipStream_t st);
 
-// K1 + K2 + K4 x 3 + K6 (gather_mlp.hip): the DeepFM / Wide&Deep tower after
-// the resolve pass in one launch, y[m] = out_act(act3(act2(relu(x W1^T + b1)
-// W2^T + b2) W3^T + b3) . hw + hbias + first[m] (+ FM(m) when fm)); W1p / W2p /
-// W3p in 32x32x16 fragment order (ops.pack_frag32); N1 = 1024, N2 = 512, N3 =
-// 256, Mp % 64 == 0, V <= 2^25.
+// K1 + K2 + K4 x 3 + K6 (gather_mlp.hip): the DeepFM / Wide&Deep tower in one
+// launch, the resolve pass included: a.table / V / lin / modulo / bias and the
+// rows (a.arena, or a.ids + a.wts) as for launch_embed_resolve, a.B rows, a.F
+// fields; y[m] = out_act(act3(act2(relu(x W1^T + b1) W2^T + b2) W3^T + b3) . hw
+// + hbias + bias + sum_f lin[row] w (+ FM(m) when fm)); W1p / W2p / W3p in
+// 32x32x16 fragment order (ops.pack_frag32); N1 = 1024, N2 = 512, N3 = 256,
+// F <= 64, V <= 2^25.
 bool gather_mlp_ok(int64_t Mp, int N1, int K1, int N2, int N3, int F, int64_t V);
-hipError_t launch_gather_mlp(const void* table, int64_t V, const int32_t* rows_t, const float* wts_t, int64_t Mp, int F,
-                             const void* W1p, const float* b1, const void* W2p, const float* b2, int act2,
-                             const void* W3p, const float* b3, int act3, const float* hw, float hbias,
-                             const float* first, bool fm, int M, int out_act, float* y, hipStream_t st);
+hipError_t launch_gather_mlp(const EmbedArgs& a, const void* W1p, const float* b1, const void* W2p, const float* b2,
+                             int act2, const void* W3p, const float* b3, int act3, const float* hw, float hbias,
+                             bool fm, int out_act, float* y, hipStream_t st);
 
 // K3: DCN-v1 cross network, all L layers fused.
 hipError_t launch_cross_v1(const void* x0, int64_t ldx, int B, int d, int L, const float* w, const float* b,

@@ -180,7 +180,8 @@ class WideDeep(CTRModel):
     resolve_lane = True
 
     def _resolve_applies(self, ids, wts) -> bool:
-        return self._gather_gemm(ids, wts, fm2=False)
+        # the one-launch tower resolves its rows itself: no separate pass to move
+        return self._gather_gemm(ids, wts, fm2=False) and not self._gather_mlp(ids, wts, fm2=False)
 
     def _resolve(self, ids, wts):
         return ops.embed_gemm_resolve(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, False)
@@ -195,7 +196,7 @@ class WideDeep(CTRModel):
     def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_mlp(ids, wts, fm2=False):  # the whole tower in one launch
             return ops.gather_mlp(self.emb, ids, wts, self.wide, self.cfg.vocab_size, self.wide_bias, self.mlp.layers,
-                                  self.head_w, self.head_b, fm=False, resolved=resolved, out=out)
+                                  self.head_w, self.head_b, fm=False, out=out)
         if self._gather_gemm(ids, wts, fm2=False):
             h, wide, hw, hb = self._gg_front(ids, wts, resolved)
             return self.mlp.forward_head(h, hw, hb, extra=wide, out=out, start=1)
@@ -225,7 +226,8 @@ class DeepFM(CTRModel):
     resolve_lane = True
 
     def _resolve_applies(self, ids, wts) -> bool:
-        return self._gather_gemm(ids, wts, fm2=True)
+        # the one-launch tower resolves its rows itself: no separate pass to move
+        return self._gather_gemm(ids, wts, fm2=True) and not self._gather_mlp(ids, wts, fm2=True)
 
     def _resolve(self, ids, wts):
         return ops.embed_gemm_resolve(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, True)
@@ -241,7 +243,7 @@ class DeepFM(CTRModel):
     def _forward(self, ids, wts, out=None, resolved=None):
         if self._gather_mlp(ids, wts, fm2=True):  # the whole tower in one launch
             return ops.gather_mlp(self.emb, ids, wts, self.lin, self.cfg.vocab_size, self.fm_bias, self.mlp.layers,
-                                  self.head_w, self.head_b, fm=True, resolved=resolved, out=out)
+                                  self.head_w, self.head_b, fm=True, out=out)
         if self._gather_gemm(ids, wts, fm2=True):
             h, fm, hw, hb = self._gg_front(ids, wts, resolved)
             return self.mlp.forward_head(h, hw, hb, extra=fm, out=out, start=1)

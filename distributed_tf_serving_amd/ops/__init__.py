@@ -761,17 +761,17 @@ def gather_mlp_ok(table: torch.Tensor, layers, rows: int) -> bool:
 
 def gather_mlp(table: torch.Tensor, ids, wts: Optional[torch.Tensor], lin: Optional[torch.Tensor], modulo: int,
                bias: float, layers, hw: torch.Tensor, hbias: float, fm: bool, sigmoid: bool = True,
-               resolved=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """K1 + K2 + K4 x 3 + K6 in one launch (GPU): the scores of a DeepFM
-    (``fm``) or Wide&Deep tower, out_act(mlp(x) . hw + hbias + first-order
-    (+ FM)), x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)). h1 and h2 stay in
-    the CU's LDS (csrc/kernels/gather_mlp.hip). ``resolved``: the front half
-    from :func:`embed_gemm_resolve`; ``out``: device or pinned host scores."""
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K0 + K1 + K2 + K4 x 3 + K6 in one launch (GPU): the scores of a
+    DeepFM (``fm``) or Wide&Deep tower, out_act(mlp(x) . hw + hbias + bias +
+    sum_f lin[row] w (+ FM)), x[b, 64f:64f+64] = bf16(T[row(b, f)] * w(b, f)).
+    Each workgroup resolves its own rows' ids / weights into LDS; h1 and h2
+    stay in the CU's LDS (csrc/kernels/gather_mlp.hip). ``ids`` may be
+    :class:`ArenaRows` (the request bytes); ``out``: device or pinned host scores."""
     l1, l2, l3 = layers
     m = int(modulo) if modulo > 0 else table.shape[0]
     args = (l1.packed("32"), l1.bias, l2.packed("32"), l2.bias, _ACTS[l2.act], l3.packed("32"), l3.bias,
-            _ACTS[l3.act], hw, float(hbias), bool(fm), bool(sigmoid), list(resolved) if resolved is not None else None,
-            out)
+            _ACTS[l3.act], hw, float(hbias), bool(fm), bool(sigmoid), out)
     if isinstance(ids, ArenaRows):
         return hip().gather_mlp(table, lin, ids.arena, None, None, int(ids.B), int(ids.F), m, float(bias), *args)
     return hip().gather_mlp(table, lin, None, _rows(ids), None if wts is None else _rows(wts), int(ids.shape[0]),

@@ -892,13 +892,46 @@ def test_gather_mlp_tower_vs_fp32(cuda, B, F, fm, act3):
                               packed_w=lambda: ops.pack_frag32(d[2]))
     y2 = ops.mlp_tail(h, ops.pack_bfrag(d[6]), d[7], "relu", ops.pack_bfrag(d[8]), d[9], act3, d[10], 0.2, parts, True)
     _close(y, y2, 2e-3, 2e-3, "gather_mlp vs gather-GEMM + MLP tail")
-    # the resolve pass done earlier (another lane) and scores into pinned host memory
-    r = ops.embed_gemm_resolve(d[0], d[4], d[5], d[1], V, bias, fm)
+    # scores into pinned host memory; int32 row ids (the fan-out's exchanged rows)
     out = torch.zeros(B, dtype=torch.float32).pin_memory()
-    y3 = ops.gather_mlp(d[0], d[4], d[5], d[1], V, bias, layers, d[10], 0.2, fm=fm, resolved=r, out=out)
+    y3 = ops.gather_mlp(d[0], d[4], d[5], d[1], V, bias, layers, d[10], 0.2, fm=fm, out=out)
     torch.cuda.synchronize()
     assert y3.data_ptr() == out.data_ptr()
-    _close(out, y, 0, 0, "resolved + pinned out vs one call")
+    _close(out, y, 0, 0, "pinned out vs device out")
+    y4 = ops.gather_mlp(d[0], torch.remainder(d[4], V).to(torch.int32), d[5], d[1], V, bias, layers, d[10], 0.2, fm=fm)
+    _close(y4, y, 0, 0, "int32 rows vs int64 ids")
+
+
+def test_gather_mlp_arena_rows(cuda):
+    """The one-launch tower resolving its rows straight from request bytes in
+    a device arena (raw and packed-varint requests, padding rows past the
+    arena's rows) scores like the same rows unpacked."""
+    from distributed_tf_serving_amd.client.synth import SyntheticRequests
+    from distributed_tf_serving_amd.serving.arena import ArenaLayout
+    from distributed_tf_serving_amd.serving.packing import PackedLayout
+
+    V = 30_000
+    table, lin, W1, b1, _, _ = _gather_gemm_case(1, V=V)
+    m = build_model(ModelConfig(family="deepfm", vocab_size=V), cuda)
+    with torch.no_grad():
+        m.emb.copy_(table.to(cuda))
+        m.lin.copy_(lin.to(cuda))
+    A, L = ArenaLayout(43, 16384), PackedLayout(43)
+    ar = A.alloc()
+    s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=13)
+    sizes = [(3, True), (1500, False), (700, True), (90, False)] * 3 + [(4000, True)]
+    reqs = [s.message(n, raw=r).SerializeToString() for n, r in sizes]
+    ab = A.build(ar, A.place(ar, reqs))
+    assert not any(ab.errors)
+    dev = ar.to(cuda)
+    A.decode_varints(dev)
+    B = 9000  # > total_rows (8879): padding rows
+    packed = A.unpack_cpu(ar, L.alloc(B))
+    ids, wts = L.ids(packed), L.wts(packed)
+    ya = m.forward_arena(dev, B)
+    assert m._gather_mlp(ids.to(cuda), wts.to(cuda), fm2=True)
+    yp = m(ids.to(cuda), wts.to(cuda))
+    _close(ya, yp, 0, 0, "arena vs unpacked rows")
 
 
 def test_gather_mlp_model_path_and_weight_update(cuda):

@@ -6,6 +6,7 @@
 // DeepFM: F = 43 fields x 64 dims -> 1024 -> 512 -> 256 -> score, FM on.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -o gm_stamps gm_stamps.hip
 // Argument "hot": every row from the first 256 table rows (L2-resident).
+// The prologue includes the rows' resolve (int32 row ids + fp32 weights here).
 #define DTFS_GM_STAMPS 1
 #include "../../csrc/kernels/gather_mlp.hip"
 
@@ -33,7 +34,7 @@ int main(int argc, char** argv) {
   const bool hot = argc > 1 && std::string(argv[1]) == "hot";
   const int F = 43, V = 1 << 20, K = F * 64;
   void *table, *W1, *W2, *W3;
-  float *b1, *b2, *b3, *hw, *first, *y, *wts;
+  float *b1, *b2, *b3, *hw, *y, *wts;
   int32_t* rows;
   const int Mmax = 16384;
   (void)hipMalloc(&table, size_t(V) * 128);
@@ -44,7 +45,6 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&b2, 512 * 4);
   (void)hipMalloc(&b3, 256 * 4);
   (void)hipMalloc(&hw, 256 * 4);
-  (void)hipMalloc(&first, size_t(2) * Mmax * 4);
   (void)hipMalloc(&y, size_t(Mmax) * 4);
   (void)hipMalloc(&rows, size_t(F) * Mmax * 4);
   (void)hipMalloc(&wts, size_t(F) * Mmax * 4);
@@ -56,7 +56,6 @@ int main(int argc, char** argv) {
   (void)hipMemset(b2, 0, 512 * 4);
   (void)hipMemset(b3, 0, 256 * 4);
   (void)hipMemset(hw, 0, 256 * 4);
-  (void)hipMemset(first, 0, size_t(2) * Mmax * 4);
   {
     std::vector<int32_t> r(size_t(F) * Mmax);
     std::vector<float> w(size_t(F) * Mmax);
@@ -70,9 +69,20 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(wts, w.data(), w.size() * 4, hipMemcpyHostToDevice);
   }
   for (int M : {8192, 16384}) {
+    dtfs::EmbedArgs a;  // int32 row ids [M][F] + fp32 weights (the resolve runs in the kernel's prologue)
+    a.table = table;
+    a.V = V;
+    a.ids = rows;
+    a.ids64 = false;
+    a.ids_ld = F;
+    a.wts = wts;
+    a.wts_ld = F;
+    a.B = M;
+    a.F = F;
+    a.D = 64;
+    a.modulo = V;
     auto run = [&] {
-      return dtfs::launch_gather_mlp(table, V, rows, wts, M, F, W1, b1, W2, b2, 1, W3, b3, 1, hw, 0.f, first, true, M,
-                                     2, y, nullptr);
+      return dtfs::launch_gather_mlp(a, W1, b1, W2, b2, 1, W3, b3, 1, hw, 0.f, true, 2, y, nullptr);
     };
     for (int i = 0; i < 20; ++i)
       if (run() != hipSuccess) {

@@ -1,7 +1,8 @@
 """The one-launch DeepFM tower (csrc/kernels/gather_mlp.hip) against the
 two-kernel form it replaces (one-wave gather-GEMM + MLP tail), interleaved, on
 the served shapes: 1M x 64 table, 43 fields, 1024-512-256, Zipf ids over 2^40.
-The resolve pass runs once outside the timing (both forms consume it).
+Both forms include the rows' resolve: the two-kernel form runs the resolve
+pass (embed_resolve) first, the one-launch tower resolves in its prologue.
 
     python -m tools.studies.gather_mlp_study [--rows 8192,16384]
 """
@@ -42,16 +43,15 @@ def main():
     for B in [int(x) for x in a.rows.split(",")]:
         ids, wts = SyntheticRequests(fields=43, id_space=1 << 40, dist="zipf", seed=B).arrays(B)
         ids, wts = torch.from_numpy(ids).to(dev), torch.from_numpy(wts).to(dev)
-        r = ops.embed_gemm_resolve(m.emb, ids, wts, m.lin, m.cfg.vocab_size, m.fm_bias, True)
         out = torch.empty(B, dtype=torch.float32, device=dev)
 
         def one():
             return ops.gather_mlp(m.emb, ids, wts, m.lin, m.cfg.vocab_size, m.fm_bias, m.mlp.layers, m.head_w,
-                                  m.head_b, fm=True, resolved=r, out=out)
+                                  m.head_b, fm=True, out=out)
 
         def two():
             h, parts = ops.embed_gemm(m.emb, ids, wts, m.lin, m.cfg.vocab_size, m.fm_bias, l1.weight, l1.bias, "relu",
-                                      fm2=True, resolved=r, packed_w=lambda: l1.packed("32"))
+                                      fm2=True, packed_w=lambda: l1.packed("32"))
             return ops.mlp_tail(h, l2.packed(), l2.bias, l2.act, l3.packed(), l3.bias, l3.act, m.head_w, m.head_b,
                                 extra=parts, out=out)
 
