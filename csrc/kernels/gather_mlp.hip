@@ -349,6 +349,12 @@ __global__ void __launch_bounds__(256, 1)
     reinterpret_cast<f32x4*>(b3s)[T] = reinterpret_cast<const f32x4*>(b3)[T];
     reinterpret_cast<f32x4*>(hws)[T] = reinterpret_cast<const f32x4*>(hw)[T];
   }
+  // W1 fragments of tile 0 for steps 0-2 (the groups of "tile -1" in the
+  // loop's issue order): 24 loads whose latency hides behind the resolve
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vm_op(-1, g, i);
   // ---- resolve (K0 + the gather's front half, in the kernel: no resolve pass,
   // no kernel boundary): this workgroup's 64 rows x F fields -> clamped table
   // rows and weights, field-major in LDS, plus each row's first-order term
@@ -396,11 +402,10 @@ __global__ void __launch_bounds__(256, 1)
   }
   __syncthreads();
   if (T < BM) firstv[T] = ea.bias + red[T] + red[BM + T] + red[2 * BM + T] + red[3 * BM + T];
-  // ---- prologue: A(0), A(1); then steps 1-3's groups of tile -1 in the
-  // loop's order, so the loop's counted waits hold from the first tile; A(0)
-  // scaled; idx(3) read; K steps 0-2 of A(0)'s fragments in flight as step 3
-  // of a tile leaves them
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- prologue: A(0), A(1), A(2); A(0) scaled; idx(3) read; K steps 0-2 of
+  // A(0)'s fragments in flight as step 3 of a tile leaves them. Tile 0's
+  // counted waits hold: every W load of "tile -1" is retired below, and only
+  // A(2) stays in flight into the loop (fewer ops than the waits allow)
   read_idx(0);
   wait_idx();
   stage_a(0, 0);
@@ -411,11 +416,9 @@ __global__ void __launch_bounds__(256, 1)
   stage_a(1, 1);
   read_idx(2);
   wait_idx();
-#pragma unroll
-  for (int g = 0; g < 3; ++g)
-#pragma unroll
-    for (int i = 0; i < (g == 2 ? 8 : 9); ++i) vm_op(-1, g, i);
-  asm volatile("s_waitcnt vmcnt(26)" ::: "memory");  // A(0), A(1) landed (this wave's share)
+  stage_a(2, 0);
+  stage_a(2, 1);
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A(0), A(1) landed (this wave's share); A(2) in flight
   barrier();
   scale_read(0);
   scale_wait();

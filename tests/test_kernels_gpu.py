@@ -919,13 +919,13 @@ def test_gather_mlp_arena_rows(cuda):
     A, L = ArenaLayout(43, 16384), PackedLayout(43)
     ar = A.alloc()
     s = SyntheticRequests(dist="zipf", id_space=1 << 50, seed=13)
-    sizes = [(3, True), (1500, False), (700, True), (90, False)] * 3 + [(4000, True)]
+    sizes = [(3, True), (1500, False), (700, True), (90, False)] * 3 + [(4000, True), (5000, False)]
     reqs = [s.message(n, raw=r).SerializeToString() for n, r in sizes]
     ab = A.build(ar, A.place(ar, reqs))
     assert not any(ab.errors)
     dev = ar.to(cuda)
     A.decode_varints(dev)
-    B = 9000  # > total_rows (8879): padding rows
+    B = 16384  # > total_rows (15879): padding rows; the served bucket the tower runs at
     packed = A.unpack_cpu(ar, L.alloc(B))
     ids, wts = L.ids(packed), L.wts(packed)
     ya = m.forward_arena(dev, B)
