@@ -263,9 +263,11 @@ def build(a, ctx):
     arena_layout = ArenaLayout(F, max_rows=max(1, rows_in_max), gpu_varint=not shared)
     seg = None
     if shared:
-        from distributed_tf_serving_amd.parallel.shared_scatter import scatter_for_engine
+        from distributed_tf_serving_amd.parallel.shared_scatter import live_narrowing, scatter_for_engine
 
-        seg = scatter_for_engine(ctx, F, arena_layout.capacity, a.slots, B, tag="bench")
+        nm, nw = live_narrowing(model, dev.type == "cuda")
+        seg = scatter_for_engine(ctx, F, arena_layout.capacity, a.slots, B, tag="bench", narrow_modulo=nm,
+                                 narrow_wts_cols=nw)
     eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", arena=arena_layout, force_fanout=a.force_fanout,
                        group=step_group, shared_scatter=seg)
     for b in buckets:

@@ -1001,21 +1001,10 @@ __global__ void __launch_bounds__(512) gemm_8ph_kernel(
 
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  // tile order inside an XCD's contiguous share: N-fastest (gm = 0), or
-  // groups of gm row tiles walked M-fastest (epi bits 8..15), so the tiles an
-  // XCD runs at once span gm row tiles x (32 / gm) column tiles instead of
-  // ~3 row tiles x every column tile (the whole W panel)
-  const int gm = (epi >> 8) & 255;
-  int tm, tn;
-  if (gm > 0) {
-    const int span = gm * tiles_n, g0 = (tile / span) * gm, r = tile % span;
-    const int gsz = min(gm, tiles_m - g0);
-    tm = g0 + r % gsz;
-    tn = r / gsz;
-  } else {
-    tm = tile / tiles_n;
-    tn = tile % tiles_n;
-  }
+  // N-fastest inside each XCD's contiguous share (a grouped M-fastest order,
+  // gm row tiles x 32 / gm column tiles in flight, measured within 0.7 %:
+  // profiles/r06_dcn_cross_tile_order.md)
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1932,13 +1921,6 @@ hipError_t launch_gemm_gather(const void* table, int64_t V, const int32_t* rows_
   return hipGetLastError();
 }
 
-// Row-tile group of the cross GEMM's tile order (gemm_8ph_kernel, gm).
-// DTFS_CROSS_GM overrides it for studies (read per launch).
-static int cross_group_m() {
-  const char* e = std::getenv("DTFS_CROSS_GM");
-  return e ? std::max(0, std::min(255, std::atoi(e))) : 0;
-}
-
 hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& g, hipStream_t st) {
   if (g.M == 0 || g.N == 0) return hipSuccess;
   const int M = g.M, N = g.N, K = g.K;
@@ -1954,7 +1936,7 @@ hipError_t launch_cross_gemm_fp8(const CrossGemmArgs& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_8ph_kernel<true, bf16, true, true>), dim3(grid), dim3(512), 0, st,
                      static_cast<const uint8_t*>(g.A), g.lda, static_cast<const uint8_t*>(g.W), g.ldw, g.bias, g.sa,
                      g.sw, static_cast<bf16*>(g.Z), g.ldz, static_cast<const bf16*>(g.X0),
-                     static_cast<const bf16*>(g.XL), g.ldx, M, N, K, int(EPI_CROSS) | (cross_group_m() << 8), xs);
+                     static_cast<const bf16*>(g.XL), g.ldx, M, N, K, int(EPI_CROSS), xs);
   return hipGetLastError();
 }
 

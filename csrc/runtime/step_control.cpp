@@ -23,7 +23,13 @@ namespace dtfs {
 namespace runtime {
 
 namespace {
-constexpr uint64_t kMagic = 0x4454465343544c31ull;  // "DTFSCTL1"
+constexpr uint64_t kMagic = 0x4454465343544c32ull;  // "DTFSCTL2" (CtlRank gained pidns)
+
+// Inode of this process's PID namespace (0 if /proc is not readable).
+uint64_t pid_namespace() {
+  struct stat st;
+  return ::stat("/proc/self/ns/pid", &st) == 0 ? uint64_t(st.st_ino) : 0;
+}
 
 uint64_t tag(uint64_t k, int bucket) { return ((k + 1) << 16) | uint64_t(uint16_t(bucket)); }
 
@@ -77,14 +83,22 @@ StepControl::StepControl(const std::string& name, int world, int rank, bool crea
     }
   }
   attach_us_ = now_us();
+  my_pidns_ = pid_namespace();
+  s_->ranks[rank_].pidns.store(my_pidns_, std::memory_order_release);
   s_->ranks[rank_].pid.store(int32_t(getpid()), std::memory_order_release);
   s_->ranks[rank_].attached.store(1, std::memory_order_release);
   heartbeat();
 }
 
 bool StepControl::process_gone(int r) const {
+  if (r < 0 || r >= world_) throw std::out_of_range("step control: rank out of range");
   const int32_t pid = s_->ranks[r].pid.load(std::memory_order_acquire);
-  return pid > 0 && ::kill(pid, 0) != 0 && errno == ESRCH;  // signal 0: existence probe only
+  // a pid names the peer only inside the peer's own PID namespace: ranks in
+  // other namespaces sharing /dev/shm (sidecar containers) are judged by their
+  // heartbeat alone
+  const uint64_t ns = s_->ranks[r].pidns.load(std::memory_order_acquire);
+  if (pid <= 0 || ns == 0 || ns != my_pidns_) return false;
+  return ::kill(pid, 0) != 0 && errno == ESRCH;  // signal 0: existence probe only
 }
 
 StepControl::~StepControl() {

@@ -42,6 +42,7 @@ struct alignas(64) CtlRank {
   std::atomic<uint32_t> closing;          // this rank stopped admitting and has nothing queued
   std::atomic<uint32_t> attached;
   std::atomic<int32_t> pid;               // the rank's process: a peer whose process is gone is dead at once
+  std::atomic<uint64_t> pidns;            // inode of its /proc/self/ns/pid: the pid probe is trusted only within one namespace
 };
 
 struct CtlShared {
@@ -123,6 +124,7 @@ class StepControl {
   int world_, rank_;
   CtlShared* s_ = nullptr;
   int64_t attach_us_ = 0;
+  uint64_t my_pidns_ = 0;  // this process's PID namespace inode (process_gone)
   std::atomic<bool> abort_{false};
 };
 

@@ -160,11 +160,19 @@ class HotRowCache:
     whole; the sample period (0 = ``sample_every``) lets a learning phase
     sample every candidate without re-capturing the step's graphs.
 
-    Slot safety: :meth:`refresh` first waits for the device (every step that
-    could still read the index replaced by the previous refresh is done); the
-    rows it adds go only into slots the CURRENT index does not reference, and
-    it keeps at most ``fill`` x capacity rows hot so there are free slots for
-    the next turnover."""
+    Slot safety: :meth:`refresh` first waits until every step that could still
+    read the index replaced by the previous refresh is done; the rows it adds
+    go only into slots the CURRENT index does not reference, and it keeps at
+    most ``fill`` x capacity rows hot so there are free slots for the next
+    turnover. The wait is one event: with the serving step's stream registered
+    (:meth:`set_step_stream`, the live server's StepRunner compute stream -
+    every kernel of a peer-exchange step runs there), each swap records an
+    event on it once the swap's store has landed, and the next refresh waits
+    for that event alone (the steps enqueued before it; later steps read the
+    new index). Without a registered stream it falls back to a device-wide
+    synchronize. The refresh's own kernels (unique / topk / fill, a few ms
+    once per refresh period) run on a side stream of their own so they overlap
+    the steps instead of queueing between them."""
 
     def __init__(self, peer: PeerTables, capacity: Optional[int] = -1, ring_cap: Optional[int] = None,
                  sample_every: int = 8, decay: float = 0.5, fill: float = 0.75):
@@ -200,6 +208,8 @@ class HotRowCache:
         self.last_error: Optional[str] = None
         self.last_filled = 0
         self._stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._step_stream = None  # set_step_stream: the stream the serving steps run on
+        self._fence = None        # event on it after the last swap: older steps are done when it is
         self._lock = threading.Lock()
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
@@ -269,10 +279,26 @@ class HotRowCache:
         with self._lock:
             return self._refresh()
 
+    def set_step_stream(self, stream_ptr: int) -> None:
+        """Register the raw HIP stream the serving steps run on (every kernel
+        that reads the cache): refreshes then fence on one event there instead
+        of synchronizing the whole device."""
+        if self.device.type == "cuda" and stream_ptr:
+            self._step_stream = torch.cuda.ExternalStream(int(stream_ptr), device=self.device)
+            self._fence = None
+
+    def _wait_old_readers(self) -> None:
+        """Every step that may read the index replaced by the previous swap
+        (the one this refresh rebuilds) is done."""
+        if self._step_stream is None:
+            torch.cuda.synchronize(self.device)
+        elif self._fence is not None:
+            self._fence.synchronize()  # host wait on one event: this thread only
+
     def _refresh(self) -> int:
         cuda = self.device.type == "cuda"
-        if cuda:  # every step that may read the previously replaced index is done
-            torch.cuda.synchronize(self.device)
+        if cuda:
+            self._wait_old_readers()
         with (torch.cuda.stream(self._stream) if cuda else nullcontext()):
             samp = self.ring.clone()
             self.ring.fill_(-1)  # each refresh counts only the keys pushed since the last one
@@ -313,7 +339,11 @@ class HotRowCache:
                     hip().cache_index_build(keys, slots, idx)
                 self.desc[0:1].fill_(self.index[side].data_ptr())  # one 8-byte store: the swap
         if cuda:
-            self._stream.synchronize()
+            self._stream.synchronize()  # the swap's store has landed
+            if self._step_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(self._step_stream)  # steps enqueued from here on read the new index
+                self._fence = ev
         self.keys, self.slots = keys, slots
         self.active = side
         self.refreshes += 1

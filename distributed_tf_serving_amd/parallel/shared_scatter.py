@@ -63,19 +63,46 @@ def create_shared_scatter(module, world: int, rank: int, fields: int, n_arenas: 
     return seg
 
 
+def expected_row_bytes(fields: int, narrow_modulo: int = 0, narrow_wts_cols: int = 0) -> int:
+    """Arena payload bytes one candidate row takes, for placing each rank's
+    share of a batch on its NUMA node. Raw tensor_content: 8 B id + 4 B weight
+    per feature + framing. Narrowed on the host (GPU live servers, the
+    default; csrc/runtime/narrow.h): 3-byte rows for tables of <= 2^24 rows
+    (else 4) + the row's weights + its 8-byte row-table entry. Weights are
+    priced as fp32, the widest form a narrowed request carries (bf16-exact
+    weights travel in 2 bytes, all-ones in none): the placement then matches
+    the heaviest traffic, where it matters."""
+    if narrow_modulo <= 0:
+        return 12 * fields + 16
+    idb = 3 if narrow_modulo <= (1 << 24) else 4
+    wcols = narrow_wts_cols if 0 < narrow_wts_cols < fields else fields
+    return idb * fields + 4 * wcols + 8
+
+
+def live_narrowing(model, cuda: bool, narrow: bool = True):
+    """(narrow_modulo, narrow_wts_cols) the live server will use for this model
+    (serving/live.py: GPU servables narrow on the host by default)."""
+    from ..serving.packing import host_narrow_modulo
+
+    m = host_narrow_modulo(model.cfg) if (narrow and cuda) else 0
+    wc = int(getattr(model, "narrow_weight_cols", lambda: 0)()) if m else 0
+    return m, wc
+
+
 def scatter_for_engine(ctx, fields: int, arena_cap: int, slots: int, max_rows_per_rank: int, tag: str = "serve",
-                       store=None, n_arenas: int = 0):
+                       store=None, n_arenas: int = 0, narrow_modulo: int = 0, narrow_wts_cols: int = 0):
     """The segment of a scatter-mode job on one node (None for one rank).
-    ``n_arenas`` defaults to what the live server allocates (slots + 3)."""
+    ``n_arenas`` defaults to what the live server allocates (slots + 3).
+    ``narrow_modulo`` / ``narrow_wts_cols``: the live server's host narrowing
+    (serving/live.py), which sets how many bytes each rank's share takes."""
     if ctx.world <= 1:
         return None
     from ..ops import hip, native
     from ..utils.affinity import current_node
 
     cuda = ctx.device.type == "cuda"
-    # a full batch's request bytes (raw tensor_content: 8 B id + 4 B weight per
-    # feature, + framing): where each rank's share of an arena will sit
-    expected = ctx.world * max_rows_per_rank * (12 * fields + 16)
+    # a full batch's request bytes: where each rank's share of an arena will sit
+    expected = ctx.world * max_rows_per_rank * expected_row_bytes(fields, narrow_modulo, narrow_wts_cols)
     return create_shared_scatter(hip() if cuda else native(), ctx.world, ctx.rank, fields, n_arenas or slots + 3,
                                  arena_cap, slots, ctx.world * max_rows_per_rank, store=store,
                                  prefix=f"dtfs/scatter/{tag}", node=current_node() if cuda else -1, register=cuda,

@@ -119,6 +119,11 @@ class LiveScheduler:
             spec = [(R, engine.loop_slots(B)) for B, R in zip(self.buckets, self.step_rows)]
             self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas, control, seg,
                                         self.buckets if seg is not None else None)
+            cache = getattr(model, "cache", None)
+            if cache is not None and hasattr(cache, "set_step_stream"):
+                # the peer-exchange step's kernels all run on the runner's compute
+                # stream: replica-cache refreshes fence on an event there
+                cache.set_step_stream(engine.runner().compute_stream)
         else:
             slots = self.ex.slots
             scores = [[engine.host_out(B, s) for B in self.buckets] for s in range(slots)]

@@ -91,10 +91,11 @@ def build_engine(cfg: Config, device=None, slots: int = 3, ctx: Optional[DistCon
         arena = ArenaLayout(cfg.model.num_fields, max_rows=rows_in, gpu_varint=not shared)
         seg = None
         if shared:
-            from ..parallel.shared_scatter import scatter_for_engine
+            from ..parallel.shared_scatter import live_narrowing, scatter_for_engine
 
+            nm, nw = live_narrowing(model, dev.type == "cuda", bool(getattr(sc, "narrow_ingest", True)))
             seg = scatter_for_engine(ctx, cfg.model.num_fields, arena.capacity, slots, max(buckets),
-                                     tag=scatter_tag, store=store)
+                                     tag=scatter_tag, store=store, narrow_modulo=nm, narrow_wts_cols=nw)
         eng = FanoutEngine(ex, ctx, mode=mode, ingest="arena", group=group, arena=arena, shared_scatter=seg)
     else:
         eng = FanoutEngine(ex, ctx, mode=mode, group=group)

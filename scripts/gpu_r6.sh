@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU steps on one MI355X; each step under its own time limit, the script stops at the first failure.
 #   TESTS="tests" SMOKE=1 BENCHES="--model deepfm;--model dlrm" PROFS="deepfm|--model deepfm;ff|--model deepfm --force-fanout" \
-#     STUDY=tools.studies.microbench STUDY_ARGS=--tail bash scripts/gpu_r5.sh
+#     COUNTERS="deepfm dcn_v2" STUDY=tools.studies.microbench STUDY_ARGS=--tail bash scripts/gpu_r6.sh
 # BENCHES / PROFS: ';'-separated bench.py argument sets (leading VAR=value words are environment settings);
 # PROFS entries are tag|args: a kernel + copy trace (rocprofv3 --kernel-trace --memory-copy-trace --stats,
 # never with counters) summarised by tools/prof_summary.py into gpurun_out/prof_summary_<tag>.md.
@@ -28,6 +28,29 @@ if [ -n "${STUDY:-}" ]; then
   timeout -k 10 ${STUDY_TIMEOUT:-300} python -u -m $STUDY ${STUDY_ARGS:-} > gpurun_out/study.log 2>&1 \
     || { echo "study failed"; tail -30 gpurun_out/study.log; exit 1; }
   cat gpurun_out/study.log
+fi
+if [ -n "${COUNTERS:-}" ]; then
+  # counter passes (rocprofv3 --pmc, one run each, kernel trace only - never with a sys/runtime trace)
+  OUT=gpurun_out/ctr6
+  rm -rf $OUT && mkdir -p $OUT
+  P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+  P2="FETCH_SIZE GRBM_GUI_ACTIVE"
+  P3="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
+  P4="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+  for model in $COUNTERS; do
+    rows=16384; [ $model = dcn_v2 ] && rows=8192
+    i=0
+    for pass in "$P1" "$P2" "$P3" "$P4"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d $OUT/${model}_p$i -o run \
+        -- python3 -m tools.studies.kernel_drive --model $model --rows $rows --iters 10 \
+        > $OUT/${model}_p$i.log 2>&1 || { echo "pass $i of $model failed"; tail -5 $OUT/${model}_p$i.log; exit 1; }
+    done
+    python -m tools.counters_summary $OUT --only ${model}_ \
+      --title "$model serving-shape forward ($rows rows), 1 MI355X (rocprofv3 --pmc, 4 passes)" > $OUT/summary_$model.md
+    cat $OUT/summary_$model.md
+    rm -rf $OUT/${model}_p*  # raw CSVs: tens of MB each (gpurun copies back <= 64 MiB)
+  done
 fi
 if [ -n "${BENCHES:-}" ]; then
   IFS=';' read -ra SETS <<< "$BENCHES"

@@ -278,11 +278,15 @@ def test_ipc_export_open_same_process(cuda):
 
 
 @pytest.mark.gpu
-def test_refresh_while_lookups_run(cuda):
+@pytest.mark.parametrize("fence", [False, True])
+def test_refresh_while_lookups_run(cuda, fence):
     """Refreshes (new rows copied into free slots, the other index built and
     swapped in by one 8-byte store) while another thread keeps launching
-    cached lookups on its own stream: every lookup returns exactly the rows of
-    the uncached lookup, through hot-set turnover."""
+    cached lookups on its own stream, four in flight at a time: every lookup
+    returns exactly the rows of the uncached lookup, through hot-set turnover.
+    fence: the lookups' stream is registered (set_step_stream, as the live
+    server registers its compute stream) and each refresh waits for the event
+    recorded there after the previous swap instead of the whole device."""
     import threading
     import time
 
@@ -297,18 +301,19 @@ def test_refresh_while_lookups_run(cuda):
     dense = torch.randn(B, 64, generator=g).to(torch.bfloat16).to(cuda)
     want = [ops.dot_interaction_gather_peer(dense, ids, p, None) for ids in batches]
     torch.cuda.synchronize()
+    s = torch.cuda.Stream(cuda)
+    if fence:
+        c.set_step_stream(s.cuda_stream)
     stop, errs, done = threading.Event(), [], [0]
 
     def worker():
-        s = torch.cuda.Stream(cuda)
         k = 0
         with torch.cuda.stream(s):
             while not stop.is_set():
-                z = ops.dot_interaction_gather_peer(dense, batches[k % 3], p, c)
+                zs = [(k + j, ops.dot_interaction_gather_peer(dense, batches[(k + j) % 3], p, c)) for j in range(4)]
                 s.synchronize()
-                if not torch.equal(z, want[k % 3]):
-                    errs.append(k)
-                k += 1
+                errs.extend(i for i, z in zs if not torch.equal(z, want[i % 3]))
+                k += 4
         done[0] = k
 
     t = threading.Thread(target=worker)
@@ -322,5 +327,6 @@ def test_refresh_while_lookups_run(cuda):
         t.join(timeout=60)
     assert not errs, errs[:5]
     assert done[0] > 12 and c.refreshes == 12 and c.keys.numel() > 0
+    assert (c._fence is not None) == fence
     h, m = c.counts()
     assert h > 0

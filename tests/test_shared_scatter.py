@@ -161,3 +161,21 @@ def test_numa_placement_puts_each_share_on_its_reader_node():
             native().SharedScatter(name + "c", world, 0, True, F, 3, lay.capacity, 2, world * B, -1, [0, 1], expected)
     finally:
         seg.unlink()
+
+
+def test_placement_sizes_shares_from_the_narrowed_rows():
+    """The per-rank NUMA ranges follow the bytes a share actually takes: GPU
+    live servers narrow requests on the host (3-byte rows for tables of <= 2^24
+    rows, weights, an 8-byte row-table entry), far below raw tensor_content."""
+    from distributed_tf_serving_amd.config import ModelConfig
+    from distributed_tf_serving_amd.models import build_model
+    from distributed_tf_serving_amd.parallel.shared_scatter import expected_row_bytes, live_narrowing
+
+    assert expected_row_bytes(43) == 12 * 43 + 16
+    assert expected_row_bytes(43, 1_000_000) == 3 * 43 + 4 * 43 + 8
+    assert expected_row_bytes(43, 1 << 30) == 4 * 43 + 4 * 43 + 8
+    assert expected_row_bytes(39, 1 << 20, narrow_wts_cols=13) == 3 * 39 + 4 * 13 + 8
+    m = build_model(ModelConfig(family="deepfm", vocab_size=1000, embed_dim=16, num_fields=8, mlp_dims=[16]), "cpu")
+    assert live_narrowing(m, cuda=False) == (0, 0)  # CPU servables do not narrow
+    assert live_narrowing(m, cuda=True) == (1000, 0)
+    assert live_narrowing(m, cuda=True, narrow=False) == (0, 0)

@@ -123,5 +123,8 @@ def test_exited_peer_is_dead_at_once():
         assert c0.process_gone(1) and not c0.process_gone(0)
         assert c0.heartbeat_age(1) > 1e6
         assert time.monotonic() - t0 < 1.0
+        for r in (-1, 2, 64):  # bounds-checked: no read past the segment's ranks
+            with pytest.raises(IndexError):
+                c0.process_gone(r)
     finally:
         c0.unlink()
