@@ -161,10 +161,11 @@ def parse_args():
                     help="keep the fan-out collectives on a 1-GPU run (exercises the N>1 step path)")
     ap.add_argument("--step-timeout-s", type=float, default=30.0,
                     help="a step not finished by then fails the run instead of hanging it")
-    ap.add_argument("--h2d-wait", default=None, choices=["host", "device"],
+    ap.add_argument("--h2d-wait", default=None, choices=["host", "device", "feed"],
                     help="local steps: the launcher waits for each step's H2D copy on the host before it enqueues "
-                         "the kernels (copies never overlap) or the compute stream waits on the device (the next "
-                         "step's copy starts at once); default: the runtime's")
+                         "the kernels (host: copies never overlap), the compute stream waits on the copy's event on "
+                         "the device (device), or a feeder thread enqueues the kernels once the host sees the copy "
+                         "landed while the launcher issues the next copies (feed); default: the runtime's (feed)")
     ap.add_argument("--embed-geometry", default=None, metavar="WAVES,ROWS",
                     help="pipelined gather geometry for a study: resident-wave cap and rows in flight per wave "
                          "(default: the kernel's 4096,1)")
@@ -274,6 +275,7 @@ def build(a, ctx):
         eng.prepare(b)
     if a.h2d_wait and dev.type == "cuda":
         eng.runner().host_wait_h2d = a.h2d_wait == "host"
+        eng.runner().feed_h2d = a.h2d_wait == "feed"
     if eng.program_active or eng.mode != "local":
         # one synthetic step of every bucket checked against a local / eager
         # forward on every rank (collective): a fan-out that scores wrong is

@@ -1824,6 +1824,25 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("narrow_modulo") = 0);
   m.def("arena_varint_decode", &arena_varint_decode, py::arg("arena"), py::arg("blocks") = 256);
   m.def("pull_host", &pull_host, py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("blocks") = 128);
+  // stream-ordered 32-bit flag write / wait (a lighter cross-queue dependency
+  // than an event; tools/studies/step_gap_study.py)
+  m.def(
+      "stream_write_u32",
+      [](uintptr_t stream, torch::Tensor flag, uint32_t value) {
+        TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 GPU tensor");
+        check_hip(hipStreamWriteValue32(reinterpret_cast<hipStream_t>(stream), flag.data_ptr(), value, 0),
+                  "hipStreamWriteValue32");
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("value"));
+  m.def(
+      "stream_wait_u32",
+      [](uintptr_t stream, torch::Tensor flag, uint32_t value) {
+        TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == torch::kInt32 && flag.numel() >= 1, "flag: int32 GPU tensor");
+        check_hip(hipStreamWaitValue32(reinterpret_cast<hipStream_t>(stream), flag.data_ptr(), value,
+                                       hipStreamWaitValueGte, 0xffffffffu),
+                  "hipStreamWaitValue32");
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("value"));
   m.def("sort_scores", &sort_scores, py::arg("scores"), py::arg("descending") = false, py::arg("k") = -1);
   m.def("sort_max_elems", &dtfs::sort_max_elems);
 
@@ -1892,6 +1911,9 @@ PYBIND11_MODULE(_hip, m) {
           "Bounded wait for the slot's step: (ok, error). Also polls the communicators' async errors.")
       .def("query", &dtfs::runtime::StepRunner::query, py::arg("slot"))
       .def_property_readonly("slots", &dtfs::runtime::StepRunner::slots)
+      .def_property("feed_h2d", &dtfs::runtime::StepRunner::feed_h2d, &dtfs::runtime::StepRunner::set_feed_h2d,
+                    "local steps: a feeder thread enqueues each step's kernels once the host sees its H2D landed "
+                    "(True, default) instead of a device-side wait on the copy's event")
       .def_property("host_wait_h2d", &dtfs::runtime::StepRunner::host_wait_h2d,
                     &dtfs::runtime::StepRunner::set_host_wait_h2d,
                     "local steps: wait for each step's H2D on the host (True) or on the device (False)")

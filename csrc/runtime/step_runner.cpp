@@ -49,9 +49,24 @@ StepRunner::StepRunner(int device, int slots) : device_(device) {
     ck(hipEventCreateWithFlags(&h2d_done_[i], hipEventDisableTiming), "hipEventCreate");
     ck(hipEventCreateWithFlags(&done_[i], done_flags), "hipEventCreate");
   }
+  queued_.reset(new std::atomic<uint64_t>[size_t(slots)]);
+  launched_.reset(new std::atomic<uint64_t>[size_t(slots)]);
+  for (int i = 0; i < slots; ++i) {
+    queued_[i].store(0);
+    launched_[i].store(0);
+  }
+  if (const char* e = std::getenv("DTFS_FEED_H2D")) feed_h2d_ = std::atoi(e) != 0;
 }
 
 StepRunner::~StepRunner() {
+  if (feeder_.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(feed_mu_);
+      feed_stop_ = true;
+    }
+    feed_cv_.notify_all();
+    feeder_.join();
+  }
   hipSetDevice(device_);
   for (hipStream_t s : {compute_, copy_, copy2_, ingress_, egress_})
     if (s) hipStreamSynchronize(s);
@@ -135,8 +150,76 @@ void StepRunner::h2d(int slot, void* dst, const void* src, int64_t nbytes, hipSt
   h2d_copies(slot, dst, one, consumer, alternate);
 }
 
+// Feeder: local steps' kernels, enqueued in launch order once their copy landed.
+void StepRunner::feed(const FeedJob& j) {
+  if (!feeder_.joinable()) feeder_ = std::thread([this] { feeder_loop(); });
+  queued_[j.slot].fetch_add(1, std::memory_order_acq_rel);
+  {
+    std::lock_guard<std::mutex> lk(feed_mu_);
+    feed_q_.push_back(j);
+  }
+  feed_cv_.notify_one();
+}
+
+void StepRunner::feeder_loop() {
+  try {
+    ck(hipSetDevice(device_), "hipSetDevice(feeder)");
+    for (;;) {
+      FeedJob j;
+      {
+        std::unique_lock<std::mutex> lk(feed_mu_);
+        feed_cv_.wait(lk, [&] { return feed_stop_ || !feed_q_.empty(); });
+        if (feed_q_.empty()) return;  // stopping, nothing left
+        j = feed_q_.front();
+      }
+      // the copy: spin-yield for the first 2 ms (it normally landed long ago:
+      // the next step's copy runs under the current step's kernels), then
+      // 20 us sleeps; the runner's destruction ends the wait
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t e = hipEventQuery(h2d_done_[j.slot]);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) ck(e, "hipEventQuery(h2d, feeder)");
+        {
+          std::lock_guard<std::mutex> lk(feed_mu_);
+          if (feed_stop_) return;
+        }
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+      if (j.seq) {
+        j.seq->launch(compute_, done_[j.slot], true, j.skip_varint);
+      } else {
+        ck(hipGraphLaunch(j.graph, compute_), "hipGraphLaunch(feeder)");
+        ck(hipEventRecord(done_[j.slot], compute_), "hipEventRecord(done, feeder)");
+      }
+      {
+        std::lock_guard<std::mutex> lk(feed_mu_);
+        feed_q_.pop_front();
+      }
+      launched_[j.slot].fetch_add(1, std::memory_order_acq_rel);
+    }
+  } catch (const std::exception& e) {
+    feed_error_ = e.what();
+    feed_failed_.store(true, std::memory_order_release);
+    std::fprintf(stderr, "[step_runner] feeder: %s\n", e.what());
+  }
+}
+
+void StepRunner::wait_slot_launched(int slot) const {
+  while (!slot_launched(slot) && !feed_failed_.load(std::memory_order_acquire)) std::this_thread::yield();
+}
+
+void StepRunner::drain_feeder() const {
+  for (int s = 0; s < int(done_.size()); ++s) wait_slot_launched(s);
+}
+
 void StepRunner::h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& copies, hipStream_t consumer,
                             bool alternate) {
+  // the slot's previous job must be on the device before its events are
+  // re-recorded or waited on (the live server observed that step complete,
+  // so this is normally already true)
+  wait_slot_launched(slot);
   hipStream_t st = copy_;
   if (alternate) {
     if (!copy2_) ck(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking), "hipStreamCreate(copy2)");
@@ -170,7 +253,7 @@ void StepRunner::h2d_copies(int slot, void* dst, const std::vector<ShareCopy>& c
       if (e != hipErrorNotReady) ck(e, "hipEventQuery(h2d)");
       std::this_thread::yield();
     }
-  } else {
+  } else if (consumer) {  // null: the feeder waits for the copy on the host
     ck(hipStreamWaitEvent(consumer, h2d_done_[slot], 0), "hipStreamWaitEvent(h2d)");
   }
   observed_[slot].store(false, std::memory_order_release);
@@ -181,6 +264,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   if (!s.cin || !s.cout || !(s.forward || s.forward_seq))
     throw std::invalid_argument("fan-out step needs both communicators and a forward");
   ck(hipSetDevice(device_), "hipSetDevice");
+  drain_feeder();
   ensure_fanout_streams();
   // copy (WAR on the slot's buffers), then ingress: unpack + row exchange, off
   // the compute stream
@@ -266,6 +350,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
+  drain_feeder();
   ensure_aux_stream(true);  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
@@ -327,6 +412,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
 void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hipGraphExec_t graph) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
+  drain_feeder();
   h2d(slot, dst, src, nbytes, compute_, true);
   ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
@@ -338,6 +424,13 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
+  if (feed_h2d_ && !host_wait_h2d_ && nbytes > 0) {
+    h2d(slot, dst, src, nbytes, nullptr, true);
+    used_[slot] = 1;
+    feed(FeedJob{slot, seq, nullptr, skip_varint});
+    return;
+  }
+  drain_feeder();  // keep launch order on the compute stream
   h2d(slot, dst, src, nbytes, compute_, true);
   seq->launch(compute_, done_[slot], true, skip_varint);
   used_[slot] = 1;
@@ -348,6 +441,15 @@ void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq && !graph) throw std::invalid_argument("launch_copies: no kernel sequence or graph");
   ck(hipSetDevice(device_), "hipSetDevice");
+  int64_t nbytes = 0;
+  for (const ShareCopy& c : copies) nbytes += c.n > 0 ? c.n : 0;
+  if (feed_h2d_ && !host_wait_h2d_ && nbytes > 0) {
+    h2d_copies(slot, dst, copies, nullptr, true);
+    used_[slot] = 1;
+    feed(FeedJob{slot, seq, seq ? nullptr : graph, skip_varint});
+    return;
+  }
+  drain_feeder();
   h2d_copies(slot, dst, copies, compute_, true);
   if (seq) {
     seq->launch(compute_, done_[slot], true, skip_varint);
@@ -360,6 +462,8 @@ void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>
 
 void StepRunner::wait(int slot) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
+  wait_slot_launched(slot);
+  if (feed_failed_.load(std::memory_order_acquire)) throw std::runtime_error("step feeder: " + feed_error_);
   if (used_[slot]) ck(hipEventSynchronize(done_[slot]), "hipEventSynchronize");
   observed_[slot].store(true, std::memory_order_release);
 }
@@ -372,7 +476,12 @@ bool StepRunner::wait_for(int slot, int64_t timeout_us, const std::vector<comm::
   auto last_comm_check = t0;
   if (used_[slot]) {
     for (;;) {
-      const hipError_t e = hipEventQuery(done_[slot]);
+      if (feed_failed_.load(std::memory_order_acquire)) {
+        *err = "step feeder: " + feed_error_;
+        return false;
+      }
+      // a job still with the feeder has not recorded its done event yet
+      const hipError_t e = slot_launched(slot) ? hipEventQuery(done_[slot]) : hipErrorNotReady;
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) {
         *err = std::string("hipEventQuery: ") + hipGetErrorString(e);
@@ -415,6 +524,10 @@ bool StepRunner::wait_for(int slot, int64_t timeout_us, const std::vector<comm::
 
 bool StepRunner::query(int slot) {
   if (!used_[slot]) return true;
+  if (!slot_launched(slot)) {
+    if (feed_failed_.load(std::memory_order_acquire)) throw std::runtime_error("step feeder: " + feed_error_);
+    return false;
+  }
   hipError_t e = hipEventQuery(done_[slot]);
   if (e == hipErrorNotReady) return false;
   ck(e, "hipEventQuery");

@@ -13,9 +13,13 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../comm/rccl_comm.h"
@@ -166,6 +170,13 @@ class StepRunner {
   // copy's event on the device (false) - see h2d().
   void set_host_wait_h2d(bool v) { host_wait_h2d_ = v; }
   bool host_wait_h2d() const { return host_wait_h2d_; }
+  // Local steps (launch_seq / launch_copies): a feeder thread enqueues each
+  // step's kernels once the host sees its H2D landed, so the compute queue
+  // carries no cross-queue wait packet (true, the default), or the compute
+  // stream waits on the copy's event on the device (false). Set before the
+  // first launch.
+  void set_feed_h2d(bool v) { feed_h2d_ = v; }
+  bool feed_h2d() const { return feed_h2d_; }
 
  private:
   int device_;
@@ -190,6 +201,36 @@ class StepRunner {
   int last_prog_slot_ = -1;
   int aux_cus_ = 0;  // CUs of the program aux lane's queue (0: unmasked)
   std::vector<char> used_;  // not vector<bool>: written by the launcher, read by the waiter
+
+  // feeder (feed_h2d_): local steps whose kernels wait for their H2D on the host
+  // The compute queue then holds no barrier packet in front of a step: an
+  // event wait on the SDMA copy costs ~6 us of idle GPU at every step boundary
+  // even when the copy landed long before (tools/native/step_gap.hip: 221.9 vs
+  // 217.3 us per launch for a 216 us kernel), and a host-observed copy needs
+  // none - its bytes are visible to every kernel enqueued after that.
+  struct FeedJob {
+    int slot = 0;
+    const KernelSequence* seq = nullptr;
+    hipGraphExec_t graph = nullptr;
+    bool skip_varint = false;
+  };
+  bool feed_h2d_ = true;
+  std::thread feeder_;
+  std::mutex feed_mu_;
+  std::condition_variable feed_cv_;
+  std::deque<FeedJob> feed_q_;
+  bool feed_stop_ = false;
+  std::atomic<bool> feed_failed_{false};
+  std::string feed_error_;  // written once by the feeder before feed_failed_ is set
+  // per slot: jobs handed to the feeder / jobs it has enqueued on the device
+  std::unique_ptr<std::atomic<uint64_t>[]> queued_, launched_;
+  void feed(const FeedJob& j);
+  void feeder_loop();
+  bool slot_launched(int slot) const {
+    return launched_[slot].load(std::memory_order_acquire) == queued_[slot].load(std::memory_order_acquire);
+  }
+  void wait_slot_launched(int slot) const;  // spin until the feeder enqueued the slot's last job
+  void drain_feeder() const;                 // ... every slot's
 };
 
 }  // namespace runtime

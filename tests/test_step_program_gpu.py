@@ -151,17 +151,18 @@ def test_gather_gemm_resolved_on_another_stream_is_identical(cuda):
 
 
 def test_resolve_lane_program_engine_and_live_server(cuda, monkeypatch):
-    """A local DeepFM step at the gather-GEMM bucket runs as a two-lane program
-    (resolve on the aux lane after the H2D, the compute lane waits only for
-    it; the default), the small bucket as the one-stream step; self-check and
-    served requests match the model."""
+    """A local step at the gather-GEMM bucket runs as a two-lane program with
+    DTFS_RESOLVE_LANE=1 (resolve on the aux lane after the H2D, the compute
+    lane waits only for it), the small bucket as the one-stream step;
+    self-check and served requests match the model. DCN v1: DeepFM and
+    Wide&Deep resolve their rows inside the one-launch tower (no pass to move)."""
     from distributed_tf_serving_amd.client.synth import SyntheticRequests
     from distributed_tf_serving_amd.serving.live import LiveScheduler
     from distributed_tf_serving_amd.wire import schema as pb
     from distributed_tf_serving_amd.wire import tensor as T
 
     monkeypatch.setenv("DTFS_RESOLVE_LANE", "1")
-    cfg = ModelConfig(family="deepfm", vocab_size=100_003, embed_dim=64, mlp_dims=(1024, 512, 256))
+    cfg = ModelConfig(family="dcn", vocab_size=100_003, embed_dim=64, mlp_dims=(1024, 512, 256))
     m = build_model(cfg, cuda)
     F, S = cfg.num_fields, 3
     buckets = [2048, 16384]

@@ -78,7 +78,8 @@ def step_timeline(rows, copies, step_kernel: str, min_us: float) -> list:
     report the start-to-start period, the kernel time inside it and the idle
     rest - GPU-bound when idle ~ 0, host / copy-bound otherwise."""
     starts = [i for i, r in enumerate(rows) if step_kernel in r[0]]
-    per, busy, idle, h2d = [], [], [], []
+    per, busy, idle, h2d, late, after = [], [], [], [], [], []
+    big = [c for c in copies if c[4] >= (1 << 20) and "HOST_TO_DEVICE" in c[0]]  # the steps' request copies
     for a, b in zip(starts, starts[1:]):
         if rows[a][3] / 1e3 < min_us or rows[b][3] / 1e3 < min_us:
             continue
@@ -99,13 +100,25 @@ def step_timeline(rows, copies, step_kernel: str, min_us: float) -> list:
         busy.append(tot / 1e3)
         idle.append((t1 - t0 - tot) / 1e3)
         h2d.append(sum((min(e, t1) - max(s, t0)) for _, s, e, _, _ in copies if s < t1 and e > t0) / 1e3)
+        # the request copy step b waited for: the last large H2D that landed
+        # before b started; "late" = how long after the previous step's last
+        # kernel ended it landed (> 0: the step waited for its bytes)
+        fed = [c for c in big if c[2] <= t1]
+        if fed and cur_e is not None:
+            late.append((fed[-1][2] - cur_e) / 1e3)
+            after.append((t1 - fed[-1][2]) / 1e3)
     if not per:
         return ["", f"no back-to-back full steps of `{step_kernel}` (>= {min_us} us)"]
     med = statistics.median
     return ["", f"back-to-back full steps ({len(per)} pairs, step starts at `{step_kernel}` >= {min_us} us): "
             f"period {med(per):.1f} us, kernels busy {med(busy):.1f} us, GPU idle {med(idle):.1f} us, "
             f"copy time inside the period {med(h2d):.1f} us (medians; p10/p90 period "
-            f"{sorted(per)[len(per) // 10]:.1f} / {sorted(per)[9 * len(per) // 10]:.1f} us)"]
+            f"{sorted(per)[len(per) // 10]:.1f} / {sorted(per)[9 * len(per) // 10]:.1f} us)"] + (
+        [f"gap anatomy: the next step's request copy landed {med(late):.1f} us after the previous step's last kernel "
+         f"ended (p10/p90 {sorted(late)[len(late) // 10]:.1f} / {sorted(late)[9 * len(late) // 10]:.1f}; > 0 = the "
+         f"step waited for its H2D), and the step's first kernel started {med(after):.1f} us after that copy "
+         f"landed (p10/p90 {sorted(after)[len(after) // 10]:.1f} / {sorted(after)[9 * len(after) // 10]:.1f})"]
+        if late else [])
 
 
 def main():
