@@ -264,22 +264,31 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   if (!s.cin || !s.cout || !(s.forward || s.forward_seq))
     throw std::invalid_argument("fan-out step needs both communicators and a forward");
   ck(hipSetDevice(device_), "hipSetDevice");
-  drain_feeder();
   ensure_fanout_streams();
-  // copy (WAR on the slot's buffers), then ingress: unpack + row exchange, off
-  // the compute stream
+  // copy (WAR on the slot's buffers), then ingress: unpack + row exchange
   // one copy stream here: with the ingress / egress streams a second one
   // shares a hardware queue (GPU_MAX_HW_QUEUES = 4) and serialises the step
   // (329 vs 187 us per step measured)
+  // (fed like a local step - the feeder enqueuing the ingress once the host
+  // saw the copy, on the compute stream or the ingress lane - it measured
+  // slower: 109.2 / 112.0 and 105.4 vs 115.4 M with --force-fanout,
+  // profiles/r06_feed_h2d.md)
+  drain_feeder();
   h2d(slot, s.h2d_dst, s.h2d_src, s.h2d_bytes, ingress_, false);
-  if (s.ingress_seq) s.ingress_seq->launch(ingress_, nullptr, false, s.skip_varint);
-  else if (s.ingress) ck(hipGraphLaunch(s.ingress, ingress_), "hipGraphLaunch(ingress)");
-  if (s.mode == 0) s.cin->alltoall(s.send, s.recv, s.in_bytes, ingress_);
-  else s.cin->scatter(s.send, s.recv, s.in_bytes, 0, ingress_);
+  fanout_body(slot, s);
+  used_[slot] = 1;
+}
+
+void StepRunner::fanout_body(int slot, const FanoutStep& s) {
+  hipStream_t in = ingress_;
+  if (s.ingress_seq) s.ingress_seq->launch(in, nullptr, false, s.skip_varint);
+  else if (s.ingress) ck(hipGraphLaunch(s.ingress, in), "hipGraphLaunch(ingress)");
+  if (s.mode == 0) s.cin->alltoall(s.send, s.recv, s.in_bytes, in);
+  else s.cin->scatter(s.send, s.recv, s.in_bytes, 0, in);
   // the forward's resolve pass on this lane: step k+1's runs beside step k's forward
-  if (s.resolve_seq) s.resolve_seq->launch(ingress_);
-  else if (s.resolve) ck(hipGraphLaunch(s.resolve, ingress_), "hipGraphLaunch(resolve)");
-  ck(hipEventRecord(in_done_[slot], ingress_), "hipEventRecord(in)");
+  if (s.resolve_seq) s.resolve_seq->launch(in);
+  else if (s.resolve) ck(hipGraphLaunch(s.resolve, in), "hipGraphLaunch(resolve)");
+  ck(hipEventRecord(in_done_[slot], in), "hipEventRecord(in)");
   // compute: the forward graph
   ck(hipStreamWaitEvent(compute_, in_done_[slot], 0), "hipStreamWaitEvent(compute)");
   if (s.forward_seq) {
@@ -294,7 +303,6 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   else s.cout->gather(s.scores, s.back, s.out_bytes, 0, egress_);
   if (s.d2h_bytes > 0) copy_checked(s.h_out, s.back, s.d2h_bytes, hipMemcpyDeviceToHost, egress_, slot, "D2H");
   ck(hipEventRecord(done_[slot], egress_), "hipEventRecord(done)");
-  used_[slot] = 1;
 }
 
 void StepProgram::validate() const {

@@ -214,6 +214,9 @@ class StepRunner {
     hipGraphExec_t graph = nullptr;
     bool skip_varint = false;
   };
+  // a fan-out step after its H2D: ingress (unpack + row exchange), forward on
+  // the compute stream, egress (score exchange + D2H)
+  void fanout_body(int slot, const FanoutStep& s);
   bool feed_h2d_ = true;
   std::thread feeder_;
   std::mutex feed_mu_;
