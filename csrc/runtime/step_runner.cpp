@@ -187,7 +187,9 @@ void StepRunner::feeder_loop() {
         if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2)) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
-      if (j.seq) {
+      if (j.program) {
+        program_body(j.slot, j.prog, j.skip_varint, true);
+      } else if (j.seq) {
         j.seq->launch(compute_, done_[j.slot], true, j.skip_varint);
       } else {
         ck(hipGraphLaunch(j.graph, compute_), "hipGraphLaunch(feeder)");
@@ -358,7 +360,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
-  drain_feeder();
+  if (!(feed_h2d_ && !host_wait_h2d_ && h2d_bytes > 0)) drain_feeder();
   ensure_aux_stream(true);  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
@@ -373,12 +375,45 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alternate over two copy streams unless the fan-out streams exist too
   // (copy, copy2, compute, aux = GPU_MAX_HW_QUEUES 4; a fifth stream would
   // alias a queue and serialise the step)
+  if (feed_h2d_ && !host_wait_h2d_ && h2d_bytes > 0) {
+    // fed like a local step: the feeder enqueues the program once the host
+    // saw the copy land (program_body(fed): no lane waits just for the copy)
+    h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, nullptr, egress_ == nullptr);
+    used_[slot] = 1;
+    FeedJob j;
+    j.slot = slot;
+    j.skip_varint = skip_varint;
+    j.program = true;
+    j.prog = p;
+    feed(j);
+    return;
+  }
   h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, lanes[p.h2d_lane], egress_ == nullptr);
+  program_body(slot, p, skip_varint, false);
+  used_[slot] = 1;
+}
+
+void StepRunner::program_body(int slot, const StepProgram& p, bool skip_varint, bool fed) {
+  hipStream_t lanes[2] = {compute_, ingress_};
   hipEvent_t* ev = &prog_ev_[size_t(slot) * kProgEvents];
   const ProgOp* last = p.ops.empty() ? nullptr : &p.ops.back();
   const bool bound = last && last->kind == ProgOp::kKernels && last->lane == 0 && last->seq;
+  // fed: the copy is host-observed, so an aux-lane record with no aux work
+  // before it (the lane only carried the copy) joins nothing - it and the
+  // compute-lane waits on it are dropped (a cross-queue wait packet costs a
+  // few us of idle GPU even when satisfied)
+  bool aux_work = false, trivial[kProgEvents] = {};
   for (const ProgOp& o : p.ops) {
     hipStream_t st = lanes[o.lane];
+    if (fed) {
+      if (o.lane == 1 && o.kind != ProgOp::kRecord && o.kind != ProgOp::kWait && o.kind != ProgOp::kWaitPrev)
+        aux_work = true;
+      if (o.kind == ProgOp::kRecord && o.lane == 1 && !aux_work) {
+        trivial[o.event] = true;
+        continue;
+      }
+      if (o.kind == ProgOp::kWait && trivial[o.event]) continue;
+    }
     switch (o.kind) {
       case ProgOp::kKernels:
         if (o.seq) {
@@ -413,7 +448,6 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
     }
   }
   if (!bound) ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
-  used_[slot] = 1;
   last_prog_slot_ = slot;
 }
 

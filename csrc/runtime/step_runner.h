@@ -213,7 +213,10 @@ class StepRunner {
     const KernelSequence* seq = nullptr;
     hipGraphExec_t graph = nullptr;
     bool skip_varint = false;
+    bool program = false;  // a programmed step (prog): its ops after the H2D
+    StepProgram prog;
   };
+  void program_body(int slot, const StepProgram& p, bool skip_varint, bool fed);
   // a fan-out step after its H2D: ingress (unpack + row exchange), forward on
   // the compute stream, egress (score exchange + D2H)
   void fanout_body(int slot, const FanoutStep& s);
