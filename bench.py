@@ -536,7 +536,11 @@ def run_live(a, ctx, cfg, model, eng, B):
             done = 0
             while done < per_pass:
                 n = min(chunk, per_pass - done)
-                live.run_load(pool, warmup=0, count=n, concurrency=conc, threads=a.client_threads,
+                # this chunk's slice of the pool (run_load starts at its list's
+                # first request: the whole pool each time would replay the same
+                # first n requests every chunk and learn only their keys)
+                part = [pool[(done + i) % len(pool)] for i in range(n)]
+                live.run_load(part, warmup=0, count=n, concurrency=conc, threads=a.client_threads,
                               timeout_us=timeout_us)
                 cache.refresh()
                 done += n
