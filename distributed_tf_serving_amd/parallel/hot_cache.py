@@ -32,7 +32,9 @@ misses at odd entries, summed by :meth:`HotRowCache.counts`).
 """
 from __future__ import annotations
 
+import os
 import threading
+import time
 from contextlib import nullcontext
 from typing import List, Optional, Sequence, Tuple
 
@@ -145,6 +147,9 @@ def auto_capacity(peer: "PeerTables", free_bytes: Optional[int] = None, fraction
         free_bytes = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else 1 << 30
     fit = int(fraction * free_bytes) // CACHE_BYTES_PER_ROW
     return max(min(floor, remote_rows), min(remote_rows, fit))
+
+
+_DEBUG = os.environ.get("DTFS_CACHE_DEBUG", "0") == "1"  # per-phase refresh timings (synchronizing)
 
 
 class HotRowCache:
@@ -297,8 +302,17 @@ class HotRowCache:
 
     def _refresh(self) -> int:
         cuda = self.device.type == "cuda"
+        dbg = _DEBUG and cuda
+        marks = [("start", time.perf_counter())]
+
+        def mark(what):
+            if dbg:
+                self._stream.synchronize()
+                marks.append((what, time.perf_counter()))
+
         if cuda:
             self._wait_old_readers()
+            mark("fence")
         with (torch.cuda.stream(self._stream) if cuda else nullcontext()):
             samp = self.ring.clone()
             self.ring.fill_(-1)  # each refresh counts only the keys pushed since the last one
@@ -312,15 +326,18 @@ class HotRowCache:
                 s = torch.zeros(uk.numel(), dtype=torch.float32, device=self.device).scatter_add_(0, inv, score)
                 top = torch.topk(s, min(uk.numel(), 4 * self.cap)).indices  # sorted by score
                 self.cand_keys, self.cand_score = uk[top], s[top]
+            mark("count")
             target = min(self.cand_keys.numel(), max(1, int(self.fill * self.cap)))
             hot = self.cand_keys[:target]
             kept = torch.isin(self.keys, hot)
             kept_keys, kept_slots = self.keys[kept], self.slots[kept]
             new = hot[~torch.isin(hot, self.keys)]  # hottest first
+            mark("isin")
             used = torch.zeros(self.cap, dtype=torch.bool, device=self.device)
             if self.slots.numel():
                 used[self.slots.long()] = True  # referenced by the active index: not writable now
             free = (~used).nonzero().view(-1)
+            mark("free")
             new = new[:free.numel()]
             new_slots = free[:new.numel()].to(torch.int32)
             if new.numel():
@@ -329,6 +346,7 @@ class HotRowCache:
             slots = torch.cat([kept_slots, new_slots])
             order = torch.argsort(keys)
             keys, slots = keys[order].contiguous(), slots[order].contiguous()
+            mark("fill+sort")
             side = 0 if self.active != 0 else 1
             if cuda:
                 idx = self.index[side]
@@ -338,6 +356,7 @@ class HotRowCache:
 
                     hip().cache_index_build(keys, slots, idx)
                 self.desc[0:1].fill_(self.index[side].data_ptr())  # one 8-byte store: the swap
+            mark("index")
         if cuda:
             self._stream.synchronize()  # the swap's store has landed
             if self._step_stream is not None:
@@ -348,6 +367,9 @@ class HotRowCache:
         self.active = side
         self.refreshes += 1
         self.last_filled = int(new.numel())
+        if dbg:
+            t = [(w, round((b - a) * 1e3, 2)) for (_, a), (w, b) in zip(marks, marks[1:])]
+            print(f"[hot_cache] refresh {self.refreshes}: {t} ms, keys {int(keys.numel())}", flush=True)
         return self.last_filled
 
     def _fill(self, keys: torch.Tensor, slots: torch.Tensor) -> None:
