@@ -152,6 +152,15 @@ def auto_capacity(peer: "PeerTables", free_bytes: Optional[int] = None, fraction
 _DEBUG = os.environ.get("DTFS_CACHE_DEBUG", "0") == "1"  # per-phase refresh timings (synchronizing)
 
 
+def _member(x: torch.Tensor, sorted_set: torch.Tensor) -> torch.Tensor:
+    """Bool mask: x[i] in sorted_set (one binary search per element; torch.isin
+    re-sorts both inputs)."""
+    if sorted_set.numel() == 0:
+        return torch.zeros_like(x, dtype=torch.bool)
+    pos = torch.searchsorted(sorted_set, x).clamp_(max=sorted_set.numel() - 1)
+    return sorted_set[pos] == x
+
+
 class HotRowCache:
     """This rank's replica of hot rows of tables owned by other ranks.
 
@@ -165,19 +174,22 @@ class HotRowCache:
     whole; the sample period (0 = ``sample_every``) lets a learning phase
     sample every candidate without re-capturing the step's graphs.
 
-    Slot safety: :meth:`refresh` first waits until every step that could still
-    read the index replaced by the previous refresh is done; the rows it adds
-    go only into slots the CURRENT index does not reference, and it keeps at
-    most ``fill`` x capacity rows hot so there are free slots for the next
-    turnover. The wait is one event: with the serving step's stream registered
-    (:meth:`set_step_stream`, the live server's StepRunner compute stream -
-    every kernel of a peer-exchange step runs there), each swap records an
-    event on it once the swap's store has landed, and the next refresh waits
-    for that event alone (the steps enqueued before it; later steps read the
-    new index). Without a registered stream it falls back to a device-wide
-    synchronize. The refresh's own kernels (unique / topk / fill, a few ms
-    once per refresh period) run on a side stream of their own so they overlap
-    the steps instead of queueing between them."""
+    Slot safety: the rows a refresh adds go only into slots the CURRENT index
+    does not reference, it keeps at most ``fill`` x capacity rows hot so there
+    are free slots for the next turnover, and the index it rebuilds (the one
+    the previous refresh replaced) must no longer be read by any step. With the
+    serving step's stream registered (:meth:`set_step_stream`: the live
+    server's StepRunner compute stream, where every kernel of a peer-exchange
+    step runs) the refresh's kernels are enqueued on that stream, so stream
+    order alone keeps them behind every step that could still read the old
+    index and ahead of every step that reads the new one: no event, no
+    device-wide synchronize, no stream of its own. (A side stream beside the
+    steps stalled them for 10-30 s once refreshes ran while two ranks shared
+    one GPU, profiles/r06_hot_cache_refresh.md.) The price is the refresh's own
+    GPU time in the step stream, ~1.5 ms per refresh when the hot set did not
+    change (the index is then left as it is) and a few ms when it did.
+    Without a registered stream (tests, eager use) the refresh runs on a side
+    stream after a device-wide synchronize."""
 
     def __init__(self, peer: PeerTables, capacity: Optional[int] = -1, ring_cap: Optional[int] = None,
                  sample_every: int = 8, decay: float = 0.5, fill: float = 0.75):
@@ -213,8 +225,7 @@ class HotRowCache:
         self.last_error: Optional[str] = None
         self.last_filled = 0
         self._stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-        self._step_stream = None  # set_step_stream: the stream the serving steps run on
-        self._fence = None        # event on it after the last swap: older steps are done when it is
+        self._ordered = False  # set_step_stream: _stream IS the steps' stream
         self._lock = threading.Lock()
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
@@ -285,20 +296,11 @@ class HotRowCache:
             return self._refresh()
 
     def set_step_stream(self, stream_ptr: int) -> None:
-        """Register the raw HIP stream the serving steps run on (every kernel
-        that reads the cache): refreshes then fence on one event there instead
-        of synchronizing the whole device."""
+        """Run refreshes on the raw HIP stream the serving steps run on (every
+        kernel that reads the cache): stream-ordered with the steps."""
         if self.device.type == "cuda" and stream_ptr:
-            self._step_stream = torch.cuda.ExternalStream(int(stream_ptr), device=self.device)
-            self._fence = None
-
-    def _wait_old_readers(self) -> None:
-        """Every step that may read the index replaced by the previous swap
-        (the one this refresh rebuilds) is done."""
-        if self._step_stream is None:
-            torch.cuda.synchronize(self.device)
-        elif self._fence is not None:
-            self._fence.synchronize()  # host wait on one event: this thread only
+            self._stream = torch.cuda.ExternalStream(int(stream_ptr), device=self.device)
+            self._ordered = True
 
     def _refresh(self) -> int:
         cuda = self.device.type == "cuda"
@@ -310,9 +312,9 @@ class HotRowCache:
                 self._stream.synchronize()
                 marks.append((what, time.perf_counter()))
 
-        if cuda:
-            self._wait_old_readers()
-            mark("fence")
+        if cuda and not self._ordered:  # side stream: every step that may read the old index is done
+            torch.cuda.synchronize(self.device)
+            mark("sync")
         with (torch.cuda.stream(self._stream) if cuda else nullcontext()):
             samp = self.ring.clone()
             self.ring.fill_(-1)  # each refresh counts only the keys pushed since the last one
@@ -329,13 +331,28 @@ class HotRowCache:
             mark("count")
             target = min(self.cand_keys.numel(), max(1, int(self.fill * self.cap)))
             hot = self.cand_keys[:target]
-            kept = torch.isin(self.keys, hot)
+            hot_sorted = torch.sort(hot).values
+            if self.active >= 0 and hot_sorted.numel() == self.keys.numel() and torch.equal(hot_sorted, self.keys):
+                mark("same")
+                self.refreshes += 1
+                self.last_filled = 0
+                if dbg:
+                    print(f"[hot_cache] refresh {self.refreshes}: hot set unchanged "
+                          f"({(time.perf_counter() - marks[0][1]) * 1e3:.2f} ms)", flush=True)
+                return 0  # the active index already holds exactly this set
+            kept = _member(self.keys, hot_sorted)  # self.keys is sorted
             kept_keys, kept_slots = self.keys[kept], self.slots[kept]
-            new = hot[~torch.isin(hot, self.keys)]  # hottest first
-            mark("isin")
-            used = torch.zeros(self.cap, dtype=torch.bool, device=self.device)
-            if self.slots.numel():
-                used[self.slots.long()] = True  # referenced by the active index: not writable now
+            new = hot[~_member(hot, self.keys)]  # hottest first
+            mark("member")
+            # free slots for the new rows among the first |new| + |active| slots:
+            # at most |active| of those are referenced by the active index (not
+            # writable now), so the window holds enough - O(hot set) work and
+            # memory per refresh instead of O(capacity)
+            window = min(self.cap, int(new.numel()) + int(self.slots.numel()))
+            used = torch.zeros(window, dtype=torch.bool, device=self.device)
+            if self.slots.numel() and window:
+                act = self.slots.long()
+                used[act[act < window]] = True
             free = (~used).nonzero().view(-1)
             mark("free")
             new = new[:free.numel()]
@@ -359,10 +376,6 @@ class HotRowCache:
             mark("index")
         if cuda:
             self._stream.synchronize()  # the swap's store has landed
-            if self._step_stream is not None:
-                ev = torch.cuda.Event()
-                ev.record(self._step_stream)  # steps enqueued from here on read the new index
-                self._fence = ev
         self.keys, self.slots = keys, slots
         self.active = side
         self.refreshes += 1

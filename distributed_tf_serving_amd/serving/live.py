@@ -20,8 +20,6 @@ forward as its backend.
 """
 from __future__ import annotations
 
-import os
-
 import concurrent.futures as cf
 import logging
 from typing import List, Optional, Sequence
@@ -122,9 +120,9 @@ class LiveScheduler:
             self.srv = hip().LiveServer(engine.runner(), self.config, spec, self.arenas, control, seg,
                                         self.buckets if seg is not None else None)
             cache = getattr(model, "cache", None)
-            if cache is not None and hasattr(cache, "set_step_stream") and os.environ.get("DTFS_CACHE_FENCE", "1") != "0":
+            if cache is not None and hasattr(cache, "set_step_stream"):
                 # the peer-exchange step's kernels all run on the runner's compute
-                # stream: replica-cache refreshes fence on an event there
+                # stream: replica-cache refreshes run there, stream-ordered with them
                 cache.set_step_stream(engine.runner().compute_stream)
         else:
             slots = self.ex.slots

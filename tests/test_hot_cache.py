@@ -278,15 +278,16 @@ def test_ipc_export_open_same_process(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fence", [False, True])
-def test_refresh_while_lookups_run(cuda, fence):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_refresh_while_lookups_run(cuda, ordered):
     """Refreshes (new rows copied into free slots, the other index built and
     swapped in by one 8-byte store) while another thread keeps launching
     cached lookups on its own stream, four in flight at a time: every lookup
     returns exactly the rows of the uncached lookup, through hot-set turnover.
-    fence: the lookups' stream is registered (set_step_stream, as the live
-    server registers its compute stream) and each refresh waits for the event
-    recorded there after the previous swap instead of the whole device."""
+    ordered: the lookups' stream is registered (set_step_stream, as the live
+    server registers its compute stream) and the refreshes run on it,
+    stream-ordered with the lookups, instead of on a side stream after a
+    device-wide synchronize."""
     import threading
     import time
 
@@ -302,7 +303,7 @@ def test_refresh_while_lookups_run(cuda, fence):
     want = [ops.dot_interaction_gather_peer(dense, ids, p, None) for ids in batches]
     torch.cuda.synchronize()
     s = torch.cuda.Stream(cuda)
-    if fence:
+    if ordered:
         c.set_step_stream(s.cuda_stream)
     stop, errs, done = threading.Event(), [], [0]
 
@@ -327,6 +328,6 @@ def test_refresh_while_lookups_run(cuda, fence):
         t.join(timeout=60)
     assert not errs, errs[:5]
     assert done[0] > 12 and c.refreshes == 12 and c.keys.numel() > 0
-    assert (c._fence is not None) == fence
+    assert c._ordered == ordered
     h, m = c.counts()
     assert h > 0
