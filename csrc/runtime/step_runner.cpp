@@ -208,6 +208,22 @@ void StepRunner::feeder_loop() {
   }
 }
 
+// Feed this step (rather than enqueue it with a device-side wait) only while
+// the GPU is busy with earlier steps: that is where the wait packet costs idle
+// time between back-to-back steps. On an idle GPU the feeder thread's wake-up
+// (a condition variable, tens of us on a loaded host) would only add latency
+// to a lone request's step.
+bool StepRunner::want_feed(int64_t nbytes) {
+  if (!feed_h2d_ || host_wait_h2d_ || nbytes <= 0) return false;
+  {
+    std::lock_guard<std::mutex> lk(feed_mu_);
+    if (!feed_q_.empty()) return true;  // keep launch order: behind the jobs still queued
+  }
+  const int last = last_slot_;
+  if (last < 0 || !slot_launched(last)) return last >= 0;
+  return hipEventQuery(done_[last]) == hipErrorNotReady;
+}
+
 void StepRunner::wait_slot_launched(int slot) const {
   while (!slot_launched(slot) && !feed_failed_.load(std::memory_order_acquire)) std::this_thread::yield();
 }
@@ -276,6 +292,7 @@ void StepRunner::launch_fanout(int slot, const FanoutStep& s) {
   // slower: 109.2 / 112.0 and 105.4 vs 115.4 M with --force-fanout,
   // profiles/r06_feed_h2d.md)
   drain_feeder();
+  last_slot_ = slot;
   h2d(slot, s.h2d_dst, s.h2d_src, s.h2d_bytes, ingress_, false);
   fanout_body(slot, s);
   used_[slot] = 1;
@@ -360,7 +377,9 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
                                 bool skip_varint) {
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
-  if (!(feed_h2d_ && !host_wait_h2d_ && h2d_bytes > 0)) drain_feeder();
+  const bool fed = want_feed(h2d_bytes);
+  last_slot_ = slot;
+  if (!fed) drain_feeder();
   ensure_aux_stream(true);  // the aux lane is the ingress stream
   if (prog_ev_.empty()) {
     prog_ev_.resize(done_.size() * kProgEvents);
@@ -375,7 +394,7 @@ void StepRunner::launch_program(int slot, const StepProgram& p, const void* h2d_
   // alternate over two copy streams unless the fan-out streams exist too
   // (copy, copy2, compute, aux = GPU_MAX_HW_QUEUES 4; a fifth stream would
   // alias a queue and serialise the step)
-  if (feed_h2d_ && !host_wait_h2d_ && h2d_bytes > 0) {
+  if (fed) {
     // fed like a local step: the feeder enqueues the program once the host
     // saw the copy land (program_body(fed): no lane waits just for the copy)
     h2d(slot, p.h2d_dst, h2d_src, h2d_bytes, nullptr, egress_ == nullptr);
@@ -455,6 +474,7 @@ void StepRunner::launch(int slot, void* dst, const void* src, int64_t nbytes, hi
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   ck(hipSetDevice(device_), "hipSetDevice");
   drain_feeder();
+  last_slot_ = slot;
   h2d(slot, dst, src, nbytes, compute_, true);
   ck(hipGraphLaunch(graph, compute_), "hipGraphLaunch");
   ck(hipEventRecord(done_[slot], compute_), "hipEventRecord(done)");
@@ -466,7 +486,9 @@ void StepRunner::launch_seq(int slot, void* dst, const void* src, int64_t nbytes
   if (slot < 0 || slot >= int(done_.size())) throw std::out_of_range("slot");
   if (!seq) throw std::invalid_argument("null kernel sequence");
   ck(hipSetDevice(device_), "hipSetDevice");
-  if (feed_h2d_ && !host_wait_h2d_ && nbytes > 0) {
+  const bool fed = want_feed(nbytes);
+  last_slot_ = slot;
+  if (fed) {
     h2d(slot, dst, src, nbytes, nullptr, true);
     used_[slot] = 1;
     feed(FeedJob{slot, seq, nullptr, skip_varint});
@@ -485,7 +507,9 @@ void StepRunner::launch_copies(int slot, void* dst, const std::vector<ShareCopy>
   ck(hipSetDevice(device_), "hipSetDevice");
   int64_t nbytes = 0;
   for (const ShareCopy& c : copies) nbytes += c.n > 0 ? c.n : 0;
-  if (feed_h2d_ && !host_wait_h2d_ && nbytes > 0) {
+  const bool fed = want_feed(nbytes);
+  last_slot_ = slot;
+  if (fed) {
     h2d_copies(slot, dst, copies, nullptr, true);
     used_[slot] = 1;
     feed(FeedJob{slot, seq, seq ? nullptr : graph, skip_varint});

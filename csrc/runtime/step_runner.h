@@ -170,10 +170,11 @@ class StepRunner {
   // copy's event on the device (false) - see h2d().
   void set_host_wait_h2d(bool v) { host_wait_h2d_ = v; }
   bool host_wait_h2d() const { return host_wait_h2d_; }
-  // Local steps (launch_seq / launch_copies): a feeder thread enqueues each
-  // step's kernels once the host sees its H2D landed, so the compute queue
-  // carries no cross-queue wait packet (true, the default), or the compute
-  // stream waits on the copy's event on the device (false). Set before the
+  // Local and programmed steps launched while earlier steps still run: a
+  // feeder thread enqueues each step's kernels once the host sees its H2D
+  // landed, so the compute queue carries no cross-queue wait packet (true, the
+  // default), or the compute stream waits on the copy's event on the device
+  // (false; always so for a step launched on an idle GPU). Set before the
   // first launch.
   void set_feed_h2d(bool v) { feed_h2d_ = v; }
   bool feed_h2d() const { return feed_h2d_; }
@@ -235,6 +236,8 @@ class StepRunner {
   bool slot_launched(int slot) const {
     return launched_[slot].load(std::memory_order_acquire) == queued_[slot].load(std::memory_order_acquire);
   }
+  bool want_feed(int64_t nbytes);            // feed this step: the GPU is still busy with earlier ones
+  int last_slot_ = -1;                       // slot of the last launch (launcher thread)
   void wait_slot_launched(int slot) const;  // spin until the feeder enqueued the slot's last job
   void drain_feeder() const;                 // ... every slot's
 };
