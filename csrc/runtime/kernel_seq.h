@@ -32,6 +32,13 @@ class KernelSequence {
   // found no packed varint ids in this step's requests).
   void launch(hipStream_t st, hipEvent_t done = nullptr, bool bind = false, bool skip_varint = false) const;
   int size() const { return int(ops_.size()); }
+  // launching it with skip_varint enqueues nothing (the sequence is only the
+  // arena varint-decode kernel, or empty)
+  bool empty_without_varint() const {
+    for (const Op& o : ops_)
+      if (!o.varint) return false;
+    return true;
+  }
   std::string describe() const;
 
  private:

@@ -425,7 +425,9 @@ void StepRunner::program_body(int slot, const StepProgram& p, bool skip_varint, 
   for (const ProgOp& o : p.ops) {
     hipStream_t st = lanes[o.lane];
     if (fed) {
-      if (o.lane == 1 && o.kind != ProgOp::kRecord && o.kind != ProgOp::kWait && o.kind != ProgOp::kWaitPrev)
+      // (a varint-only sequence launched with skip_varint enqueues nothing)
+      const bool noop = o.kind == ProgOp::kKernels && o.seq && skip_varint && o.seq->empty_without_varint();
+      if (o.lane == 1 && o.kind != ProgOp::kRecord && o.kind != ProgOp::kWait && o.kind != ProgOp::kWaitPrev && !noop)
         aux_work = true;
       if (o.kind == ProgOp::kRecord && o.lane == 1 && !aux_work) {
         trivial[o.event] = true;

@@ -377,17 +377,21 @@ class DCNv2(CTRModel):
     # one-stream, profiles/r04_session2.md - the cross GEMMs hold every CU;
     # the hooks were removed in round 5)
 
-    def _forward(self, ids, wts, out=None, resolved=None):
-        # fp8 towers: x0 is quantised once, for the first cross layer AND the
-        # first MLP layer (both read it) - by the gather itself, which holds each
-        # row in one wave's registers (ops.embed_fp8; no separate quant pass)
+    def _front(self, ids, wts):
+        """x0 and (fp8 towers) its e4m3 copy + row scales. x0 is quantised once,
+        for the first cross layer AND the first MLP layer (both read it) - by
+        the gather itself, which holds each row in one wave's registers
+        (ops.embed_fp8; no separate quant pass)."""
         fp8_full = self.fp8 and not self.low_rank
         if fp8_full and self.cfg.num_fields <= 64:
             x0, *q0 = ops.embed_fp8(self.emb, ids, wts, self.cfg.vocab_size, ops.FP8_K_PAD)
-            q0 = tuple(q0)
-        else:
-            x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
-            q0 = ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None
+            return x0, tuple(q0)
+        x0, _ = ops.embed(self.emb, ids, wts, modulo=self.cfg.vocab_size, want_x=True)
+        return x0, (ops.quant_rows_fp8(x0, ops.FP8_K_PAD) if fp8_full else None)
+
+    def _cross_net(self, x0, q0):
+        """The cross layers -> the cross half of the head logit."""
+        fp8_full = self.fp8 and not self.low_rank
         L = self.cfg.num_cross_layers
         if fp8_full and self.d % 8 == 0 and L > 0:
             # split cross layers: plain-epilogue GEMM y = xl W^T + b (the
@@ -416,13 +420,24 @@ class DCNv2(CTRModel):
                                                               k_pad=0 if last else ops.FP8_K_PAD,
                                                               head_w=self.head_wc if last else None)
                 xl = z
-        else:
-            xl, xq = x0, q0
-            for i in range(L):
-                xl, xq = self._cross_layer(i, x0, xl, xq), None
-            cross_logit = ops.head(xl, self.head_wc, 0.0, sigmoid=False)
-        mlp_q = q0 if (q0 is not None and self.mlp.layers[0].fp8 and self.mlp.layers[0].k == x0.shape[1]) else None
-        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out, xq=mlp_q)
+            return cross_logit
+        xl, xq = x0, q0
+        for i in range(L):
+            xl, xq = self._cross_layer(i, x0, xl, xq), None
+        return ops.head(xl, self.head_wc, 0.0, sigmoid=False)
+
+    def _mlp_q(self, x0, q0):
+        return q0 if (q0 is not None and self.mlp.layers[0].fp8 and self.mlp.layers[0].k == x0.shape[1]) else None
+
+    def _forward(self, ids, wts, out=None, resolved=None):
+        x0, q0 = self._front(ids, wts)
+        cross_logit = self._cross_net(x0, q0)
+        return self.mlp.forward_head(x0, self.head_wd, self.head_b, extra=cross_logit, out=out, xq=self._mlp_q(x0, q0))
+
+    # (not adopted, round 6: the first MLP layer on a step program's aux lane
+    # beside the cross layers, to fill the CUs the cross GEMMs' last tile round
+    # leaves idle - 27.86 / 28.05 / 27.49 M with the aux lane on 128 / all / 64
+    # CUs vs 27.78 M one-lane, profiles/r06_dcn_mlp_lane.jsonl)
 
 
 class DLRM(CTRModel):
