@@ -117,10 +117,11 @@ def parse_args():
     ap.add_argument("--decode-threads", type=int, default=4,
                     help="native host pool per rank (4 measured best on a 16-CPU MI355X slice)")
     ap.add_argument("--client-threads", type=int, default=8, help="load-generator submitting threads per rank")
-    ap.add_argument("--open-loop-threads", type=int, default=12,
-                    help="submitting threads per rank of the open-loop runs (fixed QPS, latency sweep): each "
-                         "512-candidate request costs its submitter ~25 us of copying and narrowing, so at 90 %% of "
-                         "a ~290 k requests/s capacity 8 threads have ~10 %% slack and a hiccup becomes a backlog")
+    ap.add_argument("--open-loop-threads", type=int, default=8,
+                    help="submitting threads per rank of the open-loop runs (fixed QPS, latency sweep). Each "
+                         "512-candidate request costs its submitter ~25 us of copying and narrowing (~6.5 CPUs of "
+                         "work at 90 %% of a ~290 k requests/s capacity, whatever the thread count); 12 threads "
+                         "measured no better and, on a box whose 16-CPU quota was contended, worse")
     ap.add_argument("--pool", type=int, default=64, help="distinct pre-serialized requests per rank")
     ap.add_argument("--gemm-dtype", default=None, choices=["bf16", "fp8"],
                     help="default: the model preset's (fp8 towers for dcn_v2 = BASELINE config 5)")
